@@ -1,0 +1,107 @@
+"""Pin the oracle (oracle/cpu_ref.py) against fixtures produced by running the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import cpu_ref, recipe
+
+FWD_CASES = ["fwd_r18_k2_96x128", "fwd_r34_k4_96x128", "fwd_r34_k4_75x100", "fwd_r50_k8_96x128"]
+
+
+def test_state_dict_matches_reference_layout():
+    # R34: 218 keys and the reference's parameter counts
+    sd = recipe.seeded_state_dict("resnet34", 0)
+    assert len(sd) == 218
+    n = {bb: sum(int(np.prod(s)) for _, s, kind in cpu_ref.state_dict_spec(bb)
+                 if kind in ("conv", "fc_weight", "fc_bias", "bn_weight", "bn_bias"))
+         for bb in cpu_ref.BACKBONES}
+    assert n == {"resnet18": 11689512, "resnet34": 21797672, "resnet50": 25557032}
+
+
+def test_layer_plan_dilations():
+    plan = {b["name"]: b for b in cpu_ref.layer_plan("resnet34")}
+    assert plan["layer2.0"]["stride"] == 2 and plan["layer2.0"]["dilation"] == 1
+    assert plan["layer3.0"]["stride"] == 1 and plan["layer3.0"]["dilation"] == 2
+    assert plan["layer4.2"]["dilation"] == 4
+    assert plan["layer3.0"]["downsample"] == (128, 256, 1)
+    p50 = {b["name"]: b for b in cpu_ref.layer_plan("resnet50")}
+    assert p50["layer1.0"]["downsample"] == (64, 256, 1)
+
+
+@pytest.mark.parametrize("case", FWD_CASES)
+def test_forward_matches_reference(golden, case):
+    g = golden(case)
+    bb, k = str(g["backbone"]), int(g["k"])
+    x = recipe.to_tensor_nchw(g["images_u8"])
+    sd = recipe.seeded_state_dict(bb, int(g["wseed"]))
+    with torch.no_grad():
+        heat, low = cpu_ref.forward(sd, x, bb, k, return_lowres=True)
+    np.testing.assert_allclose(low.numpy(), g["lowres"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(heat.numpy(), g["heat"], rtol=0, atol=1e-6)
+    assert (cpu_ref.argmax_yx(heat) == g["argmax_yx"]).all()
+    rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
+    assert abs(rm - g["running_checksum"][0]) < 1e-6 * max(1, abs(rm))
+    np.testing.assert_allclose(sd["resnet.%s_8s.bn1.running_var" % bb].numpy(), g["bn1_running_var"], atol=1e-6)
+
+
+def test_k_only_head_equals_faithful(golden):
+    g = golden("fwd_r34_k4_96x128")
+    x = recipe.to_tensor_nchw(g["images_u8"])
+    with torch.no_grad():
+        h1 = cpu_ref.forward(recipe.seeded_state_dict("resnet34", 2), x, "resnet34", 4, head="k_only")
+    np.testing.assert_allclose(h1.numpy(), g["heat"], rtol=0, atol=1e-6)
+
+
+def test_eval_bn_matches_reference(golden):
+    g = golden("fwd_r34_k4_96x128")
+    x = recipe.to_tensor_nchw(g["images_u8"])
+    with torch.no_grad():
+        h = cpu_ref.forward(recipe.seeded_state_dict("resnet34", 2), x, "resnet34", 4, bn_mode="eval")
+    np.testing.assert_allclose(h.numpy(), g["heat_eval"], rtol=0, atol=1e-6)
+
+
+def test_gauss_matches_reference(golden):
+    g = golden("gauss")
+    i = 0
+    while "case%d_G" % i in g:
+        w, h, s = g["case%d_whs" % i]
+        G = cpu_ref.gauss_2d_batch(int(w), int(h), int(s), g["case%d_U" % i], g["case%d_V" % i])
+        assert G.dtype == torch.float64
+        assert np.array_equal(G.numpy(), g["case%d_G" % i])
+        i += 1
+    assert i == 3
+
+
+def test_bce_matches_reference(golden):
+    g = golden("bce")
+    p = torch.tensor(g["p"], requires_grad=True)
+    L = cpu_ref.bce_loss(p, torch.tensor(g["y"]))
+    L.backward()
+    assert L.item() == g["loss"]
+    assert np.array_equal(p.grad.numpy(), g["grad"])
+    p2 = torch.tensor(g["p"], requires_grad=True)
+    M = cpu_ref.mse_loss(p2, torch.tensor(g["y"]))
+    M.backward()
+    assert M.item() == g["mse"]
+    assert np.array_equal(p2.grad.numpy(), g["mse_grad"])
+
+
+@pytest.mark.parametrize("case", ["train_r18_k2_64x80", "train_r34_k4_48x64"])
+def test_train_step_matches_reference(golden, case):
+    g = golden(case)
+    bb, k = str(g["backbone"]), int(g["k"])
+    x = recipe.to_tensor_nchw(g["images_u8"])
+    sd = recipe.seeded_state_dict(bb, int(g["wseed"]))
+    names = list(g["param_names"])
+    opt = None
+    for s in range(int(g["steps"])):
+        L, grads, opt = cpu_ref.train_step(sd, x, g["uv"], bb, k, adam_state=None)
+        assert abs(L.item() - float(g["loss%d" % s])) < 1e-9
+        gs = np.array([float(grads[n].double().sum()) for n in names])
+        ga = np.array([float(grads[n].double().abs().sum()) for n in names])
+        np.testing.assert_allclose(ga, g["grad_abs%d" % s], rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(gs, g["grad_sum%d" % s], rtol=1e-3, atol=1e-6 * ga.max())
+        np.testing.assert_allclose(grads["resnet.%s_8s.conv1.weight" % bb].numpy(), g["stem_grad%d" % s],
+                                   rtol=1e-4, atol=1e-8)
+        break  # Adam state is per-call in train_step; step-0 grads pin the math
