@@ -1,0 +1,219 @@
+// BatchNorm (train-mode statistics, apply+ReLU+residual, stem BN+ReLU+maxpool).
+//
+// Reference semantics: nn.BatchNorm2d in TRAIN mode everywhere
+// (the reference never calls .eval()): normalise with the biased
+// batch variance over (N,H,W), eps 1e-5; running stats with momentum 0.1 and the
+// unbiased variance; num_batches_tracked += 1.  Output = x*alpha + beta with
+// alpha = invstd*gamma, beta = bias - mean*alpha (fp32, two roundings, as
+// ATen's batch_norm_cpu_transform_input).
+#include "common.h"
+
+namespace hkp {
+
+// one block (256 threads) per channel; deterministic fixed-order fp64 merge
+__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
+                                                         const float* __restrict__ part, const float* gamma,
+                                                         const float* beta, float momentum, float eps, float* rmean,
+                                                         float* rvar, int64_t* nbt, float* ss, float* mi) {
+    __shared__ double red[4];
+    __shared__ double bcast;
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    double s = 0.0;
+    for (long t = tid; t < tiles; t += 256) s += (double)part[(t * C + c) * 2];
+    s = wave_sum_d(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    if (tid == 0) bcast = ((red[0] + red[1]) + (red[2] + red[3])) / (double)count;
+    __syncthreads();
+    const double mean = bcast;
+    double q = 0.0;
+    for (long t = tid; t < tiles; t += 256) {
+        const long n_t = min((long)tile_rows, count - t * tile_rows);
+        const double st = (double)part[(t * C + c) * 2];
+        const double dm = st / (double)n_t - mean;
+        q += (double)part[(t * C + c) * 2 + 1] + (double)n_t * dm * dm;
+    }
+    q = wave_sum_d(q);
+    __syncthreads();
+    if (lane == 0) red[wid] = q;
+    __syncthreads();
+    if (tid == 0) {
+        const double m2 = (red[0] + red[1]) + (red[2] + red[3]);
+        const double var = m2 / (double)count;
+        const double invstd = 1.0 / sqrt(var + (double)eps);
+        const float inv_f = (float)invstd, mean_f = (float)mean;
+        const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+        const float alpha = __fmul_rn(inv_f, g);
+        ss[c] = alpha;
+        ss[C + c] = __fsub_rn(b, __fmul_rn(mean_f, alpha));
+        if (mi) {
+            mi[c] = mean_f;
+            mi[C + c] = inv_f;
+        }
+        if (rmean) {
+            const double unbiased = count > 1 ? m2 / (double)(count - 1) : var;
+            rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
+            rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
+        }
+        if (nbt && c == 0) nbt[0] += 1;
+    }
+}
+
+__global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
+                               float eps, float* ss, float* mi) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const float inv = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float alpha = __fmul_rn(inv, g);
+    ss[c] = alpha;
+    ss[C + c] = __fsub_rn(b, __fmul_rn(rm[c], alpha));
+    if (mi) {
+        mi[c] = rm[c];
+        mi[C + c] = inv;
+    }
+}
+
+// RES: 0 none, 1 raw residual, 2 affine residual (downsample BN)
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f32x4* __restrict__ y,
+                                                       const f32x4* __restrict__ sc, const f32x4* __restrict__ sh,
+                                                       const f32x4* __restrict__ res, const f32x4* __restrict__ rsc,
+                                                       const f32x4* __restrict__ rsh, f32x4* __restrict__ out) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const int c4 = (int)(i % C4);
+        const f32x4 v = y[i], a = sc[c4], b = sh[c4];
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(__fmul_rn(v[e], a[e]), b[e]);
+        if constexpr (RES == 1) {
+            const f32x4 r = res[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], r[e]);
+        } else if constexpr (RES == 2) {
+            const f32x4 r = res[i], ra = rsc[c4], rb = rsh[c4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn(r[e], ra[e]), rb[e]));
+        }
+        if constexpr (RELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
+        }
+        out[i] = o;
+    }
+}
+
+// maxpool 3x3 / s2 / p1 (-inf padding) of relu(y*a+b); one thread per 4 channels of one output pixel
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                             const float* __restrict__ y,
+                                                             const float* __restrict__ ss,
+                                                             float* __restrict__ out) {
+    const int C4 = C >> 2;
+    const long total = (long)N * Ho * Wo * C4;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int c4 = (int)(i % C4);
+        long p = i / C4;
+        const int wo = (int)(p % Wo);
+        p /= Wo;
+        const int ho = (int)(p % Ho);
+        const int n = (int)(p / Ho);
+        const f32x4 a = *(const f32x4*)(ss + 4 * c4), b = *(const f32x4*)(ss + C + 4 * c4);
+        f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int dr = 0; dr < 3; ++dr) {
+            const int hi = ho * 2 - 1 + dr;
+            if ((unsigned)hi >= (unsigned)H) continue;
+#pragma unroll
+            for (int ds = 0; ds < 3; ++ds) {
+                const int wi = wo * 2 - 1 + ds;
+                if ((unsigned)wi >= (unsigned)W) continue;
+                const f32x4 v = *(const f32x4*)(y + (((long)n * H + hi) * W + wi) * C + 4 * c4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    float t = __fadd_rn(__fmul_rn(v[e], a[e]), b[e]);
+                    t = t > 0.f ? t : 0.f;
+                    m[e] = t > m[e] ? t : m[e];
+                }
+            }
+        }
+        *(f32x4*)(out + i * 4) = m;
+    }
+}
+
+static inline int grid_for(long work, int block = 256) {
+    long g = (work + block - 1) / block;
+    if (g > 256L * 16) g = 256L * 16;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace hkp
+
+using namespace hkp;
+
+extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                               const float* gamma, const float* beta, float momentum, float eps, float* running_mean,
+                               float* running_var, int64_t* num_batches_tracked, float* scale_shift,
+                               float* mean_invstd, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && count > 0 && tiles > 0 && tile_rows > 0, "hkp_bn_finalize: bad sizes");
+    HKP_CHECK_ARG(partials && scale_shift, "hkp_bn_finalize: null tensor");
+    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "hkp_bn_finalize: running stats pair");
+    HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
+                  "hkp_bn_finalize: tiles/tile_rows inconsistent with count");
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, as_stream(stream), c, (long)count, (long)tiles,
+                       tile_rows, partials, gamma, beta, momentum, eps, running_mean, running_var,
+                       num_batches_tracked, scale_shift, mean_invstd);
+    HKP_LAUNCH_CHECK("hkp_bn_finalize");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const float* running_mean,
+                                  const float* running_var, float eps, float* scale_shift, float* mean_invstd,
+                                  hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && running_mean && running_var && scale_shift, "hkp_bn_eval_params: bad args");
+    hipLaunchKernelGGL(bn_eval_kernel, dim3((c + 255) / 256), dim3(256), 0, as_stream(stream), c, gamma, beta,
+                       running_mean, running_var, eps, scale_shift, mean_invstd);
+    HKP_LAUNCH_CHECK("hkp_bn_eval_params");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
+                            const float* res_scale_shift, int32_t relu, float* out, hkp_stream_t stream) {
+    HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_apply: need m>0 and c%%4==0 (c=%d)", c);
+    HKP_CHECK_ARG(y && scale_shift && out, "hkp_bn_apply: null tensor");
+    HKP_CHECK_ARG(res_scale_shift == nullptr || res != nullptr, "hkp_bn_apply: res_scale_shift without res");
+    const long n4 = m * (long)c / 4;
+    const int C4 = c / 4;
+    const f32x4 *Y = (const f32x4*)y, *SC = (const f32x4*)scale_shift, *SH = (const f32x4*)(scale_shift + c);
+    const f32x4* R = (const f32x4*)res;
+    const f32x4* RSC = res_scale_shift ? (const f32x4*)res_scale_shift : nullptr;
+    const f32x4* RSH = res_scale_shift ? (const f32x4*)(res_scale_shift + c) : nullptr;
+    f32x4* O = (f32x4*)out;
+    const int g = grid_for(n4);
+    hipStream_t st = as_stream(stream);
+#define HKP_APPLY(RES, RL) \
+    hipLaunchKernelGGL((bn_apply_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, RSH, O)
+    if (!res) {
+        if (relu) HKP_APPLY(0, true); else HKP_APPLY(0, false);
+    } else if (!res_scale_shift) {
+        if (relu) HKP_APPLY(1, true); else HKP_APPLY(1, false);
+    } else {
+        if (relu) HKP_APPLY(2, true); else HKP_APPLY(2, false);
+    }
+#undef HKP_APPLY
+    HKP_LAUNCH_CHECK("hkp_bn_apply");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y,
+                                   const float* scale_shift, float* out, hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "hkp_bn_relu_maxpool: bad sizes");
+    HKP_CHECK_ARG(y && scale_shift && out, "hkp_bn_relu_maxpool: null tensor");
+    const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+    const long work = (long)n * ho * wo * (c / 4);
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n, h, w, c,
+                       ho, wo, y, scale_shift, out);
+    HKP_LAUNCH_CHECK("hkp_bn_relu_maxpool");
+    return HKP_OK;
+}

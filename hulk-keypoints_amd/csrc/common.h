@@ -1,0 +1,58 @@
+// Shared helpers for the libhulkkp HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/hulkkp.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace hkp {
+
+// thread-local last-error message (hkp_last_error)
+void set_error(const char* fmt, ...);
+
+#define HKP_CHECK_ARG(cond, ...)                  \
+    do {                                          \
+        if (!(cond)) {                            \
+            ::hkp::set_error(__VA_ARGS__);        \
+            return HKP_ERR_BAD_ARG;               \
+        }                                         \
+    } while (0)
+
+#define HKP_LAUNCH_CHECK(what)                                                      \
+    do {                                                                            \
+        hipError_t e_ = hipGetLastError();                                          \
+        if (e_ != hipSuccess) {                                                     \
+            ::hkp::set_error("%s: launch failed: %s", what, hipGetErrorString(e_)); \
+            return (int)e_;                                                         \
+        }                                                                           \
+    } while (0)
+
+static inline hipStream_t as_stream(hkp_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): consecutive logical tiles land on the same XCD (one L2).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+}  // namespace hkp

@@ -1,0 +1,241 @@
+// Heatmap head: K-channel 1x1 scoring conv, bilinear (align_corners=True)
+// upsample + sigmoid + argmax decode, and the Gaussian target.
+//
+//  * hkp_head_fc          src/resnet_dilated.py:16 (fc 1x1 + bias), only the K
+//                         rows src/model.py:21 keeps (per-channel ops,
+//                         so dropping rows >= K changes no kept value).
+//  * hkp_upsample_sigmoid src/resnet_dilated.py:27 + src/model.py:21 + the
+//                         argmax of src/prediction.py:46.  The interpolation
+//                         reproduces ATen's CPU arithmetic bit for bit:
+//                         t(h) = fma(x[h][w0], lw0, x[h][w1]*lw1),
+//                         out  = fma(t(h0), lh0, t(h1)*lh1), weights in fp32
+//                         (verified against torch 2.10 CPU on 4 shapes).
+//  * hkp_gauss_target     src/dataset.py:36-44.
+#include "common.h"
+
+namespace hkp {
+
+// one wave per pixel; W (K x C) and bias staged in LDS
+template <int KMAX>
+__global__ __launch_bounds__(256) void head_fc_kernel(int npix, int hw, int C, int K, const float* __restrict__ feat,
+                                                      const float* __restrict__ w, const float* __restrict__ bias,
+                                                      float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) float wl[];  // [K][C]
+    for (int i = threadIdx.x; i < K * C; i += blockDim.x) wl[i] = w[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int waves = blockDim.x >> 6;
+    for (int p = blockIdx.x * waves + wid; p < npix; p += gridDim.x * waves) {
+        float acc[KMAX];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) acc[k] = 0.f;
+        const float* f = feat + (long)p * C;
+        for (int c = lane * 4; c < C; c += 256) {
+            const f32x4 v = *(const f32x4*)(f + c);
+#pragma unroll
+            for (int k = 0; k < KMAX; ++k) {
+                if (k < K) {
+                    const f32x4 ww = *(const f32x4*)(wl + k * C + c);
+                    acc[k] += v[0] * ww[0] + v[1] * ww[1] + v[2] * ww[2] + v[3] * ww[3];
+                }
+            }
+        }
+        const int n = p / hw, q = p - n * hw;
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+            if (k < K) {
+                const float s = wave_sum(acc[k]);
+                if (lane == k) out[((long)n * K + k) * hw + q] = s + bias[k];
+            }
+        }
+    }
+}
+
+struct Lerp {
+    int i0, i1;
+    float l0, l1;
+};
+
+// ATen compute_indices_weights_linear, align_corners=True, fp32 opmath
+__device__ __forceinline__ Lerp lerp_index(int o, int in, int out, float scale) {
+    Lerp r;
+    if (in == out) {
+        r.i0 = r.i1 = o;
+        r.l0 = 1.f;
+        r.l1 = 0.f;
+        return r;
+    }
+    const float src = __fmul_rn(scale, (float)o);
+    int i0 = (int)floorf(src);
+    i0 = i0 < in - 1 ? i0 : in - 1;
+    float l1 = __fsub_rn(src, (float)i0);
+    l1 = fminf(fmaxf(l1, 0.f), 1.f);
+    r.i0 = i0;
+    r.i1 = i0 + (i0 < in - 1 ? 1 : 0);
+    r.l1 = l1;
+    r.l0 = __fsub_rn(1.f, l1);
+    return r;
+}
+
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) {
+    return a > b ? a : b;
+}
+
+// grid: x over ceil(H*W/4/256) chunks, y over n*k planes
+template <bool SIGMOID>
+__global__ __launch_bounds__(256) void upsample_sigmoid_kernel(int h, int w, int H, int W, float sh, float sw,
+                                                              const float* __restrict__ low, float* __restrict__ heat,
+                                                              unsigned long long* __restrict__ keys) {
+    const int plane = blockIdx.y;
+    const long HW = (long)H * W;
+    const float* x = low + (long)plane * h * w;
+    const long base = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    unsigned long long best = 0ull;
+    if (base < HW) {
+        float v[4];
+        int cnt = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const long o = base + e;
+            if (o < HW) {
+                const int oh = (int)(o / W), ow = (int)(o - (long)oh * W);
+                const Lerp lh = lerp_index(oh, h, H, sh), lw = lerp_index(ow, w, W, sw);
+                const float* r0 = x + (long)lh.i0 * w;
+                const float* r1 = x + (long)lh.i1 * w;
+                const float t0 = __builtin_fmaf(r0[lw.i0], lw.l0, __fmul_rn(r0[lw.i1], lw.l1));
+                const float t1 = __builtin_fmaf(r1[lw.i0], lw.l0, __fmul_rn(r1[lw.i1], lw.l1));
+                const float z = __builtin_fmaf(t0, lh.l0, __fmul_rn(t1, lh.l1));
+                const float p = SIGMOID ? sigmoid_f(z) : z;
+                v[e] = p;
+                const unsigned long long key =
+                    ((unsigned long long)__float_as_uint(p) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)o);
+                best = umax64(best, key);
+                ++cnt;
+            }
+        }
+        if (heat) {
+            float* dst = heat + (long)plane * HW + base;
+            if (cnt == 4 && (HW & 3) == 0) {
+                *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
+            } else {
+                for (int e = 0; e < cnt; ++e) dst[e] = v[e];
+            }
+        }
+    }
+    if (keys) {
+        unsigned lo = (unsigned)best, hi = (unsigned)(best >> 32);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned ol = __shfl_xor(lo, off), oh = __shfl_xor(hi, off);
+            const unsigned long long other = ((unsigned long long)oh << 32) | ol;
+            const unsigned long long mine = ((unsigned long long)hi << 32) | lo;
+            const unsigned long long m = umax64(mine, other);
+            lo = (unsigned)m;
+            hi = (unsigned)(m >> 32);
+        }
+        if ((threadIdx.x & 63) == 0) atomicMax(keys + plane, ((unsigned long long)hi << 32) | lo);
+    }
+}
+
+__global__ void argmax_decode_kernel(int nk, int W, const unsigned long long* __restrict__ keys, int* __restrict__ yx) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nk) return;
+    const unsigned idx = 0xFFFFFFFFu - (unsigned)(keys[i] & 0xFFFFFFFFull);
+    yx[2 * i] = (int)(idx / (unsigned)W);
+    yx[2 * i + 1] = (int)(idx % (unsigned)W);
+}
+
+__global__ __launch_bounds__(256) void gauss_target_kernel(int K, int H, int W, float den,
+                                                          const float* __restrict__ uv, double* __restrict__ out,
+                                                          long total) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    const long HW = (long)H * W;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const long plane = i / HW;
+        const long r = i - plane * HW;
+        const int y = (int)(r / W), x = (int)(r - (long)y * W);
+        const float u = uv[plane * 2], v = uv[plane * 2 + 1];
+        const float dx = __fsub_rn((float)x, u), dy = __fsub_rn((float)y, v);
+        const float t = __fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy));
+        out[i] = (double)expf(__fdiv_rn(-t, den));
+    }
+}
+
+}  // namespace hkp
+
+using namespace hkp;
+
+extern "C" int hkp_head_fc(int32_t n, int32_t hw, int32_t c, int32_t k, const float* feat, const float* w,
+                           const float* bias, float* lowres, hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && hw > 0 && c > 0 && k > 0, "hkp_head_fc: bad sizes");
+    HKP_CHECK_ARG(k <= 16, "hkp_head_fc: at most 16 keypoints (got %d)", k);
+    HKP_CHECK_ARG(c % 4 == 0 && (long)k * c <= 16384, "hkp_head_fc: need c%%4==0 and k*c<=16384");
+    HKP_CHECK_ARG(feat && w && bias && lowres, "hkp_head_fc: null tensor");
+    const int npix = n * hw;
+    int grid = (npix + 3) / 4;
+    if (grid > 2048) grid = 2048;
+    const size_t lds = (size_t)k * c * sizeof(float);
+    hipStream_t st = as_stream(stream);
+    if (k <= 4)
+        hipLaunchKernelGGL(head_fc_kernel<4>, dim3(grid), dim3(256), lds, st, npix, hw, c, k, feat, w, bias, lowres);
+    else if (k <= 8)
+        hipLaunchKernelGGL(head_fc_kernel<8>, dim3(grid), dim3(256), lds, st, npix, hw, c, k, feat, w, bias, lowres);
+    else
+        hipLaunchKernelGGL(head_fc_kernel<16>, dim3(grid), dim3(256), lds, st, npix, hw, c, k, feat, w, bias, lowres);
+    HKP_LAUNCH_CHECK("hkp_head_fc");
+    return HKP_OK;
+}
+
+extern "C" int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, int32_t W,
+                                    int32_t apply_sigmoid, const float* lowres, float* heat, uint64_t* argmax_ws, int32_t* argmax_yx,
+                                    hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && k > 0 && h > 0 && w > 0 && H > 0 && W > 0, "hkp_upsample_sigmoid: bad sizes");
+    HKP_CHECK_ARG(lowres != nullptr, "hkp_upsample_sigmoid: null lowres");
+    HKP_CHECK_ARG(argmax_yx == nullptr || argmax_ws != nullptr, "hkp_upsample_sigmoid: argmax needs workspace");
+    HKP_CHECK_ARG(argmax_yx == nullptr || apply_sigmoid, "hkp_upsample_sigmoid: argmax keys need sigmoid outputs");
+    HKP_CHECK_ARG((long)H * W < 0xFFFFFFFFL, "hkp_upsample_sigmoid: plane too large");
+    hipStream_t st = as_stream(stream);
+    const int nk = n * k;
+    unsigned long long* keys = argmax_yx ? (unsigned long long*)argmax_ws : nullptr;
+    if (keys) {
+        hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * nk, st);
+        if (e != hipSuccess) {
+            set_error("hkp_upsample_sigmoid: memset: %s", hipGetErrorString(e));
+            return (int)e;
+        }
+    }
+    // area_pixel_compute_scale (align_corners): (in-1)/(out-1) in fp32
+    const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
+    const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
+    const long HW = (long)H * W;
+    dim3 grid((unsigned)((HW + 1023) / 1024), (unsigned)nk);
+    if (apply_sigmoid)
+        hipLaunchKernelGGL(upsample_sigmoid_kernel<true>, grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat, keys);
+    else
+        hipLaunchKernelGGL(upsample_sigmoid_kernel<false>, grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat,
+                           keys);
+    HKP_LAUNCH_CHECK("hkp_upsample_sigmoid");
+    if (keys) {
+        hipLaunchKernelGGL(argmax_decode_kernel, dim3((nk + 255) / 256), dim3(256), 0, st, nk, W, keys, argmax_yx);
+        HKP_LAUNCH_CHECK("hkp_upsample_sigmoid(decode)");
+    }
+    return HKP_OK;
+}
+
+extern "C" int hkp_gauss_target(int32_t n, int32_t k, int32_t H, int32_t W, float sigma, const float* uv,
+                                double* out, hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && k > 0 && H > 0 && W > 0 && sigma > 0.f, "hkp_gauss_target: bad sizes");
+    HKP_CHECK_ARG(uv && out, "hkp_gauss_target: null tensor");
+    const long total = (long)n * k * H * W;
+    long g = (total + 255) / 256;
+    if (g > 4096) g = 4096;
+    // 2.0*sigma**2 as the reference computes it (python float → fp32 divisor)
+    const float den = (float)(2.0 * (double)sigma * (double)sigma);
+    hipLaunchKernelGGL(gauss_target_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), k, H, W, den, uv, out,
+                       total);
+    HKP_LAUNCH_CHECK("hkp_gauss_target");
+    return HKP_OK;
+}

@@ -1,0 +1,77 @@
+"""ctypes binding of libhulkkp.so (the C ABI declared in include/hulkkp.h).
+
+This is the only place the product touches native code.  There is no CPU or
+PyTorch fallback: if the library is missing or a call fails, it raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libhulkkp.so")
+
+HKP_LAYOUT_NHWC = 0
+HKP_LAYOUT_NCHW = 1
+HKP_LOSS_BCE = 0
+HKP_LOSS_MSE = 1
+
+
+class HkpError(RuntimeError):
+    pass
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in
+                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "dilation", "in_layout")]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F = ctypes.c_float
+_CD = ctypes.POINTER(ConvDesc)
+
+# name -> (restype, argtypes); must cover every function include/hulkkp.h declares
+SIGNATURES = {
+    "hkp_last_error": (ctypes.c_char_p, []),
+    "hkp_version": (ctypes.c_char_p, []),
+    "hkp_conv_out_hw": (ctypes.c_int, [_CD, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
+    "hkp_conv_stat_tiles": (_I64, [_CD]),
+    "hkp_conv2d_fwd": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
+    "hkp_bn_finalize": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_eval_params": (ctypes.c_int, [_I32, _P, _P, _P, _P, _F, _P, _P, _P]),
+    "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P]),
+    "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libhulkkp.so once; raise HkpError (never fall back) if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HkpError("libhulkkp.so is not built (%s); run `python -c 'import __graft_entry__ as g; g.build()'`"
+                           % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        msg = lib().hkp_last_error().decode(errors="replace")
+        raise HkpError("%s failed (rc=%d): %s" % (name, rc, msg))
+    return rc
+
+
+def version():
+    return lib().hkp_version().decode()

@@ -1,0 +1,130 @@
+"""Network executor: walks the reference-shaped module tree (src/resnet.py
+mirror) and launches libhulkkp kernels.  Activations live in NHWC fp32; the
+module tree only holds parameters and BN buffers (reference state_dict keys).
+
+Forward per BasicBlock (src/resnet.py:53-69), train-mode BN:
+    y1 = conv1(x)            [+ BN partials in the epilogue]
+    s1 = bn_finalize(bn1)    (also updates running stats)
+    a1 = relu(y1*s1)         (hkp_bn_apply)
+    y2 = conv2(a1); s2 = bn_finalize(bn2)
+    [yd = ds_conv(x); sd = bn_finalize(ds_bn)]
+    out = relu(y2*s2 + (x | yd*sd))
+"""
+import torch
+
+from . import ops
+
+
+class Trace:
+    """What a forward keeps for the backward pass (None = inference)."""
+
+    def __init__(self):
+        self.blocks = []
+        self.stem = None
+        self.head = None
+
+
+def _bn_params(bn, part, count, stats_only=False):
+    """scale_shift (+ mean_invstd) for a BN layer: batch stats in training mode
+    (and running-stat update, like nn.BatchNorm2d.forward), running stats otherwise."""
+    if bn.training:
+        return ops.bn_finalize(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                               bn.num_batches_tracked, momentum=bn.momentum if bn.momentum is not None else 0.1,
+                               eps=bn.eps)
+    return ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+
+
+def _i(v):
+    return v[0] if isinstance(v, (tuple, list)) else v
+
+
+def conv_bn(conv, bn, x, layout="nhwc"):
+    """conv (+ BN partials when training) → (y, scale_shift, mean_invstd)."""
+    y, part = ops.conv2d_fwd(x, conv.weight, _i(conv.stride), _i(conv.padding), _i(conv.dilation), layout=layout,
+                             stats=bn.training)
+    count = y.numel() // y.shape[-1]
+    ss, mi = _bn_params(bn, part, count)
+    return y, ss, mi
+
+
+def stem_forward(resnet, x_nchw, trace=None):
+    """conv1 → bn1 → relu → maxpool (src/resnet.py:199-202)."""
+    y, ss, mi = conv_bn(resnet.conv1, resnet.bn1, x_nchw, layout="nchw")
+    out = ops.bn_relu_maxpool(y, ss)
+    if trace is not None:
+        trace.stem = dict(x=x_nchw, y=y, ss=ss, mi=mi, out=out)
+    return out
+
+
+def block_forward(block, x, trace=None):
+    rec = {} if trace is not None else None
+    if block.kind == "basic":
+        y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
+        a1 = ops.bn_apply(y1, s1, relu=True)
+        y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
+        last_y, last_s = y2, s2
+        if rec is not None:
+            rec.update(x=x, y=[y1, y2], ss=[s1, s2], mi=[m1, m2], act=[a1])
+    else:
+        y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
+        a1 = ops.bn_apply(y1, s1, relu=True)
+        y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
+        a2 = ops.bn_apply(y2, s2, relu=True)
+        y3, s3, m3 = conv_bn(block.conv3, block.bn3, a2)
+        last_y, last_s = y3, s3
+        if rec is not None:
+            rec.update(x=x, y=[y1, y2, y3], ss=[s1, s2, s3], mi=[m1, m2, m3], act=[a1, a2])
+    if block.downsample is not None:
+        yd, sd, md = conv_bn(block.downsample[0], block.downsample[1], x)
+        out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True)
+        if rec is not None:
+            rec.update(yd=yd, sd=sd, md=md)
+    else:
+        out = ops.bn_apply(last_y, last_s, res=x, relu=True)
+    if rec is not None:
+        rec["out"] = out
+        trace.blocks.append(rec)
+    return out
+
+
+def backbone_forward(resnet, x_nchw, trace=None):
+    """ResNet.forward up to the fc (src/resnet.py:198-213), NHWC output."""
+    if x_nchw.dim() != 4 or x_nchw.shape[1] != 3:
+        raise ValueError("expected [B,3,H,W] input, got %s" % (tuple(x_nchw.shape),))
+    x = stem_forward(resnet, x_nchw.contiguous(), trace)
+    for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4):
+        for block in layer:
+            x = block_forward(block, x, trace)
+    return x
+
+
+def fc_rows(resnet, k):
+    """First k rows of the 1000-row scoring conv as [k, C] / [k] views."""
+    w = resnet.fc.weight
+    return w.reshape(w.shape[0], -1)[:k], resnet.fc.bias[:k]
+
+
+def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
+    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
+    feat = backbone_forward(resnet, x_nchw, trace)
+    w, b = fc_rows(resnet, k)
+    low = ops.head_fc(feat, w, b)
+    hm, yx = ops.upsample_sigmoid(low, x_nchw.shape[2], x_nchw.shape[3], heat=heat, argmax=argmax)
+    if trace is not None:
+        trace.head = dict(feat=feat, low=low, heat=hm, k=k, H=x_nchw.shape[2], W=x_nchw.shape[3])
+    return hm, yx, low
+
+
+def logits_forward(resnet, x_nchw, num_outputs=None):
+    """Resnet34_8s.forward (resnet_dilated.py:24-28): upsampled raw fc logits,
+    [B, num_outputs (default 1000), H, W]; computed 16 channels at a time."""
+    feat = backbone_forward(resnet, x_nchw)
+    n_out = resnet.fc.weight.shape[0] if num_outputs is None else num_outputs
+    W2 = resnet.fc.weight.reshape(resnet.fc.weight.shape[0], -1)
+    outs = []
+    for c0 in range(0, n_out, 16):
+        c1 = min(n_out, c0 + 16)
+        low = ops.head_fc(feat, W2[c0:c1].contiguous(), resnet.fc.bias[c0:c1].contiguous())
+        up, _ = ops.upsample_sigmoid(low, x_nchw.shape[2], x_nchw.shape[3], heat=True, argmax=False, sigmoid=False)
+        outs.append(up)
+    return torch.cat(outs, 1)

@@ -1,0 +1,128 @@
+/*
+ * libhulkkp — C ABI of the MI355X-native keypoint-heatmap CNN hot path.
+ *
+ * Replaces the device work the reference hands to PyTorch/cuDNN implicitly
+ * (reference: vainaviv/hulk-keypoints, Python only, no FFI of its own —
+ * SURVEY §8(b)).  Each entry point cites the reference code whose device work
+ * it performs.  The Python host layer (hulk-keypoints_amd/hkp/) binds these
+ * with ctypes and re-exposes the reference's own call surface
+ * (KeypointsGauss, gauss_2d_batch, Prediction, train.py forward/fit).
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes; no torch or C++ types cross it.
+ *   - Activations are NHWC fp32, conv weights KRSC ([Cout][R][S][Cin]) fp32,
+ *     except the stem, which reads the reference's NCHW image and OIHW weight.
+ *   - The caller owns and allocates every buffer (device pointers).  The
+ *     library never allocates, never synchronises; every launch goes on the
+ *     stream argument (a hipStream_t; NULL = legacy default stream).
+ *   - Return: 0 ok; <0 bad argument (see hkp_last_error()); >0 a hipError_t.
+ *   - All reductions are deterministic (fixed order, no float atomics), so
+ *     results are bitwise reproducible run to run.
+ */
+#ifndef HULKKP_H
+#define HULKKP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HKP_OK 0
+#define HKP_ERR_BAD_ARG (-1)
+#define HKP_ERR_UNSUPPORTED (-2)
+
+#define HKP_LAYOUT_NHWC 0
+#define HKP_LAYOUT_NCHW 1
+
+#define HKP_LOSS_BCE 0
+#define HKP_LOSS_MSE 1
+
+typedef void* hkp_stream_t;
+
+/* thread-local message of the last failing call on this thread */
+const char* hkp_last_error(void);
+/* "hulkkp <version> gfx950" */
+const char* hkp_version(void);
+
+/* ---------------------------------------------------------------- conv ---- */
+typedef struct hkp_conv_desc {
+    int32_t n, h, w, c;             /* input batch, height, width, channels            */
+    int32_t k, r, s;                /* output channels, filter height, filter width    */
+    int32_t stride, pad, dilation;  /* symmetric                                        */
+    int32_t in_layout;              /* HKP_LAYOUT_NHWC, or HKP_LAYOUT_NCHW (stem only)  */
+} hkp_conv_desc;
+
+/* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
+int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);
+
+/* number of BatchNorm statistic tiles the conv epilogue emits; the
+ * stat_partials buffer holds tiles * k * 2 floats */
+int64_t hkp_conv_stat_tiles(const hkp_conv_desc* d);
+
+/* y[n,ho,wo,k] = sum_{r,s,c} x[n, ho*st-pad+r*dil, wo*st-pad+s*dil, c] * w[k,r,s,c]
+ * (zero padding, no bias) on fp32 MFMA (v_mfma_f32_32x32x2_f32).
+ * Replaces: conv3x3 src/resnet.py:20-37 (BasicBlock :45,48; Bottleneck :80),
+ *           1x1 convs src/resnet.py:77,86 and downsample :184-188,
+ *           stem conv src/resnet.py:137,199 (in_layout NCHW, w OIHW).
+ * If stat_partials != NULL the epilogue also writes per-tile per-channel
+ * (sum, sum of squared deviations from the tile mean) for train-mode BN. */
+int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const float* w, float* y,
+                   float* stat_partials, hkp_stream_t stream);
+
+/* ----------------------------------------------------------- batchnorm ---- */
+/* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
+ * nn.BatchNorm2d defaults eps=1e-5, momentum=0.1): merges the conv's tile
+ * partials in fp64 (Chan), writes scale_shift = [gamma*invstd | beta - mean*scale],
+ * mean_invstd = [mean | invstd] (nullable), and updates the running stats
+ * (unbiased variance; nullable) and num_batches_tracked (nullable, +1). */
+int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                    const float* gamma, const float* beta, float momentum, float eps,
+                    float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                    float* scale_shift, float* mean_invstd, hkp_stream_t stream);
+
+/* Eval-mode BN parameters from running statistics (the reference never uses
+ * them; offered as an option). */
+int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const float* running_mean,
+                       const float* running_var, float eps, float* scale_shift, float* mean_invstd,
+                       hkp_stream_t stream);
+
+/* out = [relu]( y*scale + shift  [+ res | + res*rscale + rshift] ), NHWC [m][c].
+ * Replaces the bn→relu / bn→(+residual)→relu tails of BasicBlock
+ * (src/resnet.py:57-67) and Bottleneck (:96-110). res may be NULL;
+ * res_scale_shift NULL means the residual is added raw. */
+int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
+                 const float* res_scale_shift, int32_t relu, float* out, hkp_stream_t stream);
+
+/* Stem tail: maxpool3x3/s2/p1( relu( y*scale + shift ) ), NHWC
+ * (src/resnet.py:139-141, 200-202). Output [n, (h-1)/2+1, (w-1)/2+1, c]. */
+int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y,
+                        const float* scale_shift, float* out, hkp_stream_t stream);
+
+/* ---------------------------------------------------------------- head ---- */
+/* K-channel 1x1 scoring conv + bias (src/resnet_dilated.py:16 sliced to the K
+ * rows src/model.py:21 keeps): feat NHWC [n,hw,c] → lowres [n,k,hw]. */
+int hkp_head_fc(int32_t n, int32_t hw, int32_t c, int32_t k, const float* feat, const float* w,
+                const float* bias, float* lowres, hkp_stream_t stream);
+
+/* bilinear align_corners=True upsample [n,k,h,w] → [n,k,H,W]
+ * (src/resnet_dilated.py:27) + sigmoid (src/model.py:21; skipped when
+ * apply_sigmoid == 0, the raw Resnet34_8s.forward output), NCHW output (nullable),
+ * and the per-(n,k) argmax (src/prediction.py:46, first index wins) as
+ * int32 (y, x) pairs in argmax_yx [n*k*2] (nullable).  argmax_ws: n*k uint64
+ * workspace, required when argmax_yx != NULL. */
+int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, int32_t W,
+                         int32_t apply_sigmoid, const float* lowres, float* heat, uint64_t* argmax_ws, int32_t* argmax_yx,
+                         hkp_stream_t stream);
+
+/* Gaussian target (src/dataset.py:36-44): out[n,k,H,W] (fp64) =
+ * (double) expf( -((x-u)^2 + (y-v)^2) / (2 sigma^2) ) computed in fp32;
+ * uv [n,k,2] fp32 (u = column, v = row). */
+int hkp_gauss_target(int32_t n, int32_t k, int32_t H, int32_t W, float sigma, const float* uv,
+                     double* out, hkp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HULKKP_H */

@@ -1,0 +1,77 @@
+"""CPU-only checks of the boundary: the C-ABI library loads, exports every
+symbol include/hulkkp.h declares, and the Python module tree speaks the
+reference's state_dict (no GPU compute here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "hulkkp.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hkp_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol():
+    from hkp import _lib
+    L = _lib.lib()
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(L, n), "missing export " + n
+    assert set(names) == set(_lib.SIGNATURES), "ctypes signature table out of sync with the header"
+    assert _lib.version().startswith("hulkkp")
+
+
+def test_bad_arguments_raise_not_crash():
+    from hkp import _lib
+    d = _lib.ConvDesc(1, 8, 8, 30, 64, 3, 3, 1, 1, 1, 0)  # Cin=30 is unsupported on the NHWC path
+    with pytest.raises(_lib.HkpError, match="multiple of 32"):
+        _lib.call("hkp_conv2d_fwd", ctypes.byref(d), ctypes.c_void_p(1), ctypes.c_void_p(1), ctypes.c_void_p(1),
+                  None, None)
+    ho, wo = ctypes.c_int32(), ctypes.c_int32()
+    d = _lib.ConvDesc(2, 60, 80, 256, 256, 3, 3, 1, 2, 2, 0)
+    _lib.call("hkp_conv_out_hw", ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo))
+    assert (ho.value, wo.value) == (60, 80)
+    assert _lib.lib().hkp_conv_stat_tiles(ctypes.byref(d)) == (2 * 60 * 80 + 127) // 128
+
+
+@pytest.mark.parametrize("bb", ["resnet18", "resnet34", "resnet50"])
+def test_state_dict_is_reference_compatible(bb):
+    from oracle import cpu_ref, recipe
+    from src.model import KeypointsGauss
+    m = KeypointsGauss(4, backbone=bb, pretrained=False)
+    spec = cpu_ref.state_dict_spec(bb)
+    sd = m.state_dict()
+    assert list(sd.keys()) == [k for k, _, _ in spec]
+    for k, shape, _ in spec:
+        assert tuple(sd[k].shape) == tuple(shape), k
+    # parameters() order == reference parameters() order (Adam state / DDP buckets line up)
+    names = [n for n, _ in m.named_parameters()]
+    assert names == cpu_ref.param_keys(bb)
+    # load → save round trip is exact (OIHW ↔ KRSC repack)
+    ref_sd = recipe.seeded_state_dict(bb, 11)
+    m.load_state_dict(ref_sd)
+    back = m.state_dict()
+    for k in ref_sd:
+        assert torch.equal(back[k], ref_sd[k]), k
+    w = m.resnet.net.layer1[0].conv1.weight
+    assert tuple(w.shape[1:3]) == ((1, 1) if bb == "resnet50" else (3, 3))  # stored KRSC
+
+
+def test_reference_init_statistics():
+    from src.model import KeypointsGauss
+    torch.manual_seed(0)
+    m = KeypointsGauss(4, pretrained=False)
+    w = m.resnet.net.layer4[0].conv2.weight  # 512x3x3x512, std sqrt(2/(9*512))
+    assert abs(w.std().item() - np.sqrt(2 / (9 * 512))) < 2e-4
+    assert abs(m.resnet.net.fc.weight.std().item() - 0.01) < 2e-4
+    assert m.resnet.net.fc.bias.abs().sum().item() == 0
