@@ -8,6 +8,9 @@
 // ATen's batch_norm_cpu_transform_input).
 #include "common.h"
 
+// x*alpha + beta as two roundings (ATen's Vectorized mul then add): no contraction.
+#pragma clang fp contract(off)
+
 namespace hkp {
 
 // one block (256 threads) per channel; deterministic fixed-order fp64 merge

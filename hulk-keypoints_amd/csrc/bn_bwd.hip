@@ -1,0 +1,266 @@
+// BatchNorm backward (train mode) and the stem maxpool backward.
+//
+// For a BN layer z = y*alpha + beta (alpha = gamma*invstd) followed by ReLU
+// (src/resnet.py:57-58,64-67,97-110), given g = dL/d(relu out):
+//   dz        = g * (out > 0)                       (threshold_backward)
+//   dbeta     = sum dz,   dgamma = invstd * sum dz*(y - mean)
+//   dy        = (dz - sum(dz)/N - (y - mean) * k) * invstd*gamma,
+//               k = invstd^2 * sum dz*(y - mean) / N     (ATen batch_norm_backward)
+// Sums run per pixel tile in fp32, merged per channel in fp64 in fixed order.
+#include "common.h"
+
+// the maxpool backward must recompute relu(y*a+b) exactly as bn.hip's forward
+// did (two roundings) so its window argmax agrees: no fma contraction here.
+#pragma clang fp contract(off)
+
+namespace hkp {
+
+constexpr int BNB_TILE = 256;  // pixels per reduction tile
+
+// G = channel groups of 4 per thread (C/4 / threads-per-row); MASK: dz = g*(out>0)
+template <int G, bool MASK>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const float* __restrict__ g,
+                                                           const float* __restrict__ out, const float* __restrict__ y,
+                                                           const float* __restrict__ mean, float* __restrict__ dz,
+                                                           float* __restrict__ part) {
+    __shared__ float red[2][256 * 4 * G];
+    const int C4 = C >> 2;
+    const int tpr = C4 / G;          // threads per row
+    const int rpar = 256 / tpr;      // rows in flight per block
+    const int tid = threadIdx.x;
+    const int rl = tid / tpr, cg = tid - rl * tpr;
+    const long m0 = (long)blockIdx.x * BNB_TILE;
+    const long m1 = min(M, m0 + BNB_TILE);
+    f32x4 s[G], q[G], mu[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        s[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+        q[k] = s[k];
+        mu[k] = *(const f32x4*)(mean + 4 * (cg + k * tpr));
+    }
+    for (long m = m0 + rl; m < m1; m += rpar) {
+#pragma unroll
+        for (int k = 0; k < G; ++k) {
+            const long off = m * C + 4 * (cg + k * tpr);
+            f32x4 d = *(const f32x4*)(g + off);
+            if constexpr (MASK) {
+                const f32x4 o = *(const f32x4*)(out + off);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+            }
+            if (dz) *(f32x4*)(dz + off) = d;
+            const f32x4 v = *(const f32x4*)(y + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                s[k][e] += d[e];
+                q[k][e] += d[e] * (v[e] - mu[k][e]);
+            }
+        }
+    }
+    // combine the rpar partial rows of each channel in fixed order
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int c = 4 * (cg + k * tpr) + e;
+            red[0][rl * C + c] = s[k][e];
+            red[1][rl * C + c] = q[k][e];
+        }
+    __syncthreads();
+    for (int c = tid; c < C; c += 256) {
+        float a = 0.f, b = 0.f;
+        for (int r = 0; r < rpar; ++r) {
+            a += red[0][r * C + c];
+            b += red[1][r * C + c];
+        }
+        part[((long)blockIdx.x * C + c) * 2] = a;
+        part[((long)blockIdx.x * C + c) * 2 + 1] = b;
+    }
+}
+
+// per channel: dgamma, dbeta, and the apply coefficients (grad_mean, k, invstd*gamma)
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
+                                                             const float* __restrict__ mi, const float* gamma,
+                                                             float* dgamma, float* dbeta, float* coef) {
+    __shared__ double red[2][4];
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    double s = 0.0, d = 0.0;
+    for (long t = tid; t < tiles; t += 256) {
+        s += (double)part[(t * C + c) * 2];
+        d += (double)part[(t * C + c) * 2 + 1];
+    }
+    s = wave_sum_d(s);
+    d = wave_sum_d(d);
+    if (lane == 0) {
+        red[0][wid] = s;
+        red[1][wid] = d;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        const double S = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+        const double D = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+        const double inv = (double)mi[C + c];
+        const float gm = gamma ? gamma[c] : 1.f;
+        if (dgamma) dgamma[c] = (float)(D * inv);
+        if (dbeta) dbeta[c] = (float)S;
+        coef[c] = (float)(S / (double)M);                 // grad_mean
+        coef[C + c] = (float)(D * inv * inv / (double)M);  // k
+        coef[2 * C + c] = (float)(inv * (double)gm);       // invstd * gamma
+    }
+}
+
+// dy = ((dz - gm) - (y - mean)*k) * (invstd*gamma), dz = g*(out>0) (MASK) or g
+template <bool MASK>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, const f32x4* __restrict__ g,
+                                                          const f32x4* __restrict__ out, const f32x4* __restrict__ y,
+                                                          const f32x4* __restrict__ mean,
+                                                          const f32x4* __restrict__ coef, f32x4* __restrict__ dy) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        const int c4 = (int)(i % C4);
+        f32x4 d = g[i];
+        if constexpr (MASK) {
+            const f32x4 o = out[i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+        }
+        const f32x4 v = y[i], mu = mean[c4], gm = coef[c4], kk = coef[C4 + c4], sc = coef[2 * C4 + c4];
+        f32x4 r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] = ((d[e] - gm[e]) - (v[e] - mu[e]) * kk[e]) * sc[e];
+        dy[i] = r;
+    }
+}
+
+// Stem maxpool(3x3,s2,p1) ∘ relu ∘ BN-affine backward, as a gather over the ≤2x2
+// pooling windows that contain each input pixel.  Emits dz = dL/d(BN output)
+// (ReLU mask applied).  Window argmax = first max in (dr, ds) scan order, NaN
+// wins — ATen's CPU max_pool2d rule.
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo,
+                                                         const float* __restrict__ dpool, const float* __restrict__ y,
+                                                         const float* __restrict__ ss, float* __restrict__ dz) {
+    const int C4 = C >> 2;
+    const long total = (long)N * H * W * C4;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int c4 = (int)(i % C4);
+        long p = i / C4;
+        const int w = (int)(p % W);
+        p /= W;
+        const int h = (int)(p % H);
+        const int n = (int)(p / H);
+        const f32x4 a = *(const f32x4*)(ss + 4 * c4), b = *(const f32x4*)(ss + C + 4 * c4);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int ho0 = h >> 1, ho1 = min((h + 1) >> 1, Ho - 1);
+        const int wo0 = w >> 1, wo1 = min((w + 1) >> 1, Wo - 1);
+        for (int ho = ho0; ho <= ho1; ++ho) {
+            for (int wo = wo0; wo <= wo1; ++wo) {
+                // argmax of the window (ho, wo), per channel lane
+                f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                int bidx[4] = {-1, -1, -1, -1};
+                for (int dr = 0; dr < 3; ++dr) {
+                    const int hi = ho * 2 - 1 + dr;
+                    if ((unsigned)hi >= (unsigned)H) continue;
+                    for (int ds = 0; ds < 3; ++ds) {
+                        const int wi = wo * 2 - 1 + ds;
+                        if ((unsigned)wi >= (unsigned)W) continue;
+                        const f32x4 v = *(const f32x4*)(y + (((long)n * H + hi) * W + wi) * C + 4 * c4);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            float t = v[e] * a[e] + b[e];
+                            t = t > 0.f ? t : 0.f;
+                            if (bidx[e] < 0 || t > best[e] || t != t) {
+                                best[e] = t;
+                                bidx[e] = hi * W + wi;
+                            }
+                        }
+                    }
+                }
+                const f32x4 d = *(const f32x4*)(dpool + (((long)n * Ho + ho) * Wo + wo) * C + 4 * c4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    if (bidx[e] == h * W + w) acc[e] += d[e];
+            }
+        }
+        const f32x4 v = *(const f32x4*)(y + i * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float t = v[e] * a[e] + b[e];
+            if (!(t > 0.f)) acc[e] = 0.f;
+        }
+        *(f32x4*)(dz + i * 4) = acc;
+    }
+}
+
+static inline int grid_cap(long work) {
+    long g = (work + 255) / 256;
+    if (g > 4096) g = 4096;
+    return (int)(g < 1 ? 1 : g);
+}
+
+}  // namespace hkp
+
+using namespace hkp;
+
+extern "C" int64_t hkp_bn_bwd_tiles(int64_t m) { return (m + BNB_TILE - 1) / BNB_TILE; }
+
+extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
+                                 const float* mean_invstd, float* dz, float* partials, hkp_stream_t stream) {
+    HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_reduce: bad sizes");
+    HKP_CHECK_ARG(g && y && mean_invstd && partials, "hkp_bn_bwd_reduce: null tensor");
+    const int C4 = c / 4;
+    HKP_CHECK_ARG((C4 <= 256 && 256 % C4 == 0) || C4 == 512, "hkp_bn_bwd_reduce: unsupported C=%d", c);
+    const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
+    hipStream_t st = as_stream(stream);
+#define HKP_BNR(G, MK)                                                                                              \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<G, MK>), dim3((unsigned)tiles), dim3(256), 0, st, (long)m, c, g, out_mask, \
+                       y, mean_invstd, dz, partials)
+    if (C4 == 512) {
+        if (out_mask) HKP_BNR(2, true); else HKP_BNR(2, false);
+    } else {
+        if (out_mask) HKP_BNR(1, true); else HKP_BNR(1, false);
+    }
+#undef HKP_BNR
+    HKP_LAUNCH_CHECK("hkp_bn_bwd_reduce");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd,
+                                   const float* gamma, float* dgamma, float* dbeta, float* coef, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
+    const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, as_stream(stream), c, (long)m, tiles, partials,
+                       mean_invstd, gamma, dgamma, dbeta, coef);
+    HKP_LAUNCH_CHECK("hkp_bn_bwd_finalize");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
+                                const float* mean_invstd, const float* coef, float* dy, hkp_stream_t stream) {
+    HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_apply: bad sizes");
+    HKP_CHECK_ARG(g && y && mean_invstd && coef && dy, "hkp_bn_bwd_apply: null tensor");
+    const long n4 = m * (long)c / 4;
+    hipStream_t st = as_stream(stream);
+    if (out_mask)
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(grid_cap(n4)), dim3(256), 0, st, n4, c / 4,
+                           (const f32x4*)g, (const f32x4*)out_mask, (const f32x4*)y, (const f32x4*)mean_invstd,
+                           (const f32x4*)coef, (f32x4*)dy);
+    else
+        hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(grid_cap(n4)), dim3(256), 0, st, n4, c / 4,
+                           (const f32x4*)g, (const f32x4*)nullptr, (const f32x4*)y, (const f32x4*)mean_invstd,
+                           (const f32x4*)coef, (f32x4*)dy);
+    HKP_LAUNCH_CHECK("hkp_bn_bwd_apply");
+    return HKP_OK;
+}
+
+extern "C" int hkp_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, const float* dpool, const float* y,
+                               const float* scale_shift, float* dz, hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "hkp_maxpool_bwd: bad sizes");
+    HKP_CHECK_ARG(dpool && y && scale_shift && dz, "hkp_maxpool_bwd: null tensor");
+    const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+    const long work = (long)n * h * w * (c / 4);
+    hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_cap(work)), dim3(256), 0, as_stream(stream), n, h, w, c, ho, wo,
+                       dpool, y, scale_shift, dz);
+    HKP_LAUNCH_CHECK("hkp_maxpool_bwd");
+    return HKP_OK;
+}

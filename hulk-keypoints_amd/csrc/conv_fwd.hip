@@ -40,6 +40,7 @@ struct ConvArgs {
     const float* w;
     float* y;
     float* part;
+    const float* add;  // optional addend of the output (dgrad: the residual-branch gradient)
     int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
     int M;        // N*Ho*Wo
     int Kreal;    // R*S*C
@@ -52,8 +53,15 @@ constexpr int BK = 32;
 constexpr int LDR = BK + 4;  // padded LDS row (floats)
 constexpr int CONV_BM = 128;
 
-template <int BM, int BN, bool STEM>
+// MODE_FWD: NHWC forward; MODE_STEM: NCHW image + OIHW weight gather;
+// MODE_DGRAD: transposed conv (backward-data of a strided conv): the "input" is
+// dy, rows are dx pixels, and tap (r,s) reads dy[(h - pad' + r*dil)/stride] only
+// where that division is exact (weights pre-flipped by hkp_conv_weight_flip).
+enum { MODE_FWD = 0, MODE_STEM = 1, MODE_DGRAD = 2 };
+
+template <int BM, int BN, int MODE>
 __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvArgs a) {
+    constexpr bool STEM = MODE == MODE_STEM;
     constexpr int NT = 256, WM = 2, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     constexpr int AP = BM * (BK / 4) / NT;  // float4 A loads per thread
@@ -80,8 +88,8 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvArgs a) {
             const int n = m / hw, rem = m - n * hw;
             const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
             a_n[i] = n;
-            a_hi[i] = ho * a.stride - a.pad;
-            a_wi[i] = wo * a.stride - a.pad;
+            a_hi[i] = MODE == MODE_DGRAD ? ho - a.pad : ho * a.stride - a.pad;
+            a_wi[i] = MODE == MODE_DGRAD ? wo - a.pad : wo * a.stride - a.pad;
         } else {
             a_n[i] = 0;
             a_hi[i] = -(1 << 28);  // never in bounds
@@ -98,7 +106,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvArgs a) {
             const int rr = tap / a.S, ss = tap - rr * a.S;
 #pragma unroll
             for (int i = 0; i < AP; ++i) {
-                const int hi = a_hi[i] + rr * a.dil, wi = a_wi[i] + ss * a.dil;
+                int hi = a_hi[i] + rr * a.dil, wi = a_wi[i] + ss * a.dil;
+                if constexpr (MODE == MODE_DGRAD) {
+                    const bool exact = hi >= 0 && wi >= 0 && hi % a.stride == 0 && wi % a.stride == 0;
+                    hi = exact ? hi / a.stride : -1;
+                    wi = exact ? wi / a.stride : -1;
+                }
                 if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W) {
                     const long pix = ((long)a_n[i] * a.H + hi) * a.W + wi;
                     ra[i] = *(const f32x4*)(a.x + pix * a.C + c0);
@@ -198,7 +211,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                if (m < a.M) a.y[(long)m * a.K + n] = acc[i][j][r];
+                if (m < a.M) {
+                    const long off = (long)m * a.K + n;
+                    a.y[off] = a.add ? acc[i][j][r] + a.add[off] : acc[i][j][r];
+                }
             }
         }
     if (a.part == nullptr) return;
@@ -263,10 +279,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvArgs a) {
     }
 }
 
-template <int BM, int BN, bool STEM>
+template <int BM, int BN, int MODE>
 static int launch_conv(const ConvArgs& a, int m_tiles, hipStream_t st) {
     const int grid = m_tiles * a.n_tiles;
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, STEM>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, MODE>), dim3(grid), dim3(256), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd");
     return HKP_OK;
 }
@@ -315,7 +331,7 @@ extern "C" int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const floa
     const long M = (long)d->n * ho * wo;
     HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w < (1L << 31), "hkp_conv2d_fwd: tensor too large");
     ConvArgs a;
-    a.x = x; a.w = w; a.y = y; a.part = stat_partials;
+    a.x = x; a.w = w; a.y = y; a.part = stat_partials; a.add = nullptr;
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M;
@@ -328,11 +344,46 @@ extern "C" int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const floa
         HKP_CHECK_ARG(d->c % 32 == 0, "hkp_conv2d_fwd: NHWC Cin=%d must be a multiple of 32", d->c);
         a.cchunks = d->c / 32;
         a.nkc = d->r * d->s * a.cchunks;
-        return bn128 ? launch_conv<CONV_BM, 128, false>(a, m_tiles, st) : launch_conv<CONV_BM, 64, false>(a, m_tiles, st);
+        return bn128 ? launch_conv<CONV_BM, 128, MODE_FWD>(a, m_tiles, st)
+                      : launch_conv<CONV_BM, 64, MODE_FWD>(a, m_tiles, st);
     }
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NCHW, "hkp_conv2d_fwd: bad layout %d", d->in_layout);
     HKP_CHECK_ARG(d->c <= 8, "hkp_conv2d_fwd: NCHW path is the stem (Cin<=8), got %d", d->c);
     a.cchunks = 0;
     a.nkc = (a.Kreal + BK - 1) / BK;
-    return bn128 ? launch_conv<CONV_BM, 128, true>(a, m_tiles, st) : launch_conv<CONV_BM, 64, true>(a, m_tiles, st);
+    return bn128 ? launch_conv<CONV_BM, 128, MODE_STEM>(a, m_tiles, st)
+                  : launch_conv<CONV_BM, 64, MODE_STEM>(a, m_tiles, st);
+}
+
+// ---------------------------------------------------------------- dgrad ----
+extern "C" int hkp_conv2d_bwd_data(const hkp_conv_desc* d, const float* dy, const float* w_flip, const float* add, float* dx,
+                                   hkp_stream_t stream) {
+    int ho, wo;
+    int rc = conv_geometry(d, &ho, &wo);
+    if (rc) return rc;
+    HKP_CHECK_ARG(dy && w_flip && dx, "hkp_conv2d_bwd_data: null tensor");
+    HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "hkp_conv2d_bwd_data: NHWC convs only (the stem needs no dgrad)");
+    HKP_CHECK_ARG(d->c % 64 == 0 && d->k % 32 == 0, "hkp_conv2d_bwd_data: need Cin%%64==0 and Cout%%32==0");
+    const long M = (long)d->n * d->h * d->w;  // dx pixels
+    HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_data: tensor too large");
+    // dx = conv(dy, flip(w)) with pad' = dil*(R-1) - pad; strided convs use the transposed loader
+    const int padp = d->dilation * (d->r - 1) - d->pad;
+    HKP_CHECK_ARG(padp >= 0 && d->dilation * (d->s - 1) - d->pad == padp, "hkp_conv2d_bwd_data: asymmetric padding");
+    ConvArgs a;
+    a.x = dy; a.w = w_flip; a.y = dx; a.part = nullptr; a.add = add;
+    a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
+    a.stride = d->stride; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
+    a.M = (int)M;
+    a.Kreal = d->r * d->s * d->k;
+    a.cchunks = d->k / 32;
+    a.nkc = d->r * d->s * a.cchunks;
+    const bool bn128 = d->c % 128 == 0;
+    a.n_tiles = d->c / (bn128 ? 128 : 64);
+    const int m_tiles = (int)((M + CONV_BM - 1) / CONV_BM);
+    hipStream_t st = as_stream(stream);
+    if (d->stride == 1)
+        return bn128 ? launch_conv<CONV_BM, 128, MODE_FWD>(a, m_tiles, st)
+                     : launch_conv<CONV_BM, 64, MODE_FWD>(a, m_tiles, st);
+    return bn128 ? launch_conv<CONV_BM, 128, MODE_DGRAD>(a, m_tiles, st)
+                 : launch_conv<CONV_BM, 64, MODE_DGRAD>(a, m_tiles, st);
 }

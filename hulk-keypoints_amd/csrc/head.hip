@@ -13,6 +13,11 @@
 //  * hkp_gauss_target     src/dataset.py:36-44.
 #include "common.h"
 
+// Exact-arithmetic file: no implicit a*b+c → fma contraction (hipcc's default
+// -ffp-contract=fast would fuse e.g. scale*o - i0 and break bit parity with
+// ATen).  Every fused multiply-add below is an explicit __builtin_fmaf.
+#pragma clang fp contract(off)
+
 namespace hkp {
 
 // one wave per pixel; W (K x C) and bias staged in LDS
@@ -84,44 +89,57 @@ __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsig
     return a > b ? a : b;
 }
 
-// grid: x over ceil(H*W/4/256) chunks, y over n*k planes
-template <bool SIGMOID>
+__device__ __forceinline__ float bilerp(const float* r0, const float* r1, const Lerp& lh, const Lerp& lw) {
+    // ATen CPU order: t(h) = fma(x[h][w0], lw0, x[h][w1]*lw1); out = fma(t(h0), lh0, t(h1)*lh1)
+    const float t0 = __builtin_fmaf(r0[lw.i0], lw.l0, r0[lw.i1] * lw.l1);
+    const float t1 = __builtin_fmaf(r1[lw.i0], lw.l0, r1[lw.i1] * lw.l1);
+    return __builtin_fmaf(t0, lh.l0, t1 * lh.l1);
+}
+
+__device__ __forceinline__ unsigned long long argmax_key(float p, unsigned idx) {
+    // values are sigmoid outputs (>= 0, or NaN): their bit patterns order like the values,
+    // and NaN sorts highest (numpy's argmax also returns the first NaN)
+    return ((unsigned long long)__float_as_uint(p) << 32) | (unsigned long long)(0xFFFFFFFFu - idx);
+}
+
+// grid: x over ceil(H*W/1024) chunks of 4 outputs per thread, y over n*k planes.
+// ROW4: W % 4 == 0, so a thread's 4 outputs share one output row.
+template <bool SIGMOID, bool ROW4>
 __global__ __launch_bounds__(256) void upsample_sigmoid_kernel(int h, int w, int H, int W, float sh, float sw,
                                                               const float* __restrict__ low, float* __restrict__ heat,
                                                               unsigned long long* __restrict__ keys) {
     const int plane = blockIdx.y;
-    const long HW = (long)H * W;
-    const float* x = low + (long)plane * h * w;
-    const long base = ((long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const unsigned HW = (unsigned)H * (unsigned)W;
+    const float* x = low + (size_t)plane * h * w;
+    const unsigned base = (blockIdx.x * 256u + threadIdx.x) * 4u;
     unsigned long long best = 0ull;
     if (base < HW) {
         float v[4];
-        int cnt = 0;
+        if constexpr (ROW4) {
+            const unsigned oh = base / (unsigned)W, ow0 = base - oh * (unsigned)W;
+            const Lerp lh = lerp_index((int)oh, h, H, sh);
+            const float* r0 = x + lh.i0 * w;
+            const float* r1 = x + lh.i1 * w;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const long o = base + e;
-            if (o < HW) {
-                const int oh = (int)(o / W), ow = (int)(o - (long)oh * W);
-                const Lerp lh = lerp_index(oh, h, H, sh), lw = lerp_index(ow, w, W, sw);
-                const float* r0 = x + (long)lh.i0 * w;
-                const float* r1 = x + (long)lh.i1 * w;
-                const float t0 = __builtin_fmaf(r0[lw.i0], lw.l0, __fmul_rn(r0[lw.i1], lw.l1));
-                const float t1 = __builtin_fmaf(r1[lw.i0], lw.l0, __fmul_rn(r1[lw.i1], lw.l1));
-                const float z = __builtin_fmaf(t0, lh.l0, __fmul_rn(t1, lh.l1));
-                const float p = SIGMOID ? sigmoid_f(z) : z;
-                v[e] = p;
-                const unsigned long long key =
-                    ((unsigned long long)__float_as_uint(p) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned)o);
-                best = umax64(best, key);
-                ++cnt;
+            for (int e = 0; e < 4; ++e) {
+                const Lerp lw = lerp_index((int)ow0 + e, w, W, sw);
+                const float z = bilerp(r0, r1, lh, lw);
+                v[e] = SIGMOID ? sigmoid_f(z) : z;
+                best = umax64(best, argmax_key(v[e], base + e));
             }
-        }
-        if (heat) {
-            float* dst = heat + (long)plane * HW + base;
-            if (cnt == 4 && (HW & 3) == 0) {
-                *(f32x4*)dst = f32x4{v[0], v[1], v[2], v[3]};
-            } else {
-                for (int e = 0; e < cnt; ++e) dst[e] = v[e];
+            if (heat) *(f32x4*)(heat + (size_t)plane * HW + base) = f32x4{v[0], v[1], v[2], v[3]};
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const unsigned o = base + e;
+                if (o < HW) {
+                    const unsigned oh = o / (unsigned)W, ow = o - oh * (unsigned)W;
+                    const Lerp lh = lerp_index((int)oh, h, H, sh), lw = lerp_index((int)ow, w, W, sw);
+                    const float z = bilerp(x + lh.i0 * w, x + lh.i1 * w, lh, lw);
+                    v[e] = SIGMOID ? sigmoid_f(z) : z;
+                    best = umax64(best, argmax_key(v[e], o));
+                    if (heat) heat[(size_t)plane * HW + o] = v[e];
+                }
             }
         }
     }
@@ -130,9 +148,8 @@ __global__ __launch_bounds__(256) void upsample_sigmoid_kernel(int h, int w, int
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             const unsigned ol = __shfl_xor(lo, off), oh = __shfl_xor(hi, off);
-            const unsigned long long other = ((unsigned long long)oh << 32) | ol;
-            const unsigned long long mine = ((unsigned long long)hi << 32) | lo;
-            const unsigned long long m = umax64(mine, other);
+            const unsigned long long m =
+                umax64(((unsigned long long)hi << 32) | lo, ((unsigned long long)oh << 32) | ol);
             lo = (unsigned)m;
             hi = (unsigned)(m >> 32);
         }
@@ -196,7 +213,7 @@ extern "C" int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, 
     HKP_CHECK_ARG(lowres != nullptr, "hkp_upsample_sigmoid: null lowres");
     HKP_CHECK_ARG(argmax_yx == nullptr || argmax_ws != nullptr, "hkp_upsample_sigmoid: argmax needs workspace");
     HKP_CHECK_ARG(argmax_yx == nullptr || apply_sigmoid, "hkp_upsample_sigmoid: argmax keys need sigmoid outputs");
-    HKP_CHECK_ARG((long)H * W < 0xFFFFFFFFL, "hkp_upsample_sigmoid: plane too large");
+    HKP_CHECK_ARG((long)H * W < 0x7FFFFFFFL && (long)h * w < 0x7FFFFFFFL, "hkp_upsample_sigmoid: plane too large");
     hipStream_t st = as_stream(stream);
     const int nk = n * k;
     unsigned long long* keys = argmax_yx ? (unsigned long long*)argmax_ws : nullptr;
@@ -212,11 +229,15 @@ extern "C" int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, 
     const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
     const long HW = (long)H * W;
     dim3 grid((unsigned)((HW + 1023) / 1024), (unsigned)nk);
-    if (apply_sigmoid)
-        hipLaunchKernelGGL(upsample_sigmoid_kernel<true>, grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat, keys);
-    else
-        hipLaunchKernelGGL(upsample_sigmoid_kernel<false>, grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat,
-                           keys);
+    const bool row4 = (W & 3) == 0;
+#define HKP_UPS(SG, R4) \
+    hipLaunchKernelGGL((upsample_sigmoid_kernel<SG, R4>), grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat, keys)
+    if (apply_sigmoid) {
+        if (row4) HKP_UPS(true, true); else HKP_UPS(true, false);
+    } else {
+        if (row4) HKP_UPS(false, true); else HKP_UPS(false, false);
+    }
+#undef HKP_UPS
     HKP_LAUNCH_CHECK("hkp_upsample_sigmoid");
     if (keys) {
         hipLaunchKernelGGL(argmax_decode_kernel, dim3((nk + 255) / 256), dim3(256), 0, st, nk, W, keys, argmax_yx);

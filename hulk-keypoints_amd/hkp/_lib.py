@@ -44,6 +44,21 @@ SIGNATURES = {
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
+    # backward
+    "hkp_conv_weight_flip": (ctypes.c_int, [_CD, _P, _P, _P]),
+    "hkp_conv2d_bwd_data": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
+    "hkp_conv_bwd_filter_workspace": (_I64, [_CD]),
+    "hkp_conv2d_bwd_filter": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _I64, _P]),
+    "hkp_bn_bwd_tiles": (_I64, [_I64]),
+    "hkp_bn_bwd_reduce": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_finalize": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "hkp_heat_loss_workspace": (_I64, []),
+    "hkp_heat_loss": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _P, _P, _P, _P]),
+    "hkp_head_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "hkp_head_fc_bwd_workspace": (_I64, [_I32, _I32, _I32, _I32]),
+    "hkp_head_fc_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
 }
 
 _lib = None

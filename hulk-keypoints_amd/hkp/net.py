@@ -115,6 +115,90 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
     return hm, yx, low
 
 
+class Grads(dict):
+    """param → gradient tensor, filled in reverse layer order.  ``on_ready`` (if
+    set) is called for each parameter as soon as its gradient exists — the DP
+    bucketer hooks in here to overlap RCCL all-reduce with the rest of backward."""
+
+    def __init__(self, on_ready=None):
+        super().__init__()
+        self.on_ready = on_ready
+
+    def put(self, p, g):
+        self[p] = g
+        if self.on_ready is not None:
+            self.on_ready(p, g)
+
+
+def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
+    """wgrad (+ dgrad with the residual addend fused) for one NHWC conv."""
+    st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
+    dx = None
+    if need_dx:
+        wf = ops.conv_weight_flip(conv.weight)
+        dx = ops.conv2d_bwd_data(dy, wf, tuple(x.shape), st, pd, dl, add=add)
+    grads.put(conv.weight, ops.conv2d_bwd_filter(x, dy, tuple(conv.weight.shape), st, pd, dl))
+    return dx
+
+
+def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False):
+    dy, dgamma, dbeta, dz = ops.bn_bwd(g, out_mask, y, mi, bn.weight, want_dz=want_dz)
+    grads.put(bn.weight, dgamma)
+    grads.put(bn.bias, dbeta)
+    return dy, dz
+
+
+def block_backward(block, rec, g_out, grads):
+    """Reverse of block_forward: g_out = dL/d(block output) → dL/d(block input)."""
+    out, x = rec["out"], rec["x"]
+    ys, mis, acts = rec["y"], rec["mi"], rec["act"]
+    bns = [block.bn1, block.bn2] + ([block.bn3] if block.kind == "bottleneck" else [])
+    convs = [block.conv1, block.conv2] + ([block.conv3] if block.kind == "bottleneck" else [])
+    # last BN: relu mask from the block output; keep dz for the residual branch
+    g, dz = _bn_backward(bns[-1], g_out, out, ys[-1], mis[-1], grads, want_dz=True)
+    if block.downsample is not None:
+        gd, _ = _bn_backward(block.downsample[1], dz, None, rec["yd"], rec["md"], grads)
+        dx_res = _conv_backward(block.downsample[0], x, gd, grads)
+    else:
+        dx_res = dz
+    # main path, last conv first; inner BN masks come from the stored activations
+    for li in range(len(convs) - 1, 0, -1):
+        da = _conv_backward(convs[li], acts[li - 1], g, grads)
+        g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads)
+    return _conv_backward(convs[0], x, g, grads, add=dx_res)
+
+
+def stem_backward(resnet, st, g_pool, grads):
+    dz = ops.maxpool_bwd(g_pool, st["y"], st["ss"])
+    dy, _ = _bn_backward(resnet.bn1, dz, None, st["y"], st["mi"], grads)
+    c = resnet.conv1
+    grads.put(c.weight, ops.conv2d_bwd_filter(st["x"], dy, tuple(c.weight.shape), _i(c.stride), _i(c.padding),
+                                              _i(c.dilation), layout="nchw"))
+
+
+def keypoints_backward(resnet, trace, dheat, grads):
+    """dL/dheat → every parameter gradient (model.py:19-22 backward)."""
+    hd = trace.head
+    k = hd["k"]
+    feat, low = hd["feat"], hd["low"]
+    dlow = ops.head_bwd(dheat.contiguous(), hd["heat"], low.shape[2], low.shape[3])
+    w, _ = fc_rows(resnet, k)
+    dfeat, dw, db = ops.head_fc_bwd(dlow, feat, w)
+    fcw, fcb = resnet.fc.weight, resnet.fc.bias
+    gw = torch.zeros_like(fcw)   # rows >= K: exactly zero loss gradient (SURVEY §7)
+    gw.view(fcw.shape[0], -1)[:k] = dw
+    gb = torch.zeros_like(fcb)
+    gb[:k] = db
+    grads.put(fcw, gw)
+    grads.put(fcb, gb)
+    g = dfeat
+    for rec, block in zip(reversed(trace.blocks), reversed([b for l in (resnet.layer1, resnet.layer2, resnet.layer3,
+                                                                           resnet.layer4) for b in l])):
+        g = block_backward(block, rec, g, grads)
+    stem_backward(resnet, trace.stem, g, grads)
+    return grads
+
+
 def logits_forward(resnet, x_nchw, num_outputs=None):
     """Resnet34_8s.forward (resnet_dilated.py:24-28): upsampled raw fc logits,
     [B, num_outputs (default 1000), H, W]; computed 16 channels at a time."""

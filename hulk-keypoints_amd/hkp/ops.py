@@ -174,3 +174,153 @@ def gauss_target(uv, H, W, sigma):
     out = torch.empty((n, k, H, W), device=uv.device, dtype=torch.float64)
     call("hkp_gauss_target", n, k, H, W, float(sigma), _ptr(uv), _ptr(out), _stream())
     return out
+
+
+# ------------------------------------------------------------------ backward
+
+
+def _fwd_desc(x_shape, w_shape, stride, pad, dil, layout):
+    if layout == "nhwc":
+        n, h, wd, c = x_shape
+        k, r, s, _ = w_shape
+        lay = HKP_LAYOUT_NHWC
+    else:
+        n, c, h, wd = x_shape
+        k, _, r, s = w_shape
+        lay = HKP_LAYOUT_NCHW
+    return ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, lay)
+
+
+def conv_weight_flip(w):
+    """KRSC [K,R,S,C] → flipped CRSK [C,R,S,K] (the dgrad weight)."""
+    _need(w, torch.float32, "conv_weight_flip.w", 4)
+    k, r, s, c = w.shape
+    d = ConvDesc(1, 1, 1, c, k, r, s, 1, 0, 1, HKP_LAYOUT_NHWC)
+    wf = torch.empty((c, r, s, k), device=w.device, dtype=torch.float32)
+    call("hkp_conv_weight_flip", ctypes.byref(d), _ptr(w), _ptr(wf), _stream())
+    return wf
+
+
+def conv2d_bwd_data(dy, w_flip, x_shape, stride=1, pad=0, dil=1, add=None):
+    """dL/dx (NHWC) of conv2d_fwd; ``add`` (same shape as x, nullable) is summed in."""
+    _need(dy, torch.float32, "conv2d_bwd_data.dy", 4)
+    _need(w_flip, torch.float32, "conv2d_bwd_data.w_flip", 4)
+    c, r, s, k = w_flip.shape
+    d = _fwd_desc(x_shape, (k, r, s, c), stride, pad, dil, "nhwc")
+    ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, stride, pad, dil)
+    if tuple(dy.shape) != (x_shape[0], ho, wo, k):
+        raise HkpError("conv2d_bwd_data: dy shape %s != %s" % (tuple(dy.shape), (x_shape[0], ho, wo, k)))
+    if add is not None:
+        _need(add, torch.float32, "conv2d_bwd_data.add", 4)
+        if tuple(add.shape) != tuple(x_shape):
+            raise HkpError("conv2d_bwd_data: add shape mismatch")
+    dx = torch.empty(tuple(x_shape), device=dy.device, dtype=torch.float32)
+    call("hkp_conv2d_bwd_data", ctypes.byref(d), _ptr(dy), _ptr(w_flip), _ptr(add), _ptr(dx), _stream())
+    return dx
+
+
+def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out=None, accumulate=False):
+    """dL/dw in the weight's own layout (KRSC, or OIHW for the NCHW stem)."""
+    _need(x, torch.float32, "conv2d_bwd_filter.x", 4)
+    _need(dy, torch.float32, "conv2d_bwd_filter.dy", 4)
+    d = _fwd_desc(tuple(x.shape), tuple(w_shape), stride, pad, dil, layout)
+    ho, wo = conv_out_hw(d.h, d.w, d.r, d.s, stride, pad, dil)
+    if tuple(dy.shape) != (d.n, ho, wo, d.k):
+        raise HkpError("conv2d_bwd_filter: dy shape %s != %s" % (tuple(dy.shape), (d.n, ho, wo, d.k)))
+    from ._lib import lib
+    nbytes = lib().hkp_conv_bwd_filter_workspace(ctypes.byref(d))
+    ws = torch.empty(max(nbytes, 4) // 4, device=x.device, dtype=torch.float32)
+    dw = out if out is not None else torch.empty(tuple(w_shape), device=x.device, dtype=torch.float32)
+    _need(dw, torch.float32, "conv2d_bwd_filter.dw")
+    call("hkp_conv2d_bwd_filter", ctypes.byref(d), _ptr(x), _ptr(dy), _ptr(dw), int(bool(accumulate)), _ptr(ws),
+         nbytes, _stream())
+    return dw
+
+
+def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False):
+    """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None)."""
+    _need(g, torch.float32, "bn_bwd.g")
+    _need(y, torch.float32, "bn_bwd.y")
+    if g.shape != y.shape or (out_mask is not None and out_mask.shape != y.shape):
+        raise HkpError("bn_bwd: shape mismatch")
+    c = y.shape[-1]
+    m = y.numel() // c
+    from ._lib import lib
+    tiles = lib().hkp_bn_bwd_tiles(m)
+    part = torch.empty((tiles, c, 2), device=y.device, dtype=torch.float32)
+    dz = torch.empty_like(y) if want_dz else None
+    call("hkp_bn_bwd_reduce", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(dz), _ptr(part),
+         _stream())
+    dgamma = torch.empty(c, device=y.device, dtype=torch.float32)
+    dbeta = torch.empty(c, device=y.device, dtype=torch.float32)
+    coef = torch.empty(3 * c, device=y.device, dtype=torch.float32)
+    call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta),
+         _ptr(coef), _stream())
+    dy = torch.empty_like(y)
+    call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), _ptr(dy),
+         _stream())
+    return dy, dgamma, dbeta, dz
+
+
+def maxpool_bwd(dpool, y, ss):
+    """Stem: dL/d(BN output) from dL/d(maxpool output) (ReLU mask applied)."""
+    _need(dpool, torch.float32, "maxpool_bwd.dpool", 4)
+    _need(y, torch.float32, "maxpool_bwd.y", 4)
+    n, h, w, c = y.shape
+    if tuple(dpool.shape) != (n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c):
+        raise HkpError("maxpool_bwd: dpool shape mismatch")
+    dz = torch.empty_like(y)
+    call("hkp_maxpool_bwd", n, h, w, c, _ptr(dpool), _ptr(y), _ptr(ss), _ptr(dz), _stream())
+    return dz
+
+
+def heat_loss(heat, target=None, uv=None, sigma=8.0, kind="bce", want_grad=True):
+    """fp64 BCE/MSE over [N,K,H,W] heatmaps → (loss 0-dim f64 tensor, dheat f32 or None)."""
+    from ._lib import HKP_LOSS_BCE, HKP_LOSS_MSE, lib
+    _need(heat, torch.float32, "heat_loss.heat", 4)
+    n, k, H, W = heat.shape
+    if target is not None:
+        _need(target, torch.float64, "heat_loss.target", 4)
+        if target.shape != heat.shape:
+            raise HkpError("heat_loss: target shape %s != %s" % (tuple(target.shape), tuple(heat.shape)))
+    else:
+        _need(uv, torch.float32, "heat_loss.uv", 3)
+        if tuple(uv.shape) != (n, k, 2):
+            raise HkpError("heat_loss: uv must be [N,K,2]")
+    ws = torch.empty(lib().hkp_heat_loss_workspace() // 8, device=heat.device, dtype=torch.float64)
+    loss = torch.empty((), device=heat.device, dtype=torch.float64)
+    dheat = torch.empty_like(heat) if want_grad else None
+    call("hkp_heat_loss", n, k, H, W, HKP_LOSS_BCE if kind == "bce" else HKP_LOSS_MSE, _ptr(heat), _ptr(target),
+         _ptr(uv), float(sigma), _ptr(loss), _ptr(dheat), _ptr(ws), _stream())
+    return loss, dheat
+
+
+def head_bwd(dheat, heat, h, w):
+    """dlow [N,K,h,w] = upsample-adjoint(dheat * (1-heat) * heat)."""
+    _need(dheat, torch.float32, "head_bwd.dheat", 4)
+    n, k, H, W = dheat.shape
+    if heat is not None and heat.shape != dheat.shape:
+        raise HkpError("head_bwd: heat shape mismatch")
+    dlow = torch.empty((n, k, h, w), device=dheat.device, dtype=torch.float32)
+    call("hkp_head_bwd", n, k, h, w, H, W, _ptr(dheat), _ptr(heat), _ptr(dlow), _stream())
+    return dlow
+
+
+def head_fc_bwd(dlow, feat, w_kc):
+    """→ (dfeat NHWC, dW [K,C], db [K])."""
+    from ._lib import lib
+    _need(dlow, torch.float32, "head_fc_bwd.dlow", 4)
+    _need(feat, torch.float32, "head_fc_bwd.feat", 4)
+    _need(w_kc, torch.float32, "head_fc_bwd.w", 2)
+    n, h, w, c = feat.shape
+    k = dlow.shape[1]
+    if tuple(dlow.shape) != (n, k, h, w) or tuple(w_kc.shape) != (k, c):
+        raise HkpError("head_fc_bwd: shape mismatch")
+    nbytes = lib().hkp_head_fc_bwd_workspace(n, h * w, c, k)
+    ws = torch.empty(nbytes // 4, device=feat.device, dtype=torch.float32)
+    dfeat = torch.empty_like(feat)
+    dw = torch.empty((k, c), device=feat.device, dtype=torch.float32)
+    db = torch.empty(k, device=feat.device, dtype=torch.float32)
+    call("hkp_head_fc_bwd", n, h * w, c, k, _ptr(dlow), _ptr(feat), _ptr(w_kc), _ptr(dfeat), _ptr(dw), _ptr(db),
+         _ptr(ws), nbytes, _stream())
+    return dfeat, dw, db

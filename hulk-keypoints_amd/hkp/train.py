@@ -1,0 +1,107 @@
+"""Training step (train.py:32-36 restated for the MI355X path) and data parallelism.
+
+Trainer.step = forward (kernel walk, Trace kept) → fused fp64 loss kernel
+(dL/dheat) → backward kernels (net.keypoints_backward) → [RCCL all-reduce of
+gradients, bucketed and overlapped with the rest of backward] → Adam
+(lr 1e-4, weight_decay 1e-4, train.py:79; the optimizer stays PyTorch as the
+north star asks).
+
+Data parallelism: one process per GPU (torchrun), torch.distributed backend
+"nccl" = RCCL over xGMI.  Gradients land in flat per-bucket buffers in the
+order backward produces them (fc, layer4, …, stem); as soon as a bucket is
+complete its all-reduce is launched asynchronously, so communication of the
+late layers overlaps the backward of the early ones.  BatchNorm statistics
+stay per rank (standard DDP semantics).
+"""
+import torch
+import torch.distributed as dist
+
+from . import net, ops
+
+
+class GradBucketer:
+    """Bucketed, overlapped gradient all-reduce (mean over ranks)."""
+
+    def __init__(self, params, bucket_bytes=32 << 20, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # backward produces grads roughly in reverse parameter order
+        order = list(reversed(list(params)))
+        self.buckets = []
+        cur, cur_bytes = [], 0
+        for p in order:
+            cur.append(p)
+            cur_bytes += p.numel() * 4
+            if cur_bytes >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, cur_bytes = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.slot = {}
+        self.flat = []
+        for bi, ps in enumerate(self.buckets):
+            n = sum(p.numel() for p in ps)
+            flat = torch.zeros(n, device=ps[0].device, dtype=torch.float32)
+            off = 0
+            for p in ps:
+                self.slot[p] = (bi, off)
+                off += p.numel()
+            self.flat.append(flat)
+        self._reset()
+
+    def _reset(self):
+        self.pending = [len(ps) for ps in self.buckets]
+        self.works = [None] * len(self.buckets)
+
+    def ready(self, p, g):
+        bi, off = self.slot[p]
+        self.flat[bi][off:off + p.numel()].copy_(g.reshape(-1))
+        self.pending[bi] -= 1
+        if self.pending[bi] == 0 and self.world > 1:
+            self.works[bi] = dist.all_reduce(self.flat[bi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+
+    def finish(self):
+        """Wait for every bucket; average; point p.grad at the flat buffers."""
+        if any(self.pending):
+            raise RuntimeError("gradient missing for %d parameters" % sum(self.pending))
+        for bi, w in enumerate(self.works):
+            if w is not None:
+                w.wait()
+            if self.world > 1:
+                self.flat[bi].mul_(1.0 / self.world)
+        for p, (bi, off) in self.slot.items():
+            p.grad = self.flat[bi][off:off + p.numel()].view_as(p)
+        self._reset()
+
+
+class Trainer:
+    """One optimizer step per call, reference semantics (train.py:33-36)."""
+
+    def __init__(self, model, lr=1e-4, weight_decay=1e-4, loss="bce", sigma=8.0, distributed=False,
+                 bucket_mb=32):
+        self.model = model
+        self.params = list(model.parameters())
+        self.loss_kind = loss
+        self.sigma = sigma
+        self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay)
+        use_dp = distributed and dist.is_initialized() and dist.get_world_size() > 1
+        self.bucketer = GradBucketer(self.params, bucket_mb << 20) if use_dp else None
+
+    def forward_backward(self, x, uv=None, target=None):
+        m = self.model
+        trace = net.Trace()
+        hm, _, _ = net.keypoints_forward(m.resnet.net, x, m.num_keypoints, heat=True, trace=trace)
+        loss, dheat = ops.heat_loss(hm, target, uv, self.sigma, self.loss_kind, want_grad=True)
+        grads = net.Grads(on_ready=self.bucketer.ready if self.bucketer else None)
+        net.keypoints_backward(m.resnet.net, trace, dheat, grads)
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        else:
+            for p in self.params:
+                p.grad = grads[p]
+        return loss
+
+    def step(self, x, uv=None, target=None):
+        loss = self.forward_backward(x, uv, target)
+        self.opt.step()
+        return loss

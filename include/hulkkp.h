@@ -122,6 +122,64 @@ int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, 
 int hkp_gauss_target(int32_t n, int32_t k, int32_t H, int32_t W, float sigma, const float* uv,
                      double* out, hkp_stream_t stream);
 
+/* ============================================================ backward ==== */
+/* Everything loss.backward() (train.py:35) runs through the reference's
+ * modules, as hand-written kernels.  d = the FORWARD conv descriptor. */
+
+/* w_flip[c][r][s][k] = w[k][R-1-r][S-1-s][c]: the dgrad weight (KRSC in → CRSK-flipped out). */
+int hkp_conv_weight_flip(const hkp_conv_desc* d, const float* w, float* w_flip, hkp_stream_t stream);
+
+/* dx[n,h,w,c] = sum over taps/k of dy * w (+ add[n,h,w,c], nullable: fuses the
+ * residual-branch gradient sum): backward-data of hkp_conv2d_fwd (NHWC convs;
+ * strided convs take the transposed-loader path).  w_flip from hkp_conv_weight_flip. */
+int hkp_conv2d_bwd_data(const hkp_conv_desc* d, const float* dy, const float* w_flip, const float* add, float* dx,
+                        hkp_stream_t stream);
+
+/* dw (KRSC, or OIHW for the stem) = sum over pixels of dy x im2col(x); split-K over
+ * pixels into `workspace`, reduced in fixed order.  accumulate != 0 adds into dw. */
+int64_t hkp_conv_bwd_filter_workspace(const hkp_conv_desc* d);
+int hkp_conv2d_bwd_filter(const hkp_conv_desc* d, const float* x, const float* dy, float* dw, int32_t accumulate,
+                          void* workspace, int64_t ws_bytes, hkp_stream_t stream);
+
+/* Train-mode BatchNorm backward, three launches:
+ *   reduce:   dz = g * (out_mask > 0) (out_mask NULL: dz = g), optionally stored to dz;
+ *             partials[tiles][c][2] = (sum dz, sum dz*(y-mean)); tiles = hkp_bn_bwd_tiles(m)
+ *   finalize: dgamma = invstd*sum dz*(y-mean), dbeta = sum dz (nullable), coef[3c]
+ *   apply:    dy = ((dz - sum dz/m) - (y-mean)*invstd^2*sum dz*(y-mean)/m) * invstd*gamma
+ * mean_invstd is what hkp_bn_finalize produced in the forward. */
+int64_t hkp_bn_bwd_tiles(int64_t m);
+int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
+                      const float* mean_invstd, float* dz, float* partials, hkp_stream_t stream);
+int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd, const float* gamma,
+                        float* dgamma, float* dbeta, float* coef, hkp_stream_t stream);
+int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
+                     const float* mean_invstd, const float* coef, float* dy, hkp_stream_t stream);
+
+/* Stem: backward of maxpool3x3/s2/p1(relu(y*scale+shift)) → dz = dL/d(BN output),
+ * ReLU mask applied (src/resnet.py:200-202; ATen's first-max window rule). */
+int hkp_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, const float* dpool, const float* y,
+                    const float* scale_shift, float* dz, hkp_stream_t stream);
+
+/* Loss over the heatmaps (train.py:21,25; MSE train.py:13) in fp64: loss (device
+ * double), dheat = dL/dheat as fp32 (nullable).  Target: dense fp64 `target`
+ * [n,k,H,W], or NULL to recompute the Gaussian from uv/sigma (dataset.py:36-44).
+ * workspace: hkp_heat_loss_workspace() bytes. */
+int64_t hkp_heat_loss_workspace(void);
+int hkp_heat_loss(int32_t n, int32_t k, int32_t H, int32_t W, int32_t loss_kind, const float* heat,
+                  const double* target, const float* uv, float sigma, double* loss, float* dheat, void* workspace,
+                  hkp_stream_t stream);
+
+/* dlow = upsample-adjoint( dheat * (1-heat) * heat ) (sigmoid backward fused;
+ * heat NULL = dheat is already the pre-sigmoid gradient). */
+int hkp_head_bwd(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, int32_t W, const float* dheat,
+                 const float* heat, float* dlow, hkp_stream_t stream);
+
+/* fc (K used rows) backward: dfeat NHWC [n,hw,c], dw [k][c], db [k]. */
+int64_t hkp_head_fc_bwd_workspace(int32_t n, int32_t hw, int32_t c, int32_t k);
+int hkp_head_fc_bwd(int32_t n, int32_t hw, int32_t c, int32_t k, const float* dlow, const float* feat,
+                    const float* w, float* dfeat, float* dw, float* db, void* workspace, int64_t ws_bytes,
+                    hkp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -208,6 +208,29 @@ def param_keys(backbone):
     return [k for k, _, kind in state_dict_spec(backbone) if not kind.startswith("bn_") or kind in ("bn_weight", "bn_bias")]
 
 
+class OracleTrainer:
+    """Stateful fit loop (train.py:32-36): persistent parameters and Adam state."""
+
+    def __init__(self, sd, backbone, num_keypoints, lr=1e-4, weight_decay=1e-4, head="faithful"):
+        self.sd, self.bb, self.k, self.head = sd, backbone, num_keypoints, head
+        self.keys = param_keys(backbone)
+        self.params = OrderedDict((k, sd[k].detach().clone().requires_grad_(True)) for k in self.keys)
+        self.opt = torch.optim.Adam(list(self.params.values()), lr=lr, weight_decay=weight_decay)
+
+    def step(self, x, uv, sigma=8, loss="bce"):
+        work = OrderedDict(self.sd)
+        work.update(self.params)
+        self.opt.zero_grad()
+        pred = forward(work, x, self.bb, self.k, "train", self.head)
+        gt = gauss_target(uv, x.shape[2], x.shape[3], sigma).to(pred.dtype if pred.dtype == torch.float64
+                                                                 else torch.float64)
+        L = bce_loss(pred, gt) if loss == "bce" else mse_loss(pred, gt)
+        L.backward()
+        grads = OrderedDict((k, self.params[k].grad.detach().clone()) for k in self.keys)
+        self.opt.step()
+        return L.detach(), grads
+
+
 def train_step(sd, x, uv, backbone="resnet18", num_keypoints=2, sigma=8, loss="bce", lr=1e-4,
                weight_decay=1e-4, adam_state=None, head="faithful"):
     """One reference training iteration (train.py:33-36): zero_grad → forward →
