@@ -1,0 +1,83 @@
+"""MI355X-native restatement of src/prediction.py (Prediction, :8-66).
+
+predict() is the reference's (:16-24).  keypoints() is the fused decode the
+north star asks for: the argmax of plot() (:46, np.unravel_index(h.argmax()),
+first max wins) computed on the GPU inside the upsample kernel, so no
+[B,K,H,W] heatmap has to cross PCIe.  plot() keeps the reference's output
+(JET overlays in a 2-column grid written to preds/out%04d.png) using numpy/PIL
+when OpenCV is absent; expectation() keeps the reference's (dead, :45) math.
+"""
+import os
+
+import numpy as np
+import torch
+
+
+class Prediction:
+    def __init__(self, model, num_keypoints, img_height, img_width, use_cuda):
+        self.model = model
+        self.num_keypoints = num_keypoints
+        self.img_height = img_height
+        self.img_width = img_width
+        self.use_cuda = use_cuda
+
+    @staticmethod
+    def _batch(imgs):
+        if len(imgs.shape) == 4:
+            return imgs.view(-1, imgs.shape[1], imgs.shape[2], imgs.shape[3])
+        if len(imgs.shape) == 3:
+            return imgs.view(-1, imgs.shape[0], imgs.shape[1], imgs.shape[2])
+        return imgs
+
+    def predict(self, imgs):
+        # img: torch.Tensor(3, height, width) or (B, 3, height, width)
+        return self.model.forward(self._batch(imgs))
+
+    def keypoints(self, imgs):
+        """int32 [B,K,2] (y, x) argmax per heatmap, computed on the GPU."""
+        return self.model.predict_keypoints(self._batch(imgs))
+
+    def softmax(self, x):
+        e_x = np.exp(x - np.max(x))
+        return e_x / e_x.sum()
+
+    def expectation(self, d):
+        """prediction.py:31-38, vectorised (same values, including its index mapping)."""
+        width, height = d.T.shape
+        d = d.T.ravel()
+        d_norm = self.softmax(d)
+        i = np.arange(width * height)
+        return [int(np.dot(d_norm, i % width)), int(np.dot(d_norm, i // width))]
+
+    @staticmethod
+    def _jet(u8):
+        x = u8.astype(np.float32) / 255.0
+        r = np.clip(1.5 - np.abs(4 * x - 3), 0, 1)
+        g = np.clip(1.5 - np.abs(4 * x - 2), 0, 1)
+        b = np.clip(1.5 - np.abs(4 * x - 1), 0, 1)
+        return (np.stack([b, g, r], -1) * 255).astype(np.uint8)  # BGR like cv2.COLORMAP_JET
+
+    def plot(self, img, heatmap, image_id=0, cls=None, classes=None, keypoints=None, out_dir="preds"):
+        print("Running inferences on image: %d" % image_id)
+        overlays = []
+        for i in range(self.num_keypoints):
+            h = heatmap[0][i]
+            if keypoints is not None:
+                pred_y, pred_x = (int(v) for v in keypoints[0][i])
+            else:
+                pred_y, pred_x = np.unravel_index(h.argmax(), h.shape)
+            span = max(float(h.max() - h.min()), 1e-12)
+            vis = self._jet(((h - h.min()) / span * 255).astype(np.uint8))
+            overlay = (0.65 * img.astype(np.float32) + 0.35 * vis.astype(np.float32)).astype(np.uint8)
+            y0, y1 = max(0, pred_y - 4), min(overlay.shape[0], pred_y + 5)
+            x0, x1 = max(0, pred_x - 4), min(overlay.shape[1], pred_x + 5)
+            overlay[y0:y1, x0:x1] = 0
+            overlays.append(overlay)
+        half = self.num_keypoints // 2
+        col1 = np.concatenate(overlays[:half], 0) if half else None
+        col2 = np.concatenate(overlays[half:], 0)
+        result = col2 if col1 is None else np.concatenate([col1, col2], 1)
+        os.makedirs(out_dir, exist_ok=True)
+        from PIL import Image
+        Image.fromarray(result[:, :, ::-1]).save(os.path.join(out_dir, "out%04d.png" % image_id))
+        return result
