@@ -27,6 +27,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+PEAK_FP16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense (spec)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -41,6 +42,8 @@ def parse():
     ap.add_argument("--keypoints", type=int, default=4)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f16"], default=None,
+                    help="NHWC conv arithmetic (default: f16x3 = fp32-accurate split fp16 MFMA)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
     return ap.parse_args()
@@ -140,6 +143,9 @@ def main():
     from oracle import recipe  # synthetic inputs (seeded images / keypoints only)
 
     hkp.lib()
+    from hkp import net as hkp_net
+    precision = args.precision or "f16x3"
+    hkp_net.set_conv_precision(precision)
     B, K, H, W = args.batch, args.keypoints, args.height, args.width
     torch.manual_seed(1234 + rank)
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False).to(dev)
@@ -196,22 +202,30 @@ def main():
         return
     # dominant kernel = the conv symbol with the most event-timed time
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
-    achieved = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12
+    alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
+    if dom_sym.startswith("conv_split_kernel"):
+        passes = int(dom_sym.rstrip(">").split(",")[-1])
+        achieved, peak = alg * passes, PEAK_FP16_MFMA_TFLOPS    # issued fp16 MFMA FLOPs vs dense fp16 peak
+    else:
+        passes, achieved, peak = 0, alg, PEAK_FP32_MFMA_TFLOPS
     all_ms = sum(v[3] for v in agg.values())
     all_fl = sum(v[1] for v in agg.values())
+    dtype = {"fp32": "f32", "f16x3": "f32 (f16x3 split-precision MFMA, fp32-accurate)", "f16": "f16"}[precision]
     out = {
         "metric": "images/sec (640x480, N keypoints) inference+train at 1/2/4/8 MI355X",
         "value": value, "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32", "data": "synthetic (seeded uint8 BGR images; random-init weights)",
+        "vs_baseline": None, "dtype": dtype, "data": "synthetic (seeded uint8 BGR images; random-init weights)",
         "config": {"workload": "%s %s-8s K=%d %dx%d batch %d/GPU (%s)" % (
             "inference (C2)" if args.mode == "infer" else "training step (C3 shard)", args.backbone, K, W, H, B,
             "train-mode BN, fused K-ch head, heatmap + argmax" if args.mode == "infer"
             else "BCE fp64, Adam lr1e-4 wd1e-4"),
             "mode": args.mode, "backbone": args.backbone, "keypoints": K, "height": H, "width": W,
             "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world},
-        "roofline": {"bound": "mfma", "kernel": dom_sym, "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+        "roofline": {"bound": "mfma", "kernel": dom_sym, "achieved": achieved, "peak": peak,
+                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                     "fp32_equivalent_tflops": alg, "frac_of_fp32_mfma_peak": alg / PEAK_FP32_MFMA_TFLOPS,
+                     "mfma_passes_per_fp32_mac": passes or 1,
                      "launches_per_step": cnt // max(3, min(args.steps, 10)),
                      "avg_launch_ms": ms / cnt, "algorithmic_gflop_per_launch": fl / cnt / 1e9,
                      "all_convs_tflops": all_fl / (all_ms * 1e-3) / 1e12,

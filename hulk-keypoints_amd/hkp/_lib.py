@@ -44,8 +44,10 @@ SIGNATURES = {
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
+    "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),
+    "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _P, _P]),
     # backward
-    "hkp_conv_weight_flip": (ctypes.c_int, [_CD, _P, _P, _P]),
+    "hkp_conv_weight_flip":(ctypes.c_int, [_CD, _P, _P, _P]),
     "hkp_conv2d_bwd_data": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
     "hkp_conv_bwd_filter_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _I64, _P]),

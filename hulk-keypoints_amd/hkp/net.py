@@ -10,6 +10,8 @@ Forward per BasicBlock (src/resnet.py:53-69), train-mode BN:
     [yd = ds_conv(x); sd = bn_finalize(ds_bn)]
     out = relu(y2*s2 + (x | yd*sd))
 """
+import os
+
 import torch
 
 from . import ops
@@ -38,10 +40,48 @@ def _i(v):
     return v[0] if isinstance(v, (tuple, list)) else v
 
 
+# Conv arithmetic for the NHWC convs (the stem always runs the fp32 gather kernel):
+#   "fp32"  v_mfma_f32_32x32x2_f32, exact fp32 products
+#   "f16x3" split-precision fp16 MFMA, fp32-accurate (~2^-22 per product)
+#   "f16"   plain fp16 operands, fp32 accumulation (BASELINE config C4)
+PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
+_precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
+_split_cache = {}
+
+
+def set_conv_precision(p):
+    global _precision
+    if p not in PRECISIONS:
+        raise ValueError("precision must be one of %s" % sorted(PRECISIONS))
+    _precision = p
+
+
+def conv_precision():
+    return _precision
+
+
+def _split_weight(w, passes):
+    """Cached hi/lo fp16 split of a weight; refreshed whenever the parameter changes
+    (optimizer steps and load_state_dict bump its version counter)."""
+    key = (id(w), passes)
+    ent = _split_cache.get(key)
+    if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+        hi, lo = ops.weight_split(w.detach(), passes)
+        ent = (w._version, w.data_ptr(), hi, lo)
+        _split_cache[key] = ent
+    return ent[2], ent[3]
+
+
 def conv_bn(conv, bn, x, layout="nhwc"):
     """conv (+ BN partials when training) → (y, scale_shift, mean_invstd)."""
-    y, part = ops.conv2d_fwd(x, conv.weight, _i(conv.stride), _i(conv.padding), _i(conv.dilation), layout=layout,
-                             stats=bn.training)
+    passes = PRECISIONS[_precision]
+    if layout == "nhwc" and passes:
+        hi, lo = _split_weight(conv.weight, passes)
+        y, part = ops.conv2d_fwd_split(x, hi, lo, passes, _i(conv.stride), _i(conv.padding), _i(conv.dilation),
+                                       stats=bn.training)
+    else:
+        y, part = ops.conv2d_fwd(x, conv.weight, _i(conv.stride), _i(conv.padding), _i(conv.dilation),
+                                 layout=layout, stats=bn.training)
     count = y.numel() // y.shape[-1]
     ss, mi = _bn_params(bn, part, count)
     return y, ss, mi

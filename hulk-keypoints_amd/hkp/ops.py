@@ -89,6 +89,46 @@ def conv2d_fwd(x, w, stride=1, pad=0, dil=1, layout="nhwc", stats=True, out=None
     return y, part
 
 
+def weight_split(w, passes=3):
+    """fp32 weight → (hi fp16, lo fp16 or None) for conv2d_fwd_split."""
+    _need(w, torch.float32, "weight_split.w")
+    hi = torch.empty(w.shape, device=w.device, dtype=torch.float16)
+    lo = torch.empty(w.shape, device=w.device, dtype=torch.float16) if passes == 3 else None
+    call("hkp_weight_split", w.numel(), _ptr(w), _ptr(hi), _ptr(lo), _stream())
+    return hi, lo
+
+
+def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None):
+    """Split-precision (f16x3, passes=3) or plain fp16 (passes=1) NHWC conv; fp32 in/out."""
+    _need(x, torch.float32, "conv2d_fwd_split.x", 4)
+    _need(w_hi, torch.float16, "conv2d_fwd_split.w_hi", 4)
+    if passes == 3:
+        _need(w_lo, torch.float16, "conv2d_fwd_split.w_lo", 4)
+    n, h, wd, c = x.shape
+    k, r, s, cw = w_hi.shape
+    if cw != c:
+        raise HkpError("conv2d_fwd_split: weight Cin %d != input C %d" % (cw, c))
+    ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
+    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC)
+    y = out if out is not None else torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
+    part = None
+    if stats:
+        tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
+        part = torch.empty((tiles, k, 2), device=x.device, dtype=torch.float32)
+
+    def launch():
+        call("hkp_conv2d_fwd_split", ctypes.byref(d), _ptr(x), _ptr(w_hi), _ptr(w_lo), int(passes), _ptr(y),
+             _ptr(part), _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        bn = 128 if k % 128 == 0 else 64
+        _observer("conv_split_kernel<128, %d, %d>" % (bn, passes), 2.0 * n * ho * wo * k * r * s * c,
+                  4.0 * (x.numel() + w_hi.numel() + y.numel()), launch)
+    return y, part
+
+
 def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None,
                 momentum=0.1, eps=1e-5, want_mean_invstd=True):
     """Train-mode BN statistics from conv partials → (scale_shift [2C], mean_invstd [2C])."""

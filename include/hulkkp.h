@@ -71,6 +71,18 @@ int64_t hkp_conv_stat_tiles(const hkp_conv_desc* d);
 int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const float* w, float* y,
                    float* stat_partials, hkp_stream_t stream);
 
+/* Split-precision forward on fp16 MFMA (v_mfma_f32_32x32x16_f16), same conv and
+ * epilogue as hkp_conv2d_fwd, NHWC only.
+ *   passes = 3: fp32-accurate "f16x3" — operands split hi = f16(x),
+ *               lo = f16((x-hi)*2^11); hi*hi + 2^-11*(hi*lo + lo*hi) in fp32
+ *               accumulators (~2^-22 relative per product); needs w_lo.
+ *   passes = 1: plain fp16 operands, fp32 accumulation (BASELINE config C4).
+ * w_hi / w_lo: the KRSC weight split by hkp_weight_split (fp16 bit patterns).
+ * Operands must be finite and |x| < 65504. */
+int hkp_weight_split(int64_t n, const float* w, uint16_t* w_hi, uint16_t* w_lo, hkp_stream_t stream);
+int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t* w_hi, const uint16_t* w_lo,
+                         int32_t passes, float* y, float* stat_partials, hkp_stream_t stream);
+
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
  * nn.BatchNorm2d defaults eps=1e-5, momentum=0.1): merges the conv's tile
