@@ -46,6 +46,11 @@ SIGNATURES = {
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
     "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _P, _P]),
+    "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
+    "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
+    "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_conv_bwd_filter_split_workspace": (_I64, [_CD]),
+    "hkp_conv2d_bwd_filter_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     # backward
     "hkp_conv_weight_flip":(ctypes.c_int, [_CD, _P, _P, _P]),
     "hkp_conv2d_bwd_data": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),

@@ -11,6 +11,7 @@ Forward per BasicBlock (src/resnet.py:53-69), train-mode BN:
     out = relu(y2*s2 + (x | yd*sd))
 """
 import os
+import weakref
 
 import torch
 
@@ -46,7 +47,25 @@ def _i(v):
 #   "f16"   plain fp16 operands, fp32 accumulation (BASELINE config C4)
 PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
 _precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
+# id(parameter) → (weakref(parameter), {variant: (version, data_ptr, hi, lo)}).
+# The weakref check means a dead parameter's entry is never served to a new
+# tensor that happens to reuse its id, data pointer and version.
 _split_cache = {}
+
+
+def _cached_split(w, variant, make):
+    slot = _split_cache.get(id(w))
+    if slot is None or slot[0]() is not w:
+        wid = id(w)
+        slot = (weakref.ref(w, lambda _r, k=wid: _split_cache.pop(k, None)), {})
+        _split_cache[wid] = slot
+    per = slot[1]
+    ent = per.get(variant)
+    if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+        hi, lo = make(w.detach())
+        ent = (w._version, w.data_ptr(), hi, lo)
+        per[variant] = ent
+    return ent[2], ent[3]
 
 
 def set_conv_precision(p):
@@ -63,13 +82,7 @@ def conv_precision():
 def _split_weight(w, passes):
     """Cached hi/lo fp16 split of a weight; refreshed whenever the parameter changes
     (optimizer steps and load_state_dict bump its version counter)."""
-    key = (id(w), passes)
-    ent = _split_cache.get(key)
-    if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
-        hi, lo = ops.weight_split(w.detach(), passes)
-        ent = (w._version, w.data_ptr(), hi, lo)
-        _split_cache[key] = ent
-    return ent[2], ent[3]
+    return _cached_split(w, passes, lambda t: ops.weight_split(t, passes))
 
 
 def conv_bn(conv, bn, x, layout="nhwc"):
@@ -173,11 +186,21 @@ class Grads(dict):
 def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
     """wgrad (+ dgrad with the residual addend fused) for one NHWC conv."""
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
+    split_ok = _precision == "f16x3" and x.shape[-1] % 64 == 0 and dy.shape[-1] % 64 == 0
+    amax = ops.absmax(dy) if split_ok else None
     dx = None
     if need_dx:
-        wf = ops.conv_weight_flip(conv.weight)
-        dx = ops.conv2d_bwd_data(dy, wf, tuple(x.shape), st, pd, dl, add=add)
-    grads.put(conv.weight, ops.conv2d_bwd_filter(x, dy, tuple(conv.weight.shape), st, pd, dl))
+        if split_ok and st == 1:
+            hi, lo = _cached_split(conv.weight, "flip", ops.conv_weight_flip_split)
+            dx = ops.conv2d_bwd_data_split(dy, hi, lo, tuple(x.shape), pd, dl, add=add, amax=amax)
+        else:
+            wf = ops.conv_weight_flip(conv.weight)
+            dx = ops.conv2d_bwd_data(dy, wf, tuple(x.shape), st, pd, dl, add=add)
+    if split_ok:
+        dw = ops.conv2d_bwd_filter_split(x, dy, tuple(conv.weight.shape), st, pd, dl, amax=amax)
+    else:
+        dw = ops.conv2d_bwd_filter(x, dy, tuple(conv.weight.shape), st, pd, dl)
+    grads.put(conv.weight, dw)
     return dx
 
 

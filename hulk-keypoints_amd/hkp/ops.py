@@ -259,6 +259,62 @@ def conv2d_bwd_data(dy, w_flip, x_shape, stride=1, pad=0, dil=1, add=None):
     return dx
 
 
+def absmax(x):
+    """max |x| as a device uint32 (IEEE bits) — feeds the split kernels' power-of-two scaling."""
+    _need(x, torch.float32, "absmax.x")
+    out = torch.empty(1, device=x.device, dtype=torch.int32)
+    call("hkp_absmax", x.numel(), _ptr(x), _ptr(out), _stream())
+    return out
+
+
+def conv_weight_flip_split(w):
+    """KRSC [K,R,S,C] fp32 → flipped CRSK (hi, lo) fp16 for conv2d_bwd_data_split."""
+    _need(w, torch.float32, "conv_weight_flip_split.w", 4)
+    k, r, s, c = w.shape
+    d = ConvDesc(1, 1, 1, c, k, r, s, 1, 0, 1, HKP_LAYOUT_NHWC)
+    hi = torch.empty((c, r, s, k), device=w.device, dtype=torch.float16)
+    lo = torch.empty((c, r, s, k), device=w.device, dtype=torch.float16)
+    call("hkp_conv_weight_flip_split", ctypes.byref(d), _ptr(w), _ptr(hi), _ptr(lo), _stream())
+    return hi, lo
+
+
+def conv2d_bwd_data_split(dy, wf_hi, wf_lo, x_shape, pad=0, dil=1, add=None, amax=None):
+    """f16x3 dL/dx of a stride-1 NHWC conv; dy scaled by a power of two from amax."""
+    _need(dy, torch.float32, "conv2d_bwd_data_split.dy", 4)
+    _need(wf_hi, torch.float16, "conv2d_bwd_data_split.wf_hi", 4)
+    _need(wf_lo, torch.float16, "conv2d_bwd_data_split.wf_lo", 4)
+    c, r, s, k = wf_hi.shape
+    d = _fwd_desc(x_shape, (k, r, s, c), 1, pad, dil, "nhwc")
+    ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, 1, pad, dil)
+    if tuple(dy.shape) != (x_shape[0], ho, wo, k):
+        raise HkpError("conv2d_bwd_data_split: dy shape %s != %s" % (tuple(dy.shape), (x_shape[0], ho, wo, k)))
+    if add is not None:
+        _need(add, torch.float32, "conv2d_bwd_data_split.add", 4)
+        if tuple(add.shape) != tuple(x_shape):
+            raise HkpError("conv2d_bwd_data_split: add shape mismatch")
+    dx = torch.empty(tuple(x_shape), device=dy.device, dtype=torch.float32)
+    call("hkp_conv2d_bwd_data_split", ctypes.byref(d), _ptr(dy), _ptr(wf_hi), _ptr(wf_lo), _ptr(amax), _ptr(add),
+         _ptr(dx), _stream())
+    return dx
+
+
+def conv2d_bwd_filter_split(x, dy, w_shape, stride=1, pad=0, dil=1, amax=None):
+    """f16x3 dL/dw (KRSC) of an NHWC conv; dy scaled by a power of two from amax."""
+    from ._lib import lib
+    _need(x, torch.float32, "conv2d_bwd_filter_split.x", 4)
+    _need(dy, torch.float32, "conv2d_bwd_filter_split.dy", 4)
+    d = _fwd_desc(tuple(x.shape), tuple(w_shape), stride, pad, dil, "nhwc")
+    ho, wo = conv_out_hw(d.h, d.w, d.r, d.s, stride, pad, dil)
+    if tuple(dy.shape) != (d.n, ho, wo, d.k):
+        raise HkpError("conv2d_bwd_filter_split: dy shape %s != %s" % (tuple(dy.shape), (d.n, ho, wo, d.k)))
+    nbytes = lib().hkp_conv_bwd_filter_split_workspace(ctypes.byref(d))
+    ws = torch.empty(max(nbytes, 4) // 4, device=x.device, dtype=torch.float32)
+    dw = torch.empty(tuple(w_shape), device=x.device, dtype=torch.float32)
+    call("hkp_conv2d_bwd_filter_split", ctypes.byref(d), _ptr(x), _ptr(dy), _ptr(amax), _ptr(dw), _ptr(ws), nbytes,
+         _stream())
+    return dw
+
+
 def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out=None, accumulate=False):
     """dL/dw in the weight's own layout (KRSC, or OIHW for the NCHW stem)."""
     _need(x, torch.float32, "conv2d_bwd_filter.x", 4)

@@ -147,6 +147,26 @@ int hkp_conv_weight_flip(const hkp_conv_desc* d, const float* w, float* w_flip, 
 int hkp_conv2d_bwd_data(const hkp_conv_desc* d, const float* dy, const float* w_flip, const float* add, float* dx,
                         hkp_stream_t stream);
 
+/* f16x3 backward-data for stride-1 NHWC convs (the split kernel of
+ * hkp_conv2d_fwd_split): the gradient operand dy is scaled by an exact power of
+ * two derived from its max |dy| (dy_amax_bits from hkp_absmax, nullable = no
+ * scaling) so that tiny gradients keep fp16 precision; wf_hi/wf_lo from
+ * hkp_conv_weight_flip_split.  add (nullable) is summed into dx. */
+int hkp_absmax(int64_t n, const float* x, uint32_t* amax_bits, hkp_stream_t stream);
+int hkp_conv_weight_flip_split(const hkp_conv_desc* d, const float* w, uint16_t* wf_hi, uint16_t* wf_lo,
+                               hkp_stream_t stream);
+int hkp_conv2d_bwd_data_split(const hkp_conv_desc* d, const float* dy, const uint16_t* wf_hi,
+                              const uint16_t* wf_lo, const uint32_t* dy_amax_bits, const float* add, float* dx,
+                              hkp_stream_t stream);
+
+/* f16x3 backward-filter for NHWC convs (Cin, Cout multiples of 64): dw (KRSC)
+ * with dy scaled by the power of two from dy_amax_bits (nullable); split-K over
+ * pixels into `workspace` (hkp_conv_bwd_filter_split_workspace bytes), fixed-order reduce. */
+int64_t hkp_conv_bwd_filter_split_workspace(const hkp_conv_desc* d);
+int hkp_conv2d_bwd_filter_split(const hkp_conv_desc* d, const float* x, const float* dy,
+                                const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
+                                hkp_stream_t stream);
+
 /* dw (KRSC, or OIHW for the stem) = sum over pixels of dy x im2col(x); split-K over
  * pixels into `workspace`, reduced in fixed order.  accumulate != 0 adds into dw. */
 int64_t hkp_conv_bwd_filter_workspace(const hkp_conv_desc* d);

@@ -238,7 +238,7 @@ def test_train_step_matches_reference_golden(cuda_device, golden, case):
     np.testing.assert_allclose(pa, g["param_abs"], rtol=1e-5 if tight else 1e-4)
     rc = [sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith(sfx))
           for sfx in ("running_mean", "running_var")]
-    np.testing.assert_allclose(rc, g["running_checksum"][:2], rtol=1e-4)
+    np.testing.assert_allclose(rc, g["running_checksum"][:2], rtol=1e-4 if tight else 1e-3)
 
 
 def test_trainer_fused_loss_equals_autograd_path(cuda_device):

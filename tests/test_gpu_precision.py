@@ -48,6 +48,47 @@ def test_f16x3_is_fp32_accurate(cuda_device, case):
     assert 1e-5 < e1 < 5e-3, e1             # genuinely fp16 operands
 
 
+@pytest.mark.parametrize("case", [c for c in CASES if c[6] == 1 and c[3] % 64 == 0])
+@pytest.mark.parametrize("gscale", [1.0, 1e-9])
+def test_f16x3_dgrad_scaled(cuda_device, case, gscale):
+    """Backward-data on the split kernel: fp32-class accuracy even for gradients
+    far below fp16's normal range (power-of-two scaling from max|dy|)."""
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    wt = rand(cout, cin, k, k, seed=5, scale=(2.0 / (k * k * cout)) ** 0.5)
+    ho = (h + 2 * pad - dil * (k - 1) - 1) + 1
+    wo = (w + 2 * pad - dil * (k - 1) - 1) + 1
+    gy = rand(n, cout, ho, wo, seed=6) * gscale
+    add = rand(n, cin, h, w, seed=7) * gscale
+    ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.double(), gy.double(), 1, pad, dil) + add.double()
+    d = cuda_device
+    gy_d = gy.permute(0, 2, 3, 1).contiguous().to(d)
+    hi, lo = ops.conv_weight_flip_split(wt.permute(0, 2, 3, 1).contiguous().to(d))
+    dx = ops.conv2d_bwd_data_split(gy_d, hi, lo, (n, h, w, cin), pad, dil,
+                                   add=add.permute(0, 2, 3, 1).contiguous().to(d), amax=ops.absmax(gy_d))
+    err = (dx.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+
+
+@pytest.mark.parametrize("case", [c for c in CASES if c[3] % 64 == 0 and c[4] % 64 == 0]
+                         + [(2, 31, 41, 64, 128, 1, 2, 0, 1)])
+@pytest.mark.parametrize("gscale", [1.0, 1e-9])
+def test_f16x3_wgrad_scaled(cuda_device, case, gscale):
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    x = F.relu(rand(n, cin, h, w, seed=8))
+    ho = (h + 2 * pad - dil * (k - 1) - 1) // st + 1
+    wo = (w + 2 * pad - dil * (k - 1) - 1) // st + 1
+    gy = rand(n, cout, ho, wo, seed=9) * gscale
+    ref = torch.nn.grad.conv2d_weight(x.double(), (cout, cin, k, k), gy.double(), st, pad, dil)
+    d = cuda_device
+    gy_d = gy.permute(0, 2, 3, 1).contiguous().to(d)
+    dw = ops.conv2d_bwd_filter_split(x.permute(0, 2, 3, 1).contiguous().to(d), gy_d, (cout, k, k, cin), st, pad,
+                                     dil, amax=ops.absmax(gy_d))
+    err = (dw.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+
+
 def _model(bb, k, wseed, dev):
     from src.model import KeypointsGauss
     m = KeypointsGauss(k, backbone=bb, pretrained=False)

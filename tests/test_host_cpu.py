@@ -110,6 +110,28 @@ def test_prediction_expectation_and_plot(tmp_path):
     assert out.shape == (20, 24, 3) and (tmp_path / "out0003.png").exists()
 
 
+def test_split_weight_cache_tracks_versions_and_lifetimes():
+    import gc
+    from hkp import net
+    calls = []
+
+    def make(t):
+        calls.append(1)
+        return t.clone(), t.clone()
+    p = torch.nn.Parameter(torch.randn(3))
+    net._cached_split(p, "a", make)
+    net._cached_split(p, "a", make)
+    assert len(calls) == 1
+    with torch.no_grad():
+        p.add_(1)                    # optimizer-style in-place update → re-split
+    net._cached_split(p, "a", make)
+    assert len(calls) == 2
+    pid = id(p)
+    del p
+    gc.collect()
+    assert pid not in net._split_cache
+
+
 def test_entry_modules_import():
     import importlib
     for mod in ("config", "train", "analysis", "src.model", "src.dataset", "src.prediction", "src.resnet_dilated"):
