@@ -101,6 +101,24 @@ class LaunchTimer:
         return agg
 
 
+def pmc_traffic(kernel_sym, tag):
+    """HBM bytes per launch of `kernel_sym` from the committed rocprofv3 PMC summary
+    (profiles/*<tag>*pmc*.json, separate FETCH_SIZE / WRITE_SIZE passes):
+    (FETCH_SIZE * 2 + WRITE_SIZE) * 1024 — gfx950's FETCH_SIZE counts half of a
+    wide streaming read (MI355X_MICROARCH.md §HBM).  None if no summary matches."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*%s*pmc*.json" % tag)), reverse=True):
+        try:
+            data = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        for name, c in data.items():
+            if kernel_sym.split("<")[0] in name and kernel_sym.split("<")[1].rstrip(">") in name.replace(" ", ""):
+                if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                    return (c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024, os.path.basename(path)
+    return None, None
+
+
 def cpu_baseline(args, budget_s):
     """Oracle (reference-faithful CPU restatement: 1000-ch head, train-mode BN)
     timed on this host's cores on a bounded sample of the same workload."""
@@ -232,6 +250,12 @@ def main():
                      "conv_share_of_step": (all_ms / max(3, min(args.steps, 10))) / (elapsed / args.steps * 1e3)},
         "model_tflops": value / world * fl_img * (3 if args.mode == "train" else 1) / 1e12,
     }
+    tag = "infer_c2" if args.mode == "infer" else "train_c3"
+    traffic, src = pmc_traffic(dom_sym.replace(" ", ""), tag) if (args.backbone, K, H, W) == ("resnet34", 4, 480,
+                                                                                             640) else (None, None)
+    out["roofline"]["traffic"] = traffic
+    out["roofline"]["traffic_source"] = src
+    out["roofline"]["algorithmic_bytes_per_launch"] = nb / cnt
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     print(json.dumps(out))
