@@ -82,7 +82,8 @@ template <int RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f32x4* __restrict__ y,
                                                        const f32x4* __restrict__ sc, const f32x4* __restrict__ sh,
                                                        const f32x4* __restrict__ res, const f32x4* __restrict__ rsc,
-                                                       const f32x4* __restrict__ rsh, f32x4* __restrict__ out) {
+                                                       const f32x4* __restrict__ rsh, f32x4* __restrict__ out,
+                                                       _Float16* __restrict__ osplit, int passes) {
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         const int c4 = (int)(i % C4);
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
         }
-        out[i] = o;
+        if (out) out[i] = o;
+        if (osplit) store_split4(o, i, osplit, passes);   // operand split for the next conv
     }
 }
 
@@ -111,7 +113,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
 __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo,
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ ss,
-                                                             float* __restrict__ out) {
+                                                             float* __restrict__ out, _Float16* __restrict__ osplit,
+                                                             int passes) {
     const int C4 = C >> 2;
     const long total = (long)N * Ho * Wo * C4;
     const long stride = (long)gridDim.x * blockDim.x;
@@ -141,7 +144,8 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int 
                 }
             }
         }
-        *(f32x4*)(out + i * 4) = m;
+        if (out) *(f32x4*)(out + i * 4) = m;
+        if (osplit) store_split4(m, i, osplit, passes);
     }
 }
 
@@ -182,9 +186,12 @@ extern "C" int hkp_bn_eval_params(int32_t c, const float* gamma, const float* be
 }
 
 extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
-                            const float* res_scale_shift, int32_t relu, float* out, hkp_stream_t stream) {
+                            const float* res_scale_shift, int32_t relu, float* out, uint16_t* out_split,
+                            int32_t split_passes, hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_apply: need m>0 and c%%4==0 (c=%d)", c);
-    HKP_CHECK_ARG(y && scale_shift && out, "hkp_bn_apply: null tensor");
+    HKP_CHECK_ARG(y && scale_shift && (out || out_split), "hkp_bn_apply: null tensor");
+    HKP_CHECK_ARG(!out_split || ((split_passes == 1 || split_passes == 3) && c % 32 == 0),
+                  "hkp_bn_apply: split output needs split_passes 1|3 and c%%32==0");
     HKP_CHECK_ARG(res_scale_shift == nullptr || res != nullptr, "hkp_bn_apply: res_scale_shift without res");
     const long n4 = m * (long)c / 4;
     const int C4 = c / 4;
@@ -196,7 +203,8 @@ extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* s
     const int g = grid_for(n4);
     hipStream_t st = as_stream(stream);
 #define HKP_APPLY(RES, RL) \
-    hipLaunchKernelGGL((bn_apply_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, RSH, O)
+    hipLaunchKernelGGL((bn_apply_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, RSH, O, \
+                       (_Float16*)out_split, split_passes)
     if (!res) {
         if (relu) HKP_APPLY(0, true); else HKP_APPLY(0, false);
     } else if (!res_scale_shift) {
@@ -210,13 +218,16 @@ extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* s
 }
 
 extern "C" int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y,
-                                   const float* scale_shift, float* out, hkp_stream_t stream) {
+                                   const float* scale_shift, float* out, uint16_t* out_split,
+                                   int32_t split_passes, hkp_stream_t stream) {
     HKP_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "hkp_bn_relu_maxpool: bad sizes");
-    HKP_CHECK_ARG(y && scale_shift && out, "hkp_bn_relu_maxpool: null tensor");
+    HKP_CHECK_ARG(y && scale_shift && (out || out_split), "hkp_bn_relu_maxpool: null tensor");
+    HKP_CHECK_ARG(!out_split || ((split_passes == 1 || split_passes == 3) && c % 32 == 0),
+                  "hkp_bn_relu_maxpool: split output needs split_passes 1|3 and c%%32==0");
     const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
     const long work = (long)n * ho * wo * (c / 4);
     hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n, h, w, c,
-                       ho, wo, y, scale_shift, out);
+                       ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes);
     HKP_LAUNCH_CHECK("hkp_bn_relu_maxpool");
     return HKP_OK;
 }

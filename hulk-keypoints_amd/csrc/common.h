@@ -43,6 +43,30 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
+// f16x3 operand planes: hi = f16(x), lo = f16((x - hi) * 2^11)
+constexpr float SPLIT_LO_SCALE = 2048.f;
+typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
+
+// Operand split of 4 consecutive channels (element index e4*4, C % 32 == 0) for
+// the next conv: passes 1 → hi plane [P][C]; passes 3 → packed split layout
+// [P][C/32][hi32|lo32] (element e → 2e - (e&31), lo 32 halves later).
+__device__ __forceinline__ void store_split4(const f32x4& v, long e4, _Float16* __restrict__ out, int passes) {
+    h16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        const _Float16 hv = (_Float16)v[e];
+        h[e] = hv;
+        l[e] = (_Float16)((v[e] - (float)hv) * SPLIT_LO_SCALE);
+    }
+    if (passes == 1) {
+        ((h16x4*)out)[e4] = h;
+    } else {
+        const long e = e4 * 4, o = 2 * e - (e & 31);
+        *(h16x4*)(out + o) = h;
+        *(h16x4*)(out + o + 32) = l;
+    }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -27,6 +27,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 struct SplitArgs {
     const float* x;
+    const _Float16* xhi;   // optional pre-converted fp16 input plane (APL path, passes 1)
     const _Float16* whi;
     const _Float16* wlo;
     float* y;
@@ -55,12 +56,15 @@ constexpr int SLDR = SBK + 8;   // LDS row stride in halves (80 B)
 constexpr float LO_SCALE = 2048.f;
 constexpr float LO_INV = 1.f / 2048.f;
 
-template <int BM, int BN, int PASSES>
+// APL (PASSES 1): the input arrives as a pre-converted fp16 plane (written by its producer), so
+// the A tile is staged exactly like the weight tile — no conversion in the loop.
+template <int BM, int BN, int PASSES, bool APL>
 __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
     constexpr int NT = 256, WM = 2, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     constexpr int PL = PASSES == 3 ? 2 : 1;          // planes (hi[, lo])
-    constexpr int AP = BM * (SBK / 4) / NT;          // f32x4 A loads per thread
+    constexpr int AP = APL ? BM * (SBK / 8) / NT     // f16x8 A loads per thread per plane
+                           : BM * (SBK / 4) / NT;    // f32x4 A loads per thread
     constexpr int BP = BN * (SBK / 8) / NT;          // f16x8 B loads per thread per plane
     constexpr int STAGE = PL * (BM + BN) * SLDR;     // halves per stage
     __shared__ __attribute__((aligned(16))) _Float16 smem[2 * STAGE];
@@ -78,7 +82,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
     int a_n[AP], a_hi[AP], a_wi[AP];
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-        const int m = m0 + rowb + 32 * i;
+        const int m = m0 + (APL ? browb + 64 * i : rowb + 32 * i);
         if (m < a.M) {
             const int hw = a.Ho * a.Wo;
             const int n = m / hw, rem = m - n * hw;
@@ -93,7 +97,9 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
         }
     }
 
-    f32x4 ra[AP];
+    f32x4 ra[APL ? 1 : AP];
+    f16x8 rah[APL ? AP : 1];
+    static_assert(!APL || PASSES == 1, "pre-split f16x3 input goes through conv_x3.hip");
     f16x8 rbh[BP], rbl[BP];
 
     auto load_chunk = [&](int kc) {
@@ -103,11 +109,13 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
             const int hi = a_hi[i] + rr * a.dil, wi = a_wi[i] + ss * a.dil;
-            if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W) {
-                const long pix = ((long)a_n[i] * a.H + hi) * a.W + wi;
-                ra[i] = *(const f32x4*)(a.x + pix * a.C + c0 + col4 * 4);
+            const bool in = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const long pix = ((long)a_n[i] * a.H + hi) * a.W + wi;
+            if constexpr (APL) {
+                const f16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+                rah[i] = in ? *(const f16x8*)(a.xhi + pix * a.C + c0 + c8 * 8) : z;
             } else {
-                ra[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                ra[i] = in ? *(const f32x4*)(a.x + pix * a.C + c0 + col4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
             }
         }
 #pragma unroll
@@ -125,17 +133,22 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
         _Float16* Bl = Al + BM * SLDR;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
-            f16x4 h, l;
+            if constexpr (APL) {
+                const int off = (browb + 64 * i) * SLDR + c8 * 8;
+                *(f16x8*)(Ah + off) = rah[i];
+            } else {
+                f16x4 h, l;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float v = ra[i][e] * asc;
-                const _Float16 hv = (_Float16)v;
-                h[e] = hv;
-                if constexpr (PASSES == 3) l[e] = (_Float16)((v - (float)hv) * LO_SCALE);
+                for (int e = 0; e < 4; ++e) {
+                    const float v = ra[i][e] * asc;
+                    const _Float16 hv = (_Float16)v;
+                    h[e] = hv;
+                    if constexpr (PASSES == 3) l[e] = (_Float16)((v - (float)hv) * LO_SCALE);
+                }
+                const int off = (rowb + 32 * i) * SLDR + col4 * 4;
+                *(f16x4*)(Ah + off) = h;
+                if constexpr (PASSES == 3) *(f16x4*)(Al + off) = l;
             }
-            const int off = (rowb + 32 * i) * SLDR + col4 * 4;
-            *(f16x4*)(Ah + off) = h;
-            if constexpr (PASSES == 3) *(f16x4*)(Al + off) = l;
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i) {
@@ -535,9 +548,9 @@ __global__ __launch_bounds__(256) void wg_split_reduce_kernel(long n, int splits
     }
 }
 
-template <int BN, int PASSES>
+template <int BN, int PASSES, bool APL = false>
 static int launch_split(const SplitArgs& a, int m_tiles, hipStream_t st) {
-    hipLaunchKernelGGL((conv_split_kernel<128, BN, PASSES>), dim3(m_tiles * a.n_tiles), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv_split_kernel<128, BN, PASSES, APL>), dim3(m_tiles * a.n_tiles), dim3(256), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_split");
     return HKP_OK;
 }
@@ -556,13 +569,14 @@ extern "C" int hkp_weight_split(int64_t n, const float* w, uint16_t* w_hi, uint1
     return HKP_OK;
 }
 
-extern "C" int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t* w_hi,
-                                    const uint16_t* w_lo, int32_t passes, float* y, float* stat_partials,
-                                    hkp_stream_t stream) {
+extern "C" int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t* x_hi,
+                                    const uint16_t* w_hi, const uint16_t* w_lo, int32_t passes,
+                                    float* y, float* stat_partials, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
-    HKP_CHECK_ARG(x && w_hi && y, "hkp_conv2d_fwd_split: null tensor");
+    HKP_CHECK_ARG((x || x_hi) && w_hi && y, "hkp_conv2d_fwd_split: null tensor");
+    HKP_CHECK_ARG(!x_hi || passes == 1, "hkp_conv2d_fwd_split: x_hi plane is for passes 1 (passes 3: hkp_conv2d_fwd_x3)");
     HKP_CHECK_ARG(passes == 1 || (passes == 3 && w_lo), "hkp_conv2d_fwd_split: passes must be 1 or 3 (3 needs w_lo)");
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "hkp_conv2d_fwd_split: NHWC only");
     HKP_CHECK_ARG(d->c % 32 == 0 && d->k % 64 == 0, "hkp_conv2d_fwd_split: need Cin%%32==0, Cout%%64==0");
@@ -570,6 +584,7 @@ extern "C" int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, cons
     HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w < (1L << 31), "hkp_conv2d_fwd_split: too large");
     SplitArgs a;
     a.x = x; a.whi = (const _Float16*)w_hi; a.wlo = (const _Float16*)w_lo; a.y = y; a.part = stat_partials;
+    a.xhi = (const _Float16*)x_hi;
     a.amax = nullptr; a.add = nullptr;
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
@@ -581,6 +596,7 @@ extern "C" int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, cons
     a.n_tiles = d->k / (bn128 ? 128 : 64);
     const int m_tiles = (int)((M + 127) / 128);
     hipStream_t st = as_stream(stream);
+    if (x_hi) return bn128 ? launch_split<128, 1, true>(a, m_tiles, st) : launch_split<64, 1, true>(a, m_tiles, st);
     if (passes == 3)
         return bn128 ? launch_split<128, 3>(a, m_tiles, st) : launch_split<64, 3>(a, m_tiles, st);
     return bn128 ? launch_split<128, 1>(a, m_tiles, st) : launch_split<64, 1>(a, m_tiles, st);
@@ -631,6 +647,7 @@ extern "C" int hkp_conv2d_bwd_data_split(const hkp_conv_desc* d, const float* dy
     HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_data_split: too large");
     SplitArgs a;
     a.x = dy; a.whi = (const _Float16*)wf_hi; a.wlo = (const _Float16*)wf_lo; a.y = dx; a.part = nullptr;
+    a.xhi = nullptr;
     a.amax = dy_amax_bits; a.add = add;
     a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
     a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;

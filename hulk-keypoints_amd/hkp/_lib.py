@@ -39,13 +39,15 @@ SIGNATURES = {
     "hkp_conv2d_fwd": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
     "hkp_bn_finalize": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_eval_params": (ctypes.c_int, [_I32, _P, _P, _P, _P, _F, _P, _P, _P]),
-    "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P]),
-    "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _I32, _P]),
+    "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
     "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),
-    "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _P, _P]),
+    "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _I32, _P, _P, _P]),
+    "hkp_weight_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P]),
+    "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),

@@ -47,7 +47,7 @@ def _i(v):
 #   "f16"   plain fp16 operands, fp32 accumulation (BASELINE config C4)
 PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
 _precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
-# id(parameter) → (weakref(parameter), {variant: (version, data_ptr, hi, lo)}).
+# id(parameter) → (weakref(parameter), {variant: (version, data_ptr, derived operand)}).
 # The weakref check means a dead parameter's entry is never served to a new
 # tensor that happens to reuse its id, data pointer and version.
 _split_cache = {}
@@ -62,10 +62,9 @@ def _cached_split(w, variant, make):
     per = slot[1]
     ent = per.get(variant)
     if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
-        hi, lo = make(w.detach())
-        ent = (w._version, w.data_ptr(), hi, lo)
+        ent = (w._version, w.data_ptr(), make(w.detach()))
         per[variant] = ent
-    return ent[2], ent[3]
+    return ent[2]
 
 
 def set_conv_precision(p):
@@ -85,25 +84,43 @@ def _split_weight(w, passes):
     return _cached_split(w, passes, lambda t: ops.weight_split(t, passes))
 
 
+def _pack_weight_x3(w):
+    """Cached packed f16x3 split of a KRSC weight (conv2d_fwd_x3's operand)."""
+    return _cached_split(w, "x3", ops.weight_pack_x3)
+
+
 def conv_bn(conv, bn, x, layout="nhwc"):
-    """conv (+ BN partials when training) → (y, scale_shift, mean_invstd)."""
+    """conv (+ BN partials when training) → (y, scale_shift, mean_invstd).
+    x: fp32 NHWC (optionally carrying its producer's operand split), a split-only
+    activation (fp16, see ops.bn_apply keep_fp32=False), or NCHW for the stem."""
     passes = PRECISIONS[_precision]
-    if layout == "nhwc" and passes:
+    st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
+    sp = ops.split_of(x) if layout == "nhwc" else None
+    k = conv.weight.shape[0]
+    if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
+        y, part = ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training)
+    elif layout == "nhwc" and passes:
         hi, lo = _split_weight(conv.weight, passes)
-        y, part = ops.conv2d_fwd_split(x, hi, lo, passes, _i(conv.stride), _i(conv.padding), _i(conv.dilation),
-                                       stats=bn.training)
+        x_hi = sp[0] if (sp is not None and sp[1] == 1 and passes == 1) else None
+        y, part = ops.conv2d_fwd_split(x if x.dtype == torch.float32 else None, hi, lo, passes, st, pd, dl,
+                                       stats=bn.training, x_hi=x_hi)
     else:
-        y, part = ops.conv2d_fwd(x, conv.weight, _i(conv.stride), _i(conv.padding), _i(conv.dilation),
-                                 layout=layout, stats=bn.training)
+        y, part = ops.conv2d_fwd(x, conv.weight, st, pd, dl, layout=layout, stats=bn.training)
     count = y.numel() // y.shape[-1]
     ss, mi = _bn_params(bn, part, count)
     return y, ss, mi
 
 
+def _split_for(c):
+    """Operand split the producers of a C-channel activation emit for its consumer convs."""
+    p = PRECISIONS[_precision]
+    return p if (p and c % 32 == 0) else 0
+
+
 def stem_forward(resnet, x_nchw, trace=None):
     """conv1 → bn1 → relu → maxpool (src/resnet.py:199-202)."""
     y, ss, mi = conv_bn(resnet.conv1, resnet.bn1, x_nchw, layout="nchw")
-    out = ops.bn_relu_maxpool(y, ss)
+    out = ops.bn_relu_maxpool(y, ss, split=_split_for(y.shape[-1]))
     if trace is not None:
         trace.stem = dict(x=x_nchw, y=y, ss=ss, mi=mi, out=out)
     return out
@@ -111,29 +128,38 @@ def stem_forward(resnet, x_nchw, trace=None):
 
 def block_forward(block, x, trace=None):
     rec = {} if trace is not None else None
+    # producers also write the next conv's operand split; an activation only a
+    # conv consumes (inside the block, no backward trace) is written split-only
+    keep = rec is not None
+
+    def act(y, s):
+        sp = _split_for(y.shape[-1])
+        return ops.bn_apply(y, s, relu=True, split=sp, keep_fp32=keep or not sp)
+
     if block.kind == "basic":
         y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
-        a1 = ops.bn_apply(y1, s1, relu=True)
+        a1 = act(y1, s1)
         y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
         last_y, last_s = y2, s2
         if rec is not None:
             rec.update(x=x, y=[y1, y2], ss=[s1, s2], mi=[m1, m2], act=[a1])
     else:
         y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
-        a1 = ops.bn_apply(y1, s1, relu=True)
+        a1 = act(y1, s1)
         y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
-        a2 = ops.bn_apply(y2, s2, relu=True)
+        a2 = act(y2, s2)
         y3, s3, m3 = conv_bn(block.conv3, block.bn3, a2)
         last_y, last_s = y3, s3
         if rec is not None:
             rec.update(x=x, y=[y1, y2, y3], ss=[s1, s2, s3], mi=[m1, m2, m3], act=[a1, a2])
+    pl = _split_for(last_y.shape[-1])
     if block.downsample is not None:
         yd, sd, md = conv_bn(block.downsample[0], block.downsample[1], x)
-        out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True)
+        out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True, split=pl)
         if rec is not None:
             rec.update(yd=yd, sd=sd, md=md)
     else:
-        out = ops.bn_apply(last_y, last_s, res=x, relu=True)
+        out = ops.bn_apply(last_y, last_s, res=x, relu=True, split=pl)
     if rec is not None:
         rec["out"] = out
         trace.blocks.append(rec)

@@ -98,34 +98,98 @@ def weight_split(w, passes=3):
     return hi, lo
 
 
-def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None):
-    """Split-precision (f16x3, passes=3) or plain fp16 (passes=1) NHWC conv; fp32 in/out."""
-    _need(x, torch.float32, "conv2d_fwd_split.x", 4)
+def weight_pack_x3(w):
+    """fp32 KRSC weight → packed split fp16 [K, R, S, 2C] ([..][C/32][hi32|lo32]) for conv2d_fwd_x3."""
+    _need(w, torch.float32, "weight_pack_x3.w", 4)
+    k, r, s, c = w.shape
+    ws = torch.empty((k, r, s, 2 * c), device=w.device, dtype=torch.float16)
+    call("hkp_weight_pack_x3", w.numel(), c, _ptr(w), _ptr(ws), _stream())
+    return ws
+
+
+def split_of(x):
+    """(split tensor, passes) of an activation: x itself when it IS a split-only
+    activation (fp16), else the split a producer attached to fp32 x, else None."""
+    if x.dtype == torch.float16:
+        return x, x._hkp_split_passes
+    return getattr(x, "_hkp_split", None)
+
+
+def channels_of(x):
+    """Channel count of an fp32 activation or of a split-only one."""
+    if x.dtype == torch.float16 and x._hkp_split_passes == 3:
+        return x.shape[-1] // 2
+    return x.shape[-1]
+
+
+def conv2d_fwd_x3(xs, ws, stride=1, pad=0, dil=1, stats=True, out=None):
+    """f16x3 NHWC conv on packed split operands: xs [N,H,W,2C] (from a producer with
+    split=3), ws [K,R,S,2C] (weight_pack_x3) → fp32 y [N,Ho,Wo,K] (+ BN partials)."""
+    _need(xs, torch.float16, "conv2d_fwd_x3.x_split", 4)
+    _need(ws, torch.float16, "conv2d_fwd_x3.w_split", 4)
+    n, h, wd, c2 = xs.shape
+    k, r, s, cw2 = ws.shape
+    if cw2 != c2:
+        raise HkpError("conv2d_fwd_x3: weight Cin %d != input C %d" % (cw2 // 2, c2 // 2))
+    c = c2 // 2
+    ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
+    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC)
+    y = out if out is not None else torch.empty((n, ho, wo, k), device=xs.device, dtype=torch.float32)
+    part = None
+    if stats:
+        tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
+        part = torch.empty((tiles, k, 2), device=xs.device, dtype=torch.float32)
+
+    def launch():
+        call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(y), _ptr(part), _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        _observer("conv_x3_kernel<%d>" % (128 if k % 128 == 0 else 64), 2.0 * n * ho * wo * k * r * s * c,
+                  2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
+    return y, part
+
+
+def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None, x_hi=None):
+    """Split-precision (f16x3, passes=3) or plain fp16 (passes=1) NHWC conv; fp32 in/out,
+    the activation split inside the conv loop.  x_hi (passes 1): the input's pre-converted
+    fp16 plane (x may then be None)."""
+    if x_hi is not None:
+        if passes != 1:
+            raise HkpError("conv2d_fwd_split: x_hi is for passes 1 (passes 3: conv2d_fwd_x3)")
+        _need(x_hi, torch.float16, "conv2d_fwd_split.x_hi", 4)
+        if x is not None and x_hi.shape != x.shape:
+            raise HkpError("conv2d_fwd_split: x_hi does not match x")
+    else:
+        _need(x, torch.float32, "conv2d_fwd_split.x", 4)
+    xt = x if x is not None else x_hi
     _need(w_hi, torch.float16, "conv2d_fwd_split.w_hi", 4)
     if passes == 3:
         _need(w_lo, torch.float16, "conv2d_fwd_split.w_lo", 4)
-    n, h, wd, c = x.shape
+    n, h, wd, c = xt.shape
     k, r, s, cw = w_hi.shape
     if cw != c:
         raise HkpError("conv2d_fwd_split: weight Cin %d != input C %d" % (cw, c))
     ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC)
-    y = out if out is not None else torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
+    y = out if out is not None else torch.empty((n, ho, wo, k), device=xt.device, dtype=torch.float32)
     part = None
     if stats:
         tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
-        part = torch.empty((tiles, k, 2), device=x.device, dtype=torch.float32)
+        part = torch.empty((tiles, k, 2), device=xt.device, dtype=torch.float32)
 
     def launch():
-        call("hkp_conv2d_fwd_split", ctypes.byref(d), _ptr(x), _ptr(w_hi), _ptr(w_lo), int(passes), _ptr(y),
-             _ptr(part), _stream())
+        call("hkp_conv2d_fwd_split", ctypes.byref(d), _ptr(x), _ptr(x_hi), _ptr(w_hi), _ptr(w_lo), int(passes),
+             _ptr(y), _ptr(part), _stream())
 
     if _observer is None:
         launch()
     else:
         bn = 128 if k % 128 == 0 else 64
-        _observer("conv_split_kernel<128, %d, %d>" % (bn, passes), 2.0 * n * ho * wo * k * r * s * c,
-                  4.0 * (x.numel() + w_hi.numel() + y.numel()), launch)
+        _observer("conv_split_kernel<128, %d, %d, %s>" % (bn, passes, "true" if x_hi is not None else "false"),
+                  2.0 * n * ho * wo * k * r * s * c,
+                  4.0 * (xt.numel() + w_hi.numel() + y.numel()), launch)
     return y, part
 
 
@@ -157,26 +221,58 @@ def bn_eval_params(gamma, beta, running_mean, running_var, eps=1e-5):
     return ss, mi
 
 
-def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None):
+def _split_out(shape, device, split):
+    """Split output of a producer: passes 1 → fp16 [.., C]; passes 3 → packed [.., 2C]."""
+    shp = tuple(shape[:-1]) + (shape[-1] * (2 if split == 3 else 1),)
+    t = torch.empty(shp, device=device, dtype=torch.float16)
+    t._hkp_split_passes = split
+    return t
+
+
+def _check_split(split, c, who):
+    if split not in (0, 1, 3):
+        raise HkpError("%s: split must be 0, 1 or 3" % who)
+    if split and c % 32:
+        raise HkpError("%s: split output needs C %% 32 == 0 (C=%d)" % (who, c))
+
+
+def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None, split=0, keep_fp32=True):
+    """out = [relu](y*scale+shift [+ res | + res*rscale+rshift]).
+    split = 1 or 3 also writes the next conv's operand (attached as out._hkp_split);
+    keep_fp32=False (with split): the fp32 activation is not written and the split
+    tensor itself is returned (an activation only a conv consumes)."""
     _need(y, torch.float32, "bn_apply.y")
     c = y.shape[-1]
     m = y.numel() // c
+    _check_split(split, c, "bn_apply")
     if ss.numel() != 2 * c:
         raise HkpError("bn_apply: scale_shift size %d != 2C" % ss.numel())
     if res is not None:
         _need(res, torch.float32, "bn_apply.res")
         if res.shape != y.shape:
             raise HkpError("bn_apply: residual shape %s != %s" % (tuple(res.shape), tuple(y.shape)))
-    o = out if out is not None else torch.empty_like(y)
-    call("hkp_bn_apply", m, c, _ptr(y), _ptr(ss), _ptr(res), _ptr(res_ss), int(bool(relu)), _ptr(o), _stream())
+    if not keep_fp32 and not split:
+        raise HkpError("bn_apply: keep_fp32=False needs a split output")
+    o = None if not keep_fp32 else (out if out is not None else torch.empty_like(y))
+    sp = _split_out(y.shape, y.device, split) if split else None
+    call("hkp_bn_apply", m, c, _ptr(y), _ptr(ss), _ptr(res), _ptr(res_ss), int(bool(relu)), _ptr(o), _ptr(sp),
+         int(split), _stream())
+    if o is None:
+        return sp
+    if split:
+        o._hkp_split = (sp, split)
     return o
 
 
-def bn_relu_maxpool(y, ss):
+def bn_relu_maxpool(y, ss, split=0):
     _need(y, torch.float32, "bn_relu_maxpool.y", 4)
     n, h, w, c = y.shape
+    _check_split(split, c, "bn_relu_maxpool")
     out = torch.empty((n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c), device=y.device, dtype=torch.float32)
-    call("hkp_bn_relu_maxpool", n, h, w, c, _ptr(y), _ptr(ss), _ptr(out), _stream())
+    sp = _split_out(out.shape, y.device, split) if split else None
+    call("hkp_bn_relu_maxpool", n, h, w, c, _ptr(y), _ptr(ss), _ptr(out), _ptr(sp), int(split), _stream())
+    if split:
+        out._hkp_split = (sp, split)
     return out
 
 

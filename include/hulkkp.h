@@ -78,10 +78,26 @@ int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const float* w, float
  *               accumulators (~2^-22 relative per product); needs w_lo.
  *   passes = 1: plain fp16 operands, fp32 accumulation (BASELINE config C4).
  * w_hi / w_lo: the KRSC weight split by hkp_weight_split (fp16 bit patterns).
+ * x_hi (passes = 1 only), if given, is the input's pre-converted fp16 plane
+ * (from hkp_bn_apply / hkp_bn_relu_maxpool with split_passes = 1) and x may be NULL.
  * Operands must be finite and |x| < 65504. */
 int hkp_weight_split(int64_t n, const float* w, uint16_t* w_hi, uint16_t* w_lo, hkp_stream_t stream);
-int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t* w_hi, const uint16_t* w_lo,
-                         int32_t passes, float* y, float* stat_partials, hkp_stream_t stream);
+int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t* x_hi,
+                         const uint16_t* w_hi, const uint16_t* w_lo, int32_t passes, float* y,
+                         float* stat_partials, hkp_stream_t stream);
+
+/* The f16x3 forward conv of the main path (same conv, arithmetic and epilogue
+ * as hkp_conv2d_fwd_split with passes = 3), on operands pre-split into the
+ * "packed split" layout: per pixel (weights: per filter tap) and per 32-channel
+ * group one 128-B line [hi 32 | lo 32] (fp16 bit patterns), i.e.
+ *   x_split[n*h*w][c/32][64]   written by hkp_bn_apply / hkp_bn_relu_maxpool
+ *                              with split_passes = 3,
+ *   w_split[k][r*s][c/32][64]  written by hkp_weight_pack_x3 from KRSC fp32
+ *                              (n = k*r*s*c elements).
+ * Needs c % 32 == 0 and k % 64 == 0.  Replaces the same convs as hkp_conv2d_fwd. */
+int hkp_weight_pack_x3(int64_t n, int32_t c, const float* w, uint16_t* w_split, hkp_stream_t stream);
+int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split, float* y,
+                      float* stat_partials, hkp_stream_t stream);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
@@ -103,14 +119,22 @@ int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const f
 /* out = [relu]( y*scale + shift  [+ res | + res*rscale + rshift] ), NHWC [m][c].
  * Replaces the bn→relu / bn→(+residual)→relu tails of BasicBlock
  * (src/resnet.py:57-67) and Bottleneck (:96-110). res may be NULL;
- * res_scale_shift NULL means the residual is added raw. */
+ * res_scale_shift NULL means the residual is added raw.
+ * out_split (nullable; needs c % 32 == 0): the same values also written as the
+ * next conv's operand — split_passes = 1: fp16 plane [m][c] for
+ * hkp_conv2d_fwd_split (passes 1); split_passes = 3: the packed split layout
+ * [m][c/32][hi32|lo32] (hi = f16(out), lo = f16((out-hi)*2^11)) for
+ * hkp_conv2d_fwd_x3.  out may be NULL when out_split is given (an activation
+ * only a conv consumes).  hkp_bn_relu_maxpool takes the same optional split. */
 int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
-                 const float* res_scale_shift, int32_t relu, float* out, hkp_stream_t stream);
+                 const float* res_scale_shift, int32_t relu, float* out, uint16_t* out_split,
+                 int32_t split_passes, hkp_stream_t stream);
 
 /* Stem tail: maxpool3x3/s2/p1( relu( y*scale + shift ) ), NHWC
  * (src/resnet.py:139-141, 200-202). Output [n, (h-1)/2+1, (w-1)/2+1, c]. */
 int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y,
-                        const float* scale_shift, float* out, hkp_stream_t stream);
+                        const float* scale_shift, float* out, uint16_t* out_split, int32_t split_passes,
+                        hkp_stream_t stream);
 
 /* ---------------------------------------------------------------- head ---- */
 /* K-channel 1x1 scoring conv + bias (src/resnet_dilated.py:16 sliced to the K

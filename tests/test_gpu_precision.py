@@ -48,6 +48,64 @@ def test_f16x3_is_fp32_accurate(cuda_device, case):
     assert 1e-5 < e1 < 5e-3, e1             # genuinely fp16 operands
 
 
+def _unpack_x3(t):
+    """packed split [.., C/32, hi32|lo32] → (hi, lo) [.., C] fp16."""
+    g = t.reshape(*t.shape[:-1], t.shape[-1] // 64, 2, 32)
+    return g[..., 0, :].reshape(*t.shape[:-1], -1), g[..., 1, :].reshape(*t.shape[:-1], -1)
+
+
+def test_producer_split_layouts(cuda_device):
+    """bn_apply / bn_relu_maxpool write exactly hi = f16(x), lo = f16((x-hi)*2^11)
+    in the packed layout (split=3) and the fp16 plane (split=1); keep_fp32=False
+    writes the same split without the fp32 tensor."""
+    from hkp import ops
+    y = rand(2, 15, 20, 128, seed=11).to(cuda_device)
+    ss = torch.cat([rand(128, seed=12) * 0.5 + 1, rand(128, seed=13) * 0.1]).to(cuda_device)
+    act = ops.bn_apply(y, ss, relu=True, split=3)
+    sp, passes = ops.split_of(act)
+    assert passes == 3 and sp.shape == (2, 15, 20, 256)
+    hi, lo = _unpack_x3(sp)
+    assert torch.equal(hi, act.half())
+    assert torch.equal(lo, ((act - act.half().float()) * 2048).half())
+    only = ops.bn_apply(y, ss, relu=True, split=3, keep_fp32=False)
+    assert only.dtype == torch.float16 and torch.equal(only, sp) and ops.channels_of(only) == 128
+    one = ops.bn_apply(y, ss, relu=True, split=1)
+    assert torch.equal(ops.split_of(one)[0], act.half())
+    pool = ops.bn_relu_maxpool(rand(2, 31, 41, 64, seed=15).to(cuda_device), ss[:64].repeat(2), split=3)
+    ph, pl = _unpack_x3(ops.split_of(pool)[0])
+    assert torch.equal(ph, pool.half()) and torch.equal(pl, ((pool - pool.half().float()) * 2048).half())
+    w = rand(64, 3, 3, 96, seed=16).to(cuda_device)
+    wh, wl = _unpack_x3(ops.weight_pack_x3(w))
+    h3, l3 = ops.weight_split(w, 3)
+    assert torch.equal(wh, h3) and torch.equal(wl, l3)
+
+
+X3_CASES = CASES + [
+    (3, 13, 17, 64, 64, 3, 1, 1, 1),        # M = 663: ragged last 256-row tile (and 128-row half)
+    (2, 31, 41, 64, 128, 1, 2, 0, 1),       # 1x1 stride-2 downsample
+    (1, 9, 14, 32, 192, 3, 1, 2, 2),        # C = 32 (one channel group), K = 192 (BN 64)
+]
+
+
+@pytest.mark.parametrize("case", X3_CASES)
+def test_x3_conv_bitwise_equals_inloop_split(cuda_device, case):
+    """The deep-pipelined packed-operand conv (conv_x3_kernel) performs exactly the
+    arithmetic of the in-loop-split kernel: outputs and BN partials bit-identical."""
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    x = F.relu(rand(n, h, w, cin, seed=21)).to(cuda_device)
+    wt = rand(cout, k, k, cin, seed=22, scale=(2.0 / (k * k * cout)) ** 0.5).to(cuda_device)
+    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(cuda_device)
+    xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)      # identity BN → split of x
+    hi, lo = ops.weight_split(wt, 3)
+    y1, p1 = ops.conv2d_fwd_split(x, hi, lo, 3, st, pad, dil)
+    y2, p2 = ops.conv2d_fwd_x3(xs, ops.weight_pack_x3(wt), st, pad, dil)
+    assert torch.equal(y1, y2)
+    assert torch.equal(p1, p2)
+    y3, p3 = ops.conv2d_fwd_x3(xs, ops.weight_pack_x3(wt), st, pad, dil, stats=False)
+    assert p3 is None and torch.equal(y3, y1)
+
+
 @pytest.mark.parametrize("case", [c for c in CASES if c[6] == 1 and c[3] % 64 == 0])
 @pytest.mark.parametrize("gscale", [1.0, 1e-9])
 def test_f16x3_dgrad_scaled(cuda_device, case, gscale):
