@@ -38,19 +38,6 @@ struct SplitArgs {
     int M, Kreal, nkc, cchunks, n_tiles;
 };
 
-// 2^e with e chosen so that amax * 2^e lands in [2^13, 2^14): exact scaling
-// that keeps both hi and the 2^11-scaled lo of the split inside fp16's range
-__device__ __forceinline__ float pow2_scale_for(const unsigned* amax_bits) {
-    if (amax_bits == nullptr) return 1.f;
-    const float m = __uint_as_float(*amax_bits);
-    if (!(m > 0.f) || !(m < INFINITY)) return 1.f;
-    int e;
-    frexpf(m, &e);               // m = f * 2^e, f in [0.5, 1)
-    e = 14 - e;
-    e = e < -100 ? -100 : (e > 100 ? 100 : e);
-    return ldexpf(1.f, e);
-}
-
 constexpr int SBK = 32;         // K chunk (channels of one tap)
 constexpr int SLDR = SBK + 8;   // LDS row stride in halves (80 B)
 constexpr float LO_SCALE = 2048.f;

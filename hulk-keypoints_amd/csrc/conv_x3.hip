@@ -37,6 +37,8 @@ struct X3Args {
     const _Float16* ws;
     float* y;
     float* part;
+    const unsigned* amax;  // max|input| bits: the input was split after scaling by pow2_scale_for(amax) (dgrad)
+    const float* add;      // addend of the output (dgrad: the residual-branch gradient), nullable
     int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
     int M, nks, cch, n_tiles;
 };
@@ -175,8 +177,17 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] += accc[i][j][r] * X3_LO_INV;
+    if (a.amax) {
+        const float inv = 1.f / pow2_scale_for(a.amax);   // exact (power of two)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] *= inv;
+    }
 
-    // ---- epilogue: NHWC store + BN partials per 128-row tile ----
+    // ---- epilogue: NHWC store (+ addend) + BN partials per 128-row tile ----
     const int rbase = m0 + wm * TM * 32 + 4 * kh;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -186,7 +197,10 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                if (m < a.M) a.y[(long)m * a.K + n] = acc[i][j][r];
+                if (m < a.M) {
+                    const long off = (long)m * a.K + n;
+                    a.y[off] = a.add ? acc[i][j][r] + a.add[off] : acc[i][j][r];
+                }
             }
         }
     if (a.part == nullptr) return;
@@ -265,6 +279,251 @@ __global__ __launch_bounds__(256) void weight_pack_x3_kernel(long n, const float
     }
 }
 
+// x * 2^e (e from amax; 1 without) → packed split [P][C/32][hi32|lo32]
+__global__ __launch_bounds__(256) void split_pack_x3_kernel(long n4, const f32x4* __restrict__ x,
+                                                           const unsigned* __restrict__ amax,
+                                                           _Float16* __restrict__ out) {
+    const float sc = pow2_scale_for(amax);
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        f32x4 v = x[i];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= sc;
+        store_split4(v, i, out, 3);
+    }
+}
+
+// flipped dgrad weight, packed: element (c, r', s', k) = w[k][R-1-r'][S-1-s'][c]
+__global__ __launch_bounds__(256) void weight_flip_pack_x3_kernel(int K, int R, int S, int C,
+                                                                 const float* __restrict__ w,
+                                                                 _Float16* __restrict__ out) {
+    const long total = (long)K * R * S * C;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+        const int k = (int)(e % K);
+        long t = e / K;
+        const int sp = (int)(t % S);
+        t /= S;
+        const int rp = (int)(t % R);
+        const int c = (int)(t / R);
+        const float v = w[(((long)k * R + (R - 1 - rp)) * S + (S - 1 - sp)) * C + c];
+        const _Float16 h = (_Float16)v;
+        const long o = 2 * e - (e & 31);
+        out[o] = h;
+        out[o + 32] = (_Float16)((v - (float)h) * SPLIT_LO_SCALE);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient on packed split operands:
+//     dW[k][tap][c] = sum_p dy[p][k] * x[pixel(p, tap)][c]        (p: output pixels)
+// GEMM rows = Cout (dy side, KA per tile), columns = (tap, c) flattened (x side,
+// 256 per tile = 8 channel groups, one per wave for staging), reduction over
+// output pixels, split-K over pixel ranges into fixed-order fp32 slabs
+// [split][K][R*S*C] (summed by wg_x3_reduce_kernel — deterministic).
+// Both LDS images are pixel-major per channel group: line (group, pixel) =
+// 128 B [hi32|lo32], 32 pixels per K-step, written by LDS-DMA; the MFMA
+// fragments (8 consecutive pixels of one channel per lane) come from
+// ds_read_b64_tr_b16 transposed reads.  Swizzle: 16-B chunk ^= ((pixel>>1)&1)<<2
+// makes every 32-lane half of a transposed read cover all 64 banks once.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+struct WgX3Args {
+    const _Float16* xs;     // packed x  [N*H*W][C/32][64]
+    const _Float16* dys;    // packed, scaled dy [M][K/32][64]
+    const unsigned* amax;   // the scale dy was split with (pow2_scale_for), nullable
+    float* ws;              // slabs [splits][K][RSC]
+    int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
+    int M, RSC, r_tiles, mps, tiles;
+};
+
+__device__ __forceinline__ s16x4 ds_tr16(const char* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+}
+
+__device__ __forceinline__ f16x8 cat_tr(s16x4 lo, s16x4 hi) {
+    const auto v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+}
+
+template <int KA>
+__global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
+    constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
+    constexpr int ROW = 128, STAGE = (GX + GD) * 32 * ROW;
+    constexpr int NX = 4, ND = GD / 2, GL = NX + ND;
+    constexpr int TM = KA / 64, TN = 2;
+    static_assert(ND >= 1, "KA must be 64 or 128");
+    __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);       // same pixel range → same XCD
+    const int split = bid / a.tiles, tile = bid - split * a.tiles;
+    const int kt = tile / a.r_tiles, rt = tile - kt * a.r_tiles;
+    const int k0 = kt * KA, r0 = rt * BR;
+    const int p_begin = split * a.mps;
+    const int p_end = min(a.M, p_begin + a.mps);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // ---- staging bookkeeping ----
+    const int Lx = ((lane & 7) ^ (((lane >> 4) & 1) << 2)) * 8;   // logical chunk (halves) this lane fetches
+    const int mg = r0 + 32 * w;                                   // first column of this wave's x group
+    const bool gvalid = mg < a.RSC;
+    const int tap = gvalid ? mg / a.C : 0;
+    const int cg = gvalid ? (mg - tap * a.C) >> 5 : 0;
+    const int rr = tap / a.S, ss = tap - rr * a.S;
+    const int dh = rr * a.dil - a.pad, dw = ss * a.dil - a.pad;
+    const int xstride = a.C * 2, dstride = a.K * 2;
+    const _Float16* xg = a.xs + cg * 64 + Lx;
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    int xn[NX], xho[NX], xwo[NX];
+    const int hw = a.Ho * a.Wo;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+        const int p = p_begin + 8 * i + (lane >> 3);
+        xn[i] = p / hw;
+        const int rem = p - xn[i] * hw;
+        xho[i] = rem / a.Wo;
+        xwo[i] = rem - xho[i] * a.Wo;
+    }
+    const _Float16* dg[ND];
+    int dpp[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        const int line = 8 * (w * ND + j) + (lane >> 3);
+        dpp[j] = line & 31;
+        dg[j] = a.dys + (k0 >> 5) * 64 + (line >> 5) * 64 + Lx;
+    }
+
+    auto issue = [&](int t) {
+        char* st = smem + (t % 3) * STAGE;
+        const int pb = p_begin + 32 * t;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const int p = pb + 8 * i + (lane >> 3);
+            const int hi = xho[i] * a.stride + dh, wi = xwo[i] * a.stride + dw;
+            const bool in = gvalid && p < p_end && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const long pix = ((long)xn[i] * a.H + hi) * a.W + wi;
+            glds16(in ? xg + pix * xstride : zero, st + (w * 32 + 8 * i) * ROW);
+            xwo[i] += 32;                                    // this slot's pixel for the next K-step
+            while (xwo[i] >= a.Wo) {
+                xwo[i] -= a.Wo;
+                if (++xho[i] == a.Ho) {
+                    xho[i] = 0;
+                    ++xn[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            const int p = pb + dpp[j];
+            glds16(p < p_end ? dg[j] + (long)p * dstride : zero, st + (GX * 32 + 8 * (w * ND + j)) * ROW);
+        }
+    };
+
+    f32x16 acc[TM][TN], accc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[i][j][r] = 0.f;
+                accc[i][j][r] = 0.f;
+            }
+
+    // transposed-read addressing: 16-lane group G reads 4 pixel rows (q) x 16
+    // channels (column block cb = G&1); lane 4q+p supplies row q, channels 4p..4p+3
+    const int wk = w & 1, wr = w >> 1;
+    const int h = lane >> 5, cb = (lane >> 4) & 1, q = (lane >> 2) & 3, pq = lane & 3;
+    int toff[2];
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+        toff[pl] = (8 * h + q) * ROW + (((4 * pl + 2 * cb + (pq >> 1)) ^ (((q >> 1) & 1) << 2)) << 4) + 8 * (pq & 1);
+    const int a_line = (GX + wk * TM) * 32 * ROW;     // dy groups of this wave
+    const int b_line = (wr * TN) * 32 * ROW;          // x groups of this wave
+
+    const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
+    if (nsteps > 0) issue(0);
+    if (nsteps > 1) issue(1);
+    for (int t = 0; t < nsteps; ++t) {
+        if (t + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (t + 2 < nsteps) issue(t + 2);
+        const char* st = smem + (t % 3) * STAGE;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            f16x8 dhf[TM], dlf[TM], xhf[TN], xlf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const char* b = st + a_line + i * 32 * ROW + s * 16 * ROW;
+                dhf[i] = cat_tr(ds_tr16(b + toff[0]), ds_tr16(b + toff[0] + 4 * ROW));
+                dlf[i] = cat_tr(ds_tr16(b + toff[1]), ds_tr16(b + toff[1] + 4 * ROW));
+            }
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const char* b = st + b_line + j * 32 * ROW + s * 16 * ROW;
+                xhf[j] = cat_tr(ds_tr16(b + toff[0]), ds_tr16(b + toff[0] + 4 * ROW));
+                xlf[j] = cat_tr(ds_tr16(b + toff[1]), ds_tr16(b + toff[1] + 4 * ROW));
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dhf[i], xhf[j], acc[i][j], 0, 0, 0);
+                    accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dhf[i], xlf[j], accc[i][j], 0, 0, 0);
+                    accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dlf[i], xhf[j], accc[i][j], 0, 0, 0);
+                }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+
+    const float inv = 1.f / pow2_scale_for(a.amax);
+    float* out = a.ws + (long)split * a.K * a.RSC;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int m = r0 + wr * 64 + j * 32 + (lane & 31);
+            if (m >= a.RSC) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = k0 + wk * TM * 32 + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
+                out[(long)k * a.RSC + m] = (acc[i][j][r] + accc[i][j][r] * X3_LO_INV) * inv;
+            }
+        }
+}
+
+// dw[i] = sum_split ws[split][i], fixed order
+__global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, const f32x4* __restrict__ ws,
+                                                          f32x4* __restrict__ dw) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+        f32x4 s = ws[i];
+        for (int k = 1; k < splits; ++k) {
+            const f32x4 v = ws[(long)k * n4 + i];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) s[e] += v[e];
+        }
+        dw[i] = s;
+    }
+}
+
+static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, int* ka, int* r_tiles) {
+    *ka = d->k % 128 == 0 ? 128 : 64;
+    const long rsc = (long)d->r * d->s * d->c;
+    *r_tiles = (int)((rsc + 255) / 256);
+    const long tiles = (long)(d->k / *ka) * *r_tiles;
+    long sp = (1024 + tiles - 1) / tiles;                  // ~4 waves of blocks over 256 CUs
+    const long max_sp = (M + 511) / 512;                   // at least 16 K-steps per block
+    if (sp > max_sp) sp = max_sp;
+    if (sp < 1) sp = 1;
+    long m = (M + sp - 1) / sp;
+    m = (m + 31) / 32 * 32;
+    *splits = (int)((M + m - 1) / m);
+    *mps = (int)m;
+}
+
 }  // namespace hkp
 
 using namespace hkp;
@@ -292,6 +551,7 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w * d->c < (1L << 40), "hkp_conv2d_fwd_x3: too large");
     X3Args a;
     a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.y = y; a.part = stat_partials;
+    a.amax = nullptr; a.add = nullptr;
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.cch = d->c / 32; a.nks = d->r * d->s * a.cch;
@@ -302,5 +562,103 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     if (bn == 128) hipLaunchKernelGGL(conv_x3_kernel<128>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(conv_x3_kernel<64>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_x3");
+    return HKP_OK;
+}
+
+extern "C" int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits,
+                                 uint16_t* x_split, hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && c > 0 && c % 32 == 0 && n % c == 0 && x && x_split, "hkp_split_pack_x3: bad args");
+    long g = (n / 4 + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(split_pack_x3_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), (long)(n / 4),
+                       (const f32x4*)x, (const unsigned*)amax_bits, (_Float16*)x_split);
+    HKP_LAUNCH_CHECK("hkp_split_pack_x3");
+    return HKP_OK;
+}
+
+extern "C" int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf_split,
+                                       hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && w && wf_split, "hkp_weight_flip_pack_x3: null argument");
+    HKP_CHECK_ARG(d->k % 32 == 0, "hkp_weight_flip_pack_x3: need Cout%%32==0 (k=%d)", d->k);
+    const long total = (long)d->k * d->r * d->s * d->c;
+    long g = (total + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(weight_flip_pack_x3_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), d->k, d->r,
+                       d->s, d->c, w, (_Float16*)wf_split);
+    HKP_LAUNCH_CHECK("hkp_weight_flip_pack_x3");
+    return HKP_OK;
+}
+
+extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
+                                      const uint32_t* dy_amax_bits, const float* add, float* dx,
+                                      hkp_stream_t stream) {
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    HKP_CHECK_ARG(dy_split && wf_split && dx, "hkp_conv2d_bwd_data_x3: null tensor");
+    HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC && d->stride == 1,
+                  "hkp_conv2d_bwd_data_x3: stride-1 NHWC convs only (strided ones use hkp_conv2d_bwd_data)");
+    HKP_CHECK_ARG(d->c % 64 == 0 && d->k % 32 == 0, "hkp_conv2d_bwd_data_x3: need Cin%%64==0, Cout%%32==0");
+    const int padp = d->dilation * (d->r - 1) - d->pad;
+    HKP_CHECK_ARG(padp >= 0 && d->dilation * (d->s - 1) - d->pad == padp, "hkp_conv2d_bwd_data_x3: padding");
+    const long M = (long)d->n * d->h * d->w;
+    HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_data_x3: too large");
+    X3Args a;
+    a.xs = (const _Float16*)dy_split; a.ws = (const _Float16*)wf_split; a.y = dx; a.part = nullptr;
+    a.amax = (const unsigned*)dy_amax_bits; a.add = add;
+    a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
+    a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
+    a.M = (int)M; a.cch = d->k / 32; a.nks = d->r * d->s * a.cch;
+    const int bn = d->c % 128 == 0 ? 128 : 64;
+    a.n_tiles = d->c / bn;
+    const long m_tiles = (M + 255) / 256;
+    hipStream_t st = as_stream(stream);
+    if (bn == 128) hipLaunchKernelGGL(conv_x3_kernel<128>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(conv_x3_kernel<64>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
+    HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3");
+    return HKP_OK;
+}
+
+extern "C" int64_t hkp_conv_bwd_filter_x3_workspace(const hkp_conv_desc* d) {
+    int ho, wo;
+    if (hkp_conv_out_hw(d, &ho, &wo) != HKP_OK) return -1;
+    int sp, mps, ka, rt;
+    wg_x3_plan(d, (long)d->n * ho * wo, &sp, &mps, &ka, &rt);
+    return (int64_t)sp * d->k * d->r * d->s * d->c * (int64_t)sizeof(float);
+}
+
+extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* dy_split,
+                                        const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
+                                        hkp_stream_t stream) {
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    HKP_CHECK_ARG(x_split && dy_split && dw && workspace, "hkp_conv2d_bwd_filter_x3: null tensor");
+    HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "hkp_conv2d_bwd_filter_x3: NHWC convs only");
+    HKP_CHECK_ARG(d->k % 64 == 0 && d->c % 32 == 0, "hkp_conv2d_bwd_filter_x3: need Cout%%64==0, Cin%%32==0");
+    const long M = (long)d->n * ho * wo;
+    HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_filter_x3: too large");
+    int sp, mps, ka, rt;
+    wg_x3_plan(d, M, &sp, &mps, &ka, &rt);
+    const long n = (long)d->k * d->r * d->s * d->c;
+    HKP_CHECK_ARG(ws_bytes >= sp * n * (long)sizeof(float), "hkp_conv2d_bwd_filter_x3: workspace %ld < %ld",
+                  (long)ws_bytes, sp * n * (long)sizeof(float));
+    WgX3Args a;
+    a.xs = (const _Float16*)x_split; a.dys = (const _Float16*)dy_split; a.amax = (const unsigned*)dy_amax_bits;
+    a.ws = (float*)workspace;
+    a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
+    a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
+    a.M = (int)M; a.RSC = d->r * d->s * d->c; a.r_tiles = rt; a.mps = mps;
+    a.tiles = (d->k / ka) * rt;
+    hipStream_t st = as_stream(stream);
+    const unsigned grid = (unsigned)(a.tiles * sp);
+    if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
+    else hipLaunchKernelGGL(wgrad_x3_kernel<64>, dim3(grid), dim3(512), 0, st, a);
+    HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3");
+    long g = (n / 4 + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(wg_x3_reduce_kernel, dim3((unsigned)g), dim3(256), 0, st, n / 4, sp, (const f32x4*)workspace,
+                       (f32x4*)dw);
+    HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3 (reduce)");
     return HKP_OK;
 }

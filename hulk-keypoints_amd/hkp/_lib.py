@@ -51,6 +51,11 @@ SIGNATURES = {
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
+    "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
+    "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
+    "hkp_conv_bwd_filter_x3_workspace": (_I64, [_CD]),
+    "hkp_conv2d_bwd_filter_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_bwd_filter_split_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     # backward

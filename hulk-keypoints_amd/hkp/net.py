@@ -212,7 +212,23 @@ class Grads(dict):
 def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
     """wgrad (+ dgrad with the residual addend fused) for one NHWC conv."""
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
-    split_ok = _precision == "f16x3" and x.shape[-1] % 64 == 0 and dy.shape[-1] % 64 == 0
+    c, k = x.shape[-1], dy.shape[-1]
+    xs = ops.split_of(x)
+    if _precision == "f16x3" and xs is not None and xs[1] == 3 and k % 64 == 0 and c % 64 == 0:
+        # packed split operands: dy split once (scaled by a power of two from
+        # max|dy|) and read by both the dgrad and the wgrad conv
+        amax = ops.absmax(dy)
+        dys = ops.split_pack_x3(dy, amax)
+        dx = None
+        if need_dx:
+            if st == 1:
+                wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
+                dx = ops.conv2d_bwd_data_x3(dys, wfs, tuple(x.shape), pd, dl, add=add, amax=amax)
+            else:
+                dx = ops.conv2d_bwd_data(dy, ops.conv_weight_flip(conv.weight), tuple(x.shape), st, pd, dl, add=add)
+        grads.put(conv.weight, ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax))
+        return dx
+    split_ok = _precision == "f16x3" and c % 64 == 0 and k % 64 == 0
     amax = ops.absmax(dy) if split_ok else None
     dx = None
     if need_dx:

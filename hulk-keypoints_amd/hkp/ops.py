@@ -411,6 +411,82 @@ def conv2d_bwd_filter_split(x, dy, w_shape, stride=1, pad=0, dil=1, amax=None):
     return dw
 
 
+def split_pack_x3(x, amax=None):
+    """fp32 NHWC x (scaled by the power of two of amax, if given) → packed split [.., 2C]."""
+    _need(x, torch.float32, "split_pack_x3.x")
+    c = x.shape[-1]
+    out = torch.empty(tuple(x.shape[:-1]) + (2 * c,), device=x.device, dtype=torch.float16)
+    call("hkp_split_pack_x3", x.numel(), c, _ptr(x), _ptr(amax), _ptr(out), _stream())
+    out._hkp_split_passes = 3
+    return out
+
+
+def weight_flip_pack_x3(w):
+    """KRSC [K,R,S,C] fp32 → packed flipped [C,R,S,2K] fp16 for conv2d_bwd_data_x3."""
+    _need(w, torch.float32, "weight_flip_pack_x3.w", 4)
+    k, r, s, c = w.shape
+    d = ConvDesc(1, 1, 1, c, k, r, s, 1, 0, 1, HKP_LAYOUT_NHWC)
+    out = torch.empty((c, r, s, 2 * k), device=w.device, dtype=torch.float16)
+    call("hkp_weight_flip_pack_x3", ctypes.byref(d), _ptr(w), _ptr(out), _stream())
+    return out
+
+
+def conv2d_bwd_data_x3(dys, wfs, x_shape, pad=0, dil=1, add=None, amax=None):
+    """f16x3 dL/dx of a stride-1 NHWC conv from packed dy (split_pack_x3 with `amax`)."""
+    _need(dys, torch.float16, "conv2d_bwd_data_x3.dy_split", 4)
+    _need(wfs, torch.float16, "conv2d_bwd_data_x3.wf_split", 4)
+    c, r, s, k2 = wfs.shape
+    k = k2 // 2
+    d = _fwd_desc(x_shape, (k, r, s, c), 1, pad, dil, "nhwc")
+    ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, 1, pad, dil)
+    if tuple(dys.shape) != (x_shape[0], ho, wo, 2 * k):
+        raise HkpError("conv2d_bwd_data_x3: dy split shape %s != %s" % (tuple(dys.shape), (x_shape[0], ho, wo, 2 * k)))
+    if add is not None:
+        _need(add, torch.float32, "conv2d_bwd_data_x3.add", 4)
+        if tuple(add.shape) != tuple(x_shape):
+            raise HkpError("conv2d_bwd_data_x3: add shape mismatch")
+    dx = torch.empty(tuple(x_shape), device=dys.device, dtype=torch.float32)
+
+    def launch():
+        call("hkp_conv2d_bwd_data_x3", ctypes.byref(d), _ptr(dys), _ptr(wfs), _ptr(amax), _ptr(add), _ptr(dx),
+             _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        _observer("conv_x3_kernel<%d>" % (128 if c % 128 == 0 else 64),
+                  2.0 * x_shape[0] * x_shape[1] * x_shape[2] * c * r * s * k,
+                  2.0 * (dys.numel() + wfs.numel()) + 4.0 * dx.numel(), launch)
+    return dx
+
+
+def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None):
+    """f16x3 dL/dw (KRSC) from packed x (forward operand) and packed dy (split_pack_x3 with `amax`)."""
+    from ._lib import lib
+    _need(xs, torch.float16, "conv2d_bwd_filter_x3.x_split", 4)
+    _need(dys, torch.float16, "conv2d_bwd_filter_x3.dy_split", 4)
+    n, h, wd, c2 = xs.shape
+    d = _fwd_desc((n, h, wd, c2 // 2), tuple(w_shape), stride, pad, dil, "nhwc")
+    ho, wo = conv_out_hw(h, wd, d.r, d.s, stride, pad, dil)
+    if tuple(dys.shape) != (n, ho, wo, 2 * d.k):
+        raise HkpError("conv2d_bwd_filter_x3: dy split shape %s != %s" % (tuple(dys.shape), (n, ho, wo, 2 * d.k)))
+    nbytes = lib().hkp_conv_bwd_filter_x3_workspace(ctypes.byref(d))
+    ws = torch.empty(max(nbytes, 4) // 4, device=xs.device, dtype=torch.float32)
+    dw = torch.empty(tuple(w_shape), device=xs.device, dtype=torch.float32)
+
+    def launch():
+        call("hkp_conv2d_bwd_filter_x3", ctypes.byref(d), _ptr(xs), _ptr(dys), _ptr(amax), _ptr(dw), _ptr(ws),
+             nbytes, _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        _observer("wgrad_x3_kernel<%d>" % (128 if d.k % 128 == 0 else 64),
+                  2.0 * n * ho * wo * d.k * d.r * d.s * d.c, 2.0 * (xs.numel() + dys.numel()) + 4.0 * dw.numel(),
+                  launch)
+    return dw
+
+
 def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out=None, accumulate=False):
     """dL/dw in the weight's own layout (KRSC, or OIHW for the NCHW stem)."""
     _need(x, torch.float32, "conv2d_bwd_filter.x", 4)

@@ -191,6 +191,30 @@ int hkp_conv2d_bwd_filter_split(const hkp_conv_desc* d, const float* x, const fl
                                 const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
                                 hkp_stream_t stream);
 
+/* f16x3 backward on packed split operands (the layout of hkp_conv2d_fwd_x3):
+ *   hkp_split_pack_x3:       x * 2^e → packed split [n/c][c/32][64]; 2^e from
+ *                            amax_bits (max|x| as from hkp_absmax; NULL: 2^0) puts
+ *                            max|x|*2^e in [2^13, 2^14) — gradients far below
+ *                            fp16's normal range keep fp32-class accuracy.
+ *   hkp_weight_flip_pack_x3: KRSC w → packed flipped [c][r][s][k/32][64] (dgrad operand).
+ *   hkp_conv2d_bwd_data_x3:  dx = conv(dy, flipped w) + add for stride-1 convs,
+ *                            dy_split packed with the scale of dy_amax_bits;
+ *                            needs Cin % 64 == 0, Cout % 32 == 0.
+ *   hkp_conv2d_bwd_filter_x3: dw (KRSC) from x_split (forward operand) and dy_split;
+ *                            split-K over output pixels into `workspace`
+ *                            (hkp_conv_bwd_filter_x3_workspace bytes), fixed-order
+ *                            reduce; needs Cout % 64 == 0, Cin % 32 == 0.
+ * Replace the same cuDNN backward calls as hkp_conv2d_bwd_data / _filter. */
+int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits, uint16_t* x_split,
+                      hkp_stream_t stream);
+int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf_split, hkp_stream_t stream);
+int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
+                           const uint32_t* dy_amax_bits, const float* add, float* dx, hkp_stream_t stream);
+int64_t hkp_conv_bwd_filter_x3_workspace(const hkp_conv_desc* d);
+int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* dy_split,
+                             const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
+                             hkp_stream_t stream);
+
 /* dw (KRSC, or OIHW for the stem) = sum over pixels of dy x im2col(x); split-K over
  * pixels into `workspace`, reduced in fixed order.  accumulate != 0 adds into dw. */
 int64_t hkp_conv_bwd_filter_workspace(const hkp_conv_desc* d);

@@ -147,6 +147,57 @@ def test_f16x3_wgrad_scaled(cuda_device, case, gscale):
     assert err < 2e-6, err
 
 
+@pytest.mark.parametrize("case", [c for c in X3_CASES if c[6] == 1 and c[3] % 64 == 0])
+@pytest.mark.parametrize("gscale", [1.0, 1e-9])
+def test_x3_dgrad_bitwise_equals_inloop_split(cuda_device, case, gscale):
+    """dgrad on packed scaled dy (split_pack_x3 + conv_x3_kernel) is bit-identical to
+    the in-loop-split dgrad kernel (same scaling, k order, epilogue)."""
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    wt = rand(cout, k, k, cin, seed=5, scale=(2.0 / (k * k * cout)) ** 0.5).to(cuda_device)
+    ho = (h + 2 * pad - dil * (k - 1) - 1) + 1
+    wo = (w + 2 * pad - dil * (k - 1) - 1) + 1
+    gy = (rand(n, ho, wo, cout, seed=6) * gscale).to(cuda_device)
+    add = (rand(n, h, w, cin, seed=7) * gscale).to(cuda_device)
+    amax = ops.absmax(gy)
+    hi, lo = ops.conv_weight_flip_split(wt)
+    dx1 = ops.conv2d_bwd_data_split(gy, hi, lo, (n, h, w, cin), pad, dil, add=add, amax=amax)
+    dys = ops.split_pack_x3(gy, amax)
+    dx2 = ops.conv2d_bwd_data_x3(dys, ops.weight_flip_pack_x3(wt), (n, h, w, cin), pad, dil, add=add, amax=amax)
+    assert torch.equal(dx1, dx2)
+
+
+WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
+    (2, 7, 9, 64, 64, 3, 1, 1, 1),          # Wo = 9 < 32: a K-step spans several rows/images
+    (1, 30, 40, 96, 128, 3, 2, 1, 1),       # stride 2, RSC = 864 (ragged 256-column tile)
+]
+
+
+@pytest.mark.parametrize("case", WG_X3_CASES)
+@pytest.mark.parametrize("gscale", [1.0, 1e-9])
+def test_x3_wgrad_scaled(cuda_device, case, gscale):
+    """wgrad on packed operands (transposed LDS reads, split-K over pixels): fp32-class
+    accuracy vs fp64, also for gradients far below fp16's normal range."""
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    x = F.relu(rand(n, cin, h, w, seed=8))
+    ho = (h + 2 * pad - dil * (k - 1) - 1) // st + 1
+    wo = (w + 2 * pad - dil * (k - 1) - 1) // st + 1
+    gy = rand(n, cout, ho, wo, seed=9) * gscale
+    ref = torch.nn.grad.conv2d_weight(x.double(), (cout, cin, k, k), gy.double(), st, pad, dil)
+    d = cuda_device
+    xd = x.permute(0, 2, 3, 1).contiguous().to(d)
+    gy_d = gy.permute(0, 2, 3, 1).contiguous().to(d)
+    xs = ops.split_pack_x3(xd)
+    amax = ops.absmax(gy_d)
+    dw = ops.conv2d_bwd_filter_x3(xs, ops.split_pack_x3(gy_d, amax), (cout, k, k, cin), st, pad, dil, amax=amax)
+    err = (dw.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    if cin % 64 == 0:   # same sums as the register-staged split wgrad, different order
+        dw2 = ops.conv2d_bwd_filter_split(xd, gy_d, (cout, k, k, cin), st, pad, dil, amax=amax)
+        assert (dw - dw2).abs().max().item() <= 4e-6 * dw2.abs().max().item()
+
+
 def _model(bb, k, wseed, dev):
     from src.model import KeypointsGauss
     m = KeypointsGauss(k, backbone=bb, pretrained=False)
