@@ -90,8 +90,9 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
     f16x8 rbh[BP], rbl[BP];
 
     auto load_chunk = [&](int kc) {
-        const int tap = kc / a.cchunks;
-        const int c0 = (kc - tap * a.cchunks) * SBK;
+        const int cg = kc / (a.R * a.S);                 // channel-group-major K order (L2 reuse,
+        const int tap = kc - cg * (a.R * a.S);           // as conv_x3.hip)
+        const int c0 = cg * SBK;
         const int rr = tap / a.S, ss = tap - rr * a.S;
 #pragma unroll
         for (int i = 0; i < AP; ++i) {
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void conv_split_kernel(SplitArgs a) {
         }
 #pragma unroll
         for (int i = 0; i < BP; ++i) {
-            const long off = (long)(n0 + browb + 64 * i) * a.Kreal + kc * SBK + c8 * 8;
+            const long off = (long)(n0 + browb + 64 * i) * a.Kreal + tap * a.C + c0 + c8 * 8;
             rbh[i] = *(const f16x8*)(a.whi + off);
             if constexpr (PASSES == 3) rbl[i] = *(const f16x8*)(a.wlo + off);
         }

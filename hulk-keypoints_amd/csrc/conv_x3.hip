@@ -11,7 +11,8 @@
 // so one K-step (one filter tap x 32 channels) of one GEMM row is exactly one
 // 128-B cache line holding both planes.  The same bytes as the fp32 tensor.
 //
-// Tile 256 (pixels) x BN (output channels) x 32 channels, 8 waves as 4x2.
+// Tile 256 (pixels) x BN (output channels) x 32 channels, 8 waves as 4x2;
+// K order: channel group outer, filter tap inner (L2 reuse of pixel lines).
 // Staging is LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
 // ds_write) into a 3-stage LDS ring, two K-steps in flight ahead of the
 // compute, retired by a counted s_waitcnt vmcnt + raw s_barrier (never
@@ -40,10 +41,18 @@ struct X3Args {
     const unsigned* amax;  // max|input| bits: the input was split after scaling by pow2_scale_for(amax) (dgrad)
     const float* add;      // addend of the output (dgrad: the residual-branch gradient), nullable
     int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
-    int M, nks, cch, n_tiles;
+    int M, nks, cch, n_tiles, RS;
 };
 
 constexpr float X3_LO_INV = 1.f / 2048.f;
+
+// raw workgroup barrier (no vmcnt(0) drain: LDS-DMA stays in flight across it) +
+// compiler fence so no LDS access is moved across it
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -101,20 +110,33 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     }
     const _Float16* zero = (const _Float16*)g_x3_zero_line;
 
-    auto issue = [&](int t) {
-        char* st = smem + (t % 3) * STAGE;
-        const int tap = t / a.cch;
-        const int cc = t - tap * a.cch;
-        const int rr = tap / a.S, ss = tap - rr * a.S;
-        const int dh = rr * a.dil, dw = ss * a.dil;
-        const long toff = ((long)dh * a.W + dw) * cstride + cc * 64;
+    // staging state of the next K-step to issue (wave-uniform, advanced per issue).
+    // K order is channel-group-major: the R*S taps of one 32-channel group run
+    // back to back, so a pixel line is re-read by the next taps while it is still
+    // in L2 (tap-major order re-fetched it from HBM for most taps).
+    int q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_buf = 0;
+    auto issue_next = [&]() {
+        char* st = smem + q_buf * STAGE;
+        const int dh = q_rr * a.dil, dw = q_ss * a.dil;
+        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64;
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const bool in = (unsigned)(a_hb[i] + dh) < (unsigned)a.H && (unsigned)(a_wb[i] + dw) < (unsigned)a.W;
             glds16(in ? a_p[i] + toff : zero, st + (8 * (w * GA + i)) * ROW);
         }
+        const long boff = (long)(q_tap * a.cch + q_cc) * 64;
 #pragma unroll
-        for (int j = 0; j < GB; ++j) glds16(b_src[j] + (long)t * 64, st + (BM + 8 * (w * GB + j)) * ROW);
+        for (int j = 0; j < GB; ++j) glds16(b_src[j] + boff, st + (BM + 8 * (w * GB + j)) * ROW);
+        q_buf = q_buf == 2 ? 0 : q_buf + 1;
+        if (++q_ss == a.S) {
+            q_ss = 0;
+            ++q_rr;
+        }
+        if (++q_tap == a.RS) {
+            q_tap = 0;
+            q_rr = 0;
+            ++q_cc;
+        }
     };
 
     f32x16 acc[TM][TN], accc[TM][TN];
@@ -138,39 +160,86 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         for (int s = 0; s < 2; ++s) foff[pl][s] = frow * ROW + (((4 * pl + 2 * s + kh) ^ sw) << 4);
     const int a_base = (wm * TM * 32) * ROW, b_base = (BM + wn * TN * 32) * ROW;
 
-    const int nks = a.nks;
-    issue(0);
-    if (nks > 1) issue(1);
-    for (int t = 0; t < nks; ++t) {
-        if (t + 1 < nks) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();      // stage t landed for every wave; stage t-1 fully read
-        if (t + 2 < nks) issue(t + 2);
-        const char* st = smem + (t % 3) * STAGE;
+    struct Frag {
+        f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+    };
+    auto read_frag = [&](Frag& f, const char* st, int s) {
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            f16x8 ah[TM], al[TM], bh[TN], bl[TN];
+        for (int i = 0; i < TM; ++i) {
+            f.ah[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][s]);
+            f.al[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][s]);
+        }
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                ah[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][s]);
-                al[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][s]);
-            }
+        for (int j = 0; j < TN; ++j) {
+            f.bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][s]);
+            f.bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][s]);
+        }
+    };
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][s]);
-                bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][s]);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
+                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[j], accc[i][j], 0, 0, 0);
+                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[j], accc[i][j], 0, 0, 0);
             }
+    };
+
+    // Software pipeline, one barrier per K-step, placed between its two halves:
+    //   [issue DMA t+2] [read frags s=1 of t] [MFMA s=0 of t]
+    //   wait own DMA of t+1, barrier (t+1 landed everywhere; t fully read)
+    //   [read frags s=0 of t+1] [MFMA s=1 of t]
+    // DMA t+2 overwrites the buffer of t-1, whose last reads retired before the
+    // previous barrier (lgkmcnt(0) ahead of it).
+    const int nks = a.nks;
+    issue_next();
+    if (nks > 1) issue_next();
+    if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    Frag f0, f1;
+    int cur = 0;
+    read_frag(f0, smem, 0);
+    // one K-step; ISSUE: DMA K-step t+2, NEXT: a K-step t+1 follows.  Each half is
+    // one basic block so the ds_reads can be interleaved one per MFMA gap.
+    auto step = [&](const bool ISSUE, const bool NEXT) {
+        const char* st = smem + cur * STAGE;
+        if (ISSUE) issue_next();
+        read_frag(f1, st, 1);
+        mma(f0);
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], accc[i][j], 0, 0, 0);
-                    accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], accc[i][j], 0, 0, 0);
-                }
+        for (int k = 0; k < 2 * (TM + TN); ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 ds_read
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM * TN - 2 * (TM + TN), 0);
+        __builtin_amdgcn_sched_barrier(0);       // keep every MFMA of this half ahead of the wait
+        if (NEXT) {
+            if (ISSUE) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            cur = cur == 2 ? 0 : cur + 1;
+            mma(f1);
+            read_frag(f0, smem + cur * STAGE, 0);
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+            for (int k = 0; k < 2 * (TM + TN); ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM * TN - 1 - 2 * (TM + TN), 0);
+        } else {
+            mma(f1);
+        }
+    };
+    int t = 0;
+    for (; t + 2 < nks; ++t) step(true, true);
+    if (t + 1 < nks) {
+        step(false, true);
+        ++t;
     }
+    step(false, false);
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -554,7 +623,7 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     a.amax = nullptr; a.add = nullptr;
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
-    a.M = (int)M; a.cch = d->c / 32; a.nks = d->r * d->s * a.cch;
+    a.M = (int)M; a.cch = d->c / 32; a.nks = d->r * d->s * a.cch; a.RS = d->r * d->s;
     const int bn = d->k % 128 == 0 ? 128 : 64;
     a.n_tiles = d->k / bn;
     const long m_tiles = (M + 255) / 256;
@@ -608,7 +677,7 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     a.amax = (const unsigned*)dy_amax_bits; a.add = add;
     a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
     a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
-    a.M = (int)M; a.cch = d->k / 32; a.nks = d->r * d->s * a.cch;
+    a.M = (int)M; a.cch = d->k / 32; a.nks = d->r * d->s * a.cch; a.RS = d->r * d->s;
     const int bn = d->c % 128 == 0 ? 128 : 64;
     a.n_tiles = d->c / bn;
     const long m_tiles = (M + 255) / 256;
