@@ -406,8 +406,20 @@ struct WgX3Args {
     int M, RSC, r_tiles, mps, tiles;
 };
 
-__device__ __forceinline__ s16x4 ds_tr16(const char* p) {
-    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)p);
+// ds_read_b64_tr_b16 as inline asm: the builtin makes hipcc drain the whole
+// LDS-DMA queue (vmcnt(0)) before every transposed read, since it cannot tell
+// the read from the in-flight DMA's destination.  The caller waits lgkmcnt
+// itself before the MFMAs that consume the result (explicit waits below, each
+// followed by sched_barrier(0) so no MFMA is scheduled ahead of it).
+template <int OFF>
+__device__ __forceinline__ s16x4 ds_tr16(unsigned lds_addr) {
+    s16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lds_addr), "i"(OFF));
+    return r;
+}
+
+__device__ __forceinline__ unsigned lds_addr_of(const char* p) {
+    return (unsigned)(size_t)(const __attribute__((address_space(3))) char*)p;
 }
 
 __device__ __forceinline__ f16x8 cat_tr(s16x4 lo, s16x4 hi) {
@@ -511,40 +523,112 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     const int a_line = (GX + wk * TM) * 32 * ROW;     // dy groups of this wave
     const int b_line = (wr * TN) * 32 * ROW;          // x groups of this wave
 
-    const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
-    if (nsteps > 0) issue(0);
-    if (nsteps > 1) issue(1);
-    for (int t = 0; t < nsteps; ++t) {
-        if (t + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        if (t + 2 < nsteps) issue(t + 2);
-        const char* st = smem + (t % 3) * STAGE;
+    struct Frag {
+        f16x8 dh[TM], dl[TM], xh[TN], xl[TN];
+    };
+    // per-lane LDS byte addresses of the two planes' transposed-read blocks
+    const unsigned lds0 = lds_addr_of(smem);
+    const unsigned ta0 = lds0 + a_line + toff[0], ta1 = lds0 + a_line + toff[1];
+    const unsigned tb0 = lds0 + b_line + toff[0], tb1 = lds0 + b_line + toff[1];
+    auto read_frag = [&](Frag& f, int buf, const int s) {
+        const unsigned so = buf * STAGE;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            f16x8 dhf[TM], dlf[TM], xhf[TN], xlf[TN];
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const char* b = st + a_line + i * 32 * ROW + s * 16 * ROW;
-                dhf[i] = cat_tr(ds_tr16(b + toff[0]), ds_tr16(b + toff[0] + 4 * ROW));
-                dlf[i] = cat_tr(ds_tr16(b + toff[1]), ds_tr16(b + toff[1] + 4 * ROW));
+        for (int i = 0; i < TM; ++i) {
+            // immediate offsets: tile i (32 rows), half s (16 rows), second read +4 rows
+            if (s == 0) {
+                f.dh[i] = cat_tr(ds_tr16<0>(ta0 + so + i * 32 * ROW), ds_tr16<4 * ROW>(ta0 + so + i * 32 * ROW));
+                f.dl[i] = cat_tr(ds_tr16<0>(ta1 + so + i * 32 * ROW), ds_tr16<4 * ROW>(ta1 + so + i * 32 * ROW));
+            } else {
+                f.dh[i] = cat_tr(ds_tr16<16 * ROW>(ta0 + so + i * 32 * ROW),
+                                 ds_tr16<20 * ROW>(ta0 + so + i * 32 * ROW));
+                f.dl[i] = cat_tr(ds_tr16<16 * ROW>(ta1 + so + i * 32 * ROW),
+                                 ds_tr16<20 * ROW>(ta1 + so + i * 32 * ROW));
             }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            if (s == 0) {
+                f.xh[j] = cat_tr(ds_tr16<0>(tb0 + so + j * 32 * ROW), ds_tr16<4 * ROW>(tb0 + so + j * 32 * ROW));
+                f.xl[j] = cat_tr(ds_tr16<0>(tb1 + so + j * 32 * ROW), ds_tr16<4 * ROW>(tb1 + so + j * 32 * ROW));
+            } else {
+                f.xh[j] = cat_tr(ds_tr16<16 * ROW>(tb0 + so + j * 32 * ROW),
+                                 ds_tr16<20 * ROW>(tb0 + so + j * 32 * ROW));
+                f.xl[j] = cat_tr(ds_tr16<16 * ROW>(tb1 + so + j * 32 * ROW),
+                                 ds_tr16<20 * ROW>(tb1 + so + j * 32 * ROW));
+            }
+        }
+    };
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const char* b = st + b_line + j * 32 * ROW + s * 16 * ROW;
-                xhf[j] = cat_tr(ds_tr16(b + toff[0]), ds_tr16(b + toff[0] + 4 * ROW));
-                xlf[j] = cat_tr(ds_tr16(b + toff[1]), ds_tr16(b + toff[1] + 4 * ROW));
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dh[i], f.xh[j], acc[i][j], 0, 0, 0);
+                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dh[i], f.xl[j], accc[i][j], 0, 0, 0);
+                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dl[i], f.xh[j], accc[i][j], 0, 0, 0);
             }
+    };
+    // same software pipeline as conv_x3_kernel (see there); 4*(TM+TN) transposed
+    // b64 reads per half, two per MFMA gap
+    // same software pipeline as conv_x3_kernel (see there); 4*(TM+TN) transposed
+    // b64 reads per half, two per MFMA gap.  The reads are inline asm: every
+    // consumer MFMA sits behind an explicit lgkmcnt wait + sched_barrier.
+    constexpr int NR = 4 * (TM + TN), NM = 3 * TM * TN;
+    const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
+    if (nsteps > 0) {
+        int q_t = 0;
+        auto issue_next = [&]() { issue(q_t++); };
+        issue_next();
+        if (nsteps > 1) issue_next();
+        if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        Frag f0, f1;
+        int cur = 0;
+        read_frag(f0, 0, 0);
+        auto step = [&](const bool ISSUE, const bool NEXT) {
+            const int bcur = cur;
+            if (ISSUE) issue_next();
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // f0 (read last half) landed
+            __builtin_amdgcn_sched_barrier(0);
+            read_frag(f1, bcur, 1);
+            mma(f0);
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+            for (int k = 0; k < NR / 2; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x001, 2, 0);   // the asm reads count as ALU
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM - NR / 2, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (NEXT) {
+                if (ISSUE) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                lds_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                cur = cur == 2 ? 0 : cur + 1;
+                mma(f1);
+                read_frag(f0, cur, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dhf[i], xhf[j], acc[i][j], 0, 0, 0);
-                    accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dhf[i], xlf[j], accc[i][j], 0, 0, 0);
-                    accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dlf[i], xhf[j], accc[i][j], 0, 0, 0);
+                for (int k = 0; k < NR / 2; ++k) {
+                    __builtin_amdgcn_sched_group_barrier(0x001, 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 }
+                __builtin_amdgcn_sched_group_barrier(0x008, NM - 1 - NR / 2, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                mma(f1);
+            }
+        };
+        int t = 0;
+        for (; t + 2 < nsteps; ++t) step(true, true);
+        if (t + 1 < nsteps) {
+            step(false, true);
+            ++t;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        step(false, false);
     }
 
     const float inv = 1.f / pow2_scale_for(a.amax);
