@@ -3,7 +3,8 @@
 # combined with trace domains) for the kernels matching $KREGEX, over a short
 # bench run.  Usage (on the GPU box, from the repo root):
 #   tools/pmc_passes.sh OUTDIR "bench args..." [KREGEX]
-# Summarize locally: python tools/pmc_summary.py OUTDIR profiles/<name>.json
+# Writes OUTDIR/pmc_summary.json (tools/pmc_summary.py) and deletes the
+# per-pass databases (they can exceed gpurun's 64 MiB copy-back limit).
 set -u
 OUT=$1
 ARGS=$2
@@ -20,3 +21,5 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY" \
         -- python3 bench.py $ARGS --no-cpu-baseline > "$OUT/pass$i.log" 2>&1 || { echo "pass $i ($grp) failed: rc=$?"; exit 1; }
     echo "pass $i ok: $grp"
 done
+python3 tools/pmc_summary.py "$OUT" "$OUT/pmc_summary.json" > "$OUT/pmc_summary.txt" && rm -rf "$OUT"/pass*/
+cat "$OUT/pmc_summary.txt"
