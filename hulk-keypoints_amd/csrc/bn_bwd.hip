@@ -7,6 +7,8 @@
 //   dy        = (dz - sum(dz)/N - (y - mean) * k) * invstd*gamma,
 //               k = invstd^2 * sum dz*(y - mean) / N     (ATen batch_norm_backward)
 // Sums run per pixel tile in fp32, merged per channel in fp64 in fixed order.
+#include <algorithm>
+
 #include "common.h"
 
 // the maxpool backward must recompute relu(y*a+b) exactly as bn.hip's forward
@@ -109,13 +111,19 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, lon
     }
 }
 
-// dy = ((dz - gm) - (y - mean)*k) * (invstd*gamma), dz = g*(out>0) (MASK) or g
-template <bool MASK>
+// dy = ((dz - gm) - (y - mean)*k) * (invstd*gamma), dz = g*(out>0) (MASK) or g.
+// AMAX: also max|dy| (IEEE bits, block-reduced, one atomicMax per block; the grid
+// is capped at 512 blocks since same-address device atomics serialise) — the
+// power-of-two scale of the f16x3 backward convs' gradient operand, so they need
+// no separate absmax pass over dy
+template <bool MASK, bool AMAX>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, const f32x4* __restrict__ g,
                                                           const f32x4* __restrict__ out, const f32x4* __restrict__ y,
                                                           const f32x4* __restrict__ mean,
-                                                          const f32x4* __restrict__ coef, f32x4* __restrict__ dy) {
+                                                          const f32x4* __restrict__ coef, f32x4* __restrict__ dy,
+                                                          unsigned* __restrict__ amax) {
     const long stride = (long)gridDim.x * blockDim.x;
+    unsigned mx = 0;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         const int c4 = (int)(i % C4);
         f32x4 d = g[i];
@@ -129,6 +137,27 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, cons
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[e] = ((d[e] - gm[e]) - (v[e] - mu[e]) * kk[e]) * sc[e];
         dy[i] = r;
+        if constexpr (AMAX) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const unsigned b = __float_as_uint(r[e]) & 0x7FFFFFFFu;
+                mx = b > mx ? b : mx;
+            }
+        }
+    }
+    if constexpr (AMAX) {
+        __shared__ unsigned red[4];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned t = __shfl_xor(mx, o);
+            mx = t > mx ? t : mx;
+        }
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned a = red[0] > red[1] ? red[0] : red[1], b = red[2] > red[3] ? red[2] : red[3];
+            atomicMax(amax, a > b ? a : b);
+        }
     }
 }
 
@@ -236,19 +265,30 @@ extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, 
 }
 
 extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                                const float* mean_invstd, const float* coef, float* dy, hkp_stream_t stream) {
+                                const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
+                                hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_apply: bad sizes");
     HKP_CHECK_ARG(g && y && mean_invstd && coef && dy, "hkp_bn_bwd_apply: null tensor");
     const long n4 = m * (long)c / 4;
     hipStream_t st = as_stream(stream);
-    if (out_mask)
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<true>), dim3(grid_cap(n4)), dim3(256), 0, st, n4, c / 4,
-                           (const f32x4*)g, (const f32x4*)out_mask, (const f32x4*)y, (const f32x4*)mean_invstd,
-                           (const f32x4*)coef, (f32x4*)dy);
-    else
-        hipLaunchKernelGGL((bn_bwd_apply_kernel<false>), dim3(grid_cap(n4)), dim3(256), 0, st, n4, c / 4,
-                           (const f32x4*)g, (const f32x4*)nullptr, (const f32x4*)y, (const f32x4*)mean_invstd,
-                           (const f32x4*)coef, (f32x4*)dy);
+    if (dy_amax_bits) {
+        hipError_t e = hipMemsetAsync(dy_amax_bits, 0, sizeof(uint32_t), st);
+        if (e != hipSuccess) {
+            set_error("hkp_bn_bwd_apply: memset: %s", hipGetErrorString(e));
+            return (int)e;
+        }
+    }
+#define HKP_BWD_APPLY(MASK, AMAX)                                                                                    \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MASK, AMAX>), dim3(AMAX ? std::min(grid_cap(n4), 512) : grid_cap(n4)), \
+                       dim3(256), 0, st, n4, c / 4,                                                                \
+                       (const f32x4*)g, (const f32x4*)out_mask, (const f32x4*)y, (const f32x4*)mean_invstd,       \
+                       (const f32x4*)coef, (f32x4*)dy, (unsigned*)dy_amax_bits)
+    if (out_mask) {
+        if (dy_amax_bits) HKP_BWD_APPLY(true, true); else HKP_BWD_APPLY(true, false);
+    } else {
+        if (dy_amax_bits) HKP_BWD_APPLY(false, true); else HKP_BWD_APPLY(false, false);
+    }
+#undef HKP_BWD_APPLY
     HKP_LAUNCH_CHECK("hkp_bn_bwd_apply");
     return HKP_OK;
 }

@@ -599,7 +599,7 @@ extern "C" int hkp_absmax(int64_t n, const float* x, uint32_t* amax_bits, hkp_st
         return (int)e;
     }
     long g = (n / 4 + 255) / 256;
-    if (g > 2048) g = 2048;
+    if (g > 512) g = 512;          // one same-address atomicMax per block: keep them few
     hipLaunchKernelGGL(absmax_kernel, dim3((unsigned)g), dim3(256), 0, st, (long)(n / 4), (const f32x4*)x,
                        (unsigned*)amax_bits);
     HKP_LAUNCH_CHECK("hkp_absmax");

@@ -42,6 +42,7 @@ struct X3Args {
     const float* add;      // addend of the output (dgrad: the residual-branch gradient), nullable
     int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
     int M, nks, cch, n_tiles, RS;
+    long plane;            // STEM: halves between the hi and lo image planes
 };
 
 constexpr float X3_LO_INV = 1.f / 2048.f;
@@ -58,7 +59,11 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <int BN>
+// STEM: the 7x7/s2 stem on the zero-padded NHWC4 image planes of
+// hkp_stem_pack_x3 (a.H/a.W = padded size, stride 2, pad 0, R = 7, S = 1: one
+// K-step per filter row = 8 taps x 4 channels; logical chunk j of a row holds
+// padded pixels 2wo+2j, 2wo+2j+1 from the hi plane (j < 4) or the lo plane).
+template <int BN, bool STEM = false>
 __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -77,7 +82,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     const int wm = w / WN, wn = w % WN;
 
     // ---- DMA source bookkeeping (rows this lane feeds) ----
-    const int cstride = a.cch * 64;                // halves per pixel
+    const int cstride = STEM ? 4 : a.cch * 64;     // halves per pixel
     // per row: image-space origin (hb, wb) of its receptive field and the base
     // pointer of that (possibly padded-out) origin pixel; a tap adds a
     // wave-uniform offset.  Rows past M get an origin that is never in-bounds.
@@ -86,7 +91,8 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
         const int row = 8 * (w * GA + i) + (lane >> 3);
-        const int L = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+        const int Lc = (lane & 7) ^ ((row >> 1) & 7);       // logical 16-B chunk this lane fetches
+        const long L = STEM ? (Lc >> 2) * (long)a.plane + (Lc & 3) * 8 : Lc * 8;
         const int m = m0 + row;
         if (m < a.M) {
             const int hw = a.Ho * a.Wo;
@@ -677,6 +683,54 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, in
     *mps = (int)m;
 }
 
+// Stem operand: NCHW fp32 image → zero-padded NHWC4 planes [2][N][Hp][Wp][4]
+// (hi, then lo = f16((x-hi)*2^11)); padded pixel (hp, wp) = input (hp-3, wp-3)
+__global__ __launch_bounds__(256) void stem_pack_x3_kernel(int N, int C, int H, int W, int Hp, int Wp,
+                                                          const float* __restrict__ x, _Float16* __restrict__ out) {
+    const long total = (long)N * Hp * Wp;
+    const long plane = total * 4;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long p = (long)blockIdx.x * blockDim.x + threadIdx.x; p < total; p += stride) {
+        const int wp = (int)(p % Wp);
+        const long t = p / Wp;
+        const int hp = (int)(t % Hp);
+        const int n = (int)(t / Hp);
+        const int h = hp - 3, w = wp - 3;
+        const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+        f32x4 v;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[c] = (in && c < C) ? x[(((long)n * C + c) * H + h) * W + w] : 0.f;
+        h16x4 hv, lv;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const _Float16 hh = (_Float16)v[c];
+            hv[c] = hh;
+            lv[c] = (_Float16)((v[c] - (float)hh) * SPLIT_LO_SCALE);
+        }
+        *(h16x4*)(out + p * 4) = hv;
+        *(h16x4*)(out + plane + p * 4) = lv;
+    }
+}
+
+// Stem weight OIHW [K][C][7][7] → [K][r][hi32|lo32], 32 = 8 taps (s; 7 = 0) x 4 channels (C..3 = 0)
+__global__ __launch_bounds__(256) void stem_weight_pack_x3_kernel(int K, int C, const float* __restrict__ w,
+                                                                 _Float16* __restrict__ out) {
+    const int total = K * 7 * 32;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+        const int c = e & 3, s = (e >> 2) & 7, r = (e >> 5) % 7, k = e / (7 * 32);
+        const float v = (s < 7 && c < C) ? w[(((long)k * C + c) * 7 + r) * 7 + s] : 0.f;
+        const _Float16 h = (_Float16)v;
+        const long o = ((long)k * 7 + r) * 64 + s * 4 + c;
+        out[o] = h;
+        out[o + 32] = (_Float16)((v - (float)h) * SPLIT_LO_SCALE);
+    }
+}
+
+static bool stem_x3_shape(const hkp_conv_desc* d) {
+    return d && d->in_layout == HKP_LAYOUT_NCHW && d->c >= 1 && d->c <= 4 && d->r == 7 && d->s == 7 &&
+           d->stride == 2 && d->pad == 3 && d->dilation == 1 && d->k % 64 == 0;
+}
+
 }  // namespace hkp
 
 using namespace hkp;
@@ -704,7 +758,7 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w * d->c < (1L << 40), "hkp_conv2d_fwd_x3: too large");
     X3Args a;
     a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.y = y; a.part = stat_partials;
-    a.amax = nullptr; a.add = nullptr;
+    a.amax = nullptr; a.add = nullptr; a.plane = 0;
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.cch = d->c / 32; a.nks = d->r * d->s * a.cch; a.RS = d->r * d->s;
@@ -758,7 +812,7 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_data_x3: too large");
     X3Args a;
     a.xs = (const _Float16*)dy_split; a.ws = (const _Float16*)wf_split; a.y = dx; a.part = nullptr;
-    a.amax = (const unsigned*)dy_amax_bits; a.add = add;
+    a.amax = (const unsigned*)dy_amax_bits; a.add = add; a.plane = 0;
     a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
     a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
     a.M = (int)M; a.cch = d->k / 32; a.nks = d->r * d->s * a.cch; a.RS = d->r * d->s;
@@ -813,5 +867,59 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     hipLaunchKernelGGL(wg_x3_reduce_kernel, dim3((unsigned)g), dim3(256), 0, st, n / 4, sp, (const f32x4*)workspace,
                        (f32x4*)dw);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3 (reduce)");
+    return HKP_OK;
+}
+
+extern "C" int64_t hkp_stem_pack_x3_elems(const hkp_conv_desc* d) {
+    int ho, wo;
+    if (!stem_x3_shape(d) || hkp_conv_out_hw(d, &ho, &wo) != HKP_OK) return -1;
+    return 2L * d->n * (2L * ho + 6) * (2L * wo + 6) * 4;
+}
+
+extern "C" int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uint16_t* x_split, hkp_stream_t stream) {
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    HKP_CHECK_ARG(stem_x3_shape(d), "hkp_stem_pack_x3: needs the 7x7/s2/p3 NCHW stem with C<=4, Cout%%64==0");
+    HKP_CHECK_ARG(x_nchw && x_split, "hkp_stem_pack_x3: null tensor");
+    const int hp = 2 * ho + 6, wp = 2 * wo + 6;
+    long g = ((long)d->n * hp * wp + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(stem_pack_x3_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), d->n, d->c, d->h,
+                       d->w, hp, wp, x_nchw, (_Float16*)x_split);
+    HKP_LAUNCH_CHECK("hkp_stem_pack_x3");
+    return HKP_OK;
+}
+
+extern "C" int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split,
+                                       hkp_stream_t stream) {
+    HKP_CHECK_ARG(k > 0 && c >= 1 && c <= 4 && w_oihw && w_split, "hkp_stem_weight_pack_x3: bad args");
+    const int total = k * 7 * 32;
+    hipLaunchKernelGGL(stem_weight_pack_x3_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), k, c,
+                       w_oihw, (_Float16*)w_split);
+    HKP_LAUNCH_CHECK("hkp_stem_weight_pack_x3");
+    return HKP_OK;
+}
+
+extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
+                                      float* y, float* stat_partials, hkp_stream_t stream) {
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    HKP_CHECK_ARG(stem_x3_shape(d), "hkp_conv2d_fwd_stem_x3: needs the 7x7/s2/p3 NCHW stem with C<=4, Cout%%64==0");
+    HKP_CHECK_ARG(x_split && w_split && y, "hkp_conv2d_fwd_stem_x3: null tensor");
+    const long M = (long)d->n * ho * wo;
+    HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_fwd_stem_x3: too large");
+    X3Args a;
+    a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.y = y; a.part = stat_partials;
+    a.amax = nullptr; a.add = nullptr;
+    a.N = d->n; a.H = 2 * ho + 6; a.W = 2 * wo + 6; a.C = 4; a.K = d->k; a.R = 7; a.S = 1;
+    a.stride = 2; a.pad = 0; a.dil = 1; a.Ho = ho; a.Wo = wo;
+    a.M = (int)M; a.cch = 1; a.RS = 7; a.nks = 7;
+    a.plane = (long)d->n * a.H * a.W * 4;
+    a.n_tiles = d->k / 64;
+    const long m_tiles = (M + 255) / 256;
+    hipLaunchKernelGGL((conv_x3_kernel<64, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+    HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
     return HKP_OK;
 }

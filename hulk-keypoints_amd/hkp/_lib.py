@@ -51,6 +51,10 @@ SIGNATURES = {
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_stem_pack_x3_elems": (_I64, [_CD]),
+    "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
+    "hkp_stem_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _P, _P, _P]),
+    "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
     "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
     "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
@@ -66,7 +70,7 @@ SIGNATURES = {
     "hkp_bn_bwd_tiles": (_I64, [_I64]),
     "hkp_bn_bwd_reduce": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_bwd_finalize": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P, _P, _P]),
-    "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_heat_loss_workspace": (_I64, []),
     "hkp_heat_loss": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _P, _P, _P, _P]),

@@ -97,7 +97,10 @@ def conv_bn(conv, bn, x, layout="nhwc"):
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
-    if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
+    if layout == "nchw" and passes == 3 and ops.stem_x3_ok(tuple(x.shape), tuple(conv.weight.shape), st, pd, dl):
+        y, part = ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
+                                         stats=bn.training)
+    elif layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
         y, part = ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training)
     elif layout == "nhwc" and passes:
         hi, lo = _split_weight(conv.weight, passes)
@@ -217,7 +220,9 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
     if _precision == "f16x3" and xs is not None and xs[1] == 3 and k % 64 == 0 and c % 64 == 0:
         # packed split operands: dy split once (scaled by a power of two from
         # max|dy|) and read by both the dgrad and the wgrad conv
-        amax = ops.absmax(dy)
+        amax = getattr(dy, "_hkp_amax", None)     # fused into bn_bwd_apply
+        if amax is None:
+            amax = ops.absmax(dy)
         dys = ops.split_pack_x3(dy, amax)
         dx = None
         if need_dx:
@@ -247,7 +252,8 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
 
 
 def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False):
-    dy, dgamma, dbeta, dz = ops.bn_bwd(g, out_mask, y, mi, bn.weight, want_dz=want_dz)
+    dy, dgamma, dbeta, dz = ops.bn_bwd(g, out_mask, y, mi, bn.weight, want_dz=want_dz,
+                                       want_amax=_precision == "f16x3")
     grads.put(bn.weight, dgamma)
     grads.put(bn.bias, dbeta)
     return dy, dz

@@ -151,6 +151,51 @@ def conv2d_fwd_x3(xs, ws, stride=1, pad=0, dil=1, stats=True, out=None):
     return y, part
 
 
+def stem_x3_ok(x_shape, w_shape, stride, pad, dil):
+    """Whether the stem conv (NCHW x, OIHW w) takes the f16x3 stem kernel."""
+    def one(v):
+        return int(v[0]) if isinstance(v, (tuple, list)) else int(v)
+    k, c, r, s = w_shape
+    return (r, s, one(stride), one(pad), one(dil)) == (7, 7, 2, 3, 1) and 1 <= c <= 4 and k % 64 == 0 \
+        and x_shape[1] == c
+
+
+def stem_weight_pack_x3(w):
+    """OIHW [K,C<=4,7,7] fp32 stem weight → [K,7,64] fp16 (conv2d_fwd_stem_x3 operand)."""
+    _need(w, torch.float32, "stem_weight_pack_x3.w", 4)
+    k, c = w.shape[:2]
+    out = torch.empty((k, 7, 64), device=w.device, dtype=torch.float16)
+    call("hkp_stem_weight_pack_x3", k, c, _ptr(w), _ptr(out), _stream())
+    return out
+
+
+def conv2d_fwd_stem_x3(x, ws, k, stats=True):
+    """f16x3 stem conv (7x7/s2/p3) of an NCHW fp32 image → NHWC fp32 y (+ BN partials)."""
+    from ._lib import lib
+    _need(x, torch.float32, "conv2d_fwd_stem_x3.x", 4)
+    _need(ws, torch.float16, "conv2d_fwd_stem_x3.w_split", 3)
+    n, c, h, wd = x.shape
+    d = ConvDesc(n, h, wd, c, k, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW)
+    ho, wo = conv_out_hw(h, wd, 7, 7, 2, 3, 1)
+    xs = torch.empty(lib().hkp_stem_pack_x3_elems(ctypes.byref(d)), device=x.device, dtype=torch.float16)
+    call("hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())
+    y = torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
+    part = None
+    if stats:
+        tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
+        part = torch.empty((tiles, k, 2), device=x.device, dtype=torch.float32)
+
+    def launch():
+        call("hkp_conv2d_fwd_stem_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(y), _ptr(part), _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        _observer("conv_x3_kernel<64, true>", 2.0 * n * ho * wo * k * 49 * c, 2.0 * (xs.numel() + ws.numel()) +
+                  4.0 * y.numel(), launch)
+    return y, part
+
+
 def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None, x_hi=None):
     """Split-precision (f16x3, passes=3) or plain fp16 (passes=1) NHWC conv; fp32 in/out,
     the activation split inside the conv loop.  x_hi (passes 1): the input's pre-converted
@@ -505,8 +550,10 @@ def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out
     return dw
 
 
-def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False):
-    """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None)."""
+def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False):
+    """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None).
+    want_amax: max|dy| (uint32 IEEE bits, as absmax) is computed in the same pass
+    and attached as dy._hkp_amax."""
     _need(g, torch.float32, "bn_bwd.g")
     _need(y, torch.float32, "bn_bwd.y")
     if g.shape != y.shape or (out_mask is not None and out_mask.shape != y.shape):
@@ -525,8 +572,11 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False):
     call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta),
          _ptr(coef), _stream())
     dy = torch.empty_like(y)
+    amax = torch.empty(1, device=y.device, dtype=torch.int32) if want_amax else None
     call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), _ptr(dy),
-         _stream())
+         _ptr(amax), _stream())
+    if want_amax:
+        dy._hkp_amax = amax
     return dy, dgamma, dbeta, dz
 
 

@@ -191,6 +191,17 @@ int hkp_conv2d_bwd_filter_split(const hkp_conv_desc* d, const float* x, const fl
                                 const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
                                 hkp_stream_t stream);
 
+/* The stem conv (7x7, stride 2, pad 3, NCHW input with C <= 4; src/resnet.py:137,199)
+ * on the f16x3 path: hkp_stem_pack_x3 writes the image as zero-padded NHWC4 fp16
+ * planes [2][n][2*ho+6][2*wo+6][4] (hi, then lo; hkp_stem_pack_x3_elems halves),
+ * hkp_stem_weight_pack_x3 the OIHW weight as [k][7][hi32|lo32] (k*7*64 halves),
+ * hkp_conv2d_fwd_stem_x3 = hkp_conv2d_fwd on them (NHWC fp32 y + BN partials). */
+int64_t hkp_stem_pack_x3_elems(const hkp_conv_desc* d);
+int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uint16_t* x_split, hkp_stream_t stream);
+int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split, hkp_stream_t stream);
+int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split, float* y,
+                           float* stat_partials, hkp_stream_t stream);
+
 /* f16x3 backward on packed split operands (the layout of hkp_conv2d_fwd_x3):
  *   hkp_split_pack_x3:       x * 2^e → packed split [n/c][c/32][64]; 2^e from
  *                            amax_bits (max|x| as from hkp_absmax; NULL: 2^0) puts
@@ -226,14 +237,17 @@ int hkp_conv2d_bwd_filter(const hkp_conv_desc* d, const float* x, const float* d
  *             partials[tiles][c][2] = (sum dz, sum dz*(y-mean)); tiles = hkp_bn_bwd_tiles(m)
  *   finalize: dgamma = invstd*sum dz*(y-mean), dbeta = sum dz (nullable), coef[3c]
  *   apply:    dy = ((dz - sum dz/m) - (y-mean)*invstd^2*sum dz*(y-mean)/m) * invstd*gamma
- * mean_invstd is what hkp_bn_finalize produced in the forward. */
+ * mean_invstd is what hkp_bn_finalize produced in the forward.  apply also writes
+ * max|dy| (IEEE bits, as hkp_absmax) to dy_amax_bits when non-NULL — the scale
+ * input of hkp_split_pack_x3 for the f16x3 backward convs. */
 int64_t hkp_bn_bwd_tiles(int64_t m);
 int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
                       const float* mean_invstd, float* dz, float* partials, hkp_stream_t stream);
 int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd, const float* gamma,
                         float* dgamma, float* dbeta, float* coef, hkp_stream_t stream);
 int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                     const float* mean_invstd, const float* coef, float* dy, hkp_stream_t stream);
+                     const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
+                     hkp_stream_t stream);
 
 /* Stem: backward of maxpool3x3/s2/p1(relu(y*scale+shift)) → dz = dL/d(BN output),
  * ReLU mask applied (src/resnet.py:200-202; ATen's first-max window rule). */

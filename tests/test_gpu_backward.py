@@ -98,7 +98,8 @@ def test_bn_backward(cuda_device, mask, c):
          ctypes.c_void_p(mi.data_ptr()), ops._stream())
     out_d = ops.bn_apply(y_d, ss, relu=mask)
     dy, dgamma, dbeta, dz = ops.bn_bwd(nhwc(g).to(d), out_d if mask else None, y_d, mi, gamma.detach().to(d),
-                                       want_dz=True)
+                                       want_dz=True, want_amax=True)
+    assert torch.equal(dy._hkp_amax, ops.absmax(dy))     # fused max|dy| == the separate pass
     assert (nchw(dy.cpu()) - y.grad).abs().max() < 1e-5 * max(1, y.grad.abs().max().item())
     assert (dgamma.cpu() - gamma.grad).abs().max() < 1e-4 * max(1, gamma.grad.abs().max().item())
     assert (dbeta.cpu() - beta.grad).abs().max() < 1e-4 * max(1, beta.grad.abs().max().item())

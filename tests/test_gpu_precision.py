@@ -198,6 +198,24 @@ def test_x3_wgrad_scaled(cuda_device, case, gscale):
         assert (dw - dw2).abs().max().item() <= 4e-6 * dw2.abs().max().item()
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 50, 70), (3, 3, 33, 41), (1, 1, 20, 26), (2, 3, 480 // 4, 640 // 4)])
+def test_stem_x3_fp32_accurate(cuda_device, shape):
+    """f16x3 stem (zero-padded NHWC4 planes, one K-step per filter row): fp32-class
+    accuracy vs fp64, BN partials as the fp32 stem kernel's; odd sizes, C < 3."""
+    from hkp import ops
+    n, c, h, w = shape
+    x = torch.rand(*shape, generator=torch.Generator().manual_seed(3))
+    wt = rand(64, c, 7, 7, seed=4, scale=(2.0 / (49 * 64)) ** 0.5)
+    ref = F.conv2d(x.double(), wt.double(), None, 2, 3)
+    xd, wd = x.to(cuda_device), wt.to(cuda_device)
+    assert ops.stem_x3_ok(tuple(x.shape), tuple(wt.shape), 2, 3, 1)
+    y, part = ops.conv2d_fwd_stem_x3(xd, ops.stem_weight_pack_x3(wd), 64)
+    err = (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    y32, p32 = ops.conv2d_fwd(xd, wd, 2, 3, 1, layout="nchw")
+    assert torch.allclose(part, p32, rtol=1e-4, atol=1e-3)
+
+
 def _model(bb, k, wseed, dev):
     from src.model import KeypointsGauss
     m = KeypointsGauss(k, backbone=bb, pretrained=False)
