@@ -17,7 +17,7 @@
 
 namespace hkp {
 
-constexpr int BNB_TILE = 256;  // pixels per reduction tile
+constexpr int BNB_TILE = 64;   // pixels per reduction tile (small: enough blocks to fill the chip at batch 8)
 
 // G = channel groups of 4 per thread (C/4 / threads-per-row); MASK: dz = g*(out>0)
 template <int G, bool MASK>

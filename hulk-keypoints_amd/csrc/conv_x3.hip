@@ -25,6 +25,9 @@
 // (the same partials format as every other conv here).
 //
 // Replaces the same cuDNN convs as conv_fwd.hip (src/resnet.py:20-37,77,86,184-188).
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace hkp {
@@ -63,7 +66,9 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
 // hkp_stem_pack_x3 (a.H/a.W = padded size, stride 2, pad 0, R = 7, S = 1: one
 // K-step per filter row = 8 taps x 4 channels; logical chunk j of a row holds
 // padded pixels 2wo+2j, 2wo+2j+1 from the hi plane (j < 4) or the lo plane).
-template <int BN, bool STEM = false>
+// VAR (schedule variant, A/B-tested in one process via HKP_X3_VARIANT): bit 0 =
+// s_setprio(1) around each MFMA cluster
+template <int BN, bool STEM = false, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -212,6 +217,11 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     auto step = [&](const bool ISSUE, const bool NEXT) {
         const char* st = smem + cur * STAGE;
         if (ISSUE) issue_next();
+        if (VAR & 1) {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         read_frag(f1, st, 1);
         mma(f0);
 #pragma unroll
@@ -221,11 +231,20 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM * TN - 2 * (TM + TN), 0);
         __builtin_amdgcn_sched_barrier(0);       // keep every MFMA of this half ahead of the wait
+        if (VAR & 1) {
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         if (NEXT) {
             if (ISSUE) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();
             cur = cur == 2 ? 0 : cur + 1;
+            if (VAR & 1) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
             mma(f1);
             read_frag(f0, smem + cur * STAGE, 0);
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -235,6 +254,11 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM * TN - 1 - 2 * (TM + TN), 0);
+            if (VAR & 1) {
+                __builtin_amdgcn_sched_barrier(0);
+                __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         } else {
             mma(f1);
         }
@@ -673,10 +697,23 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, in
     const long rsc = (long)d->r * d->s * d->c;
     *r_tiles = (int)((rsc + 255) / 256);
     const long tiles = (long)(d->k / *ka) * *r_tiles;
-    long sp = (1024 + tiles - 1) / tiles;                  // ~4 waves of blocks over 256 CUs
-    const long max_sp = (M + 511) / 512;                   // at least 16 K-steps per block
-    if (sp > max_sp) sp = max_sp;
-    if (sp < 1) sp = 1;
+    // One 512-thread block per CU at a time: pick the split count whose block
+    // count best fills whole rounds of 256 CUs (few rounds, few slabs to reduce),
+    // with at least 16 K-steps (512 pixels) per block.
+    const long max_sp = std::max(1L, (M + 511) / 512);
+    long sp = 1;
+    double best = -1.0;
+    for (long c = 1; c <= max_sp; ++c) {
+        const long blocks = tiles * c;
+        const long rounds = (blocks + 255) / 256;
+        if (rounds > 4) break;
+        const double fill = (double)blocks / (256.0 * rounds);
+        const double score = fill - 0.03 * rounds;            // prefer fewer rounds / slabs at equal fill
+        if (score > best + 1e-9) {
+            best = score;
+            sp = c;
+        }
+    }
     long m = (M + sp - 1) / sp;
     m = (m + 31) / 32 * 32;
     *splits = (int)((M + m - 1) / m);
@@ -731,6 +768,28 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
            d->stride == 2 && d->pad == 3 && d->dilation == 1 && d->k % 64 == 0;
 }
 
+
+// schedule variant of conv_x3_kernel (tuning knob: hkp_set_conv_variant,
+// initialised from HKP_X3_VARIANT; default 0)
+static int g_x3_variant = [] {
+    const char* e = getenv("HKP_X3_VARIANT");
+    return e ? atoi(e) : 0;
+}();
+static int x3_variant() { return g_x3_variant; }
+
+template <int BN>
+static void launch_x3_bn(int var, dim3 grid, hipStream_t st, const X3Args& a) {
+    switch (var) {
+        case 1: hipLaunchKernelGGL((conv_x3_kernel<BN, false, 1>), grid, dim3(512), 0, st, a); break;
+        default: hipLaunchKernelGGL((conv_x3_kernel<BN, false, 0>), grid, dim3(512), 0, st, a); break;
+    }
+}
+
+static void launch_x3(int bn, int var, dim3 grid, hipStream_t st, const X3Args& a) {
+    if (bn == 128) launch_x3_bn<128>(var, grid, st, a);
+    else launch_x3_bn<64>(var, grid, st, a);
+}
+
 }  // namespace hkp
 
 using namespace hkp;
@@ -766,8 +825,7 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     a.n_tiles = d->k / bn;
     const long m_tiles = (M + 255) / 256;
     hipStream_t st = as_stream(stream);
-    if (bn == 128) hipLaunchKernelGGL(conv_x3_kernel<128>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(conv_x3_kernel<64>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
+    launch_x3(bn, x3_variant(), dim3(m_tiles * a.n_tiles), st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_x3");
     return HKP_OK;
 }
@@ -820,8 +878,7 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     a.n_tiles = d->c / bn;
     const long m_tiles = (M + 255) / 256;
     hipStream_t st = as_stream(stream);
-    if (bn == 128) hipLaunchKernelGGL(conv_x3_kernel<128>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
-    else hipLaunchKernelGGL(conv_x3_kernel<64>, dim3(m_tiles * a.n_tiles), dim3(512), 0, st, a);
+    launch_x3(bn, x3_variant(), dim3(m_tiles * a.n_tiles), st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3");
     return HKP_OK;
 }
@@ -921,5 +978,11 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     const long m_tiles = (M + 255) / 256;
     hipLaunchKernelGGL((conv_x3_kernel<64, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
+    return HKP_OK;
+}
+
+extern "C" int hkp_set_conv_variant(int32_t variant) {
+    HKP_CHECK_ARG(variant >= 0 && variant < 2, "hkp_set_conv_variant: unknown variant %d", variant);
+    g_x3_variant = variant;
     return HKP_OK;
 }

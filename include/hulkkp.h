@@ -96,6 +96,9 @@ int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t*
  *                              (n = k*r*s*c elements).
  * Needs c % 32 == 0 and k % 64 == 0.  Replaces the same convs as hkp_conv2d_fwd. */
 int hkp_weight_pack_x3(int64_t n, int32_t c, const float* w, uint16_t* w_split, hkp_stream_t stream);
+/* Tuning knob: schedule variant of the x3 conv kernel (0 = default; 1 = s_setprio
+ * around the MFMA clusters).  Results are identical across variants. */
+int hkp_set_conv_variant(int32_t variant);
 int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split, float* y,
                       float* stat_partials, hkp_stream_t stream);
 
