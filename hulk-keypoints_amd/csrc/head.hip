@@ -153,16 +153,39 @@ __global__ __launch_bounds__(256) void upsample_sigmoid_kernel(int h, int w, int
             lo = (unsigned)m;
             hi = (unsigned)(m >> 32);
         }
-        if ((threadIdx.x & 63) == 0) atomicMax(keys + plane, ((unsigned long long)hi << 32) | lo);
+        // block max in fixed order, one key per block (no atomics: same-address
+        // device atomics from every wave serialised this kernel)
+        __shared__ unsigned long long wkey[4];
+        if ((threadIdx.x & 63) == 0) wkey[threadIdx.x >> 6] = ((unsigned long long)hi << 32) | lo;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            keys[(size_t)plane * gridDim.x + blockIdx.x] = umax64(umax64(wkey[0], wkey[1]), umax64(wkey[2], wkey[3]));
     }
 }
 
-__global__ void argmax_decode_kernel(int nk, int W, const unsigned long long* __restrict__ keys, int* __restrict__ yx) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nk) return;
-    const unsigned idx = 0xFFFFFFFFu - (unsigned)(keys[i] & 0xFFFFFFFFull);
-    yx[2 * i] = (int)(idx / (unsigned)W);
-    yx[2 * i + 1] = (int)(idx % (unsigned)W);
+// one block per (n,k) plane: max over the plane's per-block keys, decode (y, x)
+__global__ __launch_bounds__(256) void argmax_decode_kernel(int nblk, int W, const unsigned long long* __restrict__ keys,
+                                                           int* __restrict__ yx) {
+    const int plane = blockIdx.x;
+    unsigned long long best = 0ull;
+    for (int b = threadIdx.x; b < nblk; b += 256) best = umax64(best, keys[(size_t)plane * nblk + b]);
+    unsigned lo = (unsigned)best, hi = (unsigned)(best >> 32);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned ol = __shfl_xor(lo, off), oh = __shfl_xor(hi, off);
+        const unsigned long long m = umax64(((unsigned long long)hi << 32) | lo, ((unsigned long long)oh << 32) | ol);
+        lo = (unsigned)m;
+        hi = (unsigned)(m >> 32);
+    }
+    __shared__ unsigned long long wkey[4];
+    if ((threadIdx.x & 63) == 0) wkey[threadIdx.x >> 6] = ((unsigned long long)hi << 32) | lo;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long k = umax64(umax64(wkey[0], wkey[1]), umax64(wkey[2], wkey[3]));
+        const unsigned idx = 0xFFFFFFFFu - (unsigned)(k & 0xFFFFFFFFull);
+        yx[2 * plane] = (int)(idx / (unsigned)W);
+        yx[2 * plane + 1] = (int)(idx % (unsigned)W);
+    }
 }
 
 __global__ __launch_bounds__(256) void gauss_target_kernel(int K, int H, int W, float den,
@@ -217,13 +240,6 @@ extern "C" int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, 
     hipStream_t st = as_stream(stream);
     const int nk = n * k;
     unsigned long long* keys = argmax_yx ? (unsigned long long*)argmax_ws : nullptr;
-    if (keys) {
-        hipError_t e = hipMemsetAsync(keys, 0, sizeof(unsigned long long) * nk, st);
-        if (e != hipSuccess) {
-            set_error("hkp_upsample_sigmoid: memset: %s", hipGetErrorString(e));
-            return (int)e;
-        }
-    }
     // area_pixel_compute_scale (align_corners): (in-1)/(out-1) in fp32
     const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
     const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
@@ -240,7 +256,7 @@ extern "C" int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, 
 #undef HKP_UPS
     HKP_LAUNCH_CHECK("hkp_upsample_sigmoid");
     if (keys) {
-        hipLaunchKernelGGL(argmax_decode_kernel, dim3((nk + 255) / 256), dim3(256), 0, st, nk, W, keys, argmax_yx);
+        hipLaunchKernelGGL(argmax_decode_kernel, dim3(nk), dim3(256), 0, st, (int)grid.x, W, keys, argmax_yx);
         HKP_LAUNCH_CHECK("hkp_upsample_sigmoid(decode)");
     }
     return HKP_OK;
@@ -259,4 +275,9 @@ extern "C" int hkp_gauss_target(int32_t n, int32_t k, int32_t H, int32_t W, floa
                        total);
     HKP_LAUNCH_CHECK("hkp_gauss_target");
     return HKP_OK;
+}
+
+extern "C" int64_t hkp_upsample_argmax_ws_bytes(int32_t n, int32_t k, int32_t H, int32_t W) {
+    if (n <= 0 || k <= 0 || H <= 0 || W <= 0) return -1;
+    return (int64_t)n * k * (((int64_t)H * W + 1023) / 1024) * (int64_t)sizeof(uint64_t);
 }

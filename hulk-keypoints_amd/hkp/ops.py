@@ -342,7 +342,8 @@ def upsample_sigmoid(low, H, W, heat=True, argmax=True, sigmoid=True):
     hm = torch.empty((n, k, H, W), device=low.device, dtype=torch.float32) if heat else None
     ws = yx = None
     if argmax:
-        ws = torch.empty(n * k, device=low.device, dtype=torch.int64)
+        from ._lib import lib
+        ws = torch.empty(lib().hkp_upsample_argmax_ws_bytes(n, k, H, W) // 8, device=low.device, dtype=torch.int64)
         yx = torch.empty((n, k, 2), device=low.device, dtype=torch.int32)
     call("hkp_upsample_sigmoid", n, k, h, w, H, W, int(bool(sigmoid)), _ptr(low), _ptr(hm), _ptr(ws), _ptr(yx), _stream())
     return hm, yx

@@ -149,8 +149,10 @@ int hkp_head_fc(int32_t n, int32_t hw, int32_t c, int32_t k, const float* feat, 
  * (src/resnet_dilated.py:27) + sigmoid (src/model.py:21; skipped when
  * apply_sigmoid == 0, the raw Resnet34_8s.forward output), NCHW output (nullable),
  * and the per-(n,k) argmax (src/prediction.py:46, first index wins) as
- * int32 (y, x) pairs in argmax_yx [n*k*2] (nullable).  argmax_ws: n*k uint64
- * workspace, required when argmax_yx != NULL. */
+ * int32 (y, x) pairs in argmax_yx [n*k*2] (nullable).  argmax_ws: workspace of
+ * hkp_upsample_argmax_ws_bytes(n,k,H,W) bytes (one key per 1024-pixel block per
+ * plane; reduced in fixed order, no atomics), required when argmax_yx != NULL. */
+int64_t hkp_upsample_argmax_ws_bytes(int32_t n, int32_t k, int32_t H, int32_t W);
 int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, int32_t W,
                          int32_t apply_sigmoid, const float* lowres, float* heat, uint64_t* argmax_ws, int32_t* argmax_yx,
                          hkp_stream_t stream);
