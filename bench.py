@@ -249,6 +249,7 @@ def main():
                      "all_convs_tflops": all_fl / (all_ms * 1e-3) / 1e12,
                      "conv_share_of_step": (all_ms / max(3, min(args.steps, 10))) / (elapsed / args.steps * 1e3)},
         "model_tflops": value / world * fl_img * (3 if args.mode == "train" else 1) / 1e12,
+        "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9,
     }
     tag = "infer_c2" if args.mode == "infer" else "train_c3"
     traffic, src = pmc_traffic(dom_sym.replace(" ", ""), tag) if (args.backbone, K, H, W) == ("resnet34", 4, 480,
