@@ -49,14 +49,15 @@ typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
 
 // Operand split of 4 consecutive channels (element index e4*4, C % 32 == 0) for
 // the next conv: passes 1 → hi plane [P][C]; passes 3 → packed split layout
-// [P][C/32][hi32|lo32] (element e → 2e - (e&31), lo 32 halves later).
+// [P][C/32][hi32|lo32] (element e → 2e - (e&31), lo 32 halves later) with
+// hi = f16(v), lo = f16(v - hi) — the operand format of conv_x3.hip.
 __device__ __forceinline__ void store_split4(const f32x4& v, long e4, _Float16* __restrict__ out, int passes) {
     h16x4 h, l;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
         const _Float16 hv = (_Float16)v[e];
         h[e] = hv;
-        l[e] = (_Float16)((v[e] - (float)hv) * SPLIT_LO_SCALE);
+        l[e] = (_Float16)(v[e] - (float)hv);
     }
     if (passes == 1) {
         ((h16x4*)out)[e4] = h;

@@ -1,30 +1,48 @@
-// f16x3 implicit-GEMM convolution forward, deep-pipelined (the main-path conv of
-// the f16x3 precision; arithmetic identical to conv_f16.hip's PASSES=3 kernel).
+// f16x3 implicit-GEMM convolution (the main-path conv arithmetic), deep-pipelined:
+// forward, stride-1 backward-data (the same kernel on the gradient with flipped
+// weights), backward-filter, and the 7x7/s2 stem.
+//
+// f16x3 arithmetic: every operand v is split as hi = f16(v), lo = f16(v - hi) and
+//     v_a * v_b ≈ hi_a*hi_b + hi_a*lo_b + lo_a*hi_b
+// (3 fp16 MFMAs, fp32 accumulation, the dropped lo*lo and lo's own rounding cost
+// ~2^-22 relative per product).  All three products go into ONE fp32
+// accumulator — fp32-class with the same rounding as separate ones, and half the
+// accumulator registers, which is what pays for the 256x256 tiles below.  lo is
+// stored unscaled, so it is exact only while v - hi is an fp16 normal
+// (|v| >= 2^-3): operands with no natural scale are scaled by a power of two —
+// weights per output channel (max|w| -> [2^13, 2^14), inverse applied in the
+// epilogue), gradients per tensor from max|dy| — and activations keep an
+// absolute error floor of 2^-25 below 2^-3, negligible next to fp32 rounding of
+// the sums they feed.
 //
 // Operands arrive PRE-SPLIT in the "packed split" layout written by their
-// producers (bn_apply / bn_relu_maxpool with split_passes=3; weights by
+// producers (bn_apply / bn_relu_maxpool with split_passes=3, hkp_split_pack_x3,
 // hkp_weight_pack_x3):
-//
 //     xs[pixel][C/32][ hi(32 ch) | lo(32 ch) ]        fp16, 128 B per (pixel, group)
-//     ws[k][tap][C/32][ hi(32 ch) | lo(32 ch) ]
+//     ws[k][tap][C/32][ hi(32 ch) | lo(32 ch) ]       (+ ws_scale[k]: 2^-e_k)
+// so the 32 channels of one filter tap of one GEMM row are one 128-B cache line
+// holding both planes — the same bytes as the fp32 tensor.
 //
-// so one K-step (one filter tap x 32 channels) of one GEMM row is exactly one
-// 128-B cache line holding both planes.  The same bytes as the fp32 tensor.
+// Forward kernel (conv_x3_kernel<BN, KH>): tile 256 pixels x BN output channels,
+// 8 waves as 4x2 (wave tile 64 x BN/2, 32x32x16 MFMAs).  A K-step stages KH
+// 16-channel slices: KH = 2 → 128-B LDS rows (a whole line), 3-stage ring;
+// KH = 1 → 64-B rows (half a line), 4-stage ring (BN = 256: 32 KB per stage).
+// Staging is LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no ds_write),
+// NST-1 K-steps in flight ahead of the compute, retired by a counted
+// s_waitcnt vmcnt + raw s_barrier (never __syncthreads inside the loop: its
+// fence would drain the DMA queue).  LDS rows are unpadded (the DMA writes
+// lane-linear 1 KiB pieces); an XOR swizzle of the 16-B chunk index (with
+// (row>>1)&7 for 128-B rows, (row>>2)&3 for 64-B rows), applied to the per-lane
+// DMA SOURCE address and to the ds_read address, makes the fragment reads
+// conflict-free (0 conflicts measured).  K order: channel group outer, filter
+// tap inner (a pixel line is re-read by the next taps while in L2).
+// Out-of-image taps / rows past M load a zero line.  The mainloop is software-
+// pipelined (next fragments read during the current MFMAs, one ds_read per MFMA
+// gap, one barrier per K-step).  Epilogue: NHWC fp32 store (x weight scale,
+// x gradient scale, + addend) + BN tile partials per 128-row tile.
 //
-// Tile 256 (pixels) x BN (output channels) x 32 channels, 8 waves as 4x2;
-// K order: channel group outer, filter tap inner (L2 reuse of pixel lines).
-// Staging is LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no
-// ds_write) into a 3-stage LDS ring, two K-steps in flight ahead of the
-// compute, retired by a counted s_waitcnt vmcnt + raw s_barrier (never
-// __syncthreads inside the loop: its fence would drain the DMA queue).
-// LDS rows are 128 B and unpadded (the DMA writes lane-linear 1 KiB pieces);
-// bank conflicts of the fragment reads are removed by an XOR swizzle of the
-// 16-B chunk index with (row>>1)&7, applied to the per-lane SOURCE address of
-// the DMA and to the ds_read address.  Out-of-image taps / rows past M load a
-// zero line.  Epilogue: NHWC fp32 store + BN tile partials per 128-row tile
-// (the same partials format as every other conv here).
-//
-// Replaces the same cuDNN convs as conv_fwd.hip (src/resnet.py:20-37,77,86,184-188).
+// Replaces the cuDNN convs of src/resnet.py:20-37,77,86,137,184-188 and their
+// backward under loss.backward() (train.py:35).
 #include <algorithm>
 #include <cstdlib>
 
@@ -39,16 +57,25 @@ __device__ __attribute__((aligned(256))) uint4 g_x3_zero_line[8];   // 128 B of 
 struct X3Args {
     const _Float16* xs;
     const _Float16* ws;
+    const float* wscale;   // per output channel inverse weight scale [K] (nullable: 1)
     float* y;
     float* part;
-    const unsigned* amax;  // max|input| bits: the input was split after scaling by pow2_scale_for(amax) (dgrad)
+    const unsigned* amax;  // max|input| bits: the input was scaled by pow2_scale_for(amax) (dgrad)
     const float* add;      // addend of the output (dgrad: the residual-branch gradient), nullable
     int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
     int M, nks, cch, n_tiles, RS;
     long plane;            // STEM: halves between the hi and lo image planes
 };
 
-constexpr float X3_LO_INV = 1.f / 2048.f;
+// 2^e putting max|x| in [2^13, 2^14) (1 for 0 / non-finite): exact scaling
+__device__ __forceinline__ float pow2_scale_of(float m) {
+    if (!(m > 0.f) || !(m < INFINITY)) return 1.f;
+    int e;
+    frexpf(m, &e);
+    e = 14 - e;
+    e = e < -100 ? -100 : (e > 100 ? 100 : e);
+    return ldexpf(1.f, e);
+}
 
 // raw workgroup barrier (no vmcnt(0) drain: LDS-DMA stays in flight across it) +
 // compiler fence so no LDS access is moved across it
@@ -62,22 +89,42 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
+// schedule NM MFMAs and NR ds_reads of one basic block as evenly spread
+// groups: MFMA first, then one read after every NM/NR MFMAs
+template <int NM, int NR>
+__device__ __forceinline__ void interleave() {
+    constexpr int per = NM >= NR ? NM / NR : 1;
+    constexpr int nr = NM >= NR ? NR : NM;          // reads paired with MFMA groups
+#pragma unroll
+    for (int k = 0; k < nr; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, per, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);     // ds_read
+    }
+    if constexpr (NR > nr) __builtin_amdgcn_sched_group_barrier(0x100, NR - nr, 0);
+    if constexpr (NM > per * nr) __builtin_amdgcn_sched_group_barrier(0x008, NM - per * nr, 0);
+}
+
 // STEM: the 7x7/s2 stem on the zero-padded NHWC4 image planes of
 // hkp_stem_pack_x3 (a.H/a.W = padded size, stride 2, pad 0, R = 7, S = 1: one
 // K-step per filter row = 8 taps x 4 channels; logical chunk j of a row holds
 // padded pixels 2wo+2j, 2wo+2j+1 from the hi plane (j < 4) or the lo plane).
-// VAR (schedule variant, A/B-tested in one process via HKP_X3_VARIANT): bit 0 =
-// s_setprio(1) around each MFMA cluster
-template <int BN, bool STEM = false, int VAR = 0>
+template <int BN, int KH, bool STEM = false, int ORD = 0>
 __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-    constexpr int ROW = 128;                       // bytes per LDS row
+    constexpr int ROW = 64 * KH;                   // bytes per LDS row
+    constexpr int CPR = ROW / 16;                  // 16-B chunks per row
+    constexpr int RPI = 1024 / ROW;                // rows per DMA wave-instruction
+    constexpr bool WIDE2 = BN == 256 && KH == 2;    // 256x256 with 32-channel stages: 2-stage ring
+    constexpr int NST = WIDE2 ? 2 : (KH == 2 ? 3 : 4);   // LDS ring depth
     constexpr int STAGE = (BM + BN) * ROW;
-    constexpr int GA = BM / 64, GB = BN / 64;      // DMA instructions per thread per stage
-    constexpr int GL = GA + GB;
-    static_assert(TN >= 1 && GB >= 1, "BN must be a multiple of 64");
-    __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+    constexpr int GA = BM / RPI / 8;               // A DMA instructions per wave per stage
+    constexpr int GBT = BN / RPI;                  // B DMA instructions per stage (all waves)
+    constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
+    constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
+    static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
+    static_assert(NST * STAGE <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
 
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
@@ -85,6 +132,16 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = w / WN, wn = w % WN;
+
+    // swizzled physical chunk of a logical chunk in row r
+    auto swz = [](int row) { return KH == 2 ? (row >> 1) & 7 : (row >> 2) & 3; };
+    // halves offset, inside a packed line, of logical chunk L of a KH-slice row
+    // (KH = 1: + 16*s for the line's second 16-channel half)
+    auto lofs = [&](int L) -> long {
+        if constexpr (STEM) return (L >> 2) * a.plane + (L & 3) * 8;
+        else if constexpr (KH == 2) return L * 8;
+        else return (L < 2 ? L : L + 2) * 8;
+    };
 
     // ---- DMA source bookkeeping (rows this lane feeds) ----
     const int cstride = STEM ? 4 : a.cch * 64;     // halves per pixel
@@ -95,9 +152,9 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     const _Float16* a_p[GA];
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
-        const int row = 8 * (w * GA + i) + (lane >> 3);
-        const int Lc = (lane & 7) ^ ((row >> 1) & 7);       // logical 16-B chunk this lane fetches
-        const long L = STEM ? (Lc >> 2) * (long)a.plane + (Lc & 3) * 8 : Lc * 8;
+        const int row = RPI * (w * GA + i) + lane / CPR;
+        const int Lc = (lane % CPR) ^ swz(row);
+        const long L = lofs(Lc);
         const int m = m0 + row;
         if (m < a.M) {
             const int hw = a.Ho * a.Wo;
@@ -112,33 +169,36 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
             a_p[i] = a.xs;
         }
     }
+    const int bline = a.RS * a.cch * 64;           // halves per weight row (output channel)
     const _Float16* b_src[GB];
+    int b_dst[GB];
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
-        const int row = 8 * (w * GB + j) + (lane >> 3);
-        const int L = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
-        b_src[j] = a.ws + (long)(n0 + row) * a.nks * 64 + L;
+        const int bi = (w * GB + j) % GBT;
+        const int row = RPI * bi + lane / CPR;
+        const int Lc = (lane % CPR) ^ swz(row);
+        b_src[j] = a.ws + (long)(n0 + row) * bline + (STEM ? Lc * 8 : lofs(Lc));
+        b_dst[j] = (BM + RPI * bi) * ROW;
     }
     const _Float16* zero = (const _Float16*)g_x3_zero_line;
 
-    // staging state of the next K-step to issue (wave-uniform, advanced per issue).
-    // K order is channel-group-major: the R*S taps of one 32-channel group run
-    // back to back, so a pixel line is re-read by the next taps while it is still
-    // in L2 (tap-major order re-fetched it from HBM for most taps).
-    int q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_buf = 0;
+    // staging state of the next K-step to issue (wave-uniform, advanced per issue)
+    int q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_half = 0, q_buf = 0;
     auto issue_next = [&]() {
         char* st = smem + q_buf * STAGE;
         const int dh = q_rr * a.dil, dw = q_ss * a.dil;
-        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64;
+        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64 + q_half * 16;
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const bool in = (unsigned)(a_hb[i] + dh) < (unsigned)a.H && (unsigned)(a_wb[i] + dw) < (unsigned)a.W;
-            glds16(in ? a_p[i] + toff : zero, st + (8 * (w * GA + i)) * ROW);
+            glds16(in ? a_p[i] + toff : zero, st + (RPI * (w * GA + i)) * ROW);
         }
-        const long boff = (long)(q_tap * a.cch + q_cc) * 64;
+        const long boff = (long)(q_tap * a.cch + q_cc) * 64 + q_half * 16;
 #pragma unroll
-        for (int j = 0; j < GB; ++j) glds16(b_src[j] + boff, st + (BM + 8 * (w * GB + j)) * ROW);
-        q_buf = q_buf == 2 ? 0 : q_buf + 1;
+        for (int j = 0; j < GB; ++j) glds16(b_src[j] + boff, st + b_dst[j]);
+        q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
+        if (KH == 1 && ++q_half < 2) return;       // the line's second 16-channel half, same tap
+        q_half = 0;
         if (++q_ss == a.S) {
             q_ss = 0;
             ++q_rr;
@@ -150,158 +210,275 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         }
     };
 
-    f32x16 acc[TM][TN], accc[TM][TN];
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc[i][j][r] = 0.f;
-                accc[i][j][r] = 0.f;
-            }
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // fragment read offsets: lane reads row (lane&31) of each 32-row tile, logical
-    // chunk 4*plane + 2*s + (lane>>5), stored at chunk ^ ((row>>1)&7)
-    const int frow = lane & 31, sw = (frow >> 1) & 7, kh = lane >> 5;
-    int foff[2][2];
+    // fragment reads: lane reads row (lane&31) of each 32-row tile; logical chunk
+    // hi: KH*u... (u = k16 slice within the stage), lo: the same + CPR/2
+    const int frow = lane & 31, kh = lane >> 5;
+    int foff[2][KH];
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) foff[pl][s] = frow * ROW + (((4 * pl + 2 * s + kh) ^ sw) << 4);
+        for (int u = 0; u < KH; ++u) foff[pl][u] = frow * ROW + ((((CPR / 2) * pl + 2 * u + kh) ^ swz(frow)) << 4);
     const int a_base = (wm * TM * 32) * ROW, b_base = (BM + wn * TN * 32) * ROW;
 
     struct Frag {
         f16x8 ah[TM], al[TM], bh[TN], bl[TN];
     };
-    auto read_frag = [&](Frag& f, const char* st, int s) {
+    auto read_frag = [&](Frag& f, const char* st, int u) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-            f.ah[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][s]);
-            f.al[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][s]);
+            f.ah[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][u]);
+            f.al[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][u]);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            f.bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][s]);
-            f.bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][s]);
+            f.bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][u]);
+            f.bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][u]);
         }
     };
+    // ORD 0: the three products of one tile back to back; ORD 1: product-major
+    // (consecutive MFMAs accumulate into different tiles)
     auto mma = [&](const Frag& f) {
+        if constexpr (ORD == 0) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
-                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[j], accc[i][j], 0, 0, 0);
-                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[j], accc[i][j], 0, 0, 0);
-            }
-    };
-
-    // Software pipeline, one barrier per K-step, placed between its two halves:
-    //   [issue DMA t+2] [read frags s=1 of t] [MFMA s=0 of t]
-    //   wait own DMA of t+1, barrier (t+1 landed everywhere; t fully read)
-    //   [read frags s=0 of t+1] [MFMA s=1 of t]
-    // DMA t+2 overwrites the buffer of t-1, whose last reads retired before the
-    // previous barrier (lgkmcnt(0) ahead of it).
-    const int nks = a.nks;
-    issue_next();
-    if (nks > 1) issue_next();
-    if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    Frag f0, f1;
-    int cur = 0;
-    read_frag(f0, smem, 0);
-    // one K-step; ISSUE: DMA K-step t+2, NEXT: a K-step t+1 follows.  Each half is
-    // one basic block so the ds_reads can be interleaved one per MFMA gap.
-    auto step = [&](const bool ISSUE, const bool NEXT) {
-        const char* st = smem + cur * STAGE;
-        if (ISSUE) issue_next();
-        if (VAR & 1) {
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_setprio(1);
-            __builtin_amdgcn_sched_barrier(0);
+                for (int j = 0; j < TN; ++j) {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
+                }
+            return;
         }
-        read_frag(f1, st, 1);
-        mma(f0);
-#pragma unroll
-        for (int k = 0; k < 2 * (TM + TN); ++k) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // 1 ds_read
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM * TN - 2 * (TM + TN), 0);
-        __builtin_amdgcn_sched_barrier(0);       // keep every MFMA of this half ahead of the wait
-        if (VAR & 1) {
-            __builtin_amdgcn_s_setprio(0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (NEXT) {
-            if (ISSUE) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            cur = cur == 2 ? 0 : cur + 1;
-            if (VAR & 1) {
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_setprio(1);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            mma(f1);
-            read_frag(f0, smem + cur * STAGE, 0);
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-#pragma unroll
-            for (int k = 0; k < 2 * (TM + TN); ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM * TN - 1 - 2 * (TM + TN), 0);
-            if (VAR & 1) {
-                __builtin_amdgcn_sched_barrier(0);
-                __builtin_amdgcn_s_setprio(0);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        } else {
-            mma(f1);
-        }
-    };
-    int t = 0;
-    for (; t + 2 < nks; ++t) step(true, true);
-    if (t + 1 < nks) {
-        step(false, true);
-        ++t;
-    }
-    step(false, false);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] += accc[i][j][r] * X3_LO_INV;
-    if (a.amax) {
-        const float inv = 1.f / pow2_scale_for(a.amax);   // exact (power of two)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[i][j][r] *= inv;
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
+    };
+    constexpr int NR = 2 * (TM + TN), NM = 3 * TM * TN;   // ds_reads / MFMAs per k16 slice
+
+    const int nks = a.nks;
+    // prologue: NST-1 stages in flight, stage 0 landed everywhere
+    issue_next();
+    for (int s = 1; s < (WIDE2 ? 2 : NST - 1); ++s)
+        if (s < nks) issue_next();
+    {
+        const int after = std::min(nks - 1, WIDE2 ? 1 : NST - 2);   // stages issued after stage 0
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    Frag f0, f1;
+    int cur = 0;
+    read_frag(f0, smem, 0);
+
+    // wait for this wave's DMA of stage t+1, given that the stages up to
+    // min(nks-1, t+NST-1) have been issued; lgkmcnt(0) retires this wave's
+    // fragment reads of the buffer the next DMA will overwrite
+    auto wait_next = [&](int t) {
+        const int after = std::min(nks - 1, t + NST - 1) - (t + 1);
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * GL) : "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    };
+
+    if constexpr (WIDE2) {
+        // 256x256 tile, two k16 halves per 32-channel stage, 48 MFMAs per wave per
+        // barrier, 2-stage ring:
+        //   [MFMAs u=0 of t | read u=1 frags of t]  wait own DMA of t+1, barrier
+        //   [issue DMA t+2 into t's buffer (fully read before the barrier)]
+        //   [MFMAs u=1 of t | read u=0 frags of t+1]
+        // A fragments double-buffered, B refilled in place after each column.
+        struct FA {
+            f16x8 h[TM], l[TM];
+        };
+        f16x8 bh[TN], bl[TN];
+        auto read_a = [&](FA& f, const char* st, int u) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                f.h[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][u]);
+                f.l[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][u]);
+            }
+        };
+        auto read_b = [&](int j, const char* st, int u) {
+            bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][u]);
+            bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][u]);
+        };
+        auto mma_col = [&](const FA& f, int j) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+        };
+        auto half = [&](const FA& fc, FA& fn, const char* st, int u) {   // MFMAs on fc/B, read fn/B from (st, u)
+            read_a(fn, st, u);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                mma_col(fc, j);
+                read_b(j, st, u);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM, 0);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        FA fa0, fa1;
+        read_a(fa0, smem, 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) read_b(j, smem, 0);
+        for (int t = 0; t + 1 < nks; ++t) {
+            const char* st = smem + cur * STAGE;
+            half(fa0, fa1, st, 1);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            if (t + 2 < nks) issue_next();        // into t's buffer: every read of it retired above
+            cur ^= 1;
+            half(fa1, fa0, smem + cur * STAGE, 0);
+        }
+        half(fa0, fa1, smem + cur * STAGE, 1);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mma_col(fa1, j);
+    } else if constexpr (KH == 2) {
+        // one barrier per K-step, placed between its two k16 halves:
+        //   [issue DMA t+2] [read frags u=1 of t] [MFMA u=0 of t]
+        //   wait own DMA of t+1, barrier (t+1 landed everywhere; t-1 fully read)
+        //   [read frags u=0 of t+1] [MFMA u=1 of t]
+        // DMA t+2 overwrites the buffer of t-1, whose reads retired before the
+        // previous barrier.  Each half is one basic block so the ds_reads can be
+        // interleaved one per MFMA gap.
+        // the last K-step is peeled so the loop body has no branch around the
+        // MFMAs (a join of two differently scheduled acc writers costs a full
+        // accumulator copy)
+        for (int t = 0; t + 1 < nks; ++t) {
+            const char* st = smem + cur * STAGE;
+            if (t + NST - 1 < nks) issue_next();
+            read_frag(f1, st, 1);
+            mma(f0);
+            interleave<NM, NR>();
+            __builtin_amdgcn_sched_barrier(0);       // every MFMA of this half ahead of the wait
+            wait_next(t);
+            lds_barrier();
+            cur = cur == NST - 1 ? 0 : cur + 1;
+            mma(f1);
+            read_frag(f0, smem + cur * STAGE, 0);
+            interleave<NM, NR>();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        read_frag(f1, smem + cur * STAGE, 1);
+        mma(f0);
+        mma(f1);
+    } else {
+        // one k16 slice per stage:
+        //   [issue DMA t+3] wait own DMA of t+1, barrier (t+1 landed; t-1 fully read)
+        //   [read A frags of t+1] then per column block j: [MFMAs of t with B_j]
+        //   [refill B_j with t+1's]
+        // DMA t+3 overwrites the buffer of t-1, whose reads retired before the
+        // previous barrier.  Only the A fragments are double-buffered (unrolled by
+        // two so they stay in named registers); each B fragment is refilled in
+        // place right after its last MFMA of the step.
+        struct FA {
+            f16x8 h[TM], l[TM];
+        };
+        f16x8 bh[TN], bl[TN];
+        auto read_a = [&](FA& f, const char* st) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                f.h[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][0]);
+                f.l[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][0]);
+            }
+        };
+        auto read_b = [&](int j, const char* st) {
+            bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][0]);
+            bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][0]);
+        };
+        auto mma_col = [&](const FA& f, int j) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
+            }
+        };
+        FA fa0, fa1;
+        read_a(fa0, smem);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) read_b(j, smem);
+        auto step = [&](int t, FA& fc, FA& fn) {     // a K-step followed by another
+            if (t + NST - 1 < nks) issue_next();
+            wait_next(t);
+            lds_barrier();
+            cur = cur == NST - 1 ? 0 : cur + 1;
+            const char* st = smem + cur * STAGE;
+            read_a(fn, st);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                mma_col(fc, j);
+                read_b(j, st);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM, 0);      // next A frags
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);  // column j's MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // pairs of full steps, then the peeled last pair; nks is even here (two
+        // 16-channel halves per tap), so nothing branches around the MFMAs
+        int t = 0;
+        for (; t + 2 < nks; t += 2) {
+            step(t, fa0, fa1);
+            step(t + 1, fa1, fa0);
+        }
+        step(t, fa0, fa1);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mma_col(fa1, j);
     }
 
-    // ---- epilogue: NHWC store (+ addend) + BN partials per 128-row tile ----
+    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
+
+    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
     const int rbase = m0 + wm * TM * 32 + 4 * kh;
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + j * 32 + frow;
+        const float sc = (a.wscale ? a.wscale[n] : 1.f) * ginv;
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int n = n0 + wn * TN * 32 + j * 32 + frow;
+        for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
+                acc[i][j][r] *= sc;
                 const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
                 if (m < a.M) {
                     const long off = (long)m * a.K + n;
                     a.y[off] = a.add ? acc[i][j][r] + a.add[off] : acc[i][j][r];
                 }
             }
-        }
+    }
     if (a.part == nullptr) return;
     __syncthreads();                       // every wave done reading the ring
     float* red = (float*)smem;             // [WM][BN] column sums, then [2][BN] half-tile means
@@ -326,8 +503,8 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     }
     __syncthreads();
     const long tile128 = (long)(m0 >> 7);
-    if (tid < 2 * BN) {
-        const int h = tid / BN, c = tid - h * BN;
+    for (int e = tid; e < 2 * BN; e += 512) {
+        const int h = e / BN, c = e - h * BN;
         const int cnt = min(128, a.M - (m0 + 128 * h));
         if (cnt > 0) {
             const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
@@ -358,24 +535,70 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         for (int j = 0; j < TN; ++j) red[wm * BN + wn * TN * 32 + j * 32 + lane] = colsum[j];
     }
     __syncthreads();
-    if (tid < 2 * BN) {
-        const int h = tid / BN, c = tid - h * BN;
+    for (int e = tid; e < 2 * BN; e += 512) {
+        const int h = e / BN, c = e - h * BN;
         if (a.M - (m0 + 128 * h) > 0)
             a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
     }
 }
 
-// w[k][tap][c] fp32 (KRSC) → ws[k][tap][c/32][hi32|lo32]; element e → 2e - (c&31) (+32 for lo)
-__global__ __launch_bounds__(256) void weight_pack_x3_kernel(long n, const float* __restrict__ w,
-                                                            _Float16* __restrict__ ws) {
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-        const float v = w[e];
-        const _Float16 h = (_Float16)v;
-        const long o = 2 * e - (e & 31);
-        ws[o] = h;
-        ws[o + 32] = (_Float16)((v - (float)h) * SPLIT_LO_SCALE);
+// ---------------------------------------------------------------------------
+// operand packing
+
+__device__ __forceinline__ void split_store(float v, _Float16* hi_p) {   // hi at p, lo at p + 32
+    const _Float16 h = (_Float16)v;
+    hi_p[0] = h;
+    hi_p[32] = (_Float16)(v - (float)h);
+}
+
+// block max |x| over a row of n elements addressed by idx(i); result broadcast
+template <typename F>
+__device__ __forceinline__ float block_absmax(int n, F&& val) {
+    __shared__ float red[8];
+    float m = 0.f;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(val(i)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    float r = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r = fmaxf(r, red[i]);
+    __syncthreads();
+    return r;
+}
+
+// w[k][tap][c] fp32 (KRSC) * 2^e_k → ws[k][tap][c/32][hi32|lo32]; one block per k.
+// Element e → 2e - (c&31) (lo 32 halves later); wscale[k] = 2^-e_k.
+__global__ __launch_bounds__(256) void weight_pack_x3_kernel(int rsc, const float* __restrict__ w,
+                                                            _Float16* __restrict__ ws, float* __restrict__ wscale) {
+    const int k = blockIdx.x;
+    const float* row = w + (long)k * rsc;
+    const float sc = pow2_scale_of(block_absmax(rsc, [&](int i) { return row[i]; }));
+    for (int i = threadIdx.x; i < rsc; i += blockDim.x) {
+        const long e = (long)k * rsc + i;
+        split_store(row[i] * sc, ws + 2 * e - (e & 31));
     }
+    if (threadIdx.x == 0) wscale[k] = 1.f / sc;
+}
+
+// flipped dgrad weight, packed: row c (forward input channel) holds element
+// (r', s', k) = w[k][R-1-r'][S-1-s'][c] * 2^e_c; one block per c
+__global__ __launch_bounds__(256) void weight_flip_pack_x3_kernel(int K, int R, int S, int C,
+                                                                 const float* __restrict__ w,
+                                                                 _Float16* __restrict__ out,
+                                                                 float* __restrict__ wscale) {
+    const int c = blockIdx.x;
+    const int n = R * S * K;
+    auto val = [&](int i) {
+        const int k = i % K, t = i / K, sp = t % S, rp = t / S;
+        return w[(((long)k * R + (R - 1 - rp)) * S + (S - 1 - sp)) * C + c];
+    };
+    const float sc = pow2_scale_of(block_absmax(n, val));
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const long e = (long)c * n + i;
+        split_store(val(i) * sc, out + 2 * e - (e & 31));
+    }
+    if (threadIdx.x == 0) wscale[c] = 1.f / sc;
 }
 
 // x * 2^e (e from amax; 1 without) → packed split [P][C/32][hi32|lo32]
@@ -389,27 +612,6 @@ __global__ __launch_bounds__(256) void split_pack_x3_kernel(long n4, const f32x4
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] *= sc;
         store_split4(v, i, out, 3);
-    }
-}
-
-// flipped dgrad weight, packed: element (c, r', s', k) = w[k][R-1-r'][S-1-s'][c]
-__global__ __launch_bounds__(256) void weight_flip_pack_x3_kernel(int K, int R, int S, int C,
-                                                                 const float* __restrict__ w,
-                                                                 _Float16* __restrict__ out) {
-    const long total = (long)K * R * S * C;
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
-        const int k = (int)(e % K);
-        long t = e / K;
-        const int sp = (int)(t % S);
-        t /= S;
-        const int rp = (int)(t % R);
-        const int c = (int)(t / R);
-        const float v = w[(((long)k * R + (R - 1 - rp)) * S + (S - 1 - sp)) * C + c];
-        const _Float16 h = (_Float16)v;
-        const long o = 2 * e - (e & 31);
-        out[o] = h;
-        out[o + 32] = (_Float16)((v - (float)h) * SPLIT_LO_SCALE);
     }
 }
 
@@ -531,16 +733,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
         }
     };
 
-    f32x16 acc[TM][TN], accc[TM][TN];
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc[i][j][r] = 0.f;
-                accc[i][j][r] = 0.f;
-            }
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     // transposed-read addressing: 16-lane group G reads 4 pixel rows (q) x 16
     // channels (column block cb = G&1); lane 4q+p supplies row q, channels 4p..4p+3
@@ -594,15 +793,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dh[i], f.xh[j], acc[i][j], 0, 0, 0);
-                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dh[i], f.xl[j], accc[i][j], 0, 0, 0);
-                accc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dl[i], f.xh[j], accc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dh[i], f.xl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.dl[i], f.xh[j], acc[i][j], 0, 0, 0);
             }
     };
-    // same software pipeline as conv_x3_kernel (see there); 4*(TM+TN) transposed
-    // b64 reads per half, two per MFMA gap
-    // same software pipeline as conv_x3_kernel (see there); 4*(TM+TN) transposed
-    // b64 reads per half, two per MFMA gap.  The reads are inline asm: every
-    // consumer MFMA sits behind an explicit lgkmcnt wait + sched_barrier.
+    // same software pipeline as conv_x3_kernel<*, 2> (see there); 4*(TM+TN)
+    // transposed b64 reads per half, two per MFMA gap.  The reads are inline
+    // asm: every consumer MFMA sits behind an explicit lgkmcnt wait + sched_barrier.
     constexpr int NR = 4 * (TM + TN), NM = 3 * TM * TN;
     const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
     if (nsteps > 0) {
@@ -672,7 +869,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const int k = k0 + wk * TM * 32 + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-                out[(long)k * a.RSC + m] = (acc[i][j][r] + accc[i][j][r] * X3_LO_INV) * inv;
+                out[(long)k * a.RSC + m] = acc[i][j][r] * inv;
             }
         }
 }
@@ -721,7 +918,7 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, in
 }
 
 // Stem operand: NCHW fp32 image → zero-padded NHWC4 planes [2][N][Hp][Wp][4]
-// (hi, then lo = f16((x-hi)*2^11)); padded pixel (hp, wp) = input (hp-3, wp-3)
+// (hi, then lo = f16(x-hi)); padded pixel (hp, wp) = input (hp-3, wp-3)
 __global__ __launch_bounds__(256) void stem_pack_x3_kernel(int N, int C, int H, int W, int Hp, int Wp,
                                                           const float* __restrict__ x, _Float16* __restrict__ out) {
     const long total = (long)N * Hp * Wp;
@@ -742,25 +939,27 @@ __global__ __launch_bounds__(256) void stem_pack_x3_kernel(int N, int C, int H, 
         for (int c = 0; c < 4; ++c) {
             const _Float16 hh = (_Float16)v[c];
             hv[c] = hh;
-            lv[c] = (_Float16)((v[c] - (float)hh) * SPLIT_LO_SCALE);
+            lv[c] = (_Float16)(v[c] - (float)hh);
         }
         *(h16x4*)(out + p * 4) = hv;
         *(h16x4*)(out + plane + p * 4) = lv;
     }
 }
 
-// Stem weight OIHW [K][C][7][7] → [K][r][hi32|lo32], 32 = 8 taps (s; 7 = 0) x 4 channels (C..3 = 0)
-__global__ __launch_bounds__(256) void stem_weight_pack_x3_kernel(int K, int C, const float* __restrict__ w,
-                                                                 _Float16* __restrict__ out) {
-    const int total = K * 7 * 32;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-        const int c = e & 3, s = (e >> 2) & 7, r = (e >> 5) % 7, k = e / (7 * 32);
-        const float v = (s < 7 && c < C) ? w[(((long)k * C + c) * 7 + r) * 7 + s] : 0.f;
-        const _Float16 h = (_Float16)v;
-        const long o = ((long)k * 7 + r) * 64 + s * 4 + c;
-        out[o] = h;
-        out[o + 32] = (_Float16)((v - (float)h) * SPLIT_LO_SCALE);
+// Stem weight OIHW [K][C][7][7] * 2^e_k → [K][r][hi32|lo32], 32 = 8 taps (s; 7 = 0)
+// x 4 channels (C..3 = 0); one block per k, wscale[k] = 2^-e_k
+__global__ __launch_bounds__(256) void stem_weight_pack_x3_kernel(int C, const float* __restrict__ w,
+                                                                 _Float16* __restrict__ out,
+                                                                 float* __restrict__ wscale) {
+    const int k = blockIdx.x;
+    const float* wk = w + (long)k * C * 49;
+    const float sc = pow2_scale_of(block_absmax(C * 49, [&](int i) { return wk[i]; }));
+    for (int e = threadIdx.x; e < 7 * 32; e += blockDim.x) {
+        const int c = e & 3, s = (e >> 2) & 7, r = e >> 5;
+        const float v = (s < 7 && c < C) ? wk[(c * 7 + r) * 7 + s] * sc : 0.f;
+        split_store(v, out + ((long)k * 7 + r) * 64 + s * 4 + c);
     }
+    if (threadIdx.x == 0) wscale[k] = 1.f / sc;
 }
 
 static bool stem_x3_shape(const hkp_conv_desc* d) {
@@ -768,44 +967,56 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
            d->stride == 2 && d->pad == 3 && d->dilation == 1 && d->k % 64 == 0;
 }
 
-
-// schedule variant of conv_x3_kernel (tuning knob: hkp_set_conv_variant,
-// initialised from HKP_X3_VARIANT; default 0)
+// Tile policy: 256x256 (32-channel stages, 2-stage ring, 48 MFMAs per wave per
+// barrier) when Cout % 256 == 0 and that still gives >= 4 rounds of blocks over
+// the 256 CUs; else 256x128 / 256x64 (32-channel stages, 3-stage ring).
+// Measured on C2 layer4 (Cout 512): 256x256 1.70 ms vs 256x128 1.82 ms; on layer3
+// (Cout 256, 600 blocks) 256x256 loses to round quantisation (0.53 vs 0.47 ms).
+// Tuning knob (hkp_set_conv_variant; results agree to fp32 summation order, in
+// practice bit-identical): 0 = policy, 1 = 256x128 32-ch stages only,
+// 2 = 256x128 16-ch stages (4-stage ring), 3 = 256x256 32-ch stages whenever
+// Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0.
 static int g_x3_variant = [] {
     const char* e = getenv("HKP_X3_VARIANT");
     return e ? atoi(e) : 0;
 }();
-static int x3_variant() { return g_x3_variant; }
 
-template <int BN>
-static void launch_x3_bn(int var, dim3 grid, hipStream_t st, const X3Args& a) {
-    switch (var) {
-        case 1: hipLaunchKernelGGL((conv_x3_kernel<BN, false, 1>), grid, dim3(512), 0, st, a); break;
-        default: hipLaunchKernelGGL((conv_x3_kernel<BN, false, 0>), grid, dim3(512), 0, st, a); break;
+static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a) {
+    const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
+    int bn = k % 128 == 0 ? 128 : 64, kh = 2;
+    if (k % 256 == 0 && (v == 3 || v == 4 || (v == 0 && m_tiles * (k / 256) >= 1024))) {
+        bn = 256;
+        kh = v == 4 ? 1 : 2;
+    } else if (bn == 128 && v == 2) {
+        kh = 1;
     }
-}
-
-static void launch_x3(int bn, int var, dim3 grid, hipStream_t st, const X3Args& a) {
-    if (bn == 128) launch_x3_bn<128>(var, grid, st, a);
-    else launch_x3_bn<64>(var, grid, st, a);
+    a.n_tiles = k / bn;
+    a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
+    const dim3 grid((unsigned)(m_tiles * a.n_tiles));
+    if (bn == 256 && kh == 2) hipLaunchKernelGGL((conv_x3_kernel<256, 2>), grid, dim3(512), 0, st, a);
+    else if (bn == 256) hipLaunchKernelGGL((conv_x3_kernel<256, 1>), grid, dim3(512), 0, st, a);
+    else if (bn == 128 && kh == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 1>), grid, dim3(512), 0, st, a);
+    else if (bn == 128 && ord) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 1>), grid, dim3(512), 0, st, a);
+    else if (bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((conv_x3_kernel<64, 2>), grid, dim3(512), 0, st, a);
 }
 
 }  // namespace hkp
 
 using namespace hkp;
 
-extern "C" int hkp_weight_pack_x3(int64_t n, int32_t c, const float* w, uint16_t* w_split, hkp_stream_t stream) {
-    HKP_CHECK_ARG(n > 0 && c > 0 && c % 32 == 0 && n % c == 0 && w && w_split, "hkp_weight_pack_x3: bad args");
-    long g = (n + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(weight_pack_x3_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), (long)n, w,
-                       (_Float16*)w_split);
+extern "C" int hkp_weight_pack_x3(int32_t k, int32_t rsc, int32_t c, const float* w, uint16_t* w_split,
+                                  float* w_inv_scale, hkp_stream_t stream) {
+    HKP_CHECK_ARG(k > 0 && c > 0 && c % 32 == 0 && rsc > 0 && rsc % c == 0 && w && w_split && w_inv_scale,
+                  "hkp_weight_pack_x3: bad args");
+    hipLaunchKernelGGL(weight_pack_x3_kernel, dim3(k), dim3(256), 0, as_stream(stream), rsc, w, (_Float16*)w_split,
+                       w_inv_scale);
     HKP_LAUNCH_CHECK("hkp_weight_pack_x3");
     return HKP_OK;
 }
 
-extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split, float* y,
-                                 float* stat_partials, hkp_stream_t stream) {
+extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
+                                 const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -816,16 +1027,12 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     const long M = (long)d->n * ho * wo;
     HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w * d->c < (1L << 40), "hkp_conv2d_fwd_x3: too large");
     X3Args a;
-    a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.y = y; a.part = stat_partials;
-    a.amax = nullptr; a.add = nullptr; a.plane = 0;
+    a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.wscale = w_inv_scale;
+    a.y = y; a.part = stat_partials; a.amax = nullptr; a.add = nullptr; a.plane = 0;
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
-    a.M = (int)M; a.cch = d->c / 32; a.nks = d->r * d->s * a.cch; a.RS = d->r * d->s;
-    const int bn = d->k % 128 == 0 ? 128 : 64;
-    a.n_tiles = d->k / bn;
-    const long m_tiles = (M + 255) / 256;
-    hipStream_t st = as_stream(stream);
-    launch_x3(bn, x3_variant(), dim3(m_tiles * a.n_tiles), st, a);
+    a.M = (int)M; a.cch = d->c / 32; a.RS = d->r * d->s;
+    launch_x3(d->k, (M + 255) / 256, as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_x3");
     return HKP_OK;
 }
@@ -842,21 +1049,18 @@ extern "C" int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uin
 }
 
 extern "C" int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf_split,
-                                       hkp_stream_t stream) {
-    HKP_CHECK_ARG(d && w && wf_split, "hkp_weight_flip_pack_x3: null argument");
+                                       float* wf_inv_scale, hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && w && wf_split && wf_inv_scale, "hkp_weight_flip_pack_x3: null argument");
     HKP_CHECK_ARG(d->k % 32 == 0, "hkp_weight_flip_pack_x3: need Cout%%32==0 (k=%d)", d->k);
-    const long total = (long)d->k * d->r * d->s * d->c;
-    long g = (total + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(weight_flip_pack_x3_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), d->k, d->r,
-                       d->s, d->c, w, (_Float16*)wf_split);
+    hipLaunchKernelGGL(weight_flip_pack_x3_kernel, dim3(d->c), dim3(256), 0, as_stream(stream), d->k, d->r, d->s,
+                       d->c, w, (_Float16*)wf_split, wf_inv_scale);
     HKP_LAUNCH_CHECK("hkp_weight_flip_pack_x3");
     return HKP_OK;
 }
 
 extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
-                                      const uint32_t* dy_amax_bits, const float* add, float* dx,
-                                      hkp_stream_t stream) {
+                                      const float* wf_inv_scale, const uint32_t* dy_amax_bits, const float* add,
+                                      float* dx, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -869,16 +1073,12 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     const long M = (long)d->n * d->h * d->w;
     HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_data_x3: too large");
     X3Args a;
-    a.xs = (const _Float16*)dy_split; a.ws = (const _Float16*)wf_split; a.y = dx; a.part = nullptr;
-    a.amax = (const unsigned*)dy_amax_bits; a.add = add; a.plane = 0;
+    a.xs = (const _Float16*)dy_split; a.ws = (const _Float16*)wf_split; a.wscale = wf_inv_scale;
+    a.y = dx; a.part = nullptr; a.amax = (const unsigned*)dy_amax_bits; a.add = add; a.plane = 0;
     a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
     a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
-    a.M = (int)M; a.cch = d->k / 32; a.nks = d->r * d->s * a.cch; a.RS = d->r * d->s;
-    const int bn = d->c % 128 == 0 ? 128 : 64;
-    a.n_tiles = d->c / bn;
-    const long m_tiles = (M + 255) / 256;
-    hipStream_t st = as_stream(stream);
-    launch_x3(bn, x3_variant(), dim3(m_tiles * a.n_tiles), st, a);
+    a.M = (int)M; a.cch = d->k / 32; a.RS = d->r * d->s;
+    launch_x3(d->c, (M + 255) / 256, as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3");
     return HKP_OK;
 }
@@ -949,17 +1149,16 @@ extern "C" int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uin
 }
 
 extern "C" int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split,
-                                       hkp_stream_t stream) {
-    HKP_CHECK_ARG(k > 0 && c >= 1 && c <= 4 && w_oihw && w_split, "hkp_stem_weight_pack_x3: bad args");
-    const int total = k * 7 * 32;
-    hipLaunchKernelGGL(stem_weight_pack_x3_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), k, c,
-                       w_oihw, (_Float16*)w_split);
+                                       float* w_inv_scale, hkp_stream_t stream) {
+    HKP_CHECK_ARG(k > 0 && c >= 1 && c <= 4 && w_oihw && w_split && w_inv_scale, "hkp_stem_weight_pack_x3: bad args");
+    hipLaunchKernelGGL(stem_weight_pack_x3_kernel, dim3(k), dim3(256), 0, as_stream(stream), c, w_oihw,
+                       (_Float16*)w_split, w_inv_scale);
     HKP_LAUNCH_CHECK("hkp_stem_weight_pack_x3");
     return HKP_OK;
 }
 
 extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
-                                      float* y, float* stat_partials, hkp_stream_t stream) {
+                                      const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -968,21 +1167,22 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     const long M = (long)d->n * ho * wo;
     HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_fwd_stem_x3: too large");
     X3Args a;
-    a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.y = y; a.part = stat_partials;
-    a.amax = nullptr; a.add = nullptr;
+    a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.wscale = w_inv_scale;
+    a.y = y; a.part = stat_partials; a.amax = nullptr; a.add = nullptr;
     a.N = d->n; a.H = 2 * ho + 6; a.W = 2 * wo + 6; a.C = 4; a.K = d->k; a.R = 7; a.S = 1;
     a.stride = 2; a.pad = 0; a.dil = 1; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.cch = 1; a.RS = 7; a.nks = 7;
     a.plane = (long)d->n * a.H * a.W * 4;
     a.n_tiles = d->k / 64;
     const long m_tiles = (M + 255) / 256;
-    hipLaunchKernelGGL((conv_x3_kernel<64, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+    hipLaunchKernelGGL((conv_x3_kernel<64, 2, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
     return HKP_OK;
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant < 2, "hkp_set_conv_variant: unknown variant %d", variant);
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 5 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
+                  variant);
     g_x3_variant = variant;
     return HKP_OK;
 }

@@ -46,8 +46,8 @@ SIGNATURES = {
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
     "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _I32, _P, _P, _P]),
-    "hkp_weight_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P]),
-    "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
+    "hkp_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P]),
+    "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
@@ -55,11 +55,11 @@ SIGNATURES = {
     "hkp_upsample_argmax_ws_bytes": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_stem_pack_x3_elems": (_I64, [_CD]),
     "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
-    "hkp_stem_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _P, _P, _P]),
-    "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
+    "hkp_stem_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),
+    "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
-    "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
-    "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
+    "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
+    "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_conv_bwd_filter_x3_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_bwd_filter_split_workspace": (_I64, [_CD]),

@@ -98,13 +98,37 @@ def weight_split(w, passes=3):
     return hi, lo
 
 
+class PackedWeight(tuple):
+    """(split, inv_scale): a weight in the packed split layout (fp16, each output
+    channel scaled by a power of two) and the per-output-channel inverse scales."""
+
+    def __new__(cls, split, inv_scale):
+        return super().__new__(cls, (split, inv_scale))
+
+    @property
+    def split(self):
+        return self[0]
+
+    @property
+    def inv_scale(self):
+        return self[1]
+
+
+def x3_symbol(k, m):
+    """Kernel symbol the x3 conv launches for Cout = k over m output pixels (the
+    default tile policy of conv_x3.hip's launch_x3)."""
+    bn = 256 if (k % 256 == 0 and ((m + 255) // 256) * (k // 256) >= 1024) else (128 if k % 128 == 0 else 64)
+    return "conv_x3_kernel<%d, 2, false>" % bn
+
+
 def weight_pack_x3(w):
-    """fp32 KRSC weight → packed split fp16 [K, R, S, 2C] ([..][C/32][hi32|lo32]) for conv2d_fwd_x3."""
+    """fp32 KRSC weight → PackedWeight: [K, R, S, 2C] fp16 ([..][C/32][hi32|lo32]) + [K] scales."""
     _need(w, torch.float32, "weight_pack_x3.w", 4)
     k, r, s, c = w.shape
     ws = torch.empty((k, r, s, 2 * c), device=w.device, dtype=torch.float16)
-    call("hkp_weight_pack_x3", w.numel(), c, _ptr(w), _ptr(ws), _stream())
-    return ws
+    sc = torch.empty(k, device=w.device, dtype=torch.float32)
+    call("hkp_weight_pack_x3", k, r * s * c, c, _ptr(w), _ptr(ws), _ptr(sc), _stream())
+    return PackedWeight(ws, sc)
 
 
 def split_of(x):
@@ -122,11 +146,13 @@ def channels_of(x):
     return x.shape[-1]
 
 
-def conv2d_fwd_x3(xs, ws, stride=1, pad=0, dil=1, stats=True, out=None):
+def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None):
     """f16x3 NHWC conv on packed split operands: xs [N,H,W,2C] (from a producer with
-    split=3), ws [K,R,S,2C] (weight_pack_x3) → fp32 y [N,Ho,Wo,K] (+ BN partials)."""
+    split=3), wp = weight_pack_x3(w) → fp32 y [N,Ho,Wo,K] (+ BN partials)."""
+    ws, wsc = wp
     _need(xs, torch.float16, "conv2d_fwd_x3.x_split", 4)
     _need(ws, torch.float16, "conv2d_fwd_x3.w_split", 4)
+    _need(wsc, torch.float32, "conv2d_fwd_x3.w_inv_scale", 1)
     n, h, wd, c2 = xs.shape
     k, r, s, cw2 = ws.shape
     if cw2 != c2:
@@ -141,12 +167,12 @@ def conv2d_fwd_x3(xs, ws, stride=1, pad=0, dil=1, stats=True, out=None):
         part = torch.empty((tiles, k, 2), device=xs.device, dtype=torch.float32)
 
     def launch():
-        call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(y), _ptr(part), _stream())
+        call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part), _stream())
 
     if _observer is None:
         launch()
     else:
-        _observer("conv_x3_kernel<%d>" % (128 if k % 128 == 0 else 64), 2.0 * n * ho * wo * k * r * s * c,
+        _observer(x3_symbol(k, n * ho * wo), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
     return y, part
 
@@ -161,17 +187,19 @@ def stem_x3_ok(x_shape, w_shape, stride, pad, dil):
 
 
 def stem_weight_pack_x3(w):
-    """OIHW [K,C<=4,7,7] fp32 stem weight → [K,7,64] fp16 (conv2d_fwd_stem_x3 operand)."""
+    """OIHW [K,C<=4,7,7] fp32 stem weight → PackedWeight [K,7,64] fp16 + [K] scales."""
     _need(w, torch.float32, "stem_weight_pack_x3.w", 4)
     k, c = w.shape[:2]
     out = torch.empty((k, 7, 64), device=w.device, dtype=torch.float16)
-    call("hkp_stem_weight_pack_x3", k, c, _ptr(w), _ptr(out), _stream())
-    return out
+    sc = torch.empty(k, device=w.device, dtype=torch.float32)
+    call("hkp_stem_weight_pack_x3", k, c, _ptr(w), _ptr(out), _ptr(sc), _stream())
+    return PackedWeight(out, sc)
 
 
-def conv2d_fwd_stem_x3(x, ws, k, stats=True):
+def conv2d_fwd_stem_x3(x, wp, k, stats=True):
     """f16x3 stem conv (7x7/s2/p3) of an NCHW fp32 image → NHWC fp32 y (+ BN partials)."""
     from ._lib import lib
+    ws, wsc = wp
     _need(x, torch.float32, "conv2d_fwd_stem_x3.x", 4)
     _need(ws, torch.float16, "conv2d_fwd_stem_x3.w_split", 3)
     n, c, h, wd = x.shape
@@ -186,12 +214,13 @@ def conv2d_fwd_stem_x3(x, ws, k, stats=True):
         part = torch.empty((tiles, k, 2), device=x.device, dtype=torch.float32)
 
     def launch():
-        call("hkp_conv2d_fwd_stem_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(y), _ptr(part), _stream())
+        call("hkp_conv2d_fwd_stem_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
+             _stream())
 
     if _observer is None:
         launch()
     else:
-        _observer("conv_x3_kernel<64, true>", 2.0 * n * ho * wo * k * 49 * c, 2.0 * (xs.numel() + ws.numel()) +
+        _observer("conv_x3_kernel<64, 2, true>", 2.0 * n * ho * wo * k * 49 * c, 2.0 * (xs.numel() + ws.numel()) +
                   4.0 * y.numel(), launch)
     return y, part
 
@@ -473,12 +502,15 @@ def weight_flip_pack_x3(w):
     k, r, s, c = w.shape
     d = ConvDesc(1, 1, 1, c, k, r, s, 1, 0, 1, HKP_LAYOUT_NHWC)
     out = torch.empty((c, r, s, 2 * k), device=w.device, dtype=torch.float16)
-    call("hkp_weight_flip_pack_x3", ctypes.byref(d), _ptr(w), _ptr(out), _stream())
-    return out
+    sc = torch.empty(c, device=w.device, dtype=torch.float32)
+    call("hkp_weight_flip_pack_x3", ctypes.byref(d), _ptr(w), _ptr(out), _ptr(sc), _stream())
+    return PackedWeight(out, sc)
 
 
-def conv2d_bwd_data_x3(dys, wfs, x_shape, pad=0, dil=1, add=None, amax=None):
-    """f16x3 dL/dx of a stride-1 NHWC conv from packed dy (split_pack_x3 with `amax`)."""
+def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None):
+    """f16x3 dL/dx of a stride-1 NHWC conv from packed dy (split_pack_x3 with `amax`)
+    and wfp = weight_flip_pack_x3(w)."""
+    wfs, wfsc = wfp
     _need(dys, torch.float16, "conv2d_bwd_data_x3.dy_split", 4)
     _need(wfs, torch.float16, "conv2d_bwd_data_x3.wf_split", 4)
     c, r, s, k2 = wfs.shape
@@ -494,13 +526,13 @@ def conv2d_bwd_data_x3(dys, wfs, x_shape, pad=0, dil=1, add=None, amax=None):
     dx = torch.empty(tuple(x_shape), device=dys.device, dtype=torch.float32)
 
     def launch():
-        call("hkp_conv2d_bwd_data_x3", ctypes.byref(d), _ptr(dys), _ptr(wfs), _ptr(amax), _ptr(add), _ptr(dx),
-             _stream())
+        call("hkp_conv2d_bwd_data_x3", ctypes.byref(d), _ptr(dys), _ptr(wfs), _ptr(wfsc), _ptr(amax), _ptr(add),
+             _ptr(dx), _stream())
 
     if _observer is None:
         launch()
     else:
-        _observer("conv_x3_kernel<%d>" % (128 if c % 128 == 0 else 64),
+        _observer(x3_symbol(c, x_shape[0] * x_shape[1] * x_shape[2]),
                   2.0 * x_shape[0] * x_shape[1] * x_shape[2] * c * r * s * k,
                   2.0 * (dys.numel() + wfs.numel()) + 4.0 * dx.numel(), launch)
     return dx

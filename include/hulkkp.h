@@ -86,21 +86,27 @@ int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t*
                          const uint16_t* w_hi, const uint16_t* w_lo, int32_t passes, float* y,
                          float* stat_partials, hkp_stream_t stream);
 
-/* The f16x3 forward conv of the main path (same conv, arithmetic and epilogue
- * as hkp_conv2d_fwd_split with passes = 3), on operands pre-split into the
- * "packed split" layout: per pixel (weights: per filter tap) and per 32-channel
- * group one 128-B line [hi 32 | lo 32] (fp16 bit patterns), i.e.
- *   x_split[n*h*w][c/32][64]   written by hkp_bn_apply / hkp_bn_relu_maxpool
- *                              with split_passes = 3,
- *   w_split[k][r*s][c/32][64]  written by hkp_weight_pack_x3 from KRSC fp32
- *                              (n = k*r*s*c elements).
+/* The f16x3 conv of the main path (same conv and epilogue as hkp_conv2d_fwd;
+ * fp32-class accuracy) on operands pre-split into the "packed split" layout:
+ * per pixel (weights: per output channel and filter tap) and per 32-channel
+ * group one 128-B line [hi 32 | lo 32] (fp16 bit patterns), hi = f16(v),
+ * lo = f16(v - hi); the conv sums hi*hi + hi*lo + lo*hi in fp32.
+ *   x_split[n*h*w][c/32][64]   written by hkp_bn_apply / hkp_bn_relu_maxpool with
+ *                              split_passes = 3 (v = the activation),
+ *   w_split[k][r*s][c/32][64]  written by hkp_weight_pack_x3 from KRSC fp32, each
+ *                              output channel scaled by a power of two (max|w| ->
+ *                              [2^13, 2^14)); w_inv_scale[k] = the inverse, which
+ *                              the conv applies to its output.
  * Needs c % 32 == 0 and k % 64 == 0.  Replaces the same convs as hkp_conv2d_fwd. */
-int hkp_weight_pack_x3(int64_t n, int32_t c, const float* w, uint16_t* w_split, hkp_stream_t stream);
-/* Tuning knob: schedule variant of the x3 conv kernel (0 = default; 1 = s_setprio
- * around the MFMA clusters).  Results are identical across variants. */
+int hkp_weight_pack_x3(int32_t k, int32_t rsc, int32_t c, const float* w, uint16_t* w_split, float* w_inv_scale,
+                       hkp_stream_t stream);
+int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
+                      const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream);
+/* Tuning knob for the x3 conv's tile choice (0 = policy: 256x256 when Cout % 256
+ * == 0 and the grid is >= 4 rounds of blocks, else 256x128 / 256x64; 1 = 256x128
+ * only; 2 = 256x128 with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel
+ * stages whenever Cout % 256 == 0).  Outputs agree to fp32 summation order. */
 int hkp_set_conv_variant(int32_t variant);
-int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split, float* y,
-                      float* stat_partials, hkp_stream_t stream);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
@@ -199,20 +205,24 @@ int hkp_conv2d_bwd_filter_split(const hkp_conv_desc* d, const float* x, const fl
 /* The stem conv (7x7, stride 2, pad 3, NCHW input with C <= 4; src/resnet.py:137,199)
  * on the f16x3 path: hkp_stem_pack_x3 writes the image as zero-padded NHWC4 fp16
  * planes [2][n][2*ho+6][2*wo+6][4] (hi, then lo; hkp_stem_pack_x3_elems halves),
- * hkp_stem_weight_pack_x3 the OIHW weight as [k][7][hi32|lo32] (k*7*64 halves),
+ * hkp_stem_weight_pack_x3 the OIHW weight as [k][7][hi32|lo32] (k*7*64 halves,
+ * per-output-channel power-of-two scale, inverse in w_inv_scale[k]),
  * hkp_conv2d_fwd_stem_x3 = hkp_conv2d_fwd on them (NHWC fp32 y + BN partials). */
 int64_t hkp_stem_pack_x3_elems(const hkp_conv_desc* d);
 int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uint16_t* x_split, hkp_stream_t stream);
-int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split, hkp_stream_t stream);
-int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split, float* y,
-                           float* stat_partials, hkp_stream_t stream);
+int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split, float* w_inv_scale,
+                            hkp_stream_t stream);
+int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
+                           const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream);
 
 /* f16x3 backward on packed split operands (the layout of hkp_conv2d_fwd_x3):
  *   hkp_split_pack_x3:       x * 2^e → packed split [n/c][c/32][64]; 2^e from
  *                            amax_bits (max|x| as from hkp_absmax; NULL: 2^0) puts
  *                            max|x|*2^e in [2^13, 2^14) — gradients far below
  *                            fp16's normal range keep fp32-class accuracy.
- *   hkp_weight_flip_pack_x3: KRSC w → packed flipped [c][r][s][k/32][64] (dgrad operand).
+ *   hkp_weight_flip_pack_x3: KRSC w → packed flipped [c][r][s][k/32][64] (dgrad
+ *                            operand), per-row power-of-two scale, inverse in
+ *                            wf_inv_scale[c].
  *   hkp_conv2d_bwd_data_x3:  dx = conv(dy, flipped w) + add for stride-1 convs,
  *                            dy_split packed with the scale of dy_amax_bits;
  *                            needs Cin % 64 == 0, Cout % 32 == 0.
@@ -223,9 +233,11 @@ int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, cons
  * Replace the same cuDNN backward calls as hkp_conv2d_bwd_data / _filter. */
 int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits, uint16_t* x_split,
                       hkp_stream_t stream);
-int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf_split, hkp_stream_t stream);
+int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf_split, float* wf_inv_scale,
+                            hkp_stream_t stream);
 int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
-                           const uint32_t* dy_amax_bits, const float* add, float* dx, hkp_stream_t stream);
+                           const float* wf_inv_scale, const uint32_t* dy_amax_bits, const float* add, float* dx,
+                           hkp_stream_t stream);
 int64_t hkp_conv_bwd_filter_x3_workspace(const hkp_conv_desc* d);
 int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* dy_split,
                              const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,

@@ -54,10 +54,16 @@ def _unpack_x3(t):
     return g[..., 0, :].reshape(*t.shape[:-1], -1), g[..., 1, :].reshape(*t.shape[:-1], -1)
 
 
+def _pow2(t):
+    m, _ = torch.frexp(t)
+    return bool((m.abs() == 0.5).all())
+
+
 def test_producer_split_layouts(cuda_device):
-    """bn_apply / bn_relu_maxpool write exactly hi = f16(x), lo = f16((x-hi)*2^11)
-    in the packed layout (split=3) and the fp16 plane (split=1); keep_fp32=False
-    writes the same split without the fp32 tensor."""
+    """bn_apply / bn_relu_maxpool write exactly hi = f16(x), lo = f16(x-hi) in the
+    packed layout (split=3) and the fp16 plane (split=1); keep_fp32=False writes the
+    same split without the fp32 tensor.  Weight packs scale each output channel by
+    a power of two (max -> [2^13, 2^14)) and return the inverse."""
     from hkp import ops
     y = rand(2, 15, 20, 128, seed=11).to(cuda_device)
     ss = torch.cat([rand(128, seed=12) * 0.5 + 1, rand(128, seed=13) * 0.1]).to(cuda_device)
@@ -66,44 +72,67 @@ def test_producer_split_layouts(cuda_device):
     assert passes == 3 and sp.shape == (2, 15, 20, 256)
     hi, lo = _unpack_x3(sp)
     assert torch.equal(hi, act.half())
-    assert torch.equal(lo, ((act - act.half().float()) * 2048).half())
+    assert torch.equal(lo, (act - act.half().float()).half())
     only = ops.bn_apply(y, ss, relu=True, split=3, keep_fp32=False)
     assert only.dtype == torch.float16 and torch.equal(only, sp) and ops.channels_of(only) == 128
     one = ops.bn_apply(y, ss, relu=True, split=1)
     assert torch.equal(ops.split_of(one)[0], act.half())
     pool = ops.bn_relu_maxpool(rand(2, 31, 41, 64, seed=15).to(cuda_device), ss[:64].repeat(2), split=3)
     ph, pl = _unpack_x3(ops.split_of(pool)[0])
-    assert torch.equal(ph, pool.half()) and torch.equal(pl, ((pool - pool.half().float()) * 2048).half())
-    w = rand(64, 3, 3, 96, seed=16).to(cuda_device)
-    wh, wl = _unpack_x3(ops.weight_pack_x3(w))
-    h3, l3 = ops.weight_split(w, 3)
-    assert torch.equal(wh, h3) and torch.equal(wl, l3)
+    assert torch.equal(ph, pool.half()) and torch.equal(pl, (pool - pool.half().float()).half())
+    w = rand(64, 3, 3, 96, seed=16, scale=0.02).to(cuda_device)
+    wp = ops.weight_pack_x3(w)
+    assert _pow2(wp.inv_scale)
+    ws = w / wp.inv_scale.view(-1, 1, 1, 1)                         # exact: power-of-two scale
+    mx = ws.abs().amax((1, 2, 3))
+    assert bool(((mx >= 2 ** 13) & (mx < 2 ** 14)).all())
+    wh, wl = _unpack_x3(wp.split)
+    assert torch.equal(wh, ws.half()) and torch.equal(wl, (ws - ws.half().float()).half())
+    fp = ops.weight_flip_pack_x3(w)                                 # [C, R, S, 2K], row = input channel
+    wf = w.flip(1, 2).permute(3, 1, 2, 0) / fp.inv_scale.view(-1, 1, 1, 1)
+    fh, fl = _unpack_x3(fp.split)
+    assert _pow2(fp.inv_scale) and torch.equal(fh, wf.half()) and torch.equal(fl, (wf - wf.half().float()).half())
 
 
 X3_CASES = CASES + [
     (3, 13, 17, 64, 64, 3, 1, 1, 1),        # M = 663: ragged last 256-row tile (and 128-row half)
     (2, 31, 41, 64, 128, 1, 2, 0, 1),       # 1x1 stride-2 downsample
     (1, 9, 14, 32, 192, 3, 1, 2, 2),        # C = 32 (one channel group), K = 192 (BN 64)
+    (2, 11, 13, 64, 256, 3, 1, 1, 1),       # 256x256 tiles, ragged M, C = 64
 ]
 
 
 @pytest.mark.parametrize("case", X3_CASES)
-def test_x3_conv_bitwise_equals_inloop_split(cuda_device, case):
-    """The deep-pipelined packed-operand conv (conv_x3_kernel) performs exactly the
-    arithmetic of the in-loop-split kernel: outputs and BN partials bit-identical."""
+def test_x3_conv_fp32_accurate(cuda_device, case):
+    """The deep-pipelined packed-operand conv: fp32-class vs fp64, BN partials as the
+    fp32 kernel's, the 256x256 / 256x128 / 16-channel-stage tile variants agree to
+    fp32 summation order, and stats=False gives the same output."""
     from hkp import ops
+    from hkp._lib import call
     n, h, w, cin, cout, k, st, pad, dil = case
-    x = F.relu(rand(n, h, w, cin, seed=21)).to(cuda_device)
-    wt = rand(cout, k, k, cin, seed=22, scale=(2.0 / (k * k * cout)) ** 0.5).to(cuda_device)
-    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(cuda_device)
-    xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)      # identity BN → split of x
-    hi, lo = ops.weight_split(wt, 3)
-    y1, p1 = ops.conv2d_fwd_split(x, hi, lo, 3, st, pad, dil)
-    y2, p2 = ops.conv2d_fwd_x3(xs, ops.weight_pack_x3(wt), st, pad, dil)
-    assert torch.equal(y1, y2)
-    assert torch.equal(p1, p2)
-    y3, p3 = ops.conv2d_fwd_x3(xs, ops.weight_pack_x3(wt), st, pad, dil, stats=False)
-    assert p3 is None and torch.equal(y3, y1)
+    x = F.relu(rand(n, h, w, cin, seed=21))
+    wt = rand(cout, k, k, cin, seed=22, scale=(2.0 / (k * k * cout)) ** 0.5)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double(), None, st, pad, dil)
+    d = cuda_device
+    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d)
+    xs = ops.bn_apply(x.to(d), ss, relu=False, split=3, keep_fp32=False)      # identity BN → split of x
+    wp = ops.weight_pack_x3(wt.to(d))
+    y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
+    scale = ref.abs().max().item()
+    err = (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / scale
+    assert err < 2e-6, err
+    y32, p32 = ops.conv2d_fwd(x.to(d), wt.to(d), st, pad, dil)
+    assert torch.allclose(p, p32, rtol=1e-4, atol=1e-3)
+    y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
+    assert p3 is None and torch.equal(y3, y)
+    try:
+        for var in (1, 2, 3, 4):
+            call("hkp_set_conv_variant", var)
+            yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
+            assert (yv - y).abs().max().item() <= 1e-6 * scale
+            assert torch.allclose(pv, p, rtol=1e-4, atol=1e-3)
+    finally:
+        call("hkp_set_conv_variant", 0)
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if c[6] == 1 and c[3] % 64 == 0])
@@ -149,22 +178,26 @@ def test_f16x3_wgrad_scaled(cuda_device, case, gscale):
 
 @pytest.mark.parametrize("case", [c for c in X3_CASES if c[6] == 1 and c[3] % 64 == 0])
 @pytest.mark.parametrize("gscale", [1.0, 1e-9])
-def test_x3_dgrad_bitwise_equals_inloop_split(cuda_device, case, gscale):
-    """dgrad on packed scaled dy (split_pack_x3 + conv_x3_kernel) is bit-identical to
-    the in-loop-split dgrad kernel (same scaling, k order, epilogue)."""
+def test_x3_dgrad_scaled(cuda_device, case, gscale):
+    """dgrad on packed scaled dy (split_pack_x3 + conv_x3_kernel, flipped weights with
+    per-channel power-of-two scales): fp32-class vs fp64, also for gradients far
+    below fp16's normal range."""
     from hkp import ops
     n, h, w, cin, cout, k, st, pad, dil = case
-    wt = rand(cout, k, k, cin, seed=5, scale=(2.0 / (k * k * cout)) ** 0.5).to(cuda_device)
+    wt = rand(cout, cin, k, k, seed=5, scale=(2.0 / (k * k * cout)) ** 0.5)
     ho = (h + 2 * pad - dil * (k - 1) - 1) + 1
     wo = (w + 2 * pad - dil * (k - 1) - 1) + 1
-    gy = (rand(n, ho, wo, cout, seed=6) * gscale).to(cuda_device)
-    add = (rand(n, h, w, cin, seed=7) * gscale).to(cuda_device)
-    amax = ops.absmax(gy)
-    hi, lo = ops.conv_weight_flip_split(wt)
-    dx1 = ops.conv2d_bwd_data_split(gy, hi, lo, (n, h, w, cin), pad, dil, add=add, amax=amax)
-    dys = ops.split_pack_x3(gy, amax)
-    dx2 = ops.conv2d_bwd_data_x3(dys, ops.weight_flip_pack_x3(wt), (n, h, w, cin), pad, dil, add=add, amax=amax)
-    assert torch.equal(dx1, dx2)
+    gy = rand(n, cout, ho, wo, seed=6) * gscale
+    add = rand(n, cin, h, w, seed=7) * gscale
+    ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.double(), gy.double(), 1, pad, dil) + add.double()
+    d = cuda_device
+    gy_d = gy.permute(0, 2, 3, 1).contiguous().to(d)
+    amax = ops.absmax(gy_d)
+    dx = ops.conv2d_bwd_data_x3(ops.split_pack_x3(gy_d, amax),
+                                ops.weight_flip_pack_x3(wt.permute(0, 2, 3, 1).contiguous().to(d)),
+                                (n, h, w, cin), pad, dil, add=add.permute(0, 2, 3, 1).contiguous().to(d), amax=amax)
+    err = (dx.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
 
 
 WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [

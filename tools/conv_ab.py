@@ -2,7 +2,7 @@
 """In-process A/B of conv_x3 schedule variants (hkp_set_conv_variant) on the
 C2 conv shapes: variants interleaved round-robin, HIP-event timed, median and
 min per variant (cdna_hip_programming.md §5.4 rule 24: never compare separate
-processes).  Checks that every variant returns bit-identical outputs.
+processes).  Reports the largest output difference between variants (fp32 summation order).
 
     python tools/conv_ab.py [--variants 0,1] [--rounds 7] [--iters 10]
 """
@@ -27,7 +27,7 @@ SHAPES = {   # name: (N, H, W, Cin, Cout, k, stride, pad, dil) — R34-8s @640x4
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--variants", default="0,1,2")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--shapes", default=",".join(SHAPES))
@@ -60,10 +60,11 @@ def main():
                 times[v].append(s.elapsed_time(e) / args.iters)
         call("hkp_set_conv_variant", 0)
         flops = 2.0 * n * h * w * co * ci * k * k * 3
-        same = all(torch.equal(outs[variants[0]], outs[v]) for v in variants)
+        ref = outs[variants[0]]
+        same = max((outs[v] - ref).abs().max().item() / ref.abs().max().item() for v in variants)
         for v in variants:
             t = sorted(times[v])
-            print("%-7s var %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  identical=%s" % (
+            print("%-7s var %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  max rel diff=%.1e" % (
                 name, v, t[len(t) // 2], t[0], flops / (t[len(t) // 2] * 1e-3) / 1e12, same))
 
 
