@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int 
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ ss,
                                                              float* __restrict__ out, _Float16* __restrict__ osplit,
-                                                             int passes) {
+                                                             int passes, uchar4* __restrict__ route) {
     const int C4 = C >> 2;
     const long total = (long)N * Ho * Wo * C4;
     const long stride = (long)gridDim.x * blockDim.x;
@@ -127,6 +127,7 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int 
         const int n = (int)(p / Ho);
         const f32x4 a = *(const f32x4*)(ss + 4 * c4), b = *(const f32x4*)(ss + C + 4 * c4);
         f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int tap[4] = {0, 0, 0, 0};
 #pragma unroll
         for (int dr = 0; dr < 3; ++dr) {
             const int hi = ho * 2 - 1 + dr;
@@ -140,12 +141,18 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int 
                 for (int e = 0; e < 4; ++e) {
                     float t = __fadd_rn(__fmul_rn(v[e], a[e]), b[e]);
                     t = t > 0.f ? t : 0.f;
-                    m[e] = t > m[e] ? t : m[e];
+                    if (t > m[e]) {            // first maximum wins (ATen's window scan)
+                        m[e] = t;
+                        tap[e] = dr * 3 + ds;
+                    }
                 }
             }
         }
         if (out) *(f32x4*)(out + i * 4) = m;
         if (osplit) store_split4(m, i, osplit, passes);
+        if (route)   // the tap the window's gradient goes to; 0xFF: max <= 0, ReLU blocks it
+            route[i] = make_uchar4(m[0] > 0.f ? tap[0] : 255, m[1] > 0.f ? tap[1] : 255,
+                                   m[2] > 0.f ? tap[2] : 255, m[3] > 0.f ? tap[3] : 255);
     }
 }
 
@@ -219,7 +226,7 @@ extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* s
 
 extern "C" int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y,
                                    const float* scale_shift, float* out, uint16_t* out_split,
-                                   int32_t split_passes, hkp_stream_t stream) {
+                                   int32_t split_passes, uint8_t* route, hkp_stream_t stream) {
     HKP_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "hkp_bn_relu_maxpool: bad sizes");
     HKP_CHECK_ARG(y && scale_shift && (out || out_split), "hkp_bn_relu_maxpool: null tensor");
     HKP_CHECK_ARG(!out_split || ((split_passes == 1 || split_passes == 3) && c % 32 == 0),
@@ -227,7 +234,7 @@ extern "C" int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, c
     const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
     const long work = (long)n * ho * wo * (c / 4);
     hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n, h, w, c,
-                       ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes);
+                       ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes, (uchar4*)route);
     HKP_LAUNCH_CHECK("hkp_bn_relu_maxpool");
     return HKP_OK;
 }

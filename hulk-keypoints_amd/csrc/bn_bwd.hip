@@ -83,9 +83,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
 // per channel: dgamma, dbeta, and the apply coefficients (grad_mean, k, invstd*gamma)
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
                                                              const float* __restrict__ mi, const float* gamma,
-                                                             float* dgamma, float* dbeta, float* coef) {
+                                                             float* dgamma, float* dbeta, float* coef,
+                                                             unsigned* amax_reset) {
     __shared__ double red[2][4];
     const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (amax_reset && c == 0 && tid == 0) *amax_reset = 0u;
     double s = 0.0, d = 0.0;
     for (long t = tid; t < tiles; t += 256) {
         s += (double)part[(t * C + c) * 2];
@@ -165,9 +167,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, cons
 // pooling windows that contain each input pixel.  Emits dz = dL/d(BN output)
 // (ReLU mask applied).  Window argmax = first max in (dr, ds) scan order, NaN
 // wins — ATen's CPU max_pool2d rule.
+// dz at input pixel (h, w): the sum of dpool over the (<= 4) windows whose
+// routed tap (written by the forward, hkp_bn_relu_maxpool) is this pixel, in
+// window order (ho, wo) ascending; 0xFF routes nothing (window max <= 0: the
+// ReLU derivative is 0 at its argmax).
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, int C, int Ho, int Wo,
-                                                         const float* __restrict__ dpool, const float* __restrict__ y,
-                                                         const float* __restrict__ ss, float* __restrict__ dz) {
+                                                         const float* __restrict__ dpool,
+                                                         const uchar4* __restrict__ route, float* __restrict__ dz) {
     const int C4 = C >> 2;
     const long total = (long)N * H * W * C4;
     const long stride = (long)gridDim.x * blockDim.x;
@@ -178,44 +184,22 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(int N, int H, int W, i
         p /= W;
         const int h = (int)(p % H);
         const int n = (int)(p / H);
-        const f32x4 a = *(const f32x4*)(ss + 4 * c4), b = *(const f32x4*)(ss + C + 4 * c4);
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
         const int ho0 = h >> 1, ho1 = min((h + 1) >> 1, Ho - 1);
         const int wo0 = w >> 1, wo1 = min((w + 1) >> 1, Wo - 1);
         for (int ho = ho0; ho <= ho1; ++ho) {
             for (int wo = wo0; wo <= wo1; ++wo) {
-                // argmax of the window (ho, wo), per channel lane
-                f32x4 best = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-                int bidx[4] = {-1, -1, -1, -1};
-                for (int dr = 0; dr < 3; ++dr) {
-                    const int hi = ho * 2 - 1 + dr;
-                    if ((unsigned)hi >= (unsigned)H) continue;
-                    for (int ds = 0; ds < 3; ++ds) {
-                        const int wi = wo * 2 - 1 + ds;
-                        if ((unsigned)wi >= (unsigned)W) continue;
-                        const f32x4 v = *(const f32x4*)(y + (((long)n * H + hi) * W + wi) * C + 4 * c4);
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            float t = v[e] * a[e] + b[e];
-                            t = t > 0.f ? t : 0.f;
-                            if (bidx[e] < 0 || t > best[e] || t != t) {
-                                best[e] = t;
-                                bidx[e] = hi * W + wi;
-                            }
-                        }
-                    }
+                const long o = (((long)n * Ho + ho) * Wo + wo) * C4 + c4;
+                const uchar4 r = route[o];
+                const unsigned me = (unsigned)((h - (ho * 2 - 1)) * 3 + (w - (wo * 2 - 1)));
+                if (r.x == me || r.y == me || r.z == me || r.w == me) {
+                    const f32x4 d = *(const f32x4*)(dpool + o * 4);
+                    if (r.x == me) acc[0] += d[0];
+                    if (r.y == me) acc[1] += d[1];
+                    if (r.z == me) acc[2] += d[2];
+                    if (r.w == me) acc[3] += d[3];
                 }
-                const f32x4 d = *(const f32x4*)(dpool + (((long)n * Ho + ho) * Wo + wo) * C + 4 * c4);
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    if (bidx[e] == h * W + w) acc[e] += d[e];
             }
-        }
-        const f32x4 v = *(const f32x4*)(y + i * 4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float t = v[e] * a[e] + b[e];
-            if (!(t > 0.f)) acc[e] = 0.f;
         }
         *(f32x4*)(dz + i * 4) = acc;
     }
@@ -255,11 +239,12 @@ extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const flo
 }
 
 extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd,
-                                   const float* gamma, float* dgamma, float* dbeta, float* coef, hkp_stream_t stream) {
+                                   const float* gamma, float* dgamma, float* dbeta, float* coef,
+                                   uint32_t* dy_amax_reset, hkp_stream_t stream) {
     HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, as_stream(stream), c, (long)m, tiles, partials,
-                       mean_invstd, gamma, dgamma, dbeta, coef);
+                       mean_invstd, gamma, dgamma, dbeta, coef, (unsigned*)dy_amax_reset);
     HKP_LAUNCH_CHECK("hkp_bn_bwd_finalize");
     return HKP_OK;
 }
@@ -271,13 +256,6 @@ extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const floa
     HKP_CHECK_ARG(g && y && mean_invstd && coef && dy, "hkp_bn_bwd_apply: null tensor");
     const long n4 = m * (long)c / 4;
     hipStream_t st = as_stream(stream);
-    if (dy_amax_bits) {
-        hipError_t e = hipMemsetAsync(dy_amax_bits, 0, sizeof(uint32_t), st);
-        if (e != hipSuccess) {
-            set_error("hkp_bn_bwd_apply: memset: %s", hipGetErrorString(e));
-            return (int)e;
-        }
-    }
 #define HKP_BWD_APPLY(MASK, AMAX)                                                                                    \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MASK, AMAX>), dim3(AMAX ? std::min(grid_cap(n4), 512) : grid_cap(n4)), \
                        dim3(256), 0, st, n4, c / 4,                                                                \
@@ -293,14 +271,14 @@ extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const floa
     return HKP_OK;
 }
 
-extern "C" int hkp_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, const float* dpool, const float* y,
-                               const float* scale_shift, float* dz, hkp_stream_t stream) {
+extern "C" int hkp_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, const float* dpool, const uint8_t* route,
+                               float* dz, hkp_stream_t stream) {
     HKP_CHECK_ARG(n > 0 && h > 0 && w > 0 && c > 0 && c % 4 == 0, "hkp_maxpool_bwd: bad sizes");
-    HKP_CHECK_ARG(dpool && y && scale_shift && dz, "hkp_maxpool_bwd: null tensor");
+    HKP_CHECK_ARG(dpool && route && dz, "hkp_maxpool_bwd: null tensor");
     const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
     const long work = (long)n * h * w * (c / 4);
     hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_cap(work)), dim3(256), 0, as_stream(stream), n, h, w, c, ho, wo,
-                       dpool, y, scale_shift, dz);
+                       dpool, (const uchar4*)route, dz);
     HKP_LAUNCH_CHECK("hkp_maxpool_bwd");
     return HKP_OK;
 }

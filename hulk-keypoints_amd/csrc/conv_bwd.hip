@@ -185,14 +185,23 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgArgs a) {
         }
 }
 
-// dw[i] = sum_s ws[s][i] in fixed split order
+// dw[i] = sum_s ws[s][i] in a fixed order: 4 lanes per element each sum every
+// 4th split (many loads in flight per thread), then the 4 lane sums pairwise
 __global__ __launch_bounds__(256) void split_reduce_kernel(long n, int splits, const float* __restrict__ ws,
                                                           float* __restrict__ out, int accumulate) {
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        float s = 0.f;
-        for (int k = 0; k < splits; ++k) s += ws[(long)k * n + i];
-        out[i] = accumulate ? out[i] + s : s;
+    __shared__ float red[4][64];
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const long i = (long)blockIdx.x * 64 + l;
+    float s = 0.f;
+    if (i < n) {
+#pragma unroll 8
+        for (int k = q; k < splits; k += 4) s += ws[(long)k * n + i];
+    }
+    red[q][l] = s;
+    __syncthreads();
+    if (q == 0 && i < n) {
+        const float t = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+        out[i] = accumulate ? out[i] + t : t;
     }
 }
 
@@ -286,9 +295,8 @@ extern "C" int hkp_conv2d_bwd_filter(const hkp_conv_desc* d, const float* x, con
     }
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter");
     const long n = (long)d->k * a.Kreal;
-    long g = (n + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(split_reduce_kernel, dim3((unsigned)g), dim3(256), 0, st, n, sp, a.ws, dw, accumulate);
+    hipLaunchKernelGGL(split_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, n, sp, a.ws, dw,
+                       accumulate);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter(reduce)");
     return HKP_OK;
 }

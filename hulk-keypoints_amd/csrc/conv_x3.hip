@@ -975,7 +975,7 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
 // Tuning knob (hkp_set_conv_variant; results agree to fp32 summation order, in
 // practice bit-identical): 0 = policy, 1 = 256x128 32-ch stages only,
 // 2 = 256x128 16-ch stages (4-stage ring), 3 = 256x256 32-ch stages whenever
-// Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0.
+// Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0, 5 = 256x64.
 static int g_x3_variant = [] {
     const char* e = getenv("HKP_X3_VARIANT");
     return e ? atoi(e) : 0;
@@ -983,7 +983,7 @@ static int g_x3_variant = [] {
 
 static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a) {
     const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
-    int bn = k % 128 == 0 ? 128 : 64, kh = 2;
+    int bn = (k % 128 == 0 && v != 5) ? 128 : 64, kh = 2;
     if (k % 256 == 0 && (v == 3 || v == 4 || (v == 0 && m_tiles * (k / 256) >= 1024))) {
         bn = 256;
         kh = v == 4 ? 1 : 2;
@@ -1181,7 +1181,7 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 5 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 6 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

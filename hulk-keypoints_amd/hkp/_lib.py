@@ -24,6 +24,12 @@ class ConvDesc(ctypes.Structure):
                 ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "dilation", "in_layout")]
 
 
+class PackJob(ctypes.Structure):
+    """hkp_pack_job (hkp_weight_pack_x3_batch)."""
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p), ("inv_scale", ctypes.c_void_p),
+                ("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("rs", ctypes.c_int32), ("c", ctypes.c_int32)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -40,7 +46,7 @@ SIGNATURES = {
     "hkp_bn_finalize": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_eval_params": (ctypes.c_int, [_I32, _P, _P, _P, _P, _F, _P, _P, _P]),
     "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _I32, _P]),
-    "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P]),
+    "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
@@ -60,6 +66,8 @@ SIGNATURES = {
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
     "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_weight_pack_x3_batch_ws_bytes": (_I64, [_I32, ctypes.POINTER(PackJob)]),
+    "hkp_weight_pack_x3_batch": (ctypes.c_int, [_I32, ctypes.POINTER(PackJob), _P, _I64, _P]),
     "hkp_conv_bwd_filter_x3_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_bwd_filter_split_workspace": (_I64, [_CD]),
@@ -71,9 +79,9 @@ SIGNATURES = {
     "hkp_conv2d_bwd_filter": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _I64, _P]),
     "hkp_bn_bwd_tiles": (_I64, [_I64]),
     "hkp_bn_bwd_reduce": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P]),
-    "hkp_bn_bwd_finalize": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_finalize": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "hkp_heat_loss_workspace": (_I64, []),
     "hkp_heat_loss": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _P, _P, _P, _P]),
     "hkp_head_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),

@@ -53,18 +53,65 @@ _precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
 _split_cache = {}
 
 
-def _cached_split(w, variant, make):
+def _cache_slot(w):
     slot = _split_cache.get(id(w))
     if slot is None or slot[0]() is not w:
         wid = id(w)
         slot = (weakref.ref(w, lambda _r, k=wid: _split_cache.pop(k, None)), {})
         _split_cache[wid] = slot
-    per = slot[1]
+    return slot[1]
+
+
+def _fresh(w, ent):
+    return ent is not None and ent[0] == w._version and ent[1] == w.data_ptr()
+
+
+def _cached_split(w, variant, make):
+    per = _cache_slot(w)
     ent = per.get(variant)
-    if ent is None or ent[0] != w._version or ent[1] != w.data_ptr():
+    if not _fresh(w, ent):
         ent = (w._version, w.data_ptr(), make(w.detach()))
         per[variant] = ent
     return ent[2]
+
+
+def _nhwc_convs(resnet):
+    for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4):
+        for block in layer:
+            yield block.conv1
+            yield block.conv2
+            if block.kind == "bottleneck":
+                yield block.conv3
+            if block.downsample is not None:
+                yield block.downsample[0]
+
+
+def prepack_x3(resnet, flip):
+    """Refresh every stale f16x3 conv operand of the backbone — the forward packs
+    and (flip=True, training) the stride-1 convs' flipped dgrad packs — in one
+    batched launch pair (hkp_weight_pack_x3_batch) instead of one pack per conv.
+    The operands land in the same cache conv_bn / _conv_backward read, with the
+    parameter versions they were packed from; buffers are reused across steps."""
+    if _precision != "f16x3":
+        return
+    items, outs, dest = [], [], []
+    for conv in _nhwc_convs(resnet):
+        w = conv.weight
+        k, c = w.shape[0], w.shape[-1]
+        want = ["x3"] if (k % 64 == 0 and c % 32 == 0) else []
+        if flip and _i(conv.stride) == 1 and k % 64 == 0 and c % 64 == 0:
+            want.append("flip_x3")
+        per = _cache_slot(w) if want else None
+        for v in want:
+            ent = per.get(v)
+            if not _fresh(w, ent):
+                items.append((v, w.detach()))
+                outs.append(ent[2] if ent is not None else None)
+                dest.append((per, v, w))
+    if not items:
+        return
+    for (per, v, w), packed in zip(dest, ops.weight_pack_x3_batch(items, outs)):
+        per[v] = (w._version, w.data_ptr(), packed)
 
 
 def set_conv_precision(p):
@@ -123,7 +170,7 @@ def _split_for(c):
 def stem_forward(resnet, x_nchw, trace=None):
     """conv1 → bn1 → relu → maxpool (src/resnet.py:199-202)."""
     y, ss, mi = conv_bn(resnet.conv1, resnet.bn1, x_nchw, layout="nchw")
-    out = ops.bn_relu_maxpool(y, ss, split=_split_for(y.shape[-1]))
+    out = ops.bn_relu_maxpool(y, ss, split=_split_for(y.shape[-1]), route=trace is not None)
     if trace is not None:
         trace.stem = dict(x=x_nchw, y=y, ss=ss, mi=mi, out=out)
     return out
@@ -173,6 +220,7 @@ def backbone_forward(resnet, x_nchw, trace=None):
     """ResNet.forward up to the fc (src/resnet.py:198-213), NHWC output."""
     if x_nchw.dim() != 4 or x_nchw.shape[1] != 3:
         raise ValueError("expected [B,3,H,W] input, got %s" % (tuple(x_nchw.shape),))
+    prepack_x3(resnet, flip=trace is not None)
     x = stem_forward(resnet, x_nchw.contiguous(), trace)
     for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4):
         for block in layer:
@@ -280,7 +328,7 @@ def block_backward(block, rec, g_out, grads):
 
 
 def stem_backward(resnet, st, g_pool, grads):
-    dz = ops.maxpool_bwd(g_pool, st["y"], st["ss"])
+    dz = ops.maxpool_bwd(g_pool, st["out"]._hkp_route, tuple(st["y"].shape))
     dy, _ = _bn_backward(resnet.bn1, dz, None, st["y"], st["mi"], grads)
     c = resnet.conv1
     grads.put(c.weight, ops.conv2d_bwd_filter(st["x"], dy, tuple(c.weight.shape), _i(c.stride), _i(c.padding),

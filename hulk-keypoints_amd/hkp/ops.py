@@ -338,15 +338,21 @@ def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None, split=0, keep_fp
     return o
 
 
-def bn_relu_maxpool(y, ss, split=0):
+def bn_relu_maxpool(y, ss, split=0, route=False):
+    """maxpool3x3/s2/p1(relu(y*scale+shift)); route=True (training) also records
+    each window's gradient tap as out._hkp_route (uint8, out's shape) for maxpool_bwd."""
     _need(y, torch.float32, "bn_relu_maxpool.y", 4)
     n, h, w, c = y.shape
     _check_split(split, c, "bn_relu_maxpool")
     out = torch.empty((n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c), device=y.device, dtype=torch.float32)
     sp = _split_out(out.shape, y.device, split) if split else None
-    call("hkp_bn_relu_maxpool", n, h, w, c, _ptr(y), _ptr(ss), _ptr(out), _ptr(sp), int(split), _stream())
+    rt = torch.empty(out.shape, device=y.device, dtype=torch.uint8) if route else None
+    call("hkp_bn_relu_maxpool", n, h, w, c, _ptr(y), _ptr(ss), _ptr(out), _ptr(sp), int(split), _ptr(rt),
+         _stream())
     if split:
         out._hkp_split = (sp, split)
+    if route:
+        out._hkp_route = rt
     return out
 
 
@@ -507,6 +513,36 @@ def weight_flip_pack_x3(w):
     return PackedWeight(out, sc)
 
 
+def weight_pack_x3_batch(items, outs=None):
+    """Many weight packs in one launch pair (hkp_weight_pack_x3_batch): items =
+    [(kind, w)] with kind "x3" (= weight_pack_x3(w)) or "flip_x3"
+    (= weight_flip_pack_x3(w)); returns the PackedWeights in order.  outs
+    (optional, same order; None entries allowed) are PackedWeights to overwrite."""
+    from ._lib import PackJob, lib
+    jobs = (PackJob * max(1, len(items)))()
+    res = []
+    for i, (kind, w) in enumerate(items):
+        _need(w, torch.float32, "weight_pack_x3_batch.w", 4)
+        k, r, s, c = w.shape
+        flip = kind == "flip_x3"
+        if not flip and kind != "x3":
+            raise HkpError("weight_pack_x3_batch: unknown kind %r" % (kind,))
+        shape, n_sc = ((c, r, s, 2 * k), c) if flip else ((k, r, s, 2 * c), k)
+        o = outs[i] if outs is not None else None
+        if o is None or tuple(o.split.shape) != shape or o.split.device != w.device:
+            o = PackedWeight(torch.empty(shape, device=w.device, dtype=torch.float16),
+                             torch.empty(n_sc, device=w.device, dtype=torch.float32))
+        res.append(o)
+        jobs[i].w, jobs[i].out, jobs[i].inv_scale = _ptr(w), _ptr(o.split), _ptr(o.inv_scale)
+        jobs[i].kind, jobs[i].k, jobs[i].rs, jobs[i].c = int(flip), k, r * s, c
+    if not items:
+        return res
+    nb = lib().hkp_weight_pack_x3_batch_ws_bytes(len(items), jobs)
+    ws = torch.empty(max(4, nb), device=items[0][1].device, dtype=torch.uint8)
+    call("hkp_weight_pack_x3_batch", len(items), jobs, _ptr(ws), nb, _stream())
+    return res
+
+
 def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None):
     """f16x3 dL/dx of a stride-1 NHWC conv from packed dy (split_pack_x3 with `amax`)
     and wfp = weight_flip_pack_x3(w)."""
@@ -602,10 +638,10 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False):
     dgamma = torch.empty(c, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(c, device=y.device, dtype=torch.float32)
     coef = torch.empty(3 * c, device=y.device, dtype=torch.float32)
-    call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta),
-         _ptr(coef), _stream())
-    dy = torch.empty_like(y)
     amax = torch.empty(1, device=y.device, dtype=torch.int32) if want_amax else None
+    call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta),
+         _ptr(coef), _ptr(amax), _stream())
+    dy = torch.empty_like(y)
     call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), _ptr(dy),
          _ptr(amax), _stream())
     if want_amax:
@@ -613,15 +649,16 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False):
     return dy, dgamma, dbeta, dz
 
 
-def maxpool_bwd(dpool, y, ss):
-    """Stem: dL/d(BN output) from dL/d(maxpool output) (ReLU mask applied)."""
+def maxpool_bwd(dpool, route, in_shape):
+    """Stem: dL/d(BN output) [in_shape] from dL/d(maxpool output) and the forward's
+    route (bn_relu_maxpool(..., route=True)._hkp_route; ReLU mask included)."""
     _need(dpool, torch.float32, "maxpool_bwd.dpool", 4)
-    _need(y, torch.float32, "maxpool_bwd.y", 4)
-    n, h, w, c = y.shape
-    if tuple(dpool.shape) != (n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c):
-        raise HkpError("maxpool_bwd: dpool shape mismatch")
-    dz = torch.empty_like(y)
-    call("hkp_maxpool_bwd", n, h, w, c, _ptr(dpool), _ptr(y), _ptr(ss), _ptr(dz), _stream())
+    _need(route, torch.uint8, "maxpool_bwd.route", 4)
+    n, h, w, c = in_shape
+    if tuple(dpool.shape) != (n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c) or route.shape != dpool.shape:
+        raise HkpError("maxpool_bwd: dpool / route shape mismatch")
+    dz = torch.empty(tuple(in_shape), device=dpool.device, dtype=torch.float32)
+    call("hkp_maxpool_bwd", n, h, w, c, _ptr(dpool), _ptr(route), _ptr(dz), _stream())
     return dz
 
 

@@ -105,7 +105,7 @@ int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uin
 /* Tuning knob for the x3 conv's tile choice (0 = policy: 256x256 when Cout % 256
  * == 0 and the grid is >= 4 rounds of blocks, else 256x128 / 256x64; 1 = 256x128
  * only; 2 = 256x128 with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel
- * stages whenever Cout % 256 == 0).  Outputs agree to fp32 summation order. */
+ * stages whenever Cout % 256 == 0; 5 = 256x64).  Outputs agree to fp32 summation order. */
 int hkp_set_conv_variant(int32_t variant);
 
 /* ----------------------------------------------------------- batchnorm ---- */
@@ -132,7 +132,7 @@ int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const f
  * out_split (nullable; needs c % 32 == 0): the same values also written as the
  * next conv's operand — split_passes = 1: fp16 plane [m][c] for
  * hkp_conv2d_fwd_split (passes 1); split_passes = 3: the packed split layout
- * [m][c/32][hi32|lo32] (hi = f16(out), lo = f16((out-hi)*2^11)) for
+ * [m][c/32][hi32|lo32] (hi = f16(out), lo = f16(out-hi)) for
  * hkp_conv2d_fwd_x3.  out may be NULL when out_split is given (an activation
  * only a conv consumes).  hkp_bn_relu_maxpool takes the same optional split. */
 int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
@@ -140,10 +140,13 @@ int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift,
                  int32_t split_passes, hkp_stream_t stream);
 
 /* Stem tail: maxpool3x3/s2/p1( relu( y*scale + shift ) ), NHWC
- * (src/resnet.py:139-141, 200-202). Output [n, (h-1)/2+1, (w-1)/2+1, c]. */
+ * (src/resnet.py:139-141, 200-202). Output [n, (h-1)/2+1, (w-1)/2+1, c].
+ * route (nullable; training): per output element the window tap 0..8 (r*3+s)
+ * of its first maximum — the pixel max_pool2d's backward routes the gradient
+ * to — or 255 when the maximum is <= 0 (the ReLU derivative there is 0). */
 int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float* y,
                         const float* scale_shift, float* out, uint16_t* out_split, int32_t split_passes,
-                        hkp_stream_t stream);
+                        uint8_t* route, hkp_stream_t stream);
 
 /* ---------------------------------------------------------------- head ---- */
 /* K-channel 1x1 scoring conv + bias (src/resnet_dilated.py:16 sliced to the K
@@ -238,6 +241,23 @@ int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf
 int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
                            const float* wf_inv_scale, const uint32_t* dy_amax_bits, const float* add, float* dx,
                            hkp_stream_t stream);
+/* Batched weight packing for a training step (one launch pair for a whole
+ * network instead of one hkp_weight_pack_x3 / hkp_weight_flip_pack_x3 per conv;
+ * outputs bit-identical to those).  jobs: host array; kind 0 = forward pack
+ * (out = w_split [k][rs][c/32][64], inv_scale [k]; needs c % 32 == 0), kind 1 =
+ * flipped dgrad pack (out = wf_split [c][rs][k/32][64], inv_scale [c]; needs
+ * c % 64 == 0, k % 32 == 0); w is KRSC fp32 [k][rs][c].  workspace:
+ * hkp_weight_pack_x3_batch_ws_bytes(njobs, jobs) bytes (per-channel column
+ * maxima of the flip jobs). */
+typedef struct hkp_pack_job {
+    const float* w;
+    uint16_t* out;
+    float* inv_scale;
+    int32_t kind, k, rs, c;
+} hkp_pack_job;
+int64_t hkp_weight_pack_x3_batch_ws_bytes(int32_t njobs, const hkp_pack_job* jobs);
+int hkp_weight_pack_x3_batch(int32_t njobs, const hkp_pack_job* jobs, void* workspace, int64_t ws_bytes,
+                             hkp_stream_t stream);
 int64_t hkp_conv_bwd_filter_x3_workspace(const hkp_conv_desc* d);
 int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* dy_split,
                              const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
@@ -254,22 +274,26 @@ int hkp_conv2d_bwd_filter(const hkp_conv_desc* d, const float* x, const float* d
  *             partials[tiles][c][2] = (sum dz, sum dz*(y-mean)); tiles = hkp_bn_bwd_tiles(m)
  *   finalize: dgamma = invstd*sum dz*(y-mean), dbeta = sum dz (nullable), coef[3c]
  *   apply:    dy = ((dz - sum dz/m) - (y-mean)*invstd^2*sum dz*(y-mean)/m) * invstd*gamma
- * mean_invstd is what hkp_bn_finalize produced in the forward.  apply also writes
- * max|dy| (IEEE bits, as hkp_absmax) to dy_amax_bits when non-NULL — the scale
- * input of hkp_split_pack_x3 for the f16x3 backward convs. */
+ * mean_invstd is what hkp_bn_finalize produced in the forward.  apply also folds
+ * max|dy| (IEEE bits, as hkp_absmax) into dy_amax_bits when non-NULL — the scale
+ * input of hkp_split_pack_x3 for the f16x3 backward convs; the word must hold 0
+ * on entry, which finalize's dy_amax_reset (nullable) sets in the same stream
+ * order (no separate memset). */
 int64_t hkp_bn_bwd_tiles(int64_t m);
 int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
                       const float* mean_invstd, float* dz, float* partials, hkp_stream_t stream);
 int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd, const float* gamma,
-                        float* dgamma, float* dbeta, float* coef, hkp_stream_t stream);
+                        float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_reset, hkp_stream_t stream);
 int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
                      const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
                      hkp_stream_t stream);
 
-/* Stem: backward of maxpool3x3/s2/p1(relu(y*scale+shift)) → dz = dL/d(BN output),
- * ReLU mask applied (src/resnet.py:200-202; ATen's first-max window rule). */
-int hkp_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, const float* dpool, const float* y,
-                    const float* scale_shift, float* dz, hkp_stream_t stream);
+/* Stem: backward of maxpool3x3/s2/p1(relu(y*scale+shift)) → dz = dL/d(BN output)
+ * [n,h,w,c], ReLU mask applied (src/resnet.py:200-202; ATen's first-max window
+ * rule): each window's dpool goes to the tap the forward recorded in `route`
+ * (hkp_bn_relu_maxpool), summed per pixel over its windows in (ho, wo) order. */
+int hkp_maxpool_bwd(int32_t n, int32_t h, int32_t w, int32_t c, const float* dpool, const uint8_t* route, float* dz,
+                    hkp_stream_t stream);
 
 /* Loss over the heatmaps (train.py:21,25; MSE train.py:13) in fp64: loss (device
  * double), dheat = dL/dheat as fp32 (nullable).  Target: dense fp64 `target`

@@ -75,3 +75,19 @@ def test_reference_init_statistics():
     assert abs(w.std().item() - np.sqrt(2 / (9 * 512))) < 2e-4
     assert abs(m.resnet.net.fc.weight.std().item() - 0.01) < 2e-4
     assert m.resnet.net.fc.bias.abs().sum().item() == 0
+
+
+def test_weight_pack_batch_host_side():
+    """hkp_pack_job layout, workspace sizing and argument checks (host only)."""
+    from hkp import _lib
+    assert ctypes.sizeof(_lib.PackJob) == 40
+    jobs = (_lib.PackJob * 3)()
+    for j, (kind, k, rs, c) in zip(jobs, [(0, 64, 9, 64), (1, 512, 9, 512), (1, 2048, 1, 512)]):
+        j.w, j.out, j.inv_scale, j.kind, j.k, j.rs, j.c = 16, 16, 16, kind, k, rs, c
+    assert _lib.lib().hkp_weight_pack_x3_batch_ws_bytes(3, jobs) == 4 * (512 // 8 * 512 + 2048 // 8 * 512)
+    with pytest.raises(_lib.HkpError, match="workspace"):
+        _lib.call("hkp_weight_pack_x3_batch", 3, jobs, None, 0, None)
+    jobs[1].c = 96                                     # flip needs c % 64 == 0
+    with pytest.raises(_lib.HkpError, match="c%64==0"):
+        _lib.call("hkp_weight_pack_x3_batch", 3, jobs, None, 0, None)
+    assert _lib.call("hkp_weight_pack_x3_batch", 0, jobs, None, 0, None) == 0

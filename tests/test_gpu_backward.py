@@ -119,10 +119,18 @@ def test_maxpool_backward(cuda_device):
     p.backward(g)
     ref = y.grad / torch.where(a == 0, torch.ones_like(a), a)[None, :, None, None]  # dL/dt
     ss = torch.cat([a, b]).to(cuda_device)
-    dz = ops.maxpool_bwd(nhwc(g).to(cuda_device), nhwc(y.detach()).to(cuda_device), ss)
+    yd = nhwc(y.detach()).to(cuda_device)
+    pool = ops.bn_relu_maxpool(yd, ss, route=True)
+    assert torch.equal(nchw(pool.cpu()), p.detach())
+    rt = pool._hkp_route
+    assert rt.dtype == torch.uint8 and int(rt[rt != 255].max()) <= 8
+    dz = ops.maxpool_bwd(nhwc(g).to(cuda_device), rt, tuple(yd.shape))
     got = nchw(dz.cpu())
     live = a != 0
     assert (got[:, live] - ref[:, live]).abs().max() < 1e-5
+    # constant channels (a = 0): the ReLU passes nothing where relu(b) == 0, and
+    # the whole window's gradient goes to the first tap where b > 0
+    assert torch.equal(got[:, ~live & (b <= 0)], torch.zeros_like(got[:, ~live & (b <= 0)]))
 
 
 def test_heat_loss_matches_reference_golden(cuda_device, golden):

@@ -94,6 +94,34 @@ def test_producer_split_layouts(cuda_device):
     assert _pow2(fp.inv_scale) and torch.equal(fh, wf.half()) and torch.equal(fl, (wf - wf.half().float()).half())
 
 
+def test_weight_pack_batch_bitexact(cuda_device):
+    """hkp_weight_pack_x3_batch == the per-conv packs, bit for bit: 1x1 and 3x3,
+    (tap, k) row counts off the 256-row tile, K = 2048 (many column partials),
+    rows longer than the register-held 5120 floats, > 32 jobs (several launches),
+    reuse of output buffers."""
+    from hkp import ops
+    shapes = [(64, 3, 3, 64), (128, 3, 3, 64), (64, 1, 1, 256), (2048, 1, 1, 512), (256, 3, 3, 1024),
+              (96, 3, 3, 128), (512, 3, 3, 512), (128, 1, 1, 64)]
+    ws = [rand(*s, seed=40 + i, scale=10.0 ** (i % 5 - 3)).to(cuda_device) for i, s in enumerate(shapes)]
+    ws[2][5].zero_()                                   # an all-zero filter: scale 1
+    items = []
+    for i in range(40):
+        w = ws[i % len(ws)]
+        kind = "flip_x3" if (i % 3 == 1 and w.shape[-1] % 64 == 0) else "x3"
+        items.append((kind, w))
+    got = ops.weight_pack_x3_batch(items)
+    for (kind, w), g in zip(items, got):
+        ref = ops.weight_flip_pack_x3(w) if kind == "flip_x3" else ops.weight_pack_x3(w)
+        assert torch.equal(g.split, ref.split) and torch.equal(g.inv_scale, ref.inv_scale), (kind, tuple(w.shape))
+    for w in ws:
+        w.mul_(-3.0)
+    again = ops.weight_pack_x3_batch(items, got)
+    for (kind, w), g, o in zip(items, again, got):
+        assert g.split.data_ptr() == o.split.data_ptr()
+        ref = ops.weight_flip_pack_x3(w) if kind == "flip_x3" else ops.weight_pack_x3(w)
+        assert torch.equal(g.split, ref.split) and torch.equal(g.inv_scale, ref.inv_scale), (kind, tuple(w.shape))
+
+
 X3_CASES = CASES + [
     (3, 13, 17, 64, 64, 3, 1, 1, 1),        # M = 663: ragged last 256-row tile (and 128-row half)
     (2, 31, 41, 64, 128, 1, 2, 0, 1),       # 1x1 stride-2 downsample

@@ -20,6 +20,10 @@ SHAPES = {   # name: (N, H, W, Cin, Cout, k, stride, pad, dil) — R34-8s @640x4
     "layer3": (32, 60, 80, 256, 256, 3, 1, 2, 2),
     "layer2": (32, 60, 80, 128, 128, 3, 1, 1, 1),
     "layer1": (32, 120, 160, 64, 64, 3, 1, 1, 1),
+    "t4": (8, 60, 80, 512, 512, 3, 1, 4, 4),             # training shard (batch 8)
+    "t3": (8, 60, 80, 256, 256, 3, 1, 2, 2),
+    "t2": (8, 60, 80, 128, 128, 3, 1, 1, 1),
+    "t1": (8, 120, 160, 64, 64, 3, 1, 1, 1),
     "layer4_n2": (2, 60, 80, 512, 512, 3, 1, 4, 4),     # 4.9 MB operand: L2/MALL-resident
     "layer3_n4": (4, 60, 80, 256, 256, 3, 1, 2, 2),
 }
