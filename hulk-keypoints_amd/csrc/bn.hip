@@ -13,35 +13,52 @@
 
 namespace hkp {
 
-// one block (256 threads) per channel; deterministic fixed-order fp64 merge
+// CPB channels per block (partials_cpb); deterministic fixed-order fp64 merge
+template <int CPB>
 __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
                                                          const float* __restrict__ part, const float* gamma,
                                                          const float* beta, float momentum, float eps, float* rmean,
                                                          float* rvar, int64_t* nbt, float* ss, float* mi) {
-    __shared__ double red[4];
-    __shared__ double bcast;
-    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int TL = 256 / CPB;
+    __shared__ double red[4][8];
+    const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
+    const bool ok = c < C;
+    // tiles t = tl, tl + TL, ... in order; 8 loads in flight per batch (the loop
+    // is latency-bound), zero-filled past the end (exact: s + 0 = s)
     double s = 0.0;
-    for (long t = tid; t < tiles; t += 256) s += (double)part[(t * C + c) * 2];
-    s = wave_sum_d(s);
-    if (lane == 0) red[wid] = s;
-    __syncthreads();
-    if (tid == 0) bcast = ((red[0] + red[1]) + (red[2] + red[3])) / (double)count;
-    __syncthreads();
-    const double mean = bcast;
+    if (ok)
+        for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const long t = t0 + (long)j * TL;
+                v[j] = t < tiles ? part[(t * C + c) * 2] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += (double)v[j];
+        }
+    const double mean = lanes_sum_d<CPB>(s, red) / (double)count;
     double q = 0.0;
-    for (long t = tid; t < tiles; t += 256) {
-        const long n_t = min((long)tile_rows, count - t * tile_rows);
-        const double st = (double)part[(t * C + c) * 2];
-        const double dm = st / (double)n_t - mean;
-        q += (double)part[(t * C + c) * 2 + 1] + (double)n_t * dm * dm;
-    }
-    q = wave_sum_d(q);
-    __syncthreads();
-    if (lane == 0) red[wid] = q;
-    __syncthreads();
-    if (tid == 0) {
-        const double m2 = (red[0] + red[1]) + (red[2] + red[3]);
+    if (ok)
+        for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
+            float2 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const long t = t0 + (long)j * TL;
+                v[j] = t < tiles ? *(const float2*)(part + (t * C + c) * 2) : make_float2(0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const long t = t0 + (long)j * TL;
+                if (t < tiles) {
+                    const long n_t = min((long)tile_rows, count - t * tile_rows);
+                    const double dm = (double)v[j].x / (double)n_t - mean;
+                    q += (double)v[j].y + (double)n_t * dm * dm;
+                }
+            }
+        }
+    const double m2 = lanes_sum_d<CPB>(q, red);
+    if (tl == 0 && ok) {
         const double var = m2 / (double)count;
         const double invstd = 1.0 / sqrt(var + (double)eps);
         const float inv_f = (float)invstd, mean_f = (float)mean;
@@ -77,13 +94,15 @@ __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, con
     }
 }
 
-// RES: 0 none, 1 raw residual, 2 affine residual (downsample BN)
+// RES: 0 none, 1 raw residual, 2 affine residual (downsample BN), 3 raw residual
+// read from its packed split (hi + lo, written by the producer of the block input)
 template <int RES, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f32x4* __restrict__ y,
                                                        const f32x4* __restrict__ sc, const f32x4* __restrict__ sh,
                                                        const f32x4* __restrict__ res, const f32x4* __restrict__ rsc,
-                                                       const f32x4* __restrict__ rsh, f32x4* __restrict__ out,
-                                                       _Float16* __restrict__ osplit, int passes) {
+                                                       const f32x4* __restrict__ rsh, const _Float16* __restrict__ rsplit,
+                                                       f32x4* __restrict__ out, _Float16* __restrict__ osplit,
+                                                       int passes) {
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         const int c4 = (int)(i % C4);
@@ -99,6 +118,11 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
             const f32x4 r = res[i], ra = rsc[c4], rb = rsh[c4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn(r[e], ra[e]), rb[e]));
+        } else if constexpr (RES == 3) {
+            const long e0 = i * 4, off = 2 * e0 - (e0 & 31);
+            const h16x4 h = *(const h16x4*)(rsplit + off), l = *(const h16x4*)(rsplit + off + 32);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn((float)h[e], (float)l[e]));
         }
         if constexpr (RELU) {
 #pragma unroll
@@ -175,9 +199,16 @@ extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t 
     HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "hkp_bn_finalize: running stats pair");
     HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
                   "hkp_bn_finalize: tiles/tile_rows inconsistent with count");
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(c), dim3(256), 0, as_stream(stream), c, (long)count, (long)tiles,
-                       tile_rows, partials, gamma, beta, momentum, eps, running_mean, running_var,
-                       num_batches_tracked, scale_shift, mean_invstd);
+    const int cpb = partials_cpb(c);
+#define HKP_FIN(CPB)                                                                                              \
+    hipLaunchKernelGGL(bn_finalize_kernel<CPB>, dim3((c + CPB - 1) / CPB), dim3(256), 0, as_stream(stream), c,     \
+                       (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,    \
+                       running_var, num_batches_tracked, scale_shift, mean_invstd)
+    if (cpb == 8) HKP_FIN(8);
+    else if (cpb == 4) HKP_FIN(4);
+    else if (cpb == 2) HKP_FIN(2);
+    else HKP_FIN(1);
+#undef HKP_FIN
     HKP_LAUNCH_CHECK("hkp_bn_finalize");
     return HKP_OK;
 }
@@ -193,13 +224,15 @@ extern "C" int hkp_bn_eval_params(int32_t c, const float* gamma, const float* be
 }
 
 extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
-                            const float* res_scale_shift, int32_t relu, float* out, uint16_t* out_split,
-                            int32_t split_passes, hkp_stream_t stream) {
+                            const float* res_scale_shift, const uint16_t* res_split, int32_t relu, float* out,
+                            uint16_t* out_split, int32_t split_passes, hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_apply: need m>0 and c%%4==0 (c=%d)", c);
     HKP_CHECK_ARG(y && scale_shift && (out || out_split), "hkp_bn_apply: null tensor");
     HKP_CHECK_ARG(!out_split || ((split_passes == 1 || split_passes == 3) && c % 32 == 0),
                   "hkp_bn_apply: split output needs split_passes 1|3 and c%%32==0");
     HKP_CHECK_ARG(res_scale_shift == nullptr || res != nullptr, "hkp_bn_apply: res_scale_shift without res");
+    HKP_CHECK_ARG(res_split == nullptr || (res == nullptr && c % 32 == 0),
+                  "hkp_bn_apply: res_split excludes res and needs c%%32==0");
     const long n4 = m * (long)c / 4;
     const int C4 = c / 4;
     const f32x4 *Y = (const f32x4*)y, *SC = (const f32x4*)scale_shift, *SH = (const f32x4*)(scale_shift + c);
@@ -210,9 +243,11 @@ extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* s
     const int g = grid_for(n4);
     hipStream_t st = as_stream(stream);
 #define HKP_APPLY(RES, RL) \
-    hipLaunchKernelGGL((bn_apply_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, RSH, O, \
-                       (_Float16*)out_split, split_passes)
-    if (!res) {
+    hipLaunchKernelGGL((bn_apply_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, RSH, \
+                       (const _Float16*)res_split, O, (_Float16*)out_split, split_passes)
+    if (res_split) {
+        if (relu) HKP_APPLY(3, true); else HKP_APPLY(3, false);
+    } else if (!res) {
         if (relu) HKP_APPLY(0, true); else HKP_APPLY(0, false);
     } else if (!res_scale_shift) {
         if (relu) HKP_APPLY(1, true); else HKP_APPLY(1, false);

@@ -81,28 +81,34 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
 }
 
 // per channel: dgamma, dbeta, and the apply coefficients (grad_mean, k, invstd*gamma)
+template <int CPB>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
                                                              const float* __restrict__ mi, const float* gamma,
                                                              float* dgamma, float* dbeta, float* coef,
                                                              unsigned* amax_reset) {
-    __shared__ double red[2][4];
-    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (amax_reset && c == 0 && tid == 0) *amax_reset = 0u;
+    constexpr int TL = 256 / CPB;
+    __shared__ double red[4][8];
+    const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
+    const bool ok = c < C;
+    if (amax_reset && blockIdx.x == 0 && threadIdx.x == 0) *amax_reset = 0u;
     double s = 0.0, d = 0.0;
-    for (long t = tid; t < tiles; t += 256) {
-        s += (double)part[(t * C + c) * 2];
-        d += (double)part[(t * C + c) * 2 + 1];
-    }
-    s = wave_sum_d(s);
-    d = wave_sum_d(d);
-    if (lane == 0) {
-        red[0][wid] = s;
-        red[1][wid] = d;
-    }
-    __syncthreads();
-    if (tid == 0) {
-        const double S = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
-        const double D = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+    if (ok)   // 8 loads in flight per batch (latency-bound loop); zero-filled past the end
+        for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
+            float2 v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const long t = t0 + (long)j * TL;
+                v[j] = t < tiles ? *(const float2*)(part + (t * C + c) * 2) : make_float2(0.f, 0.f);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                s += (double)v[j].x;
+                d += (double)v[j].y;
+            }
+        }
+    const double S = lanes_sum_d<CPB>(s, red);
+    const double D = lanes_sum_d<CPB>(d, red);
+    if (tl == 0 && ok) {
         const double inv = (double)mi[C + c];
         const float gm = gamma ? gamma[c] : 1.f;
         if (dgamma) dgamma[c] = (float)(D * inv);
@@ -243,8 +249,15 @@ extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, 
                                    uint32_t* dy_amax_reset, hkp_stream_t stream) {
     HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(c), dim3(256), 0, as_stream(stream), c, (long)m, tiles, partials,
-                       mean_invstd, gamma, dgamma, dbeta, coef, (unsigned*)dy_amax_reset);
+    const int cpb = partials_cpb(c);
+#define HKP_BFIN(CPB)                                                                                             \
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<CPB>, dim3((c + CPB - 1) / CPB), dim3(256), 0, as_stream(stream), c, \
+                       (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, (unsigned*)dy_amax_reset)
+    if (cpb == 8) HKP_BFIN(8);
+    else if (cpb == 4) HKP_BFIN(4);
+    else if (cpb == 2) HKP_BFIN(2);
+    else HKP_BFIN(1);
+#undef HKP_BFIN
     HKP_LAUNCH_CHECK("hkp_bn_bwd_finalize");
     return HKP_OK;
 }

@@ -93,4 +93,21 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// Per-channel reductions over [tiles][C][2] partials: a block covers CPB
+// channels x (256/CPB) tile lanes, so the CPB channels of one tile row are one
+// contiguous load (8*CPB bytes) instead of CPB separate sectors; lane sums are
+// combined in a fixed order.  CPB chosen so that C/CPB blocks still fill the chip.
+static inline int partials_cpb(int C) { return C >= 1024 ? 8 : C >= 512 ? 4 : C >= 256 ? 2 : 1; }
+
+template <int CPB>
+__device__ __forceinline__ double lanes_sum_d(double v, double (*red)[8]) {
+#pragma unroll
+    for (int o = CPB; o < 64; o <<= 1) v += __shfl_xor(v, o);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, cl = threadIdx.x % CPB;
+    __syncthreads();
+    if (lane < CPB) red[wid][lane] = v;
+    __syncthreads();
+    return (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
 }  // namespace hkp

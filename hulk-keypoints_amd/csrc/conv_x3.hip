@@ -967,11 +967,12 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
            d->stride == 2 && d->pad == 3 && d->dilation == 1 && d->k % 64 == 0;
 }
 
-// Tile policy: 256x256 (32-channel stages, 2-stage ring, 48 MFMAs per wave per
-// barrier) when Cout % 256 == 0 and that still gives >= 4 rounds of blocks over
-// the 256 CUs; else 256x128 / 256x64 (32-channel stages, 3-stage ring).
-// Measured on C2 layer4 (Cout 512): 256x256 1.70 ms vs 256x128 1.82 ms; on layer3
-// (Cout 256, 600 blocks) 256x256 loses to round quantisation (0.53 vs 0.47 ms).
+// Tile policy (x3_tile_n): 256x256 (32-channel stages, 2-stage ring, 48 MFMAs
+// per wave per barrier), 256x128 or 256x64 (32-channel stages, 3-stage ring) by
+// rounds of blocks x tile cost.  Measured on C2 layer4 (Cout 512): 256x256 1.70 ms
+// vs 256x128 1.82 ms; on C2 layer3 (Cout 256, 600 m-tiles) 256x256 loses to round
+// quantisation (0.53 vs 0.47 ms); training layer3 (150 m-tiles) 256x256 wins
+// (0.15 vs 0.17 ms).
 // Tuning knob (hkp_set_conv_variant; results agree to fp32 summation order, in
 // practice bit-identical): 0 = policy, 1 = 256x128 32-ch stages only,
 // 2 = 256x128 16-ch stages (4-stage ring), 3 = 256x256 32-ch stages whenever
@@ -981,15 +982,34 @@ static int g_x3_variant = [] {
     return e ? atoi(e) : 0;
 }();
 
+// Tile width for Cout = k over m_tiles 256-row tiles: one 512-thread block per CU
+// at a time, so a launch costs ~ceil(blocks / 256) rounds of one tile each;
+// minimise rounds x tile cost, with the measured per-column cost of the tiles
+// (256x256: 0.9, 256x128: 1.0, 256x64: 1.25 — wider tiles reuse each A line more).
+// E.g. training layer3 (150 m-tiles, Cout 256): one round of 256x256 beats two of
+// 256x128; C2 layer3 (600 m-tiles) stays 256x128, C2 layer4 takes 256x256.
+static int x3_tile_n(int k, long m_tiles) {
+    int best = 64;
+    double best_cost = 1e300;
+    for (int bn : {256, 128, 64}) {
+        if (k % bn) continue;
+        const long rounds = (m_tiles * (k / bn) + 255) / 256;
+        const double cost = (double)rounds * bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
+        if (cost < best_cost - 1e-9) {
+            best_cost = cost;
+            best = bn;
+        }
+    }
+    return best;
+}
+
 static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a) {
     const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
-    int bn = (k % 128 == 0 && v != 5) ? 128 : 64, kh = 2;
-    if (k % 256 == 0 && (v == 3 || v == 4 || (v == 0 && m_tiles * (k / 256) >= 1024))) {
-        bn = 256;
-        kh = v == 4 ? 1 : 2;
-    } else if (bn == 128 && v == 2) {
-        kh = 1;
-    }
+    int bn = x3_tile_n(k, m_tiles), kh = 2;
+    if (v == 1 || v == 2) bn = k % 128 == 0 ? 128 : 64;
+    if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
+    if (v == 5) bn = 64;
+    if ((v == 4 && bn == 256) || (v == 2 && bn == 128)) kh = 1;
     a.n_tiles = k / bn;
     a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
     const dim3 grid((unsigned)(m_tiles * a.n_tiles));
@@ -1179,6 +1199,8 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
     return HKP_OK;
 }
+
+extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m) { return k > 0 && m > 0 ? x3_tile_n(k, (m + 255) / 256) : -1; }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
     HKP_CHECK_ARG(variant >= 0 && variant % 10 < 6 && variant < 20, "hkp_set_conv_variant: unknown variant %d",

@@ -45,7 +45,7 @@ SIGNATURES = {
     "hkp_conv2d_fwd": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
     "hkp_bn_finalize": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_eval_params": (ctypes.c_int, [_I32, _P, _P, _P, _P, _F, _P, _P, _P]),
-    "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _I32, _P]),
+    "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _I32, _P]),
     "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
@@ -58,6 +58,7 @@ SIGNATURES = {
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_set_conv_variant": (ctypes.c_int, [_I32]),
+    "hkp_x3_tile_n": (_I32, [_I32, _I64]),
     "hkp_upsample_argmax_ws_bytes": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_stem_pack_x3_elems": (_I64, [_CD]),
     "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),

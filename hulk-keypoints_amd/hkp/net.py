@@ -170,13 +170,20 @@ def _split_for(c):
 def stem_forward(resnet, x_nchw, trace=None):
     """conv1 → bn1 → relu → maxpool (src/resnet.py:199-202)."""
     y, ss, mi = conv_bn(resnet.conv1, resnet.bn1, x_nchw, layout="nchw")
-    out = ops.bn_relu_maxpool(y, ss, split=_split_for(y.shape[-1]), route=trace is not None)
+    sp = _split_for(y.shape[-1])
+    # inference: the stem output is only read by layer1's convs and (as the raw
+    # residual, hi + lo) its first block → split-only
+    out = ops.bn_relu_maxpool(y, ss, split=sp, route=trace is not None, keep_fp32=trace is not None or sp != 3)
     if trace is not None:
         trace.stem = dict(x=x_nchw, y=y, ss=ss, mi=mi, out=out)
     return out
 
 
-def block_forward(block, x, trace=None):
+def block_forward(block, x, trace=None, final=False):
+    """One BasicBlock / Bottleneck.  x: fp32 NHWC (with its split attached) or, in
+    inference, a split-only activation.  In inference the block output is written
+    split-only too unless `final` (the head reads fp32): the next block's convs
+    read the split and its residual add reads hi + lo."""
     rec = {} if trace is not None else None
     # producers also write the next conv's operand split; an activation only a
     # conv consumes (inside the block, no backward trace) is written split-only
@@ -203,13 +210,14 @@ def block_forward(block, x, trace=None):
         if rec is not None:
             rec.update(x=x, y=[y1, y2, y3], ss=[s1, s2, s3], mi=[m1, m2, m3], act=[a1, a2])
     pl = _split_for(last_y.shape[-1])
+    keep_out = keep or final or pl != 3
     if block.downsample is not None:
         yd, sd, md = conv_bn(block.downsample[0], block.downsample[1], x)
-        out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True, split=pl)
+        out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True, split=pl, keep_fp32=keep_out)
         if rec is not None:
             rec.update(yd=yd, sd=sd, md=md)
     else:
-        out = ops.bn_apply(last_y, last_s, res=x, relu=True, split=pl)
+        out = ops.bn_apply(last_y, last_s, res=x, relu=True, split=pl, keep_fp32=keep_out)
     if rec is not None:
         rec["out"] = out
         trace.blocks.append(rec)
@@ -222,9 +230,9 @@ def backbone_forward(resnet, x_nchw, trace=None):
         raise ValueError("expected [B,3,H,W] input, got %s" % (tuple(x_nchw.shape),))
     prepack_x3(resnet, flip=trace is not None)
     x = stem_forward(resnet, x_nchw.contiguous(), trace)
-    for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4):
-        for block in layer:
-            x = block_forward(block, x, trace)
+    blocks = [b for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4) for b in layer]
+    for i, block in enumerate(blocks):
+        x = block_forward(block, x, trace, final=i == len(blocks) - 1)
     return x
 
 

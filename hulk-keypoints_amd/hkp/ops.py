@@ -116,9 +116,9 @@ class PackedWeight(tuple):
 
 def x3_symbol(k, m):
     """Kernel symbol the x3 conv launches for Cout = k over m output pixels (the
-    default tile policy of conv_x3.hip's launch_x3)."""
-    bn = 256 if (k % 256 == 0 and ((m + 255) // 256) * (k // 256) >= 1024) else (128 if k % 128 == 0 else 64)
-    return "conv_x3_kernel<%d, 2, false>" % bn
+    default tile policy of conv_x3.hip's launch_x3, hkp_x3_tile_n)."""
+    from ._lib import lib
+    return "conv_x3_kernel<%d, 2, false>" % lib().hkp_x3_tile_n(k, m)
 
 
 def weight_pack_x3(w):
@@ -314,14 +314,23 @@ def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None, split=0, keep_fp
     """out = [relu](y*scale+shift [+ res | + res*rscale+rshift]).
     split = 1 or 3 also writes the next conv's operand (attached as out._hkp_split);
     keep_fp32=False (with split): the fp32 activation is not written and the split
-    tensor itself is returned (an activation only a conv consumes)."""
+    tensor itself is returned (an activation only a conv consumes).  res may be a
+    split-only activation (packed, split=3): the residual is then read as hi + lo."""
     _need(y, torch.float32, "bn_apply.y")
     c = y.shape[-1]
     m = y.numel() // c
     _check_split(split, c, "bn_apply")
     if ss.numel() != 2 * c:
         raise HkpError("bn_apply: scale_shift size %d != 2C" % ss.numel())
-    if res is not None:
+    res_sp = None
+    if res is not None and res.dtype == torch.float16:
+        if res_ss is not None or getattr(res, "_hkp_split_passes", 0) != 3:
+            raise HkpError("bn_apply: a split residual must be a packed (split=3) raw residual")
+        _need(res, torch.float16, "bn_apply.res_split")
+        if tuple(res.shape[:-1]) != tuple(y.shape[:-1]) or res.shape[-1] != 2 * c:
+            raise HkpError("bn_apply: split residual shape %s vs %s" % (tuple(res.shape), tuple(y.shape)))
+        res, res_sp = None, res
+    elif res is not None:
         _need(res, torch.float32, "bn_apply.res")
         if res.shape != y.shape:
             raise HkpError("bn_apply: residual shape %s != %s" % (tuple(res.shape), tuple(y.shape)))
@@ -329,8 +338,8 @@ def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None, split=0, keep_fp
         raise HkpError("bn_apply: keep_fp32=False needs a split output")
     o = None if not keep_fp32 else (out if out is not None else torch.empty_like(y))
     sp = _split_out(y.shape, y.device, split) if split else None
-    call("hkp_bn_apply", m, c, _ptr(y), _ptr(ss), _ptr(res), _ptr(res_ss), int(bool(relu)), _ptr(o), _ptr(sp),
-         int(split), _stream())
+    call("hkp_bn_apply", m, c, _ptr(y), _ptr(ss), _ptr(res), _ptr(res_ss), _ptr(res_sp), int(bool(relu)), _ptr(o),
+         _ptr(sp), int(split), _stream())
     if o is None:
         return sp
     if split:
@@ -338,17 +347,23 @@ def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None, split=0, keep_fp
     return o
 
 
-def bn_relu_maxpool(y, ss, split=0, route=False):
+def bn_relu_maxpool(y, ss, split=0, route=False, keep_fp32=True):
     """maxpool3x3/s2/p1(relu(y*scale+shift)); route=True (training) also records
-    each window's gradient tap as out._hkp_route (uint8, out's shape) for maxpool_bwd."""
+    each window's gradient tap as out._hkp_route (uint8, out's shape) for maxpool_bwd.
+    keep_fp32=False (with split): only the split is written and returned."""
     _need(y, torch.float32, "bn_relu_maxpool.y", 4)
     n, h, w, c = y.shape
     _check_split(split, c, "bn_relu_maxpool")
-    out = torch.empty((n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c), device=y.device, dtype=torch.float32)
-    sp = _split_out(out.shape, y.device, split) if split else None
-    rt = torch.empty(out.shape, device=y.device, dtype=torch.uint8) if route else None
+    if not keep_fp32 and (not split or route):
+        raise HkpError("bn_relu_maxpool: keep_fp32=False needs a split output and no route")
+    shape = (n, (h - 1) // 2 + 1, (w - 1) // 2 + 1, c)
+    out = torch.empty(shape, device=y.device, dtype=torch.float32) if keep_fp32 else None
+    sp = _split_out(shape, y.device, split) if split else None
+    rt = torch.empty(shape, device=y.device, dtype=torch.uint8) if route else None
     call("hkp_bn_relu_maxpool", n, h, w, c, _ptr(y), _ptr(ss), _ptr(out), _ptr(sp), int(split), _ptr(rt),
          _stream())
+    if out is None:
+        return sp
     if split:
         out._hkp_split = (sp, split)
     if route:

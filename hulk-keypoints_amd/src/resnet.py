@@ -85,7 +85,7 @@ class BasicBlock(nn.Module):
 
     def forward(self, x_nhwc):
         """Operates on NHWC activations (the framework's internal layout)."""
-        return net.block_forward(self, x_nhwc)
+        return net.block_forward(self, x_nhwc, final=True)
 
 
 class Bottleneck(nn.Module):
@@ -105,7 +105,7 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x_nhwc):
-        return net.block_forward(self, x_nhwc)
+        return net.block_forward(self, x_nhwc, final=True)
 
 
 class ResNet(nn.Module):

@@ -102,10 +102,13 @@ int hkp_weight_pack_x3(int32_t k, int32_t rsc, int32_t c, const float* w, uint16
                        hkp_stream_t stream);
 int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
                       const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream);
-/* Tuning knob for the x3 conv's tile choice (0 = policy: 256x256 when Cout % 256
- * == 0 and the grid is >= 4 rounds of blocks, else 256x128 / 256x64; 1 = 256x128
- * only; 2 = 256x128 with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel
- * stages whenever Cout % 256 == 0; 5 = 256x64).  Outputs agree to fp32 summation order. */
+/* Tile width (256, 128 or 64 output channels per 256-pixel tile) the x3 conv
+ * uses for Cout = k over m output pixels: fewest rounds of blocks over the 256
+ * CUs weighted by the measured per-column cost of each tile (-1 on bad args).
+ * Tuning knob for the choice (0 = that policy; 1 = 256x128 only; 2 = 256x128
+ * with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel stages whenever
+ * Cout % 256 == 0; 5 = 256x64).  Outputs agree to fp32 summation order. */
+int32_t hkp_x3_tile_n(int32_t k, int64_t m);
 int hkp_set_conv_variant(int32_t variant);
 
 /* ----------------------------------------------------------- batchnorm ---- */
@@ -128,7 +131,10 @@ int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const f
 /* out = [relu]( y*scale + shift  [+ res | + res*rscale + rshift] ), NHWC [m][c].
  * Replaces the bn→relu / bn→(+residual)→relu tails of BasicBlock
  * (src/resnet.py:57-67) and Bottleneck (:96-110). res may be NULL;
- * res_scale_shift NULL means the residual is added raw.
+ * res_scale_shift NULL means the residual is added raw.  res_split (instead of res;
+ * c % 32 == 0): the raw residual read from its packed split, hi + lo (the block
+ * input a producer wrote split-only: inference keeps the residual stream as an
+ * fp16 pair with a 22-bit significand instead of fp32).
  * out_split (nullable; needs c % 32 == 0): the same values also written as the
  * next conv's operand — split_passes = 1: fp16 plane [m][c] for
  * hkp_conv2d_fwd_split (passes 1); split_passes = 3: the packed split layout
@@ -136,8 +142,8 @@ int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const f
  * hkp_conv2d_fwd_x3.  out may be NULL when out_split is given (an activation
  * only a conv consumes).  hkp_bn_relu_maxpool takes the same optional split. */
 int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
-                 const float* res_scale_shift, int32_t relu, float* out, uint16_t* out_split,
-                 int32_t split_passes, hkp_stream_t stream);
+                 const float* res_scale_shift, const uint16_t* res_split, int32_t relu, float* out,
+                 uint16_t* out_split, int32_t split_passes, hkp_stream_t stream);
 
 /* Stem tail: maxpool3x3/s2/p1( relu( y*scale + shift ) ), NHWC
  * (src/resnet.py:139-141, 200-202). Output [n, (h-1)/2+1, (w-1)/2+1, c].

@@ -94,6 +94,25 @@ def test_producer_split_layouts(cuda_device):
     assert _pow2(fp.inv_scale) and torch.equal(fh, wf.half()) and torch.equal(fl, (wf - wf.half().float()).half())
 
 
+def test_split_residual_and_splitonly_maxpool(cuda_device):
+    """bn_apply with a split-only (packed) residual adds exactly hi + lo; the
+    split-only maxpool writes the same split as the fp32 one."""
+    from hkp import ops
+    y = rand(2, 9, 11, 96, seed=21).to(cuda_device)
+    ss = torch.cat([rand(96, seed=22) * 0.5 + 1, rand(96, seed=23) * 0.1]).to(cuda_device)
+    x = ops.bn_apply(rand(2, 9, 11, 96, seed=24).to(cuda_device), ss, relu=True, split=3, keep_fp32=False)
+    hi, lo = _unpack_x3(x)
+    got = ops.bn_apply(y, ss, res=x, relu=True, split=3)
+    ref = ops.bn_apply(y, ss, res=(hi.float() + lo.float()).contiguous(), relu=True, split=3)
+    assert torch.equal(got, ref) and torch.equal(ops.split_of(got)[0], ops.split_of(ref)[0])
+    only = ops.bn_apply(y, ss, res=x, relu=True, split=3, keep_fp32=False)
+    assert torch.equal(only, ops.split_of(ref)[0])
+    yp = rand(2, 31, 41, 64, seed=25).to(cuda_device)
+    full = ops.bn_relu_maxpool(yp, ss[:64].repeat(2), split=3)
+    sp = ops.bn_relu_maxpool(yp, ss[:64].repeat(2), split=3, keep_fp32=False)
+    assert sp.dtype == torch.float16 and torch.equal(sp, ops.split_of(full)[0])
+
+
 def test_weight_pack_batch_bitexact(cuda_device):
     """hkp_weight_pack_x3_batch == the per-conv packs, bit for bit: 1x1 and 3x3,
     (tap, k) row counts off the 256-row tile, K = 2048 (many column partials),
