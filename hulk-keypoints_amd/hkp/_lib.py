@@ -30,6 +30,12 @@ class PackJob(ctypes.Structure):
                 ("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("rs", ctypes.c_int32), ("c", ctypes.c_int32)]
 
 
+class AdamTensor(ctypes.Structure):
+    """hkp_adam_tensor (hkp_adam_step)."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("n", ctypes.c_int64)]
+
+
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
@@ -73,6 +79,7 @@ SIGNATURES = {
     "hkp_conv2d_bwd_filter_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_bwd_filter_split_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
+    "hkp_adam_step": (ctypes.c_int, [_I32, ctypes.POINTER(AdamTensor), _F, _F, _F, _F, _F, _F, _F, _P]),
     # backward
     "hkp_conv_weight_flip":(ctypes.c_int, [_CD, _P, _P, _P]),
     "hkp_conv2d_bwd_data": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),

@@ -3,8 +3,9 @@
 Trainer.step = forward (kernel walk, Trace kept) → fused fp64 loss kernel
 (dL/dheat) → backward kernels (net.keypoints_backward) → [RCCL all-reduce of
 gradients, bucketed and overlapped with the rest of backward] → Adam
-(lr 1e-4, weight_decay 1e-4, train.py:79; the optimizer stays PyTorch as the
-north star asks).
+(lr 1e-4, weight_decay 1e-4, train.py:79): the optimizer loop stays a PyTorch
+optimizer object as the north star asks; its update is either hkp.optim.FusedAdam
+(default: one HIP pass over all parameters) or torch.optim.Adam.
 
 Data parallelism: one process per GPU (torchrun), torch.distributed backend
 "nccl" = RCCL over xGMI.  Gradients land in flat per-bucket buffers in the
@@ -17,6 +18,7 @@ import torch
 import torch.distributed as dist
 
 from . import net, ops
+from .optim import FusedAdam
 
 
 class GradBucketer:
@@ -78,12 +80,15 @@ class Trainer:
     """One optimizer step per call, reference semantics (train.py:33-36)."""
 
     def __init__(self, model, lr=1e-4, weight_decay=1e-4, loss="bce", sigma=8.0, distributed=False,
-                 bucket_mb=32):
+                 bucket_mb=32, optimizer="fused"):
         self.model = model
         self.params = list(model.parameters())
         self.loss_kind = loss
         self.sigma = sigma
-        self.opt = torch.optim.Adam(self.params, lr=lr, weight_decay=weight_decay)
+        if optimizer not in ("fused", "torch"):
+            raise ValueError("optimizer must be 'fused' or 'torch'")
+        opt_cls = FusedAdam if optimizer == "fused" else torch.optim.Adam
+        self.opt = opt_cls(self.params, lr=lr, weight_decay=weight_decay)
         use_dp = distributed and dist.is_initialized() and dist.get_world_size() > 1
         self.bucketer = GradBucketer(self.params, bucket_mb << 20) if use_dp else None
 

@@ -294,6 +294,26 @@ int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask
                      const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
                      hkp_stream_t stream);
 
+/* ----------------------------------------------------------- optimizer ---- */
+/* Fused multi-tensor Adam with L2 weight decay (replaces the
+ * optim.Adam(lr, weight_decay) step of train.py:36,79 — torch/optim/adam.py's
+ * multi-tensor path, amsgrad/maximize off): for every element of every tensor
+ *   g = g + wd*p;  m = m + (1-b1)*(g-m);  v = v*b2 + (1-b2)*g*g;
+ *   p = p + neg_step_size * m / (sqrt(v)/bias_correction2_sqrt + eps)
+ * with one_minus_beta1/2 = 1-b1, 1-b2, neg_step_size = -lr/(1-b1^step) and
+ * bias_correction2_sqrt = sqrt(1-b2^step) computed by the caller in double (as
+ * torch does with its Python-float scalars).  p, m, v updated in place; g read only. */
+typedef struct hkp_adam_tensor {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t n;
+} hkp_adam_tensor;
+int hkp_adam_step(int32_t ntensors, const hkp_adam_tensor* tensors, float beta2, float one_minus_beta1,
+                  float one_minus_beta2, float eps, float weight_decay, float neg_step_size,
+                  float bias_correction2_sqrt, hkp_stream_t stream);
+
 /* Stem: backward of maxpool3x3/s2/p1(relu(y*scale+shift)) → dz = dL/d(BN output)
  * [n,h,w,c], ReLU mask applied (src/resnet.py:200-202; ATen's first-max window
  * rule): each window's dpool goes to the tap the forward recorded in `route`

@@ -91,3 +91,29 @@ def test_weight_pack_batch_host_side():
     with pytest.raises(_lib.HkpError, match="c%64==0"):
         _lib.call("hkp_weight_pack_x3_batch", 3, jobs, None, 0, None)
     assert _lib.call("hkp_weight_pack_x3_batch", 0, jobs, None, 0, None) == 0
+
+
+def test_adam_abi_host_side():
+    """hkp_adam_tensor layout and argument checks (host only, no launch)."""
+    from hkp import _lib
+    assert ctypes.sizeof(_lib.AdamTensor) == 40
+    ts = (_lib.AdamTensor * 2)()
+    ts[0].param, ts[0].grad, ts[0].exp_avg, ts[0].exp_avg_sq, ts[0].n = 16, 16, 16, 16, 8
+    ts[1].n = 8                                        # null pointers with n > 0
+    with pytest.raises(_lib.HkpError, match="null pointer"):
+        _lib.call("hkp_adam_step", 2, ts, 0.999, 0.1, 0.001, 1e-8, 0.0, -1e-3, 1.0, None)
+    with pytest.raises(_lib.HkpError, match="bias_correction2_sqrt"):
+        _lib.call("hkp_adam_step", 1, ts, 0.999, 0.1, 0.001, 1e-8, 0.0, -1e-3, 0.0, None)
+    assert _lib.call("hkp_adam_step", 0, ts, 0.999, 0.1, 0.001, 1e-8, 0.0, -1e-3, 1.0, None) == 0
+
+
+def test_fused_adam_rejects_unsupported_options():
+    from hkp.optim import FusedAdam
+    from hkp._lib import HkpError
+    p = [torch.nn.Parameter(torch.zeros(4))]
+    with pytest.raises(HkpError):
+        FusedAdam(p, amsgrad=True)
+    opt = FusedAdam(p, lr=1e-4, weight_decay=1e-4)
+    p[0].grad = torch.zeros(4)
+    with pytest.raises(HkpError, match="CUDA"):       # no CPU path
+        opt.step()

@@ -195,10 +195,12 @@ def _model(bb, k, wseed, dev):
     return m.to(dev)
 
 
+@pytest.mark.parametrize("optimizer", ["torch", "fused"])
 @pytest.mark.parametrize("case", ["train_r18_k2_64x80", "train_r34_k4_48x64"])
-def test_train_step_matches_reference_golden(cuda_device, golden, case):
+def test_train_step_matches_reference_golden(cuda_device, golden, case, optimizer):
     """Reference idiom (train.py:33-36) end to end on the GPU path: heatmaps →
-    .double() → nn.BCELoss → backward → Adam(lr 1e-4, wd 1e-4), two iterations."""
+    .double() → nn.BCELoss → backward → Adam(lr 1e-4, wd 1e-4), two iterations
+    (torch.optim.Adam, and hkp.optim.FusedAdam in its place)."""
     g = golden(case)
     bb, k = str(g["backbone"]), int(g["k"])
     m = _model(bb, k, int(g["wseed"]), cuda_device)
@@ -206,7 +208,8 @@ def test_train_step_matches_reference_golden(cuda_device, golden, case):
     uv = torch.from_numpy(g["uv"]).to(cuda_device)
     from hkp import ops
     gt = ops.gauss_target(uv, x.shape[2], x.shape[3], 8)
-    opt = torch.optim.Adam(m.parameters(), lr=1.0e-4, weight_decay=1.0e-4)
+    from hkp.optim import FusedAdam
+    opt = (torch.optim.Adam if optimizer == "torch" else FusedAdam)(m.parameters(), lr=1.0e-4, weight_decay=1.0e-4)
     names = list(g["param_names"])
     params = dict(m.named_parameters())
     # Tolerances follow the problem's own conditioning, measured on the CPU
@@ -248,6 +251,50 @@ def test_train_step_matches_reference_golden(cuda_device, golden, case):
     rc = [sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith(sfx))
           for sfx in ("running_mean", "running_var")]
     np.testing.assert_allclose(rc, g["running_checksum"][:2], rtol=1e-4 if tight else 1e-3)
+
+
+def test_fused_adam_matches_torch_adam(cuda_device):
+    """hkp_adam_step == torch.optim.Adam (multi-tensor, L2 wd) to fp32 rounding over
+    several steps: vector and scalar (odd length / misaligned view) tensors, a
+    zero-gradient block (wd still moves it), state_dict round trip both ways."""
+    from hkp.optim import FusedAdam
+    gen = torch.Generator().manual_seed(5)
+    shapes = [(64, 3, 3, 64), (1000, 512), (1000,), (37,), (4097,), (64,)]
+    base = [torch.randn(*s, generator=gen) for s in shapes]
+    big = torch.randn(4099, generator=gen)
+    p1 = [b.clone().to(cuda_device).requires_grad_(True) for b in base] + \
+        [big.to(cuda_device)[1:].clone().requires_grad_(True)]
+    p2 = [b.clone().to(cuda_device).requires_grad_(True) for b in base]
+    # misaligned (non-16-B) data pointer: a view starting one float in
+    store = big.clone().to(cuda_device)
+    p2.append(torch.nn.Parameter(store[1:]))
+    o1 = torch.optim.Adam(p1, lr=1e-3, weight_decay=1e-4, foreach=True)
+    o2 = FusedAdam(p2, lr=1e-3, weight_decay=1e-4)
+    for step in range(4):
+        for a, b in zip(p1, p2):
+            g = torch.randn(a.shape, generator=gen).to(cuda_device) * (10.0 ** (step - 3))
+            if a.shape == (1000, 512):
+                g[4:] = 0.0
+            a.grad, b.grad = g.clone(), g.clone()
+        o1.step()
+        v0 = [b._version for b in p2]
+        o2.step()
+        assert all(b._version > v for b, v in zip(p2, v0))   # in-place update is visible
+        # fp32 rounding of each quantity's own scale (elements produced by a
+        # cancellation, e.g. m = lerp(m, g) with g ~ m, differ relatively more)
+        def close(x, y):
+            torch.testing.assert_close(x, y, rtol=2e-6, atol=2e-7 * float(y.abs().max()))
+        for a, b in zip(p1, p2):
+            close(b, a)
+            s1, s2 = o1.state[a], o2.state[b]
+            close(s2["exp_avg"], s1["exp_avg"])
+            close(s2["exp_avg_sq"], s1["exp_avg_sq"])
+            assert float(s2["step"]) == float(s1["step"])
+    sd = o2.state_dict()
+    assert set(sd["state"][0]) == set(o1.state_dict()["state"][0])
+    o3 = torch.optim.Adam(p2, lr=1e-3, weight_decay=1e-4)
+    o3.load_state_dict(sd)                       # FusedAdam state → torch Adam, and back
+    FusedAdam(p2, lr=1e-3, weight_decay=1e-4).load_state_dict(o3.state_dict())
 
 
 def test_trainer_fused_loss_equals_autograd_path(cuda_device):
