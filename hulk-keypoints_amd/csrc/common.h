@@ -43,8 +43,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// f16x3 operand planes: hi = f16(x), lo = f16((x - hi) * 2^11)
-constexpr float SPLIT_LO_SCALE = 2048.f;
 typedef _Float16 h16x4 __attribute__((ext_vector_type(4)));
 
 // Operand split of 4 consecutive channels (element index e4*4, C % 32 == 0) for
@@ -68,8 +66,8 @@ __device__ __forceinline__ void store_split4(const f32x4& v, long e4, _Float16* 
     }
 }
 
-// 2^e with e chosen so that amax * 2^e lands in [2^13, 2^14): exact scaling
-// that keeps both hi and the 2^11-scaled lo of the split inside fp16's range
+// 2^e with e chosen so that amax * 2^e lands in [2^13, 2^14): exact scaling that
+// keeps hi inside fp16's range and the (unscaled) lo of large elements normal
 __device__ __forceinline__ float pow2_scale_for(const unsigned* amax_bits) {
     if (amax_bits == nullptr) return 1.f;
     const float m = __uint_as_float(*amax_bits);

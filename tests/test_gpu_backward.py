@@ -283,7 +283,7 @@ def test_fused_adam_matches_torch_adam(cuda_device):
         # fp32 rounding of each quantity's own scale (elements produced by a
         # cancellation, e.g. m = lerp(m, g) with g ~ m, differ relatively more)
         def close(x, y):
-            torch.testing.assert_close(x, y, rtol=2e-6, atol=2e-7 * float(y.abs().max()))
+            torch.testing.assert_close(x, y, rtol=2e-6, atol=2e-7 * float(y.detach().abs().max()))
         for a, b in zip(p1, p2):
             close(b, a)
             s1, s2 = o1.state[a], o2.state[b]
