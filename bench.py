@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--precision", choices=["fp32", "f16x3", "f16"], default=None,
                     help="NHWC conv arithmetic (default: f16x3 = fp32-accurate split fp16 MFMA)")
+    ap.add_argument("--input", choices=["f32", "u8"], default="f32",
+                    help="f32: the reference's ToTensor NCHW tensor; u8: the cv2.imread-style uint8 HWC batch "
+                         "(ToTensor fused into the stem, SURVEY 8(f1))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
     return ap.parse_args()
@@ -168,7 +171,7 @@ def main():
     torch.manual_seed(1234 + rank)
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False).to(dev)
     imgs = recipe.seeded_images_u8(B, H, W, 1234 + rank)
-    x = recipe.to_tensor_nchw(imgs).to(dev)
+    x = recipe.to_tensor_nchw(imgs).to(dev) if args.input == "f32" else torch.from_numpy(imgs).to(dev)
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99 + rank)).to(dev)
 
     if args.mode == "infer":
@@ -239,7 +242,8 @@ def main():
             "train-mode BN, fused K-ch head, heatmap + argmax" if args.mode == "infer"
             else "BCE fp64, Adam lr1e-4 wd1e-4"),
             "mode": args.mode, "backbone": args.backbone, "keypoints": K, "height": H, "width": W,
-            "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world},
+            "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,
+            "input": "fp32 NCHW (ToTensor)" if args.input == "f32" else "uint8 HWC BGR (ToTensor fused into the stem)"},
         "roofline": {"bound": "mfma", "kernel": dom_sym, "achieved": achieved, "peak": peak,
                      "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
                      "fp32_equivalent_tflops": alg, "frac_of_fp32_mfma_peak": alg / PEAK_FP32_MFMA_TFLOPS,

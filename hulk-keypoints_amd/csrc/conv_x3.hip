@@ -917,10 +917,13 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, in
     *mps = (int)m;
 }
 
-// Stem operand: NCHW fp32 image → zero-padded NHWC4 planes [2][N][Hp][Wp][4]
-// (hi, then lo = f16(x-hi)); padded pixel (hp, wp) = input (hp-3, wp-3)
+// Stem operand: the image → zero-padded NHWC4 planes [2][N][Hp][Wp][4] (hi, then
+// lo = f16(x-hi)); padded pixel (hp, wp) = input (hp-3, wp-3).  U8: the image is
+// the uint8 HWC batch cv2.imread gives ([N][H][W][C], BGR) and x = u8 / 255 in
+// fp32 — ToTensor (dataset.py:16) fused into the stem's operand pack.
+template <bool U8>
 __global__ __launch_bounds__(256) void stem_pack_x3_kernel(int N, int C, int H, int W, int Hp, int Wp,
-                                                          const float* __restrict__ x, _Float16* __restrict__ out) {
+                                                          const void* __restrict__ src, _Float16* __restrict__ out) {
     const long total = (long)N * Hp * Wp;
     const long plane = total * 4;
     const long stride = (long)gridDim.x * blockDim.x;
@@ -933,7 +936,16 @@ __global__ __launch_bounds__(256) void stem_pack_x3_kernel(int N, int C, int H, 
         const bool in = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
         f32x4 v;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (in && c < C) ? x[(((long)n * C + c) * H + h) * W + w] : 0.f;
+        for (int c = 0; c < 4; ++c) {
+            if (!(in && c < C)) {
+                v[c] = 0.f;
+            } else if constexpr (U8) {
+                const uint8_t u = ((const uint8_t*)src)[(((long)n * H + h) * W + w) * C + c];
+                v[c] = __fdiv_rn((float)u, 255.f);
+            } else {
+                v[c] = ((const float*)src)[(((long)n * C + c) * H + h) * W + w];
+            }
+        }
         h16x4 hv, lv;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
@@ -1153,19 +1165,33 @@ extern "C" int64_t hkp_stem_pack_x3_elems(const hkp_conv_desc* d) {
     return 2L * d->n * (2L * ho + 6) * (2L * wo + 6) * 4;
 }
 
-extern "C" int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uint16_t* x_split, hkp_stream_t stream) {
+static int stem_pack(const hkp_conv_desc* d, const void* src, bool u8, uint16_t* x_split, hkp_stream_t stream,
+                     const char* who) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
-    HKP_CHECK_ARG(stem_x3_shape(d), "hkp_stem_pack_x3: needs the 7x7/s2/p3 NCHW stem with C<=4, Cout%%64==0");
-    HKP_CHECK_ARG(x_nchw && x_split, "hkp_stem_pack_x3: null tensor");
+    HKP_CHECK_ARG(stem_x3_shape(d), "%s: needs the 7x7/s2/p3 NCHW stem with C<=4, Cout%%64==0", who);
+    HKP_CHECK_ARG(src && x_split, "%s: null tensor", who);
     const int hp = 2 * ho + 6, wp = 2 * wo + 6;
     long g = ((long)d->n * hp * wp + 255) / 256;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(stem_pack_x3_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), d->n, d->c, d->h,
-                       d->w, hp, wp, x_nchw, (_Float16*)x_split);
-    HKP_LAUNCH_CHECK("hkp_stem_pack_x3");
+    if (u8)
+        hipLaunchKernelGGL(stem_pack_x3_kernel<true>, dim3((unsigned)g), dim3(256), 0, as_stream(stream), d->n, d->c,
+                           d->h, d->w, hp, wp, src, (_Float16*)x_split);
+    else
+        hipLaunchKernelGGL(stem_pack_x3_kernel<false>, dim3((unsigned)g), dim3(256), 0, as_stream(stream), d->n, d->c,
+                           d->h, d->w, hp, wp, src, (_Float16*)x_split);
+    HKP_LAUNCH_CHECK(who);
     return HKP_OK;
+}
+
+extern "C" int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uint16_t* x_split, hkp_stream_t stream) {
+    return stem_pack(d, x_nchw, false, x_split, stream, "hkp_stem_pack_x3");
+}
+
+extern "C" int hkp_stem_pack_x3_u8(const hkp_conv_desc* d, const uint8_t* img_nhwc, uint16_t* x_split,
+                                   hkp_stream_t stream) {
+    return stem_pack(d, img_nhwc, true, x_split, stream, "hkp_stem_pack_x3_u8");
 }
 
 extern "C" int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split,

@@ -68,6 +68,9 @@ SIGNATURES = {
     "hkp_upsample_argmax_ws_bytes": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_stem_pack_x3_elems": (_I64, [_CD]),
     "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
+    "hkp_stem_pack_x3_u8": (ctypes.c_int, [_CD, _P, _P, _P]),
+    "hkp_images_u8_to_nchw": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P]),
+    "hkp_heat_overlay": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "hkp_stem_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),

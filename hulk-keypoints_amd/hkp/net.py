@@ -144,7 +144,7 @@ def conv_bn(conv, bn, x, layout="nhwc"):
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
-    if layout == "nchw" and passes == 3 and ops.stem_x3_ok(tuple(x.shape), tuple(conv.weight.shape), st, pd, dl):
+    if layout == "nchw" and passes == 3 and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd, dl):
         y, part = ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
                                          stats=bn.training)
     elif layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
@@ -159,6 +159,33 @@ def conv_bn(conv, bn, x, layout="nhwc"):
     count = y.numel() // y.shape[-1]
     ss, mi = _bn_params(bn, part, count)
     return y, ss, mi
+
+
+def image_nchw_shape(x):
+    """[B,C,H,W] of an input batch: fp32 NCHW (ToTensor) or uint8 NHWC (cv2.imread)."""
+    if x.dtype == torch.uint8:
+        return (x.shape[0], x.shape[3], x.shape[1], x.shape[2])
+    return tuple(x.shape)
+
+
+def _image_input(resnet, x, trace):
+    """The stem's input: uint8 NHWC batches go straight into the f16x3 stem pack
+    (ToTensor fused); the fp32 NCHW image is materialised on the
+    device only where something needs it (training: the stem wgrad; other
+    precisions)."""
+    if x.dim() != 4:
+        raise ValueError("expected a [B,3,H,W] fp32 or [B,H,W,3] uint8 batch, got %s" % (tuple(x.shape),))
+    if x.dtype != torch.uint8:
+        if x.shape[1] != 3:
+            raise ValueError("expected [B,3,H,W] input, got %s" % (tuple(x.shape),))
+        return x.contiguous()
+    if x.shape[3] != 3:
+        raise ValueError("expected a [B,H,W,3] uint8 batch, got %s" % (tuple(x.shape),))
+    x = x.contiguous()
+    c1 = resnet.conv1
+    direct = trace is None and PRECISIONS[_precision] == 3 and ops.stem_x3_ok(
+        image_nchw_shape(x), tuple(c1.weight.shape), _i(c1.stride), _i(c1.padding), _i(c1.dilation))
+    return x if direct else ops.images_u8_to_nchw(x)
 
 
 def _split_for(c):
@@ -225,11 +252,11 @@ def block_forward(block, x, trace=None, final=False):
 
 
 def backbone_forward(resnet, x_nchw, trace=None):
-    """ResNet.forward up to the fc (src/resnet.py:198-213), NHWC output."""
-    if x_nchw.dim() != 4 or x_nchw.shape[1] != 3:
-        raise ValueError("expected [B,3,H,W] input, got %s" % (tuple(x_nchw.shape),))
+    """ResNet.forward up to the fc (src/resnet.py:198-213), NHWC output.  x_nchw:
+    the [B,3,H,W] fp32 image or the [B,H,W,3] uint8 batch (see _image_input)."""
+    x_in = _image_input(resnet, x_nchw, trace)
     prepack_x3(resnet, flip=trace is not None)
-    x = stem_forward(resnet, x_nchw.contiguous(), trace)
+    x = stem_forward(resnet, x_in, trace)
     blocks = [b for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4) for b in layer]
     for i, block in enumerate(blocks):
         x = block_forward(block, x, trace, final=i == len(blocks) - 1)
@@ -247,9 +274,10 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
     feat = backbone_forward(resnet, x_nchw, trace)
     w, b = fc_rows(resnet, k)
     low = ops.head_fc(feat, w, b)
-    hm, yx = ops.upsample_sigmoid(low, x_nchw.shape[2], x_nchw.shape[3], heat=heat, argmax=argmax)
+    H, W = image_nchw_shape(x_nchw)[2:]
+    hm, yx = ops.upsample_sigmoid(low, H, W, heat=heat, argmax=argmax)
     if trace is not None:
-        trace.head = dict(feat=feat, low=low, heat=hm, k=k, H=x_nchw.shape[2], W=x_nchw.shape[3])
+        trace.head = dict(feat=feat, low=low, heat=hm, k=k, H=H, W=W)
     return hm, yx, low
 
 
@@ -376,6 +404,6 @@ def logits_forward(resnet, x_nchw, num_outputs=None):
     for c0 in range(0, n_out, 16):
         c1 = min(n_out, c0 + 16)
         low = ops.head_fc(feat, W2[c0:c1].contiguous(), resnet.fc.bias[c0:c1].contiguous())
-        up, _ = ops.upsample_sigmoid(low, x_nchw.shape[2], x_nchw.shape[3], heat=True, argmax=False, sigmoid=False)
+        up, _ = ops.upsample_sigmoid(low, *image_nchw_shape(x_nchw)[2:], heat=True, argmax=False, sigmoid=False)
         outs.append(up)
     return torch.cat(outs, 1)

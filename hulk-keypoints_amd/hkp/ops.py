@@ -197,16 +197,22 @@ def stem_weight_pack_x3(w):
 
 
 def conv2d_fwd_stem_x3(x, wp, k, stats=True):
-    """f16x3 stem conv (7x7/s2/p3) of an NCHW fp32 image → NHWC fp32 y (+ BN partials)."""
+    """f16x3 stem conv (7x7/s2/p3) → NHWC fp32 y (+ BN partials).  x: the NCHW fp32
+    image, or the uint8 NHWC (BGR) batch cv2.imread gives — ToTensor's /255 is then
+    fused into the stem's operand pack."""
     from ._lib import lib
     ws, wsc = wp
-    _need(x, torch.float32, "conv2d_fwd_stem_x3.x", 4)
+    u8 = x.dtype == torch.uint8
+    _need(x, torch.uint8 if u8 else torch.float32, "conv2d_fwd_stem_x3.x", 4)
     _need(ws, torch.float16, "conv2d_fwd_stem_x3.w_split", 3)
-    n, c, h, wd = x.shape
+    if u8:
+        n, h, wd, c = x.shape
+    else:
+        n, c, h, wd = x.shape
     d = ConvDesc(n, h, wd, c, k, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW)
     ho, wo = conv_out_hw(h, wd, 7, 7, 2, 3, 1)
     xs = torch.empty(lib().hkp_stem_pack_x3_elems(ctypes.byref(d)), device=x.device, dtype=torch.float16)
-    call("hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())
+    call("hkp_stem_pack_x3_u8" if u8 else "hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())
     y = torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
     part = None
     if stats:
@@ -223,6 +229,35 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True):
         _observer("conv_x3_kernel<64, 2, true>", 2.0 * n * ho * wo * k * 49 * c, 2.0 * (xs.numel() + ws.numel()) +
                   4.0 * y.numel(), launch)
     return y, part
+
+
+def images_u8_to_nchw(img):
+    """ToTensor on the device: uint8 [B,H,W,C] (BGR, cv2.imread) → fp32 [B,C,H,W] / 255."""
+    _need(img, torch.uint8, "images_u8_to_nchw.img", 4)
+    n, h, w, c = img.shape
+    x = torch.empty((n, c, h, w), device=img.device, dtype=torch.float32)
+    call("hkp_images_u8_to_nchw", n, h, w, c, _ptr(img), _ptr(x), _stream())
+    return x
+
+
+def heat_overlay(heat, img, yx):
+    """Prediction.plot's picture on the GPU: heat [B,K,H,W] fp32,
+    img uint8 [B,H,W,3] BGR, yx int32 [B,K,2] argmax → uint8 [B, H*K/2, 2W, 3]
+    (K = 1: [B,H,W,3]) — the reference's two-column grid of JET overlays."""
+    _need(heat, torch.float32, "heat_overlay.heat", 4)
+    _need(img, torch.uint8, "heat_overlay.img", 4)
+    _need(yx, torch.int32, "heat_overlay.yx", 3)
+    n, k, h, w = heat.shape
+    if tuple(img.shape) != (n, h, w, 3) or tuple(yx.shape) != (n, k, 2):
+        raise HkpError("heat_overlay: img %s / yx %s do not match heat %s" % (tuple(img.shape), tuple(yx.shape),
+                                                                            tuple(heat.shape)))
+    if k != 1 and k % 2:
+        raise HkpError("heat_overlay: K must be 1 or even (two equal columns)")
+    out = torch.empty((n, h, w, 3) if k == 1 else (n, h * (k // 2), 2 * w, 3), device=heat.device,
+                      dtype=torch.uint8)
+    mm = torch.empty(n * k * 2, device=heat.device, dtype=torch.float32)
+    call("hkp_heat_overlay", n, k, h, w, _ptr(heat), _ptr(img), _ptr(yx), _ptr(mm), _ptr(out), _stream())
+    return out
 
 
 def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None, x_hi=None):

@@ -7,6 +7,11 @@
   KeypointsDataset  dataset.py:52-79  same constructor, same (img, gaussians) items; with
                     return_uv=True items are (img, uv) so the fused loss kernel recomputes
                     the target in registers instead of reading a [K,H,W] fp64 tensor.
+  DeviceBatches     SURVEY §8(f1): the device data path — uint8 HWC images batched in
+                    pinned host memory, copied asynchronously (3 B/pixel instead of the
+                    12 B/pixel fp32 tensor, one batch ahead on a side stream) and fed to
+                    the model as [B,H,W,3] uint8, where the stem's operand pack applies
+                    ToTensor; labels travel as (u, v) and the loss kernel makes the target.
 """
 import os
 
@@ -110,5 +115,60 @@ class KeypointsDataset(Dataset):
         gaussians = gauss_2d_batch(self.img_width, self.img_height, self.gauss_sigma, U, V)
         return img, gaussians
 
+    def raw(self, index):
+        """(uint8 [H,W,3] BGR image as cv2.imread gives, fp32 [K,2] (u, v) on the device)."""
+        return imread_bgr(self.imgs[index]), self.labels[index].float()
+
     def __len__(self):
         return len(self.labels)
+
+
+class DeviceBatches:
+    """Iterate a KeypointsDataset as device batches (img uint8 [B,H,W,3], uv fp32
+    [B,K,2]) for model.forward / Trainer.step(img, uv=uv).
+
+    Decode happens on the host (cv2 / PIL, as the reference); each batch is stacked
+    into a pinned uint8 buffer and copied with non_blocking=True on a side stream
+    while the previous batch computes; the consumer's stream waits on an event.
+    `shuffle` uses a seeded permutation per epoch (train.py:61-67 shuffles)."""
+
+    def __init__(self, dataset, batch_size, shuffle=False, seed=0, drop_last=False, device="cuda"):
+        self.ds, self.bs, self.shuffle, self.seed, self.drop_last = dataset, batch_size, shuffle, seed, drop_last
+        self.device = torch.device(device)
+        self.epoch = 0
+
+    def __len__(self):
+        n = len(self.ds)
+        return n // self.bs if self.drop_last else (n + self.bs - 1) // self.bs
+
+    def _host_batch(self, idx):
+        items = [self.ds.raw(i) for i in idx]
+        imgs = np.stack([it[0] for it in items])
+        buf = torch.from_numpy(imgs).pin_memory()
+        uv = torch.stack([it[1] for it in items]).to(self.device)
+        return buf, uv
+
+    def __iter__(self):
+        n = len(self.ds)
+        order = (np.random.default_rng(self.seed + self.epoch).permutation(n) if self.shuffle else np.arange(n))
+        self.epoch += 1
+        batches = [order[i:i + self.bs] for i in range(0, n, self.bs)]
+        if self.drop_last and batches and len(batches[-1]) < self.bs:
+            batches.pop()
+        copy_stream = torch.cuda.Stream(self.device)
+
+        def stage(idx):
+            buf, uv = self._host_batch(idx)
+            with torch.cuda.stream(copy_stream):
+                img = buf.to(self.device, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(copy_stream)
+            return img, uv, ev, buf
+
+        nxt = stage(batches[0]) if batches else None
+        for bi in range(len(batches)):
+            img, uv, ev, buf = nxt
+            nxt = stage(batches[bi + 1]) if bi + 1 < len(batches) else None
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            img.record_stream(torch.cuda.current_stream(self.device))
+            yield img, uv

@@ -57,6 +57,17 @@ class Prediction:
         b = np.clip(1.5 - np.abs(4 * x - 1), 0, 1)
         return (np.stack([b, g, r], -1) * 255).astype(np.uint8)  # BGR like cv2.COLORMAP_JET
 
+    def overlays(self, imgs_u8, heatmaps=None, keypoints=None):
+        """Prediction.plot's picture for a whole batch on the GPU:
+        uint8 [B, H*K/2, 2W, 3] BGR on the device, bit-identical to plot()'s numpy
+        restatement.  imgs_u8: [B,H,W,3] uint8 (BGR); heatmaps / keypoints default to
+        one fused forward of the model on imgs_u8."""
+        from hkp import ops
+        imgs_u8 = imgs_u8.to("cuda").contiguous()
+        if heatmaps is None or keypoints is None:
+            heatmaps, keypoints = self.model.heatmaps_and_keypoints(imgs_u8)
+        return ops.heat_overlay(heatmaps.contiguous(), imgs_u8, keypoints.to(torch.int32).contiguous())
+
     def plot(self, img, heatmap, image_id=0, cls=None, classes=None, keypoints=None, out_dir="preds"):
         print("Running inferences on image: %d" % image_id)
         overlays = []

@@ -172,6 +172,17 @@ int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, 
                          int32_t apply_sigmoid, const float* lowres, float* heat, uint64_t* argmax_ws, int32_t* argmax_yx,
                          hkp_stream_t stream);
 
+/* On-GPU visualisation (Prediction.plot, src/prediction.py:40-66):
+ * per heatmap plane min-max → uint8 (truncating), JET colour map (BGR), blend
+ * 0.65*img + 0.35*map (truncating), a black 9x9 dot at argmax_yx, tiled into the
+ * reference's grid: planes k < K/2 stacked in column 0, the rest in column 1 —
+ * out [n][H*K/2][2W][3] uint8 (K = 1: [n][H][W][3]; other odd K rejected, as the
+ * reference's hconcat of unequal columns fails).  heat NCHW [n,k,H,W] fp32,
+ * img_nhwc [n,H,W,3] uint8 BGR, argmax_yx [n,k,2] int32 (hkp_upsample_sigmoid),
+ * minmax_ws [n*k*2] floats of workspace. */
+int hkp_heat_overlay(int32_t n, int32_t k, int32_t H, int32_t W, const float* heat, const uint8_t* img_nhwc,
+                     const int32_t* argmax_yx, float* minmax_ws, uint8_t* out, hkp_stream_t stream);
+
 /* Gaussian target (src/dataset.py:36-44): out[n,k,H,W] (fp64) =
  * (double) expf( -((x-u)^2 + (y-v)^2) / (2 sigma^2) ) computed in fp32;
  * uv [n,k,2] fp32 (u = column, v = row). */
@@ -219,6 +230,15 @@ int hkp_conv2d_bwd_filter_split(const hkp_conv_desc* d, const float* x, const fl
  * hkp_conv2d_fwd_stem_x3 = hkp_conv2d_fwd on them (NHWC fp32 y + BN partials). */
 int64_t hkp_stem_pack_x3_elems(const hkp_conv_desc* d);
 int hkp_stem_pack_x3(const hkp_conv_desc* d, const float* x_nchw, uint16_t* x_split, hkp_stream_t stream);
+/* Device data path: the same planes straight from the uint8 batch
+ * cv2.imread gives — img_nhwc [n][h][w][c] (BGR, c = d->c = 3), x = u8 / 255 in
+ * fp32 exactly as ToTensor (src/dataset.py:16,71): 3 B per pixel read instead of
+ * 12, and no fp32 image in HBM or over PCIe. */
+int hkp_stem_pack_x3_u8(const hkp_conv_desc* d, const uint8_t* img_nhwc, uint16_t* x_split, hkp_stream_t stream);
+/* ToTensor on the device: uint8 [n][h][w][c] → fp32 NCHW / 255 (the training path's
+ * stem wgrad operand, and any consumer that wants the reference's tensor). */
+int hkp_images_u8_to_nchw(int32_t n, int32_t h, int32_t w, int32_t c, const uint8_t* img_nhwc, float* x_nchw,
+                          hkp_stream_t stream);
 int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t* w_split, float* w_inv_scale,
                             hkp_stream_t stream);
 int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
