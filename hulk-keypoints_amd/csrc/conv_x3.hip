@@ -65,6 +65,9 @@ struct X3Args {
     int N, H, W, C, K, R, S, stride, pad, dil, Ho, Wo;
     int M, nks, cch, n_tiles, RS;
     long plane;            // STEM: halves between the hi and lo image planes
+    // phase output (strided dgrad): output pixel (n, ho, wo) of this launch is
+    // written at (n, ho*ost + oy, wo*ost + ox) of an [N][OH][OW][K] tensor; ost = 0: dense
+    int ost = 0, OH = 0, OW = 0, oy = 0, ox = 0;
 };
 
 // 2^e putting max|x| in [2^13, 2^14) (1 for 0 / non-finite): exact scaling
@@ -474,7 +477,13 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
                 acc[i][j][r] *= sc;
                 const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
                 if (m < a.M) {
-                    const long off = (long)m * a.K + n;
+                    long pix = m;
+                    if (a.ost) {                   // strided dgrad: one output phase per launch
+                        const int hw = a.Ho * a.Wo, ni = m / hw, rem = m - ni * hw;
+                        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+                        pix = ((long)ni * a.OH + ho * a.ost + a.oy) * a.OW + wo * a.ost + a.ox;
+                    }
+                    const long off = pix * a.K + n;
                     a.y[off] = a.add ? acc[i][j][r] + a.add[off] : acc[i][j][r];
                 }
             }
@@ -1112,6 +1121,94 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     a.M = (int)M; a.cch = d->k / 32; a.RS = d->r * d->s;
     launch_x3(d->c, (M + 255) / 256, as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3");
+    return HKP_OK;
+}
+
+// Strided dgrad as stride-1 convs, one per output phase (py, px) of dx: dx pixel
+// (2a+py, 2b+px) receives the taps r = r_max - 2r' (r ≡ py + pad mod 2) at dy row
+// a + o_min + r', o_min = (py + pad - r_max) / 2 (likewise for columns); a phase
+// no tap reaches (e.g. odd pixels of a 1x1 stride-2 conv) is dx = add (or 0).
+static int phase_taps(int R, int pad, int stride, int ph, int* r_max, int* o_min) {
+    int rm = -1;
+    for (int r = R - 1; r >= 0; --r)
+        if ((((ph + pad - r) % stride) + stride) % stride == 0) {
+            rm = r;
+            break;
+        }
+    if (rm < 0) return 0;
+    *r_max = rm;
+    *o_min = (ph + pad - rm) / stride;
+    return rm / stride + 1;
+}
+
+__global__ __launch_bounds__(256) void phase_fill_kernel(long total, int C4, int Ha, int Wa, int OH, int OW, int ost,
+                                                        int oy, int ox, const f32x4* __restrict__ add,
+                                                        f32x4* __restrict__ dx) {
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const int c4 = (int)(i % C4);
+        long p = i / C4;
+        const int b = (int)(p % Wa);
+        p /= Wa;
+        const int a = (int)(p % Ha);
+        const long n = p / Ha;
+        const long off = ((n * OH + (long)a * ost + oy) * OW + (long)b * ost + ox) * C4 + c4;
+        dx[off] = add ? add[off] : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+}
+
+extern "C" int hkp_phase_taps(int32_t r, int32_t pad, int32_t stride, int32_t phase) {
+    int rm, om;
+    if (r <= 0 || stride <= 0 || phase < 0 || phase >= stride) return -1;
+    return phase_taps(r, pad, stride, phase, &rm, &om);
+}
+
+extern "C" int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint16_t* dy_split,
+                                              const uint16_t* const* phase_split, const float* const* phase_inv_scale,
+                                              const uint32_t* dy_amax_bits, const float* add, float* dx,
+                                              hkp_stream_t stream) {
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    HKP_CHECK_ARG(dy_split && phase_split && phase_inv_scale && dx, "hkp_conv2d_bwd_data_x3_strided: null tensor");
+    HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC && d->stride == 2 && d->dilation == 1,
+                  "hkp_conv2d_bwd_data_x3_strided: stride-2, dilation-1 NHWC convs only");
+    HKP_CHECK_ARG(d->c % 64 == 0 && d->k % 32 == 0, "hkp_conv2d_bwd_data_x3_strided: need Cin%%64==0, Cout%%32==0");
+    HKP_CHECK_ARG((long)d->n * d->h * d->w < (1L << 31), "hkp_conv2d_bwd_data_x3_strided: too large");
+    hipStream_t st = as_stream(stream);
+    for (int py = 0; py < 2; ++py)
+        for (int px = 0; px < 2; ++px) {
+            const int ph = py * 2 + px;
+            const int Ha = (d->h - py + 1) / 2, Wa = (d->w - px + 1) / 2;
+            if (Ha <= 0 || Wa <= 0) continue;
+            int rmx = 0, omy = 0, smx = 0, omx = 0;
+            const int R2 = phase_taps(d->r, d->pad, 2, py, &rmx, &omy);
+            const int S2 = phase_taps(d->s, d->pad, 2, px, &smx, &omx);
+            if (R2 == 0 || S2 == 0) {
+                HKP_CHECK_ARG(phase_split[ph] == nullptr, "hkp_conv2d_bwd_data_x3_strided: phase %d has no taps", ph);
+                const long total = (long)d->n * Ha * Wa * (d->c / 4);
+                long g = (total + 255) / 256;
+                if (g > 8192) g = 8192;
+                hipLaunchKernelGGL(phase_fill_kernel, dim3((unsigned)g), dim3(256), 0, st, total, d->c / 4, Ha, Wa,
+                                   d->h, d->w, 2, py, px, (const f32x4*)add, (f32x4*)dx);
+                HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3_strided(fill)");
+                continue;
+            }
+            HKP_CHECK_ARG(phase_split[ph] && phase_inv_scale[ph], "hkp_conv2d_bwd_data_x3_strided: phase %d weights",
+                          ph);
+            X3Args a;
+            a.xs = (const _Float16*)dy_split; a.ws = (const _Float16*)phase_split[ph]; a.wscale = phase_inv_scale[ph];
+            a.y = dx; a.part = nullptr; a.amax = (const unsigned*)dy_amax_bits; a.add = add; a.plane = 0;
+            a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = R2; a.S = S2;
+            a.stride = 1; a.pad = -omy; a.dil = 1; a.Ho = Ha; a.Wo = Wa;
+            a.M = d->n * Ha * Wa; a.cch = d->k / 32; a.RS = R2 * S2;
+            a.ost = 2; a.OH = d->h; a.OW = d->w; a.oy = py; a.ox = px;
+            // the column offset: the kernel applies one pad to both axes
+            HKP_CHECK_ARG(omx == omy, "hkp_conv2d_bwd_data_x3_strided: row/column phase offsets differ (%d, %d)",
+                          omy, omx);
+            launch_x3(d->c, ((long)a.M + 255) / 256, st, a);
+            HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3_strided");
+        }
     return HKP_OK;
 }
 

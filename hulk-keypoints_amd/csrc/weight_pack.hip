@@ -16,7 +16,10 @@
 //             through LDS so that both the fp32 reads (one 32-B sector per row)
 //             and the packed 128-B [hi32|lo32] lines are written whole.
 // Outputs are bit-identical to the per-conv kernels (same power-of-two scales,
-// same split).  Jobs travel by value in the kernel arguments, 32 per launch.
+// same split).  Kind 2 packs one output phase of a stride-2 conv's dgrad operand
+// (hkp_conv2d_bwd_data_x3_strided): the flipped filter's taps of that phase, with
+// the whole flipped filter's per-channel scales.  Jobs travel by value in the
+// kernel arguments, 32 per launch.
 #include "common.h"
 
 namespace hkp {
@@ -32,6 +35,10 @@ struct PackJob {
     float* inv;
     float* part;   // flip: [k/8][c] column maxima
     int kind, k, rs, c;
+    // flipped operands: row tap (r', s') of the output reads w tap
+    // (rmx - tstep*r', smx - tstep*s'); R2 x S2 taps (kind 1: the whole filter,
+    // tstep 1; kind 2: one output phase of a stride-2 conv, tstep 2)
+    int S, R2, S2, rmx, smx, tstep;
 };
 
 struct PackTable {
@@ -126,7 +133,7 @@ __global__ __launch_bounds__(256) void weight_pack_a_kernel(const PackTable t) {
     const PackJob& J = t.j[jb];
     const int u = blockIdx.x - t.ubeg[jb];
     if (J.kind == 0) fwd_row(J, u, red);
-    else flip_max_tile(J, u, red);
+    else flip_max_tile(J, u, red);   // kinds 1 and 2: scale from the whole filter column
 }
 
 // flip-pack tile u: channels [8*(u % (c/8)), +8), rows [1024*(u / (c/8)), +1024) of
@@ -139,7 +146,7 @@ __global__ __launch_bounds__(256) void weight_pack_b_kernel(const PackTable t) {
     const PackJob& J = t.j[jb];
     const int u = blockIdx.x - t.ubeg[jb];
     const int cg = J.c / 8, g = u % cg, p = u / cg, c0 = 8 * g;
-    const int n = J.rs * J.k, K = J.k, tid = threadIdx.x;
+    const int n = J.R2 * J.S2 * J.k, K = J.k, tid = threadIdx.x;
     // channel scales from the column partials of launch A
     {
         const int cc = tid & 7;
@@ -156,14 +163,15 @@ __global__ __launch_bounds__(256) void weight_pack_b_kernel(const PackTable t) {
             if (p == 0) J.inv[c0 + tid] = 1.f / sc;
         }
     }
-    // gather: row r = tap'*K + k reads w[k][rs-1-tap'][c0..c0+8) (one 32-B sector)
+    // gather: row r = tap'*K + k reads w[k][src tap of tap'][c0..c0+8) (one 32-B sector)
     f32x4 a[4], b[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int r = p * PK_FLIP_ROWS + tid + 256 * q;
         if (r < n) {
-            const int tp = r / K, k = r - tp * K;
-            const f32x4* s = (const f32x4*)(J.w + ((long)k * J.rs + (J.rs - 1 - tp)) * J.c + c0);
+            const int tp = r / K, k = r - tp * K, rp = tp / J.S2, sp = tp - rp * J.S2;
+            const int src = (J.rmx - J.tstep * rp) * J.S + (J.smx - J.tstep * sp);
+            const f32x4* s = (const f32x4*)(J.w + ((long)k * J.rs + src) * J.c + c0);
             a[q] = s[0];
             b[q] = s[1];
         }
@@ -197,8 +205,34 @@ __global__ __launch_bounds__(256) void weight_pack_b_kernel(const PackTable t) {
     }
 }
 
+// taps of output phase ph of a stride-2 conv along an axis of R taps (conv_x3.hip)
+static int pk_phase_taps(int R, int pad, int ph, int* r_max) {
+    for (int r = R - 1; r >= 0; --r)
+        if ((((ph + pad - r) % 2) + 2) % 2 == 0) {
+            *r_max = r;
+            return r / 2 + 1;
+        }
+    return 0;
+}
+
+static void flip_geometry(const hkp_pack_job& j, PackJob& d) {
+    if (j.kind == 2) {
+        d.S = j.s;
+        d.R2 = pk_phase_taps(j.r, j.pad, j.phase >> 1, &d.rmx);
+        d.S2 = pk_phase_taps(j.s, j.pad, j.phase & 1, &d.smx);
+        d.tstep = 2;
+    } else {   // whole flipped filter; rs taps as one axis
+        d.S = 1; d.R2 = j.rs; d.S2 = 1; d.rmx = j.rs - 1; d.smx = 0; d.tstep = 1;
+    }
+}
+
 static int units_a(const hkp_pack_job& j) { return j.kind == 0 ? j.k : (j.c / 64) * (j.k / PK_KCHUNK); }
-static int units_b(const hkp_pack_job& j) { return j.kind == 0 ? 0 : (j.c / 8) * cdiv((long)j.rs * j.k, PK_FLIP_ROWS); }
+static int units_b(const hkp_pack_job& j) {
+    if (j.kind == 0) return 0;
+    PackJob d;
+    flip_geometry(j, d);
+    return (j.c / 8) * cdiv((long)d.R2 * d.S2 * j.k, PK_FLIP_ROWS);
+}
 static long part_floats(const hkp_pack_job& j) { return j.kind == 0 ? 0 : (long)(j.k / PK_KCHUNK) * j.c; }
 
 }  // namespace hkp
@@ -218,15 +252,23 @@ extern "C" int hkp_weight_pack_x3_batch(int32_t njobs, const hkp_pack_job* jobs,
     long need = 0;
     for (int i = 0; i < njobs; ++i) {
         const hkp_pack_job& j = jobs[i];
-        HKP_CHECK_ARG(j.w && j.out && j.inv_scale && (j.kind == 0 || j.kind == 1) && j.k > 0 && j.rs > 0 && j.c > 0,
+        HKP_CHECK_ARG(j.w && j.out && j.inv_scale && j.kind >= 0 && j.kind <= 2 && j.k > 0 && j.rs > 0 && j.c > 0,
                       "hkp_weight_pack_x3_batch: job %d: bad fields", i);
+        if (j.kind == 2) {
+            int rm;
+            HKP_CHECK_ARG(j.r > 0 && j.s > 0 && j.r * j.s == j.rs && j.phase >= 0 && j.phase < 4 &&
+                              pk_phase_taps(j.r, j.pad, j.phase >> 1, &rm) > 0 &&
+                              pk_phase_taps(j.s, j.pad, j.phase & 1, &rm) > 0,
+                          "hkp_weight_pack_x3_batch: job %d: phase %d of r=%d s=%d pad=%d has no taps", i, j.phase,
+                          j.r, j.s, j.pad);
+        }
         if (j.kind == 0)
             HKP_CHECK_ARG(j.c % 32 == 0, "hkp_weight_pack_x3_batch: job %d: forward pack needs c%%32==0 (c=%d)", i,
                           j.c);
         else
             HKP_CHECK_ARG(j.c % 64 == 0 && j.k % 32 == 0,
-                          "hkp_weight_pack_x3_batch: job %d: flip pack needs c%%64==0, k%%32==0 (c=%d k=%d)", i, j.c,
-                          j.k);
+                          "hkp_weight_pack_x3_batch: job %d: flip/phase pack needs c%%64==0, k%%32==0 (c=%d k=%d)", i,
+                          j.c, j.k);
         HKP_CHECK_ARG((long)j.k * j.rs * j.c < (1L << 31), "hkp_weight_pack_x3_batch: job %d too large", i);
         need += part_floats(j);
     }
@@ -249,6 +291,7 @@ extern "C" int hkp_weight_pack_x3_batch(int32_t njobs, const hkp_pack_job* jobs,
                 PackJob& d = t.j[t.n];
                 d.w = s.w; d.out = (_Float16*)s.out; d.inv = s.inv_scale; d.part = pj;
                 d.kind = s.kind; d.k = s.k; d.rs = s.rs; d.c = s.c;
+                flip_geometry(s, d);
                 t.ubeg[t.n++] = units;
                 units += u;
             }

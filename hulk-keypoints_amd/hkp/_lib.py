@@ -27,7 +27,8 @@ class ConvDesc(ctypes.Structure):
 class PackJob(ctypes.Structure):
     """hkp_pack_job (hkp_weight_pack_x3_batch)."""
     _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p), ("inv_scale", ctypes.c_void_p),
-                ("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("rs", ctypes.c_int32), ("c", ctypes.c_int32)]
+                ("kind", ctypes.c_int32), ("k", ctypes.c_int32), ("rs", ctypes.c_int32), ("c", ctypes.c_int32),
+                ("r", ctypes.c_int32), ("s", ctypes.c_int32), ("pad", ctypes.c_int32), ("phase", ctypes.c_int32)]
 
 
 class AdamTensor(ctypes.Structure):
@@ -76,6 +77,9 @@ SIGNATURES = {
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
     "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_phase_taps": (_I32, [_I32, _I32, _I32, _I32]),
+    "hkp_conv2d_bwd_data_x3_strided": (ctypes.c_int, [_CD, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P, _P,
+                                                       _P]),
     "hkp_weight_pack_x3_batch_ws_bytes": (_I64, [_I32, ctypes.POINTER(PackJob)]),
     "hkp_weight_pack_x3_batch": (ctypes.c_int, [_I32, ctypes.POINTER(PackJob), _P, _I64, _P]),
     "hkp_conv_bwd_filter_x3_workspace": (_I64, [_CD]),

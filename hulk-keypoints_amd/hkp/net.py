@@ -97,21 +97,36 @@ def prepack_x3(resnet, flip):
     items, outs, dest = [], [], []
     for conv in _nhwc_convs(resnet):
         w = conv.weight
-        k, c = w.shape[0], w.shape[-1]
+        k, r, s, c = w.shape
+        st, pd = _i(conv.stride), _i(conv.padding)
         want = ["x3"] if (k % 64 == 0 and c % 32 == 0) else []
-        if flip and _i(conv.stride) == 1 and k % 64 == 0 and c % 64 == 0:
-            want.append("flip_x3")
+        if flip and k % 64 == 0 and c % 64 == 0:
+            if st == 1:
+                want.append("flip_x3")
+            elif st == 2 and _i(conv.dilation) == 1:
+                want.append("phase_x3")
         per = _cache_slot(w) if want else None
         for v in want:
             ent = per.get(v)
-            if not _fresh(w, ent):
+            if _fresh(w, ent):
+                continue
+            if v == "phase_x3":        # one pack per output phase a tap reaches
+                old = ent[2] if ent is not None else [None] * 4
+                val = [None] * 4
+                per[v] = (w._version, w.data_ptr(), val)
+                for ph in range(4):
+                    if ops.phase_taps(r, pd, ph >> 1) > 0 and ops.phase_taps(s, pd, ph & 1) > 0:
+                        items.append((v, w.detach(), (ph, pd)))
+                        outs.append(old[ph])
+                        dest.append((val, ph, None))
+            else:
                 items.append((v, w.detach()))
                 outs.append(ent[2] if ent is not None else None)
                 dest.append((per, v, w))
     if not items:
         return
-    for (per, v, w), packed in zip(dest, ops.weight_pack_x3_batch(items, outs)):
-        per[v] = (w._version, w.data_ptr(), packed)
+    for (tgt, key, w), packed in zip(dest, ops.weight_pack_x3_batch(items, outs)):
+        tgt[key] = packed if w is None else (w._version, w.data_ptr(), packed)
 
 
 def set_conv_precision(p):
@@ -313,6 +328,10 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
             if st == 1:
                 wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
                 dx = ops.conv2d_bwd_data_x3(dys, wfs, tuple(x.shape), pd, dl, add=add, amax=amax)
+            elif st == 2 and dl == 1:      # one stride-1 conv per output phase of dx
+                phs = _cached_split(conv.weight, "phase_x3", lambda t: ops.weight_phase_pack_x3(t, pd))
+                dx = ops.conv2d_bwd_data_x3_strided(dys, phs, tuple(x.shape), tuple(conv.weight.shape), pd, add=add,
+                                                    amax=amax)
             else:
                 dx = ops.conv2d_bwd_data(dy, ops.conv_weight_flip(conv.weight), tuple(x.shape), st, pd, dl, add=add)
         grads.put(conv.weight, ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax))

@@ -563,34 +563,95 @@ def weight_flip_pack_x3(w):
     return PackedWeight(out, sc)
 
 
+def phase_taps(r, pad, phase, stride=2):
+    """Taps of output phase `phase` along a filter axis of r taps (hkp_phase_taps)."""
+    from ._lib import lib
+    return lib().hkp_phase_taps(r, pad, stride, phase)
+
+
 def weight_pack_x3_batch(items, outs=None):
     """Many weight packs in one launch pair (hkp_weight_pack_x3_batch): items =
     [(kind, w)] with kind "x3" (= weight_pack_x3(w)) or "flip_x3"
-    (= weight_flip_pack_x3(w)); returns the PackedWeights in order.  outs
-    (optional, same order; None entries allowed) are PackedWeights to overwrite."""
+    (= weight_flip_pack_x3(w)), or ("phase_x3", w, (phase, pad)) — output phase
+    phase = py*2+px of a stride-2 conv's dgrad operand (conv2d_bwd_data_x3_strided);
+    returns the PackedWeights in order.  outs (optional, same order; None entries
+    allowed) are PackedWeights to overwrite."""
     from ._lib import PackJob, lib
     jobs = (PackJob * max(1, len(items)))()
     res = []
-    for i, (kind, w) in enumerate(items):
+    for i, item in enumerate(items):
+        kind, w = item[0], item[1]
         _need(w, torch.float32, "weight_pack_x3_batch.w", 4)
         k, r, s, c = w.shape
-        flip = kind == "flip_x3"
-        if not flip and kind != "x3":
+        if kind == "x3":
+            code, shape, n_sc = 0, (k, r, s, 2 * c), k
+        elif kind == "flip_x3":
+            code, shape, n_sc = 1, (c, r, s, 2 * k), c
+        elif kind == "phase_x3":
+            ph, pad = item[2]
+            r2, s2 = phase_taps(r, pad, ph >> 1), phase_taps(s, pad, ph & 1)
+            if r2 <= 0 or s2 <= 0:
+                raise HkpError("weight_pack_x3_batch: phase %d has no taps" % ph)
+            code, shape, n_sc = 2, (c, r2, s2, 2 * k), c
+            jobs[i].r, jobs[i].s, jobs[i].pad, jobs[i].phase = r, s, pad, ph
+        else:
             raise HkpError("weight_pack_x3_batch: unknown kind %r" % (kind,))
-        shape, n_sc = ((c, r, s, 2 * k), c) if flip else ((k, r, s, 2 * c), k)
         o = outs[i] if outs is not None else None
         if o is None or tuple(o.split.shape) != shape or o.split.device != w.device:
             o = PackedWeight(torch.empty(shape, device=w.device, dtype=torch.float16),
                              torch.empty(n_sc, device=w.device, dtype=torch.float32))
         res.append(o)
         jobs[i].w, jobs[i].out, jobs[i].inv_scale = _ptr(w), _ptr(o.split), _ptr(o.inv_scale)
-        jobs[i].kind, jobs[i].k, jobs[i].rs, jobs[i].c = int(flip), k, r * s, c
+        jobs[i].kind, jobs[i].k, jobs[i].rs, jobs[i].c = code, k, r * s, c
     if not items:
         return res
     nb = lib().hkp_weight_pack_x3_batch_ws_bytes(len(items), jobs)
     ws = torch.empty(max(4, nb), device=items[0][1].device, dtype=torch.uint8)
     call("hkp_weight_pack_x3_batch", len(items), jobs, _ptr(ws), nb, _stream())
     return res
+
+
+def weight_phase_pack_x3(w, pad):
+    """The four output-phase dgrad operands of a stride-2 KRSC conv weight (None for a
+    phase no tap reaches), for conv2d_bwd_data_x3_strided."""
+    k, r, s, c = w.shape
+    phases = [ph for ph in range(4) if phase_taps(r, pad, ph >> 1) > 0 and phase_taps(s, pad, ph & 1) > 0]
+    packs = weight_pack_x3_batch([("phase_x3", w, (ph, pad)) for ph in phases])
+    out = [None] * 4
+    for ph, pk in zip(phases, packs):
+        out[ph] = pk
+    return out
+
+
+def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=None, amax=None):
+    """f16x3 dL/dx of a stride-2 (dilation-1) NHWC conv with KRSC weight shape
+    w_shape, one stride-1 conv per output phase: dys = split_pack_x3(dy, amax),
+    phase_packs = weight_phase_pack_x3(w, pad)."""
+    _need(dys, torch.float16, "conv2d_bwd_data_x3_strided.dy_split", 4)
+    k, r, s, c = w_shape
+    if len(phase_packs) != 4:
+        raise HkpError("conv2d_bwd_data_x3_strided: need 4 phase packs (None for empty phases)")
+    for ph, p in enumerate(phase_packs):
+        taps = (phase_taps(r, pad, ph >> 1), phase_taps(s, pad, ph & 1))
+        want = None if min(taps) <= 0 else (c,) + taps + (2 * k,)
+        if (p is None) != (want is None) or (p is not None and tuple(p.split.shape) != want):
+            raise HkpError("conv2d_bwd_data_x3_strided: phase %d pack %s, expected %s" % (
+                ph, None if p is None else tuple(p.split.shape), want))
+    d = _fwd_desc(x_shape, (k, r, s, c), 2, pad, 1, "nhwc")
+    ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, 2, pad, 1)
+    if tuple(dys.shape) != (x_shape[0], ho, wo, 2 * k):
+        raise HkpError("conv2d_bwd_data_x3_strided: dy split shape %s != %s" % (tuple(dys.shape),
+                                                                               (x_shape[0], ho, wo, 2 * k)))
+    if add is not None:
+        _need(add, torch.float32, "conv2d_bwd_data_x3_strided.add", 4)
+        if tuple(add.shape) != tuple(x_shape):
+            raise HkpError("conv2d_bwd_data_x3_strided: add shape mismatch")
+    dx = torch.empty(tuple(x_shape), device=dys.device, dtype=torch.float32)
+    sp = (ctypes.c_void_p * 4)(*[None if p is None else p.split.data_ptr() for p in phase_packs])
+    sc = (ctypes.c_void_p * 4)(*[None if p is None else p.inv_scale.data_ptr() for p in phase_packs])
+    call("hkp_conv2d_bwd_data_x3_strided", ctypes.byref(d), _ptr(dys), sp, sc, _ptr(amax), _ptr(add), _ptr(dx),
+         _stream())
+    return dx
 
 
 def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None):

@@ -267,12 +267,26 @@ int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf
 int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
                            const float* wf_inv_scale, const uint32_t* dy_amax_bits, const float* add, float* dx,
                            hkp_stream_t stream);
+/* Strided (stride 2, dilation 1) backward-data on the f16x3 path: dx is computed
+ * per output phase (py, px) as a stride-1 conv of dy with that phase's taps
+ * (phase_split[py*2+px] = kind-2 packs of hkp_weight_pack_x3_batch, inverse
+ * scales phase_inv_scale[..]) written to dx pixels (2a+py, 2b+px); a phase no tap
+ * reaches (NULL entry; e.g. the odd pixels of a 1x1 stride-2 downsample) gets
+ * dx = add (or 0).  d = the forward descriptor; needs Cin % 64 == 0, Cout % 32 == 0.
+ * hkp_phase_taps: taps of phase `phase` along an axis of r taps (0: none, -1: bad args). */
+int32_t hkp_phase_taps(int32_t r, int32_t pad, int32_t stride, int32_t phase);
+int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint16_t* dy_split,
+                                   const uint16_t* const* phase_split, const float* const* phase_inv_scale,
+                                   const uint32_t* dy_amax_bits, const float* add, float* dx, hkp_stream_t stream);
 /* Batched weight packing for a training step (one launch pair for a whole
  * network instead of one hkp_weight_pack_x3 / hkp_weight_flip_pack_x3 per conv;
  * outputs bit-identical to those).  jobs: host array; kind 0 = forward pack
  * (out = w_split [k][rs][c/32][64], inv_scale [k]; needs c % 32 == 0), kind 1 =
  * flipped dgrad pack (out = wf_split [c][rs][k/32][64], inv_scale [c]; needs
- * c % 64 == 0, k % 32 == 0); w is KRSC fp32 [k][rs][c].  workspace:
+ * c % 64 == 0, k % 32 == 0), kind 2 = output phase `phase` (= py*2 + px) of a
+ * stride-2 conv's dgrad operand (fields r, s, pad; out = [c][R2][S2][k/32][64]
+ * with R2/S2 = hkp_phase_taps(r|s, pad, 2, py|px); inv_scale [c] = kind 1's) for
+ * hkp_conv2d_bwd_data_x3_strided; w is KRSC fp32 [k][rs][c].  workspace:
  * hkp_weight_pack_x3_batch_ws_bytes(njobs, jobs) bytes (per-channel column
  * maxima of the flip jobs). */
 typedef struct hkp_pack_job {
@@ -280,6 +294,7 @@ typedef struct hkp_pack_job {
     uint16_t* out;
     float* inv_scale;
     int32_t kind, k, rs, c;
+    int32_t r, s, pad, phase;   /* kind 2 only */
 } hkp_pack_job;
 int64_t hkp_weight_pack_x3_batch_ws_bytes(int32_t njobs, const hkp_pack_job* jobs);
 int hkp_weight_pack_x3_batch(int32_t njobs, const hkp_pack_job* jobs, void* workspace, int64_t ws_bytes,

@@ -80,7 +80,7 @@ def test_reference_init_statistics():
 def test_weight_pack_batch_host_side():
     """hkp_pack_job layout, workspace sizing and argument checks (host only)."""
     from hkp import _lib
-    assert ctypes.sizeof(_lib.PackJob) == 40
+    assert ctypes.sizeof(_lib.PackJob) == 56
     jobs = (_lib.PackJob * 3)()
     for j, (kind, k, rs, c) in zip(jobs, [(0, 64, 9, 64), (1, 512, 9, 512), (1, 2048, 1, 512)]):
         j.w, j.out, j.inv_scale, j.kind, j.k, j.rs, j.c = 16, 16, 16, kind, k, rs, c

@@ -247,6 +247,50 @@ def test_x3_dgrad_scaled(cuda_device, case, gscale):
     assert err < 2e-6, err
 
 
+STRIDED_CASES = [
+    (2, 30, 40, 64, 128, 3, 1),     # R34 layer2.0.conv1 shape class (3x3 s2 p1)
+    (1, 31, 41, 64, 128, 3, 1),     # odd H, W: phases of unequal size, last dy row/col half-used
+    (2, 30, 40, 64, 128, 1, 0),     # 1x1 s2 downsample: three phases are add-only
+    (1, 15, 21, 128, 256, 3, 1),    # R50 layer2 conv2 (3x3 s2), Cout 256
+]
+
+
+@pytest.mark.parametrize("case", STRIDED_CASES)
+@pytest.mark.parametrize("gscale", [1.0, 1e-9])
+def test_x3_dgrad_strided(cuda_device, case, gscale):
+    """stride-2 dgrad as one stride-1 x3 conv per output phase (phase packs from the
+    batched packer, kind 2): fp32-class vs fp64, residual addend included."""
+    from hkp import ops
+    n, h, w, cin, cout, k, pad = case
+    wt = rand(cout, cin, k, k, seed=15, scale=(2.0 / (k * k * cout)) ** 0.5)
+    ho = (h + 2 * pad - (k - 1) - 1) // 2 + 1
+    wo = (w + 2 * pad - (k - 1) - 1) // 2 + 1
+    gy = rand(n, cout, ho, wo, seed=16) * gscale
+    add = rand(n, cin, h, w, seed=17) * gscale
+    ref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.double(), gy.double(), 2, pad, 1) + add.double()
+    d = cuda_device
+    gy_d = gy.permute(0, 2, 3, 1).contiguous().to(d)
+    wk = wt.permute(0, 2, 3, 1).contiguous().to(d)
+    amax = ops.absmax(gy_d)
+    phs = ops.weight_phase_pack_x3(wk, pad)
+    assert sum(p is not None for p in phs) == (4 if k == 3 else 1)
+    dx = ops.conv2d_bwd_data_x3_strided(ops.split_pack_x3(gy_d, amax), phs, (n, h, w, cin), tuple(wk.shape), pad,
+                                        add=add.permute(0, 2, 3, 1).contiguous().to(d), amax=amax)
+    err = (dx.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    # each phase pack holds exactly the flipped filter's taps of that phase, same scales
+    fp = ops.weight_flip_pack_x3(wk)
+    fh, fl = _unpack_x3(fp.split)                     # [C, R, S, K], tap (i, j) = w tap (R-1-i, S-1-j)
+    for ph, p in enumerate(phs):
+        if p is None:
+            continue
+        assert torch.equal(p.inv_scale, fp.inv_scale)
+        ph_h, ph_l = _unpack_x3(p.split)
+        rows = [k - 1 - r for r in range(k - 1, -1, -1) if (((ph >> 1) + pad - r) % 2) == 0]
+        cols = [k - 1 - s for s in range(k - 1, -1, -1) if (((ph & 1) + pad - s) % 2) == 0]
+        assert torch.equal(ph_h, fh[:, rows][:, :, cols]) and torch.equal(ph_l, fl[:, rows][:, :, cols])
+
+
 WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (2, 7, 9, 64, 64, 3, 1, 1, 1),          # Wo = 9 < 32: a K-step spans several rows/images
     (1, 30, 40, 96, 128, 3, 2, 1, 1),       # stride 2, RSC = 864 (ragged 256-column tile)
