@@ -10,7 +10,7 @@
 //                    then cast to fp32 (the .double() cast's backward).
 //  * hkp_head_bwd    sigmoid backward (g*(1-p))*p (model.py:21) fused with the
 //                    adjoint of the align_corners=True upsample (resnet_dilated.py:27)
-//                    as a per-low-res-node gather (no atomics).
+//                    as two separable gathers (rows, then columns; no atomics).
 //  * hkp_head_fc_bwd fc 1x1 (resnet_dilated.py:16) grads: dfeat (NHWC), dW, db for
 //                    the K used rows; rows >= K get exactly zero.
 #include "common.h"
@@ -100,11 +100,53 @@ __global__ void loss_finalize_kernel(int nparts, double inv_n, const double* __r
     if (threadIdx.x == 0) loss[0] = t * inv_n;
 }
 
-// d_low[plane][i][j] = sum_{oh,ow} wr_i(oh) wc_j(ow) * (g*(1-p))*p at (oh, ow)
+// d_low[plane][i][j] = sum_oh wr_i(oh) * ( sum_ow wc_j(ow) * (g*(1-p))*p at (oh, ow) ),
+// separable in two gathers (no atomics), each in the loop order of the direct
+// double sum so the result is the same bit for bit:
+//   pass 1 (rows): rs[plane][oh][j] = sum over the ow whose lerp touches j
+//   pass 2 (cols): d_low[plane][i][j] = sum over the oh whose lerp touches i of wr * rs
+// Each high-res element is read by <= 2 pass-1 threads (vs ~4 node gathers that
+// each recomputed every candidate's lerp in the direct form).
+__device__ __forceinline__ void cand_range(int i, int in, int out, float inv, int* o0, int* o1) {
+    if (out != in) {
+        *o0 = max(0, (int)floorf((float)(i - 1) * inv) - 1);
+        *o1 = min(out - 1, (int)ceilf((float)(i + 1) * inv) + 1);
+    } else {
+        *o0 = *o1 = i;
+    }
+}
+
 template <bool SIG>
-__global__ __launch_bounds__(256) void head_bwd_kernel(int planes, int h, int w, int H, int W, float sh, float sw,
-                                                      float ih, float iw, const float* __restrict__ g,
-                                                      const float* __restrict__ p, float* __restrict__ dlow) {
+__global__ __launch_bounds__(256) void head_bwd_rows_kernel(int planes, int w, int H, int W, float sw, float iw,
+                                                           const float* __restrict__ g, const float* __restrict__ p,
+                                                           float* __restrict__ rs) {
+    const long total = (long)planes * H * w;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
+        const int j = (int)(t % w);
+        const long prow = t / w;                          // plane * H + oh
+        int ow0, ow1;
+        cand_range(j, w, W, iw, &ow0, &ow1);
+        const float* gp = g + prow * (long)W;
+        const float* pp = p + prow * (long)W;
+        float row = 0.f;
+        for (int ow = ow0; ow <= ow1; ++ow) {
+            const LerpB lc = lerp_b(ow, w, W, sw);
+            if (lc.i0 != j && lc.i1 != j) continue;
+            const float wc = (lc.i0 == j ? lc.l0 : 0.f) + (lc.i1 == j ? lc.l1 : 0.f);
+            float dzv = gp[ow];
+            if constexpr (SIG) {
+                const float pv = pp[ow];
+                dzv = dzv * (1.f - pv) * pv;
+            }
+            row += wc * dzv;
+        }
+        rs[t] = row;
+    }
+}
+
+__global__ __launch_bounds__(256) void head_bwd_cols_kernel(int planes, int h, int w, int H, float sh, float ih,
+                                                           const float* __restrict__ rs, float* __restrict__ dlow) {
     const long total = (long)planes * h * w;
     const long stride = (long)gridDim.x * blockDim.x;
     for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += stride) {
@@ -112,41 +154,15 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(int planes, int h, int w,
         const long q = t / w;
         const int i = (int)(q % h);
         const long plane = q / h;
-        // candidate output rows/cols: those whose lerp touches node i / j
-        int oh0 = 0, oh1 = H - 1, ow0 = 0, ow1 = W - 1;
-        if (H != h) {
-            oh0 = max(0, (int)floorf((float)(i - 1) * ih) - 1);
-            oh1 = min(H - 1, (int)ceilf((float)(i + 1) * ih) + 1);
-        } else {
-            oh0 = oh1 = i;
-        }
-        if (W != w) {
-            ow0 = max(0, (int)floorf((float)(j - 1) * iw) - 1);
-            ow1 = min(W - 1, (int)ceilf((float)(j + 1) * iw) + 1);
-        } else {
-            ow0 = ow1 = j;
-        }
-        const float* gp = g + plane * (long)H * W;
-        const float* pp = p + plane * (long)H * W;
+        int oh0, oh1;
+        cand_range(i, h, H, ih, &oh0, &oh1);
+        const float* r = rs + plane * (long)H * w + j;
         float acc = 0.f;
         for (int oh = oh0; oh <= oh1; ++oh) {
             const LerpB lr = lerp_b(oh, h, H, sh);
             if (lr.i0 != i && lr.i1 != i) continue;
             const float wr = (lr.i0 == i ? lr.l0 : 0.f) + (lr.i1 == i ? lr.l1 : 0.f);
-            float row = 0.f;
-            for (int ow = ow0; ow <= ow1; ++ow) {
-                const LerpB lc = lerp_b(ow, w, W, sw);
-                if (lc.i0 != j && lc.i1 != j) continue;
-                const float wc = (lc.i0 == j ? lc.l0 : 0.f) + (lc.i1 == j ? lc.l1 : 0.f);
-                const long o = (long)oh * W + ow;
-                float dzv = gp[o];
-                if constexpr (SIG) {
-                    const float pv = pp[o];
-                    dzv = dzv * (1.f - pv) * pv;
-                }
-                row += wc * dzv;
-            }
-            acc += wr * row;
+            acc += wr * r[(long)oh * w];
         }
         dlow[t] = acc;
     }
@@ -243,14 +259,21 @@ __global__ __launch_bounds__(256) void head_dw_kernel(long npix, int hw, int C, 
     }
 }
 
+// out[i] = sum_s ws[s][i] in a fixed order: 4 lanes per element each sum every
+// 4th split, then the lane sums pairwise (the split count runs to hundreds)
 __global__ __launch_bounds__(256) void sum_splits_kernel(long n, int splits, const float* __restrict__ ws,
                                                         float* __restrict__ out) {
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        float s = 0.f;
-        for (int k = 0; k < splits; ++k) s += ws[(long)k * n + i];
-        out[i] = s;
+    __shared__ float red[4][64];
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const long i = (long)blockIdx.x * 64 + l;
+    float s = 0.f;
+    if (i < n) {
+#pragma unroll 8
+        for (int k = q; k < splits; k += 4) s += ws[(long)k * n + i];
     }
+    red[q][l] = s;
+    __syncthreads();
+    if (q == 0 && i < n) out[i] = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
 }
 
 static inline int gcap(long work) {
@@ -260,7 +283,7 @@ static inline int gcap(long work) {
 }
 
 constexpr int LOSS_BLOCKS = 1024;
-constexpr long HEAD_DW_PIX = 512;
+constexpr long HEAD_DW_PIX = 128;   // pixels per dW partial (C2/C3 shard: 300 blocks)
 
 }  // namespace hkp
 
@@ -295,22 +318,32 @@ extern "C" int hkp_heat_loss(int32_t n, int32_t k, int32_t H, int32_t W, int32_t
     return HKP_OK;
 }
 
+extern "C" int64_t hkp_head_bwd_workspace(int32_t n, int32_t k, int32_t w, int32_t H) {
+    return (int64_t)n * k * H * w * (int64_t)sizeof(float);
+}
+
 extern "C" int hkp_head_bwd(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, int32_t W, const float* dheat,
-                            const float* heat, float* dlow, hkp_stream_t stream) {
+                            const float* heat, float* dlow, void* workspace, int64_t ws_bytes, hkp_stream_t stream) {
     HKP_CHECK_ARG(n > 0 && k > 0 && h > 0 && w > 0 && H >= h && W >= w, "hkp_head_bwd: bad sizes");
-    HKP_CHECK_ARG(dheat && dlow, "hkp_head_bwd: null tensor");
+    HKP_CHECK_ARG(dheat && dlow && workspace, "hkp_head_bwd: null tensor");
+    HKP_CHECK_ARG(ws_bytes >= hkp_head_bwd_workspace(n, k, w, H), "hkp_head_bwd: workspace too small");
     const float sh = H > 1 ? (float)(h - 1) / (float)(H - 1) : 0.f;
     const float sw = W > 1 ? (float)(w - 1) / (float)(W - 1) : 0.f;
     const float ih = h > 1 ? (float)(H - 1) / (float)(h - 1) : 0.f;
     const float iw = w > 1 ? (float)(W - 1) / (float)(w - 1) : 0.f;
-    const long total = (long)n * k * h * w;
+    float* rs = (float*)workspace;
+    hipStream_t st = as_stream(stream);
+    const long rows = (long)n * k * H * w;
     if (heat)
-        hipLaunchKernelGGL((head_bwd_kernel<true>), dim3(gcap(total)), dim3(256), 0, as_stream(stream), n * k, h, w, H,
-                           W, sh, sw, ih, iw, dheat, heat, dlow);
+        hipLaunchKernelGGL((head_bwd_rows_kernel<true>), dim3(gcap(rows)), dim3(256), 0, st, n * k, w, H, W, sw, iw,
+                           dheat, heat, rs);
     else
-        hipLaunchKernelGGL((head_bwd_kernel<false>), dim3(gcap(total)), dim3(256), 0, as_stream(stream), n * k, h, w,
-                           H, W, sh, sw, ih, iw, dheat, heat, dlow);
-    HKP_LAUNCH_CHECK("hkp_head_bwd");
+        hipLaunchKernelGGL((head_bwd_rows_kernel<false>), dim3(gcap(rows)), dim3(256), 0, st, n * k, w, H, W, sw, iw,
+                           dheat, heat, rs);
+    HKP_LAUNCH_CHECK("hkp_head_bwd(rows)");
+    const long total = (long)n * k * h * w;
+    hipLaunchKernelGGL(head_bwd_cols_kernel, dim3(gcap(total)), dim3(256), 0, st, n * k, h, w, H, sh, ih, rs, dlow);
+    HKP_LAUNCH_CHECK("hkp_head_bwd(cols)");
     return HKP_OK;
 }
 
@@ -346,9 +379,10 @@ extern "C" int hkp_head_fc_bwd(int32_t n, int32_t hw, int32_t c, int32_t k, cons
         hipLaunchKernelGGL(head_dw_kernel<16>, grid, dim3(256), 0, st, npix, hw, c, k, HEAD_DW_PIX, dlow, feat, ws_w,
                            ws_b);
     HKP_LAUNCH_CHECK("hkp_head_fc_bwd(dw)");
-    hipLaunchKernelGGL(sum_splits_kernel, dim3(gcap((long)k * c)), dim3(256), 0, st, (long)k * c, (int)splits, ws_w,
-                       dw);
-    hipLaunchKernelGGL(sum_splits_kernel, dim3(1), dim3(256), 0, st, (long)k, (int)splits, ws_b, db);
+    hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)(((long)k * c + 63) / 64)), dim3(256), 0, st, (long)k * c,
+                       (int)splits, ws_w, dw);
+    hipLaunchKernelGGL(sum_splits_kernel, dim3((unsigned)((k + 63) / 64)), dim3(256), 0, st, (long)k, (int)splits,
+                       ws_b, db);
     HKP_LAUNCH_CHECK("hkp_head_fc_bwd(reduce)");
     return HKP_OK;
 }

@@ -99,7 +99,8 @@ SIGNATURES = {
     "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "hkp_heat_loss_workspace": (_I64, []),
     "hkp_heat_loss": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _P, _P, _P, _P]),
-    "hkp_head_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P]),
+    "hkp_head_bwd_workspace": (_I64, [_I32, _I32, _I32, _I32]),
+    "hkp_head_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I64, _P]),
     "hkp_head_fc_bwd_workspace": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_head_fc_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
 }

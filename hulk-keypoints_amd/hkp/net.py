@@ -299,16 +299,41 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
 class Grads(dict):
     """param → gradient tensor, filled in reverse layer order.  ``on_ready`` (if
     set) is called for each parameter as soon as its gradient exists — the DP
-    bucketer hooks in here to overlap RCCL all-reduce with the rest of backward."""
+    bucketer hooks in here to overlap RCCL all-reduce with the rest of backward.
+    A gradient produced on the side stream comes with its `ready` event: the
+    current stream waits for it before on_ready, and for all of them in sync()."""
 
     def __init__(self, on_ready=None):
         super().__init__()
         self.on_ready = on_ready
+        self.events = []
 
-    def put(self, p, g):
+    def put(self, p, g, ready=None):
         self[p] = g
+        if ready is not None:
+            self.events.append(ready)
         if self.on_ready is not None:
+            if ready is not None:
+                torch.cuda.current_stream(g.device).wait_event(ready)
             self.on_ready(p, g)
+
+    def sync(self):
+        for ev in self.events:
+            torch.cuda.current_stream().wait_event(ev)
+        self.events = []
+
+
+# wgrad of a conv runs on a side stream, concurrently with its dgrad: the two
+# grids fill each other's last partial round of CUs (HKP_OVERLAP_WGRAD=0: serial)
+OVERLAP_WGRAD = os.environ.get("HKP_OVERLAP_WGRAD", "1") != "0"
+_side_streams = {}
+
+
+def _side_stream(dev):
+    s = _side_streams.get(dev)
+    if s is None:
+        s = _side_streams[dev] = torch.cuda.Stream(dev)
+    return s
 
 
 def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
@@ -323,6 +348,17 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
         if amax is None:
             amax = ops.absmax(dy)
         dys = ops.split_pack_x3(dy, amax)
+        ready = None
+        if OVERLAP_WGRAD:
+            main, side = torch.cuda.current_stream(dy.device), _side_stream(dy.device)
+            side.wait_stream(main)                     # dy split (and x split) written
+            with torch.cuda.stream(side):
+                dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
+                ready = torch.cuda.Event()
+                ready.record(side)
+            for t in (xs[0], dys, amax):              # read on the side stream: keep their memory
+                t.record_stream(side)
+            dw.record_stream(main)
         dx = None
         if need_dx:
             if st == 1:
@@ -334,7 +370,9 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
                                                     amax=amax)
             else:
                 dx = ops.conv2d_bwd_data(dy, ops.conv_weight_flip(conv.weight), tuple(x.shape), st, pd, dl, add=add)
-        grads.put(conv.weight, ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax))
+        if ready is None:
+            dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
+        grads.put(conv.weight, dw, ready)
         return dx
     split_ok = _precision == "f16x3" and c % 64 == 0 and k % 64 == 0
     amax = ops.absmax(dy) if split_ok else None
@@ -410,6 +448,7 @@ def keypoints_backward(resnet, trace, dheat, grads):
                                                                            resnet.layer4) for b in l])):
         g = block_backward(block, rec, g, grads)
     stem_backward(resnet, trace.stem, g, grads)
+    grads.sync()
     return grads
 
 

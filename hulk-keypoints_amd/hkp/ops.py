@@ -800,8 +800,11 @@ def head_bwd(dheat, heat, h, w):
     n, k, H, W = dheat.shape
     if heat is not None and heat.shape != dheat.shape:
         raise HkpError("head_bwd: heat shape mismatch")
+    from ._lib import lib
     dlow = torch.empty((n, k, h, w), device=dheat.device, dtype=torch.float32)
-    call("hkp_head_bwd", n, k, h, w, H, W, _ptr(dheat), _ptr(heat), _ptr(dlow), _stream())
+    nb = lib().hkp_head_bwd_workspace(n, k, w, H)
+    ws = torch.empty(nb // 4, device=dheat.device, dtype=torch.float32)
+    call("hkp_head_bwd", n, k, h, w, H, W, _ptr(dheat), _ptr(heat), _ptr(dlow), _ptr(ws), nb, _stream())
     return dlow
 
 

@@ -366,9 +366,12 @@ int hkp_heat_loss(int32_t n, int32_t k, int32_t H, int32_t W, int32_t loss_kind,
                   hkp_stream_t stream);
 
 /* dlow = upsample-adjoint( dheat * (1-heat) * heat ) (sigmoid backward fused;
- * heat NULL = dheat is already the pre-sigmoid gradient). */
+ * heat NULL = dheat is already the pre-sigmoid gradient): a row gather into
+ * `workspace` (hkp_head_bwd_workspace bytes: [n*k][H][w] floats), then a column
+ * gather — the direct double sum's loop order, so the same bits. */
+int64_t hkp_head_bwd_workspace(int32_t n, int32_t k, int32_t w, int32_t H);
 int hkp_head_bwd(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, int32_t W, const float* dheat,
-                 const float* heat, float* dlow, hkp_stream_t stream);
+                 const float* heat, float* dlow, void* workspace, int64_t ws_bytes, hkp_stream_t stream);
 
 /* fc (K used rows) backward: dfeat NHWC [n,hw,c], dw [k][c], db [k]. */
 int64_t hkp_head_fc_bwd_workspace(int32_t n, int32_t hw, int32_t c, int32_t k);
