@@ -20,11 +20,14 @@ namespace hkp {
 constexpr int BNB_TILE = 64;   // pixels per reduction tile (small: enough blocks to fill the chip at batch 8)
 
 // G = channel groups of 4 per thread (C/4 / threads-per-row); MASK: dz = g*(out>0)
-template <int G, bool MASK>
+// MAXIMA: also per tile and channel max|dz| and max|y - mean| (the inputs of
+// finalize's upper bound on max|dy|)
+template <int G, bool MASK, bool MAXIMA = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const float* __restrict__ g,
                                                            const float* __restrict__ out, const float* __restrict__ y,
                                                            const float* __restrict__ mean, float* __restrict__ dz,
-                                                           float* __restrict__ part) {
+                                                           float* __restrict__ part, float* __restrict__ pmax,
+                                                           unsigned* __restrict__ bound_reset) {
     __shared__ float red[2][256 * 4 * G];
     const int C4 = C >> 2;
     const int tpr = C4 / G;          // threads per row
@@ -33,11 +36,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
     const int rl = tid / tpr, cg = tid - rl * tpr;
     const long m0 = (long)blockIdx.x * BNB_TILE;
     const long m1 = min(M, m0 + BNB_TILE);
-    f32x4 s[G], q[G], mu[G];
+    if (MAXIMA && bound_reset && blockIdx.x == 0 && tid == 0) *bound_reset = 0u;
+    f32x4 s[G], q[G], mu[G], xd[G], xv[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         s[k] = f32x4{0.f, 0.f, 0.f, 0.f};
         q[k] = s[k];
+        xd[k] = s[k];
+        xv[k] = s[k];
         mu[k] = *(const f32x4*)(mean + 4 * (cg + k * tpr));
     }
     for (long m = m0 + rl; m < m1; m += rpar) {
@@ -56,6 +62,10 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
             for (int e = 0; e < 4; ++e) {
                 s[k][e] += d[e];
                 q[k][e] += d[e] * (v[e] - mu[k][e]);
+                if constexpr (MAXIMA) {
+                    xd[k][e] = fmaxf(xd[k][e], fabsf(d[e]));
+                    xv[k][e] = fmaxf(xv[k][e], fabsf(v[e] - mu[k][e]));
+                }
             }
         }
     }
@@ -78,6 +88,27 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
         part[((long)blockIdx.x * C + c) * 2] = a;
         part[((long)blockIdx.x * C + c) * 2 + 1] = b;
     }
+    if constexpr (MAXIMA) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < G; ++k)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int c = 4 * (cg + k * tpr) + e;
+                red[0][rl * C + c] = xd[k][e];
+                red[1][rl * C + c] = xv[k][e];
+            }
+        __syncthreads();
+        for (int c = tid; c < C; c += 256) {
+            float a = 0.f, b = 0.f;
+            for (int r = 0; r < rpar; ++r) {
+                a = fmaxf(a, red[0][r * C + c]);
+                b = fmaxf(b, red[1][r * C + c]);
+            }
+            pmax[((long)blockIdx.x * C + c) * 2] = a;
+            pmax[((long)blockIdx.x * C + c) * 2 + 1] = b;
+        }
+    }
 }
 
 // per channel: dgamma, dbeta, and the apply coefficients (grad_mean, k, invstd*gamma)
@@ -85,12 +116,13 @@ template <int CPB>
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
                                                              const float* __restrict__ mi, const float* gamma,
                                                              float* dgamma, float* dbeta, float* coef,
-                                                             unsigned* amax_reset) {
+                                                             const float* __restrict__ pmax, unsigned* amax) {
     constexpr int TL = 256 / CPB;
     __shared__ double red[4][8];
+    __shared__ float bmax[8];
     const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
     const bool ok = c < C;
-    if (amax_reset && blockIdx.x == 0 && threadIdx.x == 0) *amax_reset = 0u;
+    if (!pmax && amax && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;   // apply's atomicMax starts from 0
     double s = 0.0, d = 0.0;
     if (ok)   // 8 loads in flight per batch (latency-bound loop); zero-filled past the end
         for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
@@ -108,14 +140,36 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, lon
         }
     const double S = lanes_sum_d<CPB>(s, red);
     const double D = lanes_sum_d<CPB>(d, red);
+    double md = 0.0, mv = 0.0;
+    if (pmax) {   // per-channel maxima over the tiles (max: any order is exact)
+        if (ok)
+            for (long t = tl; t < tiles; t += TL) {
+                const float2 v = *(const float2*)(pmax + (t * C + c) * 2);
+                md = fmax(md, (double)v.x);
+                mv = fmax(mv, (double)v.y);
+            }
+        md = lanes_max_d<CPB>(md, red);
+        mv = lanes_max_d<CPB>(mv, red);
+    }
     if (tl == 0 && ok) {
         const double inv = (double)mi[C + c];
         const float gm = gamma ? gamma[c] : 1.f;
         if (dgamma) dgamma[c] = (float)(D * inv);
         if (dbeta) dbeta[c] = (float)S;
-        coef[c] = (float)(S / (double)M);                 // grad_mean
-        coef[C + c] = (float)(D * inv * inv / (double)M);  // k
-        coef[2 * C + c] = (float)(inv * (double)gm);       // invstd * gamma
+        const float cg = (float)(S / (double)M), ck = (float)(D * inv * inv / (double)M), cs = (float)(inv * (double)gm);
+        coef[c] = cg;                 // grad_mean
+        coef[C + c] = ck;             // k
+        coef[2 * C + c] = cs;         // invstd * gamma
+        if (pmax)   // |dy| <= (max|dz| + |gm| + max|y-mean|*|k|) * |invstd*gamma|, with slack for fp32 rounding
+            bmax[cl] = (float)((md + fabs((double)cg) + mv * fabs((double)ck)) * fabs((double)cs) * 1.0001);
+    }
+    if (pmax && amax) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float b = 0.f;
+            for (int i = 0; i < CPB && blockIdx.x * CPB + i < C; ++i) b = fmaxf(b, bmax[i]);
+            atomicMax(amax, __float_as_uint(b));   // the word was zeroed by the reduce kernel
+        }
     }
 }
 
@@ -124,14 +178,18 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, lon
 // is capped at 512 blocks since same-address device atomics serialise) — the
 // power-of-two scale of the f16x3 backward convs' gradient operand, so they need
 // no separate absmax pass over dy
-template <bool MASK, bool AMAX>
+// SPLIT: dy is written as the packed f16x3 split of dy * 2^e, e from the upper
+// bound finalize left in *amax (the operand of the x3 backward convs, which need
+// no separate hkp_split_pack_x3 pass); the fp32 dy only if dy != NULL
+template <bool MASK, bool AMAX, bool SPLIT = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, const f32x4* __restrict__ g,
                                                           const f32x4* __restrict__ out, const f32x4* __restrict__ y,
                                                           const f32x4* __restrict__ mean,
                                                           const f32x4* __restrict__ coef, f32x4* __restrict__ dy,
-                                                          unsigned* __restrict__ amax) {
+                                                          unsigned* __restrict__ amax, _Float16* __restrict__ dsplit) {
     const long stride = (long)gridDim.x * blockDim.x;
     unsigned mx = 0;
+    const float gsc = SPLIT ? pow2_scale_for(amax) : 1.f;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         const int c4 = (int)(i % C4);
         f32x4 d = g[i];
@@ -144,7 +202,13 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, cons
         f32x4 r;
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[e] = ((d[e] - gm[e]) - (v[e] - mu[e]) * kk[e]) * sc[e];
-        dy[i] = r;
+        if (!SPLIT || dy) dy[i] = r;
+        if constexpr (SPLIT) {
+            f32x4 rs;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rs[e] = r[e] * gsc;
+            store_split4(rs, i, dsplit, 3);
+        }
         if constexpr (AMAX) {
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -224,35 +288,41 @@ using namespace hkp;
 extern "C" int64_t hkp_bn_bwd_tiles(int64_t m) { return (m + BNB_TILE - 1) / BNB_TILE; }
 
 extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                                 const float* mean_invstd, float* dz, float* partials, hkp_stream_t stream) {
+                                 const float* mean_invstd, float* dz, float* partials, float* maxima,
+                                 uint32_t* dy_bound_bits, hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_reduce: bad sizes");
     HKP_CHECK_ARG(g && y && mean_invstd && partials, "hkp_bn_bwd_reduce: null tensor");
     const int C4 = c / 4;
     HKP_CHECK_ARG((C4 <= 256 && 256 % C4 == 0) || C4 == 512, "hkp_bn_bwd_reduce: unsupported C=%d", c);
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     hipStream_t st = as_stream(stream);
-#define HKP_BNR(G, MK)                                                                                              \
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<G, MK>), dim3((unsigned)tiles), dim3(256), 0, st, (long)m, c, g, out_mask, \
-                       y, mean_invstd, dz, partials)
+    HKP_CHECK_ARG(!dy_bound_bits || maxima, "hkp_bn_bwd_reduce: dy_bound_bits needs maxima");
+#define HKP_BNR(G, MK, MX)                                                                                          \
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<G, MK, MX>), dim3((unsigned)tiles), dim3(256), 0, st, (long)m, c, g,   \
+                       out_mask, y, mean_invstd, dz, partials, maxima, (unsigned*)dy_bound_bits)
+#define HKP_BNR2(G, MK)                  \
+    if (maxima) HKP_BNR(G, MK, true);    \
+    else HKP_BNR(G, MK, false)
     if (C4 == 512) {
-        if (out_mask) HKP_BNR(2, true); else HKP_BNR(2, false);
+        if (out_mask) { HKP_BNR2(2, true); } else { HKP_BNR2(2, false); }
     } else {
-        if (out_mask) HKP_BNR(1, true); else HKP_BNR(1, false);
+        if (out_mask) { HKP_BNR2(1, true); } else { HKP_BNR2(1, false); }
     }
+#undef HKP_BNR2
 #undef HKP_BNR
     HKP_LAUNCH_CHECK("hkp_bn_bwd_reduce");
     return HKP_OK;
 }
 
-extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd,
-                                   const float* gamma, float* dgamma, float* dbeta, float* coef,
-                                   uint32_t* dy_amax_reset, hkp_stream_t stream) {
+extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* maxima,
+                                   const float* mean_invstd, const float* gamma, float* dgamma, float* dbeta,
+                                   float* coef, uint32_t* dy_amax_bits, hkp_stream_t stream) {
     HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     const int cpb = partials_cpb(c);
 #define HKP_BFIN(CPB)                                                                                             \
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<CPB>, dim3((c + CPB - 1) / CPB), dim3(256), 0, as_stream(stream), c, \
-                       (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, (unsigned*)dy_amax_reset)
+                       (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, maxima, (unsigned*)dy_amax_bits)
     if (cpb == 8) HKP_BFIN(8);
     else if (cpb == 4) HKP_BFIN(4);
     else if (cpb == 2) HKP_BFIN(2);
@@ -264,22 +334,27 @@ extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, 
 
 extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
                                 const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
-                                hkp_stream_t stream) {
+                                uint16_t* dy_split, hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_apply: bad sizes");
-    HKP_CHECK_ARG(g && y && mean_invstd && coef && dy, "hkp_bn_bwd_apply: null tensor");
+    HKP_CHECK_ARG(g && y && mean_invstd && coef && (dy || dy_split), "hkp_bn_bwd_apply: null tensor");
+    HKP_CHECK_ARG(!dy_split || (dy_amax_bits && c % 32 == 0), "hkp_bn_bwd_apply: dy_split needs the bound and c%%32==0");
     const long n4 = m * (long)c / 4;
     hipStream_t st = as_stream(stream);
-#define HKP_BWD_APPLY(MASK, AMAX)                                                                                    \
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<MASK, AMAX>), dim3(AMAX ? std::min(grid_cap(n4), 512) : grid_cap(n4)), \
-                       dim3(256), 0, st, n4, c / 4,                                                                \
+#define HKP_BWD_APPLY3(MASK, AMAX, SPLIT)                                                                            \
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<MASK, AMAX, SPLIT>),                                                    \
+                       dim3(AMAX ? std::min(grid_cap(n4), 512) : grid_cap(n4)), dim3(256), 0, st, n4, c / 4,       \
                        (const f32x4*)g, (const f32x4*)out_mask, (const f32x4*)y, (const f32x4*)mean_invstd,       \
-                       (const f32x4*)coef, (f32x4*)dy, (unsigned*)dy_amax_bits)
-    if (out_mask) {
+                       (const f32x4*)coef, (f32x4*)dy, (unsigned*)dy_amax_bits, (_Float16*)dy_split)
+#define HKP_BWD_APPLY(MASK, AMAX) HKP_BWD_APPLY3(MASK, AMAX, false)
+    if (dy_split) {
+        if (out_mask) HKP_BWD_APPLY3(true, false, true); else HKP_BWD_APPLY3(false, false, true);
+    } else if (out_mask) {
         if (dy_amax_bits) HKP_BWD_APPLY(true, true); else HKP_BWD_APPLY(true, false);
     } else {
         if (dy_amax_bits) HKP_BWD_APPLY(false, true); else HKP_BWD_APPLY(false, false);
     }
 #undef HKP_BWD_APPLY
+#undef HKP_BWD_APPLY3
     HKP_LAUNCH_CHECK("hkp_bn_bwd_apply");
     return HKP_OK;
 }

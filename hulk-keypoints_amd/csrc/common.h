@@ -108,4 +108,15 @@ __device__ __forceinline__ double lanes_sum_d(double v, double (*red)[8]) {
     return (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
 }
 
+template <int CPB>
+__device__ __forceinline__ double lanes_max_d(double v, double (*red)[8]) {
+#pragma unroll
+    for (int o = CPB; o < 64; o <<= 1) v = fmax(v, __shfl_xor(v, o));
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, cl = threadIdx.x % CPB;
+    __syncthreads();
+    if (lane < CPB) red[wid][lane] = v;
+    __syncthreads();
+    return fmax(fmax(red[0][cl], red[1][cl]), fmax(red[2][cl], red[3][cl]));
+}
+
 }  // namespace hkp

@@ -336,21 +336,36 @@ def _side_stream(dev):
     return s
 
 
-def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
-    """wgrad (+ dgrad with the residual addend fused) for one NHWC conv."""
-    st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
-    c, k = x.shape[-1], dy.shape[-1]
+def _x3_backward(conv, x):
+    """Whether conv's backward runs entirely on the packed f16x3 path (x carries its
+    split; dgrad stride 1, or stride 2 without dilation) — then the BN backward
+    feeding it writes dy directly as the packed split (bn_bwd split_only)."""
     xs = ops.split_of(x)
-    if _precision == "f16x3" and xs is not None and xs[1] == 3 and k % 64 == 0 and c % 64 == 0:
+    k, c = conv.weight.shape[0], conv.weight.shape[-1]
+    st, dl = _i(conv.stride), _i(conv.dilation)
+    return (_precision == "f16x3" and xs is not None and xs[1] == 3 and k % 64 == 0 and c % 64 == 0
+            and (st == 1 or (st == 2 and dl == 1)))
+
+
+def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
+    """wgrad (+ dgrad with the residual addend fused) for one NHWC conv.  dy: fp32, or
+    (x3 path) already the packed scaled split from bn_bwd(split_only=True)."""
+    st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
+    c, k = x.shape[-1], conv.weight.shape[0]
+    xs = ops.split_of(x)
+    if _x3_backward(conv, x):
         # packed split operands: dy split once (scaled by a power of two from
-        # max|dy|) and read by both the dgrad and the wgrad conv
-        amax = getattr(dy, "_hkp_amax", None)     # fused into bn_bwd_apply
-        if amax is None:
-            amax = ops.absmax(dy)
-        dys = ops.split_pack_x3(dy, amax)
+        # max|dy| or its bound) and read by both the dgrad and the wgrad conv
+        amax = getattr(dy, "_hkp_amax", None)     # fused into the BN backward
+        if dy.dtype == torch.float16:
+            dys = dy
+        else:
+            if amax is None:
+                amax = ops.absmax(dy)
+            dys = ops.split_pack_x3(dy, amax)
         ready = None
         if OVERLAP_WGRAD:
-            main, side = torch.cuda.current_stream(dy.device), _side_stream(dy.device)
+            main, side = torch.cuda.current_stream(dys.device), _side_stream(dys.device)
             side.wait_stream(main)                     # dy split (and x split) written
             with torch.cuda.stream(side):
                 dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
@@ -364,12 +379,10 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
             if st == 1:
                 wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
                 dx = ops.conv2d_bwd_data_x3(dys, wfs, tuple(x.shape), pd, dl, add=add, amax=amax)
-            elif st == 2 and dl == 1:      # one stride-1 conv per output phase of dx
+            else:                          # stride 2: one stride-1 conv per output phase of dx
                 phs = _cached_split(conv.weight, "phase_x3", lambda t: ops.weight_phase_pack_x3(t, pd))
                 dx = ops.conv2d_bwd_data_x3_strided(dys, phs, tuple(x.shape), tuple(conv.weight.shape), pd, add=add,
                                                     amax=amax)
-            else:
-                dx = ops.conv2d_bwd_data(dy, ops.conv_weight_flip(conv.weight), tuple(x.shape), st, pd, dl, add=add)
         if ready is None:
             dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
         grads.put(conv.weight, dw, ready)
@@ -392,9 +405,9 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
     return dx
 
 
-def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False):
+def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False, split_only=False):
     dy, dgamma, dbeta, dz = ops.bn_bwd(g, out_mask, y, mi, bn.weight, want_dz=want_dz,
-                                       want_amax=_precision == "f16x3")
+                                       want_amax=_precision == "f16x3", split_only=split_only)
     grads.put(bn.weight, dgamma)
     grads.put(bn.bias, dbeta)
     return dy, dz
@@ -407,16 +420,22 @@ def block_backward(block, rec, g_out, grads):
     bns = [block.bn1, block.bn2] + ([block.bn3] if block.kind == "bottleneck" else [])
     convs = [block.conv1, block.conv2] + ([block.conv3] if block.kind == "bottleneck" else [])
     # last BN: relu mask from the block output; keep dz for the residual branch
-    g, dz = _bn_backward(bns[-1], g_out, out, ys[-1], mis[-1], grads, want_dz=True)
+    # a BN backward whose dy only feeds an x3 conv writes it as that conv's split
+    ins = [x] + list(acts)                 # input of convs[i]
+    g, dz = _bn_backward(bns[-1], g_out, out, ys[-1], mis[-1], grads, want_dz=True,
+                         split_only=_x3_backward(convs[-1], ins[len(convs) - 1]))
     if block.downsample is not None:
-        gd, _ = _bn_backward(block.downsample[1], dz, None, rec["yd"], rec["md"], grads)
-        dx_res = _conv_backward(block.downsample[0], x, gd, grads)
+        ds = block.downsample[0]
+        gd, _ = _bn_backward(block.downsample[1], dz, None, rec["yd"], rec["md"], grads,
+                             split_only=_x3_backward(ds, x))
+        dx_res = _conv_backward(ds, x, gd, grads)
     else:
         dx_res = dz
     # main path, last conv first; inner BN masks come from the stored activations
     for li in range(len(convs) - 1, 0, -1):
         da = _conv_backward(convs[li], acts[li - 1], g, grads)
-        g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads)
+        g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads,
+                            split_only=_x3_backward(convs[li - 1], ins[li - 1]))
     return _conv_backward(convs[0], x, g, grads, add=dx_res)
 
 

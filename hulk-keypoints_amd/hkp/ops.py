@@ -730,32 +730,43 @@ def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out
     return dw
 
 
-def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False):
+def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, split_only=False):
     """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None).
     want_amax: max|dy| (uint32 IEEE bits, as absmax) is computed in the same pass
-    and attached as dy._hkp_amax."""
+    and attached as dy._hkp_amax.  split_only: dy is returned as the packed f16x3
+    split of dy * 2^e (the x3 backward convs' operand, _hkp_split_passes = 3) with
+    2^e from an upper bound of max|dy| (attached as _hkp_amax, the scale's source);
+    no fp32 dy is written."""
     _need(g, torch.float32, "bn_bwd.g")
     _need(y, torch.float32, "bn_bwd.y")
     if g.shape != y.shape or (out_mask is not None and out_mask.shape != y.shape):
         raise HkpError("bn_bwd: shape mismatch")
     c = y.shape[-1]
     m = y.numel() // c
+    if split_only and c % 32:
+        raise HkpError("bn_bwd: split_only needs C % 32 == 0")
     from ._lib import lib
     tiles = lib().hkp_bn_bwd_tiles(m)
     part = torch.empty((tiles, c, 2), device=y.device, dtype=torch.float32)
+    maxima = torch.empty((tiles, c, 2), device=y.device, dtype=torch.float32) if split_only else None
+    amax = torch.empty(1, device=y.device, dtype=torch.int32) if (want_amax or split_only) else None
     dz = torch.empty_like(y) if want_dz else None
     call("hkp_bn_bwd_reduce", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(dz), _ptr(part),
-         _stream())
+         _ptr(maxima), _ptr(amax if split_only else None), _stream())
     dgamma = torch.empty(c, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(c, device=y.device, dtype=torch.float32)
     coef = torch.empty(3 * c, device=y.device, dtype=torch.float32)
-    amax = torch.empty(1, device=y.device, dtype=torch.int32) if want_amax else None
-    call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta),
-         _ptr(coef), _ptr(amax), _stream())
-    dy = torch.empty_like(y)
-    call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), _ptr(dy),
-         _ptr(amax), _stream())
-    if want_amax:
+    call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(maxima), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma),
+         _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
+    if split_only:
+        dy = _split_out(y.shape, y.device, 3)
+        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), None,
+             _ptr(amax), _ptr(dy), _stream())
+    else:
+        dy = torch.empty_like(y)
+        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), _ptr(dy),
+             _ptr(amax), None, _stream())
+    if want_amax or split_only:
         dy._hkp_amax = amax
     return dy, dgamma, dbeta, dz
 

@@ -312,22 +312,29 @@ int hkp_conv2d_bwd_filter(const hkp_conv_desc* d, const float* x, const float* d
 
 /* Train-mode BatchNorm backward, three launches:
  *   reduce:   dz = g * (out_mask > 0) (out_mask NULL: dz = g), optionally stored to dz;
- *             partials[tiles][c][2] = (sum dz, sum dz*(y-mean)); tiles = hkp_bn_bwd_tiles(m)
- *   finalize: dgamma = invstd*sum dz*(y-mean), dbeta = sum dz (nullable), coef[3c]
+ *             partials[tiles][c][2] = (sum dz, sum dz*(y-mean)); tiles = hkp_bn_bwd_tiles(m);
+ *             maxima (nullable) [tiles][c][2] = (max|dz|, max|y-mean|), and then
+ *             dy_bound_bits (nullable) is zeroed for finalize
+ *   finalize: dgamma = invstd*sum dz*(y-mean), dbeta = sum dz (nullable), coef[3c];
+ *             with maxima: dy_amax_bits receives an upper bound of max|dy|,
+ *             (max|dz| + |mean dz| + max|y-mean|*|k|) * |invstd*gamma|; without:
+ *             dy_amax_bits (nullable) is reset to 0 for apply's exact max
  *   apply:    dy = ((dz - sum dz/m) - (y-mean)*invstd^2*sum dz*(y-mean)/m) * invstd*gamma
- * mean_invstd is what hkp_bn_finalize produced in the forward.  apply also folds
- * max|dy| (IEEE bits, as hkp_absmax) into dy_amax_bits when non-NULL — the scale
- * input of hkp_split_pack_x3 for the f16x3 backward convs; the word must hold 0
- * on entry, which finalize's dy_amax_reset (nullable) sets in the same stream
- * order (no separate memset). */
+ *             dy_split (nullable): dy written as the packed f16x3 split of dy*2^e,
+ *             2^e = the power of two of the bound in dy_amax_bits — the gradient
+ *             operand of the x3 backward convs, with no hkp_split_pack_x3 pass and
+ *             dy (fp32) optional; else dy_amax_bits (nullable) gets the exact max|dy|.
+ * mean_invstd is what hkp_bn_finalize produced in the forward. */
 int64_t hkp_bn_bwd_tiles(int64_t m);
 int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                      const float* mean_invstd, float* dz, float* partials, hkp_stream_t stream);
-int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* mean_invstd, const float* gamma,
-                        float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_reset, hkp_stream_t stream);
+                      const float* mean_invstd, float* dz, float* partials, float* maxima, uint32_t* dy_bound_bits,
+                      hkp_stream_t stream);
+int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* maxima, const float* mean_invstd,
+                        const float* gamma, float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_bits,
+                        hkp_stream_t stream);
 int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
                      const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
-                     hkp_stream_t stream);
+                     uint16_t* dy_split, hkp_stream_t stream);
 
 /* ----------------------------------------------------------- optimizer ---- */
 /* Fused multi-tensor Adam with L2 weight decay (replaces the

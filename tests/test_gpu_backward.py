@@ -105,6 +105,15 @@ def test_bn_backward(cuda_device, mask, c):
     assert (dbeta.cpu() - beta.grad).abs().max() < 1e-4 * max(1, beta.grad.abs().max().item())
     ref_dz = g * (out.detach() > 0) if mask else g
     assert torch.equal(nchw(dz.cpu()), ref_dz)
+    if c % 32 == 0:   # split-only dy: bound >= max|dy|, and exactly split_pack_x3(dy, bound)
+        dys, dg2, db2, _ = ops.bn_bwd(nhwc(g).to(d), out_d if mask else None, y_d, mi, gamma.detach().to(d),
+                                      split_only=True)
+        bound = dys._hkp_amax
+        assert dys.dtype == torch.float16 and dys._hkp_split_passes == 3
+        assert bound.view(torch.float32).item() >= dy.abs().max().item()
+        assert bound.view(torch.float32).item() <= 8 * dy.abs().max().item() + 1e-30
+        assert torch.equal(dys, ops.split_pack_x3(dy, bound))
+        assert torch.equal(dg2, dgamma) and torch.equal(db2, dbeta)
 
 
 def test_maxpool_backward(cuda_device):
@@ -347,8 +356,8 @@ def test_backward_calls_exact(cuda_device, bb, k):
         log.append(("conv", conv, xx, dy, add, dx, grads[conv.weight]))
         return dx
 
-    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False):
-        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz)
+    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False, split_only=False):
+        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz, split_only)
         log.append(("bn", bn, gr, mask, y, mi, dy, grads[bn.weight], grads[bn.bias]))
         return dy, dz
 
@@ -363,9 +372,26 @@ def test_backward_calls_exact(cuda_device, bb, k):
     def rel(a, b):
         return ((a.double().cpu() - b).abs().max() / (b.abs().max() + 1e-30)).item()
 
+    n_split = 0
+
+    def dense(dy):
+        """fp32 view of a dy: a split-only dy (packed hi|lo of dy * 2^e, 2^e from the
+        bound in _hkp_amax) is decoded as (hi + lo) / 2^e (2^-22 relative)."""
+        nonlocal n_split
+        if dy.dtype != torch.float16:
+            return dy
+        n_split += 1
+        g = dy.reshape(*dy.shape[:-1], dy.shape[-1] // 64, 2, 32).double()
+        v = (g[..., 0, :] + g[..., 1, :]).reshape(*dy.shape[:-1], -1)
+        bound = dy._hkp_amax.view(torch.float32).item()
+        assert bound > 0
+        _, e = np.frexp(bound)
+        return v / 2.0 ** (14 - int(e))
+
     for rec in log:
         if rec[0] == "conv":
             _, conv, xx, dy, add, dx, dw = rec
+            dy = dense(dy)
             st, pd, dl = net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation)
             w = conv.weight.detach().double().cpu().permute(0, 3, 1, 2)
             xc, dyc = xx.double().cpu().permute(0, 3, 1, 2), dy.double().cpu().permute(0, 3, 1, 2)
@@ -384,5 +410,9 @@ def test_backward_calls_exact(cuda_device, bb, k):
             n = yc.shape[0]
             db, dgm = dz.sum(0), (dz * xh).sum(0)
             rdy = bn.weight.detach().double().cpu() * inv * (dz - db / n - xh * dgm / n)
-            assert rel(dy.reshape(-1, c), rdy) < 1e-5
+            dyd = dense(dy)
+            assert rel(dyd.reshape(-1, c), rdy) < 1e-5
+            if dy.dtype == torch.float16:        # the bound really bounds max|dy|
+                assert dy._hkp_amax.view(torch.float32).item() >= rdy.abs().max().item()
             assert rel(dgam, dgm) < 1e-5 and rel(dbet, db) < 1e-5
+    assert n_split > 0                           # the fused split-only BN backward was exercised
