@@ -107,11 +107,221 @@ __device__ __forceinline__ void interleave() {
     if constexpr (NM > per * nr) __builtin_amdgcn_sched_group_barrier(0x008, NM - per * nr, 0);
 }
 
+// NHWC offset of output (row m, channel n) of a launch (-1: row past M); strided
+// dgrad writes one output phase per launch
+__device__ __forceinline__ long x3_out_off(const X3Args& a, int m, int n) {
+    if (m >= a.M) return -1;
+    long pix = m;
+    if (a.ost) {
+        const int hw = a.Ho * a.Wo, ni = m / hw, rem = m - ni * hw;
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+        pix = ((long)ni * a.OH + ho * a.ost + a.oy) * a.OW + wo * a.ost + a.ox;
+    }
+    return pix * a.K + n;
+}
+
+// Mainloop + epilogue of conv_x3_kernel<BN, 2, false, 0, 16>: 16x16x32 MFMAs, one
+// k32 step per 32-channel stage (LDS ring, DMA issue and the swizzled 128-B rows
+// exactly as the 32x32 path).  Wave tile 64 x BN/2 = UM x UN 16x16 tiles.
+// Fragment read: lane reads row (lane & 15) of a 16-row tile, 16-B chunk
+// (lane >> 4) (hi) / 4 + (lane >> 4) (lo): with the (row >> 1) & 7 chunk swizzle
+// every ds_read_b128 lane group covers the 64 banks once.  Output fragment:
+// lane holds column (lane & 15), rows 4 * (lane >> 4) + 0..3.
+// Pipeline per K-step t (as the 16-channel-stage path): [issue DMA t+NST-1]
+// wait own DMA of t+1 (+ this wave's reads of t), barrier, [read A frags of t+1]
+// then per column block j: [MFMAs of t with B_j] [refill B_j with t+1's].
+template <int BN, int NST, int STAGE, int GL, typename Issue>
+__device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int m0, int n0, int wm, int wn,
+                                                  int lane, int tid, Issue& issue_next) {
+    constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
+    constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
+    const int nks = a.nks;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int sw = (r16 >> 1) & 7;                 // the DMA's swizzle of every row ≡ r16 (mod 16)
+    const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
+    const int a_base = (wm * UM * 16) * ROW, b_base = (BM + wn * UN * 16) * ROW;
+
+    f32x4 acc[UM][UN];
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    struct FA {
+        f16x8 h[UM], l[UM];
+    };
+    f16x8 bh[UN], bl[UN];
+    auto read_a = [&](FA& f, const char* st) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            f.h[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_h);
+            f.l[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_l);
+        }
+    };
+    auto read_b = [&](int j, const char* st) {
+        bh[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_h);
+        bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
+    };
+    auto mma_col = [&](const FA& f, int j) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    };
+
+    // prologue: NST-1 stages in flight, stage 0 landed everywhere
+    issue_next();
+    for (int s = 1; s < NST - 1; ++s)
+        if (s < nks) issue_next();
+    {
+        const int after = std::min(nks - 1, NST - 2);
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    auto wait_next = [&](int t) {
+        const int after = std::min(nks - 1, t + NST - 1) - (t + 1);
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * GL) : "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    };
+    int cur = 0;
+    FA fa0, fa1;
+    read_a(fa0, smem);
+#pragma unroll
+    for (int j = 0; j < UN; ++j) read_b(j, smem);
+    auto step = [&](int t, FA& fc, FA& fn) {       // K-step t, reading t+1's fragments
+        if (t + NST - 1 < nks) issue_next();
+        wait_next(t);
+        lds_barrier();
+        cur = cur == NST - 1 ? 0 : cur + 1;
+        const char* st = smem + cur * STAGE;
+        read_a(fn, st);
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            mma_col(fc, j);
+            read_b(j, st);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 3 * UM, 0);  // column j's MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int t = 0;
+    for (; t + 2 < nks; t += 2) {
+        step(t, fa0, fa1);
+        step(t + 1, fa1, fa0);
+    }
+    if (t + 1 < nks) {
+        step(t, fa0, fa1);
+#pragma unroll
+        for (int j = 0; j < UN; ++j) mma_col(fa1, j);
+    } else {
+#pragma unroll
+        for (int j = 0; j < UN; ++j) mma_col(fa0, j);
+    }
+
+    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
+    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
+    const int rbase = m0 + wm * UM * 16 + 4 * q;
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+        const int n = n0 + wn * UN * 16 + j * 16 + r16;
+        const float sc = (a.wscale ? a.wscale[n] : 1.f) * ginv;
+        long off[UM][4];
+        float av[UM][4];
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) off[i][r] = x3_out_off(a, rbase + i * 16 + r, n);
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) av[i][r] = (a.add && off[i][r] >= 0) ? a.add[off[i][r]] : 0.f;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                acc[i][j][r] *= sc;
+                if (off[i][r] >= 0) a.y[off[i][r]] = a.add ? acc[i][j][r] + av[i][r] : acc[i][j][r];
+            }
+    }
+    if (a.part == nullptr) return;
+    __syncthreads();                       // every wave done reading the ring
+    float* red = (float*)smem;             // [WM][BN] column sums, then [2][BN] half-tile means
+    float* tmean = red + WM * BN;
+    float colsum[UN];
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s += (rbase + i * 16 + r < a.M) ? acc[i][j][r] : 0.f;
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        colsum[j] = s;
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < UN; ++j) red[wm * BN + wn * UN * 16 + j * 16 + lane] = colsum[j];
+    }
+    __syncthreads();
+    const long tile128 = (long)(m0 >> 7);
+    for (int e = tid; e < 2 * BN; e += 512) {
+        const int h = e / BN, c = e - h * BN;
+        const int cnt = min(128, a.M - (m0 + 128 * h));
+        if (cnt > 0) {
+            const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+            tmean[h * BN + c] = s / (float)cnt;
+            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
+        }
+    }
+    __syncthreads();
+    const float* mu_h = tmean + (wm >> 1) * BN;
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+        const float mu = mu_h[wn * UN * 16 + j * 16 + r16];
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = acc[i][j][r] - mu;
+                s += (rbase + i * 16 + r < a.M) ? d * d : 0.f;
+            }
+        s += __shfl_xor(s, 16);
+        s += __shfl_xor(s, 32);
+        colsum[j] = s;
+    }
+    __syncthreads();
+    if (lane < 16) {
+#pragma unroll
+        for (int j = 0; j < UN; ++j) red[wm * BN + wn * UN * 16 + j * 16 + lane] = colsum[j];
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += 512) {
+        const int h = e / BN, c = e - h * BN;
+        if (a.M - (m0 + 128 * h) > 0)
+            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+    }
+}
+
 // STEM: the 7x7/s2 stem on the zero-padded NHWC4 image planes of
 // hkp_stem_pack_x3 (a.H/a.W = padded size, stride 2, pad 0, R = 7, S = 1: one
 // K-step per filter row = 8 taps x 4 channels; logical chunk j of a row holds
 // padded pixels 2wo+2j, 2wo+2j+1 from the hi plane (j < 4) or the lo plane).
-template <int BN, int KH, bool STEM = false, int ORD = 0>
+// MFD: MFMA shape, 32 = v_mfma_f32_32x32x16_f16 (two k16 slices per 32-channel
+// stage), 16 = v_mfma_f32_16x16x32_f16 (one k32 step per stage; same cycles per
+// FLOP, lower power per FLOP, so the chip holds a higher clock under load —
+// MI355X_MICROARCH.md "DVFS give-back" item 7).
+template <int BN, int KH, bool STEM = false, int ORD = 0, int MFD = 32>
 __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -126,6 +336,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
+    static_assert(MFD == 32 || (MFD == 16 && KH == 2 && !STEM && BN <= 128), "bad conv_x3 MFMA shape");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
 
@@ -212,6 +423,11 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
             ++q_cc;
         }
     };
+
+    if constexpr (MFD == 16) {
+        conv_x3_mf16_body<BN, NST, STAGE, GL>(a, smem, m0, n0, wm, wn, lane, tid, issue_next);
+        return;
+    }
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -471,22 +687,21 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         const int n = n0 + wn * TN * 32 + j * 32 + frow;
         const float sc = (a.wscale ? a.wscale[n] : 1.f) * ginv;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) {
+            // output offsets of the fragment's 16 rows (-1: past M), then all its
+            // addend loads in flight at once (one exposed latency per fragment)
+            long off[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) off[r] = x3_out_off(a, rbase + i * 32 + (r & 3) + 8 * (r >> 2), n);
+            float av[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) av[r] = (a.add && off[r] >= 0) ? a.add[off[r]] : 0.f;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 acc[i][j][r] *= sc;
-                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                if (m < a.M) {
-                    long pix = m;
-                    if (a.ost) {                   // strided dgrad: one output phase per launch
-                        const int hw = a.Ho * a.Wo, ni = m / hw, rem = m - ni * hw;
-                        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-                        pix = ((long)ni * a.OH + ho * a.ost + a.oy) * a.OW + wo * a.ost + a.ox;
-                    }
-                    const long off = pix * a.K + n;
-                    a.y[off] = a.add ? acc[i][j][r] + a.add[off] : acc[i][j][r];
-                }
+                if (off[r] >= 0) a.y[off[r]] = a.add ? acc[i][j][r] + av[r] : acc[i][j][r];
             }
+        }
     }
     if (a.part == nullptr) return;
     __syncthreads();                       // every wave done reading the ring
@@ -997,7 +1212,8 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
 // Tuning knob (hkp_set_conv_variant; results agree to fp32 summation order, in
 // practice bit-identical): 0 = policy, 1 = 256x128 32-ch stages only,
 // 2 = 256x128 16-ch stages (4-stage ring), 3 = 256x256 32-ch stages whenever
-// Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0, 5 = 256x64.
+// Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0, 5 = 256x64,
+// 6 = 16x16x32 MFMAs with 256x128 tiles (256x64 when Cout % 128), 7 = 16x16x32 256x64.
 static int g_x3_variant = [] {
     const char* e = getenv("HKP_X3_VARIANT");
     return e ? atoi(e) : 0;
@@ -1031,9 +1247,14 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a) {
     if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
     if (v == 5) bn = 64;
     if ((v == 4 && bn == 256) || (v == 2 && bn == 128)) kh = 1;
+    const bool mf16 = v == 6 || v == 7;
+    if (mf16) bn = (v == 7 || k % 128) ? 64 : 128;
     a.n_tiles = k / bn;
     a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
     const dim3 grid((unsigned)(m_tiles * a.n_tiles));
+    if (mf16 && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
+    else if (mf16) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
+    else
     if (bn == 256 && kh == 2) hipLaunchKernelGGL((conv_x3_kernel<256, 2>), grid, dim3(512), 0, st, a);
     else if (bn == 256) hipLaunchKernelGGL((conv_x3_kernel<256, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128 && kh == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 1>), grid, dim3(512), 0, st, a);
@@ -1326,7 +1547,7 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
 extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m) { return k > 0 && m > 0 ? x3_tile_n(k, (m + 255) / 256) : -1; }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 6 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 8 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

@@ -152,8 +152,9 @@ X3_CASES = CASES + [
 @pytest.mark.parametrize("case", X3_CASES)
 def test_x3_conv_fp32_accurate(cuda_device, case):
     """The deep-pipelined packed-operand conv: fp32-class vs fp64, BN partials as the
-    fp32 kernel's, the 256x256 / 256x128 / 16-channel-stage tile variants agree to
-    fp32 summation order, and stats=False gives the same output."""
+    fp32 kernel's, the 256x256 / 256x128 / 16-channel-stage tile variants and the
+    16x16x32-MFMA variants agree to fp32 summation order, and stats=False gives
+    the same output."""
     from hkp import ops
     from hkp._lib import call
     n, h, w, cin, cout, k, st, pad, dil = case
@@ -173,7 +174,7 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
     try:
-        for var in (1, 2, 3, 4):
+        for var in (1, 2, 3, 4, 6, 7):
             call("hkp_set_conv_variant", var)
             yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
             assert (yv - y).abs().max().item() <= 1e-6 * scale
