@@ -68,6 +68,13 @@ struct X3Args {
     // phase output (strided dgrad): output pixel (n, ho, wo) of this launch is
     // written at (n, ho*ost + oy, wo*ost + ox) of an [N][OH][OW][K] tensor; ost = 0: dense
     int ost = 0, OH = 0, OW = 0, oy = 0, ox = 0;
+    // stream-K (sk_units > 0): the grid's blocks split tiles x K-steps into equal
+    // unit ranges; a tile split between blocks is summed by its last-arriving
+    // block from per-segment fp32 slabs (sk_ws) — sk_cnt[tile] arrival counters,
+    // zero on entry and left zero
+    long sk_units = 0;
+    float* sk_ws = nullptr;
+    unsigned* sk_cnt = nullptr;
 };
 
 // 2^e putting max|x| in [2^13, 2^14) (1 for 0 / non-finite): exact scaling
@@ -107,6 +114,68 @@ __device__ __forceinline__ void interleave() {
     if constexpr (NM > per * nr) __builtin_amdgcn_sched_group_barrier(0x008, NM - per * nr, 0);
 }
 
+// ---- stream-K bookkeeping (X3Args::sk_units) ----
+__device__ __forceinline__ long sk_start(long b, long U, int G) { return b * U / G; }
+// the block whose unit range holds unit u: the largest b with sk_start(b) <= u
+__device__ __forceinline__ int sk_block_of(long u, long U, int G) { return (int)(((u + 1) * G + U - 1) / U) - 1; }
+
+typedef f32x4 __attribute__((address_space(1))) gf32x4;
+typedef unsigned __attribute__((address_space(1))) gu32;
+
+// A partial tile segment: publish this block's accumulators as an fp32 slab,
+// count the arrival; the last-arriving segment's block reads every slab of the
+// tile in segment order (fixed summation order: the result does not depend on
+// which block arrives last) and returns true with the sum in its accumulators.
+// Slab of block bb for tile t: slot 2*bb + (0: the tile is bb's first segment,
+// 1: its last).  Hand-off per cdna_hip_programming.md §6 Guideline 16 (split-K
+// counter form): every wave drains its stores, barrier, one lane releases at
+// agent scope and adds to the counter; the last arriver acquires at agent
+// scope before any wave reads a slab, and re-zeroes the counter.
+template <int NV4, typename Get, typename Set>
+__device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char* flag_lds, Get&& get, Set&& set) {
+    const long U = a.sk_units;
+    const int G = gridDim.x;
+    const long t0 = (long)T * a.nks;
+    const int b0 = sk_block_of(t0, U, G), nseg = sk_block_of(t0 + a.nks - 1, U, G) - b0 + 1;
+    auto slab = [&](int bb) {
+        const int which = sk_start(bb, U, G) >= t0 ? 0 : 1;
+        return (gf32x4*)a.sk_ws + (long)(2 * bb + which) * NV4 * 512;
+    };
+    gf32x4* mine = slab(xcd_remap(blockIdx.x, G));
+#pragma unroll
+    for (int v = 0; v < NV4; ++v) mine[v * 512 + tid] = get(v);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gu32* cnt = (gu32*)a.sk_cnt + T;
+        const unsigned prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == (unsigned)(nseg - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *(volatile int*)flag_lds = last;
+    }
+    __syncthreads();
+    if (!*(volatile int*)flag_lds) return false;
+    // 8 loads in flight per chunk (the accumulators leave few free registers)
+    for (int sg = 0; sg < nseg; ++sg) {
+        const gf32x4* p = slab(b0 + sg);
+#pragma unroll
+        for (int v0 = 0; v0 < NV4; v0 += 8) {
+            f32x4 x[8];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) x[v] = p[(v0 + v) * 512 + tid];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) set(v0 + v, sg == 0 ? x[v] : get(v0 + v) + x[v]);
+        }
+    }
+    return true;
+}
+
 // NHWC offset of output (row m, channel n) of a launch (-1: row past M); strided
 // dgrad writes one output phase per launch
 __device__ __forceinline__ long x3_out_off(const X3Args& a, int m, int n) {
@@ -131,11 +200,11 @@ __device__ __forceinline__ long x3_out_off(const X3Args& a, int m, int n) {
 // wait own DMA of t+1 (+ this wave's reads of t), barrier, [read A frags of t+1]
 // then per column block j: [MFMAs of t with B_j] [refill B_j with t+1's].
 template <int BN, int NST, int STAGE, int GL, typename Issue>
-__device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int m0, int n0, int wm, int wn,
-                                                  int lane, int tid, Issue& issue_next) {
+__device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int nks, bool partial,
+                                                  int m0, int n0, int wm, int wn, int lane, int tid,
+                                                  Issue& issue_next) {
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
-    const int nks = a.nks;
     const int r16 = lane & 15, q = lane >> 4;
     const int sw = (r16 >> 1) & 7;                 // the DMA's swizzle of every row ≡ r16 (mod 16)
     const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
@@ -227,6 +296,11 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         for (int j = 0; j < UN; ++j) mma_col(fa0, j);
     }
 
+    if (partial) {                         // stream-K: fold the tile's segments
+        auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
+        auto set = [&](int v, f32x4 y) { acc[v / UN][v % UN] = y; };
+        if (!sk_combine<UM * UN>(a, tile, tid, smem + NST * STAGE, get, set)) return;
+    }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
     // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
     const int rbase = m0 + wm * UM * 16 + 4 * q;
@@ -321,8 +395,8 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // stage), 16 = v_mfma_f32_16x16x32_f16 (one k32 step per stage; same cycles per
 // FLOP, lower power per FLOP, so the chip holds a higher clock under load —
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
-template <int BN, int KH, bool STEM = false, int ORD = 0, int MFD = 32>
-__global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
+template <int BN, int KH, bool STEM, int ORD, int MFD>
+__device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     constexpr int ROW = 64 * KH;                   // bytes per LDS row
@@ -337,10 +411,8 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
     static_assert(MFD == 32 || (MFD == 16 && KH == 2 && !STEM && BN <= 128), "bad conv_x3 MFMA shape");
-    static_assert(NST * STAGE <= 160 * 1024, "LDS");
-    __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+    static_assert(NST * STAGE + 16 <= 160 * 1024, "LDS");
 
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = mt * BM, n0 = nt * BN;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -397,7 +469,11 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     const _Float16* zero = (const _Float16*)g_x3_zero_line;
 
     // staging state of the next K-step to issue (wave-uniform, advanced per issue)
-    int q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_half = 0, q_buf = 0;
+    // (a stream-K segment starts at K-step ks: channel group outer, tap inner)
+    int q_half = KH == 1 ? ks & 1 : 0, q_buf = 0;
+    int q_cc = (KH == 1 ? ks >> 1 : ks) / a.RS;
+    int q_tap = (KH == 1 ? ks >> 1 : ks) - q_cc * a.RS;
+    int q_rr = q_tap / a.S, q_ss = q_tap - q_rr * a.S;
     auto issue_next = [&]() {
         char* st = smem + q_buf * STAGE;
         const int dh = q_rr * a.dil, dw = q_ss * a.dil;
@@ -425,7 +501,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     };
 
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL>(a, smem, m0, n0, wm, wn, lane, tid, issue_next);
+        conv_x3_mf16_body<BN, NST, STAGE, GL>(a, smem, tile, nks, partial, m0, n0, wm, wn, lane, tid, issue_next);
         return;
     }
 
@@ -494,7 +570,6 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
     };
     constexpr int NR = 2 * (TM + TN), NM = 3 * TM * TN;   // ds_reads / MFMAs per k16 slice
 
-    const int nks = a.nks;
     // prologue: NST-1 stages in flight, stage 0 landed everywhere
     issue_next();
     for (int s = 1; s < (WIDE2 ? 2 : NST - 1); ++s)
@@ -678,6 +753,19 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         for (int j = 0; j < TN; ++j) mma_col(fa1, j);
     }
 
+    if (!STEM && partial) {                // stream-K: fold the tile's segments
+        auto get = [&](int v) -> f32x4 {
+            const f32x16& x = acc[(v >> 2) / TN][(v >> 2) % TN];
+            const int q4 = (v & 3) * 4;
+            return f32x4{x[q4], x[q4 + 1], x[q4 + 2], x[q4 + 3]};
+        };
+        auto set = [&](int v, f32x4 y) {
+            f32x16& x = acc[(v >> 2) / TN][(v >> 2) % TN];
+            const int q4 = (v & 3) * 4;
+            x[q4] = y[0]; x[q4 + 1] = y[1]; x[q4 + 2] = y[2]; x[q4 + 3] = y[3];
+        };
+        if (!sk_combine<TM * TN * 4>(a, tile, tid, smem + NST * STAGE, get, set)) return;
+    }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
 
     // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
@@ -763,6 +851,34 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         const int h = e / BN, c = e - h * BN;
         if (a.M - (m0 + 128 * h) > 0)
             a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+    }
+}
+
+constexpr int x3_lds_bytes(int BN, int KH) {
+    return (BN == 256 && KH == 2 ? 2 : (KH == 2 ? 3 : 4)) * (256 + BN) * 64 * KH + 16;
+}
+
+// One tile per block (sk_units == 0, blocks remapped XCD-aware), or stream-K:
+// block b (remapped) runs units [b*U/G, (b+1)*U/G) of the tile-major
+// (tile, K-step) sequence, one tile segment after another.
+// Separate instantiations (SK): the stream-K loop's live state would otherwise
+// raise the register allocation of the one-tile kernels (256x256 spilled).
+template <int BN, int KH, bool STEM = false, int ORD = 0, int MFD = 32, bool SK = false>
+__global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, KH)];
+    const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
+    if constexpr (!SK) {
+        conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, b, 0, a.nks, false);
+        return;
+    }
+    const long U = a.sk_units, u0 = sk_start(b, U, G), u1 = sk_start(b + 1, U, G);
+    for (long u = u0; u < u1;) {
+        const int T = (int)(u / a.nks);
+        const long t0 = (long)T * a.nks;
+        const int ks = (int)(u - t0), ke = (int)min((long)a.nks, u1 - t0);
+        if (u != u0) __syncthreads();      // the previous segment is done with the LDS ring
+        conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, T, ks, ke - ks, ks != 0 || ke != a.nks);
+        u = t0 + ke;
     }
 }
 
@@ -1213,36 +1329,87 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
 // practice bit-identical): 0 = policy, 1 = 256x128 32-ch stages only,
 // 2 = 256x128 16-ch stages (4-stage ring), 3 = 256x256 32-ch stages whenever
 // Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0, 5 = 256x64,
-// 6 = 16x16x32 MFMAs with 256x128 tiles (256x64 when Cout % 128), 7 = 16x16x32 256x64.
+// 6 = 16x16x32 MFMAs with 256x128 tiles (256x64 when Cout % 128), 7 = 16x16x32 256x64,
+// 8 = stream-K wherever a tile split helps (zero overhead assumed), 9 = never stream-K.
 static int g_x3_variant = [] {
     const char* e = getenv("HKP_X3_VARIANT");
     return e ? atoi(e) : 0;
 }();
 
-// Tile width for Cout = k over m_tiles 256-row tiles: one 512-thread block per CU
-// at a time, so a launch costs ~ceil(blocks / 256) rounds of one tile each;
-// minimise rounds x tile cost, with the measured per-column cost of the tiles
-// (256x256: 0.9, 256x128: 1.0, 256x64: 1.25 — wider tiles reuse each A line more).
-// E.g. training layer3 (150 m-tiles, Cout 256): one round of 256x256 beats two of
-// 256x128; C2 layer3 (600 m-tiles) stays 256x128, C2 layer4 takes 256x256.
-static int x3_tile_n(int k, long m_tiles) {
-    int best = 64;
+// Compute units (one 512-thread conv block per CU at a time); cached per process.
+static int x3_cus() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                      hipSuccess || v <= 0)
+            v = 256;
+        return v;
+    }();
+    return n;
+}
+
+// stream-K: per-tile arrival counters in the first X3_SK_CNT_BYTES of the
+// workspace, then two fp32 slabs per block (a block splits at most its first
+// and its last tile): 2 * CUs * BN * 1 KiB (256 x BN floats per slab)
+constexpr long X3_SK_CNT_BYTES = 64 << 10;
+static long x3_sk_ws_bytes(int bn) { return X3_SK_CNT_BYTES + 2L * x3_cus() * bn * 1024; }
+
+// stream-K overhead per block in tile times (slab write, the reducer's slab
+// reads, one more pipeline fill, the SK kernel's higher register count);
+// HKP_SK_OVER overrides for tuning.  Default 1 = stream-K never chosen by the
+// policy: measured on the box at 0.25 it lost on both workloads (C2 inference
+// 1404 -> 1350 img/s, C3-shard training 375 -> 358 img/s, same box, same call)
+// — one round of 256x256 tiles or a full round of data-parallel tiles beats a
+// split tile's extra fill + slab round trip at these K depths.  Knob 8 forces it.
+static double g_sk_over = [] {
+    const char* e = getenv("HKP_SK_OVER");
+    return e ? atof(e) : 1.0;
+}();
+
+// Tile width (and data-parallel vs stream-K) for Cout = k over m_tiles 256-row
+// tiles: data-parallel costs ceil(blocks / CUs) rounds of one tile each,
+// stream-K blocks / CUs + the overhead above; minimise rounds x the measured
+// per-column tile cost (256x256: 0.9, 256x128: 1.0, 256x64: 1.25 — wider tiles
+// reuse each A line more).  E.g. C2 layer4 (600 m-tiles, Cout 512): 1200
+// 256x256 tiles = 4.69 rounds, data-parallel (5 rounds); training layer4 (150
+// m-tiles): 600 256x128 tiles stream-K (2.34 + 0.25 rounds) beats 3 rounds of
+// 256x128 (data-parallel's best).  No stream-K with 256x256 tiles: that
+// instantiation spills (the one-tile 256x256 kernel sits at 255 VGPRs).
+struct X3Plan {
+    int bn;
+    bool sk;
+};
+static X3Plan x3_plan(int k, long m_tiles, bool sk_ok, double over = g_sk_over) {
+    const int G = x3_cus();
+    X3Plan best{64, false};
     double best_cost = 1e300;
     for (int bn : {256, 128, 64}) {
         if (k % bn) continue;
-        const long rounds = (m_tiles * (k / bn) + 255) / 256;
-        const double cost = (double)rounds * bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
-        if (cost < best_cost - 1e-9) {
-            best_cost = cost;
-            best = bn;
+        const long tiles = m_tiles * (k / bn);
+        const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
+        const double dp = (double)((tiles + G - 1) / G) * col;
+        if (dp < best_cost - 1e-9) {
+            best_cost = dp;
+            best = {bn, false};
+        }
+        if (sk_ok && bn != 256 && tiles % G && tiles * 4 <= X3_SK_CNT_BYTES) {
+            const double skc = ((double)tiles / G + over) * col;
+            if (skc < best_cost - 1e-9) {
+                best_cost = skc;
+                best = {bn, true};
+            }
         }
     }
     return best;
 }
+static int x3_tile_n(int k, long m_tiles) { return x3_plan(k, m_tiles, true).bn; }
 
-static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a) {
+static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws = nullptr, int64_t ws_bytes = 0) {
     const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
-    int bn = x3_tile_n(k, m_tiles), kh = 2;
+    // stream-K needs the workspace; knob 9 = never, 8 = whenever a tile split helps
+    const bool sk_ok = ws && (v == 0 || v == 8) && ws_bytes >= x3_sk_ws_bytes(256);
+    const X3Plan pl = x3_plan(k, m_tiles, sk_ok, v == 8 ? 0.0 : g_sk_over);
+    int bn = pl.bn, kh = 2;
     if (v == 1 || v == 2) bn = k % 128 == 0 ? 128 : 64;
     if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
     if (v == 5) bn = 64;
@@ -1251,11 +1418,21 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a) {
     if (mf16) bn = (v == 7 || k % 128) ? 64 : 128;
     a.n_tiles = k / bn;
     a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
-    const dim3 grid((unsigned)(m_tiles * a.n_tiles));
-    if (mf16 && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
+    a.sk_units = 0;
+    dim3 grid((unsigned)(m_tiles * a.n_tiles));
+    if (pl.sk && bn == pl.bn && kh == 2 && !mf16) {
+        a.sk_units = (long)grid.x * a.nks;
+        a.sk_cnt = (unsigned*)ws;
+        a.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
+        // at least one unit per block: an empty block range inside a tile's block
+        // span would be counted as a segment that never arrives
+        grid = dim3((unsigned)std::min<long>(x3_cus(), a.sk_units));
+    }
+    if (a.sk_units && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
+    else if (a.sk_units) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
+    else if (mf16 && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
     else if (mf16) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
-    else
-    if (bn == 256 && kh == 2) hipLaunchKernelGGL((conv_x3_kernel<256, 2>), grid, dim3(512), 0, st, a);
+    else if (bn == 256 && kh == 2) hipLaunchKernelGGL((conv_x3_kernel<256, 2>), grid, dim3(512), 0, st, a);
     else if (bn == 256) hipLaunchKernelGGL((conv_x3_kernel<256, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128 && kh == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128 && ord) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 1>), grid, dim3(512), 0, st, a);
@@ -1277,8 +1454,11 @@ extern "C" int hkp_weight_pack_x3(int32_t k, int32_t rsc, int32_t c, const float
     return HKP_OK;
 }
 
+extern "C" int64_t hkp_conv_x3_sk_workspace_bytes(void) { return x3_sk_ws_bytes(256); }
+
 extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
-                                 const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream) {
+                                 const float* w_inv_scale, float* y, float* stat_partials, void* sk_workspace,
+                                 int64_t sk_ws_bytes, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -1294,7 +1474,7 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.cch = d->c / 32; a.RS = d->r * d->s;
-    launch_x3(d->k, (M + 255) / 256, as_stream(stream), a);
+    launch_x3(d->k, (M + 255) / 256, as_stream(stream), a, sk_workspace, sk_ws_bytes);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_x3");
     return HKP_OK;
 }
@@ -1322,7 +1502,7 @@ extern "C" int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, u
 
 extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
                                       const float* wf_inv_scale, const uint32_t* dy_amax_bits, const float* add,
-                                      float* dx, hkp_stream_t stream) {
+                                      float* dx, void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -1340,7 +1520,7 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
     a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
     a.M = (int)M; a.cch = d->k / 32; a.RS = d->r * d->s;
-    launch_x3(d->c, (M + 255) / 256, as_stream(stream), a);
+    launch_x3(d->c, (M + 255) / 256, as_stream(stream), a, sk_workspace, sk_ws_bytes);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3");
     return HKP_OK;
 }
@@ -1387,7 +1567,7 @@ extern "C" int hkp_phase_taps(int32_t r, int32_t pad, int32_t stride, int32_t ph
 extern "C" int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint16_t* dy_split,
                                               const uint16_t* const* phase_split, const float* const* phase_inv_scale,
                                               const uint32_t* dy_amax_bits, const float* add, float* dx,
-                                              hkp_stream_t stream) {
+                                              void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -1427,7 +1607,7 @@ extern "C" int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint
             // the column offset: the kernel applies one pad to both axes
             HKP_CHECK_ARG(omx == omy, "hkp_conv2d_bwd_data_x3_strided: row/column phase offsets differ (%d, %d)",
                           omy, omx);
-            launch_x3(d->c, ((long)a.M + 255) / 256, st, a);
+            launch_x3(d->c, ((long)a.M + 255) / 256, st, a, sk_workspace, sk_ws_bytes);
             HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3_strided");
         }
     return HKP_OK;
@@ -1547,7 +1727,7 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
 extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m) { return k > 0 && m > 0 ? x3_tile_n(k, (m + 255) / 256) : -1; }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 8 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

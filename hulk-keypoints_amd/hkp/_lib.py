@@ -60,7 +60,8 @@ SIGNATURES = {
     "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "hkp_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P]),
-    "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
+    "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "hkp_conv_x3_sk_workspace_bytes": (_I64, []),
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
@@ -76,10 +77,10 @@ SIGNATURES = {
     "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
     "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
-    "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_phase_taps": (_I32, [_I32, _I32, _I32, _I32]),
     "hkp_conv2d_bwd_data_x3_strided": (ctypes.c_int, [_CD, _P, ctypes.POINTER(_P), ctypes.POINTER(_P), _P, _P, _P,
-                                                       _P]),
+                                                       _P, _I64, _P]),
     "hkp_weight_pack_x3_batch_ws_bytes": (_I64, [_I32, ctypes.POINTER(PackJob)]),
     "hkp_weight_pack_x3_batch": (ctypes.c_int, [_I32, ctypes.POINTER(PackJob), _P, _I64, _P]),
     "hkp_conv_bwd_filter_x3_workspace": (_I64, [_CD]),

@@ -31,6 +31,24 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+# Stream-K workspace of the x3 convs, one per (device, stream): zeroed once (its
+# arrival counters must start at zero; every launch leaves them zero).  Launches
+# sharing one stream never run concurrently, as the workspace requires.
+_sk_ws = {}
+
+
+def _sk_workspace():
+    from ._lib import lib
+    st = torch.cuda.current_stream()
+    key = (st.device_index, st.cuda_stream)
+    ws = _sk_ws.get(key)
+    if ws is None:
+        nb = lib().hkp_conv_x3_sk_workspace_bytes()
+        ws = torch.zeros(nb, device=torch.device("cuda", st.device_index), dtype=torch.uint8)
+        _sk_ws[key] = ws
+    return ctypes.c_void_p(ws.data_ptr()), ctypes.c_int64(ws.numel())
+
+
 def _ptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
 
@@ -167,7 +185,8 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None):
         part = torch.empty((tiles, k, 2), device=xs.device, dtype=torch.float32)
 
     def launch():
-        call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part), _stream())
+        call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
+             *_sk_workspace(), _stream())
 
     if _observer is None:
         launch()
@@ -650,7 +669,7 @@ def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=No
     sp = (ctypes.c_void_p * 4)(*[None if p is None else p.split.data_ptr() for p in phase_packs])
     sc = (ctypes.c_void_p * 4)(*[None if p is None else p.inv_scale.data_ptr() for p in phase_packs])
     call("hkp_conv2d_bwd_data_x3_strided", ctypes.byref(d), _ptr(dys), sp, sc, _ptr(amax), _ptr(add), _ptr(dx),
-         _stream())
+         *_sk_workspace(), _stream())
     return dx
 
 
@@ -674,7 +693,7 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None):
 
     def launch():
         call("hkp_conv2d_bwd_data_x3", ctypes.byref(d), _ptr(dys), _ptr(wfs), _ptr(wfsc), _ptr(amax), _ptr(add),
-             _ptr(dx), _stream())
+             _ptr(dx), *_sk_workspace(), _stream())
 
     if _observer is None:
         launch()

@@ -101,13 +101,25 @@ int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t*
 int hkp_weight_pack_x3(int32_t k, int32_t rsc, int32_t c, const float* w, uint16_t* w_split, float* w_inv_scale,
                        hkp_stream_t stream);
 int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
-                      const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream);
+                      const float* w_inv_scale, float* y, float* stat_partials, void* sk_workspace,
+                      int64_t sk_ws_bytes, hkp_stream_t stream);
+/* Stream-K workspace of the x3 convs (hkp_conv2d_fwd_x3, hkp_conv2d_bwd_data_x3,
+ * hkp_conv2d_bwd_data_x3_strided; nullable: then every launch is one tile per
+ * block).  With it, a launch whose tiles fill the CUs poorly (e.g. 300 tiles on
+ * 256 CUs) splits tiles x K-steps evenly over one block per CU and sums each split
+ * tile's fp32 segments in fixed segment order (deterministic).  Its first 64 KiB
+ * are arrival counters that must be ZERO before the first call; every call
+ * leaves them zero (allocate once, zeroed, per stream: calls on one workspace
+ * must not run concurrently).  Size: hkp_conv_x3_sk_workspace_bytes(). */
+int64_t hkp_conv_x3_sk_workspace_bytes(void);
 /* Tile width (256, 128 or 64 output channels per 256-pixel tile) the x3 conv
  * uses for Cout = k over m output pixels: fewest rounds of blocks over the 256
  * CUs weighted by the measured per-column cost of each tile (-1 on bad args).
  * Tuning knob for the choice (0 = that policy; 1 = 256x128 only; 2 = 256x128
  * with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel stages whenever
- * Cout % 256 == 0; 5 = 256x64).  Outputs agree to fp32 summation order. */
+ * Cout % 256 == 0; 5 = 256x64; 6 / 7 = 16x16x32 MFMAs with 256x128 / 256x64
+ * tiles; 8 = stream-K wherever a tile split helps; 9 = never stream-K).  Outputs
+ * agree to fp32 summation order. */
 int32_t hkp_x3_tile_n(int32_t k, int64_t m);
 int hkp_set_conv_variant(int32_t variant);
 
@@ -266,7 +278,7 @@ int hkp_weight_flip_pack_x3(const hkp_conv_desc* d, const float* w, uint16_t* wf
                             hkp_stream_t stream);
 int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, const uint16_t* wf_split,
                            const float* wf_inv_scale, const uint32_t* dy_amax_bits, const float* add, float* dx,
-                           hkp_stream_t stream);
+                           void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream);
 /* Strided (stride 2, dilation 1) backward-data on the f16x3 path: dx is computed
  * per output phase (py, px) as a stride-1 conv of dy with that phase's taps
  * (phase_split[py*2+px] = kind-2 packs of hkp_weight_pack_x3_batch, inverse
@@ -277,7 +289,8 @@ int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy_split, con
 int32_t hkp_phase_taps(int32_t r, int32_t pad, int32_t stride, int32_t phase);
 int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint16_t* dy_split,
                                    const uint16_t* const* phase_split, const float* const* phase_inv_scale,
-                                   const uint32_t* dy_amax_bits, const float* add, float* dx, hkp_stream_t stream);
+                                   const uint32_t* dy_amax_bits, const float* add, float* dx, void* sk_workspace,
+                                   int64_t sk_ws_bytes, hkp_stream_t stream);
 /* Batched weight packing for a training step (one launch pair for a whole
  * network instead of one hkp_weight_pack_x3 / hkp_weight_flip_pack_x3 per conv;
  * outputs bit-identical to those).  jobs: host array; kind 0 = forward pack

@@ -174,10 +174,12 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
     try:
-        for var in (1, 2, 3, 4, 6, 7):
+        for var in (1, 2, 3, 4, 6, 7, 8, 9):
             call("hkp_set_conv_variant", var)
             yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
-            assert (yv - y).abs().max().item() <= 1e-6 * scale
+            # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
+            # segments at the end, so variants differ by fp32 summation order)
+            assert (yv.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale
             assert torch.allclose(pv, p, rtol=1e-4, atol=1e-3)
     finally:
         call("hkp_set_conv_variant", 0)
@@ -385,3 +387,50 @@ def test_f16_forward_close_to_reference(cuda_device, golden, precision):
     agree = (yx.cpu().numpy() == g["argmax_yx"]).all(-1).mean()
     print("fp16 R50: max heat err %.3g, argmax agreement %.2f" % (err, agree))
     assert err < 1e-1 and agree >= 0.5   # fp16 operands through 53 train-mode-BN layers
+
+
+SK_CASES = [
+    (1, 240, 320, 64, 128, 3, 1, 1, 1),     # 300 256x128 tiles over 256 CUs: stream-K segments span tiles
+    (2, 60, 80, 256, 512, 3, 1, 2, 2),      # layer4 class (dilation 2), 150 m-tiles x 4 column tiles
+    (1, 20, 30, 64, 64, 1, 1, 0, 1),        # 3 tiles of two K-steps each (fewer units than CUs)
+]
+
+
+@pytest.mark.parametrize("case", SK_CASES)
+def test_x3_stream_k(cuda_device, case):
+    """Stream-K x3 conv (knob 8: split tiles x K-steps over one block per CU, fixed
+    segment-order fp32 sum) vs one tile per block (knob 9), forward and stride-1
+    dgrad: same values to fp32 summation order, same BN partials, deterministic
+    run to run (the arrival counters are left zero)."""
+    from hkp import ops
+    from hkp._lib import call
+    n, h, w, cin, cout, k, st, pad, dil = case
+    d = cuda_device
+    x = F.relu(rand(n, h, w, cin, seed=31)).to(d)
+    wt = rand(cout, k, k, cin, seed=32, scale=(2.0 / (k * k * cout)) ** 0.5).to(d)
+    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d)
+    xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
+    wp = ops.weight_pack_x3(wt)
+    ho, wo = ops.conv_out_hw(h, w, k, k, st, pad, dil)
+    gy = rand(n, ho, wo, cout, seed=33).to(d)
+    amax = ops.absmax(gy)
+    dys = ops.split_pack_x3(gy, amax)
+    wfp = ops.weight_flip_pack_x3(wt)
+    add = rand(n, h, w, cin, seed=34).to(d)
+    out = {}
+    try:
+        for var in (9, 8, 8):
+            call("hkp_set_conv_variant", var)
+            y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
+            dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add, amax=amax)
+            out.setdefault(var, []).append((y, p, dx))
+    finally:
+        call("hkp_set_conv_variant", 0)
+    (y9, p9, dx9), = out[9]
+    (y8, p8, dx8), (y8b, p8b, dx8b) = out[8]
+    assert torch.equal(y8, y8b) and torch.equal(p8, p8b) and torch.equal(dx8, dx8b)
+    # both fp32-class (each within 2e-6 of fp64, test_x3_conv_fp32_accurate): K
+    # segments summed at the end reorder the fp32 sum
+    assert (y8 - y9).abs().max().item() <= 4e-6 * y9.abs().max().item()
+    assert torch.allclose(p8, p9, rtol=1e-4, atol=1e-3)
+    assert (dx8 - dx9).abs().max().item() <= 4e-6 * dx9.abs().max().item()
