@@ -1354,17 +1354,17 @@ static int x3_cus() {
 constexpr long X3_SK_CNT_BYTES = 64 << 10;
 static long x3_sk_ws_bytes(int bn) { return X3_SK_CNT_BYTES + 2L * x3_cus() * bn * 1024; }
 
-// stream-K overhead per block in tile times (slab write, the reducer's slab
-// reads, one more pipeline fill, the SK kernel's higher register count);
-// HKP_SK_OVER overrides for tuning.  Default 1 = stream-K never chosen by the
-// policy: measured on the box at 0.25 it lost on both workloads (C2 inference
-// 1404 -> 1350 img/s, C3-shard training 375 -> 358 img/s, same box, same call)
-// — one round of 256x256 tiles or a full round of data-parallel tiles beats a
-// split tile's extra fill + slab round trip at these K depths.  Knob 8 forces it.
-static double g_sk_over = [] {
+// stream-K overhead per block in tile times: every block writes up to two
+// fp32 slabs and most reduce a tile from two (~0.4 MB per CU, all CUs at once),
+// plus a second pipeline fill — so it shrinks with the K depth nks of a tile.
+// Fitted to in-process A/Bs on the box (tools/conv_ab.py, knob 8 vs 9:
+// t4 nks 144 0.43, layer3 nks 72 0.45, t2 nks 36 >= 0.59, t1 nks 18 >= 1.1 tile):
+// 0.4 + 12 / nks.  HKP_SK_OVER = a fixed value instead (tuning).
+static double g_sk_over_env = [] {
     const char* e = getenv("HKP_SK_OVER");
-    return e ? atof(e) : 1.0;
+    return e ? atof(e) : -1.0;
 }();
+static double sk_over(int nks) { return g_sk_over_env >= 0 ? g_sk_over_env : 0.4 + 12.0 / nks; }
 
 // Tile width (and data-parallel vs stream-K) for Cout = k over m_tiles 256-row
 // tiles: data-parallel costs ceil(blocks / CUs) rounds of one tile each,
@@ -1379,7 +1379,7 @@ struct X3Plan {
     int bn;
     bool sk;
 };
-static X3Plan x3_plan(int k, long m_tiles, bool sk_ok, double over = g_sk_over) {
+static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
     const int G = x3_cus();
     X3Plan best{64, false};
     double best_cost = 1e300;
@@ -1402,13 +1402,14 @@ static X3Plan x3_plan(int k, long m_tiles, bool sk_ok, double over = g_sk_over) 
     }
     return best;
 }
-static int x3_tile_n(int k, long m_tiles) { return x3_plan(k, m_tiles, true).bn; }
+static int x3_tile_n(int k, long m_tiles, int nks) { return x3_plan(k, m_tiles, nks, true, sk_over(nks)).bn; }
 
 static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws = nullptr, int64_t ws_bytes = 0) {
     const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
     // stream-K needs the workspace; knob 9 = never, 8 = whenever a tile split helps
     const bool sk_ok = ws && (v == 0 || v == 8) && ws_bytes >= x3_sk_ws_bytes(256);
-    const X3Plan pl = x3_plan(k, m_tiles, sk_ok, v == 8 ? 0.0 : g_sk_over);
+    const int nks = a.RS * a.cch;
+    const X3Plan pl = x3_plan(k, m_tiles, nks, sk_ok, v == 8 ? 0.0 : sk_over(nks));
     int bn = pl.bn, kh = 2;
     if (v == 1 || v == 2) bn = k % 128 == 0 ? 128 : 64;
     if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
@@ -1724,7 +1725,18 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     return HKP_OK;
 }
 
-extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m) { return k > 0 && m > 0 ? x3_tile_n(k, (m + 255) / 256) : -1; }
+extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc) {
+    if (k <= 0 || m <= 0 || rsc < 0) return -1;
+    if (rsc < 32) return x3_plan(k, (m + 255) / 256, 1, false, 0.0).bn;     // no stream-K workspace
+    return x3_tile_n(k, (m + 255) / 256, rsc / 32);
+}
+extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
+    if (k <= 0 || m <= 0 || rsc < 32) return -1;
+    const int v = g_x3_variant % 10;
+    if (v != 0 && v != 8) return 0;
+    const int nks = rsc / 32;
+    return x3_plan(k, (m + 255) / 256, nks, true, v == 8 ? 0.0 : sk_over(nks)).sk ? 1 : 0;
+}
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
     HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 20, "hkp_set_conv_variant: unknown variant %d",

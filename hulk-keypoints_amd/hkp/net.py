@@ -378,11 +378,11 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
         if need_dx:
             if st == 1:
                 wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
-                dx = ops.conv2d_bwd_data_x3(dys, wfs, tuple(x.shape), pd, dl, add=add, amax=amax)
+                dx = ops.conv2d_bwd_data_x3(dys, wfs, tuple(x.shape), pd, dl, add=add, amax=amax, sk=ready is None)
             else:                          # stride 2: one stride-1 conv per output phase of dx
                 phs = _cached_split(conv.weight, "phase_x3", lambda t: ops.weight_phase_pack_x3(t, pd))
                 dx = ops.conv2d_bwd_data_x3_strided(dys, phs, tuple(x.shape), tuple(conv.weight.shape), pd, add=add,
-                                                    amax=amax)
+                                                    amax=amax, sk=ready is None)
         if ready is None:
             dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
         grads.put(conv.weight, dw, ready)

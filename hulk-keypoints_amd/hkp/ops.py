@@ -37,8 +37,10 @@ def _stream():
 _sk_ws = {}
 
 
-def _sk_workspace():
+def _sk_workspace(enable=True):
     from ._lib import lib
+    if not enable:
+        return ctypes.c_void_p(0), ctypes.c_int64(0)
     st = torch.cuda.current_stream()
     key = (st.device_index, st.cuda_stream)
     ws = _sk_ws.get(key)
@@ -132,11 +134,15 @@ class PackedWeight(tuple):
         return self[1]
 
 
-def x3_symbol(k, m):
-    """Kernel symbol the x3 conv launches for Cout = k over m output pixels (the
-    default tile policy of conv_x3.hip's launch_x3, hkp_x3_tile_n)."""
+def x3_symbol(k, m, rsc, sk=True):
+    """Kernel symbol the x3 conv launches for Cout = k over m output pixels with
+    GEMM depth rsc = R*S*Cin (the tile policy of conv_x3.hip's launch_x3:
+    hkp_x3_tile_n, hkp_x3_stream_k)."""
     from ._lib import lib
-    return "conv_x3_kernel<%d, 2, false>" % lib().hkp_x3_tile_n(k, m)
+    L = lib()
+    sk = sk and L.hkp_x3_stream_k(k, m, rsc) == 1
+    bn = L.hkp_x3_tile_n(k, m, rsc) if sk else L.hkp_x3_tile_n(k, m, 0)
+    return "conv_x3_kernel<%d, 2, false, 0, 32, %s>" % (bn, "true" if sk else "false")
 
 
 def weight_pack_x3(w):
@@ -191,7 +197,7 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None):
     if _observer is None:
         launch()
     else:
-        _observer(x3_symbol(k, n * ho * wo), 2.0 * n * ho * wo * k * r * s * c,
+        _observer(x3_symbol(k, n * ho * wo, r * s * c), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
     return y, part
 
@@ -642,10 +648,11 @@ def weight_phase_pack_x3(w, pad):
     return out
 
 
-def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=None, amax=None):
+def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=None, amax=None, sk=True):
     """f16x3 dL/dx of a stride-2 (dilation-1) NHWC conv with KRSC weight shape
     w_shape, one stride-1 conv per output phase: dys = split_pack_x3(dy, amax),
-    phase_packs = weight_phase_pack_x3(w, pad)."""
+    phase_packs = weight_phase_pack_x3(w, pad).  sk=False: no stream-K (one tile
+    per block, e.g. while another stream's kernel shares the CUs)."""
     _need(dys, torch.float16, "conv2d_bwd_data_x3_strided.dy_split", 4)
     k, r, s, c = w_shape
     if len(phase_packs) != 4:
@@ -669,13 +676,13 @@ def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=No
     sp = (ctypes.c_void_p * 4)(*[None if p is None else p.split.data_ptr() for p in phase_packs])
     sc = (ctypes.c_void_p * 4)(*[None if p is None else p.inv_scale.data_ptr() for p in phase_packs])
     call("hkp_conv2d_bwd_data_x3_strided", ctypes.byref(d), _ptr(dys), sp, sc, _ptr(amax), _ptr(add), _ptr(dx),
-         *_sk_workspace(), _stream())
+         *_sk_workspace(sk), _stream())
     return dx
 
 
-def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None):
+def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=True):
     """f16x3 dL/dx of a stride-1 NHWC conv from packed dy (split_pack_x3 with `amax`)
-    and wfp = weight_flip_pack_x3(w)."""
+    and wfp = weight_flip_pack_x3(w).  sk=False: no stream-K."""
     wfs, wfsc = wfp
     _need(dys, torch.float16, "conv2d_bwd_data_x3.dy_split", 4)
     _need(wfs, torch.float16, "conv2d_bwd_data_x3.wf_split", 4)
@@ -693,12 +700,12 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None):
 
     def launch():
         call("hkp_conv2d_bwd_data_x3", ctypes.byref(d), _ptr(dys), _ptr(wfs), _ptr(wfsc), _ptr(amax), _ptr(add),
-             _ptr(dx), *_sk_workspace(), _stream())
+             _ptr(dx), *_sk_workspace(sk), _stream())
 
     if _observer is None:
         launch()
     else:
-        _observer(x3_symbol(c, x_shape[0] * x_shape[1] * x_shape[2]),
+        _observer(x3_symbol(c, x_shape[0] * x_shape[1] * x_shape[2], r * s * k, sk),
                   2.0 * x_shape[0] * x_shape[1] * x_shape[2] * c * r * s * k,
                   2.0 * (dys.numel() + wfs.numel()) + 4.0 * dx.numel(), launch)
     return dx

@@ -113,14 +113,19 @@ int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uin
  * must not run concurrently).  Size: hkp_conv_x3_sk_workspace_bytes(). */
 int64_t hkp_conv_x3_sk_workspace_bytes(void);
 /* Tile width (256, 128 or 64 output channels per 256-pixel tile) the x3 conv
- * uses for Cout = k over m output pixels: fewest rounds of blocks over the 256
- * CUs weighted by the measured per-column cost of each tile (-1 on bad args).
+ * uses for Cout = k over m output pixels and GEMM depth rsc = R*S*Cin: fewest
+ * rounds of blocks over the CUs weighted by the measured per-column cost of each
+ * tile, data-parallel or stream-K (rsc = 0: as launched without a stream-K
+ * workspace; -1 on bad args).
  * Tuning knob for the choice (0 = that policy; 1 = 256x128 only; 2 = 256x128
  * with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel stages whenever
  * Cout % 256 == 0; 5 = 256x64; 6 / 7 = 16x16x32 MFMAs with 256x128 / 256x64
  * tiles; 8 = stream-K wherever a tile split helps; 9 = never stream-K).  Outputs
  * agree to fp32 summation order. */
-int32_t hkp_x3_tile_n(int32_t k, int64_t m);
+int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc);
+/* 1 if that launch (rsc = R*S*Cin, the GEMM depth) runs stream-K under the
+ * current knob and a workspace (the conv_x3_kernel<..., true> instantiation). */
+int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc);
 int hkp_set_conv_variant(int32_t variant);
 
 /* ----------------------------------------------------------- batchnorm ---- */
