@@ -126,22 +126,29 @@ typedef unsigned __attribute__((address_space(1))) gu32;
 // count the arrival; the last-arriving segment's block reads every slab of the
 // tile in segment order (fixed summation order: the result does not depend on
 // which block arrives last) and returns true with the sum in its accumulators.
-// Slab of block bb for tile t: slot 2*bb + (0: the tile is bb's first segment,
-// 1: its last).  Hand-off per cdna_hip_programming.md §6 Guideline 16 (split-K
-// counter form): every wave drains its stores, barrier, one lane releases at
-// agent scope and adds to the counter; the last arriver acquires at agent
-// scope before any wave reads a slab, and re-zeroes the counter.
+// Stream-K is column-grouped: the grid is NG groups of n_tiles blocks; group g
+// runs units [g*U/NG, (g+1)*U/NG) of the (m-tile, K-step) sequence, block
+// g*n_tiles + nt of it for column tile nt — the n_tiles blocks of a group are
+// adjacent after the XCD remap and read the same A lines at the same time (one
+// L2 fetch), as the data-parallel grid's neighbouring tiles do.
+// Slab of group gg's block for tile (mt, nt): slot 2*(gg*n_tiles + nt) + (0: mt
+// is the group's first m-tile, 1: its last).  Hand-off per
+// cdna_hip_programming.md §6 Guideline 16 (split-K counter form): every wave
+// drains its stores, barrier, one lane releases at agent scope and adds to the
+// counter; the last arriver acquires at agent scope before any wave reads a
+// slab, and re-zeroes the counter.
 template <int NV4, typename Get, typename Set>
 __device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char* flag_lds, Get&& get, Set&& set) {
     const long U = a.sk_units;
-    const int G = gridDim.x;
-    const long t0 = (long)T * a.nks;
-    const int b0 = sk_block_of(t0, U, G), nseg = sk_block_of(t0 + a.nks - 1, U, G) - b0 + 1;
-    auto slab = [&](int bb) {
-        const int which = sk_start(bb, U, G) >= t0 ? 0 : 1;
-        return (gf32x4*)a.sk_ws + (long)(2 * bb + which) * NV4 * 512;
+    const int NT = a.n_tiles, NG = gridDim.x / NT;
+    const int mt = T / NT, nt = T - mt * NT;
+    const long t0 = (long)mt * a.nks;
+    const int b0 = sk_block_of(t0, U, NG), nseg = sk_block_of(t0 + a.nks - 1, U, NG) - b0 + 1;
+    auto slab = [&](int gg) {
+        const int which = sk_start(gg, U, NG) >= t0 ? 0 : 1;
+        return (gf32x4*)a.sk_ws + (long)(2 * (gg * NT + nt) + which) * NV4 * 512;
     };
-    gf32x4* mine = slab(xcd_remap(blockIdx.x, G));
+    gf32x4* mine = slab(xcd_remap(blockIdx.x, gridDim.x) / NT);
 #pragma unroll
     for (int v = 0; v < NV4; ++v) mine[v * 512 + tid] = get(v);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -858,9 +865,9 @@ constexpr int x3_lds_bytes(int BN, int KH) {
     return (BN == 256 && KH == 2 ? 2 : (KH == 2 ? 3 : 4)) * (256 + BN) * 64 * KH + 16;
 }
 
-// One tile per block (sk_units == 0, blocks remapped XCD-aware), or stream-K:
-// block b (remapped) runs units [b*U/G, (b+1)*U/G) of the tile-major
-// (tile, K-step) sequence, one tile segment after another.
+// One tile per block (blocks remapped XCD-aware), or (SK) column-grouped
+// stream-K: group g runs units [g*U/NG, (g+1)*U/NG) of the m-tile-major
+// (m-tile, K-step) sequence, one tile segment after another (sk_combine).
 // Separate instantiations (SK): the stream-K loop's live state would otherwise
 // raise the register allocation of the one-tile kernels (256x256 spilled).
 template <int BN, int KH, bool STEM = false, int ORD = 0, int MFD = 32, bool SK = false>
@@ -871,13 +878,16 @@ __global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
         conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, b, 0, a.nks, false);
         return;
     }
-    const long U = a.sk_units, u0 = sk_start(b, U, G), u1 = sk_start(b + 1, U, G);
+    // column-grouped stream-K (sk_combine): group g = b / n_tiles, column tile b % n_tiles
+    const int NT = a.n_tiles, NG = G / NT, g = b / NT, nt = b - g * NT;
+    if (g >= NG) return;                   // grid is NG * n_tiles; never taken
+    const long U = a.sk_units, u0 = sk_start(g, U, NG), u1 = sk_start(g + 1, U, NG);
     for (long u = u0; u < u1;) {
-        const int T = (int)(u / a.nks);
-        const long t0 = (long)T * a.nks;
+        const int mt = (int)(u / a.nks);
+        const long t0 = (long)mt * a.nks;
         const int ks = (int)(u - t0), ke = (int)min((long)a.nks, u1 - t0);
         if (u != u0) __syncthreads();      // the previous segment is done with the LDS ring
-        conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, T, ks, ke - ks, ks != 0 || ke != a.nks);
+        conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, mt * NT + nt, ks, ke - ks, ks != 0 || ke != a.nks);
         u = t0 + ke;
     }
 }
@@ -1357,14 +1367,15 @@ static long x3_sk_ws_bytes(int bn) { return X3_SK_CNT_BYTES + 2L * x3_cus() * bn
 // stream-K overhead per block in tile times: every block writes up to two
 // fp32 slabs and most reduce a tile from two (~0.4 MB per CU, all CUs at once),
 // plus a second pipeline fill — so it shrinks with the K depth nks of a tile.
-// Fitted to in-process A/Bs on the box (tools/conv_ab.py, knob 8 vs 9:
-// t4 nks 144 0.43, layer3 nks 72 0.45, t2 nks 36 >= 0.59, t1 nks 18 >= 1.1 tile):
-// 0.4 + 12 / nks.  HKP_SK_OVER = a fixed value instead (tuning).
+// Fitted to in-process A/Bs on the box (tools/conv_ab.py, knob 8 vs 9, column-
+// grouped stream-K): t4 nks 144 0.34, t3 / layer3 nks 72 0.46 / 0.48, t2 nks 36
+// 0.63, t1 / layer1 nks 18 1.18 / 1.46 tile-times: 0.2 + 19 / nks.
+// HKP_SK_OVER = a fixed value instead (tuning).
 static double g_sk_over_env = [] {
     const char* e = getenv("HKP_SK_OVER");
     return e ? atof(e) : -1.0;
 }();
-static double sk_over(int nks) { return g_sk_over_env >= 0 ? g_sk_over_env : 0.4 + 12.0 / nks; }
+static double sk_over(int nks) { return g_sk_over_env >= 0 ? g_sk_over_env : 0.2 + 19.0 / nks; }
 
 // Tile width (and data-parallel vs stream-K) for Cout = k over m_tiles 256-row
 // tiles: data-parallel costs ceil(blocks / CUs) rounds of one tile each,
@@ -1392,8 +1403,9 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
             best_cost = dp;
             best = {bn, false};
         }
-        if (sk_ok && bn != 256 && tiles % G && tiles * 4 <= X3_SK_CNT_BYTES) {
-            const double skc = ((double)tiles / G + over) * col;
+        const int ng = G / (k / bn);       // column-grouped stream-K: groups of k/bn blocks
+        if (sk_ok && bn != 256 && ng > 0 && m_tiles % ng && tiles * 4 <= X3_SK_CNT_BYTES) {
+            const double skc = ((double)m_tiles / ng + over) * col;
             if (skc < best_cost - 1e-9) {
                 best_cost = skc;
                 best = {bn, true};
@@ -1422,12 +1434,13 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     a.sk_units = 0;
     dim3 grid((unsigned)(m_tiles * a.n_tiles));
     if (pl.sk && bn == pl.bn && kh == 2 && !mf16) {
-        a.sk_units = (long)grid.x * a.nks;
+        a.sk_units = m_tiles * a.nks;
         a.sk_cnt = (unsigned*)ws;
         a.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
-        // at least one unit per block: an empty block range inside a tile's block
+        // at least one unit per group: an empty group range inside a tile's group
         // span would be counted as a segment that never arrives
-        grid = dim3((unsigned)std::min<long>(x3_cus(), a.sk_units));
+        const long ng = std::min<long>(x3_cus() / a.n_tiles, a.sk_units);
+        grid = dim3((unsigned)(ng * a.n_tiles));
     }
     if (a.sk_units && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
     else if (a.sk_units) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
