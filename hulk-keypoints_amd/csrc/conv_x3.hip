@@ -114,6 +114,13 @@ __device__ __forceinline__ void interleave() {
     if constexpr (NM > per * nr) __builtin_amdgcn_sched_group_barrier(0x008, NM - per * nr, 0);
 }
 
+// LDS ring depth of a conv_x3 tile config: 256x256 with 32-channel stages 2
+// (A fragments double-buffered instead), other 32-channel stages 3, 16-channel
+// stages 4 (a 4-stage 256x64 ring with 32-channel stages measured no faster
+// than 3: the short tiles are not load-latency bound).  The whole 160 KiB at
+// most (the stream-K flag reuses the drained ring).
+constexpr int x3_nst(int BN, int KH, int ORD = 0) { return BN == 256 && KH == 2 ? 2 : (KH == 2 ? 3 : 4); }
+
 // ---- stream-K bookkeeping (X3Args::sk_units) ----
 __device__ __forceinline__ long sk_start(long b, long U, int G) { return b * U / G; }
 // the block whose unit range holds unit u: the largest b with sk_start(b) <= u
@@ -306,7 +313,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     if (partial) {                         // stream-K: fold the tile's segments
         auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
         auto set = [&](int v, f32x4 y) { acc[v / UN][v % UN] = y; };
-        if (!sk_combine<UM * UN>(a, tile, tid, smem + NST * STAGE, get, set)) return;
+        if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return;
     }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
     // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
@@ -410,7 +417,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     constexpr int CPR = ROW / 16;                  // 16-B chunks per row
     constexpr int RPI = 1024 / ROW;                // rows per DMA wave-instruction
     constexpr bool WIDE2 = BN == 256 && KH == 2;    // 256x256 with 32-channel stages: 2-stage ring
-    constexpr int NST = WIDE2 ? 2 : (KH == 2 ? 3 : 4);   // LDS ring depth
+    constexpr int NST = x3_nst(BN, KH, ORD);         // LDS ring depth
     constexpr int STAGE = (BM + BN) * ROW;
     constexpr int GA = BM / RPI / 8;               // A DMA instructions per wave per stage
     constexpr int GBT = BN / RPI;                  // B DMA instructions per stage (all waves)
@@ -418,7 +425,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
     static_assert(MFD == 32 || (MFD == 16 && KH == 2 && !STEM && BN <= 128), "bad conv_x3 MFMA shape");
-    static_assert(NST * STAGE + 16 <= 160 * 1024, "LDS");
+    static_assert(NST * STAGE <= 160 * 1024, "LDS");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -548,7 +555,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     // ORD 0: the three products of one tile back to back; ORD 1: product-major
     // (consecutive MFMAs accumulate into different tiles)
     auto mma = [&](const Frag& f) {
-        if constexpr (ORD == 0) {
+        if constexpr (ORD != 1) {
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -771,7 +778,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             const int q4 = (v & 3) * 4;
             x[q4] = y[0]; x[q4 + 1] = y[1]; x[q4 + 2] = y[2]; x[q4 + 3] = y[3];
         };
-        if (!sk_combine<TM * TN * 4>(a, tile, tid, smem + NST * STAGE, get, set)) return;
+        if (!sk_combine<TM * TN * 4>(a, tile, tid, smem, get, set)) return;
     }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
 
@@ -861,18 +868,18 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     }
 }
 
-constexpr int x3_lds_bytes(int BN, int KH) {
-    return (BN == 256 && KH == 2 ? 2 : (KH == 2 ? 3 : 4)) * (256 + BN) * 64 * KH + 16;
-}
+constexpr int x3_lds_bytes(int BN, int KH, int ORD) { return x3_nst(BN, KH, ORD) * (256 + BN) * 64 * KH; }
 
 // One tile per block (blocks remapped XCD-aware), or (SK) column-grouped
 // stream-K: group g runs units [g*U/NG, (g+1)*U/NG) of the m-tile-major
 // (m-tile, K-step) sequence, one tile segment after another (sk_combine).
 // Separate instantiations (SK): the stream-K loop's live state would otherwise
 // raise the register allocation of the one-tile kernels (256x256 spilled).
+// ORD 3 = two blocks per CU (256x64 tiles with 16-channel stages, 80 KiB each):
+// one block's prologue / epilogue overlaps the other's main loop.
 template <int BN, int KH, bool STEM = false, int ORD = 0, int MFD = 32, bool SK = false>
-__global__ __launch_bounds__(512, 1) void conv_x3_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, KH)];
+__global__ __launch_bounds__(512, ORD == 3 ? 2 : 1) void conv_x3_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, KH, ORD)];
     const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
     if constexpr (!SK) {
         conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, b, 0, a.nks, false);
@@ -1427,8 +1434,12 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
     if (v == 5) bn = 64;
     if ((v == 4 && bn == 256) || (v == 2 && bn == 128)) kh = 1;
+    // 256x64 tiles: two blocks per CU with 16-channel stages (the short tiles'
+    // prologue / epilogue overlap the other block's main loop: layer1 +10 %);
+    // knob 20 = the one-block 32-channel-stage kernel
     const bool mf16 = v == 6 || v == 7;
     if (mf16) bn = (v == 7 || k % 128) ? 64 : 128;
+    if (bn == 64 && ord != 2 && !pl.sk && !mf16) kh = 1;
     a.n_tiles = k / bn;
     a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
     a.sk_units = 0;
@@ -1449,8 +1460,9 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     else if (bn == 256 && kh == 2) hipLaunchKernelGGL((conv_x3_kernel<256, 2>), grid, dim3(512), 0, st, a);
     else if (bn == 256) hipLaunchKernelGGL((conv_x3_kernel<256, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128 && kh == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 1>), grid, dim3(512), 0, st, a);
-    else if (bn == 128 && ord) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 1>), grid, dim3(512), 0, st, a);
+    else if (bn == 128 && ord == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2>), grid, dim3(512), 0, st, a);
+    else if (kh == 1) hipLaunchKernelGGL((conv_x3_kernel<64, 1, false, 3>), grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((conv_x3_kernel<64, 2>), grid, dim3(512), 0, st, a);
 }
 
@@ -1752,7 +1764,7 @@ extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 20, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 30, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;
