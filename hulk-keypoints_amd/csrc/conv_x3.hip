@@ -117,9 +117,12 @@ __device__ __forceinline__ void interleave() {
 // LDS ring depth of a conv_x3 tile config: 256x256 with 32-channel stages 2
 // (A fragments double-buffered instead), other 32-channel stages 3, 16-channel
 // stages 4 (a 4-stage 256x64 ring with 32-channel stages measured no faster
-// than 3: the short tiles are not load-latency bound).  The whole 160 KiB at
-// most (the stream-K flag reuses the drained ring).
-constexpr int x3_nst(int BN, int KH, int ORD = 0) { return BN == 256 && KH == 2 ? 2 : (KH == 2 ? 3 : 4); }
+// than 3: the short tiles are not load-latency bound); two blocks per CU
+// (ORD 3): 16-channel stages 4, the stem's 32-channel stages 2.  The whole
+// 160 KiB at most (the stream-K flag reuses the drained ring).
+constexpr int x3_nst(int BN, int KH, int ORD = 0) {
+    return (BN == 256 && KH == 2) || (ORD == 3 && KH == 2) ? 2 : (KH == 2 ? 3 : 4);
+}
 
 // ---- stream-K bookkeeping (X3Args::sk_units) ----
 __device__ __forceinline__ long sk_start(long b, long U, int G) { return b * U / G; }
@@ -1745,7 +1748,13 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     a.plane = (long)d->n * a.H * a.W * 4;
     a.n_tiles = d->k / 64;
     const long m_tiles = (M + 255) / 256;
-    hipLaunchKernelGGL((conv_x3_kernel<64, 2, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+    // two blocks per CU (7 K-steps per tile: prologue / epilogue dominate one block);
+    // knob 20 = one block per CU with a 3-stage ring
+    if (g_x3_variant / 10 == 2)
+        hipLaunchKernelGGL((conv_x3_kernel<64, 2, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+    else
+        hipLaunchKernelGGL((conv_x3_kernel<64, 2, true, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream),
+                           a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
     return HKP_OK;
 }

@@ -341,6 +341,13 @@ def test_stem_x3_fp32_accurate(cuda_device, shape):
     assert err < 2e-6, err
     y32, p32 = ops.conv2d_fwd(xd, wd, 2, 3, 1, layout="nchw")
     assert torch.allclose(part, p32, rtol=1e-4, atol=1e-3)
+    from hkp._lib import call
+    try:                                   # one block per CU (knob 20): same K order, same bits
+        call("hkp_set_conv_variant", 20)
+        y1, p1 = ops.conv2d_fwd_stem_x3(xd, ops.stem_weight_pack_x3(wd), 64)
+    finally:
+        call("hkp_set_conv_variant", 0)
+    assert torch.equal(y1, y) and torch.equal(p1, part)
 
 
 def _model(bb, k, wseed, dev):
