@@ -224,8 +224,8 @@ def main():
     # dominant kernel = the conv symbol with the most event-timed time
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
     alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
-    if dom_sym.startswith("conv_split_kernel") or dom_sym.startswith("conv_x3_kernel"):
-        passes = 3 if dom_sym.startswith("conv_x3") else int(dom_sym.split("<")[1].split(",")[2])
+    if dom_sym.startswith(("conv_split_kernel", "conv_x3_kernel", "wgrad_x3_kernel")):
+        passes = 3 if "_x3_" in dom_sym else int(dom_sym.split("<")[1].split(",")[2])
         achieved, peak = alg * passes, PEAK_FP16_MFMA_TFLOPS    # issued fp16 MFMA FLOPs vs dense fp16 peak
     else:
         passes, achieved, peak = 0, alg, PEAK_FP32_MFMA_TFLOPS
