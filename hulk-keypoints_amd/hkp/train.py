@@ -14,6 +14,8 @@ complete its all-reduce is launched asynchronously, so communication of the
 late layers overlaps the backward of the early ones.  BatchNorm statistics
 stay per rank (standard DDP semantics).
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -54,13 +56,25 @@ class GradBucketer:
     def _reset(self):
         self.pending = [len(ps) for ps in self.buckets]
         self.works = [None] * len(self.buckets)
+        self.streams = [set() for _ in self.buckets]
 
     def ready(self, p, g):
+        """Copy g into its bucket on the CURRENT stream (the one that produced g:
+        main, or the side stream a wgrad ran on); a full bucket's all-reduce is
+        launched after the current stream joins the other streams that copied
+        into it (once per bucket, not per gradient)."""
         bi, off = self.slot[p]
+        cur = torch.cuda.current_stream(g.device) if g.is_cuda else None    # (gloo tests: CPU tensors)
         self.flat[bi][off:off + p.numel()].copy_(g.reshape(-1))
+        self.streams[bi].add(cur)
         self.pending[bi] -= 1
-        if self.pending[bi] == 0 and self.world > 1:
-            self.works[bi] = dist.all_reduce(self.flat[bi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if self.pending[bi] == 0:
+            for s in self.streams[bi]:
+                if s is not None and s != cur:
+                    cur.wait_stream(s)
+            if self.world > 1:
+                self.works[bi] = dist.all_reduce(self.flat[bi], op=dist.ReduceOp.SUM, group=self.group,
+                                                 async_op=True)
 
     def finish(self):
         """Wait for every bucket; average; point p.grad at the flat buffers."""
@@ -69,6 +83,10 @@ class GradBucketer:
         for bi, w in enumerate(self.works):
             if w is not None:
                 w.wait()
+            else:                              # world 1: the copies themselves
+                for s in self.streams[bi]:
+                    if s is not None and s != torch.cuda.current_stream(s.device):
+                        torch.cuda.current_stream(s.device).wait_stream(s)
             if self.world > 1:
                 self.flat[bi].mul_(1.0 / self.world)
         for p, (bi, off) in self.slot.items():
@@ -90,6 +108,9 @@ class Trainer:
         opt_cls = FusedAdam if optimizer == "fused" else torch.optim.Adam
         self.opt = opt_cls(self.params, lr=lr, weight_decay=weight_decay)
         use_dp = distributed and dist.is_initialized() and dist.get_world_size() > 1
+        # HKP_FORCE_BUCKETS=1: the DP gradient path (bucket copies, stream joins) at
+        # world size 1, to time its overhead on one GPU
+        use_dp = use_dp or os.environ.get("HKP_FORCE_BUCKETS") == "1"
         self.bucketer = GradBucketer(self.params, bucket_mb << 20) if use_dp else None
 
     def forward_backward(self, x, uv=None, target=None):

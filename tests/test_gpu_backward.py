@@ -338,6 +338,30 @@ def test_backward_deterministic(cuda_device):
         assert torch.equal(a, b.grad)
 
 
+def test_dp_bucket_path_equals_plain(cuda_device, monkeypatch):
+    """The DP gradient path (bucket copies on the stream each gradient is made on,
+    one join per bucket; forced at world size 1) hands the optimizer exactly the
+    gradients of the plain path, with the side-stream wgrad on and off."""
+    from hkp import net, train
+    B, K, H, W = 2, 2, 64, 80
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 41)).to(cuda_device)
+    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 42)).to(cuda_device)
+    m = _model("resnet34", K, 43, cuda_device)
+    for overlap in (True, False):    # (off: dgrad may take stream-K — another fp32 order)
+        monkeypatch.setattr(net, "OVERLAP_WGRAD", overlap)
+        monkeypatch.setenv("HKP_FORCE_BUCKETS", "0")
+        train.Trainer(m).forward_backward(x, uv=uv)
+        ref = [p.grad.clone() for p in m.parameters()]
+        monkeypatch.setenv("HKP_FORCE_BUCKETS", "1")
+        t = train.Trainer(m)
+        assert t.bucketer is not None and len(t.bucketer.buckets) >= 2
+        for _ in range(2):                       # buckets reused across steps
+            t.forward_backward(x, uv=uv)
+            torch.cuda.synchronize()
+            for a, p in zip(ref, m.parameters()):
+                assert torch.equal(a, p.grad)
+
+
 @pytest.mark.parametrize("bb,k", [("resnet34", 4), ("resnet50", 8)])
 def test_backward_calls_exact(cuda_device, bb, k):
     """Every conv (dgrad, wgrad) and BN backward call of a full training step,
