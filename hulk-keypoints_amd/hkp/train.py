@@ -26,21 +26,28 @@ from .optim import FusedAdam
 class GradBucketer:
     """Bucketed, overlapped gradient all-reduce (mean over ranks)."""
 
-    def __init__(self, params, bucket_bytes=32 << 20, group=None):
+    def __init__(self, params, bucket_bytes=32 << 20, group=None, last_bucket_bytes=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        # backward produces grads roughly in reverse parameter order
+        # backward produces grads roughly in reverse parameter order; buckets are cut
+        # from the END of that order (the stem side), the first of them (the last
+        # to fill, its all-reduce exposed after backward) capped at
+        # last_bucket_bytes (bucket_bytes / 8 by default): for R34 the tail bucket
+        # is layer2 + layer1 + stem (~6 MB) instead of a 23 MB remainder
+        if last_bucket_bytes is None:
+            last_bucket_bytes = bucket_bytes // 8
         order = list(reversed(list(params)))
-        self.buckets = []
-        cur, cur_bytes = [], 0
-        for p in order:
-            cur.append(p)
+        tail_first = []
+        cur, cur_bytes, cap = [], 0, last_bucket_bytes
+        for p in reversed(order):
+            if cur and cur_bytes + p.numel() * 4 > cap:
+                tail_first.append(cur)
+                cur, cur_bytes, cap = [], 0, bucket_bytes
+            cur.insert(0, p)
             cur_bytes += p.numel() * 4
-            if cur_bytes >= bucket_bytes:
-                self.buckets.append(cur)
-                cur, cur_bytes = [], 0
         if cur:
-            self.buckets.append(cur)
+            tail_first.append(cur)
+        self.buckets = list(reversed(tail_first))
         self.slot = {}
         self.flat = []
         for bi, ps in enumerate(self.buckets):
