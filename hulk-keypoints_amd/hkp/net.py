@@ -51,6 +51,9 @@ _precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
 # The weakref check means a dead parameter's entry is never served to a new
 # tensor that happens to reuse its id, data pointer and version.
 _split_cache = {}
+# (id(resnet), flip) → the last prepack_x3 launch that repacked every operand
+_prepack_plans = {}
+_NO_PREPACK_PLAN = os.environ.get("HKP_NO_PREPACK_PLAN") == "1"     # A/B: always rebuild
 
 
 def _cache_slot(w):
@@ -94,6 +97,23 @@ def prepack_x3(resnet, flip):
     parameter versions they were packed from; buffers are reused across steps."""
     if _precision != "f16x3":
         return
+    # fast path: the last call's launch repeated as is when every operand it packed
+    # is stale again (a training step: the optimizer bumped every weight) and the
+    # weights still live where they did — building the job table in Python per
+    # step left the GPU idle ~0.5 ms
+    key = (id(resnet), flip)
+    plan = _prepack_plans.get(key)
+    if plan is not None and plan["net"]() is resnet and not _NO_PREPACK_PLAN:
+        units = [(wr(), per, v, obj) for wr, per, v, obj in plan["units"]]
+        if all(u[0] is not None for u in units):
+            fresh = [_fresh(w, per.get(v)) for w, per, v, _ in units]
+            if not any(fresh) and all(w.data_ptr() == ptr for (w, _, _, _), ptr in zip(units, plan["ptrs"])):
+                plan["relaunch"]()
+                for w, per, v, obj in units:
+                    per[v] = (w._version, w.data_ptr(), obj)
+                return
+            if all(fresh):
+                return
     items, outs, dest = [], [], []
     for conv in _nhwc_convs(resnet):
         w = conv.weight
@@ -125,8 +145,23 @@ def prepack_x3(resnet, flip):
                 dest.append((per, v, w))
     if not items:
         return
-    for (tgt, key, w), packed in zip(dest, ops.weight_pack_x3_batch(items, outs)):
-        tgt[key] = packed if w is None else (w._version, w.data_ptr(), packed)
+    keep = {}
+    for (tgt, k, w), packed in zip(dest, ops.weight_pack_x3_batch(items, outs, keep_launch=keep)):
+        tgt[k] = packed if w is None else (w._version, w.data_ptr(), packed)
+    # remember the launch when it repacked every operand of the network
+    units = []
+    for conv in _nhwc_convs(resnet):
+        per = _split_cache.get(id(conv.weight), (None, {}))[1]
+        for v in ("x3", "flip_x3", "phase_x3"):
+            if v in per:
+                units.append((conv.weight, per, v, per[v][2]))
+    covered = {(it[1].data_ptr(), it[0]) for it in items}
+    if all((w.data_ptr(), v) in covered for w, _, v, _ in units):
+        _prepack_plans[key] = dict(net=weakref.ref(resnet), relaunch=keep["relaunch"],
+                                   units=[(weakref.ref(w), per, v, obj) for w, per, v, obj in units],
+                                   ptrs=[w.data_ptr() for w, _, _, _ in units])
+    else:
+        _prepack_plans.pop(key, None)
 
 
 def set_conv_precision(p):

@@ -594,13 +594,15 @@ def phase_taps(r, pad, phase, stride=2):
     return lib().hkp_phase_taps(r, pad, stride, phase)
 
 
-def weight_pack_x3_batch(items, outs=None):
+def weight_pack_x3_batch(items, outs=None, keep_launch=None):
     """Many weight packs in one launch pair (hkp_weight_pack_x3_batch): items =
     [(kind, w)] with kind "x3" (= weight_pack_x3(w)) or "flip_x3"
     (= weight_flip_pack_x3(w)), or ("phase_x3", w, (phase, pad)) — output phase
     phase = py*2+px of a stride-2 conv's dgrad operand (conv2d_bwd_data_x3_strided);
     returns the PackedWeights in order.  outs (optional, same order; None entries
-    allowed) are PackedWeights to overwrite."""
+    allowed) are PackedWeights to overwrite.  keep_launch (a dict, optional)
+    receives a `relaunch()` that repeats this exact launch (same pointers) — for
+    callers that repack the same weights in place every step."""
     from ._lib import PackJob, lib
     jobs = (PackJob * max(1, len(items)))()
     res = []
@@ -632,7 +634,14 @@ def weight_pack_x3_batch(items, outs=None):
         return res
     nb = lib().hkp_weight_pack_x3_batch_ws_bytes(len(items), jobs)
     ws = torch.empty(max(4, nb), device=items[0][1].device, dtype=torch.uint8)
-    call("hkp_weight_pack_x3_batch", len(items), jobs, _ptr(ws), nb, _stream())
+    n = len(items)
+
+    def relaunch():
+        call("hkp_weight_pack_x3_batch", n, jobs, _ptr(ws), nb, _stream())
+
+    relaunch()
+    if keep_launch is not None:
+        keep_launch["relaunch"] = relaunch
     return res
 
 

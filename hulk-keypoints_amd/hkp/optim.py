@@ -11,10 +11,13 @@ parameters must be fp32 CUDA tensors.
 """
 import ctypes
 import math
+import os
 
 import torch
 
 from ._lib import AdamTensor, HkpError, call
+
+_NO_FAST = os.environ.get("HKP_ADAM_NO_FAST") == "1"      # A/B: always the slow path
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -29,6 +32,49 @@ class FusedAdam(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
                         foreach=None, capturable=False, differentiable=False, fused=None)
         super().__init__(params, defaults)
+        # per param group: the launch table of the last step (parameter / moment
+        # pointers fixed; gradient pointers refreshed each step) and the common step
+        # count — rebuilding it per parameter in Python left the GPU idle ~1.4 ms per
+        # training step.  Invalidated by load_state_dict / add_param_group.
+        self._fast = {}
+
+    def load_state_dict(self, state_dict):
+        self._fast = {}
+        super().load_state_dict(state_dict)
+
+    def add_param_group(self, param_group):
+        self._fast = {}
+        super().add_param_group(param_group)
+
+    def _fast_step(self, gi, group):
+        """One launch from the cached table, or False (cache miss: slow path)."""
+        fc = self._fast.get(gi)
+        if fc is None or _NO_FAST:
+            return False
+        ps = [p for p in group["params"] if p.grad is not None]
+        if len(ps) != len(fc["ps"]) or any(a is not b for a, b in zip(ps, fc["ps"])):
+            return False
+        arr = fc["arr"]
+        for i, p in enumerate(ps):
+            g = p.grad
+            if g.dtype != torch.float32 or g.is_sparse or not g.is_contiguous() or g.device != p.device:
+                raise HkpError("FusedAdam: fp32 contiguous CUDA gradients only")
+            arr[i].grad = g.data_ptr()
+        torch._foreach_add_(fc["steps"], 1.0)
+        fc["step"] += 1
+        self._launch(group, ps, arr, fc["step"])
+        return True
+
+    def _launch(self, group, ps, arr, step):
+        b1, b2 = group["betas"]
+        bc1 = 1.0 - b1 ** step
+        bc2 = 1.0 - b2 ** step
+        call("hkp_adam_step", len(ps), arr, b2, 1.0 - b1, 1.0 - b2, group["eps"], group["weight_decay"],
+             -group["lr"] / bc1, math.sqrt(bc2), ctypes.c_void_p(torch.cuda.current_stream(ps[0].device).cuda_stream))
+        # the kernel wrote p, exp_avg, exp_avg_sq behind autograd's back: bump
+        # their version counters as torch's in-place Adam ops do (operand caches
+        # keyed on the version — the packed conv weights — see the change)
+        torch.autograd.graph.increment_version(ps + [self.state[p][k] for p in ps for k in ("exp_avg", "exp_avg_sq")])
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -36,8 +82,10 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
-            b1, b2 = group["betas"]
+        for gi, group in enumerate(self.param_groups):
+            if self._fast_step(gi, group):
+                continue
+            self._fast.pop(gi, None)
             # one launch set per distinct step count (all equal in practice)
             by_step = {}
             for p in group["params"]:
@@ -59,20 +107,13 @@ class FusedAdam(torch.optim.Optimizer):
                 st["step"] += 1
                 by_step.setdefault(int(st["step"].item()), []).append(p)
             for step, ps in by_step.items():
-                bc1 = 1.0 - b1 ** step
-                bc2 = 1.0 - b2 ** step
                 arr = (AdamTensor * len(ps))()
                 for i, p in enumerate(ps):
                     st = self.state[p]
                     arr[i].param, arr[i].grad = p.data_ptr(), p.grad.data_ptr()
                     arr[i].exp_avg, arr[i].exp_avg_sq = st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr()
                     arr[i].n = p.numel()
-                call("hkp_adam_step", len(ps), arr, b2, 1.0 - b1, 1.0 - b2, group["eps"], group["weight_decay"],
-                     -group["lr"] / bc1, math.sqrt(bc2),
-                     ctypes.c_void_p(torch.cuda.current_stream(ps[0].device).cuda_stream))
-                # the kernel wrote p, exp_avg, exp_avg_sq behind autograd's back: bump
-                # their version counters as torch's in-place Adam ops do (operand
-                # caches keyed on the version — the packed conv weights — see the change)
-                torch.autograd.graph.increment_version(
-                    ps + [self.state[p][k] for p in ps for k in ("exp_avg", "exp_avg_sq")])
+                self._launch(group, ps, arr, step)
+                if len(by_step) == 1:      # every parameter of the group at one step count: cacheable
+                    self._fast[gi] = dict(ps=ps, arr=arr, step=step, steps=[self.state[p]["step"] for p in ps])
         return loss
