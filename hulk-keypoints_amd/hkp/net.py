@@ -190,15 +190,28 @@ def conv_bn(conv, bn, x, layout="nhwc"):
     """conv (+ BN partials when training) → (y, scale_shift, mean_invstd).
     x: fp32 NHWC (optionally carrying its producer's operand split), a split-only
     activation (fp16, see ops.bn_apply keep_fp32=False), or NCHW for the stem."""
+    y, part = _conv_fwd(conv, bn, x, layout)
+    count = y.numel() // y.shape[-1]
+    ss, mi = _bn_params(bn, part, count)
+    return y, ss, mi
+
+
+def _conv_fwd(conv, bn, x, layout="nhwc", part_out=None, sk=True):
+    """The conv of conv_bn → (y, BN tile partials or None).  part_out: where the
+    partials go (the x3 / stem x3 paths; the inference lanes); sk=False: no
+    stream-K (the lanes: a half batch must sum K in the full batch's order)."""
     passes = PRECISIONS[_precision]
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
     if layout == "nchw" and passes == 3 and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd, dl):
         y, part = ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
-                                         stats=bn.training)
+                                         stats=bn.training, part_out=part_out)
     elif layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
-        y, part = ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training)
+        y, part = ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training,
+                                    part_out=part_out, sk=sk)
+    elif part_out is not None:
+        raise ops.HkpError("conv %s: partials into a caller buffer need the x3 path" % (tuple(conv.weight.shape),))
     elif layout == "nhwc" and passes:
         hi, lo = _split_weight(conv.weight, passes)
         x_hi = sp[0] if (sp is not None and sp[1] == 1 and passes == 1) else None
@@ -206,9 +219,7 @@ def conv_bn(conv, bn, x, layout="nhwc"):
                                        stats=bn.training, x_hi=x_hi)
     else:
         y, part = ops.conv2d_fwd(x, conv.weight, st, pd, dl, layout=layout, stats=bn.training)
-    count = y.numel() // y.shape[-1]
-    ss, mi = _bn_params(bn, part, count)
-    return y, ss, mi
+    return y, part
 
 
 def image_nchw_shape(x):
@@ -320,7 +331,13 @@ def fc_rows(resnet, k):
 
 
 def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
-    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
+    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22).
+    Inference (no trace) runs as two lanes when the batch allows (hkp/lanes.py:
+    same kernels and outputs, lane B's BN applies beside lane A's convs)."""
+    if trace is None:
+        from . import lanes
+        if lanes.lanes_ok(resnet, x_nchw):
+            return lanes.keypoints_forward_lanes(resnet, x_nchw, k, heat=heat, argmax=argmax)
     feat = backbone_forward(resnet, x_nchw, trace)
     w, b = fc_rows(resnet, k)
     low = ops.head_fc(feat, w, b)

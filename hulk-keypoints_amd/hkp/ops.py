@@ -170,9 +170,23 @@ def channels_of(x):
     return x.shape[-1]
 
 
-def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None):
+def _stat_partials(n_rows, k, device, part_out, name):
+    """BN tile partials [tiles, k, 2] of an n_rows-pixel conv output: part_out (a
+    caller's slice of a larger buffer — the inference lanes share one per layer)
+    or a new tensor."""
+    tiles = (n_rows + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
+    if part_out is None:
+        return torch.empty((tiles, k, 2), device=device, dtype=torch.float32)
+    _need(part_out, torch.float32, name, 3)
+    if tuple(part_out.shape) != (tiles, k, 2):
+        raise HkpError("%s: shape %s != %s" % (name, tuple(part_out.shape), (tiles, k, 2)))
+    return part_out
+
+
+def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True):
     """f16x3 NHWC conv on packed split operands: xs [N,H,W,2C] (from a producer with
-    split=3), wp = weight_pack_x3(w) → fp32 y [N,Ho,Wo,K] (+ BN partials)."""
+    split=3), wp = weight_pack_x3(w) → fp32 y [N,Ho,Wo,K] (+ BN partials, into
+    part_out when given).  sk=False: never stream-K (one tile per block)."""
     ws, wsc = wp
     _need(xs, torch.float16, "conv2d_fwd_x3.x_split", 4)
     _need(ws, torch.float16, "conv2d_fwd_x3.w_split", 4)
@@ -185,19 +199,16 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None):
     ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC)
     y = out if out is not None else torch.empty((n, ho, wo, k), device=xs.device, dtype=torch.float32)
-    part = None
-    if stats:
-        tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
-        part = torch.empty((tiles, k, 2), device=xs.device, dtype=torch.float32)
+    part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out") if stats else None
 
     def launch():
         call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
-             *_sk_workspace(), _stream())
+             *_sk_workspace(sk), _stream())
 
     if _observer is None:
         launch()
     else:
-        _observer(x3_symbol(k, n * ho * wo, r * s * c), 2.0 * n * ho * wo * k * r * s * c,
+        _observer(x3_symbol(k, n * ho * wo, r * s * c, sk), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
     return y, part
 
@@ -221,7 +232,7 @@ def stem_weight_pack_x3(w):
     return PackedWeight(out, sc)
 
 
-def conv2d_fwd_stem_x3(x, wp, k, stats=True):
+def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None):
     """f16x3 stem conv (7x7/s2/p3) → NHWC fp32 y (+ BN partials).  x: the NCHW fp32
     image, or the uint8 NHWC (BGR) batch cv2.imread gives — ToTensor's /255 is then
     fused into the stem's operand pack."""
@@ -239,10 +250,7 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True):
     xs = torch.empty(lib().hkp_stem_pack_x3_elems(ctypes.byref(d)), device=x.device, dtype=torch.float16)
     call("hkp_stem_pack_x3_u8" if u8 else "hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())
     y = torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
-    part = None
-    if stats:
-        tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
-        part = torch.empty((tiles, k, 2), device=x.device, dtype=torch.float32)
+    part = _stat_partials(n * ho * wo, k, x.device, part_out, "conv2d_fwd_stem_x3.part_out") if stats else None
 
     def launch():
         call("hkp_conv2d_fwd_stem_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
@@ -445,11 +453,17 @@ def head_fc(feat, w_kc, bias_k):
     return low
 
 
-def upsample_sigmoid(low, H, W, heat=True, argmax=True, sigmoid=True):
-    """lowres [N,K,h,w] → (heat [N,K,H,W] or None, argmax int32 [N,K,2] (y,x) or None)."""
+def upsample_sigmoid(low, H, W, heat=True, argmax=True, sigmoid=True, out=None):
+    """lowres [N,K,h,w] → (heat [N,K,H,W] (into out when given) or None, argmax
+    int32 [N,K,2] (y,x) or None)."""
     _need(low, torch.float32, "upsample_sigmoid.lowres", 4)
     n, k, h, w = low.shape
-    hm = torch.empty((n, k, H, W), device=low.device, dtype=torch.float32) if heat else None
+    hm = None
+    if heat:
+        hm = out if out is not None else torch.empty((n, k, H, W), device=low.device, dtype=torch.float32)
+        _need(hm, torch.float32, "upsample_sigmoid.out", 4)
+        if tuple(hm.shape) != (n, k, H, W):
+            raise HkpError("upsample_sigmoid: out shape %s != %s" % (tuple(hm.shape), (n, k, H, W)))
     ws = yx = None
     if argmax:
         from ._lib import lib
