@@ -14,13 +14,15 @@
 namespace hkp {
 
 // CPB channels per block (partials_cpb); deterministic fixed-order fp64 merge
-template <int CPB>
-__global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
+// NT threads per block: 256, or 1024 for long tile lists (the stem's 19,200
+// tiles at C2: per-thread load chains of 75 tiles took 75 us with 256 threads)
+template <int CPB, int NT = 256>
+__global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
                                                          const float* __restrict__ part, const float* gamma,
                                                          const float* beta, float momentum, float eps, float* rmean,
                                                          float* rvar, int64_t* nbt, float* ss, float* mi) {
-    constexpr int TL = 256 / CPB;
-    __shared__ double red[4][8];
+    constexpr int TL = NT / CPB, NW = NT / 64;
+    __shared__ double red[NW][8];
     const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
     const bool ok = c < C;
     // tiles t = tl, tl + TL, ... in order; 8 loads in flight per batch (the loop
@@ -37,7 +39,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long count, lon
 #pragma unroll
             for (int j = 0; j < 8; ++j) s += (double)v[j];
         }
-    const double mean = lanes_sum_d<CPB>(s, red) / (double)count;
+    const double mean = lanes_sum_d<CPB, NW>(s, red) / (double)count;
     double q = 0.0;
     if (ok)
         for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
@@ -57,7 +59,7 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(int C, long count, lon
                 }
             }
         }
-    const double m2 = lanes_sum_d<CPB>(q, red);
+    const double m2 = lanes_sum_d<CPB, NW>(q, red);
     if (tl == 0 && ok) {
         const double var = m2 / (double)count;
         const double invstd = 1.0 / sqrt(var + (double)eps);
@@ -200,15 +202,19 @@ extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t 
     HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
                   "hkp_bn_finalize: tiles/tile_rows inconsistent with count");
     const int cpb = partials_cpb(c);
-#define HKP_FIN(CPB)                                                                                              \
-    hipLaunchKernelGGL(bn_finalize_kernel<CPB>, dim3((c + CPB - 1) / CPB), dim3(256), 0, as_stream(stream), c,     \
-                       (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,    \
+#define HKP_FIN1(CPB, NT)                                                                                          \
+    hipLaunchKernelGGL((bn_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), c, \
+                       (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,      \
                        running_var, num_batches_tracked, scale_shift, mean_invstd)
-    if (cpb == 8) HKP_FIN(8);
-    else if (cpb == 4) HKP_FIN(4);
-    else if (cpb == 2) HKP_FIN(2);
-    else HKP_FIN(1);
+#define HKP_FIN(CPB)                                  \
+    if (tiles >= 4096 && !g_fin_small) { HKP_FIN1(CPB, 1024); } \
+    else { HKP_FIN1(CPB, 256); }
+    if (cpb == 8) { HKP_FIN(8); }
+    else if (cpb == 4) { HKP_FIN(4); }
+    else if (cpb == 2) { HKP_FIN(2); }
+    else { HKP_FIN(1); }
 #undef HKP_FIN
+#undef HKP_FIN1
     HKP_LAUNCH_CHECK("hkp_bn_finalize");
     return HKP_OK;
 }

@@ -112,13 +112,13 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
 }
 
 // per channel: dgamma, dbeta, and the apply coefficients (grad_mean, k, invstd*gamma)
-template <int CPB>
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
+template <int CPB, int NT = 256>
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
                                                              const float* __restrict__ mi, const float* gamma,
                                                              float* dgamma, float* dbeta, float* coef,
                                                              const float* __restrict__ pmax, unsigned* amax) {
-    constexpr int TL = 256 / CPB;
-    __shared__ double red[4][8];
+    constexpr int TL = NT / CPB, NW = NT / 64;
+    __shared__ double red[NW][8];
     __shared__ float bmax[8];
     const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
     const bool ok = c < C;
@@ -138,8 +138,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, lon
                 d += (double)v[j].y;
             }
         }
-    const double S = lanes_sum_d<CPB>(s, red);
-    const double D = lanes_sum_d<CPB>(d, red);
+    const double S = lanes_sum_d<CPB, NW>(s, red);
+    const double D = lanes_sum_d<CPB, NW>(d, red);
     double md = 0.0, mv = 0.0;
     if (pmax) {   // per-channel maxima over the tiles (max: any order is exact)
         if (ok)
@@ -148,8 +148,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(int C, long M, lon
                 md = fmax(md, (double)v.x);
                 mv = fmax(mv, (double)v.y);
             }
-        md = lanes_max_d<CPB>(md, red);
-        mv = lanes_max_d<CPB>(mv, red);
+        md = lanes_max_d<CPB, NW>(md, red);
+        mv = lanes_max_d<CPB, NW>(mv, red);
     }
     if (tl == 0 && ok) {
         const double inv = (double)mi[C + c];
@@ -320,14 +320,19 @@ extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, 
     HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     const int cpb = partials_cpb(c);
-#define HKP_BFIN(CPB)                                                                                             \
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<CPB>, dim3((c + CPB - 1) / CPB), dim3(256), 0, as_stream(stream), c, \
-                       (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, maxima, (unsigned*)dy_amax_bits)
-    if (cpb == 8) HKP_BFIN(8);
-    else if (cpb == 4) HKP_BFIN(4);
-    else if (cpb == 2) HKP_BFIN(2);
-    else HKP_BFIN(1);
+#define HKP_BFIN1(CPB, NT)                                                                                         \
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), \
+                       c, (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, maxima,                  \
+                       (unsigned*)dy_amax_bits)
+#define HKP_BFIN(CPB)                                  \
+    if (tiles >= 4096 && !g_fin_small) { HKP_BFIN1(CPB, 1024); } \
+    else { HKP_BFIN1(CPB, 256); }
+    if (cpb == 8) { HKP_BFIN(8); }
+    else if (cpb == 4) { HKP_BFIN(4); }
+    else if (cpb == 2) { HKP_BFIN(2); }
+    else { HKP_BFIN(1); }
 #undef HKP_BFIN
+#undef HKP_BFIN1
     HKP_LAUNCH_CHECK("hkp_bn_bwd_finalize");
     return HKP_OK;
 }

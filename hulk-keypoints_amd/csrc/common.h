@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -96,8 +97,13 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // contiguous load (8*CPB bytes) instead of CPB separate sectors; lane sums are
 // combined in a fixed order.  CPB chosen so that C/CPB blocks still fill the chip.
 static inline int partials_cpb(int C) { return C >= 1024 ? 8 : C >= 512 ? 4 : C >= 256 ? 2 : 1; }
+// the BN finalize kernels take 1024-thread blocks for >= 4096 tiles; A/B knob
+// HKP_FIN_SMALL=1 keeps 256
+static const bool g_fin_small = getenv("HKP_FIN_SMALL") != nullptr;
 
-template <int CPB>
+// NW = waves per block (4: the 256-thread finalize; 16: the 1024-thread one for
+// long tile lists); the per-wave sums are combined pairwise in a fixed order
+template <int CPB, int NW = 4>
 __device__ __forceinline__ double lanes_sum_d(double v, double (*red)[8]) {
 #pragma unroll
     for (int o = CPB; o < 64; o <<= 1) v += __shfl_xor(v, o);
@@ -105,10 +111,17 @@ __device__ __forceinline__ double lanes_sum_d(double v, double (*red)[8]) {
     __syncthreads();
     if (lane < CPB) red[wid][lane] = v;
     __syncthreads();
-    return (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    double a[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) a[i] = red[i][cl];
+#pragma unroll
+    for (int w = NW / 2; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) a[i] = a[2 * i] + a[2 * i + 1];
+    return a[0];
 }
 
-template <int CPB>
+template <int CPB, int NW = 4>
 __device__ __forceinline__ double lanes_max_d(double v, double (*red)[8]) {
 #pragma unroll
     for (int o = CPB; o < 64; o <<= 1) v = fmax(v, __shfl_xor(v, o));
@@ -116,7 +129,10 @@ __device__ __forceinline__ double lanes_max_d(double v, double (*red)[8]) {
     __syncthreads();
     if (lane < CPB) red[wid][lane] = v;
     __syncthreads();
-    return fmax(fmax(red[0][cl], red[1][cl]), fmax(red[2][cl], red[3][cl]));
+    double m = red[0][cl];
+#pragma unroll
+    for (int i = 1; i < NW; ++i) m = fmax(m, red[i][cl]);
+    return m;
 }
 
 }  // namespace hkp
