@@ -871,6 +871,230 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     }
 }
 
+// ---------------------------------------------------------------------------
+// 256x256 tile with FOUR waves (one per SIMD, 2x2, 128x128 each): accumulators
+// 256 fp32 per lane (the AGPR half of the 512-entry register file a lone wave
+// owns), fragments double-buffered per k16 half in VGPRs.  Same LDS ring,
+// staging, swizzle and half-K-step schedule as the 8-wave WIDE2 body; per SIMD
+// the same MFMAs per barrier, a third fewer LDS fragment reads (each wave reads
+// A and B for 128x128 instead of 64x128) and 4 instead of 8 waves to align at
+// each barrier.  Forward / stride-1 dgrad (not the stem, no stream-K).
+// Opt-in (knob 40 / 43): measured 8 % SLOWER than the 8-wave body on C2 layer4
+// (1090 vs 1185 TF/s issued, same box) — a lone wave cannot cover its own
+// ds_read -> MFMA and barrier latencies; kept, parity-tested, as the base for a
+// 16x16x32-MFMA body (which needs the register room only a lone wave has).
+__device__ __forceinline__ void conv_x3_w4_tile(const X3Args& a, char* smem, int tile) {
+    constexpr int BM = 256, BN = 256, WM = 2, WN = 2, NWV = 4, NT = 256;
+    constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);   // 4 x 4 32x32 tiles per wave
+    constexpr int ROW = 128, CPR = 8, RPI = 8;               // 32-channel stages
+    constexpr int STAGE = (BM + BN) * ROW;
+    constexpr int GA = BM / RPI / NWV, GB = BN / RPI / NWV;   // DMA instructions per wave per stage
+    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w % WN;
+    auto swz = [](int row) { return (row >> 1) & 7; };
+
+    // per DMA row: receptive-field origin (hb, wb) packed as two int16 and the
+    // signed 32-bit element offset of that origin pixel (negative where the
+    // origin lies in the padding; the host checks the operand sizes fit): 2 VGPRs
+    // per row instead of 4 — the lone wave's VGPR half is tight
+    const int cstride = a.cch * 64;
+    int a_org[GA], a_off[GA];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+        const int row = RPI * (w * GA + i) + lane / CPR;
+        const int L = ((lane % CPR) ^ swz(row)) * 8;
+        const int m = m0 + row;
+        int hb = -16384, wb = -16384;
+        long off = 0;
+        if (m < a.M) {
+            const int hw = a.Ho * a.Wo;
+            const int n = m / hw, rem = m - n * hw;
+            const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+            hb = ho * a.stride - a.pad;
+            wb = wo * a.stride - a.pad;
+            off = (((long)n * a.H + hb) * a.W + wb) * cstride + L;
+        }
+        a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
+        a_off[i] = (int)off;
+    }
+    const int bline = a.RS * a.cch * 64;
+    unsigned b_off[GB];
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        const int row = RPI * (w * GB + j) + lane / CPR;
+        b_off[j] = (unsigned)((n0 + row) * bline + ((lane % CPR) ^ swz(row)) * 8);
+    }
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    const int nks = a.nks;
+    int q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_buf = 0;
+    auto issue_next = [&]() {
+        char* st = smem + q_buf * STAGE;
+        const int dh = q_rr * a.dil, dw = q_ss * a.dil;
+        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64;
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+            const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+            glds16(in ? a.xs + ((long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+        }
+        const unsigned boff = (unsigned)((q_tap * a.cch + q_cc) * 64);
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16(a.ws + (b_off[j] + boff), st + (BM + RPI * (w * GB + j)) * ROW);
+        q_buf ^= 1;
+        if (++q_ss == a.S) {
+            q_ss = 0;
+            ++q_rr;
+        }
+        if (++q_tap == a.RS) {
+            q_tap = 0;
+            q_rr = 0;
+            ++q_cc;
+        }
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    const int frow = lane & 31, kh = lane >> 5;
+    int foff[2][2];
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) foff[pl][u] = frow * ROW + ((((CPR / 2) * pl + 2 * u + kh) ^ swz(frow)) << 4);
+    const int a_base = (wm * TM * 32) * ROW, b_base = (BM + wn * TN * 32) * ROW;
+
+    issue_next();
+    if (1 < nks) issue_next();
+    if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA + GB) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+
+    struct FA {
+        f16x8 h[TM], l[TM];
+    };
+    f16x8 bh[TN], bl[TN];
+    auto read_a = [&](FA& f, const char* st, int u) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            f.h[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][u]);
+            f.l[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][u]);
+        }
+    };
+    auto read_b = [&](int j, const char* st, int u) {
+        bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][u]);
+        bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][u]);
+    };
+    auto mma_col = [&](const FA& f, int j) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    auto half = [&](const FA& fc, FA& fn, const char* st, int u) {   // MFMAs on fc/B, read fn/B from (st, u)
+        read_a(fn, st, u);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            mma_col(fc, j);
+            read_b(j, st, u);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM, 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    FA fa0, fa1;
+    int cur = 0;
+    read_a(fa0, smem, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) read_b(j, smem, 0);
+    for (int t = 0; t + 1 < nks; ++t) {
+        const char* st = smem + cur * STAGE;
+        half(fa0, fa1, st, 1);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        if (t + 2 < nks) issue_next();        // into t's buffer: every read of it retired above
+        cur ^= 1;
+        half(fa1, fa0, smem + cur * STAGE, 0);
+    }
+    half(fa0, fa1, smem + cur * STAGE, 1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) mma_col(fa1, j);
+
+    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
+    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile
+    // (wave row wm owns 128-row tile half wm) ----
+    const int rbase = m0 + wm * TM * 32 + 4 * kh;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * TN * 32 + j * 32 + frow;
+        const float sc = (a.wscale ? a.wscale[n] : 1.f) * ginv;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            long off[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) off[r] = x3_out_off(a, rbase + i * 32 + (r & 3) + 8 * (r >> 2), n);
+            float av[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) av[r] = (a.add && off[r] >= 0) ? a.add[off[r]] : 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                acc[i][j][r] *= sc;
+                if (off[r] >= 0) a.y[off[r]] = a.add ? acc[i][j][r] + av[r] : acc[i][j][r];
+            }
+        }
+    }
+    if (a.part == nullptr) return;
+    const long tile128 = (long)(m0 >> 7) + wm;
+    const int cnt = min(128, a.M - (m0 + 128 * wm));
+    if (cnt <= 0) return;                  // wave-uniform; no barrier below
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+                s += (m < a.M) ? acc[i][j][r] : 0.f;
+            }
+        s += __shfl_xor(s, 32);
+        const float mu = s / (float)cnt;
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+                const float d = acc[i][j][r] - mu;
+                q += (m < a.M) ? d * d : 0.f;
+            }
+        q += __shfl_xor(q, 32);
+        if (lane < 32) {
+            const int c = n0 + wn * TN * 32 + j * 32 + lane;
+            a.part[(tile128 * a.K + c) * 2 + 0] = s;
+            a.part[(tile128 * a.K + c) * 2 + 1] = q;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256, 1) void conv_x3_w4_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[2 * 512 * 128];
+    conv_x3_w4_tile(a, smem, xcd_remap(blockIdx.x, gridDim.x));
+}
+
 constexpr int x3_lds_bytes(int BN, int KH, int ORD) { return x3_nst(BN, KH, ORD) * (256 + BN) * 64 * KH; }
 
 // One tile per block (blocks remapped XCD-aware), or (SK) column-grouped
@@ -1456,7 +1680,12 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
         const long ng = std::min<long>(x3_cus() / a.n_tiles, a.sk_units);
         grid = dim3((unsigned)(ng * a.n_tiles));
     }
-    if (a.sk_units && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
+    // the 4-wave body keeps 32-bit element offsets: operands must fit
+    const bool w4_fits = (long)a.N * a.H * a.W * a.cch * 64 < (1L << 31) - (1L << 24) &&
+                         (long)k * a.RS * a.cch * 64 < (1L << 31) && a.H < 8192 && a.W < 8192;
+    if (ord == 4 && bn == 256 && kh == 2 && !mf16 && !a.sk_units && w4_fits)
+        hipLaunchKernelGGL(conv_x3_w4_kernel, grid, dim3(256), 0, st, a);
+    else if (a.sk_units && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
     else if (a.sk_units) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
     else if (mf16 && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
     else if (mf16) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
@@ -1773,7 +2002,7 @@ extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 30, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 50, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

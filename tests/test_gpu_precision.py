@@ -174,7 +174,7 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
     try:
-        for var in (1, 2, 3, 4, 6, 7, 8, 9):
+        for var in (1, 2, 3, 4, 6, 7, 8, 9, 40, 43):
             call("hkp_set_conv_variant", var)
             yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
             # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
@@ -441,3 +441,51 @@ def test_x3_stream_k(cuda_device, case):
     assert (y8 - y9).abs().max().item() <= 4e-6 * y9.abs().max().item()
     assert torch.allclose(p8, p9, rtol=1e-4, atol=1e-3)
     assert (dx8 - dx9).abs().max().item() <= 4e-6 * dx9.abs().max().item()
+
+
+W4_CASES = [
+    (2, 11, 13, 64, 256, 3, 1, 1, 1),       # ragged M (286 rows: second tile mostly empty)
+    (1, 15, 20, 512, 512, 3, 1, 4, 4),      # layer4 class, K = 4608
+    (2, 12, 16, 256, 512, 1, 1, 0, 1),      # 1x1 (downsample class)
+]
+
+
+@pytest.mark.parametrize("case", W4_CASES)
+def test_x3_w4_body(cuda_device, case):
+    """The 4-wave 256x256 body (knob 43: one wave per SIMD, 128x128 wave tiles in
+    AGPR accumulators): forward and stride-1 dgrad with a residual addend are
+    fp32-class vs fp64; BN partials agree with the 8-wave body's."""
+    from hkp import ops
+    from hkp._lib import call
+    n, h, w, cin, cout, k, st, pad, dil = case
+    x = F.relu(rand(n, h, w, cin, seed=61))
+    wt = rand(cout, k, k, cin, seed=62, scale=(2.0 / (k * k * cout)) ** 0.5)
+    ref = F.conv2d(x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double(), None, st, pad, dil)
+    d = cuda_device
+    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d)
+    xs = ops.bn_apply(x.to(d), ss, relu=False, split=3, keep_fp32=False)
+    wp = ops.weight_pack_x3(wt.to(d))
+    ho, wo = ops.conv_out_hw(h, w, k, k, st, pad, dil)
+    gy = rand(n, cout, ho, wo, seed=63)
+    add = rand(n, cin, h, w, seed=64)
+    dref = torch.nn.grad.conv2d_input((n, cin, h, w), wt.permute(0, 3, 1, 2).double(), gy.double(), 1, pad, dil) \
+        + add.double()
+    gy_d = gy.permute(0, 2, 3, 1).contiguous().to(d)
+    amax = ops.absmax(gy_d)
+    dys = ops.split_pack_x3(gy_d, amax)
+    wfp = ops.weight_flip_pack_x3(wt.to(d))
+    add_d = add.permute(0, 2, 3, 1).contiguous().to(d)
+    y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False)
+    try:
+        call("hkp_set_conv_variant", 43)
+        y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False)
+        dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add_d, amax=amax, sk=False) \
+            if cin % 256 == 0 else None
+    finally:
+        call("hkp_set_conv_variant", 0)
+    scale = ref.abs().max().item()
+    assert (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale
+    assert torch.allclose(p, p3, rtol=1e-4, atol=1e-3)
+    if dx is not None:
+        err = (dx.cpu().double().permute(0, 3, 1, 2) - dref).abs().max().item() / dref.abs().max().item()
+        assert err < 2e-6, err
