@@ -734,8 +734,12 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=
     return dx
 
 
-def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None):
-    """f16x3 dL/dw (KRSC) from packed x (forward operand) and packed dy (split_pack_x3 with `amax`)."""
+def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, alloc_stream=None):
+    """f16x3 dL/dw (KRSC) from packed x (forward operand) and packed dy (split_pack_x3 with `amax`).
+    alloc_stream: take dw and the workspace from that stream's memory pool (marked
+    as used by the launching stream) — a side-stream wgrad then shares the main
+    stream's cached blocks instead of growing a second pool (C5 at 245 GB: the
+    second pool forced allocator flushes every step, 5x slower)."""
     from ._lib import lib
     _need(xs, torch.float16, "conv2d_bwd_filter_x3.x_split", 4)
     _need(dys, torch.float16, "conv2d_bwd_filter_x3.dy_split", 4)
@@ -745,8 +749,16 @@ def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None):
     if tuple(dys.shape) != (n, ho, wo, 2 * d.k):
         raise HkpError("conv2d_bwd_filter_x3: dy split shape %s != %s" % (tuple(dys.shape), (n, ho, wo, 2 * d.k)))
     nbytes = lib().hkp_conv_bwd_filter_x3_workspace(ctypes.byref(d))
-    ws = torch.empty(max(nbytes, 4) // 4, device=xs.device, dtype=torch.float32)
-    dw = torch.empty(tuple(w_shape), device=xs.device, dtype=torch.float32)
+    if alloc_stream is None:
+        ws = torch.empty(max(nbytes, 4) // 4, device=xs.device, dtype=torch.float32)
+        dw = torch.empty(tuple(w_shape), device=xs.device, dtype=torch.float32)
+    else:
+        launching = torch.cuda.current_stream(xs.device)
+        with torch.cuda.stream(alloc_stream):
+            ws = torch.empty(max(nbytes, 4) // 4, device=xs.device, dtype=torch.float32)
+            dw = torch.empty(tuple(w_shape), device=xs.device, dtype=torch.float32)
+        ws.record_stream(launching)
+        dw.record_stream(launching)
 
     def launch():
         call("hkp_conv2d_bwd_filter_x3", ctypes.byref(d), _ptr(xs), _ptr(dys), _ptr(amax), _ptr(dw), _ptr(ws),
