@@ -1648,6 +1648,10 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
     }
     return best;
 }
+static double g_mf16_rounds = [] {
+    const char* e = getenv("HKP_MF16_ROUNDS");
+    return e ? atof(e) : 2.0;
+}();
 static int x3_tile_n(int k, long m_tiles, int nks) { return x3_plan(k, m_tiles, nks, true, sk_over(nks)).bn; }
 
 static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws = nullptr, int64_t ws_bytes = 0) {
@@ -1664,8 +1668,14 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     // 256x64 tiles: two blocks per CU with 16-channel stages (the short tiles'
     // prologue / epilogue overlap the other block's main loop: layer1 +10 %);
     // knob 20 = the one-block 32-channel-stage kernel
-    const bool mf16 = v == 6 || v == 7;
-    if (mf16) bn = (v == 7 || k % 128) ? 64 : 128;
+    // 16x16x32 MFMAs for 256x128 tiles on grids of >= HKP_MF16_ROUNDS (2) full
+    // rounds: the same cycles per FLOP at lower power, so the chip holds a higher
+    // clock (MI355X_MICROARCH.md DVFS item 7) — C2 layer3 +6 %, layer2 +5 %; on
+    // one-round grids the 16x16 body's longer fill loses (t3 -11 %, t2 -8 %)
+    const bool mf16_pol = v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
+                          (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus();
+    const bool mf16 = v == 6 || v == 7 || mf16_pol;
+    if (v == 6 || v == 7) bn = (v == 7 || k % 128) ? 64 : 128;
     if (bn == 64 && ord != 2 && !pl.sk && !mf16) kh = 1;
     a.n_tiles = k / bn;
     a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
@@ -1992,6 +2002,17 @@ extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc) {
     if (k <= 0 || m <= 0 || rsc < 0) return -1;
     if (rsc < 32) return x3_plan(k, (m + 255) / 256, 1, false, 0.0).bn;     // no stream-K workspace
     return x3_tile_n(k, (m + 255) / 256, rsc / 32);
+}
+extern "C" int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc) {
+    if (k <= 0 || m <= 0 || rsc < 0) return -1;
+    const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
+    if (v == 6 || v == 7) return 16;
+    const long m_tiles = (m + 255) / 256;
+    const X3Plan pl = rsc < 32 ? x3_plan(k, m_tiles, 1, false, 0.0)
+                               : x3_plan(k, m_tiles, rsc / 32, v == 0 || v == 8, v == 8 ? 0.0 : sk_over(rsc / 32));
+    const bool mf16_pol = v == 0 && ord == 0 && pl.bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
+                          (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus();
+    return mf16_pol ? 16 : 32;
 }
 extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
     if (k <= 0 || m <= 0 || rsc < 32) return -1;

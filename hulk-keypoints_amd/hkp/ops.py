@@ -142,7 +142,8 @@ def x3_symbol(k, m, rsc, sk=True):
     L = lib()
     sk = sk and L.hkp_x3_stream_k(k, m, rsc) == 1
     bn = L.hkp_x3_tile_n(k, m, rsc) if sk else L.hkp_x3_tile_n(k, m, 0)
-    return "conv_x3_kernel<%d, 2, false, 0, 32, %s>" % (bn, "true" if sk else "false")
+    mfd = L.hkp_x3_mfma_k(k, m, rsc if sk else 0)
+    return "conv_x3_kernel<%d, 2, false, 0, %d, %s>" % (bn, mfd, "true" if sk else "false")
 
 
 def weight_pack_x3(w):

@@ -489,3 +489,37 @@ def test_x3_w4_body(cuda_device, case):
     if dx is not None:
         err = (dx.cpu().double().permute(0, 3, 1, 2) - dref).abs().max().item() / dref.abs().max().item()
         assert err < 2e-6, err
+
+
+def test_x3_mf16_policy_large_grid(cuda_device):
+    """Grids of >= 2 full rounds of 256x128 tiles take the 16x16x32-MFMA body by
+    default (hkp_x3_mfma_k); it agrees with the 32x32x16 body (knob 1) to fp32
+    summation order — forward and stride-1 dgrad — and the observer symbol names it."""
+    from hkp import ops
+    from hkp._lib import call, lib
+    n, h, w, cin, cout, k, st, pad, dil = (2, 240, 320, 128, 128, 3, 1, 1, 1)   # 600 tiles
+    d = cuda_device
+    x = F.relu(rand(n, h, w, cin, seed=71)).to(d)
+    wt = rand(cout, k, k, cin, seed=72, scale=(2.0 / (k * k * cout)) ** 0.5).to(d)
+    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d)
+    xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
+    wp = ops.weight_pack_x3(wt)
+    m = n * h * w
+    assert lib().hkp_x3_mfma_k(cout, m, k * k * cin) == 16
+    assert ops.x3_symbol(cout, m, k * k * cin) == "conv_x3_kernel<128, 2, false, 0, 16, false>"
+    gy = rand(n, h, w, cout, seed=73).to(d)
+    amax = ops.absmax(gy)
+    dys = ops.split_pack_x3(gy, amax)
+    wfp = ops.weight_flip_pack_x3(wt)
+    y16, p16 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
+    dx16 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax)
+    try:
+        call("hkp_set_conv_variant", 1)
+        assert lib().hkp_x3_mfma_k(cout, m, k * k * cin) == 32
+        y32, p32 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
+        dx32 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax)
+    finally:
+        call("hkp_set_conv_variant", 0)
+    assert (y16 - y32).abs().max().item() <= 4e-6 * y32.abs().max().item()
+    assert torch.allclose(p16, p32, rtol=1e-4, atol=1e-3)
+    assert (dx16 - dx32).abs().max().item() <= 4e-6 * dx32.abs().max().item()
