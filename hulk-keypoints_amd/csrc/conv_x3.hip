@@ -257,6 +257,47 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         }
     };
 
+    if constexpr (BN == 256) {
+        // 256x256 on the 2-stage ring (the 8-wave WIDE2 ring), A single-buffered
+        // (registers: 128 acc + 32 A + 64 B): per K-step t — wait own DMA of t+1,
+        // barrier, issue DMA t+2 into t's buffer (read before the barrier), then per
+        // column j [MFMAs of t with B_j] [refill B_j with t+1's], then A of t+1
+        // (its latency covered by the SIMD's other wave)
+        static_assert(NST == 2, "256-wide 16x16x32 body runs the 2-stage ring");
+        issue_next();
+        if (nks > 1) issue_next();
+        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        FA fa;
+        read_a(fa, smem);
+#pragma unroll
+        for (int j = 0; j < UN; ++j) read_b(j, smem);
+        int cur = 0;
+        for (int t = 0; t + 1 < nks; ++t) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            if (t + 2 < nks) issue_next();
+            cur ^= 1;
+            const char* st = smem + cur * STAGE;
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                mma_col(fa, j);
+                read_b(j, st);
+            }
+            read_a(fa, st);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 3 * UM, 0);  // column j's MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < UN; ++j) mma_col(fa, j);
+    } else {
     // prologue: NST-1 stages in flight, stage 0 landed everywhere
     issue_next();
     for (int s = 1; s < NST - 1; ++s)
@@ -311,6 +352,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     } else {
 #pragma unroll
         for (int j = 0; j < UN; ++j) mma_col(fa0, j);
+    }
     }
 
     if (partial) {                         // stream-K: fold the tile's segments
@@ -427,7 +469,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
-    static_assert(MFD == 32 || (MFD == 16 && KH == 2 && !STEM && BN <= 128), "bad conv_x3 MFMA shape");
+    static_assert(MFD == 32 || (MFD == 16 && KH == 2 && !STEM), "bad conv_x3 MFMA shape");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
@@ -1672,8 +1714,11 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     // rounds: the same cycles per FLOP at lower power, so the chip holds a higher
     // clock (MI355X_MICROARCH.md DVFS item 7) — C2 layer3 +6 %, layer2 +5 %; on
     // one-round grids the 16x16 body's longer fill loses (t3 -11 %, t2 -8 %)
-    const bool mf16_pol = v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
-                          (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus();
+    // 256x256 tiles: the 16x16x32 body on the 2-stage ring always (C2 layer4
+    // 1.79 -> 1.62 ms; one-round grids equal); knob 60 = the 32x32x16 WIDE2 body
+    const bool mf16_pol = (v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
+                           (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus()) ||
+                          (bn == 256 && kh == 2 && !pl.sk && ord != 6 && ord != 4);
     const bool mf16 = v == 6 || v == 7 || mf16_pol;
     if (v == 6 || v == 7) bn = (v == 7 || k % 128) ? 64 : 128;
     if (bn == 64 && ord != 2 && !pl.sk && !mf16) kh = 1;
@@ -1693,7 +1738,9 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     // the 4-wave body keeps 32-bit element offsets: operands must fit
     const bool w4_fits = (long)a.N * a.H * a.W * a.cch * 64 < (1L << 31) - (1L << 24) &&
                          (long)k * a.RS * a.cch * 64 < (1L << 31) && a.H < 8192 && a.W < 8192;
-    if (ord == 4 && bn == 256 && kh == 2 && !mf16 && !a.sk_units && w4_fits)
+    if (mf16 && bn == 256)
+        hipLaunchKernelGGL((conv_x3_kernel<256, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
+    else if (ord == 4 && bn == 256 && kh == 2 && !mf16 && !a.sk_units && w4_fits)
         hipLaunchKernelGGL(conv_x3_w4_kernel, grid, dim3(256), 0, st, a);
     else if (a.sk_units && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
     else if (a.sk_units) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
@@ -2010,8 +2057,14 @@ extern "C" int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc) {
     const long m_tiles = (m + 255) / 256;
     const X3Plan pl = rsc < 32 ? x3_plan(k, m_tiles, 1, false, 0.0)
                                : x3_plan(k, m_tiles, rsc / 32, v == 0 || v == 8, v == 8 ? 0.0 : sk_over(rsc / 32));
-    const bool mf16_pol = v == 0 && ord == 0 && pl.bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
-                          (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus();
+    int bn = pl.bn;
+    if (v == 1 || v == 2) bn = k % 128 == 0 ? 128 : 64;
+    if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
+    if (v == 5) bn = 64;
+    const bool kh2 = !(v == 4 && bn == 256) && !(v == 2 && bn == 128);
+    const bool mf16_pol = (v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
+                           (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus()) ||
+                          (bn == 256 && kh2 && !pl.sk && ord != 6 && ord != 4);
     return mf16_pol ? 16 : 32;
 }
 extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
@@ -2023,7 +2076,7 @@ extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 50, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 70, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

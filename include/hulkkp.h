@@ -121,8 +121,9 @@ int64_t hkp_conv_x3_sk_workspace_bytes(void);
  * with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel stages whenever
  * Cout % 256 == 0; 5 = 256x64; 6 / 7 = 16x16x32 MFMAs with 256x128 / 256x64
  * tiles; 8 = stream-K wherever a tile split helps; 9 = never stream-K; + 20 =
- * one-block 256x64 / stem kernels; + 40 = the 4-wave 256x256 body).  Outputs
- * agree to fp32 summation order. */
+ * one-block 256x64 / stem kernels; + 40 = the 4-wave 256x256 body; + 60 = the
+ * 32x32x16 256x256 body instead of the 16x16x32 one).  Outputs agree to fp32
+ * summation order. */
 int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc);
 /* 1 if that launch (rsc = R*S*Cin, the GEMM depth) runs stream-K under the
  * current knob and a workspace (the conv_x3_kernel<..., true> instantiation). */

@@ -174,7 +174,7 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
     try:
-        for var in (1, 2, 3, 4, 6, 7, 8, 9, 40, 43):
+        for var in (1, 2, 3, 4, 6, 7, 8, 9, 40, 43, 60, 63):
             call("hkp_set_conv_variant", var)
             yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
             # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
@@ -451,10 +451,12 @@ W4_CASES = [
 
 
 @pytest.mark.parametrize("case", W4_CASES)
-def test_x3_w4_body(cuda_device, case):
-    """The 4-wave 256x256 body (knob 43: one wave per SIMD, 128x128 wave tiles in
-    AGPR accumulators): forward and stride-1 dgrad with a residual addend are
-    fp32-class vs fp64; BN partials agree with the 8-wave body's."""
+@pytest.mark.parametrize("knob", [43, 63])
+def test_x3_w4_body(cuda_device, case, knob):
+    """The alternative 256x256 bodies — knob 43: 4 waves (one per SIMD, 128x128
+    wave tiles in AGPR accumulators); knob 63: the 8-wave 32x32x16 body (the
+    default is the 8-wave 16x16x32 one) — forward and stride-1 dgrad with a
+    residual addend are fp32-class vs fp64; BN partials agree with the default's."""
     from hkp import ops
     from hkp._lib import call
     n, h, w, cin, cout, k, st, pad, dil = case
@@ -477,7 +479,7 @@ def test_x3_w4_body(cuda_device, case):
     add_d = add.permute(0, 2, 3, 1).contiguous().to(d)
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False)
     try:
-        call("hkp_set_conv_variant", 43)
+        call("hkp_set_conv_variant", knob)
         y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False)
         dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add_d, amax=amax, sk=False) \
             if cin % 256 == 0 else None
