@@ -1742,7 +1742,10 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
         hipLaunchKernelGGL((conv_x3_kernel<256, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
     else if (ord == 4 && bn == 256 && kh == 2 && !mf16 && !a.sk_units && w4_fits)
         hipLaunchKernelGGL(conv_x3_w4_kernel, grid, dim3(256), 0, st, a);
-    else if (a.sk_units && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
+    else if (a.sk_units && bn == 128 && ord == 7)     // knob 70: the 32x32x16 stream-K body
+        hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
+    else if (a.sk_units && bn == 128)                  // 16x16x32 (training t4 fwd +3-6 %, t3 +6 %)
+        hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16, true>), grid, dim3(512), 0, st, a);
     else if (a.sk_units) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
     else if (mf16 && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
     else if (mf16) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
@@ -2064,7 +2067,8 @@ extern "C" int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc) {
     const bool kh2 = !(v == 4 && bn == 256) && !(v == 2 && bn == 128);
     const bool mf16_pol = (v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
                            (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus()) ||
-                          (bn == 256 && kh2 && !pl.sk && ord != 6 && ord != 4);
+                          (bn == 256 && kh2 && !pl.sk && ord != 6 && ord != 4) ||
+                          (pl.sk && bn == 128 && ord != 7);
     return mf16_pol ? 16 : 32;
 }
 extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
@@ -2076,7 +2080,7 @@ extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 70, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 80, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

@@ -128,8 +128,9 @@ int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc);
 /* 1 if that launch (rsc = R*S*Cin, the GEMM depth) runs stream-K under the
  * current knob and a workspace (the conv_x3_kernel<..., true> instantiation). */
 int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc);
-/* K of the MFMA that launch uses: 32 (32x32x16) or 16 (16x16x32 — 256x128 tiles on
- * grids of >= 2 full rounds, where the lower-power shape holds a higher clock). */
+/* K of the MFMA that launch uses: 32 (32x32x16) or 16 (16x16x32: 256x256 tiles,
+ * stream-K 256x128 tiles, and 256x128 tiles on grids of >= 2 full rounds — the
+ * lower-power shape holds a higher clock under load). */
 int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc);
 int hkp_set_conv_variant(int32_t variant);
 
