@@ -257,13 +257,12 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         }
     };
 
-    if constexpr (BN == 256) {
-        // 256x256 on the 2-stage ring (the 8-wave WIDE2 ring), A single-buffered
+    if constexpr (NST == 2) {
+        // 2-stage ring (256x256 tiles; 256x64 at two blocks per CU), A single-buffered
         // (registers: 128 acc + 32 A + 64 B): per K-step t — wait own DMA of t+1,
         // barrier, issue DMA t+2 into t's buffer (read before the barrier), then per
         // column j [MFMAs of t with B_j] [refill B_j with t+1's], then A of t+1
         // (its latency covered by the SIMD's other wave)
-        static_assert(NST == 2, "256-wide 16x16x32 body runs the 2-stage ring");
         issue_next();
         if (nks > 1) issue_next();
         if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
@@ -469,7 +468,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
-    static_assert(MFD == 32 || (MFD == 16 && KH == 2 && !STEM), "bad conv_x3 MFMA shape");
+    static_assert(MFD == 32 || (MFD == 16 && KH == 2), "bad conv_x3 MFMA shape");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
@@ -1690,6 +1689,7 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
     }
     return best;
 }
+static const bool g_stem_mf16 = getenv("HKP_STEM_MF16") && atoi(getenv("HKP_STEM_MF16")) == 1;
 static double g_mf16_rounds = [] {
     const char* e = getenv("HKP_MF16_ROUNDS");
     return e ? atof(e) : 2.0;
@@ -1707,9 +1707,6 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
     if (v == 5) bn = 64;
     if ((v == 4 && bn == 256) || (v == 2 && bn == 128)) kh = 1;
-    // 256x64 tiles: two blocks per CU with 16-channel stages (the short tiles'
-    // prologue / epilogue overlap the other block's main loop: layer1 +10 %);
-    // knob 20 = the one-block 32-channel-stage kernel
     // 16x16x32 MFMAs for 256x128 tiles on grids of >= HKP_MF16_ROUNDS (2) full
     // rounds: the same cycles per FLOP at lower power, so the chip holds a higher
     // clock (MI355X_MICROARCH.md DVFS item 7) — C2 layer3 +6 %, layer2 +5 %; on
@@ -1721,7 +1718,10 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
                           (bn == 256 && kh == 2 && !pl.sk && ord != 6 && ord != 4);
     const bool mf16 = v == 6 || v == 7 || mf16_pol;
     if (v == 6 || v == 7) bn = (v == 7 || k % 128) ? 64 : 128;
-    if (bn == 64 && ord != 2 && !pl.sk && !mf16) kh = 1;
+    // 256x64 tiles run two blocks per CU: by default the 16x16x32 body on a 2-stage
+    // 32-channel ring (layer1 0.223 -> 0.166 ms, t1 0.065 -> 0.049); knob 80 = the
+    // 32x32x16 body on a 4-stage 16-channel ring, knob 20 = one block per CU
+    if (bn == 64 && ord == 8 && !pl.sk && !mf16) kh = 1;
     a.n_tiles = k / bn;
     a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
     a.sk_units = 0;
@@ -1754,6 +1754,8 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
     else if (bn == 128 && kh == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128 && ord == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 1>), grid, dim3(512), 0, st, a);
     else if (bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2>), grid, dim3(512), 0, st, a);
+    else if (bn == 64 && kh == 2 && ord != 2 && ord != 8 && !mf16 && !a.sk_units)   // 16x16x32, two blocks per CU
+        hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 3, 16>), grid, dim3(512), 0, st, a);
     else if (kh == 1) hipLaunchKernelGGL((conv_x3_kernel<64, 1, false, 3>), grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((conv_x3_kernel<64, 2>), grid, dim3(512), 0, st, a);
 }
@@ -2041,6 +2043,9 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     // knob 20 = one block per CU with a 3-stage ring
     if (g_x3_variant / 10 == 2)
         hipLaunchKernelGGL((conv_x3_kernel<64, 2, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+    else if (g_stem_mf16)              // 16x16x32 stem body (A/B: HKP_STEM_MF16=1)
+        hipLaunchKernelGGL((conv_x3_kernel<64, 2, true, 3, 16>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
+                           as_stream(stream), a);
     else
         hipLaunchKernelGGL((conv_x3_kernel<64, 2, true, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream),
                            a);
@@ -2068,7 +2073,8 @@ extern "C" int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc) {
     const bool mf16_pol = (v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
                            (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus()) ||
                           (bn == 256 && kh2 && !pl.sk && ord != 6 && ord != 4) ||
-                          (pl.sk && bn == 128 && ord != 7);
+                          (pl.sk && bn == 128 && ord != 7) ||
+                          (bn == 64 && kh2 && !pl.sk && ord != 2 && ord != 8);
     return mf16_pol ? 16 : 32;
 }
 extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
@@ -2080,7 +2086,7 @@ extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 80, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 90, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

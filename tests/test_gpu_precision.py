@@ -174,7 +174,7 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
     try:
-        for var in (1, 2, 3, 4, 6, 7, 8, 9, 40, 43, 60, 63, 70, 78):
+        for var in (1, 2, 3, 4, 6, 7, 8, 9, 40, 43, 60, 63, 70, 78, 80, 85):
             call("hkp_set_conv_variant", var)
             yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
             # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
