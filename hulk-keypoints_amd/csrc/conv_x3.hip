@@ -1499,6 +1499,206 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
         }
 }
 
+// The same weight gradient with v_mfma_f32_16x16x32_f16 (one k32 MFMA per 16x16
+// block and product per 32-pixel K-step; the lower-power shape holds a higher
+// clock).  A 16x16x32 operand lane holds 8 consecutive pixels of one channel for
+// pixel block (lane >> 4): the four 16-lane groups read rows 8G.. of the same 16
+// channels, so rows r and r+8 would share banks — the staging adds a second
+// swizzle bit (chunk ^= ((pixel >> 3) & 1) << 1) on top of the 32x32 kernel's.
+// Pipeline (3-stage ring): issue DMA t+2, wait own DMA of t+1 + this wave's
+// reads, barrier, [read t+1's fragments | MFMAs of t].
+template <int KA>
+__global__ __launch_bounds__(512, 1) void wgrad_x3_mf16_kernel(WgX3Args a) {
+    constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
+    constexpr int ROW = 128, STAGE = (GX + GD) * 32 * ROW;
+    constexpr int NX = 4, ND = GD / 2, GL = NX + ND;
+    constexpr int TM = KA / 64, TN = 2;               // 32-row / 32-column groups per wave
+    constexpr int UM = 2 * TM, UN = 2 * TN;           // 16x16 blocks per wave
+    static_assert(ND >= 1, "KA must be 64 or 128");
+    __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int split = bid / a.tiles, tile = bid - split * a.tiles;
+    const int kt = tile / a.r_tiles, rt = tile - kt * a.r_tiles;
+    const int k0 = kt * KA, r0 = rt * BR;
+    const int p_begin = split * a.mps;
+    const int p_end = min(a.M, p_begin + a.mps);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // ---- staging (as wgrad_x3_kernel, plus the pixel-bit-3 swizzle) ----
+    const int Lx = ((lane & 7) ^ (((lane >> 4) & 1) << 2)) * 8;
+    const int Lx8 = Lx ^ 16;                                      // pixel bit 3 set: chunk ^ 2
+    const int mg = r0 + 32 * w;
+    const bool gvalid = mg < a.RSC;
+    const int tap = gvalid ? mg / a.C : 0;
+    const int cg = gvalid ? (mg - tap * a.C) >> 5 : 0;
+    const int rr = tap / a.S, ss = tap - rr * a.S;
+    const int dh = rr * a.dil - a.pad, dw = ss * a.dil - a.pad;
+    const int xstride = a.C * 2, dstride = a.K * 2;
+    const _Float16* xg0 = a.xs + cg * 64 + Lx;
+    const _Float16* xg1 = a.xs + cg * 64 + Lx8;
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    int xn[NX], xho[NX], xwo[NX];
+    const int hw = a.Ho * a.Wo;
+#pragma unroll
+    for (int i = 0; i < NX; ++i) {
+        const int p = p_begin + 8 * i + (lane >> 3);
+        xn[i] = p / hw;
+        const int rem = p - xn[i] * hw;
+        xho[i] = rem / a.Wo;
+        xwo[i] = rem - xho[i] * a.Wo;
+    }
+    const _Float16* dg[ND];
+    int dpp[ND];
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+        const int line = 8 * (w * ND + j) + (lane >> 3);
+        dpp[j] = line & 31;
+        dg[j] = a.dys + (k0 >> 5) * 64 + (line >> 5) * 64 + (((w * ND + j) & 1) ? Lx8 : Lx);
+    }
+    auto issue = [&](int t) {
+        char* st = smem + (t % 3) * STAGE;
+        const int pb = p_begin + 32 * t;
+#pragma unroll
+        for (int i = 0; i < NX; ++i) {
+            const int p = pb + 8 * i + (lane >> 3);
+            const int hi = xho[i] * a.stride + dh, wi = xwo[i] * a.stride + dw;
+            const bool in = gvalid && p < p_end && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            const long pix = ((long)xn[i] * a.H + hi) * a.W + wi;
+            glds16(in ? ((i & 1) ? xg1 : xg0) + pix * xstride : zero, st + (w * 32 + 8 * i) * ROW);
+            xwo[i] += 32;
+            while (xwo[i] >= a.Wo) {
+                xwo[i] -= a.Wo;
+                if (++xho[i] == a.Ho) {
+                    xho[i] = 0;
+                    ++xn[i];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ND; ++j) {
+            const int p = pb + dpp[j];
+            glds16(p < p_end ? dg[j] + (long)p * dstride : zero, st + (GX * 32 + 8 * (w * ND + j)) * ROW);
+        }
+    };
+
+    f32x4 acc[UM][UN];
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // transposed reads: 16-lane group G reads pixel rows 8G+q (and +4) of 16
+    // channels (block c16); lane 4q+p supplies row q, channels 4p..4p+3
+    const int wk = w & 1, wr = w >> 1;
+    const int G = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+    const unsigned lds0 = lds_addr_of(smem);
+    unsigned tbase[2][2];                          // [plane][c16]: per-lane byte offset in a 32-line group
+#pragma unroll
+    for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int c16 = 0; c16 < 2; ++c16)
+            tbase[pl][c16] = (8 * G + q) * ROW +
+                             (((4 * pl + 2 * c16 + (pq >> 1)) ^ (((q >> 1) & 1) << 2) ^ ((G & 1) << 1)) << 4) +
+                             8 * (pq & 1);
+    const unsigned a_line = lds0 + (GX + wk * TM) * 32 * ROW;   // dy groups of this wave
+    const unsigned b_line = lds0 + (wr * TN) * 32 * ROW;        // x groups of this wave
+    // dy (A) fragments double-buffered; x (B) fragments refilled in place after
+    // their column's MFMAs (the conv's 16x16x32 body does the same)
+    struct FA {
+        f16x8 h[UM], l[UM];
+    };
+    f16x8 xh[UN], xl[UN];
+    auto read_a = [&](FA& f, int buf) {
+        const unsigned so = buf * STAGE;
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            const unsigned g0 = a_line + so + (i >> 1) * 32 * ROW;
+            f.h[i] = cat_tr(ds_tr16<0>(g0 + tbase[0][i & 1]), ds_tr16<4 * ROW>(g0 + tbase[0][i & 1]));
+            f.l[i] = cat_tr(ds_tr16<0>(g0 + tbase[1][i & 1]), ds_tr16<4 * ROW>(g0 + tbase[1][i & 1]));
+        }
+    };
+    auto read_b = [&](int j, int buf) {
+        const unsigned g0 = b_line + buf * STAGE + (j >> 1) * 32 * ROW;
+        xh[j] = cat_tr(ds_tr16<0>(g0 + tbase[0][j & 1]), ds_tr16<4 * ROW>(g0 + tbase[0][j & 1]));
+        xl[j] = cat_tr(ds_tr16<0>(g0 + tbase[1][j & 1]), ds_tr16<4 * ROW>(g0 + tbase[1][j & 1]));
+    };
+    auto mma_col = [&](const FA& f, int j) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], xh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], xl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.l[i], xh[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
+    if (nsteps > 0) {
+        int q_t = 0;
+        auto issue_next = [&]() { issue(q_t++); };
+        issue_next();
+        if (nsteps > 1) issue_next();
+        if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        FA fa0, fa1;
+        int cur = 0;
+        read_a(fa0, 0);
+#pragma unroll
+        for (int j = 0; j < UN; ++j) read_b(j, 0);
+        // K-step t with fc and the B registers (t's), reading t+1's A into fn and
+        // t+1's B column by column
+        auto step = [&](int t, const FA& fc, FA& fn) {
+            if (t + 2 < nsteps) issue_next();
+            if (t + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            cur = cur == 2 ? 0 : cur + 1;
+            read_a(fn, cur);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                // the inline-asm reads of B_j(t) were waited for above; refill after use
+                mma_col(fc, j);
+                read_b(j, cur);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        int t = 0;
+        for (; t + 2 < nsteps; t += 2) {
+            step(t, fa0, fa1);
+            step(t + 1, fa1, fa0);
+        }
+        if (t + 1 < nsteps) {
+            step(t, fa0, fa1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) mma_col(fa1, j);
+        } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) mma_col(fa0, j);
+        }
+    }
+
+    const float inv = 1.f / pow2_scale_for(a.amax);
+    float* out = a.ws + (long)split * a.K * a.RSC;
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            const int m = r0 + wr * 64 + j * 16 + (lane & 15);
+            if (m >= a.RSC) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int k = k0 + wk * TM * 32 + i * 16 + 4 * G + r;
+                out[(long)k * a.RSC + m] = acc[i][j][r] * inv;
+            }
+        }
+}
+
 // dw[i] = sum_split ws[split][i], fixed order
 __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, const f32x4* __restrict__ ws,
                                                           f32x4* __restrict__ dw) {
@@ -1513,6 +1713,9 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
         dw[i] = s;
     }
 }
+
+// 16x16x32 wgrad body (A/B: HKP_WG_MF16=1)
+static const bool g_wg_mf16 = getenv("HKP_WG_MF16") && atoi(getenv("HKP_WG_MF16")) == 1;
 
 static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, int* ka, int* r_tiles) {
     *ka = d->k % 128 == 0 ? 128 : 64;
@@ -1966,7 +2169,12 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     a.tiles = (d->k / ka) * rt;
     hipStream_t st = as_stream(stream);
     const unsigned grid = (unsigned)(a.tiles * sp);
-    if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
+    // 16x16x32 wgrad body: opt-in (HKP_WG_MF16=1 or knob 90) — measured equal to
+    // the 32x32x16 one on the C3 shard (345 vs 346 us per layer4-class launch)
+    const bool wg16 = g_wg_mf16 || g_x3_variant / 10 == 9;
+    if (wg16 && ka == 128) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<128>, dim3(grid), dim3(512), 0, st, a);
+    else if (wg16) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<64>, dim3(grid), dim3(512), 0, st, a);
+    else if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<64>, dim3(grid), dim3(512), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3");
     long g = (n / 4 + 255) / 256;
@@ -2086,7 +2294,7 @@ extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
 }
 
 extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 90, "hkp_set_conv_variant: unknown variant %d",
+    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 100, "hkp_set_conv_variant: unknown variant %d",
                   variant);
     g_x3_variant = variant;
     return HKP_OK;

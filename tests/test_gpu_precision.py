@@ -323,6 +323,15 @@ def test_x3_wgrad_scaled(cuda_device, case, gscale):
     if cin % 64 == 0:   # same sums as the register-staged split wgrad, different order
         dw2 = ops.conv2d_bwd_filter_split(xd, gy_d, (cout, k, k, cin), st, pad, dil, amax=amax)
         assert (dw - dw2).abs().max().item() <= 4e-6 * dw2.abs().max().item()
+    from hkp._lib import call
+    try:                # the 16x16x32 wgrad body (knob 90)
+        call("hkp_set_conv_variant", 90)
+        dw16 = ops.conv2d_bwd_filter_x3(xs, ops.split_pack_x3(gy_d, amax), (cout, k, k, cin), st, pad, dil,
+                                        amax=amax)
+    finally:
+        call("hkp_set_conv_variant", 0)
+    err16 = (dw16.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+    assert err16 < 2e-6, err16
 
 
 @pytest.mark.parametrize("shape", [(2, 3, 50, 70), (3, 3, 33, 41), (1, 1, 20, 26), (2, 3, 480 // 4, 640 // 4)])
