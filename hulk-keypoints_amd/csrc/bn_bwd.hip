@@ -22,7 +22,10 @@ constexpr int BNB_TILE = 64;   // pixels per reduction tile (small: enough block
 // G = channel groups of 4 per thread (C/4 / threads-per-row); MASK: dz = g*(out>0)
 // MAXIMA: also per tile and channel max|dz| and max|y - mean| (the inputs of
 // finalize's upper bound on max|dy|)
-template <int G, bool MASK, bool MAXIMA = false>
+// MASK 2: the ReLU mask recomputed from y as the forward's bn_apply did,
+// round(round(y*scale) + shift) > 0 (out = the forward's [scale | shift]), so an
+// inner BN's fp32 activation is not read back (bit-identical mask)
+template <int G, int MASK, bool MAXIMA = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const float* __restrict__ g,
                                                            const float* __restrict__ out, const float* __restrict__ y,
                                                            const float* __restrict__ mean, float* __restrict__ dz,
@@ -46,18 +49,29 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
         xv[k] = s[k];
         mu[k] = *(const f32x4*)(mean + 4 * (cg + k * tpr));
     }
+    f32x4 msc[G], msh[G];
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        if constexpr (MASK == 2) {
+            msc[k] = *(const f32x4*)(out + 4 * (cg + k * tpr));
+            msh[k] = *(const f32x4*)(out + C + 4 * (cg + k * tpr));
+        }
+    }
     for (long m = m0 + rl; m < m1; m += rpar) {
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             const long off = m * C + 4 * (cg + k * tpr);
             f32x4 d = *(const f32x4*)(g + off);
-            if constexpr (MASK) {
+            const f32x4 v = *(const f32x4*)(y + off);
+            if constexpr (MASK == 1) {
                 const f32x4 o = *(const f32x4*)(out + off);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+            } else if constexpr (MASK == 2) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d[e] = __fadd_rn(__fmul_rn(v[e], msc[k][e]), msh[k][e]) > 0.f ? d[e] : 0.f;
             }
             if (dz) *(f32x4*)(dz + off) = d;
-            const f32x4 v = *(const f32x4*)(y + off);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 s[k][e] += d[e];
@@ -181,7 +195,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long
 // SPLIT: dy is written as the packed f16x3 split of dy * 2^e, e from the upper
 // bound finalize left in *amax (the operand of the x3 backward convs, which need
 // no separate hkp_split_pack_x3 pass); the fp32 dy only if dy != NULL
-template <bool MASK, bool AMAX, bool SPLIT = false>
+template <int MASK, bool AMAX, bool SPLIT = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, const f32x4* __restrict__ g,
                                                           const f32x4* __restrict__ out, const f32x4* __restrict__ y,
                                                           const f32x4* __restrict__ mean,
@@ -193,12 +207,16 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long n4, int C4, cons
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         const int c4 = (int)(i % C4);
         f32x4 d = g[i];
-        if constexpr (MASK) {
+        const f32x4 v = y[i], mu = mean[c4], gm = coef[c4], kk = coef[C4 + c4], sc = coef[2 * C4 + c4];
+        if constexpr (MASK == 1) {
             const f32x4 o = out[i];
 #pragma unroll
             for (int e = 0; e < 4; ++e) d[e] = o[e] > 0.f ? d[e] : 0.f;
+        } else if constexpr (MASK == 2) {   // out = the forward's [scale | shift]
+            const f32x4 ma = out[c4], mb = out[C4 + c4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[e] = __fadd_rn(__fmul_rn(v[e], ma[e]), mb[e]) > 0.f ? d[e] : 0.f;
         }
-        const f32x4 v = y[i], mu = mean[c4], gm = coef[c4], kk = coef[C4 + c4], sc = coef[2 * C4 + c4];
         f32x4 r;
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[e] = ((d[e] - gm[e]) - (v[e] - mu[e]) * kk[e]) * sc[e];
@@ -287,27 +305,34 @@ using namespace hkp;
 
 extern "C" int64_t hkp_bn_bwd_tiles(int64_t m) { return (m + BNB_TILE - 1) / BNB_TILE; }
 
-extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                                 const float* mean_invstd, float* dz, float* partials, float* maxima,
+extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* relu_ss,
+                                 const float* y, const float* mean_invstd, float* dz, float* partials, float* maxima,
                                  uint32_t* dy_bound_bits, hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_reduce: bad sizes");
+    HKP_CHECK_ARG(!(out_mask && relu_ss), "hkp_bn_bwd_reduce: out_mask and relu_ss are exclusive");
     HKP_CHECK_ARG(g && y && mean_invstd && partials, "hkp_bn_bwd_reduce: null tensor");
     const int C4 = c / 4;
     HKP_CHECK_ARG((C4 <= 256 && 256 % C4 == 0) || C4 == 512, "hkp_bn_bwd_reduce: unsupported C=%d", c);
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     hipStream_t st = as_stream(stream);
     HKP_CHECK_ARG(!dy_bound_bits || maxima, "hkp_bn_bwd_reduce: dy_bound_bits needs maxima");
+    const float* mk = out_mask ? out_mask : relu_ss;
 #define HKP_BNR(G, MK, MX)                                                                                          \
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<G, MK, MX>), dim3((unsigned)tiles), dim3(256), 0, st, (long)m, c, g,   \
-                       out_mask, y, mean_invstd, dz, partials, maxima, (unsigned*)dy_bound_bits)
+                       mk, y, mean_invstd, dz, partials, maxima, (unsigned*)dy_bound_bits)
 #define HKP_BNR2(G, MK)                  \
     if (maxima) HKP_BNR(G, MK, true);    \
     else HKP_BNR(G, MK, false)
+#define HKP_BNR3(G)                                           \
+    if (out_mask) { HKP_BNR2(G, 1); }                         \
+    else if (relu_ss) { HKP_BNR2(G, 2); }                     \
+    else { HKP_BNR2(G, 0); }
     if (C4 == 512) {
-        if (out_mask) { HKP_BNR2(2, true); } else { HKP_BNR2(2, false); }
+        HKP_BNR3(2);
     } else {
-        if (out_mask) { HKP_BNR2(1, true); } else { HKP_BNR2(1, false); }
+        HKP_BNR3(1);
     }
+#undef HKP_BNR3
 #undef HKP_BNR2
 #undef HKP_BNR
     HKP_LAUNCH_CHECK("hkp_bn_bwd_reduce");
@@ -337,10 +362,13 @@ extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, 
     return HKP_OK;
 }
 
-extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                                const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
-                                uint16_t* dy_split, hkp_stream_t stream) {
+extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* relu_ss,
+                                const float* y, const float* mean_invstd, const float* coef, float* dy,
+                                uint32_t* dy_amax_bits, uint16_t* dy_split, hkp_stream_t stream) {
     HKP_CHECK_ARG(m > 0 && c > 0 && c % 4 == 0, "hkp_bn_bwd_apply: bad sizes");
+    HKP_CHECK_ARG(!(out_mask && relu_ss), "hkp_bn_bwd_apply: out_mask and relu_ss are exclusive");
+    const float* mk = out_mask ? out_mask : relu_ss;
+    const int mmode = out_mask ? 1 : (relu_ss ? 2 : 0);
     HKP_CHECK_ARG(g && y && mean_invstd && coef && (dy || dy_split), "hkp_bn_bwd_apply: null tensor");
     HKP_CHECK_ARG(!dy_split || (dy_amax_bits && c % 32 == 0), "hkp_bn_bwd_apply: dy_split needs the bound and c%%32==0");
     const long n4 = m * (long)c / 4;
@@ -348,16 +376,21 @@ extern "C" int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const floa
 #define HKP_BWD_APPLY3(MASK, AMAX, SPLIT)                                                                            \
     hipLaunchKernelGGL((bn_bwd_apply_kernel<MASK, AMAX, SPLIT>),                                                    \
                        dim3(AMAX ? std::min(grid_cap(n4), 512) : grid_cap(n4)), dim3(256), 0, st, n4, c / 4,       \
-                       (const f32x4*)g, (const f32x4*)out_mask, (const f32x4*)y, (const f32x4*)mean_invstd,       \
+                       (const f32x4*)g, (const f32x4*)mk, (const f32x4*)y, (const f32x4*)mean_invstd,             \
                        (const f32x4*)coef, (f32x4*)dy, (unsigned*)dy_amax_bits, (_Float16*)dy_split)
 #define HKP_BWD_APPLY(MASK, AMAX) HKP_BWD_APPLY3(MASK, AMAX, false)
+#define HKP_BWD_MODES(AMAX, SPLIT)                                                    \
+    if (mmode == 1) { HKP_BWD_APPLY3(1, AMAX, SPLIT); }                              \
+    else if (mmode == 2) { HKP_BWD_APPLY3(2, AMAX, SPLIT); }                         \
+    else { HKP_BWD_APPLY3(0, AMAX, SPLIT); }
     if (dy_split) {
-        if (out_mask) HKP_BWD_APPLY3(true, false, true); else HKP_BWD_APPLY3(false, false, true);
-    } else if (out_mask) {
-        if (dy_amax_bits) HKP_BWD_APPLY(true, true); else HKP_BWD_APPLY(true, false);
+        HKP_BWD_MODES(false, true);
+    } else if (dy_amax_bits) {
+        HKP_BWD_MODES(true, false);
     } else {
-        if (dy_amax_bits) HKP_BWD_APPLY(false, true); else HKP_BWD_APPLY(false, false);
+        HKP_BWD_MODES(false, false);
     }
+#undef HKP_BWD_MODES
 #undef HKP_BWD_APPLY
 #undef HKP_BWD_APPLY3
     HKP_LAUNCH_CHECK("hkp_bn_bwd_apply");

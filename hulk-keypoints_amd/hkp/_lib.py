@@ -96,9 +96,9 @@ SIGNATURES = {
     "hkp_conv_bwd_filter_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _I64, _P]),
     "hkp_bn_bwd_tiles": (_I64, [_I64]),
-    "hkp_bn_bwd_reduce": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_reduce": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_bwd_finalize": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "hkp_heat_loss_workspace": (_I64, []),
     "hkp_heat_loss": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _F, _P, _P, _P, _P]),

@@ -384,6 +384,8 @@ class Grads(dict):
 # wgrad of a conv runs on a side stream, concurrently with its dgrad: the two
 # grids fill each other's last partial round of CUs (HKP_OVERLAP_WGRAD=0: serial)
 OVERLAP_WGRAD = os.environ.get("HKP_OVERLAP_WGRAD", "1") != "0"
+# inner BN ReLU masks recomputed from y (HKP_MASK_FROM_Y=0: read the fp32 activation)
+_MASK_FROM_Y = os.environ.get("HKP_MASK_FROM_Y", "1") != "0"
 _side_streams = {}
 _dev_total = {}
 
@@ -476,9 +478,9 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
     return dx
 
 
-def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False, split_only=False):
+def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False, split_only=False, relu_ss=None):
     dy, dgamma, dbeta, dz = ops.bn_bwd(g, out_mask, y, mi, bn.weight, want_dz=want_dz,
-                                       want_amax=_precision == "f16x3", split_only=split_only)
+                                       want_amax=_precision == "f16x3", split_only=split_only, relu_ss=relu_ss)
     grads.put(bn.weight, dgamma)
     grads.put(bn.bias, dbeta)
     return dy, dz
@@ -502,11 +504,16 @@ def block_backward(block, rec, g_out, grads):
         dx_res = _conv_backward(ds, x, gd, grads)
     else:
         dx_res = dz
-    # main path, last conv first; inner BN masks come from the stored activations
+    # main path, last conv first; an inner BN's ReLU mask is recomputed from its
+    # y and forward scale/shift (bit-identical; the fp32 activation is not read)
     for li in range(len(convs) - 1, 0, -1):
         da = _conv_backward(convs[li], acts[li - 1], g, grads)
-        g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads,
-                            split_only=_x3_backward(convs[li - 1], ins[li - 1]))
+        if _MASK_FROM_Y:
+            g, _ = _bn_backward(bns[li - 1], da, None, ys[li - 1], mis[li - 1], grads,
+                                split_only=_x3_backward(convs[li - 1], ins[li - 1]), relu_ss=rec["ss"][li - 1])
+        else:
+            g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads,
+                                split_only=_x3_backward(convs[li - 1], ins[li - 1]))
     return _conv_backward(convs[0], x, g, grads, add=dx_res)
 
 

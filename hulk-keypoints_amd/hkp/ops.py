@@ -792,8 +792,10 @@ def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out
     return dw
 
 
-def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, split_only=False):
+def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, split_only=False, relu_ss=None):
     """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None).
+    The ReLU mask is out_mask > 0, or (relu_ss = the forward's scale_shift) is
+    recomputed from y bit-identically — no read of the fp32 activation.
     want_amax: max|dy| (uint32 IEEE bits, as absmax) is computed in the same pass
     and attached as dy._hkp_amax.  split_only: dy is returned as the packed f16x3
     split of dy * 2^e (the x3 backward convs' operand, _hkp_split_passes = 3) with
@@ -804,6 +806,12 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, s
     if g.shape != y.shape or (out_mask is not None and out_mask.shape != y.shape):
         raise HkpError("bn_bwd: shape mismatch")
     c = y.shape[-1]
+    if relu_ss is not None:
+        if out_mask is not None:
+            raise HkpError("bn_bwd: out_mask and relu_ss are exclusive")
+        _need(relu_ss, torch.float32, "bn_bwd.relu_ss", 1)
+        if relu_ss.numel() != 2 * c:
+            raise HkpError("bn_bwd: relu_ss must be [2C]")
     m = y.numel() // c
     if split_only and c % 32:
         raise HkpError("bn_bwd: split_only needs C % 32 == 0")
@@ -813,8 +821,8 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, s
     maxima = torch.empty((tiles, c, 2), device=y.device, dtype=torch.float32) if split_only else None
     amax = torch.empty(1, device=y.device, dtype=torch.int32) if (want_amax or split_only) else None
     dz = torch.empty_like(y) if want_dz else None
-    call("hkp_bn_bwd_reduce", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(dz), _ptr(part),
-         _ptr(maxima), _ptr(amax if split_only else None), _stream())
+    call("hkp_bn_bwd_reduce", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd), _ptr(dz),
+         _ptr(part), _ptr(maxima), _ptr(amax if split_only else None), _stream())
     dgamma = torch.empty(c, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(c, device=y.device, dtype=torch.float32)
     coef = torch.empty(3 * c, device=y.device, dtype=torch.float32)
@@ -822,12 +830,12 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, s
          _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
     if split_only:
         dy = _split_out(y.shape, y.device, 3)
-        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), None,
-             _ptr(amax), _ptr(dy), _stream())
+        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd),
+             _ptr(coef), None, _ptr(amax), _ptr(dy), _stream())
     else:
         dy = torch.empty_like(y)
-        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(y), _ptr(mean_invstd), _ptr(coef), _ptr(dy),
-             _ptr(amax), None, _stream())
+        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd),
+             _ptr(coef), _ptr(dy), _ptr(amax), None, _stream())
     if want_amax or split_only:
         dy._hkp_amax = amax
     return dy, dgamma, dbeta, dz

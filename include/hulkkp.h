@@ -349,15 +349,19 @@ int hkp_conv2d_bwd_filter(const hkp_conv_desc* d, const float* x, const float* d
  *             operand of the x3 backward convs, with no hkp_split_pack_x3 pass and
  *             dy (fp32) optional; else dy_amax_bits (nullable) gets the exact max|dy|.
  * mean_invstd is what hkp_bn_finalize produced in the forward. */
+/* The ReLU mask: out_mask (the BN+ReLU output, > 0), or relu_ss = the forward's
+ * [scale | shift] of this BN — the mask is then recomputed from y exactly as
+ * hkp_bn_apply made it (round(round(y*scale) + shift) > 0), so an inner BN's fp32
+ * activation is not read back; both NULL: no ReLU. */
 int64_t hkp_bn_bwd_tiles(int64_t m);
-int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                      const float* mean_invstd, float* dz, float* partials, float* maxima, uint32_t* dy_bound_bits,
-                      hkp_stream_t stream);
+int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mask, const float* relu_ss,
+                      const float* y, const float* mean_invstd, float* dz, float* partials, float* maxima,
+                      uint32_t* dy_bound_bits, hkp_stream_t stream);
 int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* maxima, const float* mean_invstd,
                         const float* gamma, float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_bits,
                         hkp_stream_t stream);
-int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* y,
-                     const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
+int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* relu_ss,
+                     const float* y, const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
                      uint16_t* dy_split, hkp_stream_t stream);
 
 /* ----------------------------------------------------------- optimizer ---- */

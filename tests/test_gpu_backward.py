@@ -114,6 +114,14 @@ def test_bn_backward(cuda_device, mask, c):
         assert bound.view(torch.float32).item() <= 8 * dy.abs().max().item() + 1e-30
         assert torch.equal(dys, ops.split_pack_x3(dy, bound))
         assert torch.equal(dg2, dgamma) and torch.equal(db2, dbeta)
+    if mask:            # mask recomputed from y and the forward's scale/shift: the same bits
+        dy3, dg3, db3, dz3 = ops.bn_bwd(nhwc(g).to(d), None, y_d, mi, gamma.detach().to(d), want_dz=True,
+                                        want_amax=True, relu_ss=ss)
+        assert torch.equal(dy3, dy) and torch.equal(dz3, dz) and torch.equal(dg3, dgamma) and torch.equal(db3, dbeta)
+        if c % 32 == 0:
+            dys3, _, _, _ = ops.bn_bwd(nhwc(g).to(d), None, y_d, mi, gamma.detach().to(d), split_only=True,
+                                       relu_ss=ss)
+            assert torch.equal(dys3, dys)
 
 
 def test_maxpool_backward(cuda_device):
@@ -380,8 +388,11 @@ def test_backward_calls_exact(cuda_device, bb, k):
         log.append(("conv", conv, xx, dy, add, dx, grads[conv.weight]))
         return dx
 
-    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False, split_only=False):
-        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz, split_only)
+    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False, split_only=False, relu_ss=None):
+        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz, split_only, relu_ss=relu_ss)
+        if relu_ss is not None:          # the mask the kernel recomputes: round(round(y*a) + b) > 0
+            c = y.shape[-1]
+            mask = (y.float() * relu_ss[:c]) + relu_ss[c:]
         log.append(("bn", bn, gr, mask, y, mi, dy, grads[bn.weight], grads[bn.bias]))
         return dy, dz
 
