@@ -277,22 +277,26 @@ def block_forward(block, x, trace=None, final=False):
     # conv consumes (inside the block, no backward trace) is written split-only
     keep = rec is not None
 
-    def act(y, s):
+    def act(y, s, consumer):
+        # training keeps the fp32 activation only where the backward reads it: an
+        # inner activation feeding an x3-backward conv is needed only as its split
+        # (its ReLU mask is recomputed from y, its wgrad reads the split)
         sp = _split_for(y.shape[-1])
-        return ops.bn_apply(y, s, relu=True, split=sp, keep_fp32=keep or not sp)
+        need32 = keep and not (sp == 3 and _MASK_FROM_Y and _x3_conv_backward_ok(consumer))
+        return ops.bn_apply(y, s, relu=True, split=sp, keep_fp32=need32 or not sp)
 
     if block.kind == "basic":
         y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
-        a1 = act(y1, s1)
+        a1 = act(y1, s1, block.conv2)
         y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
         last_y, last_s = y2, s2
         if rec is not None:
             rec.update(x=x, y=[y1, y2], ss=[s1, s2], mi=[m1, m2], act=[a1])
     else:
         y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
-        a1 = act(y1, s1)
+        a1 = act(y1, s1, block.conv2)
         y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
-        a2 = act(y2, s2)
+        a2 = act(y2, s2, block.conv3)
         y3, s3, m3 = conv_bn(block.conv3, block.bn3, a2)
         last_y, last_s = y3, s3
         if rec is not None:
@@ -409,22 +413,32 @@ def _side_stream(dev):
     return s
 
 
-def _x3_backward(conv, x):
-    """Whether conv's backward runs entirely on the packed f16x3 path (x carries its
-    split; dgrad stride 1, or stride 2 without dilation) — then the BN backward
-    feeding it writes dy directly as the packed split (bn_bwd split_only)."""
-    xs = ops.split_of(x)
+def _x3_conv_backward_ok(conv):
+    """conv's backward can run entirely on the packed f16x3 path given a packed x
+    (dgrad stride 1, or stride 2 without dilation)."""
     k, c = conv.weight.shape[0], conv.weight.shape[-1]
     st, dl = _i(conv.stride), _i(conv.dilation)
-    return (_precision == "f16x3" and xs is not None and xs[1] == 3 and k % 64 == 0 and c % 64 == 0
-            and (st == 1 or (st == 2 and dl == 1)))
+    return _precision == "f16x3" and k % 64 == 0 and c % 64 == 0 and (st == 1 or (st == 2 and dl == 1))
+
+
+def _x3_backward(conv, x):
+    """Whether conv's backward runs entirely on the packed f16x3 path (x carries its
+    split) — then the BN backward feeding it writes dy directly as the packed
+    split (bn_bwd split_only)."""
+    xs = ops.split_of(x)
+    return xs is not None and xs[1] == 3 and _x3_conv_backward_ok(conv)
+
+
+def _act_shape(x):
+    """[N,H,W,C] of an activation, fp32 or split-only (fp16 [N,H,W,2C])."""
+    return tuple(x.shape[:-1]) + (ops.channels_of(x),)
 
 
 def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
     """wgrad (+ dgrad with the residual addend fused) for one NHWC conv.  dy: fp32, or
     (x3 path) already the packed scaled split from bn_bwd(split_only=True)."""
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
-    c, k = x.shape[-1], conv.weight.shape[0]
+    c, k = ops.channels_of(x), conv.weight.shape[0]
     xs = ops.split_of(x)
     if _x3_backward(conv, x):
         # packed split operands: dy split once (scaled by a power of two from
@@ -451,10 +465,10 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
         if need_dx:
             if st == 1:
                 wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
-                dx = ops.conv2d_bwd_data_x3(dys, wfs, tuple(x.shape), pd, dl, add=add, amax=amax, sk=ready is None)
+                dx = ops.conv2d_bwd_data_x3(dys, wfs, _act_shape(x), pd, dl, add=add, amax=amax, sk=ready is None)
             else:                          # stride 2: one stride-1 conv per output phase of dx
                 phs = _cached_split(conv.weight, "phase_x3", lambda t: ops.weight_phase_pack_x3(t, pd))
-                dx = ops.conv2d_bwd_data_x3_strided(dys, phs, tuple(x.shape), tuple(conv.weight.shape), pd, add=add,
+                dx = ops.conv2d_bwd_data_x3_strided(dys, phs, _act_shape(x), tuple(conv.weight.shape), pd, add=add,
                                                     amax=amax, sk=ready is None)
         if ready is None:
             dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)

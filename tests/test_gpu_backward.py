@@ -427,6 +427,9 @@ def test_backward_calls_exact(cuda_device, bb, k):
         if rec[0] == "conv":
             _, conv, xx, dy, add, dx, dw = rec
             dy = dense(dy)
+            if xx.dtype == torch.float16:    # split-only activation: x = hi + lo (unscaled)
+                g16 = xx.reshape(*xx.shape[:-1], xx.shape[-1] // 64, 2, 32).double()
+                xx = (g16[..., 0, :] + g16[..., 1, :]).reshape(*xx.shape[:-1], -1)
             st, pd, dl = net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation)
             w = conv.weight.detach().double().cpu().permute(0, 3, 1, 2)
             xc, dyc = xx.double().cpu().permute(0, 3, 1, 2), dy.double().cpu().permute(0, 3, 1, 2)
