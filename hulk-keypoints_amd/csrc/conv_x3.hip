@@ -1284,13 +1284,18 @@ __device__ __forceinline__ f16x8 cat_tr(s16x4 lo, s16x4 hi) {
     return __builtin_bit_cast(f16x8, v);
 }
 
+// KA = 256 (Cout % 256 == 0): a 256x256 tile, 96 MAC per staged byte instead of
+// 64 (KA 128) — the 256x128 body is bound by operand delivery, not the MFMAs
+// (MFMA-busy scales with the intensity: 0.25 at KA 64, 0.42 at KA 128).  Its
+// stage holds PX = 16 pixels (one MFMA k-slice) so three stages fit in 96 KB.
 template <int KA>
 __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
-    constexpr int ROW = 128, STAGE = (GX + GD) * 32 * ROW;
-    constexpr int NX = 4, ND = GD / 2, GL = NX + ND;
+    constexpr int PX = KA == 256 ? 16 : 32;                  // pixels per stage
+    constexpr int ROW = 128, STAGE = (GX + GD) * PX * ROW;
+    constexpr int NX = PX / 8, ND = GD * PX / 64, GL = NX + ND;
     constexpr int TM = KA / 64, TN = 2;
-    static_assert(ND >= 1, "KA must be 64 or 128");
+    static_assert(ND >= 1 && (KA == 64 || KA == 128 || KA == 256), "KA must be 64, 128 or 256");
     __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);       // same pixel range → same XCD
@@ -1328,21 +1333,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
         const int line = 8 * (w * ND + j) + (lane >> 3);
-        dpp[j] = line & 31;
-        dg[j] = a.dys + (k0 >> 5) * 64 + (line >> 5) * 64 + Lx;
+        dpp[j] = line % PX;
+        dg[j] = a.dys + (k0 >> 5) * 64 + (line / PX) * 64 + Lx;
     }
 
     auto issue = [&](int t) {
         char* st = smem + (t % 3) * STAGE;
-        const int pb = p_begin + 32 * t;
+        const int pb = p_begin + PX * t;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
             const int p = pb + 8 * i + (lane >> 3);
             const int hi = xho[i] * a.stride + dh, wi = xwo[i] * a.stride + dw;
             const bool in = gvalid && p < p_end && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
             const long pix = ((long)xn[i] * a.H + hi) * a.W + wi;
-            glds16(in ? xg + pix * xstride : zero, st + (w * 32 + 8 * i) * ROW);
-            xwo[i] += 32;                                    // this slot's pixel for the next K-step
+            glds16(in ? xg + pix * xstride : zero, st + (w * PX + 8 * i) * ROW);
+            xwo[i] += PX;                                    // this slot's pixel for the next K-step
             while (xwo[i] >= a.Wo) {
                 xwo[i] -= a.Wo;
                 if (++xho[i] == a.Ho) {
@@ -1354,7 +1359,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 #pragma unroll
         for (int j = 0; j < ND; ++j) {
             const int p = pb + dpp[j];
-            glds16(p < p_end ? dg[j] + (long)p * dstride : zero, st + (GX * 32 + 8 * (w * ND + j)) * ROW);
+            glds16(p < p_end ? dg[j] + (long)p * dstride : zero, st + (GX * PX + 8 * (w * ND + j)) * ROW);
         }
     };
 
@@ -1374,8 +1379,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
         toff[pl] = (8 * h + q) * ROW + (((4 * pl + 2 * cb + (pq >> 1)) ^ (((q >> 1) & 1) << 2)) << 4) + 8 * (pq & 1);
-    const int a_line = (GX + wk * TM) * 32 * ROW;     // dy groups of this wave
-    const int b_line = (wr * TN) * 32 * ROW;          // x groups of this wave
+    const int a_line = (GX + wk * TM) * PX * ROW;     // dy groups of this wave
+    const int b_line = (wr * TN) * PX * ROW;          // x groups of this wave
 
     struct Frag {
         f16x8 dh[TM], dl[TM], xh[TN], xl[TN];
@@ -1390,25 +1395,25 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
         for (int i = 0; i < TM; ++i) {
             // immediate offsets: tile i (32 rows), half s (16 rows), second read +4 rows
             if (s == 0) {
-                f.dh[i] = cat_tr(ds_tr16<0>(ta0 + so + i * 32 * ROW), ds_tr16<4 * ROW>(ta0 + so + i * 32 * ROW));
-                f.dl[i] = cat_tr(ds_tr16<0>(ta1 + so + i * 32 * ROW), ds_tr16<4 * ROW>(ta1 + so + i * 32 * ROW));
+                f.dh[i] = cat_tr(ds_tr16<0>(ta0 + so + i * PX * ROW), ds_tr16<4 * ROW>(ta0 + so + i * PX * ROW));
+                f.dl[i] = cat_tr(ds_tr16<0>(ta1 + so + i * PX * ROW), ds_tr16<4 * ROW>(ta1 + so + i * PX * ROW));
             } else {
-                f.dh[i] = cat_tr(ds_tr16<16 * ROW>(ta0 + so + i * 32 * ROW),
-                                 ds_tr16<20 * ROW>(ta0 + so + i * 32 * ROW));
-                f.dl[i] = cat_tr(ds_tr16<16 * ROW>(ta1 + so + i * 32 * ROW),
-                                 ds_tr16<20 * ROW>(ta1 + so + i * 32 * ROW));
+                f.dh[i] = cat_tr(ds_tr16<16 * ROW>(ta0 + so + i * PX * ROW),
+                                 ds_tr16<20 * ROW>(ta0 + so + i * PX * ROW));
+                f.dl[i] = cat_tr(ds_tr16<16 * ROW>(ta1 + so + i * PX * ROW),
+                                 ds_tr16<20 * ROW>(ta1 + so + i * PX * ROW));
             }
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
             if (s == 0) {
-                f.xh[j] = cat_tr(ds_tr16<0>(tb0 + so + j * 32 * ROW), ds_tr16<4 * ROW>(tb0 + so + j * 32 * ROW));
-                f.xl[j] = cat_tr(ds_tr16<0>(tb1 + so + j * 32 * ROW), ds_tr16<4 * ROW>(tb1 + so + j * 32 * ROW));
+                f.xh[j] = cat_tr(ds_tr16<0>(tb0 + so + j * PX * ROW), ds_tr16<4 * ROW>(tb0 + so + j * PX * ROW));
+                f.xl[j] = cat_tr(ds_tr16<0>(tb1 + so + j * PX * ROW), ds_tr16<4 * ROW>(tb1 + so + j * PX * ROW));
             } else {
-                f.xh[j] = cat_tr(ds_tr16<16 * ROW>(tb0 + so + j * 32 * ROW),
-                                 ds_tr16<20 * ROW>(tb0 + so + j * 32 * ROW));
-                f.xl[j] = cat_tr(ds_tr16<16 * ROW>(tb1 + so + j * 32 * ROW),
-                                 ds_tr16<20 * ROW>(tb1 + so + j * 32 * ROW));
+                f.xh[j] = cat_tr(ds_tr16<16 * ROW>(tb0 + so + j * PX * ROW),
+                                 ds_tr16<20 * ROW>(tb0 + so + j * PX * ROW));
+                f.xl[j] = cat_tr(ds_tr16<16 * ROW>(tb1 + so + j * PX * ROW),
+                                 ds_tr16<20 * ROW>(tb1 + so + j * PX * ROW));
             }
         }
     };
@@ -1426,8 +1431,88 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     // transposed b64 reads per half, two per MFMA gap.  The reads are inline
     // asm: every consumer MFMA sits behind an explicit lgkmcnt wait + sched_barrier.
     constexpr int NR = 4 * (TM + TN), NM = 3 * TM * TN;
-    const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
-    if (nsteps > 0) {
+    const int nsteps = p_end > p_begin ? (p_end - p_begin + PX - 1) / PX : 0;
+    if constexpr (PX == 16) {
+        // one dy fragment set, refilled row by row right after its MFMAs issue
+        // (128 accumulators + 32 dy + 2x16 x registers): per stage t
+        // [issue DMA t+2 | wait own DMA t+1 and this wave's reads, barrier |
+        //  rows i = 0..TM-1 of t's MFMAs, each beside the reads of t+1's row i-1
+        //  (row 0 beside t+1's x fragments), then the reads of t+1's last row]
+        struct XF {
+            f16x8 xh[TN], xl[TN];
+        };
+        f16x8 dh[TM], dl[TM];
+        XF x0, x1;
+        auto read_d = [&](const int i, const unsigned so) {
+            dh[i] = cat_tr(ds_tr16<0>(ta0 + so + i * PX * ROW), ds_tr16<4 * ROW>(ta0 + so + i * PX * ROW));
+            dl[i] = cat_tr(ds_tr16<0>(ta1 + so + i * PX * ROW), ds_tr16<4 * ROW>(ta1 + so + i * PX * ROW));
+        };
+        auto read_x = [&](XF& x, const unsigned so) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                x.xh[j] = cat_tr(ds_tr16<0>(tb0 + so + j * PX * ROW), ds_tr16<4 * ROW>(tb0 + so + j * PX * ROW));
+                x.xl[j] = cat_tr(ds_tr16<0>(tb1 + so + j * PX * ROW), ds_tr16<4 * ROW>(tb1 + so + j * PX * ROW));
+            }
+        };
+        auto mma_row = [&](const int i, const XF& x) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dh[i], x.xh[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dh[i], x.xl[j], acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dl[i], x.xh[j], acc[i][j], 0, 0, 0);
+            }
+        };
+        if (nsteps > 0) {
+            int q_t = 0;
+            issue(q_t++);
+            if (nsteps > 1) issue(q_t++);
+            if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lds_barrier();
+            read_x(x0, 0);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) read_d(i, 0);
+            int nb = 1;                                      // buffer of stage t+1
+            // every non-final stage issues stage t+2's DMA — past the end it loads
+            // zero lines into a buffer no later stage reads — so there is one
+            // kind of non-final step, branch-free, and one final step
+            auto step = [&](const XF& xa, XF& xb) {
+                issue(q_t++);
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+                lds_barrier();
+                __builtin_amdgcn_sched_barrier(0);
+                const unsigned so = nb * STAGE;
+                read_x(xb, so);
+                mma_row(0, xa);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 1; i < TM; ++i) {
+                    read_d(i - 1, so);
+                    mma_row(i, xa);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                read_d(TM - 1, so);
+                __builtin_amdgcn_sched_barrier(0);
+                nb = nb == 2 ? 0 : nb + 1;
+            };
+            auto last = [&](const XF& xa) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // + the dummy DMA
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) mma_row(i, xa);
+            };
+            int t = 0;
+            for (; t + 2 < nsteps; t += 2) {
+                step(x0, x1);
+                step(x1, x0);
+            }
+            if (t + 1 < nsteps) {
+                step(x0, x1);
+                x0 = x1;                                     // one last() call site
+            }
+            last(x0);
+        }
+    } else if (nsteps > 0) {
         int q_t = 0;
         auto issue_next = [&]() { issue(q_t++); };
         issue_next();
@@ -1716,9 +1801,11 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
 
 // 16x16x32 wgrad body (A/B: HKP_WG_MF16=1)
 static const bool g_wg_mf16 = getenv("HKP_WG_MF16") && atoi(getenv("HKP_WG_MF16")) == 1;
+// 256x256 wgrad tile for Cout % 256 == 0 (HKP_WG_KA256=0: the 256x128 tile)
+static const bool g_wg_ka256 = !(getenv("HKP_WG_KA256") && atoi(getenv("HKP_WG_KA256")) == 0);
 
 static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, int* ka, int* r_tiles) {
-    *ka = d->k % 128 == 0 ? 128 : 64;
+    *ka = d->k % 256 == 0 && g_wg_ka256 ? 256 : d->k % 128 == 0 ? 128 : 64;
     const long rsc = (long)d->r * d->s * d->c;
     *r_tiles = (int)((rsc + 255) / 256);
     const long tiles = (long)(d->k / *ka) * *r_tiles;
@@ -2172,7 +2259,8 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     // 16x16x32 wgrad body: opt-in (HKP_WG_MF16=1 or knob 90) — measured equal to
     // the 32x32x16 one on the C3 shard (345 vs 346 us per layer4-class launch)
     const bool wg16 = g_wg_mf16 || g_x3_variant / 10 == 9;
-    if (wg16 && ka == 128) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<128>, dim3(grid), dim3(512), 0, st, a);
+    if (ka == 256) hipLaunchKernelGGL(wgrad_x3_kernel<256>, dim3(grid), dim3(512), 0, st, a);
+    else if (wg16 && ka == 128) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else if (wg16) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<64>, dim3(grid), dim3(512), 0, st, a);
     else if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<64>, dim3(grid), dim3(512), 0, st, a);

@@ -297,6 +297,8 @@ def test_x3_dgrad_strided(cuda_device, case, gscale):
 WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (2, 7, 9, 64, 64, 3, 1, 1, 1),          # Wo = 9 < 32: a K-step spans several rows/images
     (1, 30, 40, 96, 128, 3, 2, 1, 1),       # stride 2, RSC = 864 (ragged 256-column tile)
+    (2, 30, 40, 256, 256, 3, 1, 2, 2),      # 256x256 tile (16-pixel stages), several pixel splits
+    (1, 3, 5, 64, 256, 3, 1, 1, 1),         # 256x256 tile, M = 15: a single stage
 ]
 
 
