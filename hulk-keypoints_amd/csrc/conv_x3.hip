@@ -1790,10 +1790,19 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
     const long stride = (long)gridDim.x * blockDim.x;
     for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
         f32x4 s = ws[i];
-        for (int k = 1; k < splits; ++k) {
-            const f32x4 v = ws[(long)k * n4 + i];
+        // up to eight slab loads in flight per thread (one at a time the loop was
+        // latency-bound), summed in the same left-to-right order
+        for (int k = 1; k < splits; k += 8) {
+            const int cnt = min(8, splits - k);
+            f32x4 v[8];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) s[e] += v[e];
+            for (int u = 0; u < 8; ++u)
+                if (u < cnt) v[u] = __builtin_nontemporal_load(&ws[(long)(k + u) * n4 + i]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < cnt)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s[e] += v[u][e];
         }
         dw[i] = s;
     }
