@@ -2363,6 +2363,14 @@ extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc) {
     if (rsc < 32) return x3_plan(k, (m + 255) / 256, 1, false, 0.0).bn;     // no stream-K workspace
     return x3_tile_n(k, (m + 255) / 256, rsc / 32);
 }
+extern "C" int32_t hkp_wgrad_x3_tile_k(int32_t k) {
+    if (k <= 0 || k % 64 != 0) return -1;
+    hkp_conv_desc d{};
+    d.k = k; d.r = 1; d.s = 1; d.c = 32;
+    int sp, mps, ka, rt;
+    wg_x3_plan(&d, 1024, &sp, &mps, &ka, &rt);
+    return ka;
+}
 extern "C" int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc) {
     if (k <= 0 || m <= 0 || rsc < 0) return -1;
     const int v = g_x3_variant % 10, ord = g_x3_variant / 10;

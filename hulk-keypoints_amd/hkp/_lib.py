@@ -69,6 +69,7 @@ SIGNATURES = {
     "hkp_x3_tile_n": (_I32, [_I32, _I64, _I32]),
     "hkp_x3_stream_k": (_I32, [_I32, _I64, _I32]),
     "hkp_x3_mfma_k": (_I32, [_I32, _I64, _I32]),
+    "hkp_wgrad_x3_tile_k": (_I32, [_I32]),
     "hkp_upsample_argmax_ws_bytes": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_stem_pack_x3_elems": (_I64, [_CD]),
     "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),

@@ -146,6 +146,13 @@ def x3_symbol(k, m, rsc, sk=True):
     return "conv_x3_kernel<%d, 2, false, 0, %d, %s>" % (bn, mfd, "true" if sk else "false")
 
 
+def wgrad_x3_symbol(k):
+    """Kernel symbol the f16x3 weight gradient launches for Cout = k (its Cout tile:
+    conv_x3.hip's wg_x3_plan via hkp_wgrad_x3_tile_k)."""
+    from ._lib import lib
+    return "wgrad_x3_kernel<%d>" % lib().hkp_wgrad_x3_tile_k(k)
+
+
 def weight_pack_x3(w):
     """fp32 KRSC weight → PackedWeight: [K, R, S, 2C] fp16 ([..][C/32][hi32|lo32]) + [K] scales."""
     _need(w, torch.float32, "weight_pack_x3.w", 4)
@@ -768,7 +775,7 @@ def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, al
     if _observer is None:
         launch()
     else:
-        _observer("wgrad_x3_kernel<%d>" % (128 if d.k % 128 == 0 else 64),
+        _observer(wgrad_x3_symbol(d.k),
                   2.0 * n * ho * wo * d.k * d.r * d.s * d.c, 2.0 * (xs.numel() + dys.numel()) + 4.0 * dw.numel(),
                   launch)
     return dw

@@ -132,6 +132,10 @@ int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc);
  * stream-K 256x128 tiles, and 256x128 tiles on grids of >= 2 full rounds — the
  * lower-power shape holds a higher clock under load). */
 int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc);
+/* Cout rows per tile of the f16x3 weight-gradient launch (hkp_conv2d_bwd_filter_x3)
+ * for Cout = k: 256 (Cout % 256 == 0, a 256x256 tile), 128 or 64 — i.e. the
+ * wgrad_x3_kernel<KA> instantiation it runs (opt-in 16x16x32 body aside). */
+int32_t hkp_wgrad_x3_tile_k(int32_t k);
 int hkp_set_conv_variant(int32_t variant);
 
 /* ----------------------------------------------------------- batchnorm ---- */
