@@ -1288,15 +1288,16 @@ __device__ __forceinline__ f16x8 cat_tr(s16x4 lo, s16x4 hi) {
 // 64 (KA 128) — the 256x128 body is bound by operand delivery, not the MFMAs
 // (MFMA-busy scales with the intensity: 0.25 at KA 64, 0.42 at KA 128).  Its
 // stage holds PX = 16 pixels (one MFMA k-slice) so three stages fit in 96 KB.
-template <int KA>
+template <int KA, int NS = 3>
 __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
     constexpr int PX = KA == 256 ? 16 : 32;                  // pixels per stage
+    static_assert(NS == 3 || (NS == 4 && PX == 16), "4-stage ring only for 16-pixel stages");
     constexpr int ROW = 128, STAGE = (GX + GD) * PX * ROW;
     constexpr int NX = PX / 8, ND = GD * PX / 64, GL = NX + ND;
     constexpr int TM = KA / 64, TN = 2;
     static_assert(ND >= 1 && (KA == 64 || KA == 128 || KA == 256), "KA must be 64, 128 or 256");
-    __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
+    __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);       // same pixel range → same XCD
     const int split = bid / a.tiles, tile = bid - split * a.tiles;
@@ -1338,7 +1339,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     }
 
     auto issue = [&](int t) {
-        char* st = smem + (t % 3) * STAGE;
+        char* st = smem + (t % NS) * STAGE;
         const int pb = p_begin + PX * t;
 #pragma unroll
         for (int i = 0; i < NX; ++i) {
@@ -1463,11 +1464,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
             }
         };
         if (nsteps > 0) {
+            // prologue: stages 0..NS-2 (past the end: zero lines, never read)
             int q_t = 0;
-            issue(q_t++);
-            if (nsteps > 1) issue(q_t++);
-            if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int u = 0; u < NS - 1; ++u) issue(q_t++);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * GL) : "memory");
             lds_barrier();
             read_x(x0, 0);
 #pragma unroll
@@ -1477,8 +1478,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
             // zero lines into a buffer no later stage reads — so there is one
             // kind of non-final step, branch-free, and one final step
             auto step = [&](const XF& xa, XF& xb) {
-                issue(q_t++);
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+                issue(q_t++);                                 // stage t+NS-1
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NS - 2) * GL) : "memory");
                 lds_barrier();
                 __builtin_amdgcn_sched_barrier(0);
                 const unsigned so = nb * STAGE;
@@ -1493,7 +1494,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
                 }
                 read_d(TM - 1, so);
                 __builtin_amdgcn_sched_barrier(0);
-                nb = nb == 2 ? 0 : nb + 1;
+                nb = nb == NS - 1 ? 0 : nb + 1;
             };
             auto last = [&](const XF& xa) {
                 asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // + the dummy DMA
@@ -1812,6 +1813,8 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
 static const bool g_wg_mf16 = getenv("HKP_WG_MF16") && atoi(getenv("HKP_WG_MF16")) == 1;
 // 256x256 wgrad tile for Cout % 256 == 0 (HKP_WG_KA256=0: the 256x128 tile)
 static const bool g_wg_ka256 = !(getenv("HKP_WG_KA256") && atoi(getenv("HKP_WG_KA256")) == 0);
+// 4-stage ring (128 KB LDS) for the 256x256 wgrad tile (A/B: HKP_WG_NS4=1)
+static const bool g_wg_ns4 = getenv("HKP_WG_NS4") && atoi(getenv("HKP_WG_NS4")) == 1;
 
 static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, int* ka, int* r_tiles) {
     *ka = d->k % 256 == 0 && g_wg_ka256 ? 256 : d->k % 128 == 0 ? 128 : 64;
@@ -2268,7 +2271,8 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     // 16x16x32 wgrad body: opt-in (HKP_WG_MF16=1 or knob 90) — measured equal to
     // the 32x32x16 one on the C3 shard (345 vs 346 us per layer4-class launch)
     const bool wg16 = g_wg_mf16 || g_x3_variant / 10 == 9;
-    if (ka == 256) hipLaunchKernelGGL(wgrad_x3_kernel<256>, dim3(grid), dim3(512), 0, st, a);
+    if (ka == 256 && g_wg_ns4) hipLaunchKernelGGL((wgrad_x3_kernel<256, 4>), dim3(grid), dim3(512), 0, st, a);
+    else if (ka == 256) hipLaunchKernelGGL((wgrad_x3_kernel<256, 3>), dim3(grid), dim3(512), 0, st, a);
     else if (wg16 && ka == 128) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else if (wg16) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<64>, dim3(grid), dim3(512), 0, st, a);
     else if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
