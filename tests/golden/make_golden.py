@@ -146,6 +146,63 @@ def fwd_case(name, backbone, k, B, H, W, wseed, iseed, full_heat=True, eval_too=
     print(name, "margin min %.3g" % out["margin"].min(), "argmax", out["argmax_yx"].reshape(-1, 2)[:4].tolist())
 
 
+def image_digest(imgs):
+    """sha256 of the uint8 image bytes: large fixtures store this instead of the
+    images, which the tests regenerate from recipe.seeded_images_u8 (PCG64)."""
+    import hashlib
+    return np.array(hashlib.sha256(np.ascontiguousarray(imgs).tobytes()).hexdigest())
+
+
+def heat_from_lowres(low_k, size):
+    """The reference's head applied to the first K fc channels only:
+    upsample_bilinear (resnet_dilated.py:27) then sigmoid (model.py:21).  The
+    reference upsamples all 1000 channels and slices after; ATen's CPU bilinear
+    kernel computes every channel plane independently with the same arithmetic,
+    so slicing first is bit-identical (checked in __main__ on a small case) and
+    avoids a [32,1000,480,640] fp32 (39 GB) intermediate at the bench batch."""
+    return torch.sigmoid(nn.functional.upsample_bilinear(input=low_k, size=size))
+
+
+def fwd_batch_case(name, backbone, k, B, H, W, wseed, iseed):
+    """Forward at a bench-size batch (BASELINE config C2: R34 K4 640x480 B=32):
+    train-mode BN over the whole batch, as analysis.py / Prediction.predict run it.
+    Images are not stored (29 MB); the fixture keeps their digest."""
+    imgs = recipe.seeded_images_u8(B, H, W, iseed)
+    x = recipe.to_tensor_nchw(imgs)
+    m = build(backbone, k, wseed)
+    with torch.no_grad():
+        low = lowres_of(m, backbone, x)[:, :k].contiguous()
+        heat = heat_from_lowres(low, x.size()[2:])
+    sd_after = m.state_dict()
+    h = heat.numpy()
+    out = dict(backbone=np.array(backbone), k=np.int32(k), wseed=np.int32(wseed), iseed=np.int32(iseed),
+               batch=np.int32(B), height=np.int32(H), width=np.int32(W), images_sha256=image_digest(imgs),
+               lowres=low.numpy().astype(np.float32),
+               argmax_yx=np.array([[np.unravel_index(h[b, j].argmax(), h[b, j].shape) for j in range(k)]
+                                   for b in range(B)], dtype=np.int32),
+               margin=(lambda t: (t[..., 0] - t[..., 1]).numpy())(torch.topk(heat.reshape(B, k, -1), 2, -1).values),
+               heat_row_sum=h.astype(np.float64).sum(axis=3),
+               heat0=h[0].astype(np.float32),
+               running_checksum=running_checksum(sd_after),
+               bn1_running_mean=sd_after["resnet.%s_8s.bn1.running_mean" % backbone].numpy(),
+               bn1_running_var=sd_after["resnet.%s_8s.bn1.running_var" % backbone].numpy())
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "margin min %.3g" % out["margin"].min(), "argmax", out["argmax_yx"].reshape(-1, 2)[:4].tolist())
+
+
+def check_slice_first_head():
+    """heat_from_lowres(K channels) == the reference's full 1000-channel head, bitwise."""
+    imgs = recipe.seeded_images_u8(2, 120, 160, 3)
+    x = recipe.to_tensor_nchw(imgs)
+    m1, m2 = build("resnet34", 4, 9), build("resnet34", 4, 9)
+    with torch.no_grad():
+        full = m1(x)
+        low = lowres_of(m2, "resnet34", x)[:, :4].contiguous()
+        sliced = heat_from_lowres(low, x.size()[2:])
+    assert torch.equal(full, sliced), "slice-first head differs from the reference's"
+    print("slice-first head: bit-identical")
+
+
 def gauss_cases():
     cases = [(64, 48, 8, [10.0, 0.0, 63.0, 31.37], [5.0, 47.0, 0.0, 20.5]),
              (80, 60, 10, [40.25, 79.0], [30.75, 59.0]),
@@ -217,12 +274,28 @@ def train_case(name, backbone, k, B, H, W, wseed, iseed, kseed, steps=2):
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    gauss_cases()
-    bce_cases()
-    fwd_case("fwd_r18_k2_96x128", "resnet18", 2, 2, 96, 128, wseed=1, iseed=11)
-    fwd_case("fwd_r34_k4_96x128", "resnet34", 4, 2, 96, 128, wseed=2, iseed=12, eval_too=True)
-    fwd_case("fwd_r34_k4_75x100", "resnet34", 4, 2, 75, 100, wseed=3, iseed=13)
-    fwd_case("fwd_r50_k8_96x128", "resnet50", 8, 2, 96, 128, wseed=4, iseed=14)
-    fwd_case("fwd_r34_k4_480x640", "resnet34", 4, 1, 480, 640, wseed=5, iseed=15, full_heat=False)
-    train_case("train_r18_k2_64x80", "resnet18", 2, 2, 64, 80, wseed=6, iseed=16, kseed=26)
-    train_case("train_r34_k4_48x64", "resnet34", 4, 2, 48, 64, wseed=7, iseed=17, kseed=27)
+    only = sys.argv[1:]          # optional: names of the fixtures to (re)generate
+
+    def want(n):
+        return not only or n in only
+    if want("gauss"):
+        gauss_cases()
+    if want("bce"):
+        bce_cases()
+    for args in [("fwd_r18_k2_96x128", "resnet18", 2, 2, 96, 128, 1, 11, True, False),
+                 ("fwd_r34_k4_96x128", "resnet34", 4, 2, 96, 128, 2, 12, True, True),
+                 ("fwd_r34_k4_75x100", "resnet34", 4, 2, 75, 100, 3, 13, True, False),
+                 ("fwd_r50_k8_96x128", "resnet50", 8, 2, 96, 128, 4, 14, True, False),
+                 ("fwd_r34_k4_480x640", "resnet34", 4, 1, 480, 640, 5, 15, False, False)]:
+        if want(args[0]):
+            fwd_case(*args[:6], wseed=args[6], iseed=args[7], full_heat=args[8], eval_too=args[9])
+    if want("fwd_r34_k4_480x640_b32"):
+        check_slice_first_head()
+        # BASELINE config C2 at the bench's batch
+        fwd_batch_case("fwd_r34_k4_480x640_b32", "resnet34", 4, 32, 480, 640, wseed=10, iseed=20)
+    for args in [("train_r18_k2_64x80", "resnet18", 2, 2, 64, 80, 6, 16, 26),
+                 ("train_r34_k4_48x64", "resnet34", 4, 2, 48, 64, 7, 17, 27),
+                 # R50 K8 (the C4 / C5 network) train steps
+                 ("train_r50_k8_96x128", "resnet50", 8, 2, 96, 128, 8, 18, 28)]:
+        if want(args[0]):
+            train_case(*args[:6], wseed=args[6], iseed=args[7], kseed=args[8])

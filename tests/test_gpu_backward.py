@@ -212,8 +212,22 @@ def _model(bb, k, wseed, dev):
     return m.to(dev)
 
 
+# Tolerances per fixture (see the comment in the test): step-0 grad |.| sums
+# (rtol), step-1 grad sums, fc rows and stem gradient (atol relative to the
+# reference's max), step-1 loss (relative), post-step |param| sums, running stats.
+# R50@96x128: CPU fp32 vs fp64 on the same inputs differs by 6.3e-3 in the
+# |grad| sums, 1.0e-5 in the fc rows, 2.1e-2 in the stem gradient, and after
+# one Adam step its step-1 loss differs by 5.7e-4 relative (0.690897 vs 0.690503);
+# after two steps the |param| sums by 9.1e-5 (GPU: loss 9.4e-4, params 1.7e-4).
+TRAIN_TOL = {
+    "train_r18_k2_64x80": dict(g0=1e-4, fc=1e-5, stem=1e-4, loss1=1e-6, param=1e-5, run=1e-4),
+    "train_r34_k4_48x64": dict(g0=5e-2, fc=5e-3, stem=5e-2, loss1=2e-4, param=1e-4, run=1e-3),
+    "train_r50_k8_96x128": dict(g0=2e-2, fc=1e-4, stem=5e-2, loss1=2e-3, param=5e-4, run=1e-3),
+}
+
+
 @pytest.mark.parametrize("optimizer", ["torch", "fused"])
-@pytest.mark.parametrize("case", ["train_r18_k2_64x80", "train_r34_k4_48x64"])
+@pytest.mark.parametrize("case", sorted(TRAIN_TOL))
 def test_train_step_matches_reference_golden(cuda_device, golden, case, optimizer):
     """Reference idiom (train.py:33-36) end to end on the GPU path: heatmaps →
     .double() → nn.BCELoss → backward → Adam(lr 1e-4, wd 1e-4), two iterations
@@ -238,36 +252,37 @@ def test_train_step_matches_reference_golden(cuda_device, golden, case, optimize
     # sign differs move by 2*lr, so step-1 trajectories diverge further: measured
     # (tools/diag_grads.py two_step_report) GPU/CPU step-1 grad errors 3e-2 (R18)
     # and 4e-1 (R34) per element, loss 7e-9 (R18) and 4e-5 (R34).
-    tight = bb == "resnet18"
+    tol = TRAIN_TOL[case]
     for s in range(int(g["steps"])):
-        rtol_g = (1e-4 if s == 0 else 5e-3) if tight else (5e-2 if s == 0 else 1e-1)
         opt.zero_grad()
         pred = m.forward(x).double()
         loss = torch.nn.BCELoss()(pred, gt)
         loss.backward()
-        ltol = 1e-6 if (tight or s == 0) else 2e-4
+        ltol = 1e-6 if s == 0 else tol["loss1"]
+        print("%s step %d loss %.12f ref %.12f" % (case, s, loss.item(), float(g["loss%d" % s])))
         assert abs(loss.item() - float(g["loss%d" % s])) < ltol * float(g["loss%d" % s])
         if s > 0:
             opt.step()
             continue
         # gradients in the reference layout (OIHW) for comparison
         ga = np.array([float(params[n].grad.double().abs().sum()) for n in names])
-        np.testing.assert_allclose(ga, g["grad_abs%d" % s], rtol=rtol_g, atol=1e-9)
+        print("  grad |.| sums: max rel err %.3g" % (np.abs(ga - g["grad_abs0"]) / g["grad_abs0"]).max())
+        np.testing.assert_allclose(ga, g["grad_abs%d" % s], rtol=tol["g0"], atol=1e-9)
         fcw = params["resnet.%s_8s.fc.weight" % bb].grad
         fref = g["fc_grad_rows%d" % s]
         np.testing.assert_allclose(fcw[:k].reshape(k, -1).cpu().numpy(), fref, rtol=0,
-                                   atol=(1e-5 if tight else 5e-3) * np.abs(fref).max())
+                                   atol=tol["fc"] * np.abs(fref).max())
         assert fcw[k:].abs().sum().item() == 0.0
         st = params["resnet.%s_8s.conv1.weight" % bb].grad.cpu().numpy()
         sref = g["stem_grad%d" % s]
-        np.testing.assert_allclose(st, sref, rtol=0, atol=(1e-4 if tight else 5e-2) * np.abs(sref).max())
+        np.testing.assert_allclose(st, sref, rtol=0, atol=tol["stem"] * np.abs(sref).max())
         opt.step()
     sd = m.state_dict()
     pa = np.array([float(sd[n].double().abs().sum()) for n in names])
-    np.testing.assert_allclose(pa, g["param_abs"], rtol=1e-5 if tight else 1e-4)
+    np.testing.assert_allclose(pa, g["param_abs"], rtol=tol["param"])
     rc = [sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith(sfx))
           for sfx in ("running_mean", "running_var")]
-    np.testing.assert_allclose(rc, g["running_checksum"][:2], rtol=1e-4 if tight else 1e-3)
+    np.testing.assert_allclose(rc, g["running_checksum"][:2], rtol=tol["run"])
 
 
 def test_fused_adam_matches_torch_adam(cuda_device):

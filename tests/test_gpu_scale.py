@@ -1,0 +1,318 @@
+"""Parity at the bench's own configurations (BASELINE.json configs C2 and C5).
+
+* C2 (R34-8s, K=4, 640x480, batch 32 inference, train-mode BN over the batch):
+  the exact path bench.py times — default f16x3 arithmetic, default tile
+  planner at M = 32*60*80 rows — against a fixture produced by running the
+  reference itself at that batch (tests/golden/make_golden.py
+  fwd_r34_k4_480x640_b32): low-res logits, per-pixel heatmap of image 0,
+  heatmap row sums, argmax (bit-exact) and BN running statistics.
+* C5 (R50-8s, K=8, 1280x960, batch 32 training step, 245 GB): no fixture can
+  hold it, so every conv forward, conv backward (dgrad + wgrad) and BN backward
+  call of one full step is checked on sampled output elements against an fp64
+  recomputation from that call's own inputs (on the GPU, in torch fp64).  This
+  is the high-memory path (side-stream wgrad overlap off above 3/4 of HBM).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import recipe
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(bb, k, wseed, dev):
+    from src.model import KeypointsGauss
+    m = KeypointsGauss(k, backbone=bb, pretrained=False)
+    m.load_state_dict(recipe.seeded_state_dict(bb, wseed))
+    return m.to(dev)
+
+
+@pytest.mark.parametrize("inp", ["f32", "u8"])
+def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
+    """bench.py's default workload (and its --input u8 variant) vs the reference."""
+    from hkp import net, ops
+    g = golden("fwd_r34_k4_480x640_b32")
+    B, H, W, K = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["k"])
+    imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))
+    assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
+    m = _model("resnet34", K, int(g["wseed"]), cuda_device)
+    x = recipe.to_tensor_nchw(imgs).to(cuda_device) if inp == "f32" else torch.from_numpy(imgs).to(cuda_device)
+    syms = {}
+
+    def observe(sym, flops, nbytes, launch):
+        syms[sym] = syms.get(sym, 0.0) + flops
+        launch()
+    assert net.conv_precision() == "f16x3"           # the bench default
+    ops.set_observer(observe)
+    try:
+        with torch.no_grad():
+            hm, yx, low = net.keypoints_forward(m.resnet.net, x, K, heat=True, argmax=True)
+    finally:
+        ops.set_observer(None)
+    # every backbone conv ran on the packed f16x3 (LDS-DMA MFMA) kernels
+    assert syms and all(s.startswith("conv_x3_kernel") for s in syms), syms
+    print("conv kernels:", {s: "%.1f GFLOP" % (f / 1e9) for s, f in sorted(syms.items(), key=lambda kv: -kv[1])})
+    low_err = (low.cpu().numpy() - g["lowres"]).__abs__().max()
+    heat_err = (hm[0].cpu().numpy() - g["heat0"]).__abs__().max()
+    print("C2 B=32: lowres max err %.3g, heat[0] max err %.3g, min argmax margin %.3g"
+          % (low_err, heat_err, g["margin"].min()))
+    assert low_err < 1e-4
+    assert heat_err < 1e-3                                  # north_star: 1e-3 abs per pixel
+    np.testing.assert_allclose(hm.double().sum(3).cpu().numpy(), g["heat_row_sum"], rtol=1e-4)
+    assert np.array_equal(yx.cpu().numpy(), g["argmax_yx"])   # bit-exact, all 128 keypoints
+    sd = m.state_dict()
+    np.testing.assert_allclose(sd["resnet.resnet34_8s.bn1.running_var"].cpu().numpy(), g["bn1_running_var"],
+                               rtol=1e-4)
+    rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
+    assert abs(rm - g["running_checksum"][0]) < 1e-4 * max(1.0, abs(rm))
+
+
+# ---------------------------------------------------------------- C5 sampled
+
+
+class _Act:
+    """fp64 reader of an NHWC activation: fp32, or a packed f16x3 split ([.., 2C],
+    per 32 channels hi32|lo32, value = (hi + lo) / scale), or an NCHW image."""
+
+    def __init__(self, t, layout="nhwc", scale=1.0):
+        self.t, self.layout, self.scale = t, layout, scale
+        if layout == "nchw":
+            self.N, self.C, self.H, self.W = t.shape
+        else:
+            self.N, self.H, self.W = t.shape[:3]
+            self.C = t.shape[3] // 2 if t.dtype == torch.float16 else t.shape[3]
+
+    def pix(self, n, h, w):
+        """[ns, C] values at pixels (n, h, w) (index tensors)."""
+        if self.layout == "nchw":
+            return self.t[n, :, h, w].double()
+        v = self.t[n, h, w]
+        if self.t.dtype == torch.float16:
+            g = v.reshape(v.shape[0], self.C // 32, 2, 32).double()
+            return (g[:, :, 0] + g[:, :, 1]).reshape(v.shape[0], self.C) / self.scale
+        return v.double()
+
+    def chan(self, c):
+        """[N, H, W] plane of channel c."""
+        if self.layout == "nchw":
+            return self.t[:, c].double()
+        if self.t.dtype == torch.float16:
+            j = (c // 32) * 64 + c % 32
+            return (self.t[..., j].double() + self.t[..., j + 32].double()) / self.scale
+        return self.t[..., c].double()
+
+
+def _dy_scale(dy):
+    """The power of two a split-only dy was packed with (bound in dy._hkp_amax)."""
+    if dy.dtype != torch.float16:
+        return 1.0
+    bound = dy._hkp_amax.view(torch.float32).item()
+    _, e = np.frexp(bound)
+    return 2.0 ** (14 - int(e))
+
+
+def _idx(gen, hi, ns, dev):
+    return torch.randint(0, hi, (ns,), generator=gen).to(dev)
+
+
+def _check(name, got, ref, tol, stats):
+    err = (got - ref).abs()
+    ratio = (err / tol).max().item()
+    stats[name] = max(stats.get(name, 0.0), ratio)
+    assert ratio <= 1.0, "%s: error %.3g exceeds its bound (ratio %.3g)" % (name, err.max().item(), ratio)
+
+
+REL = 1e-5          # per element, relative to the sum of |products| (fp32 / f16x3 dot products)
+ABS_W = 2.0 ** -24  # plus the f16x3 activation floor (2^-25 below 2^-3), per |weight| of a valid tap
+
+
+def check_conv_fwd(x, w_krsc, y, st, pd, dl, gen, stats, ns=256):
+    N, H, W, C = x.N, x.H, x.W, x.C
+    K, R, S, _ = w_krsc.shape
+    _, Ho, Wo, _ = y.shape
+    dev = y.device
+    n, ho, wo, k = (_idx(gen, v, ns, dev) for v in (N, Ho, Wo, K))
+    w64 = w_krsc.detach().double()
+    acc = torch.zeros(ns, device=dev, dtype=torch.float64)
+    mag = torch.zeros_like(acc)
+    wmag = torch.zeros_like(acc)
+    for r in range(R):
+        for s in range(S):
+            hi, wi = ho * st - pd + r * dl, wo * st - pd + s * dl
+            ok = ((hi >= 0) & (hi < H) & (wi >= 0) & (wi < W)).double()[:, None]
+            xv = x.pix(n, hi.clamp(0, H - 1), wi.clamp(0, W - 1)) * ok
+            wv = w64[k, r, s, :]
+            acc += (xv * wv).sum(1)
+            mag += (xv * wv).abs().sum(1)
+            wmag += (wv.abs() * ok).sum(1)
+    _check("fwd", y[n, ho, wo, k].double(), acc, REL * mag + ABS_W * wmag + 1e-30, stats)
+
+
+def check_conv_dgrad(dy, w_krsc, dx, add, st, pd, dl, gen, stats, ns=256):
+    N, H, W, C = dx.shape
+    K, R, S, _ = w_krsc.shape
+    Ho, Wo = dy.H, dy.W
+    dev = dx.device
+    n, h, w, c = (_idx(gen, v, ns, dev) for v in (N, H, W, C))
+    w64 = w_krsc.detach().double()
+    acc = torch.zeros(ns, device=dev, dtype=torch.float64)
+    mag = torch.zeros_like(acc)
+    for r in range(R):
+        for s in range(S):
+            th, tw = h + pd - r * dl, w + pd - s * dl
+            ok = (th >= 0) & (tw >= 0) & (th % st == 0) & (tw % st == 0) & (th // st < Ho) & (tw // st < Wo)
+            dv = dy.pix(n, (th // st).clamp(0, Ho - 1), (tw // st).clamp(0, Wo - 1)) * ok.double()[:, None]
+            wv = w64[:, r, s, :][:, c].t()                      # [ns, K]
+            acc += (dv * wv).sum(1)
+            mag += (dv * wv).abs().sum(1)
+    if add is not None:
+        a = add[n, h, w, c].double()
+        acc += a
+        mag += a.abs()
+    _check("dgrad", dx[n, h, w, c].double(), acc, REL * mag + 1e-30, stats)
+
+
+def check_conv_wgrad(x, dy, dw_krsc, st, pd, dl, gen, stats, ns=48):
+    K, R, S, C = dw_krsc.shape
+    Ho, Wo = dy.H, dy.W
+    dev = dw_krsc.device
+    ks, rs, ss, cs = (torch.randint(0, v, (ns,), generator=gen).tolist() for v in (K, R, S, C))
+    ref, tol = [], []
+    xcache = {}
+    for k, r, s, c in zip(ks, rs, ss, cs):
+        if c not in xcache:                      # one padded plane at a time
+            xcache = {c: F.pad(x.chan(c), (pd, pd, pd, pd))}
+        xp = xcache[c][:, r * dl: r * dl + st * (Ho - 1) + 1: st, s * dl: s * dl + st * (Wo - 1) + 1: st]
+        p = dy.chan(k) * xp
+        ref.append(p.sum())
+        tol.append(REL * p.abs().sum() + ABS_W * dy.chan(k).abs().sum())
+    got = dw_krsc[torch.tensor(ks), torch.tensor(rs), torch.tensor(ss), torch.tensor(cs)].double()
+    _check("wgrad", got, torch.stack(ref), torch.stack(tol) + 1e-30, stats)
+
+
+def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, chunk=1 << 16):
+    """Train-mode BN(+ReLU) backward: dgamma / dbeta against full fp64 channel
+    reductions (row chunks) and dy on sampled elements; also the forward batch
+    statistics (mean, invstd) the forward stored."""
+    c = y.shape[-1]
+    y2, g2 = y.reshape(-1, c), g.reshape(-1, c)
+    M = y2.shape[0]
+    s1 = torch.zeros(c, device=y.device, dtype=torch.float64)
+    for r0 in range(0, M, chunk):
+        s1 += y2[r0:r0 + chunk].double().sum(0)
+    mean = s1 / M
+    var = torch.zeros_like(s1)
+    for r0 in range(0, M, chunk):
+        var += ((y2[r0:r0 + chunk].double() - mean) ** 2).sum(0)
+    inv = 1.0 / torch.sqrt(var / M + bn.eps)
+    _check("bn_mean", mi[:c].double(), mean, 1e-5 * torch.sqrt(var / M) + 1e-30, stats)
+    _check("bn_invstd", mi[c:].double(), inv, 1e-5 * inv, stats)
+    mean_k, inv_k = mi[:c].double(), mi[c:].double()            # what the kernels used
+    db = torch.zeros_like(s1)
+    dgm = torch.zeros_like(s1)
+    adb = torch.zeros_like(s1)
+    adgm = torch.zeros_like(s1)
+    for r0 in range(0, M, chunk):
+        rows = slice(r0, r0 + chunk)
+        dz = g2[rows].double() * mask_fn(rows)
+        xh = (y2[rows].double() - mean_k) * inv_k
+        db += dz.sum(0)
+        dgm += (dz * xh).sum(0)
+        adb += dz.abs().sum(0)
+        adgm += (dz * xh).abs().sum(0)
+    _check("bn_dbeta", dbeta.double(), db, 1e-5 * adb + 1e-30, stats)
+    _check("bn_dgamma", dgamma.double(), dgm, 1e-5 * adgm + 1e-30, stats)
+    rows = _idx(gen, M, ns, y.device)
+    ch = _idx(gen, c, ns, y.device)
+    mk = torch.stack([mask_fn(slice(int(r), int(r) + 1))[0, int(cc)] for r, cc in zip(rows.tolist(), ch.tolist())]) \
+        if mask_fn is not None else 1.0
+    dz = g2[rows, ch].double() * mk
+    xh = (y2[rows, ch].double() - mean_k[ch]) * inv_k[ch]
+    coef = bn.weight.detach().double()[ch] * inv_k[ch]
+    ref = coef * (dz - db[ch] / M - xh * dgm[ch] / M)
+    tol = 1e-5 * coef.abs() * (dz.abs() + adb[ch] / M + xh.abs() * adgm[ch] / M) + 1e-30
+    n_, h_, w_ = y.shape[:3]
+    rr = rows
+    dyr = _Act(dy, scale=_dy_scale(dy))
+    got = dyr.pix(rr // (h_ * w_), (rr // w_) % h_, rr % w_)[torch.arange(ns, device=y.device), ch]
+    _check("bn_dy", got, ref, tol, stats)
+
+
+def test_c5_train_step_sampled_fp64(cuda_device):
+    """One C5 training step (R50-8s K=8 1280x960 B=32, bench.py --mode train at
+    the C5 shape): every conv forward / dgrad / wgrad and BN backward call checked
+    on sampled elements against fp64 recomputations from its own inputs."""
+    from hkp import net, ops, train
+    B, K, H, W = 32, 8, 960, 1280
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 61)).to(cuda_device)
+    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 62)).to(cuda_device)
+    m = _model("resnet50", K, 63, cuda_device)
+    gen = torch.Generator().manual_seed(64)
+    stats, counts = {}, {"fwd": 0, "bwd": 0, "bn": 0, "stem_wgrad": 0}
+    oc_f, oc_b, ob, o_wst = net._conv_fwd, net._conv_backward, net._bn_backward, ops.conv2d_bwd_filter
+
+    def fwd_spy(conv, bn, xx, layout="nhwc", part_out=None, sk=True):
+        y, part = oc_f(conv, bn, xx, layout, part_out, sk)
+        torch.cuda.synchronize()
+        w = conv.weight if layout == "nhwc" else conv.weight.permute(0, 2, 3, 1)
+        check_conv_fwd(_Act(xx, layout), w, y, net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation),
+                       gen, stats)
+        counts["fwd"] += 1
+        return y, part
+
+    def bwd_spy(conv, xx, dy, grads, need_dx=True, add=None):
+        dx = oc_b(conv, xx, dy, grads, need_dx, add)
+        torch.cuda.synchronize()
+        st, pd, dl = net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation)
+        dya = _Act(dy, scale=_dy_scale(dy))
+        if dx is not None:
+            check_conv_dgrad(dya, conv.weight, dx, add, st, pd, dl, gen, stats)
+        check_conv_wgrad(_Act(xx), dya, grads[conv.weight], st, pd, dl, gen, stats)
+        counts["bwd"] += 1
+        return dx
+
+    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False, split_only=False, relu_ss=None):
+        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz, split_only, relu_ss=relu_ss)
+        torch.cuda.synchronize()
+        c = y.shape[-1]
+        y2 = y.reshape(-1, c)
+        if relu_ss is not None:         # the kernel's recomputed mask: round(round(y*a) + b) > 0
+            def mask_fn(rows):
+                return (((y2[rows] * relu_ss[:c]) + relu_ss[c:]) > 0).double()
+        elif mask is not None:
+            m2 = mask.reshape(-1, c)
+
+            def mask_fn(rows):
+                return (m2[rows] > 0).double()
+        else:
+            def mask_fn(rows):
+                return torch.ones_like(y2[rows], dtype=torch.float64)
+        check_bn_bwd(bn, gr, mask_fn, y, mi, dy, grads[bn.weight], grads[bn.bias], gen, stats)
+        counts["bn"] += 1
+        return dy, dz
+
+    def stem_wgrad_spy(xx, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out=None, accumulate=False):
+        dw = o_wst(xx, dy, w_shape, stride, pad, dil, layout, out, accumulate)
+        torch.cuda.synchronize()
+        if layout == "nchw":
+            check_conv_wgrad(_Act(xx, "nchw"), _Act(dy), dw.permute(0, 2, 3, 1), stride, pad, dil, gen, stats)
+            counts["stem_wgrad"] += 1
+        return dw
+
+    net._conv_fwd, net._conv_backward, net._bn_backward, ops.conv2d_bwd_filter = \
+        fwd_spy, bwd_spy, bn_spy, stem_wgrad_spy
+    try:
+        loss = train.Trainer(m).forward_backward(x, uv=uv)
+    finally:
+        net._conv_fwd, net._conv_backward, net._bn_backward, ops.conv2d_bwd_filter = oc_f, oc_b, ob, o_wst
+    n_conv = len([mm for mm in m.modules() if mm.__class__.__name__ == "KRSCConv2d"])
+    print("C5 step: loss %.9f, calls %s, worst error / bound: %s" % (
+        loss.item(), counts, {k: round(v, 4) for k, v in stats.items()}))
+    assert counts == {"fwd": n_conv + 1, "bwd": n_conv, "bn": n_conv + 1, "stem_wgrad": 1}
+    assert torch.isfinite(loss).item()
+    assert torch.cuda.max_memory_allocated(cuda_device) > 0.5 * torch.cuda.get_device_properties(
+        cuda_device).total_memory          # really the high-memory configuration

@@ -87,7 +87,7 @@ def test_bce_matches_reference(golden):
     assert np.array_equal(p2.grad.numpy(), g["mse_grad"])
 
 
-@pytest.mark.parametrize("case", ["train_r18_k2_64x80", "train_r34_k4_48x64"])
+@pytest.mark.parametrize("case", ["train_r18_k2_64x80", "train_r34_k4_48x64", "train_r50_k8_96x128"])
 def test_train_step_matches_reference(golden, case):
     g = golden(case)
     bb, k = str(g["backbone"]), int(g["k"])
@@ -105,3 +105,24 @@ def test_train_step_matches_reference(golden, case):
         np.testing.assert_allclose(grads["resnet.%s_8s.conv1.weight" % bb].numpy(), g["stem_grad%d" % s],
                                    rtol=1e-4, atol=1e-8)
         break  # Adam state is per-call in train_step; step-0 grads pin the math
+
+
+def test_forward_bench_batch_matches_reference(golden):
+    """BASELINE config C2 at the bench's own batch (R34 K4 640x480, B=32, train-mode
+    BN over the batch): the oracle reproduces the reference's logits, heatmap,
+    argmax and running statistics.  The fixture stores the images' digest only."""
+    import hashlib
+    g = golden("fwd_r34_k4_480x640_b32")
+    B, H, W = int(g["batch"]), int(g["height"]), int(g["width"])
+    imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))
+    assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
+    sd = recipe.seeded_state_dict("resnet34", int(g["wseed"]))
+    with torch.no_grad():
+        heat, low = cpu_ref.forward(sd, recipe.to_tensor_nchw(imgs), "resnet34", 4, head="k_only",
+                                    return_lowres=True)
+    np.testing.assert_allclose(low.numpy(), g["lowres"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(heat[0].numpy(), g["heat0"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(heat.double().sum(3).numpy(), g["heat_row_sum"], rtol=1e-6)
+    assert (cpu_ref.argmax_yx(heat) == g["argmax_yx"]).all()
+    rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
+    assert abs(rm - g["running_checksum"][0]) < 1e-6 * max(1, abs(rm))
