@@ -1,20 +1,32 @@
 #!/usr/bin/env python3
 """Benchmark of the keypoint-heatmap hot path on MI355X (BASELINE.json metric:
-images/sec, 640x480, N keypoints).
+images/sec, 640x480, N keypoints, inference+train).
 
 Default workload = BASELINE config C2: ResNet-34-8s, K=4, 640x480, batch 32
 inference per GPU (train-mode BN exactly like the reference's analysis.py /
-Prediction.predict, fused K-channel head, heatmap + argmax decode).
-``--mode train`` times one training iteration (forward, fp64 BCE, backward,
-Adam) instead (config C3 per-GPU shard: --batch 8).
+Prediction.predict, fused K-channel head, heatmap + argmax decode) — the
+line's `value`.  The same run also times, as extra keys of the one JSON line:
+  * "train": one training iteration per step (forward, fused fp64 BCE,
+    backward, RCCL all-reduce of gradients at N>1, FusedAdam) on config C3's
+    per-GPU shard (batch 8 of the 64-image global batch at N=8);
+  * "fp32_exact": C2 with exact-fp32 MFMA convs (--precision fp32) beside the
+    default f16x3 split arithmetic;
+  * "cpu_baseline": the oracle (reference-faithful CPU restatement) on this
+    host's cores: C2 inference at batch 1 and 4 and the C1 training step.
+``--mode train`` makes the training step the main line instead.
 
-One process per GPU (torchrun for N>1); each rank owns its own batch
-(weak scaling: the inference path needs no collective; training all-reduces
-gradients over RCCL).  Prints ONE JSON line on rank 0.
+One process per GPU.  ``--gpus N`` without a torchrun environment relaunches
+itself under ``torch.distributed.run`` as a child process (before any GPU
+call); under torchrun N must equal WORLD_SIZE.  Inference shards by image
+(weak scaling): each rank runs its own batch and the int32 keypoints are
+all-gathered each step (hkp.parallel); training all-reduces gradients over RCCL.
+Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,7 +35,6 @@ for p in (REPO, os.path.join(REPO, "hulk-keypoints_amd")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
@@ -47,9 +58,29 @@ def parse():
     ap.add_argument("--input", choices=["f32", "u8"], default="f32",
                     help="f32: the reference's ToTensor NCHW tensor; u8: the cv2.imread-style uint8 HWC batch "
                          "(ToTensor fused into the stem, SURVEY 8(f1))")
+    ap.add_argument("--no-extras", action="store_true", help="main line only (no train / fp32 legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
     return ap.parse_args()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def relaunch_distributed(n):
+    """bench.py --gpus N outside torchrun: run N ranks under torch.distributed.run
+    as a child process (this process has not touched the GPU) and return its exit
+    code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def conv_flops_per_image(backbone, k, H, W):
@@ -59,7 +90,7 @@ def conv_flops_per_image(backbone, k, H, W):
     fl = 2.0 * h * w * 64 * 3 * 49
     h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     for b in layer_plan(backbone):
-        s, d, cin, pl = b["stride"], b["dilation"], b["inplanes"], b["planes"]
+        s, cin, pl = b["stride"], b["inplanes"], b["planes"]
         ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
         if b["kind"] == "basic":
             fl += 2.0 * ho * wo * pl * cin * 9 + 2.0 * ho * wo * pl * pl * 9
@@ -75,7 +106,8 @@ def conv_flops_per_image(backbone, k, H, W):
 
 class LaunchTimer:
     """HIP-event timing of each conv launch, on the stream it is launched on
-    (torch's current stream — the one libhulkkp launches on)."""
+    (torch's current stream — the one libhulkkp launches on; the side stream
+    for an overlapped wgrad)."""
 
     def __init__(self):
         self.rec = []
@@ -104,80 +136,142 @@ class LaunchTimer:
         return agg
 
 
+def _nospace(s):
+    return s.replace(" ", "")
+
+
 def pmc_traffic(kernel_sym, tag):
-    """HBM bytes per launch of `kernel_sym` from the committed rocprofv3 PMC summary
-    (profiles/*<tag>*pmc*.json, separate FETCH_SIZE / WRITE_SIZE passes):
+    """HBM bytes per launch of `kernel_sym` from the newest committed rocprofv3 PMC
+    summary (profiles/*<tag>*pmc*.json, separate FETCH_SIZE / WRITE_SIZE passes):
     (FETCH_SIZE * 2 + WRITE_SIZE) * 1024 — gfx950's FETCH_SIZE counts half of a
-    wide streaming read (MI355X_MICROARCH.md §HBM).  None if no summary matches."""
+    wide streaming read (MI355X_MICROARCH.md §HBM).  The kernel name must match
+    exactly (spaces ignored).  (None, None) if no summary has it."""
     import glob
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*%s*pmc*.json" % tag)), reverse=True):
+    want = "::" + _nospace(kernel_sym) + "("
+    paths = glob.glob(os.path.join(REPO, "profiles", "*%s*pmc*.json" % tag))
+    for path in sorted(paths, reverse=True):       # rNN_..._vNN names: newest round / version first
         try:
             data = json.load(open(path))
         except (OSError, ValueError):
             continue
         for name, c in data.items():
-            if kernel_sym.split("<")[0] in name and kernel_sym.split("<")[1].rstrip(">") in name.replace(" ", ""):
-                if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-                    return (c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024, os.path.basename(path)
+            if want in _nospace(name) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+                return (c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024, os.path.basename(path)
     return None, None
 
 
+def host_cores():
+    """CPUs this process may use: os.cpu_count(), narrowed by the affinity mask and
+    the cgroup CPU quota (a GPU box shows the whole machine's CPUs in
+    os.cpu_count() but grants one GPU's share)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, budget_s):
-    """Oracle (reference-faithful CPU restatement: 1000-ch head, train-mode BN)
-    timed on this host's cores on a bounded sample of the same workload."""
+    """Oracle (reference-faithful CPU restatement: 1000-ch head, train-mode BN,
+    fp64 BCE, Adam) timed on this host's cores on a bounded sample: C2-shape
+    inference at batch 1 and 4, and the C1 training step (R18-8s K=2 320x240
+    batch 4, train.py:32-36).  One warm-up each, then the median of up to 3."""
+    import statistics
+
     from oracle import cpu_ref, recipe
-    # the host share of one GPU on the box (OMP_NUM_THREADS is set to it there)
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "16")))
-    cores = torch.get_num_threads()
+    cores = host_cores()
+    torch.set_num_threads(cores)
     sd = recipe.seeded_state_dict(args.backbone, 0)
-    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(1, args.height, args.width, 1234))
+
+    def timed(fn, reps):                   # each of the three legs gets a third of the budget
+        t_start = time.time()
+        fn()
+        ts = []
+        for _ in range(reps):
+            if ts and time.time() - t_start > budget_s / 3:
+                break
+            t0 = time.time()
+            fn()
+            ts.append(time.time() - t0)
+        return statistics.median(ts), len(ts)
+
+    legs = {}
     with torch.no_grad():
-        cpu_ref.forward(sd, x, args.backbone, args.keypoints)   # warm-up
-        n, t0 = 0, time.time()
-        while n < 1 or (n < 30 and time.time() - t0 < budget_s):
-            h = cpu_ref.forward(sd, x, args.backbone, args.keypoints)
-            cpu_ref.argmax_yx(h)
-            n += 1
-        dt = time.time() - t0
-    return {"value": n / dt, "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": "%d x batch-1 %dx%d %s-8s K=%d inference (faithful 1000-ch head, train-mode BN, argmax), "
-                      "oracle/cpu_ref.py on torch CPU, %d threads" % (n, args.width, args.height, args.backbone,
-                                                                      args.keypoints, cores)}
+        for b in (1, 4):
+            x = recipe.to_tensor_nchw(recipe.seeded_images_u8(b, args.height, args.width, 1234))
+
+            def infer():
+                cpu_ref.argmax_yx(cpu_ref.forward({k: v.clone() for k, v in sd.items()}, x, args.backbone,
+                                                  args.keypoints))
+            t, n = timed(infer, 3)
+            legs["infer_b%d" % b] = {"images_per_sec": b / t, "ms_per_batch": t * 1e3, "samples": n}
+    c1 = dict(backbone="resnet18", k=2, H=240, W=320, B=4)
+    sd1 = recipe.seeded_state_dict(c1["backbone"], 0)
+    x1 = recipe.to_tensor_nchw(recipe.seeded_images_u8(c1["B"], c1["H"], c1["W"], 4321))
+    uv1 = recipe.seeded_keypoints(c1["B"], c1["k"], c1["H"], c1["W"], 99)
+    trainer = cpu_ref.OracleTrainer(sd1, c1["backbone"], c1["k"])
+    t, n = timed(lambda: trainer.step(x1, uv1), 3)
+    legs["train_c1"] = {"images_per_sec": c1["B"] / t, "ms_per_step": t * 1e3, "samples": n,
+                        "workload": "C1: R18-8s K=2 320x240 batch 4 train step (BCE fp64 + Adam)"}
+    return {"value": legs["infer_b4"]["images_per_sec"], "unit": "images/sec", "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(),
+            "sample": "oracle/cpu_ref.py on torch CPU, %d threads; value = %dx%d %s-8s K=%d inference at batch 4 "
+                      "(faithful 1000-ch head, train-mode BN, argmax); also batch 1 and the C1 train step"
+                      % (cores, args.width, args.height, args.backbone, args.keypoints),
+            "legs": legs}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.batch is None:
-        args.batch = 32 if args.mode == "infer" else 8
-    dist = world > 1
-    if dist:
-        torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-
+def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
+    """Time `steps` steps of one workload; return its metrics (rank 0 gets them)."""
     import hkp
-    from hkp import ops
-    from src.model import KeypointsGauss
+    from hkp import net as hkp_net
+    from hkp import ops, parallel
     from oracle import recipe  # synthetic inputs (seeded images / keypoints only)
+    from src.model import KeypointsGauss
 
     hkp.lib()
-    from hkp import net as hkp_net
-    precision = args.precision or "f16x3"
+    dist = world > 1
     hkp_net.set_conv_precision(precision)
-    B, K, H, W = args.batch, args.keypoints, args.height, args.width
+    B, K, H, W = batch, args.keypoints, args.height, args.width
     torch.manual_seed(1234 + rank)
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False).to(dev)
     imgs = recipe.seeded_images_u8(B, H, W, 1234 + rank)
     x = recipe.to_tensor_nchw(imgs).to(dev) if args.input == "f32" else torch.from_numpy(imgs).to(dev)
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99 + rank)).to(dev)
 
-    if args.mode == "infer":
+    if mode == "infer":
+        gathered = torch.empty((world * B, K, 2), device=dev, dtype=torch.int32) if dist else None
+
         def step():
             with torch.no_grad():
-                return model.heatmaps_and_keypoints(x)
+                hm, yx = model.heatmaps_and_keypoints(x)
+                if dist:                                   # every rank ends with all keypoints
+                    parallel.gather_keypoints_fixed(yx, gathered)
+                return hm
     else:
         from hkp import train as hkp_train
         trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4, distributed=dist)
@@ -187,14 +281,14 @@ def main():
 
     timer = LaunchTimer()
     ops.set_observer(timer)
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if dist:
@@ -207,60 +301,109 @@ def main():
         elapsed = t.item()
 
     # roofline pass: the same steps again with every conv launch event-timed
+    reps = max(3, min(steps, 10))
     timer.on = True
-    for _ in range(max(3, min(args.steps, 10))):
+    for _ in range(reps):
         step()
     agg = timer.summary()
     timer.on = False
     ops.set_observer(None)
+    peak_mem = torch.cuda.max_memory_allocated(dev) / 1e9
+    del model, x, uv
+    if mode != "infer":
+        del trainer
+    torch.cuda.empty_cache()
+    torch.cuda.reset_peak_memory_stats(dev)
+    hkp_net.set_conv_precision("f16x3")
 
-    images = B * args.steps * world
-    value = images / elapsed
+    value = B * steps * world / elapsed
     fl_img = conv_flops_per_image(args.backbone, K, H, W)
-    if rank != 0:
-        if dist:
-            torch.distributed.destroy_process_group()
-        return
     # dominant kernel = the conv symbol with the most event-timed time
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
     alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
     if dom_sym.startswith(("conv_split_kernel", "conv_x3_kernel", "wgrad_x3_kernel")):
-        passes = 3 if "_x3_" in dom_sym else int(dom_sym.split("<")[1].split(",")[2])
+        passes = 3 if "_x3_" in dom_sym and precision == "f16x3" else (
+            1 if "_x3_" in dom_sym else int(dom_sym.split("<")[1].split(",")[2]))
         achieved, peak = alg * passes, PEAK_FP16_MFMA_TFLOPS    # issued fp16 MFMA FLOPs vs dense fp16 peak
     else:
-        passes, achieved, peak = 0, alg, PEAK_FP32_MFMA_TFLOPS
+        passes, achieved, peak = 1, alg, PEAK_FP32_MFMA_TFLOPS
     all_ms = sum(v[3] for v in agg.values())
     all_fl = sum(v[1] for v in agg.values())
+    roof = {"bound": "mfma", "kernel": dom_sym, "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+            "frac": achieved / peak, "traffic": None,
+            "fp32_equivalent_tflops": alg, "mfma_passes_per_fp32_mac": passes,
+            "launches_per_step": cnt // reps, "avg_launch_ms": ms / cnt,
+            "algorithmic_gflop_per_launch": fl / cnt / 1e9,
+            "algorithmic_bytes_per_launch": nb / cnt,
+            "all_convs_tflops": all_fl / (all_ms * 1e-3) / 1e12,
+            "conv_share_of_step": (all_ms / reps) / (elapsed / steps * 1e3)}
+    if passes == 3:
+        # f16x3 issues 3 fp16 MFMAs per fp32 MAC: its own ceiling is a third of the fp16 peak
+        roof["frac_of_x3_ceiling"] = alg / (PEAK_FP16_MFMA_TFLOPS / 3)
+    tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
+    if (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3":
+        roof["traffic"], roof["traffic_source"] = pmc_traffic(dom_sym, tag)
+    return {"value": value, "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
+            "batch_per_gpu": B, "global_batch": B * world, "roofline": roof,
+            "model_tflops": value / world * fl_img * (3 if mode == "train" else 1) / 1e12,
+            "peak_hbm_gb": peak_mem}
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch_distributed(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d (launch with torchrun --nproc-per-node %d, or without "
+              "torchrun to let bench.py start the ranks)" % (args.gpus, world, args.gpus), file=sys.stderr)
+        sys.exit(2)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    precision = args.precision or "f16x3"
+    batch = args.batch or (32 if args.mode == "infer" else 8)
+
+    main_leg = run_leg(args.mode, precision, batch, args, dev, rank, world, args.steps, args.warmup)
+    extras = {}
+    default_c2 = (args.mode, args.backbone, args.keypoints, args.height, args.width) == \
+        ("infer", "resnet34", 4, 480, 640)
+    if not args.no_extras and default_c2:
+        extras["train"] = run_leg("train", precision, 8, args, dev, rank, world, args.steps, args.warmup)
+        extras["train"]["workload"] = "training step (C3 shard) resnet34-8s K=4 640x480 batch 8/GPU " \
+                                      "(BCE fp64, backward, RCCL grad all-reduce at N>1, FusedAdam lr1e-4 wd1e-4)"
+        if precision != "fp32":
+            extras["fp32_exact"] = run_leg("infer", "fp32", batch, args, dev, rank, world, max(3, args.steps // 4),
+                                           2)
+            extras["fp32_exact"]["workload"] = "C2 with exact-fp32 MFMA convs (v_mfma_f32_32x32x2_f32)"
+    if rank != 0:
+        if dist:
+            torch.distributed.destroy_process_group()
+        return
     dtype = {"fp32": "f32", "f16x3": "f32 (f16x3 split-precision MFMA, fp32-accurate)", "f16": "f16"}[precision]
+    B = batch
     out = {
         "metric": "images/sec (640x480, N keypoints) inference+train at 1/2/4/8 MI355X",
-        "value": value, "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "value": main_leg["value"], "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": main_leg["ms_per_step"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": dtype, "data": "synthetic (seeded uint8 BGR images; random-init weights)",
         "config": {"workload": "%s %s-8s K=%d %dx%d batch %d/GPU (%s)" % (
-            "inference (C2)" if args.mode == "infer" else "training step (C3 shard)", args.backbone, K, W, H, B,
-            "train-mode BN, fused K-ch head, heatmap + argmax" if args.mode == "infer"
-            else "BCE fp64, Adam lr1e-4 wd1e-4"),
-            "mode": args.mode, "backbone": args.backbone, "keypoints": K, "height": H, "width": W,
-            "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,
+            "inference (C2)" if args.mode == "infer" else "training step (C3 shard)", args.backbone,
+            args.keypoints, args.width, args.height, B,
+            "train-mode BN, fused K-ch head, heatmap + argmax, keypoints all-gathered at N>1"
+            if args.mode == "infer" else "BCE fp64, Adam lr1e-4 wd1e-4"),
+            "mode": args.mode, "backbone": args.backbone, "keypoints": args.keypoints, "height": args.height,
+            "width": args.width, "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,
             "input": "fp32 NCHW (ToTensor)" if args.input == "f32" else "uint8 HWC BGR (ToTensor fused into the stem)"},
-        "roofline": {"bound": "mfma", "kernel": dom_sym, "achieved": achieved, "peak": peak,
-                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                     "fp32_equivalent_tflops": alg, "frac_of_fp32_mfma_peak": alg / PEAK_FP32_MFMA_TFLOPS,
-                     "mfma_passes_per_fp32_mac": passes or 1,
-                     "launches_per_step": cnt // max(3, min(args.steps, 10)),
-                     "avg_launch_ms": ms / cnt, "algorithmic_gflop_per_launch": fl / cnt / 1e9,
-                     "all_convs_tflops": all_fl / (all_ms * 1e-3) / 1e12,
-                     "conv_share_of_step": (all_ms / max(3, min(args.steps, 10))) / (elapsed / args.steps * 1e3)},
-        "model_tflops": value / world * fl_img * (3 if args.mode == "train" else 1) / 1e12,
-        "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9,
+        "roofline": main_leg["roofline"],
+        "model_tflops": main_leg["model_tflops"],
+        "peak_hbm_gb": main_leg["peak_hbm_gb"],
     }
-    tag = "infer_c2" if args.mode == "infer" else "train_c3"
-    traffic, src = pmc_traffic(dom_sym.replace(" ", ""), tag) if (args.backbone, K, H, W) == ("resnet34", 4, 480,
-                                                                                             640) else (None, None)
-    out["roofline"]["traffic"] = traffic
-    out["roofline"]["traffic_source"] = src
-    out["roofline"]["algorithmic_bytes_per_launch"] = nb / cnt
+    out.update(extras)
     if not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     print(json.dumps(out))

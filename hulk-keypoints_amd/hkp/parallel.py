@@ -1,0 +1,76 @@
+"""Data-parallel inference over the GPUs of a node.
+
+Inference shards by image: every rank runs the fused forward + argmax on its
+own slice of the batch (no collective on the data path; train-mode BN
+statistics are per shard, exactly as a per-shard run of the reference's
+analysis.py would compute them), then the int32 [b, K, 2] (y, x)
+keypoints — 8 bytes per keypoint — are all-gathered so every rank (and in
+particular rank 0, which writes results) holds the global [B, K, 2] in rank
+order.  One process per GPU, torch.distributed "nccl" = RCCL over xGMI (gloo
+for the CPU tests).
+"""
+import torch
+import torch.distributed as dist
+
+
+def world():
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def rank():
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
+def shard_range(n, rank_, world_):
+    """Contiguous [lo, hi) slice of n items owned by rank_ (the first n % world_
+    ranks take one extra item)."""
+    base, extra = divmod(n, world_)
+    lo = rank_ * base + min(rank_, extra)
+    return lo, lo + base + (1 if rank_ < extra else 0)
+
+
+def gather_keypoints(yx, group=None):
+    """all_gather of each rank's int32 [b_r, K, 2] keypoints → [sum b_r, K, 2] in
+    rank order, on every rank.  Shards may differ in size (padded to the largest
+    for the collective, trimmed after)."""
+    if yx.dtype != torch.int32 or yx.dim() != 3 or yx.shape[2] != 2:
+        raise ValueError("gather_keypoints: expected int32 [b, K, 2], got %s %s" % (yx.dtype, tuple(yx.shape)))
+    n = dist.get_world_size(group) if dist.is_initialized() else 1
+    if n == 1:
+        return yx
+    yx = yx.contiguous()
+    sizes = torch.tensor([yx.shape[0]], device=yx.device, dtype=torch.int64)
+    all_sizes = [torch.empty_like(sizes) for _ in range(n)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    counts = [int(s.item()) for s in all_sizes]
+    bmax = max(counts)
+    if yx.shape[0] < bmax:
+        pad = torch.zeros((bmax - yx.shape[0],) + tuple(yx.shape[1:]), device=yx.device, dtype=yx.dtype)
+        yx = torch.cat([yx, pad])
+    parts = [torch.empty_like(yx) for _ in range(n)]
+    dist.all_gather(parts, yx, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+def gather_keypoints_fixed(yx, out=None, group=None):
+    """gather_keypoints for equal shards (the bench's steady state): one
+    all_gather_into_tensor, no size exchange; out: a [world*b, K, 2] int32 buffer
+    reused across steps."""
+    n = dist.get_world_size(group) if dist.is_initialized() else 1
+    if n == 1:
+        return yx
+    if out is None:
+        out = torch.empty((n * yx.shape[0],) + tuple(yx.shape[1:]), device=yx.device, dtype=yx.dtype)
+    dist.all_gather_into_tensor(out, yx.contiguous(), group=group)
+    return out
+
+
+@torch.no_grad()
+def predict_keypoints_dp(model, x_shard, heat=False):
+    """Each rank's shard through the fused forward (+ argmax); keypoints gathered.
+    Returns (global int32 [B, K, 2], this rank's heatmaps or None)."""
+    if heat:
+        hm, yx = model.heatmaps_and_keypoints(x_shard)
+    else:
+        hm, yx = None, model.predict_keypoints(x_shard)
+    return gather_keypoints(yx), hm

@@ -12,7 +12,8 @@ Data parallelism: one process per GPU (torchrun), torch.distributed backend
 order backward produces them (fc, layer4, …, stem); as soon as a bucket is
 complete its all-reduce is launched asynchronously, so communication of the
 late layers overlaps the backward of the early ones.  BatchNorm statistics
-stay per rank (standard DDP semantics).
+stay per rank (standard DDP semantics); parameters and buffers are broadcast
+from rank 0 when the Trainer is built (broadcast_state).
 """
 import os
 
@@ -101,6 +102,25 @@ class GradBucketer:
         self._reset()
 
 
+def broadcast_state(model, src=0, group=None):
+    """Copy rank src's parameters and buffers (BN running stats and counters) to
+    every rank, in place — what DDP does at construction.  Tensors are flattened
+    per dtype into one buffer each, so a whole network costs a few collectives."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    tensors = [t.data for t in list(model.parameters()) + list(model.buffers())]
+    by_dtype = {}
+    for t in tensors:
+        by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (dtype, dev), ts in by_dtype.items():
+        flat = torch.cat([t.reshape(-1) for t in ts])
+        dist.broadcast(flat, src, group=group)
+        off = 0
+        for t in ts:
+            t.copy_(flat[off:off + t.numel()].view_as(t))
+            off += t.numel()
+
+
 class Trainer:
     """One optimizer step per call, reference semantics (train.py:33-36)."""
 
@@ -117,6 +137,8 @@ class Trainer:
         use_dp = distributed and dist.is_initialized() and dist.get_world_size() > 1
         # HKP_FORCE_BUCKETS=1: the DP gradient path (bucket copies, stream joins) at
         # world size 1, to time its overhead on one GPU
+        if use_dp:
+            broadcast_state(model)          # every replica starts from rank 0's weights and BN buffers
         use_dp = use_dp or os.environ.get("HKP_FORCE_BUCKETS") == "1"
         self.bucketer = GradBucketer(self.params, bucket_mb << 20) if use_dp else None
 

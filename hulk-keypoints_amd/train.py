@@ -21,7 +21,7 @@ from torch.utils.data import DataLoader
 from config import *  # noqa: F401,F403
 from config import BACKBONE, GAUSS_SIGMA, IMG_HEIGHT, IMG_WIDTH, LOSS, NUM_KEYPOINTS, batch_size, epochs
 from hkp import autograd as hkp_autograd
-from hkp.train import GradBucketer
+from hkp.train import GradBucketer, broadcast_state
 from src.dataset import KeypointsDataset, transform
 from src.model import KeypointsGauss
 
@@ -106,8 +106,7 @@ def main(dataset_dir="", output_dir="checkpoints", workers=0):
     keypoints = KeypointsGauss(NUM_KEYPOINTS, img_height=IMG_HEIGHT, img_width=IMG_WIDTH, backbone=BACKBONE).cuda()
     optimizer = torch.optim.Adam(keypoints.parameters(), lr=1.0e-4, weight_decay=1.0e-4)   # train.py:79
     if world > 1:
-        for p in keypoints.parameters():      # identical start on every rank
-            dist.broadcast(p.data, 0)
+        broadcast_state(keypoints)            # identical start on every rank (parameters + BN buffers)
         _bucketer = GradBucketer(list(keypoints.parameters()))
     fit(train_data, test_data, keypoints, epochs=epochs, checkpoint_path=save_dir)
     if dist.is_initialized():

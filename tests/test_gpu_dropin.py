@@ -1,0 +1,150 @@
+"""The drop-in surface, executed: the reference's scripts and classes run on
+the MI355X path and agree with the oracle (oracle/cpu_ref.py, pinned to the
+reference's own outputs).
+
+* train.main / fit (train.py:18-48 of the reference) on a tiny on-disk dataset
+  in the reference's layout (data/<dir>/{train,test}/{images/%05d.jpg,
+  keypoints/%05d.npy}): one epoch's loss against the oracle's train step, the
+  checkpoint's keys / shapes against the reference state_dict, and a
+  weights-only torch.load → KeypointsGauss.load_state_dict round trip.
+* analysis.main (analysis.py:18-42) on two images: argmax keypoints against
+  the oracle, overlays written.
+* hkp.autograd.HeatmapBCELoss == nn.BCELoss()(pred.double(), gt) (train.py:25).
+* the 1000-channel Resnet34_8s.forward (resnet_dilated.py:24-28) against the
+  oracle's upsampled logits.
+Images are written losslessly (PNG bytes under the reference's .jpg names:
+PIL / cv2 detect the format from the content).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import cpu_ref, recipe
+
+pytestmark = pytest.mark.gpu
+
+BB, K, H, W = "resnet34", 4, 64, 96
+
+
+def _write_split(root, split, n, seed):
+    from PIL import Image
+    img_dir, kp_dir = root / "data" / "toy" / split / "images", root / "data" / "toy" / split / "keypoints"
+    img_dir.mkdir(parents=True)
+    kp_dir.mkdir(parents=True)
+    bgr = recipe.seeded_images_u8(n, H, W, seed)
+    uv = recipe.seeded_keypoints(n, K, H, W, seed + 1)
+    for i in range(n):
+        Image.fromarray(np.ascontiguousarray(bgr[i][:, :, ::-1])).save(img_dir / ("%05d.jpg" % i), format="PNG")
+        np.save(kp_dir / ("%05d.npy" % i), uv[i].reshape(-1).astype(np.float64))
+    return bgr, uv
+
+
+@pytest.fixture
+def toy_run(tmp_path, monkeypatch, cuda_device):
+    import train as train_mod
+    bgr_tr, uv_tr = _write_split(tmp_path, "train", 4, 71)
+    bgr_te, uv_te = _write_split(tmp_path, "test", 2, 81)
+    monkeypatch.chdir(tmp_path)
+    for name, v in (("IMG_HEIGHT", H), ("IMG_WIDTH", W), ("NUM_KEYPOINTS", K), ("batch_size", 4), ("epochs", 1),
+                    ("BACKBONE", BB)):
+        monkeypatch.setattr(train_mod, name, v)
+    return train_mod, tmp_path, (bgr_tr, uv_tr), (bgr_te, uv_te)
+
+
+def test_train_main_fit_and_checkpoint(toy_run, capsys):
+    from src.model import KeypointsGauss
+    train_mod, root, (bgr_tr, uv_tr), (bgr_te, uv_te) = toy_run
+    torch.manual_seed(5)
+    with pytest.warns(UserWarning, match="pretrained"):
+        init = KeypointsGauss(K, H, W, backbone=BB).state_dict()     # the weights main() will draw
+    torch.manual_seed(5)
+    with pytest.warns(UserWarning, match="pretrained"):
+        train_mod.main("toy")
+    out = capsys.readouterr().out
+    train_loss = float(out.split("train loss:")[1].split()[0])
+    test_loss = float(out.split("test loss:")[1].split()[0])
+    # the epoch's only batch holds all 4 training images (BN statistics and the
+    # mean loss do not depend on the shuffled order): the oracle's train step
+    sd = {k: v.clone() for k, v in init.items()}
+    L, _, _ = cpu_ref.train_step(sd, recipe.to_tensor_nchw(bgr_tr), uv_tr, BB, K)
+    assert abs(train_loss - L.item()) < 1e-6 * L.item(), (train_loss, L.item())
+    # test loss: the stepped model (GPU Adam ≈ oracle Adam) on the 2 test images
+    with torch.no_grad():
+        heat = cpu_ref.forward(sd, recipe.to_tensor_nchw(bgr_te), BB, K)
+        Lt = cpu_ref.bce_loss(heat, cpu_ref.gauss_target(uv_te, H, W, 8))
+    assert abs(test_loss - Lt.item()) < 1e-3 * Lt.item(), (test_loss, Lt.item())
+    # checkpoint: reference key names, order, shapes (OIHW) and dtypes
+    ck = root / "checkpoints" / "toy" / "model_2_1_0.pth"
+    assert ck.exists()
+    state = torch.load(ck, map_location="cpu", weights_only=True)
+    spec = cpu_ref.state_dict_spec(BB)
+    assert list(state.keys()) == [k for k, _, _ in spec]
+    assert all(tuple(state[k].shape) == tuple(s) for k, s, _ in spec)
+    m2 = KeypointsGauss(K, H, W, backbone=BB, pretrained=False)
+    m2.load_state_dict(state)
+    again = m2.state_dict()
+    assert all(torch.equal(again[k], state[k]) for k in state)
+
+
+def test_analysis_main_keypoints(tmp_path, monkeypatch, cuda_device):
+    import analysis as analysis_mod
+    from PIL import Image
+    monkeypatch.setattr(analysis_mod, "IMG_HEIGHT", H)
+    monkeypatch.setattr(analysis_mod, "IMG_WIDTH", W)
+    sd = recipe.seeded_state_dict(BB, 91)
+    (tmp_path / "ck").mkdir()
+    torch.save(sd, tmp_path / "ck" / "m.pth")
+    (tmp_path / "imgs").mkdir()
+    bgr = recipe.seeded_images_u8(2, H, W, 92)
+    for i in range(2):
+        Image.fromarray(np.ascontiguousarray(bgr[i][:, :, ::-1])).save(tmp_path / "imgs" / ("f%d.png" % i))
+    kp = analysis_mod.main("m.pth", str(tmp_path / "imgs"), out_dir=str(tmp_path / "preds"),
+                           checkpoint_dir=str(tmp_path / "ck"))
+    assert kp.shape == (2, K, 2) and kp.dtype == np.int32
+    for i in range(2):          # batch 1 per image, train-mode BN (analysis.py:36-42)
+        with torch.no_grad():
+            heat = cpu_ref.forward({k: v.clone() for k, v in sd.items()}, recipe.to_tensor_nchw(bgr[i:i + 1]), BB, K)
+        assert np.array_equal(kp[i:i + 1], cpu_ref.argmax_yx(heat))
+        assert (tmp_path / "preds" / ("out%04d.png" % i)).exists()
+    assert np.array_equal(np.load(tmp_path / "preds" / "keypoints.npy"), kp)
+
+
+def test_heatmap_bce_loss_module(cuda_device):
+    from hkp.autograd import HeatmapBCELoss, HeatmapMSELoss
+    g = torch.Generator().manual_seed(3)
+    p = torch.rand(2, 3, 17, 23, generator=g)
+    p[0, 0, 0, :4] = torch.tensor([0.0, 1.0, 1e-30, 1.0 - 2 ** -24])
+    y = torch.rand(2, 3, 17, 23, generator=g, dtype=torch.float64)
+    for mod, ref in ((HeatmapBCELoss(), torch.nn.BCELoss()), (HeatmapMSELoss(), torch.nn.MSELoss())):
+        a = p.clone().to(cuda_device).requires_grad_(True)
+        b = p.clone().requires_grad_(True)
+        la = mod(a, y.to(cuda_device))
+        lb = ref(b.double(), y)
+        la.backward()
+        lb.backward()
+        assert la.dtype == torch.float64 and abs(la.item() - lb.item()) <= 1e-12 * abs(lb.item())
+        assert torch.allclose(a.grad.cpu(), b.grad, rtol=1e-6, atol=0)
+    with pytest.raises(TypeError):
+        HeatmapBCELoss()(p.double().to(cuda_device), y.to(cuda_device))
+
+
+def test_resnet_dilated_forward_1000_channels(cuda_device, golden):
+    """Resnet34_8s.forward: all 1000 upsampled logit channels (resnet_dilated.py:24-28)."""
+    from src.resnet_dilated import Resnet34_8s
+    g = golden("fwd_r34_k4_96x128")
+    sd = recipe.seeded_state_dict("resnet34", int(g["wseed"]))
+    net = Resnet34_8s(pretrained=False)
+    net.load_state_dict({k[len("resnet."):]: v for k, v in sd.items()})
+    net = net.to(cuda_device)
+    x = recipe.to_tensor_nchw(g["images_u8"])
+    with torch.no_grad():
+        out = net(x.to(cuda_device)).cpu()
+        _, low = cpu_ref.forward({k: v.clone() for k, v in sd.items()}, x, "resnet34", 1000, return_lowres=True)
+        ref = F.interpolate(low, size=x.shape[2:], mode="bilinear", align_corners=True)
+    assert out.shape == (2, 1000, 96, 128)
+    err = (out - ref).abs().max().item()
+    assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
+    assert (torch.sigmoid(out[:, :4]).numpy() - g["heat"]).__abs__().max() < 1e-3

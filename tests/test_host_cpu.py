@@ -139,3 +139,149 @@ def test_entry_modules_import():
     import config
     assert (config.NUM_KEYPOINTS, config.IMG_HEIGHT, config.IMG_WIDTH, config.GAUSS_SIGMA, config.epochs,
             config.batch_size) == (4, 480, 640, 8, 25, 4)
+
+
+def _trainer_worker(rank, world, port, q):
+    """One rank of a world-2 gloo group running hkp.train.Trainer with its
+    per-rank compute (net.keypoints_forward / ops.heat_loss /
+    net.keypoints_backward) replaced by the oracle's CPU autograd restatement."""
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hkp import net, ops, train
+    from oracle import cpu_ref, recipe
+    from src.model import KeypointsGauss
+    bb, K, B, H, W = "resnet18", 2, 2, 32, 48
+    torch.manual_seed(100 + rank)                      # replicas start DIFFERENT ...
+    m = KeypointsGauss(K, H, W, backbone=bb, pretrained=False)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.01 * rank)
+        for n_, b in m.named_buffers():
+            if "running" in n_:
+                b.add_(0.1 * (rank + 1))
+    t = train.Trainer(m, distributed=True, optimizer="torch", bucket_mb=1)
+    # ... and the Trainer broadcast rank 0's parameters and buffers
+    state = torch.cat([v.detach().reshape(-1).double() for v in m.state_dict().values()])
+    states = [torch.empty_like(state) for _ in range(world)]
+    dist.all_gather(states, state)
+    same_start = all(torch.equal(s, states[0]) for s in states)
+    start_sd = {k: v.clone() for k, v in m.state_dict().items()}       # reference layout (OIHW)
+
+    def oracle_forward(resnet, x, k, heat=True, argmax=False, trace=None):
+        sd = m.state_dict(keep_vars=True)            # conv weights: differentiable OIHW views of KRSC params
+        hm = cpu_ref.forward(sd, x, bb, k)
+        trace.head = hm
+        return hm, None, None
+
+    def oracle_loss(hm, target, uv, sigma, kind, want_grad=True):
+        gt = cpu_ref.gauss_target(uv, hm.shape[2], hm.shape[3], sigma)
+        L = cpu_ref.bce_loss(hm, gt)
+        (dheat,) = torch.autograd.grad(L, hm, retain_graph=True)
+        return L.detach(), dheat
+
+    def oracle_backward(resnet, trace, dheat, grads):
+        ps = list(m.parameters())
+        gs = torch.autograd.grad(trace.head, ps, dheat)
+        for p, g in reversed(list(zip(ps, gs))):     # backward order: the bucketer fills from the fc side
+            grads.put(p, g)
+        return grads
+
+    net.keypoints_forward, net.keypoints_backward, ops.heat_loss = oracle_forward, oracle_backward, oracle_loss
+    imgs = recipe.seeded_images_u8(B * world, H, W, 7)
+    uvs = recipe.seeded_keypoints(B * world, K, H, W, 8)
+    x = recipe.to_tensor_nchw(imgs[rank * B:(rank + 1) * B])
+    t.forward_backward(x, uv=torch.from_numpy(uvs[rank * B:(rank + 1) * B]))
+    # reference: each shard's gradient from the common start, averaged
+    ref = None
+    for r in range(world):
+        sd = {k: v.clone() for k, v in start_sd.items()}
+        _, g, _ = cpu_ref.train_step(sd, recipe.to_tensor_nchw(imgs[r * B:(r + 1) * B]), uvs[r * B:(r + 1) * B], bb,
+                                     K)
+        ref = g if ref is None else {k: ref[k] + g[k] for k in g}
+    names = [n_ for n_, _ in m.named_parameters()]
+    err = 0.0
+    for n_, p in zip(names, m.parameters()):
+        want = ref[n_] / world
+        got = p.grad if p.grad.shape == want.shape else p.grad.permute(0, 3, 1, 2)   # KRSC → OIHW
+        err = max(err, ((got - want).abs().max() / (want.abs().max() + 1e-30)).item())
+    grads_same = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+    allg = [torch.empty_like(grads_same) for _ in range(world)]
+    dist.all_gather(allg, grads_same)
+    q.put((rank, same_start, err, all(torch.equal(a, allg[0]) for a in allg), len(t.bucketer.buckets)))
+    dist.destroy_process_group()
+
+
+def test_trainer_dp_gloo_world2():
+    """Trainer(distributed=True) wiring over a real 2-process gloo group:
+    parameters/buffers broadcast from rank 0 at construction, gradients
+    all-reduced through the bucketer equal the mean of the per-shard oracle
+    gradients, identical on both ranks."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(p.exitcode == 0 for p in procs)
+    for rank, same_start, err, grads_same, nb in res:
+        assert same_start, "replicas did not start from rank 0's state"
+        assert err < 1e-5, "rank %d: DP gradient differs from the mean of per-shard gradients by %g" % (rank, err)
+        assert grads_same and nb >= 2
+
+
+def test_shard_range_and_gather_single():
+    from hkp import parallel
+    spans = [parallel.shard_range(10, r, 4) for r in range(4)]
+    assert spans == [(0, 3), (3, 6), (6, 8), (8, 10)]
+    yx = torch.zeros((3, 2, 2), dtype=torch.int32)
+    assert parallel.gather_keypoints(yx) is yx
+    with pytest.raises(ValueError):
+        parallel.gather_keypoints(yx.float())
+
+
+def _gather_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hkp import parallel
+    n = 7
+    lo, hi = parallel.shard_range(n, rank, world)
+    mine = torch.arange(lo * 6, hi * 6, dtype=torch.int32).reshape(-1, 3, 2)
+    allk = parallel.gather_keypoints(mine)
+    fixed = parallel.gather_keypoints_fixed(torch.full((2, 3, 2), rank, dtype=torch.int32))
+    q.put((rank, torch.equal(allk, torch.arange(n * 6, dtype=torch.int32).reshape(n, 3, 2)),
+           fixed[:, 0, 0].tolist()))
+    dist.destroy_process_group()
+
+
+def test_gather_keypoints_gloo_world3():
+    """Inference DP: ragged shards' int32 keypoints all-gathered in rank order."""
+    world, port = 3, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok, _ in res)
+    assert all(f == [0, 0, 1, 1, 2, 2] for _, _, f in res)
+
+
+def test_bench_gpus_must_match_world_size():
+    """bench.py --gpus N under a torchrun environment of another size refuses to
+    run (exit 2) instead of silently reporting n_gpus = WORLD_SIZE."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr, r.stderr
