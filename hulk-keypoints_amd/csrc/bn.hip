@@ -135,6 +135,49 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
     }
 }
 
+// Plain-fp16 path (BASELINE config C4, autocast semantics): y is the fp16 conv
+// output, the result is written in fp16 (the next conv's operand) and, for the
+// block feeding the head, also in fp32.  RES: 0 none, 1 raw fp16 residual (the
+// block input), 2 affine fp16 residual (the downsample conv's y with its BN).
+// The BN arithmetic itself is fp32 (x*alpha + beta, two roundings, as above).
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+template <int RES, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, const h16x8* __restrict__ y,
+                                                           const float* __restrict__ ss, const h16x8* __restrict__ res,
+                                                           const float* __restrict__ rss, h16x8* __restrict__ out,
+                                                           f32x4* __restrict__ out32) {
+    const int C = C8 * 8;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+        const int c0 = (int)(i % C8) * 8;
+        const h16x8 v = y[i];
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(__fmul_rn((float)v[e], ss[c0 + e]), ss[C + c0 + e]);
+        if constexpr (RES == 1) {
+            const h16x8 r = res[i];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(o[e], (float)r[e]);
+        } else if constexpr (RES == 2) {
+            const h16x8 r = res[i];
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn((float)r[e], rss[c0 + e]), rss[C + c0 + e]));
+        }
+        h16x8 h;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if constexpr (RELU) o[e] = o[e] > 0.f ? o[e] : 0.f;
+            h[e] = (_Float16)o[e];
+        }
+        out[i] = h;
+        if (out32) {
+            out32[2 * i] = f32x4{o[0], o[1], o[2], o[3]};
+            out32[2 * i + 1] = f32x4{o[4], o[5], o[6], o[7]};
+        }
+    }
+}
+
 // maxpool 3x3 / s2 / p1 (-inf padding) of relu(y*a+b); one thread per 4 channels of one output pixel
 __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo,
                                                              const float* __restrict__ y,
@@ -277,5 +320,31 @@ extern "C" int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, c
     hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n, h, w, c,
                        ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes, (uchar4*)route);
     HKP_LAUNCH_CHECK("hkp_bn_relu_maxpool");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_apply_f16(int64_t m, int32_t c, const uint16_t* y, const float* scale_shift, const uint16_t* res,
+                                const float* res_scale_shift, int32_t relu, uint16_t* out, float* out32,
+                                hkp_stream_t stream) {
+    HKP_CHECK_ARG(m > 0 && c > 0 && c % 8 == 0, "hkp_bn_apply_f16: need m>0 and c%%8==0 (c=%d)", c);
+    HKP_CHECK_ARG(y && scale_shift && out, "hkp_bn_apply_f16: null tensor");
+    HKP_CHECK_ARG(res_scale_shift == nullptr || res != nullptr, "hkp_bn_apply_f16: res_scale_shift without res");
+    const long n8 = m * (long)c / 8;
+    const int g = grid_for(n8);
+    hipStream_t st = as_stream(stream);
+    const h16x8 *Y = (const h16x8*)y, *R = (const h16x8*)res;
+    h16x8* O = (h16x8*)out;
+#define HKP_APPLY16(RES, RL)                                                                                    \
+    hipLaunchKernelGGL((bn_apply_f16_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n8, c / 8, Y, scale_shift, R, \
+                       res_scale_shift, O, (f32x4*)out32)
+    if (!res) {
+        if (relu) HKP_APPLY16(0, true); else HKP_APPLY16(0, false);
+    } else if (!res_scale_shift) {
+        if (relu) HKP_APPLY16(1, true); else HKP_APPLY16(1, false);
+    } else {
+        if (relu) HKP_APPLY16(2, true); else HKP_APPLY16(2, false);
+    }
+#undef HKP_APPLY16
+    HKP_LAUNCH_CHECK("hkp_bn_apply_f16");
     return HKP_OK;
 }

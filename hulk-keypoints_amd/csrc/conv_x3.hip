@@ -23,23 +23,27 @@
 // so the 32 channels of one filter tap of one GEMM row are one 128-B cache line
 // holding both planes — the same bytes as the fp32 tensor.
 //
-// Forward kernel (conv_x3_kernel<BN, KH>): tile 256 pixels x BN output channels,
-// 8 waves as 4x2 (wave tile 64 x BN/2, 32x32x16 MFMAs).  A K-step stages KH
-// 16-channel slices: KH = 2 → 128-B LDS rows (a whole line), 3-stage ring;
-// KH = 1 → 64-B rows (half a line), 4-stage ring (BN = 256: 32 KB per stage).
-// Staging is LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no ds_write),
-// NST-1 K-steps in flight ahead of the compute, retired by a counted
-// s_waitcnt vmcnt + raw s_barrier (never __syncthreads inside the loop: its
-// fence would drain the DMA queue).  LDS rows are unpadded (the DMA writes
-// lane-linear 1 KiB pieces); an XOR swizzle of the 16-B chunk index (with
-// (row>>1)&7 for 128-B rows, (row>>2)&3 for 64-B rows), applied to the per-lane
-// DMA SOURCE address and to the ds_read address, makes the fragment reads
-// conflict-free (0 conflicts measured).  K order: channel group outer, filter
-// tap inner (a pixel line is re-read by the next taps while in L2).
-// Out-of-image taps / rows past M load a zero line.  The mainloop is software-
-// pipelined (next fragments read during the current MFMAs, one ds_read per MFMA
-// gap, one barrier per K-step).  Epilogue: NHWC fp32 store (x weight scale,
-// x gradient scale, + addend) + BN tile partials per 128-row tile.
+// Forward kernel (conv_x3_kernel<BN, STEM, PAIR, MFD, SK, P>): tile 256 pixels x
+// BN output channels, 8 waves as 4x2 (wave tile 64 x BN/2).  A K-step stages one
+// 128-B line per GEMM row (32 channels hi|lo; P = 1: 64 plain fp16 channels) into
+// a 2- or 3-stage LDS ring by LDS-DMA (global_load_lds_dwordx4: no VGPR round
+// trip, no ds_write), NST-1 K-steps in flight ahead of the compute, retired by a
+// counted s_waitcnt vmcnt + raw s_barrier (never __syncthreads inside the loop:
+// its fence would drain the DMA queue).  LDS rows are unpadded (the DMA writes
+// lane-linear 1 KiB pieces); an XOR swizzle of the 16-B chunk index with
+// (row>>1)&7, applied to the per-lane DMA SOURCE address and to the ds_read
+// address, makes the fragment reads conflict-free (0 conflicts measured).  K
+// order: channel group outer, filter tap inner (a pixel line is re-read by the
+// next taps while in L2).  Out-of-image taps / rows past M load a zero line.
+// MFMA bodies: 16x16x32 (MFD 16) or 32x32x16 (MFD 32), software-pipelined (next
+// fragments read during the current MFMAs, one ds_read per MFMA gap, one barrier
+// per K-step).  Epilogue: NHWC fp32 (or fp16) store (x weight scale, x gradient
+// scale, + addend) + BN tile partials per 128-row tile.
+//
+// Operand layouts (P): 3 = the packed f16x3 split above (fp32-accurate, the
+// default arithmetic); 1 = plain fp16 NHWC activations and KRSC weights (each
+// output channel scaled by a power of two) — BASELINE config C4's "fp16 with
+// MFMA", the same kernel with 2 MFMAs per 64 channels instead of 3 per 32.
 //
 // Replaces the cuDNN convs of src/resnet.py:20-37,77,86,137,184-188 and their
 // backward under loss.backward() (train.py:35).
@@ -58,7 +62,8 @@ struct X3Args {
     const _Float16* xs;
     const _Float16* ws;
     const float* wscale;   // per output channel inverse weight scale [K] (nullable: 1)
-    float* y;
+    float* y;              // fp32 output, or
+    _Float16* y16 = nullptr;   // fp16 output (plain-fp16 path, autocast semantics)
     float* part;
     const unsigned* amax;  // max|input| bits: the input was scaled by pow2_scale_for(amax) (dgrad)
     const float* add;      // addend of the output (dgrad: the residual-branch gradient), nullable
@@ -114,15 +119,11 @@ __device__ __forceinline__ void interleave() {
     if constexpr (NM > per * nr) __builtin_amdgcn_sched_group_barrier(0x008, NM - per * nr, 0);
 }
 
-// LDS ring depth of a conv_x3 tile config: 256x256 with 32-channel stages 2
-// (A fragments double-buffered instead), other 32-channel stages 3, 16-channel
-// stages 4 (a 4-stage 256x64 ring with 32-channel stages measured no faster
-// than 3: the short tiles are not load-latency bound); two blocks per CU
-// (ORD 3): 16-channel stages 4, the stem's 32-channel stages 2.  The whole
-// 160 KiB at most (the stream-K flag reuses the drained ring).
-constexpr int x3_nst(int BN, int KH, int ORD = 0) {
-    return (BN == 256 && KH == 2) || (ORD == 3 && KH == 2) ? 2 : (KH == 2 ? 3 : 4);
-}
+// LDS ring depth of a conv_x3 tile config (32-channel / 128-B stages): 256x256
+// tiles 2 (B fragments refilled per column instead), two blocks per CU (PAIR:
+// 256x64 tiles and the stem) 2, otherwise 3.  The whole 160 KiB at most (the
+// stream-K flag reuses the drained ring).
+constexpr int x3_nst(int BN, bool PAIR) { return (BN == 256 || PAIR) ? 2 : 3; }
 
 // ---- stream-K bookkeeping (X3Args::sk_units) ----
 __device__ __forceinline__ long sk_start(long b, long U, int G) { return b * U / G; }
@@ -206,22 +207,132 @@ __device__ __forceinline__ long x3_out_off(const X3Args& a, int m, int n) {
     return pix * a.K + n;
 }
 
-// Mainloop + epilogue of conv_x3_kernel<BN, 2, false, 0, 16>: 16x16x32 MFMAs, one
-// k32 step per 32-channel stage (LDS ring, DMA issue and the swizzled 128-B rows
-// exactly as the 32x32 path).  Wave tile 64 x BN/2 = UM x UN 16x16 tiles.
+// One output element: y (fp32) or y16 (fp16, the plain-fp16 path), scaled, +
+// the addend (dgrad's residual-branch gradient)
+__device__ __forceinline__ void x3_store(const X3Args& a, long off, float v, float av) {
+    if (off < 0) return;
+    v = a.add ? v + av : v;
+    if (a.y16) a.y16[off] = (_Float16)v;
+    else a.y[off] = v;
+}
+
+// The MFMAs of one 128-B stage row pair (A fragment a0/a1, B fragment b0/b1 =
+// the row's chunks 0-3 / 4-7) for operand layout P:
+//   P = 3 (packed f16x3 split, chunks = hi32 | lo32):  hi*hi + hi*lo + lo*hi
+//   P = 1 (plain fp16, chunks = channels 0-31 | 32-63): two k-slices
+template <int P, typename V, typename Acc, typename Mfma>
+__device__ __forceinline__ void x3_products(Acc& acc, const V& a0, const V& a1, const V& b0, const V& b1, Mfma&& mfma) {
+    if constexpr (P == 3) {
+        acc = mfma(a0, b0, acc);
+        acc = mfma(a0, b1, acc);
+        acc = mfma(a1, b0, acc);
+    } else {
+        acc = mfma(a0, b0, acc);
+        acc = mfma(a1, b1, acc);
+    }
+}
+
+// BN tile partials of the tile in the accumulators: per 128-row half, the
+// column sum and the sum of squares about the half's mean (Chan-mergeable in
+// bn_finalize).  VAL(i, j, r) / ROW(i, r) address the accumulator element and
+// its output row; COLS per wave column block, LGRP lanes per column group.
+template <int BN, int NI, int NJ, int NR, int CW, int SHF, typename Val, typename Row>
+__device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int m0, int n0, int wm, int wn, int lane,
+                                               int tid, Val&& val, Row&& row) {
+    constexpr int WM = 4;
+    __syncthreads();                       // every wave done reading the ring
+    float* red = (float*)smem;             // [WM][BN] column sums, then [2][BN] half-tile means
+    float* tmean = red + WM * BN;
+    float colsum[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) s += (row(i, r) < a.M) ? val(i, j, r) : 0.f;
+        for (int o = SHF; o < 64; o <<= 1) s += __shfl_xor(s, o);
+        colsum[j] = s;
+    }
+    if (lane < CW) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) red[wm * BN + wn * NJ * CW + j * CW + lane] = colsum[j];
+    }
+    __syncthreads();
+    const long tile128 = (long)(m0 >> 7);
+    for (int e = tid; e < 2 * BN; e += 512) {
+        const int h = e / BN, c = e - h * BN;
+        const int cnt = min(128, a.M - (m0 + 128 * h));
+        if (cnt > 0) {
+            const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+            tmean[h * BN + c] = s / (float)cnt;
+            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
+        }
+    }
+    __syncthreads();
+    const float* mu_h = tmean + (wm >> 1) * BN;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const float mu = mu_h[wn * NJ * CW + j * CW + (lane % CW)];
+        float q = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                const float d = val(i, j, r) - mu;
+                q += (row(i, r) < a.M) ? d * d : 0.f;
+            }
+        for (int o = SHF; o < 64; o <<= 1) q += __shfl_xor(q, o);
+        colsum[j] = q;
+    }
+    __syncthreads();
+    if (lane < CW) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) red[wm * BN + wn * NJ * CW + j * CW + lane] = colsum[j];
+    }
+    __syncthreads();
+    for (int e = tid; e < 2 * BN; e += 512) {
+        const int h = e / BN, c = e - h * BN;
+        if (a.M - (m0 + 128 * h) > 0)
+            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+    }
+}
+
+// fp16 output tile staged in LDS ([256][BN + 8] halves: the 16-B row pad makes
+// the fragment-layout ds_write_b16s conflict-free) and written as whole 16-B
+// row chunks: 8x fewer store instructions than per-element fp16 stores, full
+// 128-B lines — the epilogue of the short-K 1x1 convs of config C4 is most of
+// their time.
+template <int BN>
+__device__ __forceinline__ void x3_store_tile_f16(const X3Args& a, const char* smem, int m0, int n0, int tid) {
+    constexpr int CH = BN / 8, PITCH = BN + 8;
+#pragma unroll 4
+    for (int e = tid; e < 256 * CH; e += 512) {
+        const int row = e / CH, cc = e - row * CH;
+        const int m = m0 + row;
+        if (m < a.M)
+            *(uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8) = *(const uint4*)(smem + (row * PITCH + cc * 8) * 2);
+    }
+}
+
+// Mainloop + epilogue of the 16x16x32-MFMA bodies: one k32 step per half of a
+// 128-B stage row (LDS ring, DMA issue and the swizzled rows exactly as the
+// 32x32 path).  Wave tile 64 x BN/2 = UM x UN 16x16 tiles.
 // Fragment read: lane reads row (lane & 15) of a 16-row tile, 16-B chunk
-// (lane >> 4) (hi) / 4 + (lane >> 4) (lo): with the (row >> 1) & 7 chunk swizzle
-// every ds_read_b128 lane group covers the 64 banks once.  Output fragment:
-// lane holds column (lane & 15), rows 4 * (lane >> 4) + 0..3.
-// Pipeline per K-step t (as the 16-channel-stage path): [issue DMA t+NST-1]
-// wait own DMA of t+1 (+ this wave's reads of t), barrier, [read A frags of t+1]
-// then per column block j: [MFMAs of t with B_j] [refill B_j with t+1's].
-template <int BN, int NST, int STAGE, int GL, typename Issue>
+// (lane >> 4) (first half) / 4 + (lane >> 4) (second half): with the
+// (row >> 1) & 7 chunk swizzle every ds_read_b128 lane group covers the 64 banks
+// once.  Output fragment: lane holds column (lane & 15), rows 4 * (lane >> 4) + 0..3.
+// Pipeline per K-step t (NST 3): [issue DMA t+NST-1] wait own DMA of t+1 (+ this
+// wave's reads of t), barrier, [read A frags of t+1] then per column block j:
+// [MFMAs of t with B_j] [refill B_j with t+1's].  NST 2 (256x256; 256x64 pairs):
+// A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
+template <int BN, int NST, int STAGE, int GL, int P, typename Issue>
 __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
                                                   Issue& issue_next) {
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
+    constexpr int NMC = (P == 3 ? 3 : 2) * UM;      // MFMAs per column block per K-step
     const int r16 = lane & 15, q = lane >> 4;
     const int sw = (r16 >> 1) & 7;                 // the DMA's swizzle of every row ≡ r16 (mod 16)
     const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
@@ -248,13 +359,12 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         bh[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_h);
         bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
     };
+    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+    };
     auto mma_col = [&](const FA& f, int j) {
 #pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
-        }
+        for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], f.h[i], f.l[i], bh[j], bl[j], mfma);
     };
 
     if constexpr (NST == 2) {
@@ -287,7 +397,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             read_a(fa, st);
 #pragma unroll
             for (int j = 0; j < UN; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 3 * UM, 0);  // column j's MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
                 __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
             }
             __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
@@ -297,61 +407,59 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
         for (int j = 0; j < UN; ++j) mma_col(fa, j);
     } else {
-    // prologue: NST-1 stages in flight, stage 0 landed everywhere
-    issue_next();
-    for (int s = 1; s < NST - 1; ++s)
-        if (s < nks) issue_next();
-    {
-        const int after = std::min(nks - 1, NST - 2);
-        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    lds_barrier();
-    auto wait_next = [&](int t) {
-        const int after = std::min(nks - 1, t + NST - 1) - (t + 1);
-        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * GL) : "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    };
-    int cur = 0;
-    FA fa0, fa1;
-    read_a(fa0, smem);
-#pragma unroll
-    for (int j = 0; j < UN; ++j) read_b(j, smem);
-    auto step = [&](int t, FA& fc, FA& fn) {       // K-step t, reading t+1's fragments
-        if (t + NST - 1 < nks) issue_next();
-        wait_next(t);
+        // prologue: NST-1 stages in flight, stage 0 landed everywhere
+        issue_next();
+        for (int s = 1; s < NST - 1; ++s)
+            if (s < nks) issue_next();
+        {
+            const int after = std::min(nks - 1, NST - 2);
+            if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         lds_barrier();
-        cur = cur == NST - 1 ? 0 : cur + 1;
-        const char* st = smem + cur * STAGE;
-        read_a(fn, st);
+        auto wait_next = [&](int t) {
+            const int after = std::min(nks - 1, t + NST - 1) - (t + 1);
+            if (after >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        };
+        int cur = 0;
+        FA fa0, fa1;
+        read_a(fa0, smem);
 #pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            mma_col(fc, j);
-            read_b(j, st);
+        for (int j = 0; j < UN; ++j) read_b(j, smem);
+        auto step = [&](int t, FA& fc, FA& fn) {       // K-step t, reading t+1's fragments
+            if (t + NST - 1 < nks) issue_next();
+            wait_next(t);
+            lds_barrier();
+            cur = cur == NST - 1 ? 0 : cur + 1;
+            const char* st = smem + cur * STAGE;
+            read_a(fn, st);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                mma_col(fc, j);
+                read_b(j, st);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        int t = 0;
+        for (; t + 2 < nks; t += 2) {
+            step(t, fa0, fa1);
+            step(t + 1, fa1, fa0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
+        if (t + 1 < nks) {
+            step(t, fa0, fa1);
 #pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 3 * UM, 0);  // column j's MFMAs
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
+            for (int j = 0; j < UN; ++j) mma_col(fa1, j);
+        } else {
+#pragma unroll
+            for (int j = 0; j < UN; ++j) mma_col(fa0, j);
         }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    int t = 0;
-    for (; t + 2 < nks; t += 2) {
-        step(t, fa0, fa1);
-        step(t + 1, fa1, fa0);
-    }
-    if (t + 1 < nks) {
-        step(t, fa0, fa1);
-#pragma unroll
-        for (int j = 0; j < UN; ++j) mma_col(fa1, j);
-    } else {
-#pragma unroll
-        for (int j = 0; j < UN; ++j) mma_col(fa0, j);
-    }
     }
 
     if (partial) {                         // stream-K: fold the tile's segments
@@ -360,8 +468,36 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return;
     }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
-    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
     const int rbase = m0 + wm * UM * 16 + 4 * q;
+    if constexpr (P == 1) {                // fp16 output: scale, partials, LDS-staged store
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            const float sc = (a.wscale ? a.wscale[n0 + wn * UN * 16 + j * 16 + r16] : 1.f) * ginv;
+#pragma unroll
+            for (int i = 0; i < UM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc;
+        }
+        if (a.part)
+            x3_bn_partials<BN, UM, UN, 4, 16, 16>(
+                a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
+                [&](int i, int r) { return rbase + i * 16 + r; });
+        __syncthreads();                   // the ring (or the partials' scratch) is free
+        _Float16* t = (_Float16*)smem;
+        constexpr int PITCH = BN + 8;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int j = 0; j < UN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    t[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * UN * 16 + j * 16 + r16] =
+                        (_Float16)acc[i][j][r];
+        __syncthreads();
+        x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
+        return;
+    }
+    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
 #pragma unroll
     for (int j = 0; j < UN; ++j) {
         const int n = n0 + wn * UN * 16 + j * 16 + r16;
@@ -381,94 +517,40 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 acc[i][j][r] *= sc;
-                if (off[i][r] >= 0) a.y[off[i][r]] = a.add ? acc[i][j][r] + av[i][r] : acc[i][j][r];
+                x3_store(a, off[i][r], acc[i][j][r], av[i][r]);
             }
     }
     if (a.part == nullptr) return;
-    __syncthreads();                       // every wave done reading the ring
-    float* red = (float*)smem;             // [WM][BN] column sums, then [2][BN] half-tile means
-    float* tmean = red + WM * BN;
-    float colsum[UN];
-#pragma unroll
-    for (int j = 0; j < UN; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) s += (rbase + i * 16 + r < a.M) ? acc[i][j][r] : 0.f;
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        colsum[j] = s;
-    }
-    if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < UN; ++j) red[wm * BN + wn * UN * 16 + j * 16 + lane] = colsum[j];
-    }
-    __syncthreads();
-    const long tile128 = (long)(m0 >> 7);
-    for (int e = tid; e < 2 * BN; e += 512) {
-        const int h = e / BN, c = e - h * BN;
-        const int cnt = min(128, a.M - (m0 + 128 * h));
-        if (cnt > 0) {
-            const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
-            tmean[h * BN + c] = s / (float)cnt;
-            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
-        }
-    }
-    __syncthreads();
-    const float* mu_h = tmean + (wm >> 1) * BN;
-#pragma unroll
-    for (int j = 0; j < UN; ++j) {
-        const float mu = mu_h[wn * UN * 16 + j * 16 + r16];
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float d = acc[i][j][r] - mu;
-                s += (rbase + i * 16 + r < a.M) ? d * d : 0.f;
-            }
-        s += __shfl_xor(s, 16);
-        s += __shfl_xor(s, 32);
-        colsum[j] = s;
-    }
-    __syncthreads();
-    if (lane < 16) {
-#pragma unroll
-        for (int j = 0; j < UN; ++j) red[wm * BN + wn * UN * 16 + j * 16 + lane] = colsum[j];
-    }
-    __syncthreads();
-    for (int e = tid; e < 2 * BN; e += 512) {
-        const int h = e / BN, c = e - h * BN;
-        if (a.M - (m0 + 128 * h) > 0)
-            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
-    }
+    x3_bn_partials<BN, UM, UN, 4, 16, 16>(
+        a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
+        [&](int i, int r) { return rbase + i * 16 + r; });
 }
 
 // STEM: the 7x7/s2 stem on the zero-padded NHWC4 image planes of
 // hkp_stem_pack_x3 (a.H/a.W = padded size, stride 2, pad 0, R = 7, S = 1: one
 // K-step per filter row = 8 taps x 4 channels; logical chunk j of a row holds
 // padded pixels 2wo+2j, 2wo+2j+1 from the hi plane (j < 4) or the lo plane).
-// MFD: MFMA shape, 32 = v_mfma_f32_32x32x16_f16 (two k16 slices per 32-channel
-// stage), 16 = v_mfma_f32_16x16x32_f16 (one k32 step per stage; same cycles per
-// FLOP, lower power per FLOP, so the chip holds a higher clock under load —
+// MFD: MFMA shape, 32 = v_mfma_f32_32x32x16_f16 (two k16 slices per 128-B
+// stage), 16 = v_mfma_f32_16x16x32_f16 (one k32 step per stage half; same cycles
+// per FLOP, lower power per FLOP, so the chip holds a higher clock under load —
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
-template <int BN, int KH, bool STEM, int ORD, int MFD>
+// P: operand layout (x3_products) — 3 packed f16x3 split, 1 plain fp16.
+template <int BN, bool STEM, bool PAIR, int MFD, int P>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-    constexpr int ROW = 64 * KH;                   // bytes per LDS row
+    constexpr int ROW = 128;                       // bytes per LDS row (one packed line)
     constexpr int CPR = ROW / 16;                  // 16-B chunks per row
     constexpr int RPI = 1024 / ROW;                // rows per DMA wave-instruction
-    constexpr bool WIDE2 = BN == 256 && KH == 2;    // 256x256 with 32-channel stages: 2-stage ring
-    constexpr int NST = x3_nst(BN, KH, ORD);         // LDS ring depth
+    constexpr int NST = x3_nst(BN, PAIR);          // LDS ring depth
     constexpr int STAGE = (BM + BN) * ROW;
     constexpr int GA = BM / RPI / 8;               // A DMA instructions per wave per stage
     constexpr int GBT = BN / RPI;                  // B DMA instructions per stage (all waves)
     constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
-    static_assert(TN >= 1 && (KH == 1 || KH == 2) && (!STEM || KH == 2), "bad conv_x3 config");
-    static_assert(MFD == 32 || (MFD == 16 && KH == 2), "bad conv_x3 MFMA shape");
+    static_assert(MFD == 16 || MFD == 32, "bad conv_x3 MFMA shape");
+    static_assert(P == 3 || (P == 1 && !STEM), "bad conv_x3 operand layout");
+    static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
@@ -478,13 +560,11 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     const int wm = w / WN, wn = w % WN;
 
     // swizzled physical chunk of a logical chunk in row r
-    auto swz = [](int row) { return KH == 2 ? (row >> 1) & 7 : (row >> 2) & 3; };
-    // halves offset, inside a packed line, of logical chunk L of a KH-slice row
-    // (KH = 1: + 16*s for the line's second 16-channel half)
+    auto swz = [](int row) { return (row >> 1) & 7; };
+    // halves offset, inside a packed line, of logical chunk L
     auto lofs = [&](int L) -> long {
         if constexpr (STEM) return (L >> 2) * a.plane + (L & 3) * 8;
-        else if constexpr (KH == 2) return L * 8;
-        else return (L < 2 ? L : L + 2) * 8;
+        else return L * 8;
     };
 
     // ---- DMA source bookkeeping (rows this lane feeds) ----
@@ -528,25 +608,23 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
 
     // staging state of the next K-step to issue (wave-uniform, advanced per issue)
     // (a stream-K segment starts at K-step ks: channel group outer, tap inner)
-    int q_half = KH == 1 ? ks & 1 : 0, q_buf = 0;
-    int q_cc = (KH == 1 ? ks >> 1 : ks) / a.RS;
-    int q_tap = (KH == 1 ? ks >> 1 : ks) - q_cc * a.RS;
+    int q_buf = 0;
+    int q_cc = ks / a.RS;
+    int q_tap = ks - q_cc * a.RS;
     int q_rr = q_tap / a.S, q_ss = q_tap - q_rr * a.S;
     auto issue_next = [&]() {
         char* st = smem + q_buf * STAGE;
         const int dh = q_rr * a.dil, dw = q_ss * a.dil;
-        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64 + q_half * 16;
+        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64;
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
             const bool in = (unsigned)(a_hb[i] + dh) < (unsigned)a.H && (unsigned)(a_wb[i] + dw) < (unsigned)a.W;
             glds16(in ? a_p[i] + toff : zero, st + (RPI * (w * GA + i)) * ROW);
         }
-        const long boff = (long)(q_tap * a.cch + q_cc) * 64 + q_half * 16;
+        const long boff = (long)(q_tap * a.cch + q_cc) * 64;
 #pragma unroll
         for (int j = 0; j < GB; ++j) glds16(b_src[j] + boff, st + b_dst[j]);
         q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
-        if (KH == 1 && ++q_half < 2) return;       // the line's second 16-channel half, same tap
-        q_half = 0;
         if (++q_ss == a.S) {
             q_ss = 0;
             ++q_rr;
@@ -559,10 +637,10 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL>(a, smem, tile, nks, partial, m0, n0, wm, wn, lane, tid, issue_next);
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P>(a, smem, tile, nks, partial, m0, n0, wm, wn, lane, tid,
+                                                 issue_next);
         return;
-    }
-
+    } else {
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -572,13 +650,13 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     // fragment reads: lane reads row (lane&31) of each 32-row tile; logical chunk
-    // hi: KH*u... (u = k16 slice within the stage), lo: the same + CPR/2
+    // of k16 slice u (of 2 per row half): 2u + kh (first half) / 4 + 2u + kh
     const int frow = lane & 31, kh = lane >> 5;
-    int foff[2][KH];
+    int foff[2][2];
 #pragma unroll
     for (int pl = 0; pl < 2; ++pl)
 #pragma unroll
-        for (int u = 0; u < KH; ++u) foff[pl][u] = frow * ROW + ((((CPR / 2) * pl + 2 * u + kh) ^ swz(frow)) << 4);
+        for (int u = 0; u < 2; ++u) foff[pl][u] = frow * ROW + ((((CPR / 2) * pl + 2 * u + kh) ^ swz(frow)) << 4);
     const int a_base = (wm * TM * 32) * ROW, b_base = (BM + wn * TN * 32) * ROW;
 
     struct Frag {
@@ -596,46 +674,24 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             f.bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][u]);
         }
     };
-    // ORD 0: the three products of one tile back to back; ORD 1: product-major
-    // (consecutive MFMAs accumulate into different tiles)
-    auto mma = [&](const Frag& f) {
-        if constexpr (ORD != 1) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
-                }
-            return;
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
+    auto mfma = [](const f16x8& x, const f16x8& y, const f32x16& c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_f16(x, y, c, 0, 0, 0);
     };
-    constexpr int NR = 2 * (TM + TN), NM = 3 * TM * TN;   // ds_reads / MFMAs per k16 slice
+    auto mma = [&](const Frag& f) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) x3_products<P>(acc[i][j], f.ah[i], f.al[i], f.bh[j], f.bl[j], mfma);
+    };
+    constexpr int NR = 2 * (TM + TN), NM = (P == 3 ? 3 : 2) * TM * TN;   // ds_reads / MFMAs per k16 slice
 
     // prologue: NST-1 stages in flight, stage 0 landed everywhere
     issue_next();
-    for (int s = 1; s < (WIDE2 ? 2 : NST - 1); ++s)
+    for (int s = 1; s < NST - 1; ++s)
         if (s < nks) issue_next();
     {
-        const int after = std::min(nks - 1, WIDE2 ? 1 : NST - 2);   // stages issued after stage 0
-        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        const int after = std::min(nks - 1, NST - 2);   // stages issued after stage 0
+        if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();
@@ -648,168 +704,37 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     // fragment reads of the buffer the next DMA will overwrite
     auto wait_next = [&](int t) {
         const int after = std::min(nks - 1, t + NST - 1) - (t + 1);
-        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * GL) : "memory");
-        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+        if (after >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
         else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     };
 
-    if constexpr (WIDE2) {
-        // 256x256 tile, two k16 halves per 32-channel stage, 48 MFMAs per wave per
-        // barrier, 2-stage ring:
-        //   [MFMAs u=0 of t | read u=1 frags of t]  wait own DMA of t+1, barrier
-        //   [issue DMA t+2 into t's buffer (fully read before the barrier)]
-        //   [MFMAs u=1 of t | read u=0 frags of t+1]
-        // A fragments double-buffered, B refilled in place after each column.
-        struct FA {
-            f16x8 h[TM], l[TM];
-        };
-        f16x8 bh[TN], bl[TN];
-        auto read_a = [&](FA& f, const char* st, int u) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                f.h[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][u]);
-                f.l[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][u]);
-            }
-        };
-        auto read_b = [&](int j, const char* st, int u) {
-            bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][u]);
-            bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][u]);
-        };
-        auto mma_col = [&](const FA& f, int j) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-        };
-        auto half = [&](const FA& fc, FA& fn, const char* st, int u) {   // MFMAs on fc/B, read fn/B from (st, u)
-            read_a(fn, st, u);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                mma_col(fc, j);
-                read_b(j, st, u);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM, 0);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        FA fa0, fa1;
-        read_a(fa0, smem, 0);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) read_b(j, smem, 0);
-        for (int t = 0; t + 1 < nks; ++t) {
-            const char* st = smem + cur * STAGE;
-            half(fa0, fa1, st, 1);
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            if (t + 2 < nks) issue_next();        // into t's buffer: every read of it retired above
-            cur ^= 1;
-            half(fa1, fa0, smem + cur * STAGE, 0);
-        }
-        half(fa0, fa1, smem + cur * STAGE, 1);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mma_col(fa1, j);
-    } else if constexpr (KH == 2) {
-        // one barrier per K-step, placed between its two k16 halves:
-        //   [issue DMA t+2] [read frags u=1 of t] [MFMA u=0 of t]
-        //   wait own DMA of t+1, barrier (t+1 landed everywhere; t-1 fully read)
-        //   [read frags u=0 of t+1] [MFMA u=1 of t]
-        // DMA t+2 overwrites the buffer of t-1, whose reads retired before the
-        // previous barrier.  Each half is one basic block so the ds_reads can be
-        // interleaved one per MFMA gap.
-        // the last K-step is peeled so the loop body has no branch around the
-        // MFMAs (a join of two differently scheduled acc writers costs a full
-        // accumulator copy)
-        for (int t = 0; t + 1 < nks; ++t) {
-            const char* st = smem + cur * STAGE;
-            if (t + NST - 1 < nks) issue_next();
-            read_frag(f1, st, 1);
-            mma(f0);
-            interleave<NM, NR>();
-            __builtin_amdgcn_sched_barrier(0);       // every MFMA of this half ahead of the wait
-            wait_next(t);
-            lds_barrier();
-            cur = cur == NST - 1 ? 0 : cur + 1;
-            mma(f1);
-            read_frag(f0, smem + cur * STAGE, 0);
-            interleave<NM, NR>();
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        read_frag(f1, smem + cur * STAGE, 1);
+    // one barrier per K-step, placed between its two k16 halves:
+    //   [issue DMA t+NST-1] [read frags u=1 of t] [MFMA u=0 of t]
+    //   wait own DMA of t+1, barrier (t+1 landed everywhere; t-1 fully read)
+    //   [read frags u=0 of t+1] [MFMA u=1 of t]
+    // DMA t+NST-1 overwrites the buffer of t-1, whose reads retired before the
+    // previous barrier.  Each half is one basic block so the ds_reads can be
+    // interleaved one per MFMA gap.  The last K-step is peeled so the loop body
+    // has no branch around the MFMAs (a join of two differently scheduled acc
+    // writers costs a full accumulator copy).
+    for (int t = 0; t + 1 < nks; ++t) {
+        const char* st = smem + cur * STAGE;
+        if (t + NST - 1 < nks) issue_next();
+        read_frag(f1, st, 1);
         mma(f0);
+        interleave<NM, NR>();
+        __builtin_amdgcn_sched_barrier(0);       // every MFMA of this half ahead of the wait
+        wait_next(t);
+        lds_barrier();
+        cur = cur == NST - 1 ? 0 : cur + 1;
         mma(f1);
-    } else {
-        // one k16 slice per stage:
-        //   [issue DMA t+3] wait own DMA of t+1, barrier (t+1 landed; t-1 fully read)
-        //   [read A frags of t+1] then per column block j: [MFMAs of t with B_j]
-        //   [refill B_j with t+1's]
-        // DMA t+3 overwrites the buffer of t-1, whose reads retired before the
-        // previous barrier.  Only the A fragments are double-buffered (unrolled by
-        // two so they stay in named registers); each B fragment is refilled in
-        // place right after its last MFMA of the step.
-        struct FA {
-            f16x8 h[TM], l[TM];
-        };
-        f16x8 bh[TN], bl[TN];
-        auto read_a = [&](FA& f, const char* st) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                f.h[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][0]);
-                f.l[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][0]);
-            }
-        };
-        auto read_b = [&](int j, const char* st) {
-            bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][0]);
-            bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][0]);
-        };
-        auto mma_col = [&](const FA& f, int j) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
-            }
-        };
-        FA fa0, fa1;
-        read_a(fa0, smem);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) read_b(j, smem);
-        auto step = [&](int t, FA& fc, FA& fn) {     // a K-step followed by another
-            if (t + NST - 1 < nks) issue_next();
-            wait_next(t);
-            lds_barrier();
-            cur = cur == NST - 1 ? 0 : cur + 1;
-            const char* st = smem + cur * STAGE;
-            read_a(fn, st);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                mma_col(fc, j);
-                read_b(j, st);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM, 0);      // next A frags
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);  // column j's MFMAs
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        // pairs of full steps, then the peeled last pair; nks is even here (two
-        // 16-channel halves per tap), so nothing branches around the MFMAs
-        int t = 0;
-        for (; t + 2 < nks; t += 2) {
-            step(t, fa0, fa1);
-            step(t + 1, fa1, fa0);
-        }
-        step(t, fa0, fa1);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mma_col(fa1, j);
+        read_frag(f0, smem + cur * STAGE, 0);
+        interleave<NM, NR>();
+        __builtin_amdgcn_sched_barrier(0);
     }
+    read_frag(f1, smem + cur * STAGE, 1);
+    mma(f0);
+    mma(f1);
 
     if (!STEM && partial) {                // stream-K: fold the tile's segments
         auto get = [&](int v) -> f32x4 {
@@ -825,9 +750,37 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         if (!sk_combine<TM * TN * 4>(a, tile, tid, smem, get, set)) return;
     }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
+    const int rbase = m0 + wm * TM * 32 + 4 * kh;
+    if constexpr (P == 1) {                // fp16 output: scale, partials, LDS-staged store
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const float sc = (a.wscale ? a.wscale[n0 + wn * TN * 32 + j * 32 + frow] : 1.f) * ginv;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] *= sc;
+        }
+        if (a.part)
+            x3_bn_partials<BN, TM, TN, 16, 32, 32>(
+                a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
+                [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); });
+        __syncthreads();
+        _Float16* t = (_Float16*)smem;
+        constexpr int PITCH = BN + 8;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    t[(wm * TM * 32 + i * 32 + 4 * kh + (r & 3) + 8 * (r >> 2)) * PITCH + wn * TN * 32 + j * 32 +
+                      frow] = (_Float16)acc[i][j][r];
+        __syncthreads();
+        x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
+        return;
+    }
 
     // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
-    const int rbase = m0 + wm * TM * 32 + 4 * kh;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
         const int n = n0 + wn * TN * 32 + j * 32 + frow;
@@ -845,312 +798,36 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 acc[i][j][r] *= sc;
-                if (off[r] >= 0) a.y[off[r]] = a.add ? acc[i][j][r] + av[r] : acc[i][j][r];
+                x3_store(a, off[r], acc[i][j][r], av[r]);
             }
         }
     }
     if (a.part == nullptr) return;
-    __syncthreads();                       // every wave done reading the ring
-    float* red = (float*)smem;             // [WM][BN] column sums, then [2][BN] half-tile means
-    float* tmean = red + WM * BN;
-    float colsum[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                s += (m < a.M) ? acc[i][j][r] : 0.f;
-            }
-        s += __shfl_xor(s, 32);
-        colsum[j] = s;
-    }
-    if (lane < 32) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) red[wm * BN + wn * TN * 32 + j * 32 + lane] = colsum[j];
-    }
-    __syncthreads();
-    const long tile128 = (long)(m0 >> 7);
-    for (int e = tid; e < 2 * BN; e += 512) {
-        const int h = e / BN, c = e - h * BN;
-        const int cnt = min(128, a.M - (m0 + 128 * h));
-        if (cnt > 0) {
-            const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
-            tmean[h * BN + c] = s / (float)cnt;
-            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
-        }
-    }
-    __syncthreads();
-    const float* mu_h = tmean + (wm >> 1) * BN;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const float mu = mu_h[wn * TN * 32 + j * 32 + frow];
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                const float d = acc[i][j][r] - mu;
-                q += (m < a.M) ? d * d : 0.f;
-            }
-        q += __shfl_xor(q, 32);
-        colsum[j] = q;
-    }
-    __syncthreads();
-    if (lane < 32) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) red[wm * BN + wn * TN * 32 + j * 32 + lane] = colsum[j];
-    }
-    __syncthreads();
-    for (int e = tid; e < 2 * BN; e += 512) {
-        const int h = e / BN, c = e - h * BN;
-        if (a.M - (m0 + 128 * h) > 0)
-            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+    x3_bn_partials<BN, TM, TN, 16, 32, 32>(
+        a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
+        [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); });
     }
 }
 
-// ---------------------------------------------------------------------------
-// 256x256 tile with FOUR waves (one per SIMD, 2x2, 128x128 each): accumulators
-// 256 fp32 per lane (the AGPR half of the 512-entry register file a lone wave
-// owns), fragments double-buffered per k16 half in VGPRs.  Same LDS ring,
-// staging, swizzle and half-K-step schedule as the 8-wave WIDE2 body; per SIMD
-// the same MFMAs per barrier, a third fewer LDS fragment reads (each wave reads
-// A and B for 128x128 instead of 64x128) and 4 instead of 8 waves to align at
-// each barrier.  Forward / stride-1 dgrad (not the stem, no stream-K).
-// Opt-in (knob 40 / 43): measured 8 % SLOWER than the 8-wave body on C2 layer4
-// (1090 vs 1185 TF/s issued, same box) — a lone wave cannot cover its own
-// ds_read -> MFMA and barrier latencies; kept, parity-tested, as the base for a
-// 16x16x32-MFMA body (which needs the register room only a lone wave has).
-__device__ __forceinline__ void conv_x3_w4_tile(const X3Args& a, char* smem, int tile) {
-    constexpr int BM = 256, BN = 256, WM = 2, WN = 2, NWV = 4, NT = 256;
-    constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);   // 4 x 4 32x32 tiles per wave
-    constexpr int ROW = 128, CPR = 8, RPI = 8;               // 32-channel stages
-    constexpr int STAGE = (BM + BN) * ROW;
-    constexpr int GA = BM / RPI / NWV, GB = BN / RPI / NWV;   // DMA instructions per wave per stage
-    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w / WN, wn = w % WN;
-    auto swz = [](int row) { return (row >> 1) & 7; };
-
-    // per DMA row: receptive-field origin (hb, wb) packed as two int16 and the
-    // signed 32-bit element offset of that origin pixel (negative where the
-    // origin lies in the padding; the host checks the operand sizes fit): 2 VGPRs
-    // per row instead of 4 — the lone wave's VGPR half is tight
-    const int cstride = a.cch * 64;
-    int a_org[GA], a_off[GA];
-#pragma unroll
-    for (int i = 0; i < GA; ++i) {
-        const int row = RPI * (w * GA + i) + lane / CPR;
-        const int L = ((lane % CPR) ^ swz(row)) * 8;
-        const int m = m0 + row;
-        int hb = -16384, wb = -16384;
-        long off = 0;
-        if (m < a.M) {
-            const int hw = a.Ho * a.Wo;
-            const int n = m / hw, rem = m - n * hw;
-            const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-            hb = ho * a.stride - a.pad;
-            wb = wo * a.stride - a.pad;
-            off = (((long)n * a.H + hb) * a.W + wb) * cstride + L;
-        }
-        a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
-        a_off[i] = (int)off;
-    }
-    const int bline = a.RS * a.cch * 64;
-    unsigned b_off[GB];
-#pragma unroll
-    for (int j = 0; j < GB; ++j) {
-        const int row = RPI * (w * GB + j) + lane / CPR;
-        b_off[j] = (unsigned)((n0 + row) * bline + ((lane % CPR) ^ swz(row)) * 8);
-    }
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
-    const int nks = a.nks;
-    int q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_buf = 0;
-    auto issue_next = [&]() {
-        char* st = smem + q_buf * STAGE;
-        const int dh = q_rr * a.dil, dw = q_ss * a.dil;
-        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64;
-#pragma unroll
-        for (int i = 0; i < GA; ++i) {
-            const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
-            const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-            glds16(in ? a.xs + ((long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
-        }
-        const unsigned boff = (unsigned)((q_tap * a.cch + q_cc) * 64);
-#pragma unroll
-        for (int j = 0; j < GB; ++j) glds16(a.ws + (b_off[j] + boff), st + (BM + RPI * (w * GB + j)) * ROW);
-        q_buf ^= 1;
-        if (++q_ss == a.S) {
-            q_ss = 0;
-            ++q_rr;
-        }
-        if (++q_tap == a.RS) {
-            q_tap = 0;
-            q_rr = 0;
-            ++q_cc;
-        }
-    };
-
-    f32x16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    const int frow = lane & 31, kh = lane >> 5;
-    int foff[2][2];
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) foff[pl][u] = frow * ROW + ((((CPR / 2) * pl + 2 * u + kh) ^ swz(frow)) << 4);
-    const int a_base = (wm * TM * 32) * ROW, b_base = (BM + wn * TN * 32) * ROW;
-
-    issue_next();
-    if (1 < nks) issue_next();
-    if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA + GB) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-
-    struct FA {
-        f16x8 h[TM], l[TM];
-    };
-    f16x8 bh[TN], bl[TN];
-    auto read_a = [&](FA& f, const char* st, int u) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            f.h[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[0][u]);
-            f.l[i] = *(const f16x8*)(st + a_base + i * 32 * ROW + foff[1][u]);
-        }
-    };
-    auto read_b = [&](int j, const char* st, int u) {
-        bh[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[0][u]);
-        bl[j] = *(const f16x8*)(st + b_base + j * 32 * ROW + foff[1][u]);
-    };
-    auto mma_col = [&](const FA& f, int j) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.h[i], bl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.l[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    };
-    auto half = [&](const FA& fc, FA& fn, const char* st, int u) {   // MFMAs on fc/B, read fn/B from (st, u)
-        read_a(fn, st, u);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            mma_col(fc, j);
-            read_b(j, st, u);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * TM, 0);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 3 * TM, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    FA fa0, fa1;
-    int cur = 0;
-    read_a(fa0, smem, 0);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) read_b(j, smem, 0);
-    for (int t = 0; t + 1 < nks; ++t) {
-        const char* st = smem + cur * STAGE;
-        half(fa0, fa1, st, 1);
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        lds_barrier();
-        if (t + 2 < nks) issue_next();        // into t's buffer: every read of it retired above
-        cur ^= 1;
-        half(fa1, fa0, smem + cur * STAGE, 0);
-    }
-    half(fa0, fa1, smem + cur * STAGE, 1);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) mma_col(fa1, j);
-
-    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
-    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile
-    // (wave row wm owns 128-row tile half wm) ----
-    const int rbase = m0 + wm * TM * 32 + 4 * kh;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        const int n = n0 + wn * TN * 32 + j * 32 + frow;
-        const float sc = (a.wscale ? a.wscale[n] : 1.f) * ginv;
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            long off[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) off[r] = x3_out_off(a, rbase + i * 32 + (r & 3) + 8 * (r >> 2), n);
-            float av[16];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) av[r] = (a.add && off[r] >= 0) ? a.add[off[r]] : 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                acc[i][j][r] *= sc;
-                if (off[r] >= 0) a.y[off[r]] = a.add ? acc[i][j][r] + av[r] : acc[i][j][r];
-            }
-        }
-    }
-    if (a.part == nullptr) return;
-    const long tile128 = (long)(m0 >> 7) + wm;
-    const int cnt = min(128, a.M - (m0 + 128 * wm));
-    if (cnt <= 0) return;                  // wave-uniform; no barrier below
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                s += (m < a.M) ? acc[i][j][r] : 0.f;
-            }
-        s += __shfl_xor(s, 32);
-        const float mu = s / (float)cnt;
-        float q = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                const float d = acc[i][j][r] - mu;
-                q += (m < a.M) ? d * d : 0.f;
-            }
-        q += __shfl_xor(q, 32);
-        if (lane < 32) {
-            const int c = n0 + wn * TN * 32 + j * 32 + lane;
-            a.part[(tile128 * a.K + c) * 2 + 0] = s;
-            a.part[(tile128 * a.K + c) * 2 + 1] = q;
-        }
-    }
+// the ring, or (P = 1) the staged fp16 output tile if that is larger (256x256: 132 KiB)
+constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
+    return P == 1 && 256 * (BN + 8) * 2 > x3_nst(BN, PAIR) * (256 + BN) * 128 ? 256 * (BN + 8) * 2
+                                                                              : x3_nst(BN, PAIR) * (256 + BN) * 128;
 }
-
-__global__ __launch_bounds__(256, 1) void conv_x3_w4_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[2 * 512 * 128];
-    conv_x3_w4_tile(a, smem, xcd_remap(blockIdx.x, gridDim.x));
-}
-
-constexpr int x3_lds_bytes(int BN, int KH, int ORD) { return x3_nst(BN, KH, ORD) * (256 + BN) * 64 * KH; }
 
 // One tile per block (blocks remapped XCD-aware), or (SK) column-grouped
 // stream-K: group g runs units [g*U/NG, (g+1)*U/NG) of the m-tile-major
 // (m-tile, K-step) sequence, one tile segment after another (sk_combine).
 // Separate instantiations (SK): the stream-K loop's live state would otherwise
-// raise the register allocation of the one-tile kernels (256x256 spilled).
-// ORD 3 = two blocks per CU (256x64 tiles with 16-channel stages, 80 KiB each):
-// one block's prologue / epilogue overlaps the other's main loop.
-template <int BN, int KH, bool STEM = false, int ORD = 0, int MFD = 32, bool SK = false>
-__global__ __launch_bounds__(512, ORD == 3 ? 2 : 1) void conv_x3_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, KH, ORD)];
+// raise the register allocation of the one-tile kernels.  PAIR = two blocks per
+// CU (256x64 tiles, the stem: 80 KiB each): one block's prologue / epilogue
+// overlaps the other's main loop.
+template <int BN, bool STEM, bool PAIR, int MFD, bool SK, int P>
+__global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, PAIR, P)];
     const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
     if constexpr (!SK) {
-        conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, b, 0, a.nks, false);
+        conv_x3_tile<BN, STEM, PAIR, MFD, P>(a, smem, b, 0, a.nks, false);
         return;
     }
     // column-grouped stream-K (sk_combine): group g = b / n_tiles, column tile b % n_tiles
@@ -1162,10 +839,11 @@ __global__ __launch_bounds__(512, ORD == 3 ? 2 : 1) void conv_x3_kernel(X3Args a
         const long t0 = (long)mt * a.nks;
         const int ks = (int)(u - t0), ke = (int)min((long)a.nks, u1 - t0);
         if (u != u0) __syncthreads();      // the previous segment is done with the LDS ring
-        conv_x3_tile<BN, KH, STEM, ORD, MFD>(a, smem, mt * NT + nt, ks, ke - ks, ks != 0 || ke != a.nks);
+        conv_x3_tile<BN, STEM, PAIR, MFD, P>(a, smem, mt * NT + nt, ks, ke - ks, ks != 0 || ke != a.nks);
         u = t0 + ke;
     }
 }
+
 
 // ---------------------------------------------------------------------------
 // operand packing
@@ -1203,6 +881,17 @@ __global__ __launch_bounds__(256) void weight_pack_x3_kernel(int rsc, const floa
         const long e = (long)k * rsc + i;
         split_store(row[i] * sc, ws + 2 * e - (e & 31));
     }
+    if (threadIdx.x == 0) wscale[k] = 1.f / sc;
+}
+
+// w[k][tap][c] fp32 (KRSC) * 2^e_k → fp16 KRSC (the plain-fp16 conv's operand:
+// 64-channel 128-B lines); one block per k, wscale[k] = 2^-e_k
+__global__ __launch_bounds__(256) void weight_pack_f16_kernel(int rsc, const float* __restrict__ w,
+                                                             _Float16* __restrict__ out, float* __restrict__ wscale) {
+    const int k = blockIdx.x;
+    const float* row = w + (long)k * rsc;
+    const float sc = pow2_scale_of(block_absmax(rsc, [&](int i) { return row[i]; }));
+    for (int i = threadIdx.x; i < rsc; i += blockDim.x) out[(long)k * rsc + i] = (_Float16)(row[i] * sc);
     if (threadIdx.x == 0) wscale[k] = 1.f / sc;
 }
 
@@ -1288,11 +977,11 @@ __device__ __forceinline__ f16x8 cat_tr(s16x4 lo, s16x4 hi) {
 // 64 (KA 128) — the 256x128 body is bound by operand delivery, not the MFMAs
 // (MFMA-busy scales with the intensity: 0.25 at KA 64, 0.42 at KA 128).  Its
 // stage holds PX = 16 pixels (one MFMA k-slice) so three stages fit in 96 KB.
-template <int KA, int NS = 3>
+template <int KA>
 __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
+    constexpr int NS = 3;                                   // LDS ring depth
     constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
     constexpr int PX = KA == 256 ? 16 : 32;                  // pixels per stage
-    static_assert(NS == 3 || (NS == 4 && PX == 16), "4-stage ring only for 16-pixel stages");
     constexpr int ROW = 128, STAGE = (GX + GD) * PX * ROW;
     constexpr int NX = PX / 8, ND = GD * PX / 64, GL = NX + ND;
     constexpr int TM = KA / 64, TN = 2;
@@ -1585,205 +1274,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
         }
 }
 
-// The same weight gradient with v_mfma_f32_16x16x32_f16 (one k32 MFMA per 16x16
-// block and product per 32-pixel K-step; the lower-power shape holds a higher
-// clock).  A 16x16x32 operand lane holds 8 consecutive pixels of one channel for
-// pixel block (lane >> 4): the four 16-lane groups read rows 8G.. of the same 16
-// channels, so rows r and r+8 would share banks — the staging adds a second
-// swizzle bit (chunk ^= ((pixel >> 3) & 1) << 1) on top of the 32x32 kernel's.
-// Pipeline (3-stage ring): issue DMA t+2, wait own DMA of t+1 + this wave's
-// reads, barrier, [read t+1's fragments | MFMAs of t].
-template <int KA>
-__global__ __launch_bounds__(512, 1) void wgrad_x3_mf16_kernel(WgX3Args a) {
-    constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
-    constexpr int ROW = 128, STAGE = (GX + GD) * 32 * ROW;
-    constexpr int NX = 4, ND = GD / 2, GL = NX + ND;
-    constexpr int TM = KA / 64, TN = 2;               // 32-row / 32-column groups per wave
-    constexpr int UM = 2 * TM, UN = 2 * TN;           // 16x16 blocks per wave
-    static_assert(ND >= 1, "KA must be 64 or 128");
-    __shared__ __attribute__((aligned(1024))) char smem[3 * STAGE];
-
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
-    const int split = bid / a.tiles, tile = bid - split * a.tiles;
-    const int kt = tile / a.r_tiles, rt = tile - kt * a.r_tiles;
-    const int k0 = kt * KA, r0 = rt * BR;
-    const int p_begin = split * a.mps;
-    const int p_end = min(a.M, p_begin + a.mps);
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-
-    // ---- staging (as wgrad_x3_kernel, plus the pixel-bit-3 swizzle) ----
-    const int Lx = ((lane & 7) ^ (((lane >> 4) & 1) << 2)) * 8;
-    const int Lx8 = Lx ^ 16;                                      // pixel bit 3 set: chunk ^ 2
-    const int mg = r0 + 32 * w;
-    const bool gvalid = mg < a.RSC;
-    const int tap = gvalid ? mg / a.C : 0;
-    const int cg = gvalid ? (mg - tap * a.C) >> 5 : 0;
-    const int rr = tap / a.S, ss = tap - rr * a.S;
-    const int dh = rr * a.dil - a.pad, dw = ss * a.dil - a.pad;
-    const int xstride = a.C * 2, dstride = a.K * 2;
-    const _Float16* xg0 = a.xs + cg * 64 + Lx;
-    const _Float16* xg1 = a.xs + cg * 64 + Lx8;
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
-    int xn[NX], xho[NX], xwo[NX];
-    const int hw = a.Ho * a.Wo;
-#pragma unroll
-    for (int i = 0; i < NX; ++i) {
-        const int p = p_begin + 8 * i + (lane >> 3);
-        xn[i] = p / hw;
-        const int rem = p - xn[i] * hw;
-        xho[i] = rem / a.Wo;
-        xwo[i] = rem - xho[i] * a.Wo;
-    }
-    const _Float16* dg[ND];
-    int dpp[ND];
-#pragma unroll
-    for (int j = 0; j < ND; ++j) {
-        const int line = 8 * (w * ND + j) + (lane >> 3);
-        dpp[j] = line & 31;
-        dg[j] = a.dys + (k0 >> 5) * 64 + (line >> 5) * 64 + (((w * ND + j) & 1) ? Lx8 : Lx);
-    }
-    auto issue = [&](int t) {
-        char* st = smem + (t % 3) * STAGE;
-        const int pb = p_begin + 32 * t;
-#pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            const int p = pb + 8 * i + (lane >> 3);
-            const int hi = xho[i] * a.stride + dh, wi = xwo[i] * a.stride + dw;
-            const bool in = gvalid && p < p_end && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-            const long pix = ((long)xn[i] * a.H + hi) * a.W + wi;
-            glds16(in ? ((i & 1) ? xg1 : xg0) + pix * xstride : zero, st + (w * 32 + 8 * i) * ROW);
-            xwo[i] += 32;
-            while (xwo[i] >= a.Wo) {
-                xwo[i] -= a.Wo;
-                if (++xho[i] == a.Ho) {
-                    xho[i] = 0;
-                    ++xn[i];
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < ND; ++j) {
-            const int p = pb + dpp[j];
-            glds16(p < p_end ? dg[j] + (long)p * dstride : zero, st + (GX * 32 + 8 * (w * ND + j)) * ROW);
-        }
-    };
-
-    f32x4 acc[UM][UN];
-#pragma unroll
-    for (int i = 0; i < UM; ++i)
-#pragma unroll
-        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // transposed reads: 16-lane group G reads pixel rows 8G+q (and +4) of 16
-    // channels (block c16); lane 4q+p supplies row q, channels 4p..4p+3
-    const int wk = w & 1, wr = w >> 1;
-    const int G = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
-    const unsigned lds0 = lds_addr_of(smem);
-    unsigned tbase[2][2];                          // [plane][c16]: per-lane byte offset in a 32-line group
-#pragma unroll
-    for (int pl = 0; pl < 2; ++pl)
-#pragma unroll
-        for (int c16 = 0; c16 < 2; ++c16)
-            tbase[pl][c16] = (8 * G + q) * ROW +
-                             (((4 * pl + 2 * c16 + (pq >> 1)) ^ (((q >> 1) & 1) << 2) ^ ((G & 1) << 1)) << 4) +
-                             8 * (pq & 1);
-    const unsigned a_line = lds0 + (GX + wk * TM) * 32 * ROW;   // dy groups of this wave
-    const unsigned b_line = lds0 + (wr * TN) * 32 * ROW;        // x groups of this wave
-    // dy (A) fragments double-buffered; x (B) fragments refilled in place after
-    // their column's MFMAs (the conv's 16x16x32 body does the same)
-    struct FA {
-        f16x8 h[UM], l[UM];
-    };
-    f16x8 xh[UN], xl[UN];
-    auto read_a = [&](FA& f, int buf) {
-        const unsigned so = buf * STAGE;
-#pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            const unsigned g0 = a_line + so + (i >> 1) * 32 * ROW;
-            f.h[i] = cat_tr(ds_tr16<0>(g0 + tbase[0][i & 1]), ds_tr16<4 * ROW>(g0 + tbase[0][i & 1]));
-            f.l[i] = cat_tr(ds_tr16<0>(g0 + tbase[1][i & 1]), ds_tr16<4 * ROW>(g0 + tbase[1][i & 1]));
-        }
-    };
-    auto read_b = [&](int j, int buf) {
-        const unsigned g0 = b_line + buf * STAGE + (j >> 1) * 32 * ROW;
-        xh[j] = cat_tr(ds_tr16<0>(g0 + tbase[0][j & 1]), ds_tr16<4 * ROW>(g0 + tbase[0][j & 1]));
-        xl[j] = cat_tr(ds_tr16<0>(g0 + tbase[1][j & 1]), ds_tr16<4 * ROW>(g0 + tbase[1][j & 1]));
-    };
-    auto mma_col = [&](const FA& f, int j) {
-#pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], xh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.h[i], xl[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(f.l[i], xh[j], acc[i][j], 0, 0, 0);
-        }
-    };
-    const int nsteps = p_end > p_begin ? (p_end - p_begin + 31) / 32 : 0;
-    if (nsteps > 0) {
-        int q_t = 0;
-        auto issue_next = [&]() { issue(q_t++); };
-        issue_next();
-        if (nsteps > 1) issue_next();
-        if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-        FA fa0, fa1;
-        int cur = 0;
-        read_a(fa0, 0);
-#pragma unroll
-        for (int j = 0; j < UN; ++j) read_b(j, 0);
-        // K-step t with fc and the B registers (t's), reading t+1's A into fn and
-        // t+1's B column by column
-        auto step = [&](int t, const FA& fc, FA& fn) {
-            if (t + 2 < nsteps) issue_next();
-            if (t + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            cur = cur == 2 ? 0 : cur + 1;
-            read_a(fn, cur);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                // the inline-asm reads of B_j(t) were waited for above; refill after use
-                mma_col(fc, j);
-                read_b(j, cur);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        int t = 0;
-        for (; t + 2 < nsteps; t += 2) {
-            step(t, fa0, fa1);
-            step(t + 1, fa1, fa0);
-        }
-        if (t + 1 < nsteps) {
-            step(t, fa0, fa1);
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) mma_col(fa1, j);
-        } else {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) mma_col(fa0, j);
-        }
-    }
-
-    const float inv = 1.f / pow2_scale_for(a.amax);
-    float* out = a.ws + (long)split * a.K * a.RSC;
-#pragma unroll
-    for (int i = 0; i < UM; ++i)
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            const int m = r0 + wr * 64 + j * 16 + (lane & 15);
-            if (m >= a.RSC) continue;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int k = k0 + wk * TM * 32 + i * 16 + 4 * G + r;
-                out[(long)k * a.RSC + m] = acc[i][j][r] * inv;
-            }
-        }
-}
 
 // dw[i] = sum_split ws[split][i], fixed order
 __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, const f32x4* __restrict__ ws,
@@ -1809,15 +1299,8 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
     }
 }
 
-// 16x16x32 wgrad body (A/B: HKP_WG_MF16=1)
-static const bool g_wg_mf16 = getenv("HKP_WG_MF16") && atoi(getenv("HKP_WG_MF16")) == 1;
-// 256x256 wgrad tile for Cout % 256 == 0 (HKP_WG_KA256=0: the 256x128 tile)
-static const bool g_wg_ka256 = !(getenv("HKP_WG_KA256") && atoi(getenv("HKP_WG_KA256")) == 0);
-// 4-stage ring (128 KB LDS) for the 256x256 wgrad tile (A/B: HKP_WG_NS4=1)
-static const bool g_wg_ns4 = getenv("HKP_WG_NS4") && atoi(getenv("HKP_WG_NS4")) == 1;
-
 static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, int* ka, int* r_tiles) {
-    *ka = d->k % 256 == 0 && g_wg_ka256 ? 256 : d->k % 128 == 0 ? 128 : 64;
+    *ka = d->k % 256 == 0 ? 256 : d->k % 128 == 0 ? 128 : 64;
     const long rsc = (long)d->r * d->s * d->c;
     *r_tiles = (int)((rsc + 255) / 256);
     const long tiles = (long)(d->k / *ka) * *r_tiles;
@@ -1843,6 +1326,7 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, in
     *splits = (int)((M + m - 1) / m);
     *mps = (int)m;
 }
+
 
 // Stem operand: the image → zero-padded NHWC4 planes [2][N][Hp][Wp][4] (hi, then
 // lo = f16(x-hi)); padded pixel (hp, wp) = input (hp-3, wp-3).  U8: the image is
@@ -1906,23 +1390,6 @@ static bool stem_x3_shape(const hkp_conv_desc* d) {
            d->stride == 2 && d->pad == 3 && d->dilation == 1 && d->k % 64 == 0;
 }
 
-// Tile policy (x3_tile_n): 256x256 (32-channel stages, 2-stage ring, 48 MFMAs
-// per wave per barrier), 256x128 or 256x64 (32-channel stages, 3-stage ring) by
-// rounds of blocks x tile cost.  Measured on C2 layer4 (Cout 512): 256x256 1.70 ms
-// vs 256x128 1.82 ms; on C2 layer3 (Cout 256, 600 m-tiles) 256x256 loses to round
-// quantisation (0.53 vs 0.47 ms); training layer3 (150 m-tiles) 256x256 wins
-// (0.15 vs 0.17 ms).
-// Tuning knob (hkp_set_conv_variant; results agree to fp32 summation order, in
-// practice bit-identical): 0 = policy, 1 = 256x128 32-ch stages only,
-// 2 = 256x128 16-ch stages (4-stage ring), 3 = 256x256 32-ch stages whenever
-// Cout % 256 == 0, 4 = 256x256 16-ch stages whenever Cout % 256 == 0, 5 = 256x64,
-// 6 = 16x16x32 MFMAs with 256x128 tiles (256x64 when Cout % 128), 7 = 16x16x32 256x64,
-// 8 = stream-K wherever a tile split helps (zero overhead assumed), 9 = never stream-K.
-static int g_x3_variant = [] {
-    const char* e = getenv("HKP_X3_VARIANT");
-    return e ? atoi(e) : 0;
-}();
-
 // Compute units (one 512-thread conv block per CU at a time); cached per process.
 static int x3_cus() {
     static int n = [] {
@@ -1944,15 +1411,10 @@ static long x3_sk_ws_bytes(int bn) { return X3_SK_CNT_BYTES + 2L * x3_cus() * bn
 // stream-K overhead per block in tile times: every block writes up to two
 // fp32 slabs and most reduce a tile from two (~0.4 MB per CU, all CUs at once),
 // plus a second pipeline fill — so it shrinks with the K depth nks of a tile.
-// Fitted to in-process A/Bs on the box (tools/conv_ab.py, knob 8 vs 9, column-
-// grouped stream-K): t4 nks 144 0.34, t3 / layer3 nks 72 0.46 / 0.48, t2 nks 36
-// 0.63, t1 / layer1 nks 18 1.18 / 1.46 tile-times: 0.2 + 19 / nks.
-// HKP_SK_OVER = a fixed value instead (tuning).
-static double g_sk_over_env = [] {
-    const char* e = getenv("HKP_SK_OVER");
-    return e ? atof(e) : -1.0;
-}();
-static double sk_over(int nks) { return g_sk_over_env >= 0 ? g_sk_over_env : 0.2 + 19.0 / nks; }
+// Fitted to in-process A/Bs on the box (column-grouped stream-K vs one tile per
+// block): t4 nks 144 0.34, t3 / layer3 nks 72 0.46 / 0.48, t2 nks 36 0.63,
+// t1 / layer1 nks 18 1.18 / 1.46 tile-times: 0.2 + 19 / nks.
+static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 
 // Tile width (and data-parallel vs stream-K) for Cout = k over m_tiles 256-row
 // tiles: data-parallel costs ceil(blocks / CUs) rounds of one tile each,
@@ -1961,8 +1423,10 @@ static double sk_over(int nks) { return g_sk_over_env >= 0 ? g_sk_over_env : 0.2
 // reuse each A line more).  E.g. C2 layer4 (600 m-tiles, Cout 512): 1200
 // 256x256 tiles = 4.69 rounds, data-parallel (5 rounds); training layer4 (150
 // m-tiles): 600 256x128 tiles stream-K (2.34 + 0.25 rounds) beats 3 rounds of
-// 256x128 (data-parallel's best).  No stream-K with 256x256 tiles: that
-// instantiation spills (the one-tile 256x256 kernel sits at 255 VGPRs).
+// 256x128 (data-parallel's best).  Measured on C2 layer4: 256x256 1.70 ms vs
+// 256x128 1.82 ms; on C2 layer3 (Cout 256, 600 m-tiles) 256x256 loses to round
+// quantisation (0.53 vs 0.47 ms).  No stream-K with 256x256 tiles (the one-tile
+// 256x256 kernel sits at 255 VGPRs; the stream-K loop would spill).
 struct X3Plan {
     int bn;
     bool sk;
@@ -1991,44 +1455,81 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
     }
     return best;
 }
-static const bool g_stem_mf16 = getenv("HKP_STEM_MF16") && atoi(getenv("HKP_STEM_MF16")) == 1;
-static double g_mf16_rounds = [] {
-    const char* e = getenv("HKP_MF16_ROUNDS");
-    return e ? atof(e) : 2.0;
-}();
-static int x3_tile_n(int k, long m_tiles, int nks) { return x3_plan(k, m_tiles, nks, true, sk_over(nks)).bn; }
 
-static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws = nullptr, int64_t ws_bytes = 0) {
-    const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
-    // stream-K needs the workspace; knob 9 = never, 8 = whenever a tile split helps
-    const bool sk_ok = ws && (v == 0 || v == 8) && ws_bytes >= x3_sk_ws_bytes(256);
+// The kernel a launch runs (conv_x3_kernel<bn, STEM, pair, mfd, sk, P>):
+//   256x256                 16x16x32 body, 2-stage ring (C2 layer4 1.79 -> 1.62 ms
+//                           vs the 32x32x16 body: same cycles per FLOP at lower
+//                           power, so the chip holds a higher clock —
+//                           MI355X_MICROARCH.md DVFS item 7)
+//   256x128, >= 2 rounds    16x16x32 body, 3-stage ring (C2 layer3 +6 %, layer2 +5 %)
+//   256x128, one round      32x32x16 body (the 16x16 body's longer fill lost 8-11 %)
+//   256x64                  16x16x32 body, two blocks per CU (layer1 0.223 -> 0.166 ms)
+//   stream-K 256x128 / 64   16x16x32 / 32x32x16 bodies (training t4 fwd +3-6 %, t3 +6 %)
+// hkp_conv_desc.tile (HKP_TILE_*) forces one of them — every body is reachable
+// for the parity tests; results agree to fp32 summation order.
+struct X3Choice {
+    int bn, mfd;
+    bool pair, sk;
+};
+static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy) {
+    switch (policy) {
+        case HKP_TILE_256:
+            if (k % 256 == 0) return {256, 16, false, false};
+            break;
+        case HKP_TILE_128_MF16:
+            if (k % 128 == 0) return {128, 16, false, false};
+            break;
+        case HKP_TILE_128_MF32:
+            if (k % 128 == 0) return {128, 32, false, false};
+            break;
+        case HKP_TILE_64_PAIR:
+            return {64, 16, true, false};
+        default:
+            break;
+    }
+    const bool sk = sk_ok && policy != HKP_TILE_NO_SK;
+    const X3Plan pl = x3_plan(k, m_tiles, nks, sk, policy == HKP_TILE_SK ? 0.0 : sk_over(nks));
+    if (pl.sk) return {pl.bn, pl.bn == 128 ? 16 : 32, false, true};
+    if (pl.bn == 256) return {256, 16, false, false};
+    if (pl.bn == 128) return {128, (double)m_tiles * (k / 128) >= 2.0 * x3_cus() ? 16 : 32, false, false};
+    return {64, 16, true, false};
+}
+
+static const X3Choice X3_STEM{64, 32, true, false};
+
+static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
+    return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
+                    c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
+}
+
+template <int P>
+static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Args& a) {
+    if (c.sk && c.bn == 128)
+        hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 16, true, P>), grid, dim3(512), 0, st, a);
+    else if (c.sk)
+        hipLaunchKernelGGL((conv_x3_kernel<64, false, false, 32, true, P>), grid, dim3(512), 0, st, a);
+    else if (c.bn == 256)
+        hipLaunchKernelGGL((conv_x3_kernel<256, false, false, 16, false, P>), grid, dim3(512), 0, st, a);
+    else if (c.bn == 128 && c.mfd == 16)
+        hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 16, false, P>), grid, dim3(512), 0, st, a);
+    else if (c.bn == 128)
+        hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 32, false, P>), grid, dim3(512), 0, st, a);
+    else
+        hipLaunchKernelGGL((conv_x3_kernel<64, false, true, 16, false, P>), grid, dim3(512), 0, st, a);
+}
+
+// a.RS, a.cch (128-B lines per pixel), a.M ... set by the caller; P = operand
+// layout (3 packed f16x3 split, 1 plain fp16)
+static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
+                      int64_t ws_bytes = 0) {
+    const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
-    const X3Plan pl = x3_plan(k, m_tiles, nks, sk_ok, v == 8 ? 0.0 : sk_over(nks));
-    int bn = pl.bn, kh = 2;
-    if (v == 1 || v == 2) bn = k % 128 == 0 ? 128 : 64;
-    if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
-    if (v == 5) bn = 64;
-    if ((v == 4 && bn == 256) || (v == 2 && bn == 128)) kh = 1;
-    // 16x16x32 MFMAs for 256x128 tiles on grids of >= HKP_MF16_ROUNDS (2) full
-    // rounds: the same cycles per FLOP at lower power, so the chip holds a higher
-    // clock (MI355X_MICROARCH.md DVFS item 7) — C2 layer3 +6 %, layer2 +5 %; on
-    // one-round grids the 16x16 body's longer fill loses (t3 -11 %, t2 -8 %)
-    // 256x256 tiles: the 16x16x32 body on the 2-stage ring always (C2 layer4
-    // 1.79 -> 1.62 ms; one-round grids equal); knob 60 = the 32x32x16 WIDE2 body
-    const bool mf16_pol = (v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
-                           (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus()) ||
-                          (bn == 256 && kh == 2 && !pl.sk && ord != 6 && ord != 4);
-    const bool mf16 = v == 6 || v == 7 || mf16_pol;
-    if (v == 6 || v == 7) bn = (v == 7 || k % 128) ? 64 : 128;
-    // 256x64 tiles run two blocks per CU: by default the 16x16x32 body on a 2-stage
-    // 32-channel ring (layer1 0.223 -> 0.166 ms, t1 0.065 -> 0.049); knob 80 = the
-    // 32x32x16 body on a 4-stage 16-channel ring, knob 20 = one block per CU
-    if (bn == 64 && ord == 8 && !pl.sk && !mf16) kh = 1;
-    a.n_tiles = k / bn;
-    a.nks = a.RS * a.cch * (kh == 1 ? 2 : 1);
+    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy);
+    a.n_tiles = k / c.bn;
+    a.nks = nks;
     a.sk_units = 0;
     dim3 grid((unsigned)(m_tiles * a.n_tiles));
-    if (pl.sk && bn == pl.bn && kh == 2 && !mf16) {
+    if (c.sk) {
         a.sk_units = m_tiles * a.nks;
         a.sk_cnt = (unsigned*)ws;
         a.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
@@ -2037,29 +1538,8 @@ static void launch_x3(int k, long m_tiles, hipStream_t st, X3Args& a, void* ws =
         const long ng = std::min<long>(x3_cus() / a.n_tiles, a.sk_units);
         grid = dim3((unsigned)(ng * a.n_tiles));
     }
-    // the 4-wave body keeps 32-bit element offsets: operands must fit
-    const bool w4_fits = (long)a.N * a.H * a.W * a.cch * 64 < (1L << 31) - (1L << 24) &&
-                         (long)k * a.RS * a.cch * 64 < (1L << 31) && a.H < 8192 && a.W < 8192;
-    if (mf16 && bn == 256)
-        hipLaunchKernelGGL((conv_x3_kernel<256, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
-    else if (ord == 4 && bn == 256 && kh == 2 && !mf16 && !a.sk_units && w4_fits)
-        hipLaunchKernelGGL(conv_x3_w4_kernel, grid, dim3(256), 0, st, a);
-    else if (a.sk_units && bn == 128 && ord == 7)     // knob 70: the 32x32x16 stream-K body
-        hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
-    else if (a.sk_units && bn == 128)                  // 16x16x32 (training t4 fwd +3-6 %, t3 +6 %)
-        hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16, true>), grid, dim3(512), 0, st, a);
-    else if (a.sk_units) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 32, true>), grid, dim3(512), 0, st, a);
-    else if (mf16 && bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
-    else if (mf16) hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 0, 16>), grid, dim3(512), 0, st, a);
-    else if (bn == 256 && kh == 2) hipLaunchKernelGGL((conv_x3_kernel<256, 2>), grid, dim3(512), 0, st, a);
-    else if (bn == 256) hipLaunchKernelGGL((conv_x3_kernel<256, 1>), grid, dim3(512), 0, st, a);
-    else if (bn == 128 && kh == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 1>), grid, dim3(512), 0, st, a);
-    else if (bn == 128 && ord == 1) hipLaunchKernelGGL((conv_x3_kernel<128, 2, false, 1>), grid, dim3(512), 0, st, a);
-    else if (bn == 128) hipLaunchKernelGGL((conv_x3_kernel<128, 2>), grid, dim3(512), 0, st, a);
-    else if (bn == 64 && kh == 2 && ord != 2 && ord != 8 && !mf16 && !a.sk_units)   // 16x16x32, two blocks per CU
-        hipLaunchKernelGGL((conv_x3_kernel<64, 2, false, 3, 16>), grid, dim3(512), 0, st, a);
-    else if (kh == 1) hipLaunchKernelGGL((conv_x3_kernel<64, 1, false, 3>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((conv_x3_kernel<64, 2>), grid, dim3(512), 0, st, a);
+    if (P == 3) launch_x3_p<3>(c, grid, st, a);
+    else launch_x3_p<1>(c, grid, st, a);
 }
 
 }  // namespace hkp
@@ -2076,29 +1556,65 @@ extern "C" int hkp_weight_pack_x3(int32_t k, int32_t rsc, int32_t c, const float
     return HKP_OK;
 }
 
+extern "C" int hkp_weight_pack_f16(int32_t k, int32_t rsc, const float* w, uint16_t* w_f16, float* w_inv_scale,
+                                   hkp_stream_t stream) {
+    HKP_CHECK_ARG(k > 0 && rsc > 0 && w && w_f16 && w_inv_scale, "hkp_weight_pack_f16: bad args");
+    hipLaunchKernelGGL(weight_pack_f16_kernel, dim3(k), dim3(256), 0, as_stream(stream), rsc, w, (_Float16*)w_f16,
+                       w_inv_scale);
+    HKP_LAUNCH_CHECK("hkp_weight_pack_f16");
+    return HKP_OK;
+}
+
 extern "C" int64_t hkp_conv_x3_sk_workspace_bytes(void) { return x3_sk_ws_bytes(256); }
+
+static int check_tile(const hkp_conv_desc* d, const char* who) {
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_64_PAIR, "%s: unknown tile policy %d", who,
+                  d->tile);
+    return HKP_OK;
+}
+
+// forward launch shared by the f16x3 (P 3) and plain-fp16 (P 1) entry points
+static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const uint16_t* ws, const float* wsc,
+                              float* y, uint16_t* y16, float* part, void* sk_ws, int64_t sk_bytes, int P,
+                              hkp_stream_t stream, const char* who) {
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    rc = check_tile(d, who);
+    if (rc) return rc;
+    HKP_CHECK_ARG(xs && ws && (P == 3 ? y != nullptr && y16 == nullptr : y == nullptr && y16 != nullptr),
+                  "%s: null tensor (P 3 writes fp32 y, P 1 fp16 y)", who);
+    HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "%s: NHWC only", who);
+    const int cg = P == 3 ? 32 : 64;
+    HKP_CHECK_ARG(d->c % cg == 0 && d->k % 64 == 0, "%s: need Cin%%%d==0, Cout%%64==0 (c=%d k=%d)", who, cg, d->c,
+                  d->k);
+    const long M = (long)d->n * ho * wo;
+    HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w * d->c < (1L << 40), "%s: too large", who);
+    X3Args a;
+    a.xs = (const _Float16*)xs; a.ws = (const _Float16*)ws; a.wscale = wsc;
+    a.y = y; a.y16 = (_Float16*)y16; a.part = part; a.amax = nullptr; a.add = nullptr; a.plane = 0;
+    a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
+    a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
+    a.M = (int)M; a.cch = d->c / cg; a.RS = d->r * d->s;
+    launch_x3(d->k, (M + 255) / 256, d->tile, P, as_stream(stream), a, sk_ws, sk_bytes);
+    HKP_LAUNCH_CHECK(who);
+    return HKP_OK;
+}
 
 extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
                                  const float* w_inv_scale, float* y, float* stat_partials, void* sk_workspace,
                                  int64_t sk_ws_bytes, hkp_stream_t stream) {
-    int ho, wo;
-    int rc = hkp_conv_out_hw(d, &ho, &wo);
-    if (rc) return rc;
-    HKP_CHECK_ARG(x_split && w_split && y, "hkp_conv2d_fwd_x3: null tensor");
-    HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "hkp_conv2d_fwd_x3: NHWC only");
-    HKP_CHECK_ARG(d->c % 32 == 0 && d->k % 64 == 0, "hkp_conv2d_fwd_x3: need Cin%%32==0, Cout%%64==0 (c=%d k=%d)",
-                  d->c, d->k);
-    const long M = (long)d->n * ho * wo;
-    HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w * d->c < (1L << 40), "hkp_conv2d_fwd_x3: too large");
-    X3Args a;
-    a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.wscale = w_inv_scale;
-    a.y = y; a.part = stat_partials; a.amax = nullptr; a.add = nullptr; a.plane = 0;
-    a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
-    a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
-    a.M = (int)M; a.cch = d->c / 32; a.RS = d->r * d->s;
-    launch_x3(d->k, (M + 255) / 256, as_stream(stream), a, sk_workspace, sk_ws_bytes);
-    HKP_LAUNCH_CHECK("hkp_conv2d_fwd_x3");
-    return HKP_OK;
+    HKP_CHECK_ARG(d && y, "hkp_conv2d_fwd_x3: null argument");
+    return conv_fwd_x3_common(d, x_split, w_split, w_inv_scale, y, nullptr, stat_partials, sk_workspace, sk_ws_bytes,
+                              3, stream, "hkp_conv2d_fwd_x3");
+}
+
+extern "C" int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
+                                  const float* w_inv_scale, uint16_t* y_f16, float* stat_partials,
+                                  void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && y_f16, "hkp_conv2d_fwd_f16: null argument");
+    return conv_fwd_x3_common(d, x_f16, w_f16, w_inv_scale, nullptr, y_f16, stat_partials, sk_workspace, sk_ws_bytes,
+                              1, stream, "hkp_conv2d_fwd_f16");
 }
 
 extern "C" int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits,
@@ -2142,7 +1658,7 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     a.N = d->n; a.H = ho; a.W = wo; a.C = d->k; a.K = d->c; a.R = d->r; a.S = d->s;
     a.stride = 1; a.pad = padp; a.dil = d->dilation; a.Ho = d->h; a.Wo = d->w;
     a.M = (int)M; a.cch = d->k / 32; a.RS = d->r * d->s;
-    launch_x3(d->c, (M + 255) / 256, as_stream(stream), a, sk_workspace, sk_ws_bytes);
+    launch_x3(d->c, (M + 255) / 256, d->tile, 3, as_stream(stream), a, sk_workspace, sk_ws_bytes);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3");
     return HKP_OK;
 }
@@ -2229,7 +1745,7 @@ extern "C" int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint
             // the column offset: the kernel applies one pad to both axes
             HKP_CHECK_ARG(omx == omy, "hkp_conv2d_bwd_data_x3_strided: row/column phase offsets differ (%d, %d)",
                           omy, omx);
-            launch_x3(d->c, ((long)a.M + 255) / 256, st, a, sk_workspace, sk_ws_bytes);
+            launch_x3(d->c, ((long)a.M + 255) / 256, d->tile, 3, st, a, sk_workspace, sk_ws_bytes);
             HKP_LAUNCH_CHECK("hkp_conv2d_bwd_data_x3_strided");
         }
     return HKP_OK;
@@ -2268,13 +1784,7 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     a.tiles = (d->k / ka) * rt;
     hipStream_t st = as_stream(stream);
     const unsigned grid = (unsigned)(a.tiles * sp);
-    // 16x16x32 wgrad body: opt-in (HKP_WG_MF16=1 or knob 90) — measured equal to
-    // the 32x32x16 one on the C3 shard (345 vs 346 us per layer4-class launch)
-    const bool wg16 = g_wg_mf16 || g_x3_variant / 10 == 9;
-    if (ka == 256 && g_wg_ns4) hipLaunchKernelGGL((wgrad_x3_kernel<256, 4>), dim3(grid), dim3(512), 0, st, a);
-    else if (ka == 256) hipLaunchKernelGGL((wgrad_x3_kernel<256, 3>), dim3(grid), dim3(512), 0, st, a);
-    else if (wg16 && ka == 128) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<128>, dim3(grid), dim3(512), 0, st, a);
-    else if (wg16) hipLaunchKernelGGL(wgrad_x3_mf16_kernel<64>, dim3(grid), dim3(512), 0, st, a);
+    if (ka == 256) hipLaunchKernelGGL(wgrad_x3_kernel<256>, dim3(grid), dim3(512), 0, st, a);
     else if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<64>, dim3(grid), dim3(512), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3");
@@ -2348,63 +1858,47 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     a.plane = (long)d->n * a.H * a.W * 4;
     a.n_tiles = d->k / 64;
     const long m_tiles = (M + 255) / 256;
-    // two blocks per CU (7 K-steps per tile: prologue / epilogue dominate one block);
-    // knob 20 = one block per CU with a 3-stage ring
-    if (g_x3_variant / 10 == 2)
-        hipLaunchKernelGGL((conv_x3_kernel<64, 2, true>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
-    else if (g_stem_mf16)              // 16x16x32 stem body (A/B: HKP_STEM_MF16=1)
-        hipLaunchKernelGGL((conv_x3_kernel<64, 2, true, 3, 16>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
-                           as_stream(stream), a);
-    else
-        hipLaunchKernelGGL((conv_x3_kernel<64, 2, true, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream),
-                           a);
+    // two blocks per CU (7 K-steps per tile: prologue / epilogue dominate one
+    // block), 32x32x16 body on a 2-stage ring
+    hipLaunchKernelGGL((conv_x3_kernel<64, true, true, 32, false, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
+                       as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
     return HKP_OK;
 }
 
-extern "C" int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc) {
-    if (k <= 0 || m <= 0 || rsc < 0) return -1;
-    if (rsc < 32) return x3_plan(k, (m + 255) / 256, 1, false, 0.0).bn;     // no stream-K workspace
-    return x3_tile_n(k, (m + 255) / 256, rsc / 32);
-}
-extern "C" int32_t hkp_wgrad_x3_tile_k(int32_t k) {
-    if (k <= 0 || k % 64 != 0) return -1;
-    hkp_conv_desc d{};
-    d.k = k; d.r = 1; d.s = 1; d.c = 32;
-    int sp, mps, ka, rt;
-    wg_x3_plan(&d, 1024, &sp, &mps, &ka, &rt);
-    return ka;
-}
-extern "C" int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc) {
-    if (k <= 0 || m <= 0 || rsc < 0) return -1;
-    const int v = g_x3_variant % 10, ord = g_x3_variant / 10;
-    if (v == 6 || v == 7) return 16;
-    const long m_tiles = (m + 255) / 256;
-    const X3Plan pl = rsc < 32 ? x3_plan(k, m_tiles, 1, false, 0.0)
-                               : x3_plan(k, m_tiles, rsc / 32, v == 0 || v == 8, v == 8 ? 0.0 : sk_over(rsc / 32));
-    int bn = pl.bn;
-    if (v == 1 || v == 2) bn = k % 128 == 0 ? 128 : 64;
-    if ((v == 3 || v == 4) && k % 256 == 0) bn = 256;
-    if (v == 5) bn = 64;
-    const bool kh2 = !(v == 4 && bn == 256) && !(v == 2 && bn == 128);
-    const bool mf16_pol = (v == 0 && ord == 0 && bn == 128 && !pl.sk && g_mf16_rounds > 0 &&
-                           (double)m_tiles * (k / 128) >= g_mf16_rounds * x3_cus()) ||
-                          (bn == 256 && kh2 && !pl.sk && ord != 6 && ord != 4) ||
-                          (pl.sk && bn == 128 && ord != 7) ||
-                          (bn == 64 && kh2 && !pl.sk && ord != 2 && ord != 8);
-    return mf16_pol ? 16 : 32;
-}
-extern "C" int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc) {
-    if (k <= 0 || m <= 0 || rsc < 32) return -1;
-    const int v = g_x3_variant % 10;
-    if (v != 0 && v != 8) return 0;
-    const int nks = rsc / 32;
-    return x3_plan(k, (m + 255) / 256, nks, true, v == 8 ? 0.0 : sk_over(nks)).sk ? 1 : 0;
-}
-
-extern "C" int hkp_set_conv_variant(int32_t variant) {
-    HKP_CHECK_ARG(variant >= 0 && variant % 10 < 10 && variant < 100, "hkp_set_conv_variant: unknown variant %d",
-                  variant);
-    g_x3_variant = variant;
-    return HKP_OK;
+// the kernel symbol a launch with this descriptor runs (see hulkkp.h)
+extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf,
+                                        int32_t len) {
+    HKP_CHECK_ARG(d && buf && len > 0, "hkp_conv_kernel_name: bad args");
+    int ho, wo;
+    int rc = hkp_conv_out_hw(d, &ho, &wo);
+    if (rc) return rc;
+    rc = check_tile(d, "hkp_conv_kernel_name");
+    if (rc) return rc;
+    const bool sk = stream_k_ok != 0;
+    switch (op) {
+        case HKP_KOP_FWD_X3:
+        case HKP_KOP_FWD_F16: {
+            const int P = op == HKP_KOP_FWD_X3 ? 3 : 1;
+            const long m = (long)d->n * ho * wo;
+            const int nks = d->r * d->s * (d->c / (P == 3 ? 32 : 64));
+            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile), false, P, buf, len);
+        }
+        case HKP_KOP_DGRAD_X3: {
+            const long m = (long)d->n * d->h * d->w;
+            const int nks = d->r * d->s * (d->k / 32);
+            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile), false, 3, buf, len);
+        }
+        case HKP_KOP_STEM_X3:
+            return x3_kernel_name(X3_STEM, true, 3, buf, len);
+        case HKP_KOP_WGRAD_X3: {
+            HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv_kernel_name: wgrad needs Cout%%64==0");
+            int sp, mps, ka, rt;
+            wg_x3_plan(d, (long)d->n * ho * wo, &sp, &mps, &ka, &rt);
+            return snprintf(buf, len, "wgrad_x3_kernel<%d>", ka);
+        }
+        default:
+            HKP_CHECK_ARG(false, "hkp_conv_kernel_name: unknown op %d", op);
+    }
+    return HKP_ERR_BAD_ARG;
 }

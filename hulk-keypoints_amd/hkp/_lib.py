@@ -20,8 +20,16 @@ class HkpError(RuntimeError):
 
 
 class ConvDesc(ctypes.Structure):
+    """hkp_conv_desc; `tile` (HKP_TILE_*, default 0 = the planner) is per call."""
     _fields_ = [(n, ctypes.c_int32) for n in
-                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "dilation", "in_layout")]
+                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "dilation", "in_layout", "tile")]
+
+
+# hkp_conv_desc.tile policies (include/hulkkp.h)
+HKP_TILE_AUTO, HKP_TILE_NO_SK, HKP_TILE_SK, HKP_TILE_256, HKP_TILE_128_MF16, HKP_TILE_128_MF32, HKP_TILE_64_PAIR = \
+    range(7)
+# hkp_conv_kernel_name ops
+HKP_KOP_FWD_X3, HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3 = range(5)
 
 
 class PackJob(ctypes.Structure):
@@ -53,6 +61,7 @@ SIGNATURES = {
     "hkp_bn_finalize": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_eval_params": (ctypes.c_int, [_I32, _P, _P, _P, _P, _F, _P, _P, _P]),
     "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _I32, _P]),
+    "hkp_bn_apply_f16": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
@@ -65,11 +74,9 @@ SIGNATURES = {
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
-    "hkp_set_conv_variant": (ctypes.c_int, [_I32]),
-    "hkp_x3_tile_n": (_I32, [_I32, _I64, _I32]),
-    "hkp_x3_stream_k": (_I32, [_I32, _I64, _I32]),
-    "hkp_x3_mfma_k": (_I32, [_I32, _I64, _I32]),
-    "hkp_wgrad_x3_tile_k": (_I32, [_I32]),
+    "hkp_weight_pack_f16": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),
+    "hkp_conv2d_fwd_f16": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "hkp_conv_kernel_name": (_I32, [_CD, _I32, _I32, ctypes.c_char_p, _I32]),
     "hkp_upsample_argmax_ws_bytes": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_stem_pack_x3_elems": (_I64, [_CD]),
     "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),

@@ -44,7 +44,9 @@ def _i(v):
 # Conv arithmetic for the NHWC convs (the stem always runs the fp32 gather kernel):
 #   "fp32"  v_mfma_f32_32x32x2_f32, exact fp32 products
 #   "f16x3" split-precision fp16 MFMA, fp32-accurate (~2^-22 per product)
-#   "f16"   plain fp16 operands, fp32 accumulation (BASELINE config C4)
+#   "f16"   plain fp16 operands and activations, fp32 accumulation (BASELINE
+#           config C4, inference): the LDS-DMA conv kernels with one fp16 MFMA
+#           per MAC, fp16 conv outputs and residual stream (autocast semantics)
 PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
 _precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
 # id(parameter) → (weakref(parameter), {variant: (version, data_ptr, derived operand)}).
@@ -197,19 +199,21 @@ def conv_bn(conv, bn, x, layout="nhwc"):
 
 
 def _conv_fwd(conv, bn, x, layout="nhwc", part_out=None, sk=True):
-    """The conv of conv_bn → (y, BN tile partials or None).  part_out: where the
-    partials go (the x3 / stem x3 paths; the inference lanes); sk=False: no
-    stream-K (the lanes: a half batch must sum K in the full batch's order)."""
+    """The conv of conv_bn → (y, BN tile partials or None).  part_out: a caller's
+    buffer for the partials (the x3 / stem x3 paths); sk=False: no stream-K."""
     passes = PRECISIONS[_precision]
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
-    if layout == "nchw" and passes == 3 and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd, dl):
+    if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd, dl):
         y, part = ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
                                          stats=bn.training, part_out=part_out)
     elif layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
         y, part = ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training,
                                     part_out=part_out, sk=sk)
+    elif layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
+        y, part = ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
+                                     stats=bn.training, sk=sk)
     elif part_out is not None:
         raise ops.HkpError("conv %s: partials into a caller buffer need the x3 path" % (tuple(conv.weight.shape),))
     elif layout == "nhwc" and passes:
@@ -220,6 +224,11 @@ def _conv_fwd(conv, bn, x, layout="nhwc", part_out=None, sk=True):
     else:
         y, part = ops.conv2d_fwd(x, conv.weight, st, pd, dl, layout=layout, stats=bn.training)
     return y, part
+
+
+def _f16_conv_ok(conv):
+    """The conv runs on the plain-fp16 LDS-DMA kernel (hkp_conv2d_fwd_f16)."""
+    return conv.weight.shape[0] % 64 == 0 and conv.weight.shape[-1] % 64 == 0
 
 
 def image_nchw_shape(x):
@@ -261,7 +270,7 @@ def stem_forward(resnet, x_nchw, trace=None):
     sp = _split_for(y.shape[-1])
     # inference: the stem output is only read by layer1's convs and (as the raw
     # residual, hi + lo) its first block → split-only
-    out = ops.bn_relu_maxpool(y, ss, split=sp, route=trace is not None, keep_fp32=trace is not None or sp != 3)
+    out = ops.bn_relu_maxpool(y, ss, split=sp, route=trace is not None, keep_fp32=trace is not None or sp == 0)
     if trace is not None:
         trace.stem = dict(x=x_nchw, y=y, ss=ss, mi=mi, out=out)
     return out
@@ -278,6 +287,8 @@ def block_forward(block, x, trace=None, final=False):
     keep = rec is not None
 
     def act(y, s, consumer):
+        if y.dtype == torch.float16:                  # plain-fp16 path (config C4)
+            return ops.bn_apply_f16(y, s, relu=True)
         # training keeps the fp32 activation only where the backward reads it: an
         # inner activation feeding an x3-backward conv is needed only as its split
         # (its ReLU mask is recomputed from y, its wgrad reads the split)
@@ -303,6 +314,12 @@ def block_forward(block, x, trace=None, final=False):
             rec.update(x=x, y=[y1, y2, y3], ss=[s1, s2, s3], mi=[m1, m2, m3], act=[a1, a2])
     pl = _split_for(last_y.shape[-1])
     keep_out = keep or final or pl != 3
+    if last_y.dtype == torch.float16:                 # plain-fp16 path: fp16 residual stream
+        res = x if x.dtype == torch.float16 else ops.split_of(x)[0]
+        if block.downsample is not None:
+            yd, sd, _ = conv_bn(block.downsample[0], block.downsample[1], x)
+            return ops.bn_apply_f16(last_y, last_s, res=yd, res_ss=sd, relu=True, keep_fp32=final)
+        return ops.bn_apply_f16(last_y, last_s, res=res, relu=True, keep_fp32=final)
     if block.downsample is not None:
         yd, sd, md = conv_bn(block.downsample[0], block.downsample[1], x)
         out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True, split=pl, keep_fp32=keep_out)
@@ -335,13 +352,9 @@ def fc_rows(resnet, k):
 
 
 def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
-    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22).
-    Inference (no trace) runs as two lanes when the batch allows (hkp/lanes.py:
-    same kernels and outputs, lane B's BN applies beside lane A's convs)."""
-    if trace is None:
-        from . import lanes
-        if lanes.lanes_ok(resnet, x_nchw):
-            return lanes.keypoints_forward_lanes(resnet, x_nchw, k, heat=heat, argmax=argmax)
+    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
+    if trace is not None and _precision == "f16":
+        raise ops.HkpError("precision 'f16' (BASELINE config C4) is inference-only; train with 'f16x3' or 'fp32'")
     feat = backbone_forward(resnet, x_nchw, trace)
     w, b = fc_rows(resnet, k)
     low = ops.head_fc(feat, w, b)

@@ -8,7 +8,8 @@ import ctypes
 
 import torch
 
-from ._lib import ConvDesc, HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, HkpError, call
+from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3,
+                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, ConvDesc, HkpError, call)
 
 CONV_TILE_ROWS = 128  # BM of conv_fwd.hip (rows per BN statistic tile)
 
@@ -134,23 +135,15 @@ class PackedWeight(tuple):
         return self[1]
 
 
-def x3_symbol(k, m, rsc, sk=True):
-    """Kernel symbol the x3 conv launches for Cout = k over m output pixels with
-    GEMM depth rsc = R*S*Cin (the tile policy of conv_x3.hip's launch_x3:
-    hkp_x3_tile_n, hkp_x3_stream_k)."""
+def kernel_name(d, op, sk=True):
+    """The kernel symbol a launch with ConvDesc d runs (hkp_conv_kernel_name: the
+    launcher's own tile choice, so the name cannot drift from what runs)."""
     from ._lib import lib
-    L = lib()
-    sk = sk and L.hkp_x3_stream_k(k, m, rsc) == 1
-    bn = L.hkp_x3_tile_n(k, m, rsc) if sk else L.hkp_x3_tile_n(k, m, 0)
-    mfd = L.hkp_x3_mfma_k(k, m, rsc if sk else 0)
-    return "conv_x3_kernel<%d, 2, false, 0, %d, %s>" % (bn, mfd, "true" if sk else "false")
-
-
-def wgrad_x3_symbol(k):
-    """Kernel symbol the f16x3 weight gradient launches for Cout = k (its Cout tile:
-    conv_x3.hip's wg_x3_plan via hkp_wgrad_x3_tile_k)."""
-    from ._lib import lib
-    return "wgrad_x3_kernel<%d>" % lib().hkp_wgrad_x3_tile_k(k)
+    buf = ctypes.create_string_buffer(128)
+    n = lib().hkp_conv_kernel_name(ctypes.byref(d), op, int(bool(sk)), buf, 128)
+    if n < 0:
+        raise HkpError("hkp_conv_kernel_name failed: %s" % lib().hkp_last_error().decode(errors="replace"))
+    return buf.value.decode()
 
 
 def weight_pack_x3(w):
@@ -191,10 +184,11 @@ def _stat_partials(n_rows, k, device, part_out, name):
     return part_out
 
 
-def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True):
+def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True, tile=0):
     """f16x3 NHWC conv on packed split operands: xs [N,H,W,2C] (from a producer with
     split=3), wp = weight_pack_x3(w) → fp32 y [N,Ho,Wo,K] (+ BN partials, into
-    part_out when given).  sk=False: never stream-K (one tile per block)."""
+    part_out when given).  sk=False: never stream-K (one tile per block);
+    tile: HKP_TILE_* policy (0 = the planner)."""
     ws, wsc = wp
     _need(xs, torch.float16, "conv2d_fwd_x3.x_split", 4)
     _need(ws, torch.float16, "conv2d_fwd_x3.w_split", 4)
@@ -205,7 +199,7 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
         raise HkpError("conv2d_fwd_x3: weight Cin %d != input C %d" % (cw2 // 2, c2 // 2))
     c = c2 // 2
     ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
-    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC)
+    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = out if out is not None else torch.empty((n, ho, wo, k), device=xs.device, dtype=torch.float32)
     part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out") if stats else None
 
@@ -216,8 +210,48 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     if _observer is None:
         launch()
     else:
-        _observer(x3_symbol(k, n * ho * wo, r * s * c, sk), 2.0 * n * ho * wo * k * r * s * c,
+        _observer(kernel_name(d, HKP_KOP_FWD_X3, sk), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
+    return y, part
+
+
+def weight_pack_f16(w):
+    """fp32 KRSC weight → PackedWeight: [K, R, S, C] fp16 (each output channel scaled
+    by a power of two) + [K] inverse scales — the plain-fp16 conv's operand."""
+    _need(w, torch.float32, "weight_pack_f16.w", 4)
+    k, r, s, c = w.shape
+    out = torch.empty((k, r, s, c), device=w.device, dtype=torch.float16)
+    sc = torch.empty(k, device=w.device, dtype=torch.float32)
+    call("hkp_weight_pack_f16", k, r * s * c, _ptr(w), _ptr(out), _ptr(sc), _stream())
+    return PackedWeight(out, sc)
+
+
+def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0):
+    """Plain-fp16 NHWC conv (BASELINE config C4): x16 fp16 [N,H,W,C] (a producer's
+    split=1 output), wp = weight_pack_f16(w) → y fp16 [N,Ho,Wo,K] (autocast
+    semantics) + BN partials from the fp32 accumulators."""
+    ws, wsc = wp
+    _need(x16, torch.float16, "conv2d_fwd_f16.x", 4)
+    _need(ws, torch.float16, "conv2d_fwd_f16.w", 4)
+    _need(wsc, torch.float32, "conv2d_fwd_f16.w_inv_scale", 1)
+    n, h, wd, c = x16.shape
+    k, r, s, cw = ws.shape
+    if cw != c:
+        raise HkpError("conv2d_fwd_f16: weight Cin %d != input C %d" % (cw, c))
+    ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
+    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
+    y = torch.empty((n, ho, wo, k), device=x16.device, dtype=torch.float16)
+    part = _stat_partials(n * ho * wo, k, x16.device, None, "conv2d_fwd_f16") if stats else None
+
+    def launch():
+        call("hkp_conv2d_fwd_f16", ctypes.byref(d), _ptr(x16), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
+             *_sk_workspace(sk), _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        _observer(kernel_name(d, HKP_KOP_FWD_F16, sk), 2.0 * n * ho * wo * k * r * s * c,
+                  2.0 * (x16.numel() + ws.numel() + y.numel()), launch)
     return y, part
 
 
@@ -267,8 +301,8 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None):
     if _observer is None:
         launch()
     else:
-        _observer("conv_x3_kernel<64, 2, true>", 2.0 * n * ho * wo * k * 49 * c, 2.0 * (xs.numel() + ws.numel()) +
-                  4.0 * y.numel(), launch)
+        _observer(kernel_name(d, HKP_KOP_STEM_X3), 2.0 * n * ho * wo * k * 49 * c,
+                  2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
     return y, part
 
 
@@ -421,6 +455,32 @@ def bn_apply(y, ss, res=None, res_ss=None, relu=True, out=None, split=0, keep_fp
     if split:
         o._hkp_split = (sp, split)
     return o
+
+
+def bn_apply_f16(y16, ss, res=None, res_ss=None, relu=True, keep_fp32=False):
+    """Plain-fp16 path (config C4): fp16 out = [relu](y16*scale+shift [+ res | +
+    res*rscale+rshift]), res an fp16 activation or (with res_ss) the downsample's
+    fp16 y.  Returns the fp16 activation (a split=1 operand of the next conv), or
+    with keep_fp32 the fp32 copy carrying it as its split (the head reads fp32)."""
+    _need(y16, torch.float16, "bn_apply_f16.y")
+    c = y16.shape[-1]
+    m = y16.numel() // c
+    if ss.numel() != 2 * c:
+        raise HkpError("bn_apply_f16: scale_shift size %d != 2C" % ss.numel())
+    if res is not None:
+        _need(res, torch.float16, "bn_apply_f16.res")
+        if res.shape != y16.shape:
+            raise HkpError("bn_apply_f16: residual shape %s != %s" % (tuple(res.shape), tuple(y16.shape)))
+    if res_ss is not None and (res is None or res_ss.numel() != 2 * c):
+        raise HkpError("bn_apply_f16: res_scale_shift needs a residual and 2C entries")
+    out = _split_out(y16.shape, y16.device, 1)
+    o32 = torch.empty(y16.shape, device=y16.device, dtype=torch.float32) if keep_fp32 else None
+    call("hkp_bn_apply_f16", m, c, _ptr(y16), _ptr(ss), _ptr(res), _ptr(res_ss), int(bool(relu)), _ptr(out),
+         _ptr(o32), _stream())
+    if o32 is None:
+        return out
+    o32._hkp_split = (out, 1)
+    return o32
 
 
 def bn_relu_maxpool(y, ss, split=0, route=False, keep_fp32=True):
@@ -679,7 +739,7 @@ def weight_phase_pack_x3(w, pad):
     return out
 
 
-def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=None, amax=None, sk=True):
+def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=None, amax=None, sk=True, tile=0):
     """f16x3 dL/dx of a stride-2 (dilation-1) NHWC conv with KRSC weight shape
     w_shape, one stride-1 conv per output phase: dys = split_pack_x3(dy, amax),
     phase_packs = weight_phase_pack_x3(w, pad).  sk=False: no stream-K (one tile
@@ -695,6 +755,7 @@ def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=No
             raise HkpError("conv2d_bwd_data_x3_strided: phase %d pack %s, expected %s" % (
                 ph, None if p is None else tuple(p.split.shape), want))
     d = _fwd_desc(x_shape, (k, r, s, c), 2, pad, 1, "nhwc")
+    d.tile = tile
     ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, 2, pad, 1)
     if tuple(dys.shape) != (x_shape[0], ho, wo, 2 * k):
         raise HkpError("conv2d_bwd_data_x3_strided: dy split shape %s != %s" % (tuple(dys.shape),
@@ -711,15 +772,16 @@ def conv2d_bwd_data_x3_strided(dys, phase_packs, x_shape, w_shape, pad=0, add=No
     return dx
 
 
-def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=True):
+def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=True, tile=0):
     """f16x3 dL/dx of a stride-1 NHWC conv from packed dy (split_pack_x3 with `amax`)
-    and wfp = weight_flip_pack_x3(w).  sk=False: no stream-K."""
+    and wfp = weight_flip_pack_x3(w).  sk=False: no stream-K; tile: HKP_TILE_*."""
     wfs, wfsc = wfp
     _need(dys, torch.float16, "conv2d_bwd_data_x3.dy_split", 4)
     _need(wfs, torch.float16, "conv2d_bwd_data_x3.wf_split", 4)
     c, r, s, k2 = wfs.shape
     k = k2 // 2
     d = _fwd_desc(x_shape, (k, r, s, c), 1, pad, dil, "nhwc")
+    d.tile = tile
     ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, 1, pad, dil)
     if tuple(dys.shape) != (x_shape[0], ho, wo, 2 * k):
         raise HkpError("conv2d_bwd_data_x3: dy split shape %s != %s" % (tuple(dys.shape), (x_shape[0], ho, wo, 2 * k)))
@@ -736,7 +798,7 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=
     if _observer is None:
         launch()
     else:
-        _observer(x3_symbol(c, x_shape[0] * x_shape[1] * x_shape[2], r * s * k, sk),
+        _observer(kernel_name(d, HKP_KOP_DGRAD_X3, sk),
                   2.0 * x_shape[0] * x_shape[1] * x_shape[2] * c * r * s * k,
                   2.0 * (dys.numel() + wfs.numel()) + 4.0 * dx.numel(), launch)
     return dx
@@ -775,7 +837,7 @@ def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, al
     if _observer is None:
         launch()
     else:
-        _observer(wgrad_x3_symbol(d.k),
+        _observer(kernel_name(d, HKP_KOP_WGRAD_X3),
                   2.0 * n * ho * wo * d.k * d.r * d.s * d.c, 2.0 * (xs.numel() + dys.numel()) + 4.0 * dw.numel(),
                   launch)
     return dw

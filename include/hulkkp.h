@@ -52,7 +52,25 @@ typedef struct hkp_conv_desc {
     int32_t k, r, s;                /* output channels, filter height, filter width    */
     int32_t stride, pad, dilation;  /* symmetric                                        */
     int32_t in_layout;              /* HKP_LAYOUT_NHWC, or HKP_LAYOUT_NCHW (stem only)  */
+    int32_t tile;                   /* x3 / fp16 conv tile policy, HKP_TILE_* (0: the
+                                       planner).  Per call — no process-global state */
 } hkp_conv_desc;
+
+/* Tile policies of the packed-operand convs (hkp_conv2d_fwd_x3 / _fwd_f16 /
+ * _bwd_data_x3 / _bwd_data_x3_strided).  AUTO: fewest rounds of blocks over the
+ * CUs weighted by the measured per-column cost of each tile width (256x256,
+ * 256x128, 256x64), data-parallel or stream-K (with a workspace).  The others
+ * force one kernel body (for tests and tuning; outputs agree to fp32 summation
+ * order): NO_SK never stream-K; SK stream-K wherever a tile split helps;
+ * 256 = 256x256 16x16x32 (Cout % 256 == 0); 128_MF16 / 128_MF32 = 256x128 with
+ * 16x16x32 / 32x32x16 MFMAs; 64_PAIR = 256x64, two blocks per CU. */
+#define HKP_TILE_AUTO 0
+#define HKP_TILE_NO_SK 1
+#define HKP_TILE_SK 2
+#define HKP_TILE_256 3
+#define HKP_TILE_128_MF16 4
+#define HKP_TILE_128_MF32 5
+#define HKP_TILE_64_PAIR 6
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);
@@ -112,31 +130,30 @@ int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uin
  * leaves them zero (allocate once, zeroed, per stream: calls on one workspace
  * must not run concurrently).  Size: hkp_conv_x3_sk_workspace_bytes(). */
 int64_t hkp_conv_x3_sk_workspace_bytes(void);
-/* Tile width (256, 128 or 64 output channels per 256-pixel tile) the x3 conv
- * uses for Cout = k over m output pixels and GEMM depth rsc = R*S*Cin: fewest
- * rounds of blocks over the CUs weighted by the measured per-column cost of each
- * tile, data-parallel or stream-K (rsc = 0: as launched without a stream-K
- * workspace; -1 on bad args).
- * Tuning knob for the choice (0 = that policy; 1 = 256x128 only; 2 = 256x128
- * with 16-channel stages; 3 / 4 = 256x256 with 32- / 16-channel stages whenever
- * Cout % 256 == 0; 5 = 256x64; 6 / 7 = 16x16x32 MFMAs with 256x128 / 256x64
- * tiles; 8 = stream-K wherever a tile split helps; 9 = never stream-K; + 20 =
- * one-block 256x64 / stem kernels; + 40 = the 4-wave 256x256 body; + 60 = the
- * 32x32x16 256x256 body instead of the 16x16x32 one).  Outputs agree to fp32
- * summation order. */
-int32_t hkp_x3_tile_n(int32_t k, int64_t m, int32_t rsc);
-/* 1 if that launch (rsc = R*S*Cin, the GEMM depth) runs stream-K under the
- * current knob and a workspace (the conv_x3_kernel<..., true> instantiation). */
-int32_t hkp_x3_stream_k(int32_t k, int64_t m, int32_t rsc);
-/* K of the MFMA that launch uses: 32 (32x32x16) or 16 (16x16x32: 256x256 tiles,
- * stream-K 256x128 tiles, and 256x128 tiles on grids of >= 2 full rounds — the
- * lower-power shape holds a higher clock under load). */
-int32_t hkp_x3_mfma_k(int32_t k, int64_t m, int32_t rsc);
-/* Cout rows per tile of the f16x3 weight-gradient launch (hkp_conv2d_bwd_filter_x3)
- * for Cout = k: 256 (Cout % 256 == 0, a 256x256 tile), 128 or 64 — i.e. the
- * wgrad_x3_kernel<KA> instantiation it runs (opt-in 16x16x32 body aside). */
-int32_t hkp_wgrad_x3_tile_k(int32_t k);
-int hkp_set_conv_variant(int32_t variant);
+/* Plain-fp16 conv (BASELINE config C4, "fp16 with MFMA"): the same LDS-DMA
+ * kernel family as hkp_conv2d_fwd_x3 with one fp16 product per MAC (fp32
+ * accumulation).  x_f16: NHWC fp16 [n][h][w][c] (a producer's split_passes = 1
+ * output); w_f16: KRSC fp16 written by hkp_weight_pack_f16 (each output channel
+ * scaled by a power of two, max|w| -> [2^13, 2^14); w_inv_scale[k] the inverse).
+ * Output y_f16: fp16 NHWC (autocast semantics; the tile is staged in LDS and
+ * written as whole 16-B row chunks); BN partials from the fp32 accumulators.
+ * Needs c % 64 == 0 and k % 64 == 0.  Stream-K workspace as hkp_conv2d_fwd_x3. */
+int hkp_weight_pack_f16(int32_t k, int32_t rsc, const float* w, uint16_t* w_f16, float* w_inv_scale,
+                        hkp_stream_t stream);
+int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
+                       const float* w_inv_scale, uint16_t* y_f16, float* stat_partials, void* sk_workspace,
+                       int64_t sk_ws_bytes, hkp_stream_t stream);
+/* The kernel a launch with descriptor d runs — its template name as rocprofv3
+ * reports it (e.g. "conv_x3_kernel<256, false, false, 16, false, 3>"), for
+ * profiling / roofline attribution.  op: HKP_KOP_*; stream_k_ok: whether the
+ * call passes a stream-K workspace.  Writes at most len bytes (NUL-terminated);
+ * returns the name's length, or < 0 on bad args. */
+#define HKP_KOP_FWD_X3 0
+#define HKP_KOP_DGRAD_X3 1
+#define HKP_KOP_FWD_F16 2
+#define HKP_KOP_STEM_X3 3
+#define HKP_KOP_WGRAD_X3 4
+int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf, int32_t len);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
@@ -171,6 +188,14 @@ int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const f
 int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* scale_shift, const float* res,
                  const float* res_scale_shift, const uint16_t* res_split, int32_t relu, float* out,
                  uint16_t* out_split, int32_t split_passes, hkp_stream_t stream);
+
+/* Plain-fp16 path (BASELINE config C4; autocast semantics): out (fp16) =
+ * [relu](y*scale + shift [+ res | + res*rscale + rshift]) for an fp16 conv output
+ * y [m][c] (hkp_conv2d_fwd_f16), fp16 residual res (the block input, or with
+ * res_scale_shift the downsample conv's fp16 y); the arithmetic is fp32.  out32
+ * (nullable): the same values in fp32 (the block feeding the head).  c % 8 == 0. */
+int hkp_bn_apply_f16(int64_t m, int32_t c, const uint16_t* y, const float* scale_shift, const uint16_t* res,
+                     const float* res_scale_shift, int32_t relu, uint16_t* out, float* out32, hkp_stream_t stream);
 
 /* Stem tail: maxpool3x3/s2/p1( relu( y*scale + shift ) ), NHWC
  * (src/resnet.py:139-141, 200-202). Output [n, (h-1)/2+1, (w-1)/2+1, c].

@@ -117,3 +117,21 @@ def test_fused_adam_rejects_unsupported_options():
     p[0].grad = torch.zeros(4)
     with pytest.raises(HkpError, match="CUDA"):       # no CPU path
         opt.step()
+
+
+def test_kernel_name_query():
+    """hkp_conv_kernel_name: the tile planner's choice for a descriptor, as the
+    kernel symbol rocprofv3 reports — per call (hkp_conv_desc.tile), no global knob."""
+    from hkp import _lib, ops
+    # C2 layer4 conv (R34, 640x480, B=32, dilation 4): 1200 256x256 tiles
+    d = _lib.ConvDesc(32, 60, 80, 512, 512, 3, 3, 1, 4, 4, 0)
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<256, false, false, 16, false, 3>"
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_F16) == "conv_x3_kernel<256, false, false, 16, false, 1>"
+    assert ops.kernel_name(d, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_kernel<256>"
+    d.tile = _lib.HKP_TILE_64_PAIR
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"
+    d.tile = 99
+    with pytest.raises(_lib.HkpError, match="tile policy"):
+        ops.kernel_name(d, _lib.HKP_KOP_FWD_X3)
+    stem = _lib.ConvDesc(32, 480, 640, 3, 64, 7, 7, 2, 3, 1, _lib.HKP_LAYOUT_NCHW)
+    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3) == "conv_x3_kernel<64, true, true, 32, false, 3>"

@@ -229,42 +229,3 @@ def test_forward_deterministic(cuda_device):
         a = m(x)
         b = m(x)
     assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("bb,k,train_bn,u8", [("resnet34", 4, True, False), ("resnet50", 8, True, True),
-                                              ("resnet18", 2, False, False)])
-def test_lanes_bit_identical(cuda_device, monkeypatch, bb, k, train_bn, u8):
-    """The two-lane inference forward (hkp/lanes.py: half batches on two streams,
-    one BN finalize per layer over both halves' tile partials) gives exactly the
-    one-lane heatmaps, argmax and BN running statistics."""
-    from hkp import lanes
-    from hkp._lib import call
-    call("hkp_set_conv_variant", 9)       # no stream-K on the one-lane path either (the lanes never take it)
-    B, H, W = 4, 128, 192
-    imgs = recipe.seeded_images_u8(B, H, W, 51)
-    x = torch.from_numpy(imgs).to(cuda_device) if u8 else recipe.to_tensor_nchw(imgs).to(cuda_device)
-    out = {}
-    try:
-        _lanes_runs(out, lanes, monkeypatch, bb, k, train_bn, x, cuda_device)
-    finally:
-        call("hkp_set_conv_variant", 0)
-    assert torch.equal(out[True][0], out[False][0])
-    assert torch.equal(out[True][1], out[False][1]) and torch.equal(out[True][2], out[False][2])
-    for n, t in out[False][3].items():
-        assert torch.equal(out[True][3][n], t), n
-    # odd batch: one lane
-    assert not lanes.lanes_ok(out[True][4], x[:3])
-
-
-def _lanes_runs(out, lanes, monkeypatch, bb, k, train_bn, x, cuda_device):
-    for on in (False, True):
-        monkeypatch.setattr(lanes, "ENABLED", on)
-        m = _model(bb, k, 52, cuda_device)
-        if not train_bn:
-            m.eval()
-        assert lanes.lanes_ok(m.resnet.net, x) == on
-        with torch.no_grad():
-            hm, yx = m.heatmaps_and_keypoints(x)
-            yx2 = m.predict_keypoints(x)
-        torch.cuda.synchronize()
-        out[on] = (hm, yx, yx2, {n: t.clone() for n, t in m.state_dict().items() if "running" in n}, m.resnet.net)

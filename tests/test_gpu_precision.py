@@ -152,11 +152,10 @@ X3_CASES = CASES + [
 @pytest.mark.parametrize("case", X3_CASES)
 def test_x3_conv_fp32_accurate(cuda_device, case):
     """The deep-pipelined packed-operand conv: fp32-class vs fp64, BN partials as the
-    fp32 kernel's, the 256x256 / 256x128 / 16-channel-stage tile variants and the
-    16x16x32-MFMA variants agree to fp32 summation order, and stats=False gives
-    the same output."""
+    fp32 kernel's, every kernel body (hkp_conv_desc.tile: 256x256, 256x128 with
+    16x16x32 / 32x32x16 MFMAs, 256x64 pairs, stream-K) agrees to fp32 summation
+    order, and stats=False gives the same output."""
     from hkp import ops
-    from hkp._lib import call
     n, h, w, cin, cout, k, st, pad, dil = case
     x = F.relu(rand(n, h, w, cin, seed=21))
     wt = rand(cout, k, k, cin, seed=22, scale=(2.0 / (k * k * cout)) ** 0.5)
@@ -173,16 +172,12 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     assert torch.allclose(p, p32, rtol=1e-4, atol=1e-3)
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
-    try:
-        for var in (1, 2, 3, 4, 6, 7, 8, 9, 40, 43, 60, 63, 70, 78, 80, 85):
-            call("hkp_set_conv_variant", var)
-            yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
-            # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
-            # segments at the end, so variants differ by fp32 summation order)
-            assert (yv.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale
-            assert torch.allclose(pv, p, rtol=1e-4, atol=1e-3)
-    finally:
-        call("hkp_set_conv_variant", 0)
+    for tile in range(1, 7):
+        yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
+        # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
+        # segments at the end, so variants differ by fp32 summation order)
+        assert (yv.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale, tile
+        assert torch.allclose(pv, p, rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("case", [c for c in CASES if c[6] == 1 and c[3] % 64 == 0])
@@ -299,6 +294,8 @@ WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (1, 30, 40, 96, 128, 3, 2, 1, 1),       # stride 2, RSC = 864 (ragged 256-column tile)
     (2, 30, 40, 256, 256, 3, 1, 2, 2),      # 256x256 tile (16-pixel stages), several pixel splits
     (1, 3, 5, 64, 256, 3, 1, 1, 1),         # 256x256 tile, M = 15: a single stage
+    (1, 30, 40, 96, 256, 3, 2, 1, 1),       # 256x256 tile, RSC 864: column groups past R*S*Cin
+    (2, 7, 9, 64, 256, 3, 1, 1, 1),         # 256x256 tile, Wo = 9: 16-pixel stages wrap rows / images
 ]
 
 
@@ -325,15 +322,6 @@ def test_x3_wgrad_scaled(cuda_device, case, gscale):
     if cin % 64 == 0:   # same sums as the register-staged split wgrad, different order
         dw2 = ops.conv2d_bwd_filter_split(xd, gy_d, (cout, k, k, cin), st, pad, dil, amax=amax)
         assert (dw - dw2).abs().max().item() <= 4e-6 * dw2.abs().max().item()
-    from hkp._lib import call
-    try:                # the 16x16x32 wgrad body (knob 90)
-        call("hkp_set_conv_variant", 90)
-        dw16 = ops.conv2d_bwd_filter_x3(xs, ops.split_pack_x3(gy_d, amax), (cout, k, k, cin), st, pad, dil,
-                                        amax=amax)
-    finally:
-        call("hkp_set_conv_variant", 0)
-    err16 = (dw16.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
-    assert err16 < 2e-6, err16
 
 
 @pytest.mark.parametrize("shape", [(2, 3, 50, 70), (3, 3, 33, 41), (1, 1, 20, 26), (2, 3, 480 // 4, 640 // 4)])
@@ -352,13 +340,6 @@ def test_stem_x3_fp32_accurate(cuda_device, shape):
     assert err < 2e-6, err
     y32, p32 = ops.conv2d_fwd(xd, wd, 2, 3, 1, layout="nchw")
     assert torch.allclose(part, p32, rtol=1e-4, atol=1e-3)
-    from hkp._lib import call
-    try:                                   # one block per CU (knob 20): same K order, same bits
-        call("hkp_set_conv_variant", 20)
-        y1, p1 = ops.conv2d_fwd_stem_x3(xd, ops.stem_weight_pack_x3(wd), 64)
-    finally:
-        call("hkp_set_conv_variant", 0)
-    assert torch.equal(y1, y) and torch.equal(p1, part)
 
 
 def _model(bb, k, wseed, dev):
@@ -416,12 +397,12 @@ SK_CASES = [
 
 @pytest.mark.parametrize("case", SK_CASES)
 def test_x3_stream_k(cuda_device, case):
-    """Stream-K x3 conv (knob 8: split tiles x K-steps over one block per CU, fixed
-    segment-order fp32 sum) vs one tile per block (knob 9), forward and stride-1
-    dgrad: same values to fp32 summation order, same BN partials, deterministic
-    run to run (the arrival counters are left zero)."""
+    """Stream-K x3 conv (HKP_TILE_SK: split tiles x K-steps over one block per CU,
+    fixed segment-order fp32 sum) vs one tile per block (HKP_TILE_NO_SK), forward
+    and stride-1 dgrad: same values to fp32 summation order, same BN partials,
+    deterministic run to run (the arrival counters are left zero)."""
     from hkp import ops
-    from hkp._lib import call
+    from hkp._lib import HKP_KOP_FWD_X3, HKP_TILE_NO_SK, HKP_TILE_SK, ConvDesc
     n, h, w, cin, cout, k, st, pad, dil = case
     d = cuda_device
     x = F.relu(rand(n, h, w, cin, seed=31)).to(d)
@@ -435,17 +416,15 @@ def test_x3_stream_k(cuda_device, case):
     dys = ops.split_pack_x3(gy, amax)
     wfp = ops.weight_flip_pack_x3(wt)
     add = rand(n, h, w, cin, seed=34).to(d)
+    assert ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, HKP_TILE_SK),
+                           HKP_KOP_FWD_X3).endswith(", true, 3>")          # really the stream-K body
     out = {}
-    try:
-        for var in (9, 8, 8):
-            call("hkp_set_conv_variant", var)
-            y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
-            dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add, amax=amax)
-            out.setdefault(var, []).append((y, p, dx))
-    finally:
-        call("hkp_set_conv_variant", 0)
-    (y9, p9, dx9), = out[9]
-    (y8, p8, dx8), (y8b, p8b, dx8b) = out[8]
+    for tile in (HKP_TILE_NO_SK, HKP_TILE_SK, HKP_TILE_SK):
+        y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
+        dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=tile)
+        out.setdefault(tile, []).append((y, p, dx))
+    (y9, p9, dx9), = out[HKP_TILE_NO_SK]
+    (y8, p8, dx8), (y8b, p8b, dx8b) = out[HKP_TILE_SK]
     assert torch.equal(y8, y8b) and torch.equal(p8, p8b) and torch.equal(dx8, dx8b)
     # both fp32-class (each within 2e-6 of fp64, test_x3_conv_fp32_accurate): K
     # segments summed at the end reorder the fp32 sum
@@ -454,22 +433,20 @@ def test_x3_stream_k(cuda_device, case):
     assert (dx8 - dx9).abs().max().item() <= 4e-6 * dx9.abs().max().item()
 
 
-W4_CASES = [
+BODY_CASES = [
     (2, 11, 13, 64, 256, 3, 1, 1, 1),       # ragged M (286 rows: second tile mostly empty)
     (1, 15, 20, 512, 512, 3, 1, 4, 4),      # layer4 class, K = 4608
     (2, 12, 16, 256, 512, 1, 1, 0, 1),      # 1x1 (downsample class)
 ]
 
 
-@pytest.mark.parametrize("case", W4_CASES)
-@pytest.mark.parametrize("knob", [43, 63])
-def test_x3_w4_body(cuda_device, case, knob):
-    """The alternative 256x256 bodies — knob 43: 4 waves (one per SIMD, 128x128
-    wave tiles in AGPR accumulators); knob 63: the 8-wave 32x32x16 body (the
-    default is the 8-wave 16x16x32 one) — forward and stride-1 dgrad with a
-    residual addend are fp32-class vs fp64; BN partials agree with the default's."""
+@pytest.mark.parametrize("case", BODY_CASES)
+@pytest.mark.parametrize("tile", [3, 4, 5, 6])
+def test_x3_tile_bodies_dgrad(cuda_device, case, tile):
+    """Every kernel body (256x256 / 256x128 16x16x32 / 256x128 32x32x16 / 256x64
+    pairs) on the forward and the stride-1 dgrad with a residual addend:
+    fp32-class vs fp64; BN partials agree with the planner's choice."""
     from hkp import ops
-    from hkp._lib import call
     n, h, w, cin, cout, k, st, pad, dil = case
     x = F.relu(rand(n, h, w, cin, seed=61))
     wt = rand(cout, k, k, cin, seed=62, scale=(2.0 / (k * k * cout)) ** 0.5)
@@ -489,27 +466,22 @@ def test_x3_w4_body(cuda_device, case, knob):
     wfp = ops.weight_flip_pack_x3(wt.to(d))
     add_d = add.permute(0, 2, 3, 1).contiguous().to(d)
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False)
-    try:
-        call("hkp_set_conv_variant", knob)
-        y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False)
-        dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add_d, amax=amax, sk=False) \
-            if cin % 256 == 0 else None
-    finally:
-        call("hkp_set_conv_variant", 0)
+    y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=tile)
+    dx = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, add=add_d, amax=amax, sk=False, tile=tile)
     scale = ref.abs().max().item()
     assert (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale
     assert torch.allclose(p, p3, rtol=1e-4, atol=1e-3)
-    if dx is not None:
-        err = (dx.cpu().double().permute(0, 3, 1, 2) - dref).abs().max().item() / dref.abs().max().item()
-        assert err < 2e-6, err
+    err = (dx.cpu().double().permute(0, 3, 1, 2) - dref).abs().max().item() / dref.abs().max().item()
+    assert err < 2e-6, err
 
 
 def test_x3_mf16_policy_large_grid(cuda_device):
     """Grids of >= 2 full rounds of 256x128 tiles take the 16x16x32-MFMA body by
-    default (hkp_x3_mfma_k); it agrees with the 32x32x16 body (knob 1) to fp32
-    summation order — forward and stride-1 dgrad — and the observer symbol names it."""
+    default; it agrees with the 32x32x16 body (HKP_TILE_128_MF32) to fp32
+    summation order — forward and stride-1 dgrad — and hkp_conv_kernel_name
+    (the observer's symbol) names each."""
     from hkp import ops
-    from hkp._lib import call, lib
+    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_KOP_FWD_X3, HKP_TILE_128_MF32, ConvDesc
     n, h, w, cin, cout, k, st, pad, dil = (2, 240, 320, 128, 128, 3, 1, 1, 1)   # 600 tiles
     d = cuda_device
     x = F.relu(rand(n, h, w, cin, seed=71)).to(d)
@@ -517,22 +489,83 @@ def test_x3_mf16_policy_large_grid(cuda_device):
     ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d)
     xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
     wp = ops.weight_pack_x3(wt)
-    m = n * h * w
-    assert lib().hkp_x3_mfma_k(cout, m, k * k * cin) == 16
-    assert ops.x3_symbol(cout, m, k * k * cin) == "conv_x3_kernel<128, 2, false, 0, 16, false>"
+    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0)
+    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_kernel<128, false, false, 16, false, 3>"
+    assert ops.kernel_name(desc, HKP_KOP_DGRAD_X3) == "conv_x3_kernel<128, false, false, 16, false, 3>"
+    desc.tile = HKP_TILE_128_MF32
+    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_kernel<128, false, false, 32, false, 3>"
     gy = rand(n, h, w, cout, seed=73).to(d)
     amax = ops.absmax(gy)
     dys = ops.split_pack_x3(gy, amax)
     wfp = ops.weight_flip_pack_x3(wt)
     y16, p16 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
     dx16 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax)
-    try:
-        call("hkp_set_conv_variant", 1)
-        assert lib().hkp_x3_mfma_k(cout, m, k * k * cin) == 32
-        y32, p32 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
-        dx32 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax)
-    finally:
-        call("hkp_set_conv_variant", 0)
+    y32, p32 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_128_MF32)
+    dx32 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax, tile=HKP_TILE_128_MF32)
     assert (y16 - y32).abs().max().item() <= 4e-6 * y32.abs().max().item()
     assert torch.allclose(p16, p32, rtol=1e-4, atol=1e-3)
     assert (dx16 - dx32).abs().max().item() <= 4e-6 * dx32.abs().max().item()
+
+
+F16_CASES = [
+    (2, 17, 23, 64, 64, 3, 1, 1, 1),
+    (2, 30, 40, 64, 128, 3, 2, 1, 1),       # stride 2
+    (1, 15, 20, 128, 256, 3, 1, 2, 2),      # dilation 2, 256x256 tiles
+    (1, 15, 20, 512, 512, 3, 1, 4, 4),      # layer4 class (dilation 4), K = 4608
+    (3, 13, 17, 256, 64, 1, 1, 0, 1),       # 1x1 reduce (bottleneck conv1), 256x64 pairs, ragged M
+    (1, 12, 16, 256, 1024, 1, 1, 0, 1),     # 1x1 expand (bottleneck conv3)
+    (2, 31, 41, 256, 512, 1, 2, 0, 1),      # 1x1 stride-2 downsample
+]
+
+
+@pytest.mark.parametrize("case", F16_CASES)
+def test_f16_conv_exact_products(cuda_device, case):
+    """Plain-fp16 LDS-DMA conv (config C4): its operands are the fp16 roundings of
+    x and of the power-of-two-scaled weights; products of fp16 values are exact in
+    fp32, so against an fp64 conv of those same operands only fp32 accumulation
+    error and the output's one fp16 rounding remain (every tile body; BN partials
+    from the unrounded accumulators)."""
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    x = F.relu(rand(n, h, w, cin, seed=81))
+    wt = rand(cout, k, k, cin, seed=82, scale=(2.0 / (k * k * cout)) ** 0.5)
+    d = cuda_device
+    x16 = x.half().to(d)
+    wp = ops.weight_pack_f16(wt.to(d))
+    w_eff = (wp.split.double() * wp.inv_scale.double().view(-1, 1, 1, 1)).cpu()     # the weights it multiplies
+    ref = F.conv2d(x.half().double().permute(0, 3, 1, 2), w_eff.permute(0, 3, 1, 2), None, st, pad, dil)
+    scale = ref.abs().max().item()
+    y16, p16 = ops.conv2d_fwd_f16(x16, wp, st, pad, dil)
+    assert y16.dtype == torch.float16
+
+    def err_ratio(y):          # fp32 accumulation error + one fp16 rounding of the output
+        e = (y.cpu().double().permute(0, 3, 1, 2) - ref).abs()
+        return (e / (2.0 ** -11 * ref.abs() + 2e-6 * scale)).max().item()
+    assert err_ratio(y16) <= 1.0
+    # BN partials (from the fp32 accumulators) as the fp32 conv's on the same fp16-rounded operands
+    yr, pr = ops.conv2d_fwd(x.half().float().to(d), w_eff.float().to(d), st, pad, dil)
+    assert torch.allclose(p16, pr, rtol=1e-4, atol=1e-3)
+    for tile in range(1, 7):
+        yv, pv = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, tile=tile)
+        assert err_ratio(yv) <= 1.0, tile
+        assert torch.allclose(pv, p16, rtol=1e-4, atol=1e-3)
+
+
+def test_bn_apply_f16(cuda_device):
+    """fp16 BN apply (config C4): fp32 arithmetic on fp16 y / residuals, one fp16
+    rounding of the result; the fp32 copy is the unrounded value."""
+    from hkp import ops
+    d = cuda_device
+    y = rand(2, 9, 11, 96, seed=91).half().to(d)
+    r = rand(2, 9, 11, 96, seed=92).half().to(d)
+    ss = torch.cat([rand(96, seed=93) * 0.5 + 1, rand(96, seed=94) * 0.1]).to(d)
+    rs = torch.cat([rand(96, seed=95) * 0.5 + 1, rand(96, seed=96) * 0.1]).to(d)
+    c = 96
+    base = y.float() * ss[:c] + ss[c:]
+    for res, res_ss, want in ((None, None, base), (r, None, base + r.float()),
+                              (r, rs, base + (r.float() * rs[:c] + rs[c:]))):
+        o = ops.bn_apply_f16(y, ss, res=res, res_ss=res_ss, relu=True, keep_fp32=True)
+        assert torch.equal(o, torch.relu(want))
+        assert torch.equal(ops.split_of(o)[0], torch.relu(want).half())
+        o16 = ops.bn_apply_f16(y, ss, res=res, res_ss=res_ss, relu=False)
+        assert o16.dtype == torch.float16 and torch.equal(o16, want.half())

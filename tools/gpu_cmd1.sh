@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?"
+timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline > gpurun_out/bench_c2.log 2>&1 && echo c2 ok
+timeout -k 10 300 python -u bench.py --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --no-extras --no-cpu-baseline > gpurun_out/bench_c4.log 2>&1 && echo c4 ok
