@@ -568,40 +568,46 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     // ---- DMA source bookkeeping (rows this lane feeds) ----
+    // Per row: the image-space origin (hb, wb) of its receptive field packed as
+    // two int16, and the unsigned 32-bit element offset of that (possibly
+    // padded-out) origin pixel from xbase = a.xs - pad*(W+1)*cstride (the
+    // furthest a padded-out origin reaches before a.xs); a tap adds a
+    // wave-uniform offset.  Rows past M get an origin that is never in-bounds.  B
+    // rows: 32-bit offsets from a.ws.  (64-bit pointers here pushed the 256x256
+    // kernels past 256 VGPRs; the spill reload inside the DMA issue waited
+    // vmcnt(0) on every K-step.  The host checks the operand sizes fit.)
     const int cstride = STEM ? 4 : a.cch * 64;     // halves per pixel
-    // per row: image-space origin (hb, wb) of its receptive field and the base
-    // pointer of that (possibly padded-out) origin pixel; a tap adds a
-    // wave-uniform offset.  Rows past M get an origin that is never in-bounds.
-    int a_hb[GA], a_wb[GA];
-    const _Float16* a_p[GA];
+    const long xbias = (long)a.pad * (a.W + 1) * cstride;
+    const _Float16* xbase = a.xs - xbias;
+    int a_org[GA];
+    unsigned a_off[GA];
 #pragma unroll
     for (int i = 0; i < GA; ++i) {
         const int row = RPI * (w * GA + i) + lane / CPR;
         const int Lc = (lane % CPR) ^ swz(row);
         const long L = lofs(Lc);
         const int m = m0 + row;
+        int hb = -16384, wb = -16384;
+        long off = 0;
         if (m < a.M) {
             const int hw = a.Ho * a.Wo;
             const int n = m / hw, rem = m - n * hw;
             const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-            a_hb[i] = ho * a.stride - a.pad;
-            a_wb[i] = wo * a.stride - a.pad;
-            a_p[i] = a.xs + (((long)n * a.H + a_hb[i]) * a.W + a_wb[i]) * cstride + L;
-        } else {
-            a_hb[i] = -(1 << 28);
-            a_wb[i] = -(1 << 28);
-            a_p[i] = a.xs;
+            hb = ho * a.stride - a.pad;
+            wb = wo * a.stride - a.pad;
+            off = (((long)n * a.H + hb) * a.W + wb) * cstride + L;
         }
+        a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
+        a_off[i] = (unsigned)(off + xbias);
     }
     const int bline = a.RS * a.cch * 64;           // halves per weight row (output channel)
-    const _Float16* b_src[GB];
-    int b_dst[GB];
+    int b_off[GB], b_dst[GB];
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
         const int bi = (w * GB + j) % GBT;
         const int row = RPI * bi + lane / CPR;
         const int Lc = (lane % CPR) ^ swz(row);
-        b_src[j] = a.ws + (long)(n0 + row) * bline + (STEM ? Lc * 8 : lofs(Lc));
+        b_off[j] = (n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc));
         b_dst[j] = (BM + RPI * bi) * ROW;
     }
     const _Float16* zero = (const _Float16*)g_x3_zero_line;
@@ -618,12 +624,13 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64;
 #pragma unroll
         for (int i = 0; i < GA; ++i) {
-            const bool in = (unsigned)(a_hb[i] + dh) < (unsigned)a.H && (unsigned)(a_wb[i] + dw) < (unsigned)a.W;
-            glds16(in ? a_p[i] + toff : zero, st + (RPI * (w * GA + i)) * ROW);
+            const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+            const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+            glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
         }
-        const long boff = (long)(q_tap * a.cch + q_cc) * 64;
+        const int boff = (q_tap * a.cch + q_cc) * 64;
 #pragma unroll
-        for (int j = 0; j < GB; ++j) glds16(b_src[j] + boff, st + b_dst[j]);
+        for (int j = 0; j < GB; ++j) glds16(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
         q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
         if (++q_ss == a.S) {
             q_ss = 0;
@@ -1567,6 +1574,13 @@ extern "C" int hkp_weight_pack_f16(int32_t k, int32_t rsc, const float* w, uint1
 
 extern "C" int64_t hkp_conv_x3_sk_workspace_bytes(void) { return x3_sk_ws_bytes(256); }
 
+// the kernels address operands with 32-bit element offsets (see conv_x3_tile):
+// the input ([n][h][w][cstride] halves, plus a padded-out margin of up to 64
+// rows) and the weights ([k][rs][cstride]) must fit
+static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs) {
+    return (n * h * w + 64 * (w + 65)) * cstride < (1L << 32) && k * rs * cstride < (1L << 31);
+}
+
 static int check_tile(const hkp_conv_desc* d, const char* who) {
     HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_64_PAIR, "%s: unknown tile policy %d", who,
                   d->tile);
@@ -1589,7 +1603,8 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
     HKP_CHECK_ARG(d->c % cg == 0 && d->k % 64 == 0, "%s: need Cin%%%d==0, Cout%%64==0 (c=%d k=%d)", who, cg, d->c,
                   d->k);
     const long M = (long)d->n * ho * wo;
-    HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w * d->c < (1L << 40), "%s: too large", who);
+    HKP_CHECK_ARG(M < (1L << 31) && x3_offsets_fit(d->n, d->h, d->w, d->c / cg * 64, d->k, d->r * d->s), "%s: too large",
+                  who);
     X3Args a;
     a.xs = (const _Float16*)xs; a.ws = (const _Float16*)ws; a.wscale = wsc;
     a.y = y; a.y16 = (_Float16*)y16; a.part = part; a.amax = nullptr; a.add = nullptr; a.plane = 0;
@@ -1651,7 +1666,8 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     const int padp = d->dilation * (d->r - 1) - d->pad;
     HKP_CHECK_ARG(padp >= 0 && d->dilation * (d->s - 1) - d->pad == padp, "hkp_conv2d_bwd_data_x3: padding");
     const long M = (long)d->n * d->h * d->w;
-    HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_data_x3: too large");
+    HKP_CHECK_ARG(M < (1L << 31) && x3_offsets_fit(d->n, ho, wo, d->k / 32 * 64, d->c, d->r * d->s),
+                  "hkp_conv2d_bwd_data_x3: too large");
     X3Args a;
     a.xs = (const _Float16*)dy_split; a.ws = (const _Float16*)wf_split; a.wscale = wf_inv_scale;
     a.y = dx; a.part = nullptr; a.amax = (const unsigned*)dy_amax_bits; a.add = add; a.plane = 0;
@@ -1713,7 +1729,9 @@ extern "C" int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC && d->stride == 2 && d->dilation == 1,
                   "hkp_conv2d_bwd_data_x3_strided: stride-2, dilation-1 NHWC convs only");
     HKP_CHECK_ARG(d->c % 64 == 0 && d->k % 32 == 0, "hkp_conv2d_bwd_data_x3_strided: need Cin%%64==0, Cout%%32==0");
-    HKP_CHECK_ARG((long)d->n * d->h * d->w < (1L << 31), "hkp_conv2d_bwd_data_x3_strided: too large");
+    HKP_CHECK_ARG((long)d->n * d->h * d->w < (1L << 31) && x3_offsets_fit(d->n, ho, wo, d->k / 32 * 64, d->c,
+                                                                         d->r * d->s),
+                  "hkp_conv2d_bwd_data_x3_strided: too large");
     hipStream_t st = as_stream(stream);
     for (int py = 0; py < 2; ++py)
         for (int px = 0; px < 2; ++px) {
@@ -1848,7 +1866,8 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     HKP_CHECK_ARG(stem_x3_shape(d), "hkp_conv2d_fwd_stem_x3: needs the 7x7/s2/p3 NCHW stem with C<=4, Cout%%64==0");
     HKP_CHECK_ARG(x_split && w_split && y, "hkp_conv2d_fwd_stem_x3: null tensor");
     const long M = (long)d->n * ho * wo;
-    HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_fwd_stem_x3: too large");
+    HKP_CHECK_ARG(M < (1L << 31) && x3_offsets_fit(d->n, 2L * ho + 6, 2L * wo + 6, 8, d->k, 7),
+                  "hkp_conv2d_fwd_stem_x3: too large");
     X3Args a;
     a.xs = (const _Float16*)x_split; a.ws = (const _Float16*)w_split; a.wscale = w_inv_scale;
     a.y = y; a.part = stat_partials; a.amax = nullptr; a.add = nullptr;
