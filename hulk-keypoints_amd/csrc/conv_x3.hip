@@ -367,12 +367,26 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], f.h[i], f.l[i], bh[j], bl[j], mfma);
     };
 
+    // The next stage's DMA (GL pieces per wave) is issued inside the K-step's
+    // MFMA stream, one piece per column block, instead of as a burst after the
+    // barrier (a piece costs ~60 issue cycles, MI355X_MICROARCH.md; the burst
+    // left every SIMD without an MFMA to issue right after each barrier).  The
+    // last K-steps issue nothing (peeled: no branch inside the scheduled region).
+    auto sched_kstep = [&](const bool dma) {
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
+            if (dma && j * ((GL + UN - 1) / UN) < GL)
+                __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);   // DMA pieces
+        }
+    };
     if constexpr (NST == 2) {
         // 2-stage ring (256x256 tiles; 256x64 at two blocks per CU), A single-buffered
         // (registers: 128 acc + 32 A + 64 B): per K-step t — wait own DMA of t+1,
-        // barrier, issue DMA t+2 into t's buffer (read before the barrier), then per
-        // column j [MFMAs of t with B_j] [refill B_j with t+1's], then A of t+1
-        // (its latency covered by the SIMD's other wave)
+        // barrier, then per column j [MFMAs of t with B_j] [refill B_j with t+1's]
+        // [a DMA piece of t+2 into t's buffer, read before the barrier], then A of
+        // t+1 (its latency covered by the SIMD's other wave)
         issue_next();
         if (nks > 1) issue_next();
         if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
@@ -383,26 +397,25 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
         for (int j = 0; j < UN; ++j) read_b(j, smem);
         int cur = 0;
-        for (int t = 0; t + 1 < nks; ++t) {
+        auto kstep = [&](const bool dma) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();
-            if (t + 2 < nks) issue_next();
             cur ^= 1;
             const char* st = smem + cur * STAGE;
+            if (dma) issue_next();
 #pragma unroll
             for (int j = 0; j < UN; ++j) {
                 mma_col(fa, j);
                 read_b(j, st);
             }
             read_a(fa, st);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
-            }
+            sched_kstep(dma);
             __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
             __builtin_amdgcn_sched_barrier(0);
-        }
+        };
+        int t = 0;
+        for (; t + 2 < nks; ++t) kstep(true);
+        if (t + 1 < nks) kstep(false);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int j = 0; j < UN; ++j) mma_col(fa, j);
@@ -461,6 +474,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             for (int j = 0; j < UN; ++j) mma_col(fa0, j);
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the ring past here
 
     if (partial) {                         // stream-K: fold the tile's segments
         auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
