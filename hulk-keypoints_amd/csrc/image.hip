@@ -56,8 +56,34 @@ __device__ __forceinline__ uint8_t jet_channel(float x, float centre) {
     return (uint8_t)__fmul_rn(t, 255.f);
 }
 
+// Half-width of row |d| of a filled circle of radius r as OpenCV's cv::circle
+// draws it (thickness -1, LINE_8, no shift → the midpoint "Circle" rasteriser of
+// imgproc/drawing.cpp: per step (dx, dy) rows ±dy span ±dx and rows ±dx span ±dy)
+// — prediction.py:52 cv2.circle(overlay, (x, y), 4, (0, 0, 0), -1).  -1: outside.
+__host__ __device__ inline int disc_halfwidth(int r, int d) {
+    if (d < 0) d = -d;
+    int hw = -1, err = 0, dx = r, dy = 0, plus = 1, minus = (r << 1) - 1;
+    while (dx >= dy) {
+        if (d == dy && dx > hw) hw = dx;
+        if (d == dx && dy > hw) hw = dy;
+        ++dy;
+        err += plus;
+        plus += 2;
+        const int mask = (err <= 0) - 1;
+        err -= minus & mask;
+        dx += mask;
+        minus -= mask & 2;
+    }
+    return hw;
+}
+
 // out [n][rows][cols][3]: keypoint plane k sits in column k / half (half = K/2;
-// K == 1: one column), row block k % half
+// K == 1: one column), row block k % half.  Per pixel, as prediction.py:47-52:
+//   u   = uint8(float(v * s + t)) with s = 255 / (max - min), t = -min * s in
+//         double (cv2.normalize NORM_MINMAX into float32, then .astype(uint8));
+//   vis = JET(u) (BGR; the analytic JET — cv2's LUT is not available here);
+//   out = round(0.65 * img + 0.35 * vis) saturated (cv2.addWeighted);
+//   the filled radius-4 disc at the argmax (cv2.circle) is black.
 __global__ __launch_bounds__(256) void heat_overlay_kernel(int N, int K, int H, int W, int half,
                                                           const float* __restrict__ heat,
                                                           const uint8_t* __restrict__ img,
@@ -74,21 +100,69 @@ __global__ __launch_bounds__(256) void heat_overlay_kernel(int N, int K, int H, 
         const int k = (int)(t % K);
         const int n = (int)(t / K);
         const long plane = (long)n * K + k;
-        const float mn = mm[2 * plane], mx = mm[2 * plane + 1];
-        float span = __fsub_rn(mx, mn);
-        span = span > 1e-12f ? span : 1e-12f;
+        const double mn = mm[2 * plane], mx = mm[2 * plane + 1];
+        const double sc = mx - mn > 2.220446049250313e-16 ? 255.0 / (mx - mn) : 0.0;
+        const double sh = 0.0 - mn * sc;
         const float v = heat[(plane * H + y) * W + x];
-        const uint8_t u = (uint8_t)__fmul_rn(__fdiv_rn(__fsub_rn(v, mn), span), 255.f);
+        const float nv = (float)((double)v * sc + sh);
+        const uint8_t u = (uint8_t)fminf(fmaxf(nv, 0.f), 255.f);
         const float xn = __fdiv_rn((float)u, 255.f);
         const uint8_t vis[3] = {jet_channel(xn, 1.f), jet_channel(xn, 2.f), jet_channel(xn, 3.f)};   // B, G, R
         const int py = yx[2 * plane], px = yx[2 * plane + 1];
-        const bool dot = abs(y - py) <= 4 && abs(x - px) <= 4;
+        const int hw = abs(y - py) <= 4 ? disc_halfwidth(4, y - py) : -1;
+        const bool dot = hw >= 0 && abs(x - px) <= hw;
         const int col = K == 1 ? 0 : k / half, rb = K == 1 ? 0 : k % half;
         uint8_t* o = out + ((((long)n * (H * (K == 1 ? 1 : half)) + rb * H + y) * (cols * W)) + col * W + x) * 3;
         const uint8_t* im = img + (((long)n * H + y) * W + x) * 3;
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-            o[c] = dot ? 0 : (uint8_t)__fadd_rn(__fmul_rn(0.65f, (float)im[c]), __fmul_rn(0.35f, (float)vis[c]));
+        for (int c = 0; c < 3; ++c) {
+            const float b = rintf(__fadd_rn(__fmul_rn(0.65f, (float)im[c]), __fmul_rn(0.35f, (float)vis[c])));
+            o[c] = dot ? 0 : (uint8_t)fminf(fmaxf(b, 0.f), 255.f);
+        }
+    }
+}
+
+// Soft-argmax of each heatmap plane with the reference's index mapping FIXED
+// (prediction.py:31-38 builds x from i % width over d.T.ravel(), i.e. mixes the
+// axes, and its result is discarded at :45): p = softmax(beta * h) over the
+// plane, out = (sum p * x, sum p * y) in fp64, fixed-order block reduction
+// (deterministic).  One block per plane.
+__global__ __launch_bounds__(256) void soft_argmax_kernel(int H, int W, float beta, const float* __restrict__ heat,
+                                                         float* __restrict__ out_xy) {
+    __shared__ double red[4][3];
+    __shared__ float mxs[4];
+    const long HW = (long)H * W;
+    const float* h = heat + (long)blockIdx.x * HW;
+    float m = -INFINITY;
+    for (long i = threadIdx.x; i < HW; i += 256) m = fmaxf(m, beta * h[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) mxs[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(mxs[0], mxs[1]), fmaxf(mxs[2], mxs[3]));
+    double s = 0.0, sx = 0.0, sy = 0.0;
+    for (long i = threadIdx.x; i < HW; i += 256) {
+        const double e = exp((double)(beta * h[i] - m));
+        s += e;
+        sx += e * (double)(i % W);
+        sy += e * (double)(i / W);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o);
+        sx += __shfl_xor(sx, o);
+        sy += __shfl_xor(sy, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6][0] = s;
+        red[threadIdx.x >> 6][1] = sx;
+        red[threadIdx.x >> 6][2] = sy;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double S = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+        out_xy[2 * blockIdx.x] = (float)(((red[0][1] + red[1][1]) + (red[2][1] + red[3][1])) / S);
+        out_xy[2 * blockIdx.x + 1] = (float)(((red[0][2] + red[1][2]) + (red[2][2] + red[3][2])) / S);
     }
 }
 
@@ -124,5 +198,14 @@ extern "C" int hkp_heat_overlay(int32_t n, int32_t k, int32_t H, int32_t W, cons
     hipLaunchKernelGGL(heat_overlay_kernel, dim3(grid_of(total)), dim3(256), 0, st, n, k, H, W, k == 1 ? 1 : k / 2,
                        heat, img_nhwc, argmax_yx, minmax_ws, out);
     HKP_LAUNCH_CHECK("hkp_heat_overlay");
+    return HKP_OK;
+}
+
+extern "C" int hkp_soft_argmax(int32_t n, int32_t k, int32_t H, int32_t W, float beta, const float* heat, float* out_xy,
+                               hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && k > 0 && H > 0 && W > 0 && heat && out_xy, "hkp_soft_argmax: bad args");
+    hipLaunchKernelGGL(soft_argmax_kernel, dim3((unsigned)(n * k)), dim3(256), 0, as_stream(stream), H, W, beta, heat,
+                       out_xy);
+    HKP_LAUNCH_CHECK("hkp_soft_argmax");
     return HKP_OK;
 }

@@ -82,6 +82,7 @@ SIGNATURES = {
     "hkp_stem_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P]),
     "hkp_stem_pack_x3_u8": (ctypes.c_int, [_CD, _P, _P, _P]),
     "hkp_images_u8_to_nchw": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P]),
+    "hkp_soft_argmax": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
     "hkp_heat_overlay": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "hkp_stem_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),

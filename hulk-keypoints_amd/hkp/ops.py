@@ -335,6 +335,17 @@ def heat_overlay(heat, img, yx):
     return out
 
 
+def soft_argmax(heat, beta=1.0):
+    """heat [N,K,H,W] fp32 → float32 [N,K,2] (x, y): softmax(beta*h)-weighted mean
+    position per plane — Prediction.expectation (prediction.py:31-38) with its
+    axis mix-up fixed."""
+    _need(heat, torch.float32, "soft_argmax.heat", 4)
+    n, k, h, w = heat.shape
+    out = torch.empty((n, k, 2), device=heat.device, dtype=torch.float32)
+    call("hkp_soft_argmax", n, k, h, w, float(beta), _ptr(heat), _ptr(out), _stream())
+    return out
+
+
 def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None, x_hi=None):
     """Split-precision (f16x3, passes=3) or plain fp16 (passes=1) NHWC conv; fp32 in/out,
     the activation split inside the conv loop.  x_hi (passes 1): the input's pre-converted

@@ -7,11 +7,14 @@
   KeypointsDataset  dataset.py:52-79  same constructor, same (img, gaussians) items; with
                     return_uv=True items are (img, uv) so the fused loss kernel recomputes
                     the target in registers instead of reading a [K,H,W] fp64 tensor.
-  DeviceBatches     SURVEY §8(f1): the device data path — uint8 HWC images batched in
-                    pinned host memory, copied asynchronously (3 B/pixel instead of the
-                    12 B/pixel fp32 tensor, one batch ahead on a side stream) and fed to
-                    the model as [B,H,W,3] uint8, where the stem's operand pack applies
-                    ToTensor; labels travel as (u, v) and the loss kernel makes the target.
+  DeviceBatches     SURVEY §8(f1): the device data path — images decoded by `workers`
+                    DataLoader processes (the reference decodes one image at a time in
+                    the training process, dataset.py:71 with num_workers=0,
+                    train.py:51), batched as uint8 HWC in pinned host memory, copied
+                    asynchronously (3 B/pixel instead of the 12 B/pixel fp32 tensor,
+                    one batch ahead on a side stream) and fed to the model as
+                    [B,H,W,3] uint8, where the stem's operand pack applies ToTensor;
+                    labels travel as (u, v) and the loss kernel makes the target.
 """
 import os
 
@@ -98,12 +101,14 @@ class KeypointsDataset(Dataset):
         self.return_uv = return_uv
         self.imgs = []
         self.labels = []
+        self.labels_np = []           # host copies (DataLoader workers never touch the device)
         for i in range(len(os.listdir(labels_folder))):
             label = np.load(os.path.join(labels_folder, "%05d.npy" % i)).reshape(num_keypoints, 2)
             label[:, 0] = np.clip(label[:, 0], 0, self.img_width - 1)      # dataset.py:65
             label[:, 1] = np.clip(label[:, 1], 0, self.img_height - 1)     # dataset.py:66
             self.imgs.append(os.path.join(img_folder, "%05d.jpg" % i))
             self.labels.append(torch.from_numpy(label).to(device))
+            self.labels_np.append(label.astype(np.float32))
 
     def __getitem__(self, index):
         img = self.transform(imread_bgr(self.imgs[index]))
@@ -123,30 +128,79 @@ class KeypointsDataset(Dataset):
         return len(self.labels)
 
 
+class _RawView(Dataset):
+    """(uint8 [H,W,3] BGR, float32 [K,2]) host items of a KeypointsDataset — what
+    DeviceBatches' decode workers produce."""
+
+    def __init__(self, ds):
+        self.paths, self.labels = ds.imgs, ds.labels_np
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __getitem__(self, i):
+        return imread_bgr(self.paths[i]), self.labels[i]
+
+
+class _EpochBatches:
+    """Batch sampler of the persistent decode loader: the current epoch's index
+    batches (set by DeviceBatches before each epoch; iterated in the main process)."""
+
+    def __init__(self):
+        self.batches = []
+
+    def __iter__(self):
+        return iter(self.batches)
+
+    def __len__(self):
+        return len(self.batches)
+
+
+def _collate_u8(items):
+    imgs = torch.from_numpy(np.stack([it[0] for it in items]))
+    uv = torch.from_numpy(np.stack([it[1] for it in items]))
+    return imgs, uv
+
+
 class DeviceBatches:
     """Iterate a KeypointsDataset as device batches (img uint8 [B,H,W,3], uv fp32
     [B,K,2]) for model.forward / Trainer.step(img, uv=uv).
 
-    Decode happens on the host (cv2 / PIL, as the reference); each batch is stacked
-    into a pinned uint8 buffer and copied with non_blocking=True on a side stream
-    while the previous batch computes; the consumer's stream waits on an event.
-    `shuffle` uses a seeded permutation per epoch (train.py:61-67 shuffles)."""
+    Decode happens on the host (cv2 / PIL, as the reference): in the calling thread
+    (workers=0), or in `workers` DataLoader processes that decode and stack whole
+    batches ahead (`prefetch` batches per worker) into pinned memory.  Each batch
+    is copied with non_blocking=True on a side stream while the previous batch
+    computes; the consumer's stream waits on an event.  `shuffle` uses a seeded
+    permutation per epoch (train.py:61-67 shuffles); batches come in order for
+    any worker count."""
 
-    def __init__(self, dataset, batch_size, shuffle=False, seed=0, drop_last=False, device="cuda"):
+    def __init__(self, dataset, batch_size, shuffle=False, seed=0, drop_last=False, device="cuda", workers=0,
+                 prefetch=4):
         self.ds, self.bs, self.shuffle, self.seed, self.drop_last = dataset, batch_size, shuffle, seed, drop_last
         self.device = torch.device(device)
+        self.workers, self.prefetch = workers, prefetch
         self.epoch = 0
+        self._loader = None
+        self._sampler = _EpochBatches()
 
     def __len__(self):
         n = len(self.ds)
         return n // self.bs if self.drop_last else (n + self.bs - 1) // self.bs
 
-    def _host_batch(self, idx):
-        items = [self.ds.raw(i) for i in idx]
-        imgs = np.stack([it[0] for it in items])
-        buf = torch.from_numpy(imgs).pin_memory()
-        uv = torch.stack([it[1] for it in items]).to(self.device)
-        return buf, uv
+    def _host_batches(self, batches):
+        """(pinned uint8 [B,H,W,3], float32 [B,K,2]) per index batch, in order."""
+        if self.workers <= 0:
+            for idx in batches:
+                imgs, uv = _collate_u8([(imread_bgr(self.ds.imgs[i]), self.ds.labels_np[i]) for i in idx])
+                yield imgs.pin_memory(), uv
+            return
+        if self._loader is None:               # persistent workers: started once, reused every epoch
+            from torch.utils.data import DataLoader
+            self._loader = DataLoader(_RawView(self.ds), batch_sampler=self._sampler, num_workers=self.workers,
+                                      collate_fn=_collate_u8, pin_memory=True, prefetch_factor=self.prefetch,
+                                      persistent_workers=True)
+        self._sampler.batches = [list(map(int, b)) for b in batches]
+        yield from self._loader
 
     def __iter__(self):
         n = len(self.ds)
@@ -156,19 +210,23 @@ class DeviceBatches:
         if self.drop_last and batches and len(batches[-1]) < self.bs:
             batches.pop()
         copy_stream = torch.cuda.Stream(self.device)
+        host = self._host_batches(batches)
 
-        def stage(idx):
-            buf, uv = self._host_batch(idx)
+        def stage():
+            buf, uv = next(host)
             with torch.cuda.stream(copy_stream):
                 img = buf.to(self.device, non_blocking=True)
+                uvd = uv.to(self.device, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(copy_stream)
-            return img, uv, ev, buf
+            return img, uvd, ev, buf
 
-        nxt = stage(batches[0]) if batches else None
+        nxt = stage() if batches else None
         for bi in range(len(batches)):
             img, uv, ev, buf = nxt
-            nxt = stage(batches[bi + 1]) if bi + 1 < len(batches) else None
-            torch.cuda.current_stream(self.device).wait_event(ev)
-            img.record_stream(torch.cuda.current_stream(self.device))
+            nxt = stage() if bi + 1 < len(batches) else None
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            img.record_stream(cur)
+            uv.record_stream(cur)
             yield img, uv

@@ -5,7 +5,10 @@ north star asks for: the argmax of plot() (:46, np.unravel_index(h.argmax()),
 first max wins) computed on the GPU inside the upsample kernel, so no
 [B,K,H,W] heatmap has to cross PCIe.  plot() keeps the reference's output
 (JET overlays in a 2-column grid written to preds/out%04d.png) using numpy/PIL
-when OpenCV is absent; expectation() keeps the reference's (dead, :45) math.
+when OpenCV is absent — cv2.normalize / addWeighted / circle(r=4, filled)
+restated; the JET table is analytic, so pixel parity with cv2 is unpinned;
+expectation() keeps the reference's (dead, :45) math and soft_argmax() is its
+fixed form on the GPU (hkp_soft_argmax).
 """
 import os
 
@@ -51,11 +54,53 @@ class Prediction:
 
     @staticmethod
     def _jet(u8):
-        x = u8.astype(np.float32) / 255.0
-        r = np.clip(1.5 - np.abs(4 * x - 3), 0, 1)
-        g = np.clip(1.5 - np.abs(4 * x - 2), 0, 1)
-        b = np.clip(1.5 - np.abs(4 * x - 1), 0, 1)
-        return (np.stack([b, g, r], -1) * 255).astype(np.uint8)  # BGR like cv2.COLORMAP_JET
+        x = u8.astype(np.float32) / np.float32(255.0)
+        r = np.clip(np.float32(1.5) - np.abs(np.float32(4) * x - np.float32(3)), 0, 1)
+        g = np.clip(np.float32(1.5) - np.abs(np.float32(4) * x - np.float32(2)), 0, 1)
+        b = np.clip(np.float32(1.5) - np.abs(np.float32(4) * x - np.float32(1)), 0, 1)
+        return (np.stack([b, g, r], -1) * np.float32(255)).astype(np.uint8)  # BGR like cv2.COLORMAP_JET
+
+    @staticmethod
+    def disc_halfwidths(r=4):
+        """Row half-widths of cv2.circle(img, c, r, color, -1) (LINE_8: OpenCV's
+        midpoint Circle rasteriser, imgproc/drawing.cpp) for rows |dy| = 0..r."""
+        hw = [-1] * (r + 1)
+        err, dx, dy, plus, minus = 0, r, 0, 1, 2 * r - 1
+        while dx >= dy:
+            hw[dy] = max(hw[dy], dx)
+            if dx <= r:
+                hw[dx] = max(hw[dx], dy)
+            dy += 1
+            err += plus
+            plus += 2
+            mask = -1 if err > 0 else 0
+            err -= minus & mask
+            dx += mask
+            minus -= mask & 2
+        return hw
+
+    @staticmethod
+    def _normalize_u8(h):
+        """cv2.normalize(h, None, 0, 255, NORM_MINMAX) (double scale / shift into a
+        float32 image), then .astype(np.uint8) (prediction.py:48)."""
+        mn, mx = float(h.min()), float(h.max())
+        sc = 255.0 / (mx - mn) if mx - mn > np.finfo(np.float64).eps else 0.0
+        v = (h.astype(np.float64) * sc + (0.0 - mn * sc)).astype(np.float32)
+        return np.clip(v, 0, 255).astype(np.uint8)
+
+    def soft_argmax(self, heatmaps, beta=1.0):
+        """float32 [B,K,2] (x, y) on the GPU: Prediction.expectation (prediction.py:31-38)
+        with its axis mix-up fixed — softmax(beta * h)-weighted mean position."""
+        from hkp import ops
+        return ops.soft_argmax(heatmaps.contiguous(), beta)
+
+    def expectation_fixed(self, d, beta=1.0):
+        """numpy restatement of soft_argmax for one [H,W] plane: (x, y) floats."""
+        d = np.asarray(d, dtype=np.float64)
+        e = np.exp(beta * d - np.max(beta * d))
+        p = e / e.sum()
+        ys, xs = np.mgrid[0:d.shape[0], 0:d.shape[1]]
+        return float((p * xs).sum()), float((p * ys).sum())
 
     def overlays(self, imgs_u8, heatmaps=None, keypoints=None):
         """Prediction.plot's picture for a whole batch on the GPU:
@@ -77,12 +122,15 @@ class Prediction:
                 pred_y, pred_x = (int(v) for v in keypoints[0][i])
             else:
                 pred_y, pred_x = np.unravel_index(h.argmax(), h.shape)
-            span = max(float(h.max() - h.min()), 1e-12)
-            vis = self._jet(((h - h.min()) / span * 255).astype(np.uint8))
-            overlay = (0.65 * img.astype(np.float32) + 0.35 * vis.astype(np.float32)).astype(np.uint8)
-            y0, y1 = max(0, pred_y - 4), min(overlay.shape[0], pred_y + 5)
-            x0, x1 = max(0, pred_x - 4), min(overlay.shape[1], pred_x + 5)
-            overlay[y0:y1, x0:x1] = 0
+            vis = self._jet(self._normalize_u8(h))
+            blend = np.float32(0.65) * img.astype(np.float32) + np.float32(0.35) * vis.astype(np.float32)
+            overlay = np.clip(np.rint(blend), 0, 255).astype(np.uint8)         # cv2.addWeighted
+            hw = self.disc_halfwidths(4)                                        # cv2.circle(.., 4, (0,0,0), -1)
+            for dy in range(-4, 5):
+                y = pred_y + dy
+                if 0 <= y < overlay.shape[0]:
+                    x0, x1 = max(0, pred_x - hw[abs(dy)]), min(overlay.shape[1], pred_x + hw[abs(dy)] + 1)
+                    overlay[y, x0:x1] = 0
             overlays.append(overlay)
         half = self.num_keypoints // 2
         col1 = np.concatenate(overlays[:half], 0) if half else None

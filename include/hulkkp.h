@@ -225,15 +225,25 @@ int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, int32_t H, 
                          hkp_stream_t stream);
 
 /* On-GPU visualisation (Prediction.plot, src/prediction.py:40-66):
- * per heatmap plane min-max → uint8 (truncating), JET colour map (BGR), blend
- * 0.65*img + 0.35*map (truncating), a black 9x9 dot at argmax_yx, tiled into the
- * reference's grid: planes k < K/2 stacked in column 0, the rest in column 1 —
- * out [n][H*K/2][2W][3] uint8 (K = 1: [n][H][W][3]; other odd K rejected, as the
+ * per heatmap plane cv2.normalize NORM_MINMAX → .astype(uint8) (double scale /
+ * shift, truncation), JET colour map (BGR; analytic — OpenCV's LUT is not in
+ * this image, so cv2-pixel parity is unpinned), cv2.addWeighted(img, 0.65, map,
+ * 0.35, 0) (rounded, saturated), a black filled radius-4 disc at argmax_yx as
+ * cv2.circle's midpoint rasteriser draws it, tiled into the reference's grid:
+ * planes k < K/2 stacked in column 0, the rest in column 1 — out
+ * [n][H*K/2][2W][3] uint8 (K = 1: [n][H][W][3]; other odd K rejected, as the
  * reference's hconcat of unequal columns fails).  heat NCHW [n,k,H,W] fp32,
  * img_nhwc [n,H,W,3] uint8 BGR, argmax_yx [n,k,2] int32 (hkp_upsample_sigmoid),
  * minmax_ws [n*k*2] floats of workspace. */
 int hkp_heat_overlay(int32_t n, int32_t k, int32_t H, int32_t W, const float* heat, const uint8_t* img_nhwc,
                      const int32_t* argmax_yx, float* minmax_ws, uint8_t* out, hkp_stream_t stream);
+
+/* Soft-argmax per heatmap plane, the reference's Prediction.expectation
+ * (src/prediction.py:31-38) with its axis mix-up fixed: p = softmax(beta * h)
+ * over the plane (beta = 1: the reference's softmax), out_xy[n][k] = (sum p*x,
+ * sum p*y) as fp32 from fp64 sums in fixed order (deterministic). */
+int hkp_soft_argmax(int32_t n, int32_t k, int32_t H, int32_t W, float beta, const float* heat, float* out_xy,
+                    hkp_stream_t stream);
 
 /* Gaussian target (src/dataset.py:36-44): out[n,k,H,W] (fp64) =
  * (double) expf( -((x-u)^2 + (y-v)^2) / (2 sigma^2) ) computed in fp32;

@@ -78,6 +78,12 @@ def test_device_batches(cuda_device, tmp_path):
     assert torch.equal(got, torch.from_numpy(imgs[order]))
     uvs = torch.cat([s[1] for s in seen])
     assert float(uvs[0, 0, 0]) == min(3.5 + order[0], W - 1) and float(uvs[0, 1, 0]) == 0.0   # clipped (dataset.py:65)
+    # decode workers (DataLoader processes): the same batches in the same order
+    for workers in (1, 3):
+        again = [(i.cpu(), u.cpu()) for i, u in DeviceBatches(ds, 2, shuffle=True, seed=3, workers=workers)]
+        assert len(again) == len(seen)
+        for (a, ua), (b, ub) in zip(again, seen):
+            assert torch.equal(a, b) and torch.equal(ua, ub)
 
 
 @pytest.mark.parametrize("k", [4, 1])
@@ -102,3 +108,20 @@ def test_overlays_match_plot(cuda_device, k, tmp_path):
     ov0 = pred.overlays(x8[:1], flat, yx0).cpu().numpy()[0]
     ref0 = pred.plot(u8[0], flat.cpu().numpy(), keypoints=yx0.cpu().numpy(), out_dir=str(tmp_path))
     assert np.array_equal(ov0, ref0)
+
+
+def test_soft_argmax_fixed(cuda_device):
+    """hkp_soft_argmax = Prediction.expectation (prediction.py:31-38) with the axis
+    mix-up fixed, against its numpy restatement; a sharp peak lands on the argmax."""
+    from src.prediction import Prediction
+    g = torch.Generator().manual_seed(5)
+    heat = torch.rand(2, 3, 37, 53, generator=g)
+    heat[1, 2, 20, 7] = 30.0
+    p = Prediction(None, 3, 37, 53, True)
+    for beta in (1.0, 40.0):
+        got = p.soft_argmax(heat.to(cuda_device), beta).cpu().numpy()
+        for b in range(2):
+            for k in range(3):
+                ref = p.expectation_fixed(heat[b, k].numpy(), beta)
+                np.testing.assert_allclose(got[b, k], ref, rtol=1e-5, atol=1e-4)
+    assert np.allclose(p.soft_argmax(heat.to(cuda_device), 40.0).cpu().numpy()[1, 2], [7.0, 20.0], atol=1e-3)

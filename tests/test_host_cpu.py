@@ -285,3 +285,47 @@ def test_bench_gpus_must_match_world_size():
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr, r.stderr
+
+
+def test_local_pretrained_import(tmp_path, monkeypatch):
+    """pretrained=True reads a torchvision-format ImageNet checkpoint from
+    $TORCH_HOME/hub/checkpoints (resnet.py:237-238 fetches the same file from
+    download.pytorch.org): backbone weights and BN buffers land in the model
+    (conv weights stored KRSC, state_dict OIHW), the 1000-way Linear fc of the
+    file is ignored and the 1x1 scoring conv keeps its N(0, 0.01) init
+    (resnet_dilated.py:15-22, applied after the load)."""
+    from oracle import cpu_ref, recipe
+    from src.model import KeypointsGauss
+    from src.resnet import model_files
+    sd = recipe.seeded_state_dict("resnet34", 77)
+    pre = "resnet.resnet34_8s."
+    tv = {k[len(pre):]: v for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    tv["fc.weight"] = torch.randn(1000, 512)          # torchvision: nn.Linear(512, 1000)
+    tv["fc.bias"] = torch.randn(1000)
+    ck = tmp_path / "hub" / "checkpoints"
+    ck.mkdir(parents=True)
+    torch.save(tv, ck / model_files["resnet34"])
+    monkeypatch.setenv("TORCH_HOME", str(tmp_path))
+    torch.manual_seed(0)
+    m = KeypointsGauss(4, pretrained=True)
+    got = m.state_dict()
+    for k, v in tv.items():
+        if k.startswith("fc."):
+            continue
+        assert torch.equal(got[pre + k], v), k
+    fc = got[pre + "fc.weight"]
+    assert fc.shape == (1000, 512, 1, 1) and abs(fc.std().item() - 0.01) < 1e-3 and got[pre + "fc.bias"].abs().max() == 0
+    # without the file: a warning, random init kept
+    monkeypatch.setenv("TORCH_HOME", str(tmp_path / "none"))
+    with pytest.warns(UserWarning, match="not found"):
+        KeypointsGauss(4, pretrained=True)
+
+
+def test_cv2_circle_disc_halfwidths():
+    """cv2.circle(img, c, 4, color, -1) as OpenCV's midpoint Circle rasteriser
+    (LINE_8) fills it: rows |dy| = 0..4 span ±4, ±3, ±3, ±2, ±0 — 49 pixels
+    (prediction.py:52; cv2 absent here, so pixel parity stays unpinned)."""
+    from src.prediction import Prediction
+    hw = Prediction.disc_halfwidths(4)
+    assert hw == [4, 3, 3, 2, 0]
+    assert sum(2 * h + 1 for h in hw[1:]) * 2 + 2 * hw[0] + 1 == 49
