@@ -12,9 +12,9 @@ echo "pytest ok"
 timeout -k 10 300 python -u bench.py > $O/bench_infer.log 2>&1
 timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline > $O/bench_train.log 2>&1
 echo "bench ok"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_infer -o run -- python3 bench.py --steps 10 --no-cpu-baseline > $O/prof_infer.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_infer -o run -- python3 bench.py --steps 10 --no-extras --no-cpu-baseline > $O/prof_infer.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run -- python3 bench.py --mode train --steps 10 --no-cpu-baseline > $O/prof_train.log 2>&1
 echo "kernel trace ok"
-bash tools/pmc_passes.sh $O/pmc_infer "--steps 5" "conv_x3"
+bash tools/pmc_passes.sh $O/pmc_infer "--steps 5 --no-extras" "conv_x3"
 bash tools/pmc_passes.sh $O/pmc_train "--mode train --steps 5" "conv_x3|wgrad_x3"
 echo "pmc ok"
