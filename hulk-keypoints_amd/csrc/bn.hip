@@ -141,19 +141,36 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
 // block input), 2 affine fp16 residual (the downsample conv's y with its BN).
 // The BN arithmetic itself is fp32 (x*alpha + beta, two roundings, as above).
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
-template <int RES, bool RELU>
+// FIX: the grid stride is a multiple of C/8, so every element a thread visits
+// has the same 8 channels — their scale/shift are loaded once, not per element
+// (16-32 scalar loads per 16-B vector otherwise).
+template <int RES, bool RELU, bool FIX>
 __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, const h16x8* __restrict__ y,
                                                            const float* __restrict__ ss, const h16x8* __restrict__ res,
                                                            const float* __restrict__ rss, h16x8* __restrict__ out,
                                                            f32x4* __restrict__ out32) {
     const int C = C8 * 8;
     const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
-        const int c0 = (int)(i % C8) * 8;
+    const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    float a[8], b[8], ra[8], rb[8];
+    auto load_ss = [&](int c0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            a[e] = ss[c0 + e];
+            b[e] = ss[C + c0 + e];
+            if constexpr (RES == 2) {
+                ra[e] = rss[c0 + e];
+                rb[e] = rss[C + c0 + e];
+            }
+        }
+    };
+    if constexpr (FIX) load_ss((int)(i0 % C8) * 8);
+    for (long i = i0; i < n8; i += stride) {
+        if constexpr (!FIX) load_ss((int)(i % C8) * 8);
         const h16x8 v = y[i];
         float o[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(__fmul_rn((float)v[e], ss[c0 + e]), ss[C + c0 + e]);
+        for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(__fmul_rn((float)v[e], a[e]), b[e]);
         if constexpr (RES == 1) {
             const h16x8 r = res[i];
 #pragma unroll
@@ -161,8 +178,7 @@ __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, cons
         } else if constexpr (RES == 2) {
             const h16x8 r = res[i];
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-                o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn((float)r[e], rss[c0 + e]), rss[C + c0 + e]));
+            for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn((float)r[e], ra[e]), rb[e]));
         }
         h16x8 h;
 #pragma unroll
@@ -334,9 +350,14 @@ extern "C" int hkp_bn_apply_f16(int64_t m, int32_t c, const uint16_t* y, const f
     hipStream_t st = as_stream(stream);
     const h16x8 *Y = (const h16x8*)y, *R = (const h16x8*)res;
     h16x8* O = (h16x8*)out;
-#define HKP_APPLY16(RES, RL)                                                                                    \
-    hipLaunchKernelGGL((bn_apply_f16_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n8, c / 8, Y, scale_shift, R, \
-                       res_scale_shift, O, (f32x4*)out32)
+    const bool fix = ((long)g * 256) % (c / 8) == 0;
+#define HKP_APPLY16(RES, RL)                                                                                       \
+    if (fix)                                                                                                       \
+        hipLaunchKernelGGL((bn_apply_f16_kernel<RES, RL, true>), dim3(g), dim3(256), 0, st, n8, c / 8, Y,          \
+                           scale_shift, R, res_scale_shift, O, (f32x4*)out32);                                     \
+    else                                                                                                           \
+        hipLaunchKernelGGL((bn_apply_f16_kernel<RES, RL, false>), dim3(g), dim3(256), 0, st, n8, c / 8, Y,         \
+                           scale_shift, R, res_scale_shift, O, (f32x4*)out32)
     if (!res) {
         if (relu) HKP_APPLY16(0, true); else HKP_APPLY16(0, false);
     } else if (!res_scale_shift) {

@@ -57,6 +57,140 @@ __global__ __launch_bounds__(256) void head_fc_kernel(int npix, int hw, int C, i
     }
 }
 
+// Sum of v[0..KP) over the 64 lanes of a wave, reduce-scatter form: at offset
+// 32, 16, ... each lane keeps half of its values (plus its partner's copy of
+// that half) until one is left, then the remaining offsets fold it whole —
+// KP-1 + log2(64/KP) shuffles instead of 6 per value.  Lane l ends with the
+// sum for k = ksel(l); the fold order is fixed (deterministic).
+template <int KP>
+__device__ __forceinline__ float wave_reduce_scatter(float (&v)[KP], int lane) {
+    int o = 32;
+#pragma unroll
+    for (int n = KP; n > 1; n >>= 1, o >>= 1) {
+        const int half = n >> 1;
+        const bool upper = (lane & o) != 0;
+#pragma unroll
+        for (int i = 0; i < half; ++i) {
+            const float send = upper ? v[i] : v[half + i];
+            const float keep = upper ? v[half + i] : v[i];
+            v[i] = keep + __shfl_xor(send, o);
+        }
+    }
+    float s = v[0];
+    for (; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    return s;
+}
+
+// the k whose total lane l holds after wave_reduce_scatter<KP>
+template <int KP>
+__device__ __forceinline__ int wave_reduce_scatter_k(int lane) {
+    int k = 0, o = 32;
+#pragma unroll
+    for (int n = KP; n > 1; n >>= 1, o >>= 1) k += (lane & o) ? (n >> 1) : 0;
+    return k;
+}
+
+// Inference tail: the last block's BN apply (+ residual, ReLU; the arithmetic of
+// hkp_bn_apply / hkp_bn_apply_f16 exactly) fused with the K-row head, so the
+// backbone's final activation (the only fp32 feature map of the forward: 315 MB
+// at C2, 5 GB at C4) is never written nor read back.  A lane owns 8 channels,
+// a wave 512, G = C/512 waves one pixel; each wave group runs PB pixels per
+// iteration (their loads in flight together), folds each pixel's K partial dots
+// with wave_reduce_scatter, and the G waves' totals are summed in wave order
+// through LDS.  YH: y (and a raw residual) fp16 (config C4) instead of fp32.
+// RES: 0 none, 1 raw residual, 2 residual*rscale + rshift, 3 packed split (hi+lo)
+// raw residual (fp32 path).
+constexpr int HEAD_PB = 4;
+template <bool YH, int RES, int KP>
+__global__ __launch_bounds__(256) void bn_apply_head_kernel(long M, int hw, int C, int K, const void* __restrict__ yv,
+                                                            const float* __restrict__ ss, const void* __restrict__ resv,
+                                                            const float* __restrict__ rss, const float* __restrict__ w,
+                                                            const float* __restrict__ bias, float* __restrict__ low) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    __shared__ float red[4][HEAD_PB][KP];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int G = C >> 9, GPB = 4 / G;                       // waves per pixel, pixel groups per block
+    const int c0 = (wv % G) * 512 + lane * 8;
+    float sc[8], sh[8], rsc[8], rsh[8], wk[KP][8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sc[e] = ss[c0 + e];
+        sh[e] = ss[C + c0 + e];
+        rsc[e] = RES == 2 ? rss[c0 + e] : 0.f;
+        rsh[e] = RES == 2 ? rss[C + c0 + e] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) wk[k][e] = k < K ? w[(long)k * C + c0 + e] : 0.f;
+    }
+    const long chunks = (M + HEAD_PB - 1) / HEAD_PB;
+    const int ks = wave_reduce_scatter_k<KP>(lane);
+    constexpr int LOW_LANES = 64 / KP;                       // lanes holding the same k after the fold
+    for (long ch0 = (long)blockIdx.x * GPB; ch0 < chunks; ch0 += (long)gridDim.x * GPB) {
+        const long ch = ch0 + wv / G;
+        float v[HEAD_PB][8], r[HEAD_PB][8];
+#pragma unroll
+        for (int u = 0; u < HEAD_PB; ++u) {
+            const long p = ch * HEAD_PB + u;
+            const bool ok = ch < chunks && p < M;
+            const long e0 = (ok ? p : 0) * C + c0;
+            if constexpr (YH) {
+                const h8 t = ok ? *(const h8*)((const _Float16*)yv + e0) : h8{};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[u][e] = (float)t[e];
+            } else {
+                const f32x4 a = ok ? *(const f32x4*)((const float*)yv + e0) : f32x4{};
+                const f32x4 b = ok ? *(const f32x4*)((const float*)yv + e0 + 4) : f32x4{};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { v[u][e] = a[e]; v[u][4 + e] = b[e]; }
+            }
+            if constexpr (RES == 3) {
+                const long off = 2 * e0 - (e0 & 31);
+                const h8 h = ok ? *(const h8*)((const _Float16*)resv + off) : h8{};
+                const h8 l = ok ? *(const h8*)((const _Float16*)resv + off + 32) : h8{};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) r[u][e] = __fadd_rn((float)h[e], (float)l[e]);
+            } else if constexpr (RES != 0 && YH) {
+                const h8 t = ok ? *(const h8*)((const _Float16*)resv + e0) : h8{};
+#pragma unroll
+                for (int e = 0; e < 8; ++e) r[u][e] = (float)t[e];
+            } else if constexpr (RES != 0) {
+                const f32x4 a = ok ? *(const f32x4*)((const float*)resv + e0) : f32x4{};
+                const f32x4 b = ok ? *(const f32x4*)((const float*)resv + e0 + 4) : f32x4{};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) { r[u][e] = a[e]; r[u][4 + e] = b[e]; }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < HEAD_PB; ++u) {
+            float part[KP];
+#pragma unroll
+            for (int k = 0; k < KP; ++k) part[k] = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float o = __fadd_rn(__fmul_rn(v[u][e], sc[e]), sh[e]);
+                if constexpr (RES == 1 || RES == 3) o = __fadd_rn(o, r[u][e]);
+                else if constexpr (RES == 2) o = __fadd_rn(o, __fadd_rn(__fmul_rn(r[u][e], rsc[e]), rsh[e]));
+                o = o > 0.f ? o : 0.f;
+#pragma unroll
+                for (int k = 0; k < KP; ++k) part[k] = __fadd_rn(part[k], __fmul_rn(o, wk[k][e]));
+            }
+            const float s = wave_reduce_scatter<KP>(part, lane);
+            if (lane % LOW_LANES == 0) red[wv][u][ks] = s;
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < GPB * HEAD_PB * K; t += 256) {
+            const int g = t / (HEAD_PB * K), rem = t - g * HEAD_PB * K, u = rem / K, k = rem - u * K;
+            const long p = (ch0 + g) * HEAD_PB + u;
+            if (ch0 + g < chunks && p < M) {
+                float s = red[g * G][u][k];
+                for (int i = 1; i < G; ++i) s = __fadd_rn(s, red[g * G + i][u][k]);
+                const long n = p / hw, q = p - n * hw;
+                low[(n * K + k) * hw + q] = __fadd_rn(s, bias[k]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 struct Lerp {
     int i0, i1;
     float l0, l1;
@@ -226,6 +360,41 @@ extern "C" int hkp_head_fc(int32_t n, int32_t hw, int32_t c, int32_t k, const fl
     else
         hipLaunchKernelGGL(head_fc_kernel<16>, dim3(grid), dim3(256), lds, st, npix, hw, c, k, feat, w, bias, lowres);
     HKP_LAUNCH_CHECK("hkp_head_fc");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_apply_head(int32_t n, int32_t hw, int32_t c, int32_t k, int32_t y_f16, const void* y,
+                                 const float* scale_shift, const void* res, const float* res_scale_shift,
+                                 int32_t res_kind, const float* w, const float* bias, float* lowres,
+                                 hkp_stream_t stream) {
+    HKP_CHECK_ARG(n > 0 && hw > 0 && k > 0 && k <= 16, "hkp_bn_apply_head: bad sizes (n=%d hw=%d k=%d)", n, hw, k);
+    HKP_CHECK_ARG(c > 0 && c % 512 == 0 && c <= 2048, "hkp_bn_apply_head: need c %% 512 == 0 and c <= 2048 (c=%d)", c);
+    HKP_CHECK_ARG(y && scale_shift && w && bias && lowres, "hkp_bn_apply_head: null tensor");
+    HKP_CHECK_ARG(res_kind >= 0 && res_kind <= 3 && (res_kind == 0) == (res == nullptr) &&
+                      (res_kind == 2) == (res_scale_shift != nullptr) && !(res_kind == 3 && y_f16),
+                  "hkp_bn_apply_head: bad residual (kind %d)", res_kind);
+    const long M = (long)n * hw;
+    const int gpb = 4 / (c / 512);
+    long chunks = (M + HEAD_PB - 1) / HEAD_PB;
+    long g = (chunks + gpb - 1) / gpb;
+    if (g > 256L * 8) g = 256L * 8;
+    hipStream_t st = as_stream(stream);
+#define HKP_AH(YH, RES, KP)                                                                                       \
+    hipLaunchKernelGGL((bn_apply_head_kernel<YH, RES, KP>), dim3((unsigned)g), dim3(256), 0, st, M, hw, c, k, y, \
+                       scale_shift, res, res_scale_shift, w, bias, lowres)
+#define HKP_AH_K(YH, RES) \
+    if (k <= 4) HKP_AH(YH, RES, 4); else if (k <= 8) HKP_AH(YH, RES, 8); else HKP_AH(YH, RES, 16)
+    if (y_f16) {
+        if (res_kind == 0) HKP_AH_K(true, 0); else if (res_kind == 1) HKP_AH_K(true, 1); else HKP_AH_K(true, 2);
+    } else {
+        if (res_kind == 0) HKP_AH_K(false, 0);
+        else if (res_kind == 1) HKP_AH_K(false, 1);
+        else if (res_kind == 2) HKP_AH_K(false, 2);
+        else HKP_AH_K(false, 3);
+    }
+#undef HKP_AH_K
+#undef HKP_AH
+    HKP_LAUNCH_CHECK("hkp_bn_apply_head");
     return HKP_OK;
 }
 

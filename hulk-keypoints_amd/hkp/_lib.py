@@ -64,6 +64,7 @@ SIGNATURES = {
     "hkp_bn_apply_f16": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "hkp_bn_apply_head": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
     "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),

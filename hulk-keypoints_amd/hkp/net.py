@@ -56,6 +56,7 @@ _split_cache = {}
 # (id(resnet), flip) → the last prepack_x3 launch that repacked every operand
 _prepack_plans = {}
 _NO_PREPACK_PLAN = os.environ.get("HKP_NO_PREPACK_PLAN") == "1"     # A/B: always rebuild
+_UNFUSED_HEAD = os.environ.get("HKP_UNFUSED_HEAD") == "1"           # A/B: bn_apply + head_fc
 
 
 def _cache_slot(w):
@@ -276,11 +277,13 @@ def stem_forward(resnet, x_nchw, trace=None):
     return out
 
 
-def block_forward(block, x, trace=None, final=False):
+def block_forward(block, x, trace=None, final=False, head=None):
     """One BasicBlock / Bottleneck.  x: fp32 NHWC (with its split attached) or, in
     inference, a split-only activation.  In inference the block output is written
     split-only too unless `final` (the head reads fp32): the next block's convs
-    read the split and its residual add reads hi + lo."""
+    read the split and its residual add reads hi + lo.  head = (w [K,C], bias [K])
+    (inference, last block): the tail BN apply runs fused with the K-row head and
+    the block returns the lowres logits instead (hkp_bn_apply_head)."""
     rec = {} if trace is not None else None
     # producers also write the next conv's operand split; an activation only a
     # conv consumes (inside the block, no backward trace) is written split-only
@@ -314,6 +317,13 @@ def block_forward(block, x, trace=None, final=False):
             rec.update(x=x, y=[y1, y2, y3], ss=[s1, s2, s3], mi=[m1, m2, m3], act=[a1, a2])
     pl = _split_for(last_y.shape[-1])
     keep_out = keep or final or pl != 3
+    if head is not None:
+        if last_y.dtype == torch.float16 and x.dtype != torch.float16:
+            x = ops.split_of(x)[0]
+        if block.downsample is not None:
+            yd, sd, _ = conv_bn(block.downsample[0], block.downsample[1], x)
+            return ops.bn_apply_head(last_y, last_s, yd, sd, *head)
+        return ops.bn_apply_head(last_y, last_s, x, None, *head)
     if last_y.dtype == torch.float16:                 # plain-fp16 path: fp16 residual stream
         res = x if x.dtype == torch.float16 else ops.split_of(x)[0]
         if block.downsample is not None:
@@ -333,16 +343,24 @@ def block_forward(block, x, trace=None, final=False):
     return out
 
 
-def backbone_forward(resnet, x_nchw, trace=None):
+def backbone_forward(resnet, x_nchw, trace=None, head=None):
     """ResNet.forward up to the fc (src/resnet.py:198-213), NHWC output.  x_nchw:
-    the [B,3,H,W] fp32 image or the [B,H,W,3] uint8 batch (see _image_input)."""
+    the [B,3,H,W] fp32 image or the [B,H,W,3] uint8 batch (see _image_input).
+    head = (w [K,C], bias [K]) (inference): returns the head's lowres logits
+    [B,K,h,w] instead, the last block's BN apply fused with the head."""
     x_in = _image_input(resnet, x_nchw, trace)
     prepack_x3(resnet, flip=trace is not None)
     x = stem_forward(resnet, x_in, trace)
     blocks = [b for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4) for b in layer]
     for i, block in enumerate(blocks):
-        x = block_forward(block, x, trace, final=i == len(blocks) - 1)
+        last = i == len(blocks) - 1
+        x = block_forward(block, x, trace, final=last, head=head if last else None)
     return x
+
+
+def _feat_channels(resnet):
+    last = resnet.layer4[-1]
+    return (last.conv3 if last.kind == "bottleneck" else last.conv2).weight.shape[0]
 
 
 def fc_rows(resnet, k):
@@ -355,9 +373,12 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
     """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
     if trace is not None and _precision == "f16":
         raise ops.HkpError("precision 'f16' (BASELINE config C4) is inference-only; train with 'f16x3' or 'fp32'")
-    feat = backbone_forward(resnet, x_nchw, trace)
     w, b = fc_rows(resnet, k)
-    low = ops.head_fc(feat, w, b)
+    if trace is None and not _UNFUSED_HEAD and ops.head_fusable(_feat_channels(resnet), k):
+        feat, low = None, backbone_forward(resnet, x_nchw, None, head=(w, b))
+    else:
+        feat = backbone_forward(resnet, x_nchw, trace)
+        low = ops.head_fc(feat, w, b)
     H, W = image_nchw_shape(x_nchw)[2:]
     hm, yx = ops.upsample_sigmoid(low, H, W, heat=heat, argmax=argmax)
     if trace is not None:

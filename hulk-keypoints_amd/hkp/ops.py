@@ -532,6 +532,48 @@ def head_fc(feat, w_kc, bias_k):
     return low
 
 
+def head_fusable(c, k):
+    """hkp_bn_apply_head covers this (channels, keypoints) pair."""
+    return c % 512 == 0 and c <= 2048 and 0 < k <= 16
+
+
+def bn_apply_head(y, ss, res, res_ss, w_kc, bias_k):
+    """Inference tail: lowres [N,K,h,w] = head_fc(relu(y*scale+shift + residual))
+    without writing the feature map.  y fp32 or fp16 NHWC; res: None, a raw
+    residual of y's dtype, a packed split-only activation (fp32 y), or (with
+    res_ss) the downsample's y."""
+    n, h, w, c = y.shape
+    k = w_kc.shape[0]
+    if y.dtype not in (torch.float32, torch.float16):
+        raise HkpError("bn_apply_head: y must be fp32 or fp16")
+    _need(y, y.dtype, "bn_apply_head.y", 4)
+    _need(w_kc, torch.float32, "bn_apply_head.w", 2)
+    _need(bias_k, torch.float32, "bn_apply_head.bias", 1)
+    if not head_fusable(c, k) or w_kc.shape[1] != c or bias_k.numel() != k or ss.numel() != 2 * c:
+        raise HkpError("bn_apply_head: C=%d K=%d weight %s bias %d ss %d" % (c, k, tuple(w_kc.shape), bias_k.numel(),
+                                                                         ss.numel()))
+    kind = 0
+    if res is not None:
+        if res.dtype == torch.float16 and y.dtype == torch.float32:
+            if res_ss is not None or getattr(res, "_hkp_split_passes", 0) != 3 or res.shape[-1] != 2 * c:
+                raise HkpError("bn_apply_head: a split residual must be a packed (split=3) raw residual")
+            kind = 3
+        else:
+            if res.dtype != y.dtype or res.shape != y.shape:
+                raise HkpError("bn_apply_head: residual %s %s vs y %s %s" % (res.dtype, tuple(res.shape), y.dtype,
+                                                                           tuple(y.shape)))
+            kind = 2 if res_ss is not None else 1
+        _need(res, res.dtype, "bn_apply_head.res")
+        if tuple(res.shape[:-1]) != tuple(y.shape[:-1]):
+            raise HkpError("bn_apply_head: residual pixels %s vs %s" % (tuple(res.shape), tuple(y.shape)))
+    if res_ss is not None and (res is None or res_ss.numel() != 2 * c):
+        raise HkpError("bn_apply_head: res_scale_shift needs a residual and 2C entries")
+    low = torch.empty((n, k, h, w), device=y.device, dtype=torch.float32)
+    call("hkp_bn_apply_head", n, h * w, c, k, int(y.dtype == torch.float16), _ptr(y), _ptr(ss), _ptr(res),
+         _ptr(res_ss), kind, _ptr(w_kc), _ptr(bias_k), _ptr(low), _stream())
+    return low
+
+
 def upsample_sigmoid(low, H, W, heat=True, argmax=True, sigmoid=True, out=None):
     """lowres [N,K,h,w] → (heat [N,K,H,W] (into out when given) or None, argmax
     int32 [N,K,2] (y,x) or None)."""

@@ -212,6 +212,18 @@ int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, const float*
 int hkp_head_fc(int32_t n, int32_t hw, int32_t c, int32_t k, const float* feat, const float* w,
                 const float* bias, float* lowres, hkp_stream_t stream);
 
+/* Inference tail: the last block's BN apply (+ residual, ReLU — hkp_bn_apply /
+ * hkp_bn_apply_f16's arithmetic) fused with hkp_head_fc, so the final feature
+ * map is never written (src/resnet.py:110-112 / :68-69 of the last block, then
+ * src/resnet_dilated.py:16 sliced to the K rows src/model.py:21 keeps).
+ * y [n*hw][c] fp32 (y_f16 = 0) or fp16 (y_f16 = 1); res_kind 0: none, 1: raw
+ * residual of y's dtype, 2: residual * rscale + rshift (res_scale_shift [2c]),
+ * 3: packed split raw residual (fp32 y only); w [k][c], bias [k] →
+ * lowres [n][k][hw].  Needs c % 512 == 0, c <= 2048, k <= 16. */
+int hkp_bn_apply_head(int32_t n, int32_t hw, int32_t c, int32_t k, int32_t y_f16, const void* y,
+                      const float* scale_shift, const void* res, const float* res_scale_shift, int32_t res_kind,
+                      const float* w, const float* bias, float* lowres, hkp_stream_t stream);
+
 /* bilinear align_corners=True upsample [n,k,h,w] → [n,k,H,W]
  * (src/resnet_dilated.py:27) + sigmoid (src/model.py:21; skipped when
  * apply_sigmoid == 0, the raw Resnet34_8s.forward output), NCHW output (nullable),

@@ -162,6 +162,54 @@ def test_head_fc(cuda_device):
     assert (low.cpu() - ref).abs().max() < 1e-5
 
 
+HEAD_CASES = [
+    # n, h, w, C, K, y dtype, residual kind (0 none, 1 raw, 2 affine, 3 packed split)
+    (2, 7, 9, 512, 4, "f32", 3),      # C2's last BasicBlock (split-only residual stream)
+    (1, 5, 13, 512, 4, "f32", 1),     # fp32 residual (fp32 precision mode)
+    (1, 6, 6, 512, 16, "f32", 2),     # downsample residual, K = 16
+    (1, 3, 5, 1024, 8, "f32", 0),     # two waves per pixel, ragged M (15 pixels)
+    (2, 5, 7, 2048, 8, "f16", 1),     # C4's last Bottleneck (fp16 residual stream)
+    (1, 4, 9, 2048, 3, "f16", 2),     # K = 3 < KP
+]
+
+
+@pytest.mark.parametrize("case", HEAD_CASES)
+def test_bn_apply_head_fused(cuda_device, case):
+    """hkp_bn_apply_head = the final block's BN apply (+ residual, ReLU) followed by
+    the K-row head, against the same two steps in float64 (and the activation it
+    fuses is exactly hkp_bn_apply's / hkp_bn_apply_f16's)."""
+    from hkp import ops
+    n, h, w, c, k, yt, kind = case
+    dt = torch.float16 if yt == "f16" else torch.float32
+    y = rand(n, h, w, c, seed=11).to(dt)
+    ss = torch.cat([rand(c, seed=12) * 0.5 + 1.0, rand(c, seed=13) * 0.3])
+    res = rss = None
+    res_dev = None
+    if kind in (1, 2):
+        res = rand(n, h, w, c, seed=14).to(dt)
+        res_dev = res.to(cuda_device)
+    if kind == 2:
+        rss = torch.cat([rand(c, seed=15) * 0.5 + 1.0, rand(c, seed=16) * 0.3])
+    if kind == 3:
+        res = rand(n, h, w, c, seed=14)
+        res_dev = ops.split_pack_x3(res.to(cuda_device))
+        hi = res.half().float()
+        res = hi + (res - hi).half().float()           # what the packed pair holds
+    wk = rand(k, c, seed=17) * 0.05
+    bk = rand(k, seed=18)
+    low = ops.bn_apply_head(y.to(cuda_device), ss.to(cuda_device), res_dev,
+                            None if rss is None else rss.to(cuda_device), wk.to(cuda_device), bk.to(cuda_device))
+    o = y.double() * ss[:c].double() + ss[c:].double()
+    if res is not None:
+        r = res.double()
+        o = o + (r * rss[:c].double() + rss[c:].double() if rss is not None else r)
+    o = o.clamp_min(0)
+    ref = torch.einsum("nhwc,kc->nkhw", o, wk.double()) + bk.double()[None, :, None, None]
+    got = low.cpu().double()
+    assert got.shape == ref.shape
+    assert (got - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+
+
 def test_gauss_target_matches_reference(cuda_device, golden):
     from hkp import ops
     g = golden("gauss")
