@@ -80,7 +80,14 @@ struct X3Args {
     long sk_units = 0;
     float* sk_ws = nullptr;
     unsigned* sk_cnt = nullptr;
+    unsigned long long* stamps = nullptr;   // debug: per-block phase clocks (hkp_debug_x3_stamps)
 };
+
+// debug phase stamps (s_memrealtime, 100 MHz) of one-tile conv blocks: slot k of
+// block b at stamps[b * 8 + k]; written by lane 0 of wave 0
+__device__ __forceinline__ void x3_stamp(const X3Args& a, int k) {
+    if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // 2^e putting max|x| in [2^13, 2^14) (1 for 0 / non-finite): exact scaling
 __device__ __forceinline__ float pow2_scale_of(float m) {
@@ -100,8 +107,37 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// workgroup barrier for LDS traffic only: this wave's LDS ops retired, no
+// vmcnt(0) — __syncthreads() would also wait for every global store of the
+// epilogue to complete (~2-5 us under the other CUs' output writes)
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_barrier();
+}
+
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
     __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+// LDS-DMA through a raw buffer resource: address = base + soffset + voffset; a
+// voffset >= num_records (soffset is not range-checked) loads zeros — the
+// out-of-image taps and the rows past M cost one v_cndmask instead of a 64-bit
+// address select, and the per-K-step tap offset rides in the scalar soffset.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+extern "C" __device__ void hkp_raw_buffer_load_lds(i32x4 rsrc, __attribute__((address_space(3))) void* lds, int size,
+                                                   int voffset, int soffset, int offset,
+                                                   int aux) __asm("llvm.amdgcn.raw.buffer.load.lds");
+__device__ __forceinline__ i32x4 buffer_rsrc(const void* base, unsigned bytes) {
+    const unsigned long long p = (unsigned long long)base;
+    i32x4 r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(unsigned)p);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(unsigned)(p >> 32) & 0xFFFF);   // stride 0
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);                          // num_records
+    r[3] = 0x00020000;                                                            // gfx9 raw-buffer config
+    return r;
+}
+__device__ __forceinline__ void blds16(i32x4 rsrc, unsigned voff, unsigned soff, char* lds_wave_base) {
+    hkp_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_wave_base, 16, (int)voff, (int)soff, 0, 0);
 }
 
 // schedule NM MFMAs and NR ds_reads of one basic block as evenly spread
@@ -124,6 +160,18 @@ __device__ __forceinline__ void interleave() {
 // 256x64 tiles and the stem) 2, otherwise 3.  The whole 160 KiB at most (the
 // stream-K flag reuses the drained ring).
 constexpr int x3_nst(int BN, bool PAIR) { return (BN == 256 || PAIR) ? 2 : 3; }
+
+// the ring, or (P = 1) the staged fp16 output tile if that is larger (256x256: 132 KiB)
+constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
+    return P == 1 && 256 * (BN + 8) * 2 > x3_nst(BN, PAIR) * (256 + BN) * 128 ? 256 * (BN + 8) * 2
+                                                                              : x3_nst(BN, PAIR) * (256 + BN) * 128;
+}
+// BN-partials scratch (x3_bn_partials_w: [2][WM][BN] floats) past the ring, so
+// the epilogue needs no barrier before it, then the tile's BN column scales
+// (loaded during the pipeline fill: a global load in the epilogue waited ~4 us
+// behind the other CUs' output writes); the two-blocks-per-CU tiles (PAIR) have
+// no LDS to spare: they reuse the ring after a barrier and load scales late
+constexpr int x3_red_bytes(int BN, bool PAIR) { return PAIR ? 0 : 2 * 4 * BN * 4 + BN * 4; }
 
 // ---- stream-K bookkeeping (X3Args::sk_units) ----
 __device__ __forceinline__ long sk_start(long b, long U, int G) { return b * U / G; }
@@ -298,6 +346,116 @@ __device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int 
     }
 }
 
+// BN tile partials, one barrier, VALU-lean (a wave64 VALU op costs 4 cycles;
+// the first version's ~1700 per wave, mostly row masks and selects, took ~6 us
+// per tile): each lane reduces its own NI*NR rows of a column to (sum, M2 about
+// its own mean) in registers — on f32x4 vectors (packed fp32 ops), without row
+// masks when all 64 rows of the wave are valid (every tile but the last) — the
+// lane groups of a column merge pairwise by Chan's formula over log2(64/CW)
+// shuffle steps (sums and M2s are symmetric in the pair, so both lanes get the
+// same bits), and the two waves of a 128-row half merge through a small LDS
+// scratch (red: [2][WM][BN] floats, outside anything still being read):
+//   n = na + nb,  sum = sa + sb,  M2 = M2a + M2b + (mb - ma)^2 * na*nb / n.
+// Same quantities as x3_bn_partials (sum, M2 about the half-tile mean).
+// VEC(i, j): the f32x4 of accumulator rows ROW(i, 0..3) of column block j.
+// SC(j): the column's output scale (a power of two: sums scale by it, M2 by its
+// square, exactly) when VEC is the unscaled accumulator.
+template <int BN, int NI, int NJ, int CW, int SHF, typename Vec, typename Row, typename Sc>
+__device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, int m0, int n0, int wm, int wn,
+                                                 int lane, Vec&& vec, Row&& row, Sc&& sc_of) {
+    float* rs = red;                                                 // [WM][BN] wave sums
+    float* rq = red + 4 * BN;                                        // [WM][BN] wave M2
+    const int nw = min(64, max(0, a.M - (m0 + 64 * wm)));          // valid rows of this wave (a prefix)
+    float ls[NJ], lq[NJ], ln;
+    if (nw == 64) {                                                  // every row valid: no masks
+        ln = (float)(NI * 4);
+        constexpr float inv = 1.f / (NI * 4);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            f32x4 s4 = vec(0, j);
+#pragma unroll
+            for (int i = 1; i < NI; ++i) s4 += vec(i, j);
+            const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            const f32x4 mu = {s * inv, s * inv, s * inv, s * inv};
+            f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const f32x4 d = vec(i, j) - mu;
+                q4 += d * d;
+            }
+            ls[j] = s;
+            lq[j] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+        }
+    } else {
+        ln = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ln += (row(i, r) < a.M) ? 1.f : 0.f;
+        const float linv = ln > 0.f ? 1.f / ln : 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s += (row(i, r) < a.M) ? vec(i, j)[r] : 0.f;
+            const float mu = s * linv;
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float d = vec(i, j)[r] - mu;
+                    q += (row(i, r) < a.M) ? d * d : 0.f;
+                }
+            ls[j] = s;
+            lq[j] = q;
+        }
+    }
+    // pairwise Chan merge across the lane groups of a column (counts ride along)
+    for (int o = SHF; o < 64; o <<= 1) {
+        const float nb = __shfl_xor(ln, o);
+        const float nt = ln + nb;
+        const float f = nt > 0.f ? ln * nb / nt : 0.f;
+        const float ia = ln > 0.f ? 1.f / ln : 0.f, ib = nb > 0.f ? 1.f / nb : 0.f;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const float sb = __shfl_xor(ls[j], o), qb = __shfl_xor(lq[j], o);
+            const float d = sb * ib - ls[j] * ia;
+            ls[j] = ls[j] + sb;
+            lq[j] = (lq[j] + qb) + d * d * f;
+        }
+        ln = nt;
+    }
+    if (lane < CW) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = wn * NJ * CW + j * CW + lane;
+            rs[wm * BN + c] = ls[j];
+            rq[wm * BN + c] = lq[j];
+        }
+    }
+    lds_sync();
+    const int nb = min(64, max(0, a.M - (m0 + 64 * (wm | 1))));     // valid rows of the odd wave of the half
+    if ((wm & 1) || nw == 0 || lane >= CW) return;
+    const long tile128 = (long)(m0 >> 7) + (wm >> 1);
+    const float ia = 1.f / (float)nw, ib = nb > 0 ? 1.f / (float)nb : 0.f;
+    const float f = (float)nw * (float)nb / (float)(nw + nb);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int c = wn * NJ * CW + j * CW + lane;
+        const float sa = rs[wm * BN + c], qa = rq[wm * BN + c];
+        const float sb = rs[(wm + 1) * BN + c], qb = rq[(wm + 1) * BN + c];
+        const float d = sb * ib - sa * ia;
+        const float sum = nb > 0 ? sa + sb : sa;
+        const float m2 = nb > 0 ? (qa + qb) + d * d * f : qa;
+        const float sc = sc_of(j);
+        a.part[(tile128 * a.K + n0 + c) * 2 + 0] = sum * sc;
+        a.part[(tile128 * a.K + n0 + c) * 2 + 1] = m2 * (sc * sc);
+    }
+}
+
 // fp16 output tile staged in LDS ([256][BN + 8] halves: the 16-B row pad makes
 // the fragment-layout ds_write_b16s conflict-free) and written as whole 16-B
 // row chunks: 8x fewer store instructions than per-element fp16 stores, full
@@ -333,6 +491,18 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
     constexpr int NMC = (P == 3 ? 3 : 2) * UM;      // MFMAs per column block per K-step
+    constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
+    constexpr int RED_OFF = PAIRB ? 0 : x3_lds_bytes(BN, PAIRB, P);
+    float* const scl = (float*)(smem + RED_OFF + 2 * 4 * BN * 4);   // [BN] column scales (!PAIRB)
+    float sclv = 1.f;                              // issued before the fill, stored after it
+    if constexpr (!PAIRB) {
+        if (tid < BN) sclv = (a.wscale ? a.wscale[n0 + tid] : 1.f) * (a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f);
+    }
+    auto store_scl = [&]() {
+        if constexpr (!PAIRB) {
+            if (tid < BN) scl[tid] = sclv;
+        }
+    };
     const int r16 = lane & 15, q = lane >> 4;
     const int sw = (r16 >> 1) & 7;                 // the DMA's swizzle of every row ≡ r16 (mod 16)
     const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
@@ -389,9 +559,11 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         // t+1 (its latency covered by the SIMD's other wave)
         issue_next();
         if (nks > 1) issue_next();
+        store_scl();
         if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
+        x3_stamp(a, 1);
         FA fa;
         read_a(fa, smem);
 #pragma unroll
@@ -424,6 +596,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         issue_next();
         for (int s = 1; s < NST - 1; ++s)
             if (s < nks) issue_next();
+        store_scl();
         {
             const int after = std::min(nks - 1, NST - 2);
             if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
@@ -475,28 +648,32 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the ring past here
+    x3_stamp(a, 2);
 
     if (partial) {                         // stream-K: fold the tile's segments
         auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
         auto set = [&](int v, f32x4 y) { acc[v / UN][v % UN] = y; };
         if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return;
     }
-    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
     const int rbase = m0 + wm * UM * 16 + 4 * q;
-    if constexpr (P == 1) {                // fp16 output: scale, partials, LDS-staged store
+    // column scale (weight scale x gradient scale): the prefetched LDS copy, or
+    // (PAIRB) loaded now
+    auto col_scale = [&](int c) -> float {
+        if constexpr (PAIRB) return (a.wscale ? a.wscale[n0 + c] : 1.f) * (a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f);
+        else return scl[c];
+    };
+    if constexpr (P == 1) {                // fp16 output: partials, scale, LDS-staged store
+        float sc[UN];
 #pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            const float sc = (a.wscale ? a.wscale[n0 + wn * UN * 16 + j * 16 + r16] : 1.f) * ginv;
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc;
+        for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
+        if (a.part) {
+            if constexpr (PAIRB) lds_sync();           // the scratch is the ring
+            x3_bn_partials_w<BN, UM, UN, 16, 16>(
+                a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
+                [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
         }
-        if (a.part)
-            x3_bn_partials<BN, UM, UN, 4, 16, 16>(
-                a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
-                [&](int i, int r) { return rbase + i * 16 + r; });
-        __syncthreads();                   // the ring (or the partials' scratch) is free
+        lds_sync();                        // the ring is free
+        x3_stamp(a, 3);
         _Float16* t = (_Float16*)smem;
         constexpr int PITCH = BN + 8;
 #pragma unroll
@@ -506,38 +683,80 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     t[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * UN * 16 + j * 16 + r16] =
-                        (_Float16)acc[i][j][r];
-        __syncthreads();
+                        (_Float16)(acc[i][j][r] * sc[j]);
+        lds_sync();
+        x3_stamp(a, 4);
         x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
+        x3_stamp(a, 5);
         return;
     }
-    // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
+    // ---- epilogue (fp32 output): BN partials, then the scaled tile ----
+    float sc[UN];
 #pragma unroll
-    for (int j = 0; j < UN; ++j) {
-        const int n = n0 + wn * UN * 16 + j * 16 + r16;
-        const float sc = (a.wscale ? a.wscale[n] : 1.f) * ginv;
-        long off[UM][4];
-        float av[UM][4];
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) off[i][r] = x3_out_off(a, rbase + i * 16 + r, n);
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) av[i][r] = (a.add && off[i][r] >= 0) ? a.add[off[i][r]] : 0.f;
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                acc[i][j][r] *= sc;
-                x3_store(a, off[i][r], acc[i][j][r], av[i][r]);
-            }
+    for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
+    if (a.part) {
+        if constexpr (PAIRB) lds_sync();               // the scratch is the ring
+        x3_bn_partials_w<BN, UM, UN, 16, 16>(
+            a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
+            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
     }
-    if (a.part == nullptr) return;
-    x3_bn_partials<BN, UM, UN, 4, 16, 16>(
-        a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
-        [&](int i, int r) { return rbase + i * 16 + r; });
+    x3_stamp(a, 3);
+    if (!a.add && !a.ost) {
+        // Dense output: staged through the (drained) ring as fp32 rows and written
+        // as whole 16-B row chunks — 32 store instructions per thread, full 128-B
+        // lines.  The fragment-layout stores (128 4-B stores per thread, 64-B
+        // pieces) of every CU at once took ~34 us per C2 layer4 tile (10 %):
+        // more than a wave's 63 outstanding memory ops, so the waves stalled on
+        // their completion instead of ending and letting the next block start.
+        // 256-wide tiles stage half the rows per pass (128 KiB).
+        constexpr int PASSES = BN == 256 ? 2 : 1, RPP = 256 / PASSES, PITCH = BN + 4, C4 = BN / 4;
+        static_assert(RPP * PITCH * 4 <= x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB), "staging");
+        float* t = (float*)smem;
+        lds_sync();                                    // every wave done with the ring and the partials' scratch
+#pragma unroll
+        for (int h = 0; h < PASSES; ++h) {
+            if (PASSES == 1 || (wm >> 1) == h) {
+#pragma unroll
+                for (int i = 0; i < UM; ++i)
+#pragma unroll
+                    for (int j = 0; j < UN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            t[(wm * UM * 16 + i * 16 + 4 * q + r - h * RPP) * PITCH + wn * UN * 16 + j * 16 + r16] =
+                                acc[i][j][r] * sc[j];
+            }
+            lds_sync();
+#pragma unroll 4
+            for (int e = tid; e < RPP * C4; e += 512) {
+                const int row = e / C4, c4 = e - row * C4;
+                const int m = m0 + h * RPP + row;
+                if (m < a.M) *(f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4) = *(const f32x4*)(t + row * PITCH + c4 * 4);
+            }
+            if (h + 1 < PASSES) lds_sync();            // the next pass overwrites the rows just read
+        }
+    } else {
+        // phase outputs (strided dgrad) / addend: per element, from the fragments
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            const int n = n0 + wn * UN * 16 + j * 16 + r16;
+            long off[UM][4];
+            float av[UM][4];
+#pragma unroll
+            for (int i = 0; i < UM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) off[i][r] = x3_out_off(a, rbase + i * 16 + r, n);
+#pragma unroll
+            for (int i = 0; i < UM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) av[i][r] = (a.add && off[i][r] >= 0) ? a.add[off[i][r]] : 0.f;
+#pragma unroll
+            for (int i = 0; i < UM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) x3_store(a, off[i][r], acc[i][j][r] * sc[j], av[i][r]);
+        }
+    }
+    x3_stamp(a, 4);
+    x3_stamp(a, 5);
 }
 
 // STEM: the 7x7/s2 stem on the zero-padded NHWC4 image planes of
@@ -830,12 +1049,6 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     }
 }
 
-// the ring, or (P = 1) the staged fp16 output tile if that is larger (256x256: 132 KiB)
-constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
-    return P == 1 && 256 * (BN + 8) * 2 > x3_nst(BN, PAIR) * (256 + BN) * 128 ? 256 * (BN + 8) * 2
-                                                                              : x3_nst(BN, PAIR) * (256 + BN) * 128;
-}
-
 // One tile per block (blocks remapped XCD-aware), or (SK) column-grouped
 // stream-K: group g runs units [g*U/NG, (g+1)*U/NG) of the m-tile-major
 // (m-tile, K-step) sequence, one tile segment after another (sk_combine).
@@ -845,7 +1058,8 @@ constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
 // overlaps the other's main loop.
 template <int BN, bool STEM, bool PAIR, int MFD, bool SK, int P>
 __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, PAIR, P)];
+    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, PAIR, P) + x3_red_bytes(BN, PAIR)];
+    x3_stamp(a, 0);
     const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
     if constexpr (!SK) {
         conv_x3_tile<BN, STEM, PAIR, MFD, P>(a, smem, b, 0, a.nks, false);
@@ -863,6 +1077,375 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
         conv_x3_tile<BN, STEM, PAIR, MFD, P>(a, smem, mt * NT + nt, ks, ke - ks, ks != 0 || ke != a.nks);
         u = t0 + ke;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent form (conv_x3p_kernel<BN, P>): one block per CU walks tiles
+// lb, lb + G, lb + 2G, ... (lb = the XCD-remapped block index, so the blocks of
+// one XCD work on adjacent tiles at any time, as the one-tile grid's do) and the
+// LDS-DMA stage stream runs across tile boundaries: the last K-steps of a tile
+// already issue the next tile's first stages, so no tile pays a pipeline fill,
+// and no block launch or prologue sits between tiles.  Short-K convs (the R50
+// 1x1 GEMMs of configs C4/C5: 4-16 K-steps per tile) spent ~14 us per tile
+// outside the K loop in the one-tile kernel (~1.4 us per K-step inside it).
+//
+// The MFMAs run with the operands swapped (D^T = W . X^T): a lane's four
+// accumulator values are four consecutive output channels of one pixel, so the
+// epilogue stores 8 B (fp16) / 16 B (fp32) vectors straight from registers — no
+// LDS staging (the ring holds the next tile's stages while the epilogue runs)
+// and no per-element scalar stores.  The BN tile partials use a small LDS
+// scratch past the ring.  Counting: the epilogue's stores share vmcnt with the
+// DMA loads; loads complete in order among themselves, so a counted wait for
+// stage s still proves stage s landed (stores only make it wait longer).
+// Tail past the last tile: zero-filling DMAs keep every K-step's count uniform.
+// ONE: a 1x1 conv without padding (every row < M in-bounds for every K-step):
+// a row past M gets the out-of-range offset once per tile and no per-K-step
+// bounds check is kept (4 VGPRs: the 256x256 body has none to spare).
+template <int BN, int P, bool ONE>
+__global__ __launch_bounds__(512, 1) void conv_x3p_kernel(X3Args a) {
+    constexpr int BM = 256, WM = 4, WN = 2, ROW = 128, CPR = 8, RPI = 8;
+    constexpr int NST = x3_nst(BN, false);
+    constexpr int STAGE = (BM + BN) * ROW;
+    constexpr int GA = BM / RPI / 8;
+    constexpr int GBT = BN / RPI;
+    constexpr int GB = GBT >= 8 ? GBT / 8 : 1;
+    constexpr int GL = GA + GB;
+    constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
+    constexpr int NMC = (P == 3 ? 3 : 2) * UM;
+    static_assert(NST * STAGE + (WM + 2) * BN * 4 <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE + (WM + 2) * BN * 4];
+    float* red = (float*)(smem + NST * STAGE);     // [WM][BN] column sums, then [2][BN] half means
+    float* tmean = red + WM * BN;
+
+    const int G = gridDim.x, lb = xcd_remap(blockIdx.x, G);
+    const long T = (long)((a.M + BM - 1) / BM) * a.n_tiles;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w % WN;
+    const int nks = a.nks;
+
+    // ---- issue side: the stage stream over (tile, K-step) ----
+    // byte offsets from xbase = a.xs - pad*(W+1)*cstride halves (the furthest a
+    // padded-out origin reaches before a.xs; the host checks they fit 32 bits)
+    const int cstride = a.cch * 64;
+    const long xbias = (long)a.pad * (a.W + 1) * cstride;
+    const unsigned xbytes = (unsigned)((xbias + (long)a.N * a.H * a.W * cstride) * 2);
+    const i32x4 xrs = buffer_rsrc(a.xs - xbias, xbytes);
+    const unsigned wbytes = (unsigned)((long)a.K * a.RS * cstride * 2);
+    const i32x4 wrs = buffer_rsrc(a.ws, wbytes);
+    const unsigned wdead = wbytes;                     // B voffset past the last tile: zeros
+    const int bline = a.RS * a.cch * 64;
+    int a_org[ONE ? 1 : GA];
+    unsigned a_off[GA];
+    // B rows of this wave: row_j = RPI*((w*GB + j) % GBT) + lane/CPR — for both
+    // tile widths consecutive j are consecutive 8-row groups and the swizzle
+    // depends only on j's parity: two per-lane bases + a scalar step
+    unsigned b_off2[2];
+    const unsigned bstep = (unsigned)(2 * RPI * a.RS * a.cch * 64 * 2);   // bytes per j += 2
+    long it = lb;
+    int q_buf = 0, q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, ik = 0;
+    auto setup_issue = [&]() {
+        const int mt = (int)(it / a.n_tiles), nt = (int)(it - (long)mt * a.n_tiles);
+        const int m0 = mt * BM, n0 = nt * BN;
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            const int row = RPI * (w * GA + i) + lane / CPR;
+            const int Lc = (lane % CPR) ^ ((row >> 1) & 7);
+            const int m = m0 + row;
+            int hb = -16384, wb = -16384;
+            long off = 0;
+            if (m < a.M) {
+                const int hw = a.Ho * a.Wo;
+                const int n = m / hw, rem = m - n * hw;
+                const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+                hb = ho * a.stride - a.pad;
+                wb = wo * a.stride - a.pad;
+                off = (((long)n * a.H + hb) * a.W + wb) * cstride + Lc * 8;
+            }
+            if constexpr (ONE) a_off[i] = m < a.M ? (unsigned)((off + xbias) * 2) : xbytes;
+            else {
+                a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
+                a_off[i] = (unsigned)((off + xbias) * 2);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 2 && j < GB; ++j) {
+            const int bi = (w * GB + j) % GBT;
+            const int row = RPI * bi + lane / CPR;
+            const int Lc = (lane % CPR) ^ ((row >> 1) & 7);
+            b_off2[j] = (unsigned)(((n0 + row) * bline + Lc * 8) * 2);
+        }
+    };
+    auto b_dst = [&](int j) { return (BM + RPI * ((w * GB + j) % GBT)) * ROW; };
+    if (it < T) setup_issue();
+    // issue_stage: the DMA of the stream's next stage (branch-free: past the last
+    // tile every piece loads zeros), inside the scheduled MFMA region; advance:
+    // its bookkeeping, after the region (the tile switch branches)
+    auto issue_stage = [&]() {
+        char* st = smem + q_buf * STAGE;
+        const bool live = it < T;
+        const int dh = q_rr * a.dil, dw = q_ss * a.dil;
+        const unsigned toff = (unsigned)((((long)dh * a.W + dw) * cstride + q_cc * 64) * 2);
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            if constexpr (ONE) {
+                blds16(xrs, a_off[i], toff, st + (RPI * (w * GA + i)) * ROW);
+            } else {
+                const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+                const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+                blds16(xrs, in ? a_off[i] : xbytes, toff, st + (RPI * (w * GA + i)) * ROW);
+            }
+        }
+        const unsigned boff = (unsigned)((q_tap * a.cch + q_cc) * 128);
+#pragma unroll
+        for (int j = 0; j < GB; ++j)
+            blds16(wrs, live ? b_off2[j & 1] + (unsigned)(j >> 1) * bstep : wdead, boff, st + b_dst(j));
+    };
+    auto advance = [&]() {
+        q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
+        if (++q_ss == a.S) {
+            q_ss = 0;
+            ++q_rr;
+        }
+        if (++q_tap == a.RS) {
+            q_tap = 0;
+            q_rr = 0;
+            ++q_cc;
+        }
+        if (++ik == nks) {                     // the stream moves on to this block's next tile
+            ik = q_cc = q_tap = q_rr = q_ss = 0;
+            it += G;
+            if (it < T) setup_issue();
+            else {
+#pragma unroll
+                for (int i = 0; i < GA; ++i) {
+                    if constexpr (ONE) a_off[i] = xbytes;
+                    else a_org[i] = (int)(((unsigned)-16384 << 16) | ((unsigned)-16384 & 0xFFFFu));
+                }
+            }
+        }
+    };
+    auto issue_next = [&]() {
+        issue_stage();
+        advance();
+    };
+
+    // ---- compute side (MFMA operands swapped: acc[i][j] = channels x pixels) ----
+    const int r16 = lane & 15, q = lane >> 4;
+    const int sw = (r16 >> 1) & 7;
+    const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
+    const int a_base = (wm * UM * 16) * ROW, b_base = (BM + wn * UN * 16) * ROW;
+    struct FA {
+        f16x8 h[UM], l[UM];
+    };
+    f16x8 bh[UN], bl[UN];
+    f32x4 acc[UM][UN];
+    auto read_a = [&](FA& f, const char* st) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            f.h[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_h);
+            f.l[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_l);
+        }
+    };
+    auto read_b = [&](int j, const char* st) {
+        bh[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_h);
+        bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
+    };
+    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+    };
+    auto mma_col = [&](const FA& f, int j) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], bh[j], bl[j], f.h[i], f.l[i], mfma);
+    };
+    int cur = 0;
+    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
+
+    // prologue: stages 0 and 1 of the stream issued, stage 0 landed everywhere
+    issue_next();
+    issue_next();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+    lds_barrier();
+
+    for (long ct = lb; ct < T; ct += G) {
+        const int mt = (int)(ct / a.n_tiles), nt = (int)(ct - (long)mt * a.n_tiles);
+        const int m0 = mt * BM, n0 = nt * BN;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // invariant here: K-step 0 of tile ct landed in slot cur (every wave past a
+        // barrier since), the stream's next stage issued
+        if constexpr (NST == 2) {
+            FA fa;
+            read_a(fa, smem + cur * STAGE);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) read_b(j, smem + cur * STAGE);
+            // K-step t: wait stage t+1, barrier, issue stage t+2 into t's slot (its
+            // fragments are in registers), MFMAs of t while reading t+1's
+            auto kstep = [&](const bool rd) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                lds_barrier();
+                cur ^= 1;
+                const char* st = smem + cur * STAGE;
+                issue_stage();
+#pragma unroll
+                for (int j = 0; j < UN; ++j) {
+                    mma_col(fa, j);
+                    if (rd) read_b(j, st);
+                }
+                if (rd) read_a(fa, st);
+#pragma unroll
+                for (int j = 0; j < UN; ++j) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
+                    if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    if (j * ((GL + UN - 1) / UN) < GL) __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);
+                }
+                if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);
+                __builtin_amdgcn_sched_barrier(0);
+                advance();
+            };
+            for (int t = 0; t + 1 < nks; ++t) kstep(true);
+            kstep(false);
+        } else {
+            FA fa0, fa1;
+            read_a(fa0, smem + cur * STAGE);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) read_b(j, smem + cur * STAGE);
+            // K-step t: issue stage t+2 into t-1's slot (read before the last
+            // barrier), wait stage t+1, barrier, MFMAs of t while reading t+1's
+            auto step = [&](FA& fc, FA& fn, const bool rd) {
+                issue_stage();
+                advance();
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+                lds_barrier();
+                cur = cur == NST - 1 ? 0 : cur + 1;
+                const char* st = smem + cur * STAGE;
+                if (rd) read_a(fn, st);
+#pragma unroll
+                for (int j = 0; j < UN; ++j) {
+                    mma_col(fc, j);
+                    if (rd) read_b(j, st);
+                }
+                if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);
+#pragma unroll
+                for (int j = 0; j < UN; ++j) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
+                    if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            };
+            int t = 0;
+            for (; t + 2 < nks; t += 2) {
+                step(fa0, fa1, true);
+                step(fa1, fa0, true);
+            }
+            if (t + 1 < nks) {
+                step(fa0, fa1, true);
+                step(fa1, fa0, false);
+            } else {
+                step(fa0, fa1, false);
+            }
+        }
+
+        // ---- epilogue: scale, BN partials, vector stores from registers ----
+        // (thread indices laundered per tile: the epilogue's address arithmetic
+        // is otherwise hoisted out of the tile loop and held in registers across
+        // the K loop, which spilled)
+        int etid = tid;
+        asm volatile("" : "+v"(etid));
+        const int elane = etid & 63, er16 = elane & 15, eq = elane >> 4;
+        // lane (r16, q) of fragment (i, j): pixel m0 + wm*16*UM + 16i + r16,
+        // channels n0 + wn*16*UN + 16j + 4q .. +3
+        const int pbase = m0 + wm * UM * 16 + er16;
+        const int cbase = n0 + wn * UN * 16 + 4 * eq;
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            const f32x4 sc = a.wscale ? *(const f32x4*)(a.wscale + cbase + 16 * j) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+            for (int i = 0; i < UM; ++i)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc[r] * ginv;
+        }
+        if (a.part) {
+            auto reduce16 = [](float s) {
+#pragma unroll
+                for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);
+                return s;
+            };
+            const int crow = wn * UN * 16 + 4 * eq;             // tile column of r = 0
+#pragma unroll
+            for (int j = 0; j < UN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    float s = 0.f;
+#pragma unroll
+                    for (int i = 0; i < UM; ++i) s += (pbase + 16 * i < a.M) ? acc[i][j][r] : 0.f;
+                    s = reduce16(s);
+                    if (er16 == 0) red[wm * BN + crow + 16 * j + r] = s;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            const long tile128 = (long)(m0 >> 7);
+            for (int e = etid; e < 2 * BN; e += 512) {
+                const int h = e / BN, c = e - h * BN;
+                const int cnt = min(128, a.M - (m0 + 128 * h));
+                if (cnt > 0) {
+                    const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+                    tmean[h * BN + c] = s / (float)cnt;
+                    a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            const float* mu_h = tmean + (wm >> 1) * BN;
+#pragma unroll
+            for (int j = 0; j < UN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float mu = mu_h[crow + 16 * j + r];
+                    float s = 0.f;
+#pragma unroll
+                    for (int i = 0; i < UM; ++i) {
+                        const float d = acc[i][j][r] - mu;
+                        s += (pbase + 16 * i < a.M) ? d * d : 0.f;
+                    }
+                    s = reduce16(s);
+                    if (er16 == 0) red[wm * BN + crow + 16 * j + r] = s;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            for (int e = etid; e < 2 * BN; e += 512) {
+                const int h = e / BN, c = e - h * BN;
+                if (a.M - (m0 + 128 * h) > 0)
+                    a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
+            }
+            // red / tmean are next written after this tile's successor's K loop
+            // (barriers in between)
+        }
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            const int p = pbase + 16 * i;
+            if (p >= a.M) continue;
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                if constexpr (P == 1) {
+                    const h16x4 h = {(_Float16)acc[i][j][0], (_Float16)acc[i][j][1], (_Float16)acc[i][j][2],
+                                     (_Float16)acc[i][j][3]};
+                    *(h16x4*)(a.y16 + (long)p * a.K + cbase + 16 * j) = h;
+                } else {
+                    const long off = x3_out_off(a, p, cbase + 16 * j);
+                    f32x4 v = acc[i][j];
+                    if (a.add) v += *(const f32x4*)(a.add + off);
+                    *(f32x4*)(a.y + off) = v;
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zero-line tail DMAs land before the block ends
 }
 
 
@@ -1491,8 +2074,13 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
 struct X3Choice {
     int bn, mfd;
     bool pair, sk;
+    bool persist = false;              // conv_x3p_kernel<bn, P, one>
+    bool one = false;
 };
-static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy) {
+// one: a 1x1 conv without padding; pfit: the persistent kernel's 32-bit byte
+// offsets cover the operands (x3p_fits)
+static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, bool one = false,
+                          bool pfit = false) {
     switch (policy) {
         case HKP_TILE_256:
             if (k % 256 == 0) return {256, 16, false, false};
@@ -1505,6 +2093,13 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy) 
             break;
         case HKP_TILE_64_PAIR:
             return {64, 16, true, false};
+        case HKP_TILE_256_PERSIST:         // 256x256 only as the 1x1 body (the KxK one spills)
+            if (pfit && k % 256 == 0 && one) return {256, 16, false, false, true, true};
+            if (pfit && k % 128 == 0) return {128, 16, false, false, true, one};
+            break;
+        case HKP_TILE_128_PERSIST:
+            if (pfit && k % 128 == 0) return {128, 16, false, false, true, one};
+            break;
         default:
             break;
     }
@@ -1519,12 +2114,20 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy) 
 static const X3Choice X3_STEM{64, 32, true, false};
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
+    if (c.persist) return snprintf(buf, len, "conv_x3p_kernel<%d, %d, %s>", c.bn, P, c.one ? "true" : "false");
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
 
 template <int P>
 static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Args& a) {
+    if (c.persist) {
+        const unsigned g = (unsigned)std::min<long>((long)grid.x, x3_cus());
+        if (c.bn == 256) hipLaunchKernelGGL((conv_x3p_kernel<256, P, true>), dim3(g), dim3(512), 0, st, a);
+        else if (c.one) hipLaunchKernelGGL((conv_x3p_kernel<128, P, true>), dim3(g), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_x3p_kernel<128, P, false>), dim3(g), dim3(512), 0, st, a);
+        return;
+    }
     if (c.sk && c.bn == 128)
         hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 16, true, P>), grid, dim3(512), 0, st, a);
     else if (c.sk)
@@ -1541,11 +2144,23 @@ static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Ar
 
 // a.RS, a.cch (128-B lines per pixel), a.M ... set by the caller; P = operand
 // layout (3 packed f16x3 split, 1 plain fp16)
+// the persistent kernel addresses its operands with 32-bit BYTE offsets from
+// the input base less the padded-out margin, and from the weights
+static bool x3p_fits(long n, long h, long w, long cstride, long pad, long k, long rs) {
+    return ((long)pad * (w + 1) * cstride + n * h * w * cstride) * 2 < (1L << 32) - 256 &&
+           k * rs * cstride * 2 < (1L << 32) - 256;
+}
+
+static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
+
 static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
                       int64_t ws_bytes = 0) {
+    a.stamps = g_x3_stamps;
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
-    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy);
+    const bool one = a.RS == 1 && a.pad == 0;
+    const bool pfit = x3p_fits(a.N, a.H, a.W, a.cch * 64L, a.pad, a.K, a.RS);
+    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, one, pfit);
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
@@ -1596,7 +2211,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_64_PAIR, "%s: unknown tile policy %d", who,
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_128_PERSIST, "%s: unknown tile policy %d", who,
                   d->tile);
     return HKP_OK;
 }
@@ -1914,8 +2529,11 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
         case HKP_KOP_FWD_F16: {
             const int P = op == HKP_KOP_FWD_X3 ? 3 : 1;
             const long m = (long)d->n * ho * wo;
-            const int nks = d->r * d->s * (d->c / (P == 3 ? 32 : 64));
-            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile), false, P, buf, len);
+            const int cg = P == 3 ? 32 : 64;
+            const int nks = d->r * d->s * (d->c / cg);
+            const bool one = d->r * d->s == 1 && d->pad == 0;
+            const bool pfit = x3p_fits(d->n, d->h, d->w, d->c / cg * 64L, d->pad, d->k, d->r * d->s);
+            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, one, pfit), false, P, buf, len);
         }
         case HKP_KOP_DGRAD_X3: {
             const long m = (long)d->n * d->h * d->w;
@@ -1935,3 +2553,10 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
     }
     return HKP_ERR_BAD_ARG;
 }
+
+// Debug: forward conv launches record per-block phase clocks into buf (8 slots of
+// s_memrealtime per block: start, pipeline filled, K loop done, BN partials
+// done, fp16 tile staged, stores issued; 0 where a body records none); NULL
+// turns it off.  Not thread-safe; for tools/ only.
+extern "C" void hkp_debug_x3_stamps(uint64_t* buf) { g_x3_stamps = (unsigned long long*)buf; }
+

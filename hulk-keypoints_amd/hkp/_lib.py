@@ -26,8 +26,8 @@ class ConvDesc(ctypes.Structure):
 
 
 # hkp_conv_desc.tile policies (include/hulkkp.h)
-HKP_TILE_AUTO, HKP_TILE_NO_SK, HKP_TILE_SK, HKP_TILE_256, HKP_TILE_128_MF16, HKP_TILE_128_MF32, HKP_TILE_64_PAIR = \
-    range(7)
+(HKP_TILE_AUTO, HKP_TILE_NO_SK, HKP_TILE_SK, HKP_TILE_256, HKP_TILE_128_MF16, HKP_TILE_128_MF32, HKP_TILE_64_PAIR,
+ HKP_TILE_256_PERSIST, HKP_TILE_128_PERSIST) = range(9)
 # hkp_conv_kernel_name ops
 HKP_KOP_FWD_X3, HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3 = range(5)
 
@@ -64,6 +64,7 @@ SIGNATURES = {
     "hkp_bn_apply_f16": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
+    "hkp_debug_x3_stamps": (None, [_P]),
     "hkp_bn_apply_head": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),

@@ -57,6 +57,8 @@ _split_cache = {}
 _prepack_plans = {}
 _NO_PREPACK_PLAN = os.environ.get("HKP_NO_PREPACK_PLAN") == "1"     # A/B: always rebuild
 _UNFUSED_HEAD = os.environ.get("HKP_UNFUSED_HEAD") == "1"           # A/B: bn_apply + head_fc
+_F16_TILE_1X1 = int(os.environ.get("HKP_F16_TILE_1X1", "0"))         # A/B: HKP_TILE_* for plain-fp16 1x1 convs
+_F16_TILE_KXK = int(os.environ.get("HKP_F16_TILE_KXK", "0"))
 
 
 def _cache_slot(w):
@@ -214,7 +216,8 @@ def _conv_fwd(conv, bn, x, layout="nhwc", part_out=None, sk=True):
                                     part_out=part_out, sk=sk)
     elif layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
         y, part = ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
-                                     stats=bn.training, sk=sk)
+                                     stats=bn.training, sk=sk,
+                                     tile=_F16_TILE_1X1 if conv.weight.shape[1] == 1 else _F16_TILE_KXK)
     elif part_out is not None:
         raise ops.HkpError("conv %s: partials into a caller buffer need the x3 path" % (tuple(conv.weight.shape),))
     elif layout == "nhwc" and passes:

@@ -71,6 +71,8 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_128_MF16 4
 #define HKP_TILE_128_MF32 5
 #define HKP_TILE_64_PAIR 6
+#define HKP_TILE_256_PERSIST 7        /* persistent 256x256 (conv_x3p_kernel) */
+#define HKP_TILE_128_PERSIST 8        /* persistent 256x128 */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);
@@ -154,6 +156,12 @@ int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16, const uint
 #define HKP_KOP_STEM_X3 3
 #define HKP_KOP_WGRAD_X3 4
 int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf, int32_t len);
+
+/* Debug (tools/ only, not thread-safe): one-tile forward conv launches record
+ * per-block phase clocks (s_memrealtime, 100 MHz) into buf[block * 8 + slot]
+ * (start, pipeline filled, K loop done, BN partials done, output staged, stores
+ * issued); NULL turns it off. */
+void hkp_debug_x3_stamps(uint64_t* buf);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--nostats", action="store_true", help="no BN partials (epilogue cost A/B)")
     args = ap.parse_args()
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
@@ -60,14 +61,14 @@ def main():
             passes, op = 3, HKP_KOP_FWD_X3
 
             def run(t):
-                return ops.conv2d_fwd_x3(xs, ws, st, pd, dl, tile=t)[0]
+                return ops.conv2d_fwd_x3(xs, ws, st, pd, dl, stats=not args.nostats, tile=t)[0]
         else:
             xs = x.half()
             ws = ops.weight_pack_f16(wt)
             passes, op = 1, HKP_KOP_FWD_F16
 
             def run(t):
-                return ops.conv2d_fwd_f16(xs, ws, st, pd, dl, tile=t)[0]
+                return ops.conv2d_fwd_f16(xs, ws, st, pd, dl, stats=not args.nostats, tile=t)[0]
         del x
         outs, times = {}, {t: [] for t in tiles}
         for r in range(args.rounds):

@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Per-block phase timeline of the one-tile x3/fp16 conv (hkp_debug_x3_stamps):
+runs a conv shape once warm, then once with stamps, and prints the median
+per-block phase durations (us) and the launch span.
+
+    python tools/x3_stamps.py c4_l4_c3 [c4_l1_c3 ...]
+"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "hulk-keypoints_amd"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+import torch  # noqa: E402
+
+from conv_ab import SHAPES  # noqa: E402
+
+PHASES = ["fill", "kloop", "partials|stores(x3)", "stage|partials(x3)", "store"]
+
+
+def main():
+    from hkp import ops
+    from hkp._lib import lib
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    for name in sys.argv[1:]:
+        prec, n, h, w, ci, co, k, st, pd, dl = SHAPES[name]
+        x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
+        wt = torch.randn(co, k, k, ci, device=dev, generator=g) * (2.0 / (k * k * co)) ** 0.5
+        if prec == "x3":
+            ss = torch.cat([torch.ones(ci, device=dev), torch.zeros(ci, device=dev)])
+            xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
+            ws = ops.weight_pack_x3(wt)
+            run = lambda: ops.conv2d_fwd_x3(xs, ws, st, pd, dl, sk=False)  # noqa: E731
+        else:
+            xs = x.half()
+            ws = ops.weight_pack_f16(wt)
+            run = lambda: ops.conv2d_fwd_f16(xs, ws, st, pd, dl, sk=False)  # noqa: E731
+        for _ in range(3):
+            run()
+        ho, wo = ops.conv_out_hw(h, w, k, k, st, pd, dl)
+        blocks = ((n * ho * wo + 255) // 256) * (co // (256 if co % 256 == 0 else 128)) * 2 + 64
+        buf = torch.zeros(blocks * 8, dtype=torch.int64, device=dev)
+        lib().hkp_debug_x3_stamps(buf.data_ptr())
+        run()
+        torch.cuda.synchronize()
+        lib().hkp_debug_x3_stamps(None)
+        s = buf.view(-1, 8).cpu()
+        s = s[s[:, 0] != 0].double()
+        t0 = s[:, 0].min()
+        span = (s[:, 5].max() - t0) / 100.0
+        out = []
+        for i, ph in enumerate(PHASES):
+            d = (s[:, i + 1] - s[:, i]) / 100.0
+            out.append("%s %.2f" % (ph, d.median().item()))
+        tot = ((s[:, 5] - s[:, 0]) / 100.0).median().item()
+        print("%-9s blocks %d  span %.1f us  per-block median total %.2f us: %s" % (
+            name, s.shape[0], span.item(), tot, ", ".join(out)), flush=True)
+        # start-time spread of consecutive waves of blocks
+        starts = ((s[:, 0] - t0) / 100.0).sort().values
+        print("          block starts: p10 %.1f p50 %.1f p90 %.1f us" % (
+            starts[int(0.1 * len(starts))].item(), starts[len(starts) // 2].item(),
+            starts[int(0.9 * len(starts))].item()))
+
+
+if __name__ == "__main__":
+    main()
