@@ -701,13 +701,15 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
     }
     x3_stamp(a, 3);
-    if (!a.add && !a.ost) {
-        // Dense output: staged through the (drained) ring as fp32 rows and written
-        // as whole 16-B row chunks — 32 store instructions per thread, full 128-B
-        // lines.  The fragment-layout stores (128 4-B stores per thread, 64-B
-        // pieces) of every CU at once took ~34 us per C2 layer4 tile (10 %):
-        // more than a wave's 63 outstanding memory ops, so the waves stalled on
-        // their completion instead of ending and letting the next block start.
+    {
+        // The output tile is staged through the (drained) ring as fp32 rows and
+        // written as whole 16-B row chunks — 32 store instructions per thread,
+        // full 128-B lines (a phase output row of the strided dgrad is still 4
+        // contiguous channels per chunk; the addend is read the same way).  The
+        // fragment-layout stores (128 4-B stores per thread, 64-B pieces) of
+        // every CU at once took ~34 us per C2 layer4 tile (10 %): more than a
+        // wave's 63 outstanding memory ops, so the waves stalled on their
+        // completion instead of ending and letting the next block start.
         // 256-wide tiles stage half the rows per pass (128 KiB).
         constexpr int PASSES = BN == 256 ? 2 : 1, RPP = 256 / PASSES, PITCH = BN + 4, C4 = BN / 4;
         static_assert(RPP * PITCH * 4 <= x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB), "staging");
@@ -726,33 +728,31 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                                 acc[i][j][r] * sc[j];
             }
             lds_sync();
+            if (!a.add && !a.ost) {
 #pragma unroll 4
-            for (int e = tid; e < RPP * C4; e += 512) {
-                const int row = e / C4, c4 = e - row * C4;
-                const int m = m0 + h * RPP + row;
-                if (m < a.M) *(f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4) = *(const f32x4*)(t + row * PITCH + c4 * 4);
+                for (int e = tid; e < RPP * C4; e += 512) {
+                    const int row = e / C4, c4 = e - row * C4;
+                    const int m = m0 + h * RPP + row;
+                    if (m < a.M)
+                        *(f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4) = *(const f32x4*)(t + row * PITCH + c4 * 4);
+                }
+            } else {
+#pragma unroll 2
+                for (int e = tid; e < RPP * C4; e += 512) {
+                    const int row = e / C4, c4 = e - row * C4;
+                    const long off = x3_out_off(a, m0 + h * RPP + row, n0 + c4 * 4);
+                    if (off >= 0) {
+                        f32x4 v = *(const f32x4*)(t + row * PITCH + c4 * 4);
+                        if (a.add) {
+                            const f32x4 ad = *(const f32x4*)(a.add + off);
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) v[k] = v[k] + ad[k];
+                        }
+                        *(f32x4*)(a.y + off) = v;
+                    }
+                }
             }
             if (h + 1 < PASSES) lds_sync();            // the next pass overwrites the rows just read
-        }
-    } else {
-        // phase outputs (strided dgrad) / addend: per element, from the fragments
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            const int n = n0 + wn * UN * 16 + j * 16 + r16;
-            long off[UM][4];
-            float av[UM][4];
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) off[i][r] = x3_out_off(a, rbase + i * 16 + r, n);
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) av[i][r] = (a.add && off[i][r] >= 0) ? a.add[off[i][r]] : 0.f;
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) x3_store(a, off[i][r], acc[i][j][r] * sc[j], av[i][r]);
         }
     }
     x3_stamp(a, 4);
