@@ -1590,7 +1590,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     constexpr int NX = PX / 8, ND = GD * PX / 64, GL = NX + ND;
     constexpr int TM = KA / 64, TN = 2;
     static_assert(ND >= 1 && (KA == 64 || KA == 128 || KA == 256), "KA must be 64, 128 or 256");
-    __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
+    // the epilogue stages the slab tile (KA x 256 fp32, pitch 264) in passes of
+    // 128 rows through the drained ring: at least 132 KiB
+    constexpr int EPI_ROWS = KA < 128 ? KA : 128, EPI_PITCH = BR + 8;
+    constexpr int LDS = NS * STAGE > EPI_ROWS * EPI_PITCH * 4 ? NS * STAGE : EPI_ROWS * EPI_PITCH * 4;
+    __shared__ __attribute__((aligned(1024))) char smem[LDS];
 
     const int bid = xcd_remap(blockIdx.x, gridDim.x);       // same pixel range → same XCD
     const int split = bid / a.tiles, tile = bid - split * a.tiles;
@@ -1862,20 +1866,46 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
         step(false, false);
     }
 
+    // ---- epilogue: the slab tile staged through the drained ring in passes of
+    // EPI_ROWS output-channel rows and written as 16-B row chunks (whole 128-B
+    // lines, 32-64 stores per thread).  Per-element stores from the fragments
+    // (128 per thread, past a wave's 63 outstanding memory ops) stalled every
+    // wave on their completion while all CUs wrote their slabs at once.
     const float inv = 1.f / pow2_scale_for(a.amax);
     float* out = a.ws + (long)split * a.K * a.RSC;
+    float* t = (float*)smem;
+    constexpr int PASSES = KA / EPI_ROWS, C4 = BR / 4;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_barrier();                                             // every wave done with the ring
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int ps = 0; ps < PASSES; ++ps) {
+        // wave rows: k_local = wk*TM*32 + i*32 + 8*(r>>2) + 4*h + (r&3) in [ps*EPI_ROWS, +EPI_ROWS)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int m = r0 + wr * 64 + j * 32 + (lane & 31);
-            if (m >= a.RSC) continue;
+        for (int i = 0; i < TM; ++i) {
+            const int kb = wk * TM * 32 + i * 32;
+            if (kb / EPI_ROWS != ps) continue;                 // wave-uniform
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int k = k0 + wk * TM * 32 + i * 32 + 8 * (r >> 2) + 4 * h + (r & 3);
-                out[(long)k * a.RSC + m] = acc[i][j][r] * inv;
-            }
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    t[(kb - ps * EPI_ROWS + 8 * (r >> 2) + 4 * h + (r & 3)) * EPI_PITCH + wr * 64 + j * 32 + (lane & 31)] =
+                        acc[i][j][r] * inv;
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        const int mcols = min(BR, a.RSC - r0);                 // multiple of 4 (RSC = R*S*C, C % 32 == 0)
+#pragma unroll 4
+        for (int e = tid; e < EPI_ROWS * C4; e += 512) {
+            const int row = e / C4, c4 = e - row * C4;
+            if (c4 * 4 < mcols)
+                *(f32x4*)(out + (long)(k0 + ps * EPI_ROWS + row) * a.RSC + r0 + c4 * 4) =
+                    *(const f32x4*)(t + row * EPI_PITCH + c4 * 4);
+        }
+        if (ps + 1 < PASSES) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+        }
+    }
 }
 
 
