@@ -77,6 +77,7 @@ struct X3Args {
     // unit ranges; a tile split between blocks is summed by its last-arriving
     // block from per-segment fp32 slabs (sk_ws) — sk_cnt[tile] arrival counters,
     // zero on entry and left zero
+    int mt0 = 0;           // m-tile offset of this launch (the split-K tail launch of conv_x3_tail_kernel)
     long sk_units = 0;
     float* sk_ws = nullptr;
     unsigned* sk_cnt = nullptr;
@@ -787,7 +788,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
-    const int m0 = mt * BM, n0 = nt * BN;
+    const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = w / WN, wn = w % WN;
@@ -1077,6 +1078,25 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
         conv_x3_tile<BN, STEM, PAIR, MFD, P>(a, smem, mt * NT + nt, ks, ke - ks, ks != 0 || ke != a.nks);
         u = t0 + ke;
     }
+}
+
+// Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
+// each cut into S equal K segments — one block per segment, a single round —
+// summed by the tile's last-arriving segment in segment order (sk_combine; the
+// launch is laid out as a column-grouped stream-K grid of NG = tiles x S groups,
+// so every group's unit range lies inside one tile).  The stream-K kernel's
+// segment loop is what made the 256x256 stream-K body spill; a block here runs
+// exactly one segment.  E.g. C2 layer3 on 256x256 tiles: 600 tiles = 2 rounds +
+// 88 tiles, which run as 176 half tiles (~0.6 of a tile time instead of 1).
+template <int BN, int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_tail_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, false, P) + x3_red_bytes(BN, false)];
+    const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
+    const int NT = a.n_tiles, NG = G / NT, g = b / NT, nt = b - g * NT;
+    const long U = a.sk_units, u0 = sk_start(g, U, NG), u1 = sk_start(g + 1, U, NG);
+    const int mt = (int)(u0 / a.nks);
+    const int ks = (int)(u0 - (long)mt * a.nks), ke = (int)(u1 - (long)mt * a.nks);
+    conv_x3_tile<BN, false, false, 16, P>(a, smem, mt * NT + nt, ks, ke - ks, true);
 }
 
 // ---------------------------------------------------------------------------
@@ -2061,6 +2081,30 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // 256x128 1.82 ms; on C2 layer3 (Cout 256, 600 m-tiles) 256x256 loses to round
 // quantisation (0.53 vs 0.47 ms).  No stream-K with 256x256 tiles (the one-tile
 // 256x256 kernel sits at 255 VGPRs; the stream-K loop would spill).
+// Split-K tail (conv_x3_tail_kernel) for a one-tile grid of `tiles` tiles: the
+// segment count S for the tiles past the last full round (0: none), cost in
+// tile times 1/S + 0.08 — the 0.08 is a segment's fill, slab hand-off and
+// combine.  The tail is ONE round (Tr*S <= CUs): the stream-K workspace holds
+// two slabs per CU.  C2 layer3 on 256x256 tiles (88 tail tiles): S = 2, ~0.58
+// instead of 1.
+static int x3_tail_split(long tiles, int nks, double* cost = nullptr) {
+    const int G = x3_cus();
+    const long tr = tiles % G;
+    double best = 1.0;
+    int bs = 0;
+    if (tr > 0) {
+        for (int S = 2; S <= 8 && nks / S >= 4 && tr * S <= G; ++S) {
+            const double c = 1.0 / S + 0.08;
+            if (c < best - 1e-9) {
+                best = c;
+                bs = S;
+            }
+        }
+    }
+    if (cost) *cost = tr > 0 ? best : 0.0;
+    return bs;
+}
+
 struct X3Plan {
     int bn;
     bool sk;
@@ -2073,7 +2117,9 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
         if (k % bn) continue;
         const long tiles = m_tiles * (k / bn);
         const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
-        const double dp = (double)((tiles + G - 1) / G) * col;
+        double tail = (tiles % G) ? 1.0 : 0.0;             // the last, partly filled round
+        if (bn == 256 && sk_ok) x3_tail_split(tiles, nks, &tail);
+        const double dp = ((double)(tiles / G) + tail) * col;
         if (dp < best_cost - 1e-9) {
             best_cost = dp;
             best = {bn, false};
@@ -2129,6 +2175,9 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
             break;
         case HKP_TILE_128_PERSIST:
             if (pfit && k % 128 == 0) return {128, 16, false, false, true, one};
+            break;
+        case HKP_TILE_256_TAIL:            // 256x256, the partial last round as split-K segments
+            if (k % 256 == 0) return {256, 16, false, false};
             break;
         default:
             break;
@@ -2204,6 +2253,38 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         const long ng = std::min<long>(x3_cus() / a.n_tiles, a.sk_units);
         grid = dim3((unsigned)(ng * a.n_tiles));
     }
+    // split-K tail for the 256x256 one-tile grid (auto, or forced by HKP_TILE_256_TAIL)
+    const long tiles = m_tiles * a.n_tiles;
+    int S = (!c.sk && !c.persist && c.bn == 256 && sk_ok &&
+             (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))
+                ? x3_tail_split(tiles, nks) : 0;
+    // the tail grid holds two slabs per block in the stream-K workspace and one
+    // arrival counter per tail tile: at most one round (x3_tail_split), checked
+    if (S > 0) {
+        const long tm = m_tiles - tiles / x3_cus() * x3_cus() / a.n_tiles;
+        const long gx = tm * S * a.n_tiles;
+        if (gx > x3_cus() || 2L * gx * 256 * 1024 + X3_SK_CNT_BYTES > ws_bytes || tm * a.n_tiles * 4 > X3_SK_CNT_BYTES)
+            S = 0;
+    }
+    if (S > 0) {
+        const long G = x3_cus();
+        const long rm = tiles / G * G / a.n_tiles;          // m-tiles of the full rounds
+        if (rm > 0) {
+            dim3 g0((unsigned)(rm * a.n_tiles));
+            if (P == 3) launch_x3_p<3>(c, g0, st, a);
+            else launch_x3_p<1>(c, g0, st, a);
+        }
+        X3Args t = a;
+        t.mt0 = (int)rm;
+        const long tm = m_tiles - rm;
+        t.sk_units = tm * nks;
+        t.sk_cnt = (unsigned*)ws;
+        t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
+        const dim3 gt((unsigned)(tm * S * a.n_tiles));
+        if (P == 3) hipLaunchKernelGGL((conv_x3_tail_kernel<256, 3>), gt, dim3(512), 0, st, t);
+        else hipLaunchKernelGGL((conv_x3_tail_kernel<256, 1>), gt, dim3(512), 0, st, t);
+        return;
+    }
     if (P == 3) launch_x3_p<3>(c, grid, st, a);
     else launch_x3_p<1>(c, grid, st, a);
 }
@@ -2241,7 +2322,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_128_PERSIST, "%s: unknown tile policy %d", who,
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_256_TAIL, "%s: unknown tile policy %d", who,
                   d->tile);
     return HKP_OK;
 }

@@ -172,7 +172,7 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     assert torch.allclose(p, p32, rtol=1e-4, atol=1e-3)
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
-    for tile in range(1, 9):
+    for tile in range(1, 10):
         yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
         # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
         # segments at the end, so variants differ by fp32 summation order)
@@ -441,7 +441,7 @@ BODY_CASES = [
 
 
 @pytest.mark.parametrize("case", BODY_CASES)
-@pytest.mark.parametrize("tile", [3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("tile", [3, 4, 5, 6, 7, 8, 9])
 def test_x3_tile_bodies_dgrad(cuda_device, case, tile):
     """Every kernel body (256x256 / 256x128 16x16x32 / 256x128 32x32x16 / 256x64
     pairs) on the forward and the stride-1 dgrad with a residual addend:
@@ -545,7 +545,7 @@ def test_f16_conv_exact_products(cuda_device, case):
     # BN partials (from the fp32 accumulators) as the fp32 conv's on the same fp16-rounded operands
     yr, pr = ops.conv2d_fwd(x.half().float().to(d), w_eff.float().to(d), st, pad, dil)
     assert torch.allclose(p16, pr, rtol=1e-4, atol=1e-3)
-    for tile in range(1, 9):
+    for tile in range(1, 10):
         yv, pv = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, tile=tile)
         assert err_ratio(yv) <= 1.0, tile
         assert torch.allclose(pv, p16, rtol=1e-4, atol=1e-3)
@@ -598,6 +598,42 @@ def test_persistent_conv(cuda_device, case, tile):
         y2, _ = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, tile=tile)
     else:
         y2, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
+    assert torch.equal(y1, y2)
+
+
+TAIL_CASES = [
+    # (precision, n, h, w, cin, cout, k, stride, pad, dil): one full round + a split-K tail
+    ("x3", 16, 60, 80, 256, 256, 3, 1, 2, 2),      # C2 layer3 class: 300 tiles = 256 + 44 halves
+    ("x3", 9, 60, 80, 256, 512, 3, 1, 4, 4),       # two column tiles, 338 tiles, ragged M
+    ("f16", 16, 60, 80, 512, 256, 1, 1, 0, 1),     # plain fp16, 8 K-steps per tile
+]
+
+
+@pytest.mark.parametrize("case", TAIL_CASES)
+def test_split_k_tail(cuda_device, case):
+    """HKP_TILE_256_TAIL: 256x256 tiles, the tiles past the last full round run as
+    S split-K segments (conv_x3_tail_kernel, fixed-order sum by the last-arriving
+    segment) — the same values as the plain one-tile grid (fp32 summation order),
+    the same BN partials, and run to run bit-identical."""
+    from hkp import ops
+    from hkp._lib import HKP_TILE_256, HKP_TILE_256_TAIL
+    prec, n, h, w, cin, cout, k, st, pad, dil = case
+    d = cuda_device
+    g = torch.Generator(device=d).manual_seed(9)
+    x = torch.relu(torch.randn(n, h, w, cin, device=d, generator=g))
+    wt = torch.randn(cout, k, k, cin, device=d, generator=g) * (2.0 / (k * k * cout)) ** 0.5
+    if prec == "f16":
+        xs, wp, fwd = x.half(), ops.weight_pack_f16(wt), ops.conv2d_fwd_f16
+    else:
+        ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
+        xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
+        wp, fwd = ops.weight_pack_x3(wt), ops.conv2d_fwd_x3
+    y0, p0 = fwd(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256)
+    y1, p1 = fwd(xs, wp, st, pad, dil, tile=HKP_TILE_256_TAIL)
+    y2, _ = fwd(xs, wp, st, pad, dil, tile=HKP_TILE_256_TAIL)
+    tol = 2.0 ** -10 if prec == "f16" else 4e-6
+    assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item()
+    assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
     assert torch.equal(y1, y2)
 
 
