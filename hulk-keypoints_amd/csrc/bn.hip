@@ -6,6 +6,8 @@
 // unbiased variance; num_batches_tracked += 1.  Output = x*alpha + beta with
 // alpha = invstd*gamma, beta = bias - mean*alpha (fp32, two roundings, as
 // ATen's batch_norm_cpu_transform_input).
+#include <cstdlib>
+
 #include "common.h"
 
 // x*alpha + beta as two roundings (ATen's Vectorized mul then add): no contraction.
@@ -98,7 +100,10 @@ __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, con
 
 // RES: 0 none, 1 raw residual, 2 affine residual (downsample BN), 3 raw residual
 // read from its packed split (hi + lo, written by the producer of the block input)
-template <int RES, bool RELU>
+// FIX: the grid stride is a multiple of C/4 — every vector a thread visits has
+// the same 4 channels: scale/shift loaded once, and two vectors (i, i + stride)
+// in flight per thread.
+template <int RES, bool RELU, bool FIX>
 __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f32x4* __restrict__ y,
                                                        const f32x4* __restrict__ sc, const f32x4* __restrict__ sh,
                                                        const f32x4* __restrict__ res, const f32x4* __restrict__ rsc,
@@ -106,25 +111,35 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
                                                        f32x4* __restrict__ out, _Float16* __restrict__ osplit,
                                                        int passes) {
     const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        const int c4 = (int)(i % C4);
-        const f32x4 v = y[i], a = sc[c4], b = sh[c4];
+    const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    struct In {
+        f32x4 v, r;
+        h16x4 h, l;
+    };
+    auto load = [&](long i) {
+        In x;
+        x.v = y[i];
+        if constexpr (RES == 1 || RES == 2) x.r = res[i];
+        if constexpr (RES == 3) {
+            const long e0 = i * 4, off = 2 * e0 - (e0 & 31);
+            x.h = *(const h16x4*)(rsplit + off);
+            x.l = *(const h16x4*)(rsplit + off + 32);
+        }
+        return x;
+    };
+    auto one = [&](long i, const In& x, const f32x4& a, const f32x4& b, const f32x4& ra, const f32x4& rb) {
         f32x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(__fmul_rn(v[e], a[e]), b[e]);
+        for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(__fmul_rn(x.v[e], a[e]), b[e]);
         if constexpr (RES == 1) {
-            const f32x4 r = res[i];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], r[e]);
+            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], x.r[e]);
         } else if constexpr (RES == 2) {
-            const f32x4 r = res[i], ra = rsc[c4], rb = rsh[c4];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn(r[e], ra[e]), rb[e]));
+            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn(x.r[e], ra[e]), rb[e]));
         } else if constexpr (RES == 3) {
-            const long e0 = i * 4, off = 2 * e0 - (e0 & 31);
-            const h16x4 h = *(const h16x4*)(rsplit + off), l = *(const h16x4*)(rsplit + off + 32);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn((float)h[e], (float)l[e]));
+            for (int e = 0; e < 4; ++e) o[e] = __fadd_rn(o[e], __fadd_rn((float)x.h[e], (float)x.l[e]));
         }
         if constexpr (RELU) {
 #pragma unroll
@@ -132,6 +147,24 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(long n4, int C4, const f3
         }
         if (out) out[i] = o;
         if (osplit) store_split4(o, i, osplit, passes);   // operand split for the next conv
+    };
+    const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (FIX) {
+        const int c4 = (int)(i0 % C4);
+        const f32x4 a = sc[c4], b = sh[c4];
+        const f32x4 ra = RES == 2 ? rsc[c4] : z, rb = RES == 2 ? rsh[c4] : z;
+        long i = i0;
+        for (; i + stride < n4; i += 2 * stride) {
+            const In x0 = load(i), x1 = load(i + stride);
+            one(i, x0, a, b, ra, rb);
+            one(i + stride, x1, a, b, ra, rb);
+        }
+        if (i < n4) one(i, load(i), a, b, ra, rb);
+    } else {
+        for (long i = i0; i < n4; i += stride) {
+            const int c4 = (int)(i % C4);
+            one(i, load(i), sc[c4], sh[c4], RES == 2 ? rsc[c4] : z, RES == 2 ? rsh[c4] : z);
+        }
     }
 }
 
@@ -164,19 +197,14 @@ __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, cons
             }
         }
     };
-    if constexpr (FIX) load_ss((int)(i0 % C8) * 8);
-    for (long i = i0; i < n8; i += stride) {
-        if constexpr (!FIX) load_ss((int)(i % C8) * 8);
-        const h16x8 v = y[i];
+    auto one = [&](long i, const h16x8& v, const h16x8& r) {
         float o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(__fmul_rn((float)v[e], a[e]), b[e]);
         if constexpr (RES == 1) {
-            const h16x8 r = res[i];
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(o[e], (float)r[e]);
         } else if constexpr (RES == 2) {
-            const h16x8 r = res[i];
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = __fadd_rn(o[e], __fadd_rn(__fmul_rn((float)r[e], ra[e]), rb[e]));
         }
@@ -190,6 +218,33 @@ __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, cons
         if (out32) {
             out32[2 * i] = f32x4{o[0], o[1], o[2], o[3]};
             out32[2 * i + 1] = f32x4{o[4], o[5], o[6], o[7]};
+        }
+    };
+    if constexpr (FIX) {
+        // two vectors per thread in flight (i and i + stride share the channels)
+        load_ss((int)(i0 % C8) * 8);
+        long i = i0;
+        for (; i + stride < n8; i += 2 * stride) {
+            const h16x8 v0 = y[i], v1 = y[i + stride];
+            h16x8 r0{}, r1{};
+            if constexpr (RES != 0) {
+                r0 = res[i];
+                r1 = res[i + stride];
+            }
+            one(i, v0, r0);
+            one(i + stride, v1, r1);
+        }
+        if (i < n8) {
+            h16x8 r0{};
+            if constexpr (RES != 0) r0 = res[i];
+            one(i, y[i], r0);
+        }
+    } else {
+        for (long i = i0; i < n8; i += stride) {
+            load_ss((int)(i % C8) * 8);
+            h16x8 r0{};
+            if constexpr (RES != 0) r0 = res[i];
+            one(i, y[i], r0);
         }
     }
 }
@@ -307,9 +362,14 @@ extern "C" int hkp_bn_apply(int64_t m, int32_t c, const float* y, const float* s
     f32x4* O = (f32x4*)out;
     const int g = grid_for(n4);
     hipStream_t st = as_stream(stream);
-#define HKP_APPLY(RES, RL) \
-    hipLaunchKernelGGL((bn_apply_kernel<RES, RL>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, RSH, \
-                       (const _Float16*)res_split, O, (_Float16*)out_split, split_passes)
+    const bool fix = ((long)g * 256) % C4 == 0;
+#define HKP_APPLY(RES, RL)                                                                                         \
+    if (fix)                                                                                                       \
+        hipLaunchKernelGGL((bn_apply_kernel<RES, RL, true>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R, RSC, \
+                           RSH, (const _Float16*)res_split, O, (_Float16*)out_split, split_passes);               \
+    else                                                                                                           \
+        hipLaunchKernelGGL((bn_apply_kernel<RES, RL, false>), dim3(g), dim3(256), 0, st, n4, C4, Y, SC, SH, R,     \
+                           RSC, RSH, (const _Float16*)res_split, O, (_Float16*)out_split, split_passes)
     if (res_split) {
         if (relu) HKP_APPLY(3, true); else HKP_APPLY(3, false);
     } else if (!res) {
