@@ -2182,7 +2182,7 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
         default:
             break;
     }
-    const bool sk = sk_ok && policy != HKP_TILE_NO_SK;
+    const bool sk = sk_ok && policy != HKP_TILE_NO_SK && policy != HKP_TILE_256_TAIL;
     const X3Plan pl = x3_plan(k, m_tiles, nks, sk, policy == HKP_TILE_SK ? 0.0 : sk_over(nks));
     if (pl.sk) return {pl.bn, pl.bn == 128 ? 16 : 32, false, true};
     if (pl.bn == 256) return {256, 16, false, false};
