@@ -1086,8 +1086,10 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
 // launch is laid out as a column-grouped stream-K grid of NG = tiles x S groups,
 // so every group's unit range lies inside one tile).  The stream-K kernel's
 // segment loop is what made the 256x256 stream-K body spill; a block here runs
-// exactly one segment.  E.g. C2 layer3 on 256x256 tiles: 600 tiles = 2 rounds +
-// 88 tiles, which run as 176 half tiles (~0.6 of a tile time instead of 1).
+// exactly one segment (a two-segment form that balanced C2 layer4's 176 tail
+// tiles over all 256 CUs spilled outside the K loop and measured no faster than
+// the plain partial round, whose CUs run at a higher clock).  C2 layer3 on
+// 256x256 tiles: 600 tiles = 2 rounds + 88 tiles, which run as 176 half tiles.
 template <int BN, int P>
 __global__ __launch_bounds__(512, 1) void conv_x3_tail_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, false, P) + x3_red_bytes(BN, false)];
@@ -2081,28 +2083,27 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // 256x128 1.82 ms; on C2 layer3 (Cout 256, 600 m-tiles) 256x256 loses to round
 // quantisation (0.53 vs 0.47 ms).  No stream-K with 256x256 tiles (the one-tile
 // 256x256 kernel sits at 255 VGPRs; the stream-K loop would spill).
-// Split-K tail (conv_x3_tail_kernel) for a one-tile grid of `tiles` tiles: the
-// segment count S for the tiles past the last full round (0: none), cost in
-// tile times 1/S + 0.08 — the 0.08 is a segment's fill, slab hand-off and
-// combine.  The tail is ONE round (Tr*S <= CUs): the stream-K workspace holds
-// two slabs per CU.  C2 layer3 on 256x256 tiles (88 tail tiles): S = 2, ~0.58
-// instead of 1.
-static int x3_tail_split(long tiles, int nks, double* cost = nullptr) {
-    const int G = x3_cus();
-    const long tr = tiles % G;
+// Split-K tail (conv_x3_tail_kernel) for a one-tile grid of m_tiles x nt tiles:
+// the group count NG = tm*S of the tail grid (0: no tail) — each of the tm
+// m-tiles past the last full round in S equal K segments, one per group, in ONE
+// round (tm*S <= CUs/nt) — and its cost in tile times, 1/S + 0.08 (a segment's
+// fill, slab hand-off and combine).  C2 layer3 on 256x256 tiles (88 tail
+// tiles): S = 2, ~0.58 instead of 1; training t4: S = 5.  C2 layer4 (88 tail
+// m-tiles x 2 columns) has no S >= 2 that fits one round.
+static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr) {
+    const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G, ngmax = G / nt;
+    const long tm = m_tiles - tiles / G * G / nt;
     double best = 1.0;
-    int bs = 0;
+    long ng = 0;
     if (tr > 0) {
-        for (int S = 2; S <= 8 && nks / S >= 4 && tr * S <= G; ++S) {
-            const double c = 1.0 / S + 0.08;
-            if (c < best - 1e-9) {
-                best = c;
-                bs = S;
+        for (int S = 2; S <= 8 && nks / S >= 4 && tm * S <= ngmax; ++S)
+            if (1.0 / S + 0.08 < best - 1e-9) {
+                best = 1.0 / S + 0.08;
+                ng = tm * S;
             }
-        }
     }
     if (cost) *cost = tr > 0 ? best : 0.0;
-    return bs;
+    return ng;
 }
 
 struct X3Plan {
@@ -2118,7 +2119,7 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
         const long tiles = m_tiles * (k / bn);
         const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
         double tail = (tiles % G) ? 1.0 : 0.0;             // the last, partly filled round
-        if (bn == 256 && sk_ok) x3_tail_split(tiles, nks, &tail);
+        if (bn == 256 && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail);
         const double dp = ((double)(tiles / G) + tail) * col;
         if (dp < best_cost - 1e-9) {
             best_cost = dp;
@@ -2255,20 +2256,18 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     }
     // split-K tail for the 256x256 one-tile grid (auto, or forced by HKP_TILE_256_TAIL)
     const long tiles = m_tiles * a.n_tiles;
-    int S = (!c.sk && !c.persist && c.bn == 256 && sk_ok &&
-             (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))
-                ? x3_tail_split(tiles, nks) : 0;
-    // the tail grid holds two slabs per block in the stream-K workspace and one
-    // arrival counter per tail tile: at most one round (x3_tail_split), checked
-    if (S > 0) {
-        const long tm = m_tiles - tiles / x3_cus() * x3_cus() / a.n_tiles;
-        const long gx = tm * S * a.n_tiles;
-        if (gx > x3_cus() || 2L * gx * 256 * 1024 + X3_SK_CNT_BYTES > ws_bytes || tm * a.n_tiles * 4 > X3_SK_CNT_BYTES)
-            S = 0;
-    }
-    if (S > 0) {
-        const long G = x3_cus();
-        const long rm = tiles / G * G / a.n_tiles;          // m-tiles of the full rounds
+    const long G = x3_cus();
+    const long rm = tiles / G * G / a.n_tiles;              // m-tiles of the full rounds
+    const long tm = m_tiles - rm;
+    long NG = (!c.sk && !c.persist && c.bn == 256 && sk_ok &&
+               (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))
+                  ? x3_tail_groups(m_tiles, a.n_tiles, nks) : 0;
+    // one round, every group non-empty and inside two tiles, slabs and counters in the workspace
+    if (NG > 0 && !(tm > 0 && NG * a.n_tiles <= G && tm * nks >= NG && tm < NG &&
+                    2L * G * 256 * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
+        NG = 0;
+    const bool tail = NG > 0;
+    if (tail) {
         if (rm > 0) {
             dim3 g0((unsigned)(rm * a.n_tiles));
             if (P == 3) launch_x3_p<3>(c, g0, st, a);
@@ -2276,11 +2275,10 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         }
         X3Args t = a;
         t.mt0 = (int)rm;
-        const long tm = m_tiles - rm;
         t.sk_units = tm * nks;
         t.sk_cnt = (unsigned*)ws;
         t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
-        const dim3 gt((unsigned)(tm * S * a.n_tiles));
+        const dim3 gt((unsigned)(NG * a.n_tiles));
         if (P == 3) hipLaunchKernelGGL((conv_x3_tail_kernel<256, 3>), gt, dim3(512), 0, st, t);
         else hipLaunchKernelGGL((conv_x3_tail_kernel<256, 1>), gt, dim3(512), 0, st, t);
         return;

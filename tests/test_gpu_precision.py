@@ -385,7 +385,9 @@ def test_f16_forward_close_to_reference(cuda_device, golden, precision):
     err = np.abs(hm.cpu().numpy() - g["heat"]).max()
     agree = (yx.cpu().numpy() == g["argmax_yx"]).all(-1).mean()
     print("fp16 R50: max heat err %.3g, argmax agreement %.2f" % (err, agree))
-    assert err < 1e-1 and agree >= 0.5   # fp16 operands through 53 train-mode-BN layers
+    # fp16 operands through 53 train-mode-BN layers: gate at the measured values
+    # (round 2: max err 0.057, 13 of 16 argmax (y, x) equal) with a small margin
+    assert err < 0.075 and agree >= 0.75
 
 
 SK_CASES = [
