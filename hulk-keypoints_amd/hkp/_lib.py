@@ -7,7 +7,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhulkkp.so")
+# HKP_LIB_AB: an alternative build of the same ABI for in-tree A/B runs (tools/ab.sh);
+# unset, the product loads its own in-tree library
+LIB_PATH = os.environ.get("HKP_LIB_AB") or os.path.join(_HERE, "libhulkkp.so")
 
 HKP_LAYOUT_NHWC = 0
 HKP_LAYOUT_NCHW = 1
