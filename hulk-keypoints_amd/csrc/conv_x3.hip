@@ -116,8 +116,9 @@ __device__ __forceinline__ void lds_sync() {
     lds_barrier();
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
 }
 
 // LDS-DMA through a raw buffer resource: address = base + soffset + voffset; a
@@ -140,6 +141,24 @@ __device__ __forceinline__ i32x4 buffer_rsrc(const void* base, unsigned bytes) {
 __device__ __forceinline__ void blds16(i32x4 rsrc, unsigned voff, unsigned soff, char* lds_wave_base) {
     hkp_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_wave_base, 16, (int)voff, (int)soff, 0, 0);
 }
+
+// the 2-stage bodies' next-stage DMA pieces go out with the MFMAs of the first
+// X3_DMA_COLS column blocks of a K-step (build-time knob for A/B builds)
+// timing probes (A/B builds only, results meaningless): 1 = no DMA inside the
+// 2-stage K loop, 2 = no MFMA (operand reads kept)
+#ifndef X3_PROBE
+#define X3_PROBE 0
+#endif
+// cache policy bits of the conv's A / B operand DMA (A/B builds)
+#ifndef X3_AUX_A
+#define X3_AUX_A 0
+#endif
+#ifndef X3_AUX_B
+#define X3_AUX_B 0
+#endif
+#ifndef X3_DMA_COLS
+#define X3_DMA_COLS 8
+#endif
 
 // schedule NM MFMAs and NR ds_reads of one basic block as evenly spread
 // groups: MFMA first, then one read after every NM/NR MFMAs
@@ -531,7 +550,12 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
     };
     auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
+#if X3_PROBE == 2
+        asm volatile("" ::"v"(x), "v"(y));
+        return c;
+#else
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+#endif
     };
     auto mma_col = [&](const FA& f, int j) {
 #pragma unroll
@@ -543,13 +567,15 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     // barrier (a piece costs ~60 issue cycles, MI355X_MICROARCH.md; the burst
     // left every SIMD without an MFMA to issue right after each barrier).  The
     // last K-steps issue nothing (peeled: no branch inside the scheduled region).
+    constexpr int DC = X3_DMA_COLS < UN ? X3_DMA_COLS : UN;     // columns the pieces spread over
+    constexpr int DPC = (GL + DC - 1) / DC;                     // pieces per such column
     auto sched_kstep = [&](const bool dma) {
 #pragma unroll
         for (int j = 0; j < UN; ++j) {
             __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
-            if (dma && j * ((GL + UN - 1) / UN) < GL)
-                __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);   // DMA pieces
+            if (dma && j < DC && j * DPC < GL)
+                __builtin_amdgcn_sched_group_barrier(0x020, DPC, 0);     // DMA pieces
         }
     };
     if constexpr (NST == 2) {
@@ -575,7 +601,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             lds_barrier();
             cur ^= 1;
             const char* st = smem + cur * STAGE;
-            if (dma) issue_next();
+            if (dma && X3_PROBE != 1) issue_next();
 #pragma unroll
             for (int j = 0; j < UN; ++j) {
                 mma_col(fa, j);
@@ -860,11 +886,11 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         for (int i = 0; i < GA; ++i) {
             const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
             const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-            glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+            glds16<X3_AUX_A>(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
         }
         const int boff = (q_tap * a.cch + q_cc) * 64;
 #pragma unroll
-        for (int j = 0; j < GB; ++j) glds16(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
+        for (int j = 0; j < GB; ++j) glds16<X3_AUX_B>(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
         q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
         if (++q_ss == a.S) {
             q_ss = 0;

@@ -86,7 +86,7 @@ def main():
         ho, wo = ops.conv_out_hw(h, w, k, k, st, pd, dl)
         flops = 2.0 * n * ho * wo * co * ci * k * k * passes
         ref = outs[tiles[0]]
-        same = max((outs[t] - ref).abs().max().item() / ref.abs().max().item() for t in tiles)
+        same = max((outs[t] - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30) for t in tiles)
         for t in tiles:
             ts = sorted(times[t])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
