@@ -145,9 +145,17 @@ def pmc_traffic(kernel_sym, tag):
     summary (profiles/*<tag>*pmc*.json, separate FETCH_SIZE / WRITE_SIZE passes):
     (FETCH_SIZE * 2 + WRITE_SIZE) * 1024 — gfx950's FETCH_SIZE counts half of a
     wide streaming read (MI355X_MICROARCH.md §HBM).  The kernel name must match
-    exactly (spaces ignored).  (None, None) if no summary has it."""
+    exactly (spaces ignored).  A 256x256 conv_x3 launch whose last round runs as
+    the split-K tail (conv_x3_tail_kernel, same stream, inside the same event
+    pair) gets the tail's bytes and time folded in per main dispatch, so the
+    figures describe what the event timed.  Returns (bytes, source file,
+    rocprof average ms of the same scope, folded kernel or None); Nones if no
+    summary has the kernel."""
     import glob
     want = "::" + _nospace(kernel_sym) + "("
+    tail_want = None
+    if kernel_sym.startswith("conv_x3_kernel<256,"):
+        tail_want = "::conv_x3_tail_kernel<256,%s>(" % _nospace(kernel_sym).rstrip(">").split(",")[-1]
     paths = glob.glob(os.path.join(REPO, "profiles", "*%s*pmc*.json" % tag))
     for path in sorted(paths, reverse=True):       # rNN_..._vNN names: newest round / version first
         try:
@@ -156,8 +164,17 @@ def pmc_traffic(kernel_sym, tag):
             continue
         for name, c in data.items():
             if want in _nospace(name) and "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-                return (c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024, os.path.basename(path)
-    return None, None
+                nbytes = (c["FETCH_SIZE"] * 2 + c["WRITE_SIZE"]) * 1024
+                ms = c.get("avg_duration_ns", 0.0) * 1e-6
+                folded = None
+                for tname, t in data.items():
+                    if tail_want and tail_want in _nospace(tname) and "FETCH_SIZE" in t and "WRITE_SIZE" in t:
+                        per = t.get("dispatches", 0) / max(c.get("dispatches", 1), 1)
+                        nbytes += (t["FETCH_SIZE"] * 2 + t["WRITE_SIZE"]) * 1024 * per
+                        ms += t.get("avg_duration_ns", 0.0) * 1e-6 * per
+                        folded = tname
+                return nbytes, os.path.basename(path), ms or None, folded
+    return None, None, None, None
 
 
 def host_cores():
@@ -344,7 +361,8 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
         roof["frac_of_x3_ceiling"] = alg / (PEAK_FP16_MFMA_TFLOPS / 3)
     tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
     if (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3":
-        roof["traffic"], roof["traffic_source"] = pmc_traffic(dom_sym, tag)
+        (roof["traffic"], roof["traffic_source"], roof["rocprof_avg_ms"],
+         roof["folded_kernel"]) = pmc_traffic(dom_sym, tag)
     return {"value": value, "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
             "batch_per_gpu": B, "global_batch": B * world, "roofline": roof,
             "model_tflops": value / world * fl_img * (3 if mode == "train" else 1) / 1e12,

@@ -156,6 +156,10 @@ __device__ __forceinline__ void blds16(i32x4 rsrc, unsigned voff, unsigned soff,
 #ifndef X3_AUX_B
 #define X3_AUX_B 0
 #endif
+// operand DMA through raw buffer resources (A/B build)
+#ifndef X3_BUF
+#define X3_BUF 0
+#endif
 #ifndef X3_DMA_COLS
 #define X3_DMA_COLS 8
 #endif
@@ -812,6 +816,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(P == 3 || (P == 1 && !STEM), "bad conv_x3 operand layout");
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
+    constexpr bool BUF = X3_BUF && !STEM;
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
@@ -858,7 +863,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             off = (((long)n * a.H + hb) * a.W + wb) * cstride + L;
         }
         a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
-        a_off[i] = (unsigned)(off + xbias);
+        a_off[i] = (unsigned)(off + xbias) * (BUF ? 2u : 1u);
     }
     const int bline = a.RS * a.cch * 64;           // halves per weight row (output channel)
     int b_off[GB], b_dst[GB];
@@ -867,10 +872,18 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         const int bi = (w * GB + j) % GBT;
         const int row = RPI * bi + lane / CPR;
         const int Lc = (lane % CPR) ^ swz(row);
-        b_off[j] = (n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc));
+        b_off[j] = ((n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc))) * (BUF ? 2 : 1);
         b_dst[j] = (BM + RPI * bi) * ROW;
     }
     const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    // BUF: byte offsets through raw buffer resources (tap / K-step offsets in the
+    // scalar soffset, out-of-image taps = a voffset past num_records: zeros)
+    const unsigned xbytes = (unsigned)((xbias + (long)a.N * a.H * a.W * cstride) * 2);
+    i32x4 xrs{}, wrs{};
+    if constexpr (BUF) {
+        xrs = buffer_rsrc(xbase, xbytes);
+        wrs = buffer_rsrc(a.ws, (unsigned)((long)a.K * a.RS * cstride * 2));
+    }
 
     // staging state of the next K-step to issue (wave-uniform, advanced per issue)
     // (a stream-K segment starts at K-step ks: channel group outer, tap inner)
@@ -886,11 +899,15 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         for (int i = 0; i < GA; ++i) {
             const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
             const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-            glds16<X3_AUX_A>(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+            if constexpr (BUF) blds16(xrs, in ? a_off[i] : xbytes, (unsigned)toff * 2u, st + (RPI * (w * GA + i)) * ROW);
+            else glds16<X3_AUX_A>(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
         }
         const int boff = (q_tap * a.cch + q_cc) * 64;
 #pragma unroll
-        for (int j = 0; j < GB; ++j) glds16<X3_AUX_B>(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
+        for (int j = 0; j < GB; ++j) {
+            if constexpr (BUF) blds16(wrs, (unsigned)b_off[j], (unsigned)boff * 2u, st + b_dst[j]);
+            else glds16<X3_AUX_B>(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
+        }
         q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
         if (++q_ss == a.S) {
             q_ss = 0;

@@ -1,6 +1,7 @@
 """CPU tests of the host-side logic: DP gradient bucketing over a real
 2-process gloo group, the dataset / transform surface, and Prediction helpers."""
 import os
+import sys
 import socket
 
 import numpy as np
@@ -329,3 +330,30 @@ def test_cv2_circle_disc_halfwidths():
     hw = Prediction.disc_halfwidths(4)
     assert hw == [4, 3, 3, 2, 0]
     assert sum(2 * h + 1 for h in hw[1:]) * 2 + 2 * hw[0] + 1 == 49
+
+
+def test_bench_pmc_traffic_folds_split_k_tail():
+    """The dominant 256x256 conv's event pair also brackets its split-K tail
+    launch: bench.pmc_traffic folds the tail's bytes and rocprof time in per main
+    dispatch, and the folded average equals main + tail * (tail / main dispatches)
+    of the committed summary it read."""
+    import json
+    sys.path.insert(0, REPO)
+    import bench
+    sym = "conv_x3_kernel<256, false, false, 16, false, 3>"
+    nbytes, src, ms, folded = bench.pmc_traffic(sym, "infer_c2")
+    if src is None:
+        pytest.skip("no committed C2 PMC summary")
+    data = json.load(open(os.path.join(REPO, "profiles", src)))
+    main = next(c for n, c in data.items() if "::" + sym.replace(" ", "") + "(" in n.replace(" ", ""))
+    plain = (main["FETCH_SIZE"] * 2 + main["WRITE_SIZE"]) * 1024
+    if folded is None:
+        assert nbytes == plain
+    else:
+        t = data[folded]
+        per = t["dispatches"] / main["dispatches"]
+        assert nbytes == pytest.approx(plain + (t["FETCH_SIZE"] * 2 + t["WRITE_SIZE"]) * 1024 * per)
+        assert ms == pytest.approx((main["avg_duration_ns"] + t["avg_duration_ns"] * per) * 1e-6)
+    # kernels without a tail are looked up unchanged
+    nb2, _, _, f2 = bench.pmc_traffic("wgrad_x3_kernel<256>", "train_c3")
+    assert f2 is None
