@@ -116,9 +116,8 @@ __device__ __forceinline__ void lds_sync() {
     lds_barrier();
 }
 
-template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* src, char* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, AUX);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
 // LDS-DMA through a raw buffer resource: address = base + soffset + voffset; a
@@ -141,28 +140,6 @@ __device__ __forceinline__ i32x4 buffer_rsrc(const void* base, unsigned bytes) {
 __device__ __forceinline__ void blds16(i32x4 rsrc, unsigned voff, unsigned soff, char* lds_wave_base) {
     hkp_raw_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_wave_base, 16, (int)voff, (int)soff, 0, 0);
 }
-
-// the 2-stage bodies' next-stage DMA pieces go out with the MFMAs of the first
-// X3_DMA_COLS column blocks of a K-step (build-time knob for A/B builds)
-// timing probes (A/B builds only, results meaningless): 1 = no DMA inside the
-// 2-stage K loop, 2 = no MFMA (operand reads kept)
-#ifndef X3_PROBE
-#define X3_PROBE 0
-#endif
-// cache policy bits of the conv's A / B operand DMA (A/B builds)
-#ifndef X3_AUX_A
-#define X3_AUX_A 0
-#endif
-#ifndef X3_AUX_B
-#define X3_AUX_B 0
-#endif
-// operand DMA through raw buffer resources (A/B build)
-#ifndef X3_BUF
-#define X3_BUF 0
-#endif
-#ifndef X3_DMA_COLS
-#define X3_DMA_COLS 8
-#endif
 
 // schedule NM MFMAs and NR ds_reads of one basic block as evenly spread
 // groups: MFMA first, then one read after every NM/NR MFMAs
@@ -554,12 +531,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
     };
     auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
-#if X3_PROBE == 2
-        asm volatile("" ::"v"(x), "v"(y));
-        return c;
-#else
         return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
-#endif
     };
     auto mma_col = [&](const FA& f, int j) {
 #pragma unroll
@@ -571,15 +543,13 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     // barrier (a piece costs ~60 issue cycles, MI355X_MICROARCH.md; the burst
     // left every SIMD without an MFMA to issue right after each barrier).  The
     // last K-steps issue nothing (peeled: no branch inside the scheduled region).
-    constexpr int DC = X3_DMA_COLS < UN ? X3_DMA_COLS : UN;     // columns the pieces spread over
-    constexpr int DPC = (GL + DC - 1) / DC;                     // pieces per such column
     auto sched_kstep = [&](const bool dma) {
 #pragma unroll
         for (int j = 0; j < UN; ++j) {
             __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
             __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
-            if (dma && j < DC && j * DPC < GL)
-                __builtin_amdgcn_sched_group_barrier(0x020, DPC, 0);     // DMA pieces
+            if (dma && j * ((GL + UN - 1) / UN) < GL)
+                __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);   // DMA pieces
         }
     };
     if constexpr (NST == 2) {
@@ -605,7 +575,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             lds_barrier();
             cur ^= 1;
             const char* st = smem + cur * STAGE;
-            if (dma && X3_PROBE != 1) issue_next();
+            if (dma) issue_next();
 #pragma unroll
             for (int j = 0; j < UN; ++j) {
                 mma_col(fa, j);
@@ -816,7 +786,6 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(P == 3 || (P == 1 && !STEM), "bad conv_x3 operand layout");
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
-    constexpr bool BUF = X3_BUF && !STEM;
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
@@ -863,7 +832,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             off = (((long)n * a.H + hb) * a.W + wb) * cstride + L;
         }
         a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
-        a_off[i] = (unsigned)(off + xbias) * (BUF ? 2u : 1u);
+        a_off[i] = (unsigned)(off + xbias);
     }
     const int bline = a.RS * a.cch * 64;           // halves per weight row (output channel)
     int b_off[GB], b_dst[GB];
@@ -872,18 +841,10 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         const int bi = (w * GB + j) % GBT;
         const int row = RPI * bi + lane / CPR;
         const int Lc = (lane % CPR) ^ swz(row);
-        b_off[j] = ((n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc))) * (BUF ? 2 : 1);
+        b_off[j] = (n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc));
         b_dst[j] = (BM + RPI * bi) * ROW;
     }
     const _Float16* zero = (const _Float16*)g_x3_zero_line;
-    // BUF: byte offsets through raw buffer resources (tap / K-step offsets in the
-    // scalar soffset, out-of-image taps = a voffset past num_records: zeros)
-    const unsigned xbytes = (unsigned)((xbias + (long)a.N * a.H * a.W * cstride) * 2);
-    i32x4 xrs{}, wrs{};
-    if constexpr (BUF) {
-        xrs = buffer_rsrc(xbase, xbytes);
-        wrs = buffer_rsrc(a.ws, (unsigned)((long)a.K * a.RS * cstride * 2));
-    }
 
     // staging state of the next K-step to issue (wave-uniform, advanced per issue)
     // (a stream-K segment starts at K-step ks: channel group outer, tap inner)
@@ -899,15 +860,11 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         for (int i = 0; i < GA; ++i) {
             const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
             const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-            if constexpr (BUF) blds16(xrs, in ? a_off[i] : xbytes, (unsigned)toff * 2u, st + (RPI * (w * GA + i)) * ROW);
-            else glds16<X3_AUX_A>(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+            glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
         }
         const int boff = (q_tap * a.cch + q_cc) * 64;
 #pragma unroll
-        for (int j = 0; j < GB; ++j) {
-            if constexpr (BUF) blds16(wrs, (unsigned)b_off[j], (unsigned)boff * 2u, st + b_dst[j]);
-            else glds16<X3_AUX_B>(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
-        }
+        for (int j = 0; j < GB; ++j) glds16(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
         q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
         if (++q_ss == a.S) {
             q_ss = 0;
