@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, cons
             if constexpr (RELU) o[e] = o[e] > 0.f ? o[e] : 0.f;
             h[e] = (_Float16)o[e];
         }
-        out[i] = h;
+        __builtin_nontemporal_store(h, out + i);
         if (out32) {
             out32[2 * i] = f32x4{o[0], o[1], o[2], o[3]};
             out32[2 * i + 1] = f32x4{o[4], o[5], o[6], o[7]};
@@ -225,11 +225,11 @@ __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, cons
         load_ss((int)(i0 % C8) * 8);
         long i = i0;
         for (; i + stride < n8; i += 2 * stride) {
-            const h16x8 v0 = y[i], v1 = y[i + stride];
+            const h16x8 v0 = __builtin_nontemporal_load(y + i), v1 = __builtin_nontemporal_load(y + i + stride);
             h16x8 r0{}, r1{};
             if constexpr (RES != 0) {
-                r0 = res[i];
-                r1 = res[i + stride];
+                r0 = __builtin_nontemporal_load(res + i);
+                r1 = __builtin_nontemporal_load(res + i + stride);
             }
             one(i, v0, r0);
             one(i + stride, v1, r1);
@@ -296,9 +296,9 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int 
     }
 }
 
-static inline int grid_for(long work, int block = 256) {
+static inline int grid_for(long work, int block = 256, long cap = 256L * 16) {
     long g = (work + block - 1) / block;
-    if (g > 256L * 16) g = 256L * 16;
+    if (g > cap) g = cap;
     return (int)(g < 1 ? 1 : g);
 }
 
@@ -406,7 +406,11 @@ extern "C" int hkp_bn_apply_f16(int64_t m, int32_t c, const uint16_t* y, const f
     HKP_CHECK_ARG(y && scale_shift && out, "hkp_bn_apply_f16: null tensor");
     HKP_CHECK_ARG(res_scale_shift == nullptr || res != nullptr, "hkp_bn_apply_f16: res_scale_shift without res");
     const long n8 = m * (long)c / 8;
-    const int g = grid_for(n8);
+    // two 4-wave blocks per CU, streaming loads/stores: the fp16 tensors here
+    // (0.3-2.5 GB at C4) stream through once; 16 blocks per CU and cached
+    // accesses ran 5.0-5.1 TB/s vs 6.1 on the same 2-read-1-write stream
+    // (tools/apply_bw.hip), C4 +3.5 % end to end
+    const int g = grid_for(n8, 256, 512);
     hipStream_t st = as_stream(stream);
     const h16x8 *Y = (const h16x8*)y, *R = (const h16x8*)res;
     h16x8* O = (h16x8*)out;

@@ -84,16 +84,17 @@ int main() {
     };
     const double b3 = 3.0 * n8 * 16, b2 = 2.0 * n8 * 16;
     const int C8 = C / 8;
-    for (int g : {4096, 2048, 1024}) {
+    for (int rep = 0; rep < 2; ++rep)
+    for (int g : {4096, 2048, 1536, 1024, 768, 512}) {
         char nm[64];
         snprintf(nm, 64, "apply U2 grid %d", g);
         timeit(nm, b3, [&] { hipLaunchKernelGGL((apply_res<2, false>), dim3(g), dim3(256), 0, 0, n8, C8, y, ss, r, o); });
-        snprintf(nm, 64, "apply U4 grid %d", g);
-        timeit(nm, b3, [&] { hipLaunchKernelGGL((apply_res<4, false>), dim3(g), dim3(256), 0, 0, n8, C8, y, ss, r, o); });
         snprintf(nm, 64, "apply U2 nt grid %d", g);
         timeit(nm, b3, [&] { hipLaunchKernelGGL((apply_res<2, true>), dim3(g), dim3(256), 0, 0, n8, C8, y, ss, r, o); });
         snprintf(nm, 64, "apply U1 grid %d", g);
         timeit(nm, b3, [&] { hipLaunchKernelGGL((apply_res<1, false>), dim3(g), dim3(256), 0, 0, n8, C8, y, ss, r, o); });
+        snprintf(nm, 64, "apply U1 nt grid %d", g);
+        timeit(nm, b3, [&] { hipLaunchKernelGGL((apply_res<1, true>), dim3(g), dim3(256), 0, 0, n8, C8, y, ss, r, o); });
     }
     timeit("copy grid 4096", b2, [&] { hipLaunchKernelGGL(copy16, dim3(4096), dim3(256), 0, 0, n8, y, o); });
     timeit("copy grid 2048", b2, [&] { hipLaunchKernelGGL(copy16, dim3(2048), dim3(256), 0, 0, n8, y, o); });
