@@ -15,6 +15,30 @@
 
 namespace hkp {
 
+// scale/shift, mean/invstd and running statistics of channel c from the merged
+// fp64 mean and M2 (sum of squared deviations over all `count` rows)
+__device__ __forceinline__ void bn_fin_store(int c, int C, long count, double mean, double m2, const float* gamma,
+                                             const float* beta, float momentum, float eps, float* rmean, float* rvar,
+                                             int64_t* nbt, float* ss, float* mi) {
+    const double var = m2 / (double)count;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const float inv_f = (float)invstd, mean_f = (float)mean;
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float alpha = __fmul_rn(inv_f, g);
+    ss[c] = alpha;
+    ss[C + c] = __fsub_rn(b, __fmul_rn(mean_f, alpha));
+    if (mi) {
+        mi[c] = mean_f;
+        mi[C + c] = inv_f;
+    }
+    if (rmean) {
+        const double unbiased = count > 1 ? m2 / (double)(count - 1) : var;
+        rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
+        rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+}
+
 // CPB channels per block (partials_cpb); deterministic fixed-order fp64 merge
 // NT threads per block: 256, or 1024 for long tile lists (the stem's 19,200
 // tiles at C2: per-thread load chains of 75 tiles took 75 us with 256 threads)
@@ -62,25 +86,93 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long
             }
         }
     const double m2 = lanes_sum_d<CPB, NW>(q, red);
-    if (tl == 0 && ok) {
-        const double var = m2 / (double)count;
-        const double invstd = 1.0 / sqrt(var + (double)eps);
-        const float inv_f = (float)invstd, mean_f = (float)mean;
-        const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
-        const float alpha = __fmul_rn(inv_f, g);
-        ss[c] = alpha;
-        ss[C + c] = __fsub_rn(b, __fmul_rn(mean_f, alpha));
-        if (mi) {
-            mi[c] = mean_f;
-            mi[C + c] = inv_f;
-        }
-        if (rmean) {
-            const double unbiased = count > 1 ? m2 / (double)(count - 1) : var;
-            rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
-            rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
-        }
-        if (nbt && c == 0) nbt[0] += 1;
+    if (tl == 0 && ok)
+        bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+}
+
+// Two-level form for long tile lists (hkp_bn_finalize_ws).  The one-kernel merge
+// above runs C/CPB blocks whose threads walk `tiles` partials in dependent load
+// batches: the stem and layer1 (C = 64, 19,200 / 4,800 tiles at C2) used 64 CUs
+// for 23 us, and R50's C = 2048 convs (C4: 4,800 tiles, 78 MB of partials) 30-60 us.
+// Level 1 (bn_fin_chunk_kernel, grid [C/64][chunks]): a block = 64 channel lanes x
+// 16 tile lanes reduces one chunk of FIN_CHUNK tiles — each lane holds its 8
+// partials in registers — to the chunk's (sum, M2 about the chunk mean), both
+// fixed-order fp64 (Chan, as the one-kernel form does over all tiles).  A wave
+// reads one tile row of 64 channels: 512 contiguous bytes.
+// Level 2 (bn_fin_merge_kernel, grid C/64): the chunks merged by the same formula
+// in fixed order -> mean, M2 -> bn_fin_store.  Deterministic run to run.
+constexpr int FIN_TL = 16, FIN_TPL = 8, FIN_CHUNK = FIN_TL * FIN_TPL;
+
+__device__ __forceinline__ double fin_col_sum(double v, double (*red)[64], int tl, int cl) {
+    __syncthreads();                               // red free (a previous call's readers are done)
+    red[tl][cl] = v;
+    __syncthreads();
+    double a[FIN_TL];
+#pragma unroll
+    for (int i = 0; i < FIN_TL; ++i) a[i] = red[i][cl];
+#pragma unroll
+    for (int w = FIN_TL / 2; w >= 1; w >>= 1)
+#pragma unroll
+        for (int i = 0; i < w; ++i) a[i] = a[2 * i] + a[2 * i + 1];
+    return a[0];
+}
+
+__global__ __launch_bounds__(1024) void bn_fin_chunk_kernel(int C, long count, long tiles, int tile_rows,
+                                                            const float* __restrict__ part, double2* __restrict__ ws) {
+    __shared__ double red[FIN_TL][64];
+    const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+    const bool ok = c < C;
+    const long t0 = (long)blockIdx.y * FIN_CHUNK;
+    float2 v[FIN_TPL];
+#pragma unroll
+    for (int j = 0; j < FIN_TPL; ++j) {
+        const long t = t0 + tl + (long)FIN_TL * j;
+        v[j] = ok && t < tiles ? *(const float2*)(part + (t * C + c) * 2) : make_float2(0.f, 0.f);
     }
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < FIN_TPL; ++j) s += (double)v[j].x;
+    const double S = fin_col_sum(s, red, tl, cl);
+    const long te = min(tiles, t0 + FIN_CHUNK);
+    const long nk = min(count, te * (long)tile_rows) - t0 * (long)tile_rows;   // rows in this chunk
+    const double mk = S / (double)nk;
+    double q = 0.0;
+#pragma unroll
+    for (int j = 0; j < FIN_TPL; ++j) {
+        const long t = t0 + tl + (long)FIN_TL * j;
+        if (t < tiles) {
+            const long n_t = min((long)tile_rows, count - t * tile_rows);
+            const double dm = (double)v[j].x / (double)n_t - mk;
+            q += (double)v[j].y + (double)n_t * dm * dm;
+        }
+    }
+    const double Q = fin_col_sum(q, red, tl, cl);
+    if (tl == 0 && ok) ws[blockIdx.y * (long)C + c] = make_double2(S, Q);
+}
+
+__global__ __launch_bounds__(1024) void bn_fin_merge_kernel(int C, long count, long chunks, int tile_rows,
+                                                            const double2* __restrict__ ws, const float* gamma,
+                                                            const float* beta, float momentum, float eps,
+                                                            float* rmean, float* rvar, int64_t* nbt, float* ss,
+                                                            float* mi) {
+    __shared__ double red[FIN_TL][64];
+    const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+    const bool ok = c < C;
+    const long rows = (long)FIN_CHUNK * tile_rows;     // rows per full chunk
+    double s = 0.0;
+    if (ok)
+        for (long k = tl; k < chunks; k += FIN_TL) s += ws[k * C + c].x;
+    const double mean = fin_col_sum(s, red, tl, cl) / (double)count;
+    double q = 0.0;
+    if (ok)
+        for (long k = tl; k < chunks; k += FIN_TL) {
+            const double2 w = ws[k * C + c];
+            const long nk = min(rows, count - k * rows);
+            const double dm = w.x / (double)nk - mean;
+            q += w.y + (double)nk * dm * dm;
+        }
+    const double m2 = fin_col_sum(q, red, tl, cl);
+    if (tl == 0 && ok) bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
 }
 
 __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
@@ -330,6 +422,36 @@ extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t 
 #undef HKP_FIN
 #undef HKP_FIN1
     HKP_LAUNCH_CHECK("hkp_bn_finalize");
+    return HKP_OK;
+}
+
+extern "C" int64_t hkp_bn_finalize_workspace_bytes(int32_t c, int64_t tiles) {
+    if (c <= 0 || tiles <= 0) return -1;
+    return ((tiles + FIN_CHUNK - 1) / FIN_CHUNK) * (int64_t)c * (int64_t)sizeof(double2);
+}
+
+extern "C" int hkp_bn_finalize_ws(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                                  const float* gamma, const float* beta, float momentum, float eps,
+                                  float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                                  float* scale_shift, float* mean_invstd, void* workspace, int64_t ws_bytes,
+                                  hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && count > 0 && tiles > 0 && tile_rows > 0, "hkp_bn_finalize_ws: bad sizes");
+    HKP_CHECK_ARG(partials && scale_shift && workspace, "hkp_bn_finalize_ws: null tensor");
+    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "hkp_bn_finalize_ws: running stats pair");
+    HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
+                  "hkp_bn_finalize_ws: tiles/tile_rows inconsistent with count");
+    const int64_t need = hkp_bn_finalize_workspace_bytes(c, tiles);
+    HKP_CHECK_ARG(ws_bytes >= need, "hkp_bn_finalize_ws: workspace %ld < %ld", (long)ws_bytes, (long)need);
+    const long chunks = (tiles + FIN_CHUNK - 1) / FIN_CHUNK;
+    hipStream_t st = as_stream(stream);
+    const unsigned cg = (unsigned)((c + 63) / 64);
+    hipLaunchKernelGGL(bn_fin_chunk_kernel, dim3(cg, (unsigned)chunks), dim3(1024), 0, st, c, (long)count,
+                       (long)tiles, tile_rows, partials, (double2*)workspace);
+    HKP_LAUNCH_CHECK("hkp_bn_finalize_ws (chunks)");
+    hipLaunchKernelGGL(bn_fin_merge_kernel, dim3(cg), dim3(1024), 0, st, c, (long)count, chunks, tile_rows,
+                       (const double2*)workspace, gamma, beta, momentum, eps, running_mean, running_var,
+                       num_batches_tracked, scale_shift, mean_invstd);
+    HKP_LAUNCH_CHECK("hkp_bn_finalize_ws (merge)");
     return HKP_OK;
 }
 

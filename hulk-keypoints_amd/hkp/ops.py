@@ -5,6 +5,7 @@ launch (a mis-shaped launch can fault the GPU), launches on PyTorch's current
 stream, and allocates outputs with the caching allocator.  No fallback path.
 """
 import ctypes
+import os
 
 import torch
 
@@ -388,6 +389,14 @@ def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True
     return y, part
 
 
+# two-level finalize (hkp_bn_finalize_ws) from this many partial tiles on: C4 +2.2 %
+# (R50 C = 2048 convs, 4,800+ tiles); at 300-1,200 tiles (C2 layer2-4, the C3
+# shard) the one-kernel merge already fills the chip and its single launch won
+# (C2 neutral, C3 training -1.2 % with the two-level form everywhere)
+FIN_TWO_LEVEL_TILES = 2048
+_FIN_ONE_KERNEL = os.environ.get("HKP_FIN_ONE_KERNEL") == "1"     # A/B: always the one-kernel merge
+
+
 def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None,
                 momentum=0.1, eps=1e-5, want_mean_invstd=True):
     """Train-mode BN statistics from conv partials → (scale_shift [2C], mean_invstd [2C])."""
@@ -402,6 +411,15 @@ def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, n
                 raise HkpError("bn_finalize.%s: %d != C=%d" % (nm, t.numel(), c))
     if num_batches_tracked is not None:
         _need(num_batches_tracked, torch.int64, "bn_finalize.num_batches_tracked")
+    if tiles >= FIN_TWO_LEVEL_TILES and not _FIN_ONE_KERNEL:
+        # two-level merge (chunks of 128 tiles over [C/64][chunks] blocks, then per channel)
+        from ._lib import lib
+        nb = lib().hkp_bn_finalize_workspace_bytes(c, tiles)
+        ws = torch.empty((nb + 7) // 8, device=part.device, dtype=torch.float64)
+        call("hkp_bn_finalize_ws", c, count, tiles, CONV_TILE_ROWS, _ptr(part), _ptr(gamma), _ptr(beta), momentum,
+             eps, _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi), _ptr(ws),
+             nb, _stream())
+        return ss, mi
     call("hkp_bn_finalize", c, count, tiles, CONV_TILE_ROWS, _ptr(part), _ptr(gamma), _ptr(beta), momentum, eps,
          _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi), _stream())
     return ss, mi

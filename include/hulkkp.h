@@ -175,6 +175,19 @@ int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, 
                     float* running_mean, float* running_var, int64_t* num_batches_tracked,
                     float* scale_shift, float* mean_invstd, hkp_stream_t stream);
 
+/* The same statistics in two levels for long tile lists (tiles > 128): chunks of
+ * 128 tiles reduced by [C/64][chunks] blocks into a caller-allocated fp64
+ * workspace of hkp_bn_finalize_workspace_bytes(c, tiles) bytes, then merged per
+ * channel in fixed order (Chan at both levels).  Same outputs and argument
+ * meaning as hkp_bn_finalize (src/resnet.py:46,49,78,85,87,139,187); the two
+ * forms agree to fp64 summation order. */
+int64_t hkp_bn_finalize_workspace_bytes(int32_t c, int64_t tiles);
+int hkp_bn_finalize_ws(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                       const float* gamma, const float* beta, float momentum, float eps,
+                       float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                       float* scale_shift, float* mean_invstd, void* workspace, int64_t ws_bytes,
+                       hkp_stream_t stream);
+
 /* Eval-mode BN parameters from running statistics (the reference never uses
  * them; offered as an option). */
 int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const float* running_mean,

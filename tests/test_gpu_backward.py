@@ -469,3 +469,57 @@ def test_backward_calls_exact(cuda_device, bb, k):
                 assert dy._hkp_amax.view(torch.float32).item() >= rdy.abs().max().item()
             assert rel(dgam, dgm) < 1e-5 and rel(dbet, db) < 1e-5
     assert n_split > 0                           # the fused split-only BN backward was exercised
+
+
+@pytest.mark.parametrize("c,rows", [(64, 130 * 128 - 37), (96, 300 * 128), (512, 1200 * 128 - 5), (2048, 260 * 128)])
+def test_bn_finalize_two_level(cuda_device, c, rows):
+    """hkp_bn_finalize_ws (chunks of 128 tiles, then a per-channel merge) vs the
+    one-kernel merge and an fp64 reference over the raw rows: mean/invstd and
+    running statistics; partials built per 128-row tile as the conv epilogue does
+    (sum, M2 about the tile mean), a ragged last tile included."""
+    from hkp import ops
+    d = cuda_device
+    g = torch.Generator(device=d).manual_seed(c + rows)
+    y = torch.randn(rows, c, device=d, generator=g, dtype=torch.float64) * 3 + 1.5
+    tiles = (rows + 127) // 128
+    pad = torch.zeros(tiles * 128, c, device=d, dtype=torch.float64)
+    pad[:rows] = y
+    n_t = torch.clamp(rows - torch.arange(tiles, device=d) * 128, max=128).to(torch.float64)
+    yt = pad.view(tiles, 128, c)
+    s = yt.sum(1)
+    valid = (torch.arange(128, device=d)[None, :] < n_t[:, None]).to(torch.float64)
+    m2 = (((yt - (s / n_t[:, None])[:, None, :]) ** 2) * valid[:, :, None]).sum(1)
+    part = torch.stack([s, m2], -1).float().contiguous()
+    gamma = torch.rand(c, device=d, generator=g) + 0.5
+    beta = torch.rand(c, device=d, generator=g) - 0.5
+    outs = []
+    for one in (True, False):
+        ops._FIN_ONE_KERNEL = one
+        lvl, ops.FIN_TWO_LEVEL_TILES = ops.FIN_TWO_LEVEL_TILES, 129     # every case takes the two-level form
+        try:
+            rm, rv = torch.zeros(c, device=d), torch.ones(c, device=d)
+            nbt = torch.zeros(1, device=d, dtype=torch.int64)
+            ss, mi = ops.bn_finalize(part, rows, gamma, beta, rm, rv, nbt)
+            outs.append((ss, mi, rm, rv, nbt))
+        finally:
+            ops._FIN_ONE_KERNEL = False
+            ops.FIN_TWO_LEVEL_TILES = lvl
+    torch.cuda.synchronize()
+    # the two forms: fp64 merges in different orders, rounded to fp32 -> at most 1 ulp apart
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert torch.allclose(a, b, rtol=2.5e-7, atol=0)
+    assert outs[1][4].item() == 1
+    # fp64 reference over the rows (the partials are fp32-rounded: 1e-6 relative)
+    mean = y.mean(0)
+    var = y.var(0, unbiased=False)
+    ss, mi, rm, rv, _ = outs[1]
+    assert torch.allclose(mi[:c].double(), mean, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(mi[c:].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-5)
+    assert torch.allclose(rv.double(), 0.9 + 0.1 * y.var(0, unbiased=True), rtol=1e-5)
+    # deterministic run to run
+    lvl, ops.FIN_TWO_LEVEL_TILES = ops.FIN_TWO_LEVEL_TILES, 129
+    try:
+        ss2, mi2 = ops.bn_finalize(part, rows, gamma, beta)
+    finally:
+        ops.FIN_TWO_LEVEL_TILES = lvl
+    assert torch.equal(ss2, ss) and torch.equal(mi2, mi)
