@@ -1603,11 +1603,16 @@ __device__ __forceinline__ f16x8 cat_tr(s16x4 lo, s16x4 hi) {
 // 64 (KA 128) — the 256x128 body is bound by operand delivery, not the MFMAs
 // (MFMA-busy scales with the intensity: 0.25 at KA 64, 0.42 at KA 128).  Its
 // stage holds PX = 16 pixels (one MFMA k-slice) so three stages fit in 96 KB.
+// The PX = 16 body runs a 4-stage ring (128 KB, inside the epilogue's 132 KB) and
+// issues each stage's DMA as GL = TM pieces placed after the MFMAs of one row
+// (address math branch-free: one wrap per stage, Wo >= PX, see wg_x3_plan), so
+// the per-lane address VALU runs in the MFMA shadow instead of between the
+// barrier and the first MFMA of every stage.
 template <int KA>
 __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
-    constexpr int NS = 3;                                   // LDS ring depth
     constexpr int BR = 256, GX = BR / 32, GD = KA / 32;
     constexpr int PX = KA == 256 ? 16 : 32;                  // pixels per stage
+    constexpr int NS = PX == 16 ? 4 : 3;                     // LDS ring depth
     constexpr int ROW = 128, STAGE = (GX + GD) * PX * ROW;
     constexpr int NX = PX / 8, ND = GD * PX / 64, GL = NX + ND;
     constexpr int TM = KA / 64, TN = 2;
@@ -1683,6 +1688,38 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
         }
     };
 
+    // one DMA piece of stage t (PX == 16 body): k < NX an x slot, else a dy slot.
+    // The x slot's pixel advances by PX per stage with at most one row wrap
+    // (Wo >= PX): selects, no branches, so the piece can sit between MFMAs.
+    auto piece = [&](int t, const int k) {
+        char* st = smem + (t & (NS - 1)) * STAGE;
+        const int pb = p_begin + PX * t;
+        // 32-bit byte offsets (wg_x3_plan: both operands < 4 GiB for KA 256), the
+        // validity as a mask and the zero line as a select: no branch
+        if (k < NX) {
+            const int i = k;
+            const int p = pb + 8 * i + (lane >> 3);
+            const int hi = xho[i] * a.stride + dh, wi = xwo[i] * a.stride + dw;
+            const bool in = gvalid & (p < p_end) & ((unsigned)hi < (unsigned)a.H) & ((unsigned)wi < (unsigned)a.W);
+            const unsigned off = (((unsigned)xn[i] * a.H + hi) * a.W + wi) * (unsigned)(xstride * 2);
+            const char* src = in ? (const char*)xg : (const char*)zero;
+            glds16(src + (in ? off : 0u), st + (w * PX + 8 * i) * ROW);
+            const int w2 = xwo[i] + PX;
+            const bool wrap = w2 >= a.Wo;
+            xwo[i] = wrap ? w2 - a.Wo : w2;
+            const int h2 = xho[i] + (wrap ? 1 : 0);
+            const bool wrap2 = h2 == a.Ho;
+            xho[i] = wrap2 ? 0 : h2;
+            xn[i] += wrap2 ? 1 : 0;
+        } else {
+            const int j = k - NX;
+            const int p = pb + dpp[j];
+            const bool in = p < p_end;
+            const char* src = in ? (const char*)dg[j] : (const char*)zero;
+            glds16(src + (in ? (unsigned)p * (unsigned)(dstride * 2) : 0u), st + (GX * PX + 8 * (w * ND + j)) * ROW);
+        }
+    };
+
     f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1755,9 +1792,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     if constexpr (PX == 16) {
         // one dy fragment set, refilled row by row right after its MFMAs issue
         // (128 accumulators + 32 dy + 2x16 x registers): per stage t
-        // [issue DMA t+2 | wait own DMA t+1 and this wave's reads, barrier |
-        //  rows i = 0..TM-1 of t's MFMAs, each beside the reads of t+1's row i-1
-        //  (row 0 beside t+1's x fragments), then the reads of t+1's last row]
+        // [wait own DMA t+1 and this wave's reads, barrier | t+1's x fragments |
+        //  rows i = 0..TM-1: t's MFMAs, one DMA piece of stage t+3, t+1's row i]
         struct XF {
             f16x8 xh[TN], xl[TN];
         };
@@ -1782,52 +1818,51 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(dl[i], x.xh[j], acc[i][j], 0, 0, 0);
             }
         };
+        static_assert(PX != 16 || GL == TM, "one DMA piece per MFMA row");
         if (nsteps > 0) {
             // prologue: stages 0..NS-2 (past the end: zero lines, never read)
-            int q_t = 0;
 #pragma unroll
-            for (int u = 0; u < NS - 1; ++u) issue(q_t++);
+            for (int u = 0; u < NS - 1; ++u)
+#pragma unroll
+                for (int k = 0; k < GL; ++k) piece(u, k);
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * GL) : "memory");
             lds_barrier();
             read_x(x0, 0);
 #pragma unroll
             for (int i = 0; i < TM; ++i) read_d(i, 0);
-            int nb = 1;                                      // buffer of stage t+1
-            // every non-final stage issues stage t+2's DMA — past the end it loads
-            // zero lines into a buffer no later stage reads — so there is one
-            // kind of non-final step, branch-free, and one final step
-            auto step = [&](const XF& xa, XF& xb) {
-                issue(q_t++);                                 // stage t+NS-1
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NS - 2) * GL) : "memory");
+            // step t: wait for stage t+1 (stage t+2's pieces stay in flight), barrier,
+            // read t+1's fragments row by row beside t's MFMAs, and issue stage
+            // t+3's pieces (into the buffer stage t-1 used: every wave finished
+            // reading it before this step's barrier) one per MFMA row.  Stages past
+            // the end load zero lines into buffers no later stage reads, so every
+            // non-final step is the same branch-free code.
+            auto step = [&](const int t, const XF& xa, XF& xb) {
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NS - 3) * GL) : "memory");
                 lds_barrier();
                 __builtin_amdgcn_sched_barrier(0);
-                const unsigned so = nb * STAGE;
+                const unsigned so = ((t + 1) & (NS - 1)) * STAGE;
                 read_x(xb, so);
-                mma_row(0, xa);
-                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int i = 1; i < TM; ++i) {
-                    read_d(i - 1, so);
+                for (int i = 0; i < TM; ++i) {
                     mma_row(i, xa);
+                    piece(t + NS - 1, i);
+                    read_d(i, so);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                read_d(TM - 1, so);
-                __builtin_amdgcn_sched_barrier(0);
-                nb = nb == NS - 1 ? 0 : nb + 1;
             };
             auto last = [&](const XF& xa) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // + the dummy DMA
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // + the dummy DMAs
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int i = 0; i < TM; ++i) mma_row(i, xa);
             };
             int t = 0;
             for (; t + 2 < nsteps; t += 2) {
-                step(x0, x1);
-                step(x1, x0);
+                step(t, x0, x1);
+                step(t + 1, x1, x0);
             }
             if (t + 1 < nsteps) {
-                step(x0, x1);
+                step(t, x0, x1);
                 x0 = x1;                                     // one last() call site
             }
             last(x0);
@@ -1955,8 +1990,12 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
     }
 }
 
-static void wg_x3_plan(const hkp_conv_desc* d, long M, int* splits, int* mps, int* ka, int* r_tiles) {
-    *ka = d->k % 256 == 0 ? 256 : d->k % 128 == 0 ? 128 : 64;
+static void wg_x3_plan(const hkp_conv_desc* d, long M, int wo, int* splits, int* mps, int* ka, int* r_tiles) {
+    // KA 256's 16-pixel stages advance each x slot with at most one row wrap
+    // (and 32-bit byte offsets into both operands)
+    const bool ka256 = d->k % 256 == 0 && wo >= 16 && (long)d->n * d->h * d->w * d->c * 4 < (1L << 32) &&
+                       M * d->k * 4 < (1L << 32);
+    *ka = ka256 ? 256 : d->k % 128 == 0 ? 128 : 64;
     const long rsc = (long)d->r * d->s * d->c;
     *r_tiles = (int)((rsc + 255) / 256);
     const long tiles = (long)(d->k / *ka) * *r_tiles;
@@ -2511,7 +2550,7 @@ extern "C" int64_t hkp_conv_bwd_filter_x3_workspace(const hkp_conv_desc* d) {
     int ho, wo;
     if (hkp_conv_out_hw(d, &ho, &wo) != HKP_OK) return -1;
     int sp, mps, ka, rt;
-    wg_x3_plan(d, (long)d->n * ho * wo, &sp, &mps, &ka, &rt);
+    wg_x3_plan(d, (long)d->n * ho * wo, wo, &sp, &mps, &ka, &rt);
     return (int64_t)sp * d->k * d->r * d->s * d->c * (int64_t)sizeof(float);
 }
 
@@ -2527,7 +2566,7 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     const long M = (long)d->n * ho * wo;
     HKP_CHECK_ARG(M < (1L << 31), "hkp_conv2d_bwd_filter_x3: too large");
     int sp, mps, ka, rt;
-    wg_x3_plan(d, M, &sp, &mps, &ka, &rt);
+    wg_x3_plan(d, M, wo, &sp, &mps, &ka, &rt);
     const long n = (long)d->k * d->r * d->s * d->c;
     HKP_CHECK_ARG(ws_bytes >= sp * n * (long)sizeof(float), "hkp_conv2d_bwd_filter_x3: workspace %ld < %ld",
                   (long)ws_bytes, sp * n * (long)sizeof(float));
@@ -2654,7 +2693,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
         case HKP_KOP_WGRAD_X3: {
             HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv_kernel_name: wgrad needs Cout%%64==0");
             int sp, mps, ka, rt;
-            wg_x3_plan(d, (long)d->n * ho * wo, &sp, &mps, &ka, &rt);
+            wg_x3_plan(d, (long)d->n * ho * wo, wo, &sp, &mps, &ka, &rt);
             return snprintf(buf, len, "wgrad_x3_kernel<%d>", ka);
         }
         default:
