@@ -593,60 +593,53 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
         for (int j = 0; j < UN; ++j) mma_col(fa, j);
     } else {
-        // prologue: NST-1 stages in flight, stage 0 landed everywhere
-        issue_next();
-        for (int s = 1; s < NST - 1; ++s)
+        // 3-stage ring (256x128 tiles), the 2-stage body's schedule with two
+        // stages of DMA lead: A single-buffered, per K-step t — wait own DMA of
+        // t+1 (t+2 stays in flight), barrier, then per column j [MFMAs of t with
+        // B_j] [refill B_j with t+1's] [a DMA piece of t+3 into t's buffer: t's
+        // fragments were all read during step t-1], then A of t+1.  (The burst
+        // of t+2's DMA before the barrier, with A double-buffered, left every SIMD
+        // without an MFMA to issue after each barrier.)
+        static_assert(NST == 3, "stage t+3 goes into stage t's buffer");
+        for (int s = 0; s < NST; ++s)
             if (s < nks) issue_next();
         store_scl();
         {
-            const int after = std::min(nks - 1, NST - 2);
-            if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+            const int after = std::min(nks, NST) - 1;         // stages in flight past stage 0
+            if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+            else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         lds_barrier();
-        auto wait_next = [&](int t) {
-            const int after = std::min(nks - 1, t + NST - 1) - (t + 1);
-            if (after >= 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        };
-        int cur = 0;
-        FA fa0, fa1;
-        read_a(fa0, smem);
+        x3_stamp(a, 1);
+        FA fa;
+        read_a(fa, smem);
 #pragma unroll
         for (int j = 0; j < UN; ++j) read_b(j, smem);
-        auto step = [&](int t, FA& fc, FA& fn) {       // K-step t, reading t+1's fragments
-            if (t + NST - 1 < nks) issue_next();
-            wait_next(t);
+        int cur = 0;
+        auto kstep = [&](const int t, const bool dma) {
+            if (t + 2 < nks) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();
             cur = cur == NST - 1 ? 0 : cur + 1;
             const char* st = smem + cur * STAGE;
-            read_a(fn, st);
+            if (dma) issue_next();
 #pragma unroll
             for (int j = 0; j < UN; ++j) {
-                mma_col(fc, j);
+                mma_col(fa, j);
                 read_b(j, st);
             }
+            read_a(fa, st);
+            sched_kstep(dma);
             __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);     // column j's MFMAs
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);       // refill B_j
-            }
             __builtin_amdgcn_sched_barrier(0);
         };
         int t = 0;
-        for (; t + 2 < nks; t += 2) {
-            step(t, fa0, fa1);
-            step(t + 1, fa1, fa0);
-        }
-        if (t + 1 < nks) {
-            step(t, fa0, fa1);
+        for (; t + 3 < nks; ++t) kstep(t, true);
+        for (; t + 1 < nks; ++t) kstep(t, false);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-            for (int j = 0; j < UN; ++j) mma_col(fa1, j);
-        } else {
-#pragma unroll
-            for (int j = 0; j < UN; ++j) mma_col(fa0, j);
-        }
+        for (int j = 0; j < UN; ++j) mma_col(fa, j);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the ring past here
     x3_stamp(a, 2);
