@@ -2223,7 +2223,7 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
     return {64, 16, true, false};
 }
 
-static const X3Choice X3_STEM{64, 32, true, false};
+static const X3Choice X3_STEM{64, 16, true, false};
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.persist) return snprintf(buf, len, "conv_x3p_kernel<%d, %d, %s>", c.bn, P, c.one ? "true" : "false");
@@ -2648,8 +2648,8 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     a.n_tiles = d->k / 64;
     const long m_tiles = (M + 255) / 256;
     // two blocks per CU (7 K-steps per tile: prologue / epilogue dominate one
-    // block), 32x32x16 body on a 2-stage ring
-    hipLaunchKernelGGL((conv_x3_kernel<64, true, true, 32, false, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
+    // block), 16x16x32 body on a 2-stage ring (the layer1 256x64 pair's body)
+    hipLaunchKernelGGL((conv_x3_kernel<64, true, true, 16, false, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
                        as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
     return HKP_OK;

@@ -134,4 +134,4 @@ def test_kernel_name_query():
     with pytest.raises(_lib.HkpError, match="tile policy"):
         ops.kernel_name(d, _lib.HKP_KOP_FWD_X3)
     stem = _lib.ConvDesc(32, 480, 640, 3, 64, 7, 7, 2, 3, 1, _lib.HKP_LAYOUT_NCHW)
-    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3) == "conv_x3_kernel<64, true, true, 32, false, 3>"
+    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3) == "conv_x3_kernel<64, true, true, 16, false, 3>"
