@@ -293,9 +293,10 @@ WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (2, 7, 9, 64, 64, 3, 1, 1, 1),          # Wo = 9 < 32: a K-step spans several rows/images
     (1, 30, 40, 96, 128, 3, 2, 1, 1),       # stride 2, RSC = 864 (ragged 256-column tile)
     (2, 30, 40, 256, 256, 3, 1, 2, 2),      # 256x256 tile (16-pixel stages), several pixel splits
-    (1, 3, 5, 64, 256, 3, 1, 1, 1),         # 256x256 tile, M = 15: a single stage
+    (1, 3, 5, 64, 256, 3, 1, 1, 1),         # Cout 256 with Wo = 5 < 16: the KA-128 fallback, one stage
     (1, 30, 40, 96, 256, 3, 2, 1, 1),       # 256x256 tile, RSC 864: column groups past R*S*Cin
-    (2, 7, 9, 64, 256, 3, 1, 1, 1),         # 256x256 tile, Wo = 9: 16-pixel stages wrap rows / images
+    (2, 7, 9, 64, 256, 3, 1, 1, 1),         # Cout 256 with Wo = 9 < 16: the KA-128 fallback wraps rows
+    (2, 9, 20, 64, 256, 3, 1, 1, 1),        # 256x256 tile, Wo = 20: 16-pixel stages wrap rows and images
 ]
 
 
