@@ -23,6 +23,7 @@ all-gathered each step (hkp.parallel); training all-reduces gradients over RCCL.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import contextlib
 import json
 import os
 import socket
@@ -58,6 +59,8 @@ def parse():
     ap.add_argument("--input", choices=["f32", "u8"], default="f32",
                     help="f32: the reference's ToTensor NCHW tensor; u8: the cv2.imread-style uint8 HWC batch "
                          "(ToTensor fused into the stem, SURVEY 8(f1))")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="inference at N>1: BN statistics over the global batch (hkp.parallel.sync_bn)")
     ap.add_argument("--no-extras", action="store_true", help="main line only (no train / fp32 legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
@@ -283,8 +286,10 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     if mode == "infer":
         gathered = torch.empty((world * B, K, 2), device=dev, dtype=torch.int32) if dist else None
 
+        sync = parallel.sync_bn() if dist and getattr(args, "sync_bn", False) else contextlib.nullcontext()
+
         def step():
-            with torch.no_grad():
+            with torch.no_grad(), sync:
                 hm, yx = model.heatmaps_and_keypoints(x)
                 if dist:                                   # every rank ends with all keypoints
                     parallel.gather_keypoints_fixed(yx, gathered)
@@ -418,6 +423,8 @@ def main():
             if args.mode == "infer" else "BCE fp64, Adam lr1e-4 wd1e-4"),
             "mode": args.mode, "backbone": args.backbone, "keypoints": args.keypoints, "height": args.height,
             "width": args.width, "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,
+            "bn": "sync (global-batch statistics)" if args.sync_bn and world > 1 and args.mode == "infer"
+            else "per-rank",
             "input": "fp32 NCHW (ToTensor)" if args.input == "f32" else "uint8 HWC BGR (ToTensor fused into the stem)"},
         "roofline": main_leg["roofline"],
         "model_tflops": main_leg["model_tflops"],

@@ -39,6 +39,14 @@ __device__ __forceinline__ void bn_fin_store(int c, int C, long count, double me
     if (nbt && c == 0) nbt[0] += 1;
 }
 
+// SyncBN: instead of the scale/shift, a rank's statistics for the
+// cross-rank merge (hkp_bn_finalize_ranks): [mean[C] | M2[C] | count], fp64
+__device__ __forceinline__ void bn_rank_stats_store(int c, int C, long count, double mean, double m2, double* stats) {
+    stats[c] = mean;
+    stats[C + c] = m2;
+    if (c == 0) stats[2 * C] = (double)count;
+}
+
 // CPB channels per block (partials_cpb); deterministic fixed-order fp64 merge
 // NT threads per block: 256, or 1024 for long tile lists (the stem's 19,200
 // tiles at C2: per-thread load chains of 75 tiles took 75 us with 256 threads)
@@ -46,7 +54,8 @@ template <int CPB, int NT = 256>
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
                                                          const float* __restrict__ part, const float* gamma,
                                                          const float* beta, float momentum, float eps, float* rmean,
-                                                         float* rvar, int64_t* nbt, float* ss, float* mi) {
+                                                         float* rvar, int64_t* nbt, float* ss, float* mi,
+                                                         double* stats) {
     constexpr int TL = NT / CPB, NW = NT / 64;
     __shared__ double red[NW][8];
     const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
@@ -86,8 +95,10 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long
             }
         }
     const double m2 = lanes_sum_d<CPB, NW>(q, red);
-    if (tl == 0 && ok)
-        bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+    if (tl == 0 && ok) {
+        if (stats) bn_rank_stats_store(c, C, count, mean, m2, stats);
+        else bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+    }
 }
 
 // Two-level form for long tile lists (hkp_bn_finalize_ws).  The one-kernel merge
@@ -154,7 +165,7 @@ __global__ __launch_bounds__(1024) void bn_fin_merge_kernel(int C, long count, l
                                                             const double2* __restrict__ ws, const float* gamma,
                                                             const float* beta, float momentum, float eps,
                                                             float* rmean, float* rvar, int64_t* nbt, float* ss,
-                                                            float* mi) {
+                                                            float* mi, double* stats) {
     __shared__ double red[FIN_TL][64];
     const int cl = threadIdx.x & 63, tl = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
     const bool ok = c < C;
@@ -172,7 +183,36 @@ __global__ __launch_bounds__(1024) void bn_fin_merge_kernel(int C, long count, l
             q += w.y + (double)nk * dm * dm;
         }
     const double m2 = fin_col_sum(q, red, tl, cl);
-    if (tl == 0 && ok) bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+    if (tl == 0 && ok) {
+        if (stats) bn_rank_stats_store(c, C, count, mean, m2, stats);
+        else bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+    }
+}
+
+// Cross-rank merge of SyncBN statistics: st = [R][2C+1] (each rank's
+// bn_rank_stats_store block, gathered in rank order).  Fixed order over ranks,
+// the same two-pass form as the chunk merge: mean = sum_r n_r*mean_r / N,
+// M2 = sum_r (M2_r + n_r*(mean_r - mean)^2).  Every rank merges the same bytes
+// in the same order, so every rank gets the same scale/shift and running stats.
+__global__ void bn_fin_ranks_kernel(int C, int R, const double* __restrict__ st, const float* gamma, const float* beta,
+                                    float momentum, float eps, float* rmean, float* rvar, int64_t* nbt, float* ss,
+                                    float* mi) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const long L = 2L * C + 1;
+    double n = 0.0, s = 0.0;
+    for (int r = 0; r < R; ++r) {
+        const double nr = st[r * L + 2 * C];
+        n += nr;
+        s += nr * st[r * L + c];
+    }
+    const double mean = R == 1 ? st[c] : s / n;
+    double m2 = 0.0;
+    for (int r = 0; r < R; ++r) {
+        const double nr = st[r * L + 2 * C], dm = st[r * L + c] - mean;
+        m2 += st[r * L + C + c] + nr * dm * dm;
+    }
+    bn_fin_store(c, C, (long)n, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
 }
 
 __global__ void bn_eval_kernel(int C, const float* gamma, const float* beta, const float* rm, const float* rv,
@@ -398,20 +438,22 @@ static inline int grid_for(long work, int block = 256, long cap = 256L * 16) {
 
 using namespace hkp;
 
-extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
-                               const float* gamma, const float* beta, float momentum, float eps, float* running_mean,
-                               float* running_var, int64_t* num_batches_tracked, float* scale_shift,
-                               float* mean_invstd, hkp_stream_t stream) {
-    HKP_CHECK_ARG(c > 0 && count > 0 && tiles > 0 && tile_rows > 0, "hkp_bn_finalize: bad sizes");
-    HKP_CHECK_ARG(partials && scale_shift, "hkp_bn_finalize: null tensor");
-    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "hkp_bn_finalize: running stats pair");
+// The one-kernel (fin_one) and two-level (fin_two) merges of the tile partials:
+// scale/shift (+ running stats), or (stats != null) the rank's SyncBN statistics.
+static int fin_one(const char* who, int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                   const float* gamma, const float* beta, float momentum, float eps, float* running_mean,
+                   float* running_var, int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd,
+                   double* stats, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && count > 0 && tiles > 0 && tile_rows > 0, "%s: bad sizes", who);
+    HKP_CHECK_ARG(partials && (scale_shift || stats), "%s: null tensor", who);
+    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "%s: running stats pair", who);
     HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
-                  "hkp_bn_finalize: tiles/tile_rows inconsistent with count");
+                  "%s: tiles/tile_rows inconsistent with count", who);
     const int cpb = partials_cpb(c);
 #define HKP_FIN1(CPB, NT)                                                                                          \
     hipLaunchKernelGGL((bn_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), c, \
                        (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,      \
-                       running_var, num_batches_tracked, scale_shift, mean_invstd)
+                       running_var, num_batches_tracked, scale_shift, mean_invstd, stats)
 #define HKP_FIN(CPB)                                  \
     if (tiles >= 4096 && !g_fin_small) { HKP_FIN1(CPB, 1024); } \
     else { HKP_FIN1(CPB, 256); }
@@ -421,7 +463,7 @@ extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t 
     else { HKP_FIN(1); }
 #undef HKP_FIN
 #undef HKP_FIN1
-    HKP_LAUNCH_CHECK("hkp_bn_finalize");
+    HKP_LAUNCH_CHECK(who);
     return HKP_OK;
 }
 
@@ -430,28 +472,71 @@ extern "C" int64_t hkp_bn_finalize_workspace_bytes(int32_t c, int64_t tiles) {
     return ((tiles + FIN_CHUNK - 1) / FIN_CHUNK) * (int64_t)c * (int64_t)sizeof(double2);
 }
 
-extern "C" int hkp_bn_finalize_ws(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
-                                  const float* gamma, const float* beta, float momentum, float eps,
-                                  float* running_mean, float* running_var, int64_t* num_batches_tracked,
-                                  float* scale_shift, float* mean_invstd, void* workspace, int64_t ws_bytes,
-                                  hkp_stream_t stream) {
-    HKP_CHECK_ARG(c > 0 && count > 0 && tiles > 0 && tile_rows > 0, "hkp_bn_finalize_ws: bad sizes");
-    HKP_CHECK_ARG(partials && scale_shift && workspace, "hkp_bn_finalize_ws: null tensor");
-    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "hkp_bn_finalize_ws: running stats pair");
+static int fin_two(const char* who, int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                   const float* gamma, const float* beta, float momentum, float eps, float* running_mean,
+                   float* running_var, int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd,
+                   double* stats, void* workspace, int64_t ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && count > 0 && tiles > 0 && tile_rows > 0, "%s: bad sizes", who);
+    HKP_CHECK_ARG(partials && (scale_shift || stats) && workspace, "%s: null tensor", who);
+    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "%s: running stats pair", who);
     HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
-                  "hkp_bn_finalize_ws: tiles/tile_rows inconsistent with count");
+                  "%s: tiles/tile_rows inconsistent with count", who);
     const int64_t need = hkp_bn_finalize_workspace_bytes(c, tiles);
-    HKP_CHECK_ARG(ws_bytes >= need, "hkp_bn_finalize_ws: workspace %ld < %ld", (long)ws_bytes, (long)need);
+    HKP_CHECK_ARG(ws_bytes >= need, "%s: workspace %ld < %ld", who, (long)ws_bytes, (long)need);
     const long chunks = (tiles + FIN_CHUNK - 1) / FIN_CHUNK;
     hipStream_t st = as_stream(stream);
     const unsigned cg = (unsigned)((c + 63) / 64);
     hipLaunchKernelGGL(bn_fin_chunk_kernel, dim3(cg, (unsigned)chunks), dim3(1024), 0, st, c, (long)count,
                        (long)tiles, tile_rows, partials, (double2*)workspace);
-    HKP_LAUNCH_CHECK("hkp_bn_finalize_ws (chunks)");
+    HKP_LAUNCH_CHECK(who);
     hipLaunchKernelGGL(bn_fin_merge_kernel, dim3(cg), dim3(1024), 0, st, c, (long)count, chunks, tile_rows,
                        (const double2*)workspace, gamma, beta, momentum, eps, running_mean, running_var,
-                       num_batches_tracked, scale_shift, mean_invstd);
-    HKP_LAUNCH_CHECK("hkp_bn_finalize_ws (merge)");
+                       num_batches_tracked, scale_shift, mean_invstd, stats);
+    HKP_LAUNCH_CHECK(who);
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_finalize(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                               const float* gamma, const float* beta, float momentum, float eps, float* running_mean,
+                               float* running_var, int64_t* num_batches_tracked, float* scale_shift,
+                               float* mean_invstd, hkp_stream_t stream) {
+    HKP_CHECK_ARG(scale_shift, "hkp_bn_finalize: null tensor");
+    return fin_one("hkp_bn_finalize", c, count, tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,
+                   running_var, num_batches_tracked, scale_shift, mean_invstd, nullptr, stream);
+}
+
+extern "C" int hkp_bn_finalize_ws(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                                  const float* gamma, const float* beta, float momentum, float eps,
+                                  float* running_mean, float* running_var, int64_t* num_batches_tracked,
+                                  float* scale_shift, float* mean_invstd, void* workspace, int64_t ws_bytes,
+                                  hkp_stream_t stream) {
+    HKP_CHECK_ARG(scale_shift, "hkp_bn_finalize_ws: null tensor");
+    return fin_two("hkp_bn_finalize_ws", c, count, tiles, tile_rows, partials, gamma, beta, momentum, eps,
+                   running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd, nullptr, workspace,
+                   ws_bytes, stream);
+}
+
+extern "C" int hkp_bn_stats(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                            double* stats, void* workspace, int64_t ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(stats, "hkp_bn_stats: null tensor");
+    if (workspace)
+        return fin_two("hkp_bn_stats", c, count, tiles, tile_rows, partials, nullptr, nullptr, 0.f, 0.f, nullptr,
+                       nullptr, nullptr, nullptr, nullptr, stats, workspace, ws_bytes, stream);
+    return fin_one("hkp_bn_stats", c, count, tiles, tile_rows, partials, nullptr, nullptr, 0.f, 0.f, nullptr, nullptr,
+                   nullptr, nullptr, nullptr, stats, stream);
+}
+
+extern "C" int hkp_bn_finalize_ranks(int32_t c, int32_t nranks, const double* stats, const float* gamma,
+                                     const float* beta, float momentum, float eps, float* running_mean,
+                                     float* running_var, int64_t* num_batches_tracked, float* scale_shift,
+                                     float* mean_invstd, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && nranks > 0, "hkp_bn_finalize_ranks: bad sizes");
+    HKP_CHECK_ARG(stats && scale_shift, "hkp_bn_finalize_ranks: null tensor");
+    HKP_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr), "hkp_bn_finalize_ranks: running stats pair");
+    hipLaunchKernelGGL(bn_fin_ranks_kernel, dim3((c + 255) / 256), dim3(256), 0, as_stream(stream), c, nranks, stats,
+                       gamma, beta, momentum, eps, running_mean, running_var, num_batches_tracked, scale_shift,
+                       mean_invstd);
+    HKP_LAUNCH_CHECK("hkp_bn_finalize_ranks");
     return HKP_OK;
 }
 

@@ -64,6 +64,8 @@ SIGNATURES = {
     "hkp_bn_finalize_workspace_bytes": (_I64, [_I32, _I64]),
     "hkp_bn_finalize_ws": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P, _I64,
                                           _P]),
+    "hkp_bn_stats": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _I64, _P]),
+    "hkp_bn_finalize_ranks": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_eval_params": (ctypes.c_int, [_I32, _P, _P, _P, _P, _F, _P, _P, _P]),
     "hkp_bn_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _I32, _P, _P, _I32, _P]),
     "hkp_bn_apply_f16": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),

@@ -15,7 +15,7 @@ import weakref
 
 import torch
 
-from . import ops
+from . import ops, parallel
 
 
 class Trace:
@@ -31,6 +31,12 @@ def _bn_params(bn, part, count, stats_only=False):
     """scale_shift (+ mean_invstd) for a BN layer: batch stats in training mode
     (and running-stat update, like nn.BatchNorm2d.forward), running stats otherwise."""
     if bn.training:
+        sync = parallel.sync_bn_group()
+        if sync is not None:                       # SyncBN: statistics over every rank's shard
+            st = parallel.gather_bn_stats(ops.bn_stats(part, count), sync[0])
+            return ops.bn_finalize_ranks(st, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                         bn.num_batches_tracked,
+                                         momentum=bn.momentum if bn.momentum is not None else 0.1, eps=bn.eps)
         return ops.bn_finalize(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var,
                                bn.num_batches_tracked, momentum=bn.momentum if bn.momentum is not None else 0.1,
                                eps=bn.eps)
@@ -376,6 +382,8 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
     """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
     if trace is not None and _precision == "f16":
         raise ops.HkpError("precision 'f16' (BASELINE config C4) is inference-only; train with 'f16x3' or 'fp32'")
+    if trace is not None and parallel.sync_bn_group() is not None:
+        raise ops.HkpError("SyncBN is inference-only (the BN backward uses per-rank sums); train with DDP BN")
     w, b = fc_rows(resnet, k)
     if trace is None and not _UNFUSED_HEAD and ops.head_fusable(_feat_channels(resnet), k):
         feat, low = None, backbone_forward(resnet, x_nchw, None, head=(w, b))

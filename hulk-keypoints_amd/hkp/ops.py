@@ -425,6 +425,45 @@ def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, n
     return ss, mi
 
 
+def bn_stats(part, count):
+    """SyncBN: this rank's per-channel BN statistics from its conv tile partials →
+    fp64 [2C+1] = [mean | M2 | count] (hkp_bn_stats; gathered in rank order and
+    merged by bn_finalize_ranks)."""
+    _need(part, torch.float32, "bn_stats.partials", 3)
+    tiles, c, _ = part.shape
+    st = torch.empty(2 * c + 1, device=part.device, dtype=torch.float64)
+    ws, nb = None, 0
+    if tiles >= FIN_TWO_LEVEL_TILES and not _FIN_ONE_KERNEL:
+        from ._lib import lib
+        nb = lib().hkp_bn_finalize_workspace_bytes(c, tiles)
+        ws = torch.empty((nb + 7) // 8, device=part.device, dtype=torch.float64)
+    call("hkp_bn_stats", c, count, tiles, CONV_TILE_ROWS, _ptr(part), _ptr(st), _ptr(ws), nb, _stream())
+    return st
+
+
+def bn_finalize_ranks(stats, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None,
+                      momentum=0.1, eps=1e-5):
+    """SyncBN: the ranks' bn_stats blocks [R, 2C+1] (rank order) merged in fixed
+    order → (scale_shift [2C], mean_invstd [2C]) of the global batch, as bn_finalize."""
+    _need(stats, torch.float64, "bn_finalize_ranks.stats", 2)
+    r, l = stats.shape
+    if l % 2 != 1:
+        raise HkpError("bn_finalize_ranks.stats: row length %d is not 2C+1" % l)
+    c = (l - 1) // 2
+    for t, nm in ((gamma, "gamma"), (beta, "beta"), (running_mean, "running_mean"), (running_var, "running_var")):
+        if t is not None:
+            _need(t, torch.float32, "bn_finalize_ranks." + nm, 1)
+            if t.numel() != c:
+                raise HkpError("bn_finalize_ranks.%s: %d != C=%d" % (nm, t.numel(), c))
+    if num_batches_tracked is not None:
+        _need(num_batches_tracked, torch.int64, "bn_finalize_ranks.num_batches_tracked")
+    ss = torch.empty(2 * c, device=stats.device, dtype=torch.float32)
+    mi = torch.empty(2 * c, device=stats.device, dtype=torch.float32)
+    call("hkp_bn_finalize_ranks", c, r, _ptr(stats.contiguous()), _ptr(gamma), _ptr(beta), momentum, eps,
+         _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi), _stream())
+    return ss, mi
+
+
 def bn_eval_params(gamma, beta, running_mean, running_var, eps=1e-5):
     c = running_mean.numel()
     ss = torch.empty(2 * c, device=running_mean.device, dtype=torch.float32)

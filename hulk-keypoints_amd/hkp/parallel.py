@@ -74,3 +74,63 @@ def predict_keypoints_dp(model, x_shard, heat=False):
     else:
         hm, yx = None, model.predict_keypoints(x_shard)
     return gather_keypoints(yx), hm
+
+
+# ---- SyncBN (caveat D5) ----------------------------------------
+# Off by default: per-rank BN statistics (standard DDP semantics, as above).  On:
+# every train-mode BN layer's batch statistics are taken over the whole sharded
+# batch — each rank's [mean | M2 | count] block (hkp_bn_stats, fp64) is
+# all-gathered in rank order and merged in fixed order (hkp_bn_finalize_ranks),
+# so every rank applies the same scale/shift and a DP inference over N ranks
+# gives the outputs of one forward over the global batch (torch SyncBatchNorm's
+# forward).  One all_gather of 2C+1 doubles per BN layer (36 for R34).
+# Inference only: the BN backward uses per-rank sums (training keeps DDP BN).
+_sync_bn = None          # None: off; else (group,)
+
+
+def set_sync_bn(enabled=True, group=None):
+    """Turn cross-rank BN statistics on (over `group`, default the world) or off."""
+    global _sync_bn
+    _sync_bn = (group,) if enabled else None
+
+
+def sync_bn_group():
+    """(group,) while SyncBN is on and more than one rank takes part, else None."""
+    if _sync_bn is None or not dist.is_initialized() or dist.get_world_size(_sync_bn[0]) == 1:
+        return None
+    return _sync_bn
+
+
+class sync_bn:
+    """Context manager: SyncBN on inside the block, the previous setting after it."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def __enter__(self):
+        global _sync_bn
+        self.prev = _sync_bn
+        _sync_bn = (self.group,)
+        return self
+
+    def __exit__(self, *exc):
+        global _sync_bn
+        _sync_bn = self.prev
+        return False
+
+
+def gather_bn_stats(st, group=None):
+    """all_gather of each rank's fp64 [2C+1] statistics block → [world, 2C+1] in
+    rank order.  RCCL gathers on the device; other backends (gloo) through host
+    copies (the blocks are a few KB)."""
+    n = dist.get_world_size(group) if dist.is_initialized() else 1
+    if n == 1:
+        return st.reshape(1, -1)
+    if st.is_cuda and dist.get_backend(group) == "nccl":
+        out = torch.empty((n, st.numel()), device=st.device, dtype=st.dtype)
+        dist.all_gather_into_tensor(out, st.contiguous(), group=group)
+        return out
+    host = st.detach().cpu().contiguous()
+    parts = [torch.empty_like(host) for _ in range(n)]
+    dist.all_gather(parts, host, group=group)
+    return torch.stack(parts).to(st.device)

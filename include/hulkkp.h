@@ -188,6 +188,26 @@ int hkp_bn_finalize_ws(int32_t c, int64_t count, int64_t tiles, int32_t tile_row
                        float* scale_shift, float* mean_invstd, void* workspace, int64_t ws_bytes,
                        hkp_stream_t stream);
 
+/* SyncBN for data-parallel ranks (caveat D5: train-mode BN makes a
+ * shard's outputs depend on the shard; torch.nn.SyncBatchNorm's forward
+ * statistics).  hkp_bn_stats: this rank's per-channel statistics from its conv
+ * tile partials, written as stats = [mean[c] | M2[c] | count] (2c+1 fp64) —
+ * the merge of hkp_bn_finalize (workspace == NULL) or hkp_bn_finalize_ws
+ * (workspace of hkp_bn_finalize_workspace_bytes) without the scale/shift.  The
+ * caller all-gathers the blocks in rank order into stats[nranks][2c+1], and
+ * hkp_bn_finalize_ranks merges them in fixed rank order (Chan:
+ * mean = sum n_r mean_r / N, M2 = sum M2_r + n_r (mean_r - mean)^2) into the same
+ * outputs as hkp_bn_finalize over the global batch (running stats with the global
+ * count's unbiased variance, num_batches_tracked += 1).  Identical bytes on every
+ * rank.  Replaces the batch statistics of nn.BatchNorm2d.forward
+ * (src/resnet.py:46,49,78,85,87,139,187) for a batch sharded over ranks. */
+int hkp_bn_stats(int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
+                 double* stats, void* workspace, int64_t ws_bytes, hkp_stream_t stream);
+int hkp_bn_finalize_ranks(int32_t c, int32_t nranks, const double* stats, const float* gamma, const float* beta,
+                          float momentum, float eps, float* running_mean, float* running_var,
+                          int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd,
+                          hkp_stream_t stream);
+
 /* Eval-mode BN parameters from running statistics (the reference never uses
  * them; offered as an option). */
 int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const float* running_mean,

@@ -1,0 +1,174 @@
+"""SyncBN for data-parallel inference (caveat D5).
+
+Train-mode BN (the reference never calls .eval()) makes a shard's outputs depend
+on the shard: N ranks with per-rank statistics do not reproduce the reference's
+forward over the global batch.  With hkp.parallel.sync_bn each rank's BN
+statistics block (hkp_bn_stats) is all-gathered and merged in fixed rank order
+(hkp_bn_finalize_ranks), and the sharded run matches the reference at the
+global batch:
+
+* kernel level: the rank merge of tile-aligned row shards == hkp_bn_finalize
+  over all tiles (one-kernel and two-level forms; R = 1 bit-identical);
+* end to end: 2 ranks (gloo, both on cuda:0) x 16 images of the C2 workload
+  (R34-8s, K=4, 640x480) against the reference fixture for the whole batch of
+  32 (tests/golden/make_golden.py fwd_r34_k4_480x640_b32): low-res logits,
+  heatmap of image 0, argmax bit-exact, BN running statistics; and per-rank BN
+  visibly misses that fixture.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "hulk-keypoints_amd")
+
+
+def _partials(y, rows=128):
+    """[tiles, C, 2] fp32 (sum, M2 about the tile mean) of 128-row tiles of y [M, C]
+    — what the conv epilogues write."""
+    m, c = y.shape
+    full = m // rows
+    parts = []
+    if full:
+        blk = y[:full * rows].double().reshape(full, rows, c)
+        parts.append(torch.stack([blk.sum(1), ((blk - blk.mean(1, keepdim=True)) ** 2).sum(1)], -1))
+    if m % rows:
+        blk = y[full * rows:].double()
+        parts.append(torch.stack([blk.sum(0), ((blk - blk.mean(0)) ** 2).sum(0)], -1)[None])
+    return torch.cat(parts).float().contiguous()
+
+
+def _bn_state(c, dev):
+    g = torch.Generator().manual_seed(c)
+    gamma = (1 + 0.1 * torch.randn(c, generator=g)).to(dev)
+    beta = (0.1 * torch.randn(c, generator=g)).to(dev)
+    rm = (0.05 * torch.randn(c, generator=g)).to(dev)
+    rv = (1 + 0.1 * torch.rand(c, generator=g)).to(dev)
+    return gamma, beta, rm, rv, torch.zeros(1, dtype=torch.int64, device=dev)
+
+
+@pytest.mark.parametrize("m,c,cuts", [(2000, 96, [1024]), (1000, 64, []), (300_000, 64, [102_400, 204_800])])
+def test_bn_finalize_ranks_matches_global(cuda_device, m, c, cuts):
+    from hkp import ops
+    torch.manual_seed(m)
+    y = (torch.randn(m, c, device=cuda_device) * 3 + torch.linspace(-2, 2, c, device=cuda_device)).float()
+    part = _partials(y)
+    gamma, beta, rm, rv, nbt = _bn_state(c, cuda_device)
+    ref_state = [t.clone() for t in (rm, rv, nbt)]
+    ss_ref, mi_ref = ops.bn_finalize(part, m, gamma, beta, *ref_state)
+    bounds = [0] + cuts + [m]
+    blocks = []
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        assert lo % 128 == 0
+        blocks.append(ops.bn_stats(part[lo // 128:(hi + 127) // 128].contiguous(), hi - lo))
+    st = torch.stack(blocks)
+    assert st[:, -1].tolist() == [float(hi - lo) for lo, hi in zip(bounds[:-1], bounds[1:])]
+    state = [t.clone() for t in (rm, rv, nbt)]
+    ss, mi = ops.bn_finalize_ranks(st, gamma, beta, *state)
+    torch.cuda.synchronize()
+    if len(blocks) == 1:                       # one rank: the same bits as bn_finalize
+        assert torch.equal(ss, ss_ref) and torch.equal(mi, mi_ref)
+        assert all(torch.equal(a, b) for a, b in zip(state, ref_state))
+    # fp64 merges in another order, rounded to fp32: at most an ulp or two apart
+    torch.testing.assert_close(ss, ss_ref, rtol=3e-7, atol=1e-7)
+    torch.testing.assert_close(mi, mi_ref, rtol=3e-7, atol=1e-7)
+    torch.testing.assert_close(state[0], ref_state[0], rtol=3e-7, atol=1e-8)
+    torch.testing.assert_close(state[1], ref_state[1], rtol=3e-7, atol=1e-8)
+    assert int(state[2]) == int(ref_state[2]) == 1
+    # and both against fp64 torch over the whole tensor
+    yd = y.double()
+    mean, var = yd.mean(0), yd.var(0, unbiased=False)
+    torch.testing.assert_close(mi[:c].double(), mean, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(mi[c:].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-6, atol=1e-6)
+
+
+def test_bn_finalize_ranks_bad_args(cuda_device):
+    from hkp import ops
+    with pytest.raises(ops.HkpError):
+        ops.bn_finalize_ranks(torch.zeros(2, 10, dtype=torch.float64, device=cuda_device), None, None)
+    with pytest.raises(ops.HkpError):
+        ops.bn_finalize_ranks(torch.zeros(2, 9, dtype=torch.float32, device=cuda_device), None, None)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from hkp import net, parallel
+        from oracle import recipe
+        from src.model import KeypointsGauss
+        dev = torch.device("cuda:0")
+        g = np.load(os.path.join(REPO, "tests", "golden", "fwd_r34_k4_480x640_b32.npz"), allow_pickle=False)
+        B, H, W, K = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["k"])
+        lo, hi = parallel.shard_range(B, rank, world)
+        imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))[lo:hi]
+        x = torch.from_numpy(imgs).to(dev)
+
+        def model():
+            m = KeypointsGauss(K, backbone="resnet34", pretrained=False)
+            m.load_state_dict(recipe.seeded_state_dict("resnet34", int(g["wseed"])))
+            return m.to(dev)
+        m = model()
+        with torch.no_grad(), parallel.sync_bn():
+            hm, yx, low = net.keypoints_forward(m.resnet.net, x, K, heat=True, argmax=True)
+        yx_all = parallel.gather_keypoints(yx.to(torch.int32).cpu())        # gloo: host tensors
+        res = dict(rank=rank,
+                   low_err=float(np.abs(low.cpu().numpy() - g["lowres"][lo:hi]).max()),
+                   rowsum_err=float(np.abs(hm.double().sum(3).cpu().numpy() / g["heat_row_sum"][lo:hi] - 1).max()),
+                   argmax_ok=bool(np.array_equal(yx_all.cpu().numpy(), g["argmax_yx"])))
+        if lo == 0:
+            res["heat0_err"] = float(np.abs(hm[0].cpu().numpy() - g["heat0"]).max())
+        sd = m.state_dict()
+        res["rv_err"] = float(np.abs(sd["resnet.resnet34_8s.bn1.running_var"].cpu().numpy() / g["bn1_running_var"]
+                                     - 1).max())
+        rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
+        res["rm_err"] = abs(rm - float(g["running_checksum"][0])) / max(1.0, abs(rm))
+        m2 = model()                          # per-rank BN (the default): the shard's own statistics
+        with torch.no_grad():
+            _, _, low2 = net.keypoints_forward(m2.resnet.net, x, K, heat=True, argmax=True)
+        res["low_err_per_rank_bn"] = float(np.abs(low2.cpu().numpy() - g["lowres"][lo:hi]).max())
+        torch.cuda.synchronize()
+        q.put(res)
+        dist.destroy_process_group()
+    except Exception as e:            # report instead of hanging the parent on q.get
+        q.put(dict(rank=rank, error=repr(e)))
+        raise
+
+
+def test_syncbn_dp_inference_matches_reference_global_batch(cuda_device):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    print(res)
+    assert all("error" not in r for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
+    for r in res:
+        assert r["low_err"] < 1e-4, r
+        assert r["rowsum_err"] < 1e-4, r
+        assert r["argmax_ok"], r                       # all 128 keypoints, bit-exact
+        assert r["rv_err"] < 1e-4 and r["rm_err"] < 1e-4, r
+        assert r["low_err_per_rank_bn"] > 1e-3, r      # without SyncBN the shard misses the batch-32 fixture
+    assert [r for r in res if "heat0_err" in r][0]["heat0_err"] < 1e-3

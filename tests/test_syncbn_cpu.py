@@ -1,0 +1,102 @@
+"""SyncBN host logic on CPU (the kernels are checked by tests/test_gpu_syncbn.py).
+
+* the fixed-order rank merge hkp_bn_finalize_ranks implements
+  (mean = sum n_r mean_r / N, M2 = sum M2_r + n_r (mean_r - mean)^2), restated in
+  numpy, equals the statistics of the whole batch (ragged shards included);
+* hkp.parallel.gather_bn_stats over a gloo world of 2 returns the blocks in rank
+  order on every rank; sync_bn() / sync_bn_group() switch it on and off.
+"""
+import os
+import socket
+
+import numpy as np
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "hulk-keypoints_amd")
+
+
+def _rank_block(y):
+    """[mean | M2 | count] of rows y [n, C] (hkp_bn_stats' layout), fp64."""
+    mean = y.mean(0)
+    return np.concatenate([mean, ((y - mean) ** 2).sum(0), [float(len(y))]])
+
+
+def _merge(blocks):
+    """numpy restatement of bn_fin_ranks_kernel (csrc/bn.hip)."""
+    st = np.stack(blocks)
+    c = (st.shape[1] - 1) // 2
+    n = st[:, 2 * c]
+    if len(st) == 1:
+        mean = st[0, :c]
+    else:
+        mean = (n[:, None] * st[:, :c]).sum(0) / n.sum()
+    m2 = (st[:, c:2 * c] + n[:, None] * (st[:, :c] - mean) ** 2).sum(0)
+    return n.sum(), mean, m2
+
+
+def test_rank_merge_formula_matches_whole_batch():
+    rng = np.random.default_rng(5)
+    y = rng.normal(3.0, 2.0, size=(1000, 17)) + np.linspace(-50, 50, 17)
+    for cuts in ([], [512], [1, 999], [100, 350, 351, 800]):
+        b = [0] + cuts + [len(y)]
+        n, mean, m2 = _merge([_rank_block(y[lo:hi]) for lo, hi in zip(b[:-1], b[1:])])
+        assert n == len(y)
+        np.testing.assert_allclose(mean, y.mean(0), rtol=1e-13, atol=1e-12)
+        np.testing.assert_allclose(m2 / n, y.var(0), rtol=1e-12)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gather_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hkp import parallel
+    ok = parallel.sync_bn_group() is None                      # off by default
+    with parallel.sync_bn():
+        ok &= parallel.sync_bn_group() is not None
+        st = torch.arange(7, dtype=torch.float64) + 100.0 * rank
+        g = parallel.gather_bn_stats(st, parallel.sync_bn_group()[0])
+        ok &= tuple(g.shape) == (world, 7) and g.dtype == torch.float64
+        ok &= all(torch.equal(g[r], torch.arange(7, dtype=torch.float64) + 100.0 * r) for r in range(world))
+    ok &= parallel.sync_bn_group() is None                     # restored
+    parallel.set_sync_bn(True)
+    ok &= parallel.sync_bn_group() is not None
+    parallel.set_sync_bn(False)
+    ok &= parallel.sync_bn_group() is None
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_gather_bn_stats_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok in res), res
+
+
+def test_sync_bn_single_process_is_off():
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    from hkp import parallel
+    with parallel.sync_bn():
+        assert parallel.sync_bn_group() is None                # one rank: nothing to sync
+        st = torch.ones(5, dtype=torch.float64)
+        assert torch.equal(parallel.gather_bn_stats(st), st[None])
