@@ -130,13 +130,14 @@ template <int CPB, int NT = 256>
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
                                                              const float* __restrict__ mi, const float* gamma,
                                                              float* dgamma, float* dbeta, float* coef,
-                                                             const float* __restrict__ pmax, unsigned* amax) {
+                                                             const float* __restrict__ pmax, unsigned* amax,
+                                                             double* stats) {
     constexpr int TL = NT / CPB, NW = NT / 64;
     __shared__ double red[NW][8];
     __shared__ float bmax[8];
     const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
     const bool ok = c < C;
-    if (!pmax && amax && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;   // apply's atomicMax starts from 0
+    if (!pmax && amax && !stats && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;   // apply's atomicMax starts from 0
     double s = 0.0, d = 0.0;
     if (ok)   // 8 loads in flight per batch (latency-bound loop); zero-filled past the end
         for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
@@ -165,6 +166,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long
         md = lanes_max_d<CPB, NW>(md, red);
         mv = lanes_max_d<CPB, NW>(mv, red);
     }
+    if (stats) {                 // SyncBN: this rank's sums for the cross-rank merge (bn_bwd_fin_ranks_kernel)
+        if (tl == 0 && ok) {
+            stats[c] = S;
+            stats[C + c] = D;
+            stats[2 * C + c] = md;
+            stats[3 * C + c] = mv;
+            if (c == 0) stats[4 * C] = (double)M;
+        }
+        return;
+    }
     if (tl == 0 && ok) {
         const double inv = (double)mi[C + c];
         const float gm = gamma ? gamma[c] : 1.f;
@@ -184,6 +195,54 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long
             for (int i = 0; i < CPB && blockIdx.x * CPB + i < C; ++i) b = fmaxf(b, bmax[i]);
             atomicMax(amax, __float_as_uint(b));   // the word was zeroed by the reduce kernel
         }
+    }
+}
+
+// SyncBN backward: the ranks' [S | D | max|dz| | max|y-mean| | M] blocks (st,
+// [R][4C+1], rank order) summed in fixed rank order — the apply coefficients
+// from the global sums and count (torch SyncBatchNorm's all-reduced sum_dy /
+// sum_dy_xmu), dgamma / dbeta from this rank's own block (DDP then averages them
+// with the other parameters' gradients), the split-scale bound from this rank's
+// maxima with the global coefficients.  One rank: bn_bwd_finalize_kernel's bits.
+__global__ __launch_bounds__(256) void bn_bwd_fin_ranks_kernel(int C, int R, const double* __restrict__ st,
+                                                               const double* __restrict__ own, int has_max,
+                                                               const float* __restrict__ mi, const float* gamma,
+                                                               float* dgamma, float* dbeta, float* coef,
+                                                               unsigned* amax) {
+    __shared__ float bmax[256];
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    float b = 0.f;
+    if (c < C) {
+        const long L = 4L * C + 1;
+        double S = 0.0, D = 0.0, M = 0.0;
+        for (int r = 0; r < R; ++r) {
+            S += st[r * L + c];
+            D += st[r * L + C + c];
+            M += st[r * L + 4 * C];
+        }
+        const double inv = (double)mi[C + c];
+        const float gm = gamma ? gamma[c] : 1.f;
+        if (dgamma) dgamma[c] = (float)(own[C + c] * inv);
+        if (dbeta) dbeta[c] = (float)own[c];
+        const float cg = (float)(S / M), ck = (float)(D * inv * inv / M), cs = (float)(inv * (double)gm);
+        coef[c] = cg;
+        coef[C + c] = ck;
+        coef[2 * C + c] = cs;
+        if (has_max)
+            b = (float)((own[2 * C + c] + fabs((double)cg) + own[3 * C + c] * fabs((double)ck)) * fabs((double)cs) *
+                        1.0001);
+    }
+    if (!amax) return;
+    if (!has_max) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;   // the apply's atomicMax starts from 0
+        return;
+    }
+    bmax[threadIdx.x] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float m = 0.f;
+        for (int i = 0; i < 256; ++i) m = fmaxf(m, bmax[i]);
+        atomicMax(amax, __float_as_uint(m));                  // zeroed by the reduce kernel
     }
 }
 
@@ -339,16 +398,15 @@ extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const flo
     return HKP_OK;
 }
 
-extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* maxima,
-                                   const float* mean_invstd, const float* gamma, float* dgamma, float* dbeta,
-                                   float* coef, uint32_t* dy_amax_bits, hkp_stream_t stream) {
-    HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
+static int bwd_fin(int32_t c, int64_t m, const float* partials, const float* maxima, const float* mean_invstd,
+                   const float* gamma, float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_bits,
+                   double* stats, hkp_stream_t stream) {
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     const int cpb = partials_cpb(c);
 #define HKP_BFIN1(CPB, NT)                                                                                         \
     hipLaunchKernelGGL((bn_bwd_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), \
                        c, (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, maxima,                  \
-                       (unsigned*)dy_amax_bits)
+                       (unsigned*)dy_amax_bits, stats)
 #define HKP_BFIN(CPB)                                  \
     if (tiles >= 4096 && !g_fin_small) { HKP_BFIN1(CPB, 1024); } \
     else { HKP_BFIN1(CPB, 256); }
@@ -359,6 +417,31 @@ extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, 
 #undef HKP_BFIN
 #undef HKP_BFIN1
     HKP_LAUNCH_CHECK("hkp_bn_bwd_finalize");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* maxima,
+                                   const float* mean_invstd, const float* gamma, float* dgamma, float* dbeta,
+                                   float* coef, uint32_t* dy_amax_bits, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && coef, "hkp_bn_bwd_finalize: bad args");
+    return bwd_fin(c, m, partials, maxima, mean_invstd, gamma, dgamma, dbeta, coef, dy_amax_bits, nullptr, stream);
+}
+
+extern "C" int hkp_bn_bwd_stats(int32_t c, int64_t m, const float* partials, const float* maxima,
+                                const float* mean_invstd, double* stats, hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && m > 0 && partials && mean_invstd && stats, "hkp_bn_bwd_stats: bad args");
+    return bwd_fin(c, m, partials, maxima, mean_invstd, nullptr, nullptr, nullptr, nullptr, nullptr, stats, stream);
+}
+
+extern "C" int hkp_bn_bwd_finalize_ranks(int32_t c, int32_t nranks, const double* stats, const double* own,
+                                         int32_t has_maxima, const float* mean_invstd, const float* gamma,
+                                         float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_bits,
+                                         hkp_stream_t stream) {
+    HKP_CHECK_ARG(c > 0 && nranks > 0 && stats && own && mean_invstd && coef, "hkp_bn_bwd_finalize_ranks: bad args");
+    hipLaunchKernelGGL(bn_bwd_fin_ranks_kernel, dim3((c + 255) / 256), dim3(256), 0, as_stream(stream), c, nranks,
+                       stats, own, has_maxima ? 1 : 0, mean_invstd, gamma, dgamma, dbeta, coef,
+                       (unsigned*)dy_amax_bits);
+    HKP_LAUNCH_CHECK("hkp_bn_bwd_finalize_ranks");
     return HKP_OK;
 }
 

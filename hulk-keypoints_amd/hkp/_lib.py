@@ -116,6 +116,8 @@ SIGNATURES = {
     "hkp_bn_bwd_tiles": (_I64, [_I64]),
     "hkp_bn_bwd_reduce": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_bwd_finalize": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_stats": (ctypes.c_int, [_I32, _I64, _P, _P, _P, _P, _P]),
+    "hkp_bn_bwd_finalize_ranks": (ctypes.c_int, [_I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_bwd_apply": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_maxpool_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P]),
     "hkp_heat_loss_workspace": (_I64, []),

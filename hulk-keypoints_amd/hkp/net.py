@@ -382,8 +382,6 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
     """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
     if trace is not None and _precision == "f16":
         raise ops.HkpError("precision 'f16' (BASELINE config C4) is inference-only; train with 'f16x3' or 'fp32'")
-    if trace is not None and parallel.sync_bn_group() is not None:
-        raise ops.HkpError("SyncBN is inference-only (the BN backward uses per-rank sums); train with DDP BN")
     w, b = fc_rows(resnet, k)
     if trace is None and not _UNFUSED_HEAD and ops.head_fusable(_feat_channels(resnet), k):
         feat, low = None, backbone_forward(resnet, x_nchw, None, head=(w, b))

@@ -1005,8 +1005,17 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, s
     dgamma = torch.empty(c, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(c, device=y.device, dtype=torch.float32)
     coef = torch.empty(3 * c, device=y.device, dtype=torch.float32)
-    call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(maxima), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma),
-         _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
+    from . import parallel
+    sync = parallel.sync_bn_group()
+    if sync is None:
+        call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(maxima), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma),
+             _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
+    else:                                          # SyncBN: sums over every rank's shard
+        own = torch.empty(4 * c + 1, device=y.device, dtype=torch.float64)
+        call("hkp_bn_bwd_stats", c, m, _ptr(part), _ptr(maxima), _ptr(mean_invstd), _ptr(own), _stream())
+        st = parallel.gather_bn_stats(own, sync[0])
+        call("hkp_bn_bwd_finalize_ranks", c, st.shape[0], _ptr(st), _ptr(own), 1 if maxima is not None else 0,
+             _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
     if split_only:
         dy = _split_out(y.shape, y.device, 3)
         call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd),

@@ -12,15 +12,18 @@ Data parallelism: one process per GPU (torchrun), torch.distributed backend
 order backward produces them (fc, layer4, …, stem); as soon as a bucket is
 complete its all-reduce is launched asynchronously, so communication of the
 late layers overlaps the backward of the early ones.  BatchNorm statistics
-stay per rank (standard DDP semantics); parameters and buffers are broadcast
-from rank 0 when the Trainer is built (broadcast_state).
+stay per rank (standard DDP semantics) unless Trainer(sync_bn=True): then the
+BN statistics and the BN backward sums are taken over every rank's shard
+(hkp.parallel.sync_bn), and a step equals one step over the global batch.
+Parameters and buffers are broadcast from rank 0 when the Trainer is built
+(broadcast_state).
 """
 import os
 
 import torch
 import torch.distributed as dist
 
-from . import net, ops
+from . import net, ops, parallel
 from .optim import FusedAdam
 
 
@@ -125,8 +128,12 @@ class Trainer:
     """One optimizer step per call, reference semantics (train.py:33-36)."""
 
     def __init__(self, model, lr=1e-4, weight_decay=1e-4, loss="bce", sigma=8.0, distributed=False,
-                 bucket_mb=32, optimizer="fused"):
+                 bucket_mb=32, optimizer="fused", sync_bn=False):
+        """sync_bn: BN statistics and their backward sums over every rank's shard
+        (hkp.parallel.sync_bn; the step then equals one step over the global
+        batch), instead of per-rank BN (DDP semantics, the default)."""
         self.model = model
+        self.sync_bn = sync_bn
         self.params = list(model.parameters())
         self.loss_kind = loss
         self.sigma = sigma
@@ -143,6 +150,12 @@ class Trainer:
         self.bucketer = GradBucketer(self.params, bucket_mb << 20) if use_dp else None
 
     def forward_backward(self, x, uv=None, target=None):
+        if self.sync_bn:
+            with parallel.sync_bn():
+                return self._forward_backward(x, uv, target)
+        return self._forward_backward(x, uv, target)
+
+    def _forward_backward(self, x, uv=None, target=None):
         m = self.model
         trace = net.Trace()
         hm, _, _ = net.keypoints_forward(m.resnet.net, x, m.num_keypoints, heat=True, trace=trace)

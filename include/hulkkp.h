@@ -453,6 +453,21 @@ int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const float* out_mas
 int hkp_bn_bwd_finalize(int32_t c, int64_t m, const float* partials, const float* maxima, const float* mean_invstd,
                         const float* gamma, float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_bits,
                         hkp_stream_t stream);
+/* SyncBN backward (torch SyncBatchNorm: sum_dy and sum_dy_xmu over all ranks).
+ * hkp_bn_bwd_stats: in place of hkp_bn_bwd_finalize's outputs, this rank's
+ * per-channel [S = sum dz | D = sum dz*(y-mean) | max|dz| | max|y-mean| | m]
+ * (4c+1 fp64; the maxima are 0 when maxima == NULL).  The caller all-gathers the
+ * blocks in rank order into stats[nranks][4c+1]; hkp_bn_bwd_finalize_ranks sums
+ * them in fixed rank order and writes hkp_bn_bwd_finalize's outputs: coef from
+ * the global sums and count, dgamma/dbeta from this rank's block `own`, the
+ * dy-split scale bound (has_maxima) from own maxima.  One rank: the same bits as
+ * hkp_bn_bwd_finalize.  Replaces the backward of nn.BatchNorm2d in train mode
+ * (src/resnet.py:46,49,78,85,87,139,187) for a batch sharded over ranks. */
+int hkp_bn_bwd_stats(int32_t c, int64_t m, const float* partials, const float* maxima, const float* mean_invstd,
+                     double* stats, hkp_stream_t stream);
+int hkp_bn_bwd_finalize_ranks(int32_t c, int32_t nranks, const double* stats, const double* own, int32_t has_maxima,
+                              const float* mean_invstd, const float* gamma, float* dgamma, float* dbeta, float* coef,
+                              uint32_t* dy_amax_bits, hkp_stream_t stream);
 int hkp_bn_bwd_apply(int64_t m, int32_t c, const float* g, const float* out_mask, const float* relu_ss,
                      const float* y, const float* mean_invstd, const float* coef, float* dy, uint32_t* dy_amax_bits,
                      uint16_t* dy_split, hkp_stream_t stream);

@@ -172,3 +172,87 @@ def test_syncbn_dp_inference_matches_reference_global_batch(cuda_device):
         assert r["rv_err"] < 1e-4 and r["rm_err"] < 1e-4, r
         assert r["low_err_per_rank_bn"] > 1e-3, r      # without SyncBN the shard misses the batch-32 fixture
     assert [r for r in res if "heat0_err" in r][0]["heat0_err"] < 1e-3
+
+
+# ---------------------------------------------------------------- training
+
+
+def _train_worker(rank, world, port, out_dir, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from hkp import parallel, train
+        from oracle import recipe
+        from src.model import KeypointsGauss
+        dev = torch.device("cuda:0")
+        B, H, W, K = 4, 96, 128, 2
+        lo, hi = parallel.shard_range(B, rank, world)
+        imgs = recipe.seeded_images_u8(B, H, W, 21)
+        uv_all = recipe.seeded_keypoints(B, K, H, W, 22)
+
+        def grads_of(x, uv, sync):
+            m = KeypointsGauss(K, backbone="resnet18", pretrained=False)
+            m.load_state_dict(recipe.seeded_state_dict("resnet18", 23))
+            m = m.to(dev)
+            t = train.Trainer(m, distributed=False, sync_bn=sync)
+            loss = t.forward_backward(x, uv=uv)
+            torch.cuda.synchronize()
+            g = {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
+            rm = {n: b.detach().cpu() for n, b in m.named_buffers() if n.endswith("running_mean")}
+            return float(loss), g, rm
+        x = torch.from_numpy(imgs[lo:hi]).to(dev)
+        uv = torch.from_numpy(uv_all[lo:hi]).to(dev)
+        res = {}
+        res["sync"] = grads_of(x, uv, True)
+        res["local"] = grads_of(x, uv, False)
+        if rank == 0:
+            res["global"] = grads_of(torch.from_numpy(imgs).to(dev), torch.from_numpy(uv_all).to(dev), False)
+        torch.save(res, os.path.join(out_dir, "rank%d.pt" % rank))
+        q.put(dict(rank=rank))
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put(dict(rank=rank, error=repr(e)))
+        raise
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
+
+
+def test_syncbn_training_step_equals_global_batch(cuda_device, tmp_path):
+    """2 ranks x 2 images with SyncBN: the mean of the ranks' gradients (what the
+    DP all-reduce computes) and of their losses == one step over all 4 images;
+    BN running statistics too.  Per-rank BN misses it by orders of magnitude."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_train_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    assert all("error" not in r for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
+    r0 = torch.load(os.path.join(tmp_path, "rank0.pt"), weights_only=True)
+    r1 = torch.load(os.path.join(tmp_path, "rank1.pt"), weights_only=True)
+    lg, gg, rmg = r0["global"]
+    for kind in ("sync", "local"):
+        l0, g0, rm0 = r0[kind]
+        l1, g1, rm1 = r1[kind]
+        loss_err = abs((l0 + l1) / 2 - lg) / abs(lg)
+        grad_err = max(_rel((g0[n] + g1[n]) / 2, gg[n]) for n in gg)
+        rm_err = max(_rel(rm0[n], rmg[n]) for n in rmg)
+        print("%s: loss rel err %.3g, worst grad rel err %.3g, running-mean rel err %.3g"
+              % (kind, loss_err, grad_err, rm_err))
+        if kind == "sync":
+            assert loss_err < 1e-6
+            assert grad_err < 1e-4
+            assert rm_err < 1e-5
+            assert all(torch.equal(rm0[n], rm1[n]) for n in rm0)      # every rank holds the same statistics
+            sync_grad_err = grad_err
+        else:
+            assert grad_err > 100 * sync_grad_err                      # per-rank BN: another computation
