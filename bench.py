@@ -60,7 +60,7 @@ def parse():
                     help="f32: the reference's ToTensor NCHW tensor; u8: the cv2.imread-style uint8 HWC batch "
                          "(ToTensor fused into the stem, SURVEY 8(f1))")
     ap.add_argument("--sync-bn", action="store_true",
-                    help="inference at N>1: BN statistics over the global batch (hkp.parallel.sync_bn)")
+                    help="N>1: BN statistics (and, training, their backward sums) over the global batch")
     ap.add_argument("--no-extras", action="store_true", help="main line only (no train / fp32 legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
@@ -296,7 +296,8 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
                 return hm
     else:
         from hkp import train as hkp_train
-        trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4, distributed=dist)
+        trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4, distributed=dist,
+                                    sync_bn=dist and getattr(args, "sync_bn", False))
 
         def step():
             return trainer.step(x, uv)
@@ -423,8 +424,7 @@ def main():
             if args.mode == "infer" else "BCE fp64, Adam lr1e-4 wd1e-4"),
             "mode": args.mode, "backbone": args.backbone, "keypoints": args.keypoints, "height": args.height,
             "width": args.width, "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,
-            "bn": "sync (global-batch statistics)" if args.sync_bn and world > 1 and args.mode == "infer"
-            else "per-rank",
+            "bn": "sync (global-batch statistics)" if args.sync_bn and world > 1 else "per-rank",
             "input": "fp32 NCHW (ToTensor)" if args.input == "f32" else "uint8 HWC BGR (ToTensor fused into the stem)"},
         "roofline": main_leg["roofline"],
         "model_tflops": main_leg["model_tflops"],
