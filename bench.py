@@ -387,9 +387,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # HKP_DIST_REHEARSE=1: N ranks share the visible GPU(s) over gloo — rehearses
+    # the multi-rank path (relaunch, barriers, max-over-ranks timing, DP wiring) on
+    # a one-GPU box; RCCL refuses two ranks on one device.  Never a measurement.
+    rehearse = dist and os.environ.get("HKP_DIST_REHEARSE") == "1"
+    if rehearse:
+        local = local % max(1, torch.cuda.device_count())
     if dist:
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            torch.distributed.init_process_group("gloo")
+        else:
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     precision = args.precision or "f16x3"
     batch = args.batch or (32 if args.mode == "infer" else 8)
@@ -425,6 +434,8 @@ def main():
             "mode": args.mode, "backbone": args.backbone, "keypoints": args.keypoints, "height": args.height,
             "width": args.width, "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,
             "bn": "sync (global-batch statistics)" if args.sync_bn and world > 1 else "per-rank",
+            "collectives": ("gloo REHEARSAL (ranks share one GPU: not a measurement)" if rehearse
+                            else "rccl" if world > 1 else "none"),
             "input": "fp32 NCHW (ToTensor)" if args.input == "f32" else "uint8 HWC BGR (ToTensor fused into the stem)"},
         "roofline": main_leg["roofline"],
         "model_tflops": main_leg["model_tflops"],
