@@ -40,6 +40,7 @@ import torch  # noqa: E402
 
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 PEAK_FP16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16/FP16 MFMA ~2.5 PF dense (spec)
+PEAK_HBM_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 PEAK_HBM_GBS = 8000.0
 
 
@@ -365,6 +366,21 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     if passes == 3:
         # f16x3 issues 3 fp16 MFMAs per fp32 MAC: its own ceiling is a third of the fp16 peak
         roof["frac_of_x3_ceiling"] = alg / (PEAK_FP16_MFMA_TFLOPS / 3)
+    # the classic roofline per launch: attainable time = max(issued FLOPs / MFMA
+    # peak, algorithmic bytes / HBM peak); frac_of_roofline = sum attainable /
+    # sum measured over the dominant symbol's launches (= frac when every launch
+    # is MFMA-bound; short-K 1x1 GEMMs writing wide fp16 outputs are HBM-bound)
+    t_att = t_meas = t_hbm = 0.0
+    for sym, f, b, s_ev, e_ev in timer.rec:
+        if sym != dom_sym:
+            continue
+        tc, tm = f * passes / (peak * 1e12), b / (PEAK_HBM_GBPS * 1e9)
+        t_att += max(tc, tm)
+        t_meas += s_ev.elapsed_time(e_ev) * 1e-3
+        t_hbm += tm if tm > tc else 0.0
+    if t_meas > 0:
+        roof["frac_of_roofline"] = t_att / t_meas
+        roof["hbm_bound_share_of_attainable"] = t_hbm / t_att if t_att > 0 else 0.0
     tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
     if (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3":
         (roof["traffic"], roof["traffic_source"], roof["rocprof_avg_ms"],
