@@ -9,6 +9,8 @@ particular rank 0, which writes results) holds the global [B, K, 2] in rank
 order.  One process per GPU, torch.distributed "nccl" = RCCL over xGMI (gloo
 for the CPU tests).
 """
+from contextlib import nullcontext as _nullcontext
+
 import torch
 import torch.distributed as dist
 
@@ -66,13 +68,16 @@ def gather_keypoints_fixed(yx, out=None, group=None):
 
 
 @torch.no_grad()
-def predict_keypoints_dp(model, x_shard, heat=False):
+def predict_keypoints_dp(model, x_shard, heat=False, sync=False):
     """Each rank's shard through the fused forward (+ argmax); keypoints gathered.
+    sync: BN statistics over the whole sharded batch (SyncBN, below) — the
+    result then equals one forward over the global batch.
     Returns (global int32 [B, K, 2], this rank's heatmaps or None)."""
-    if heat:
-        hm, yx = model.heatmaps_and_keypoints(x_shard)
-    else:
-        hm, yx = None, model.predict_keypoints(x_shard)
+    with (sync_bn() if sync else _nullcontext()):
+        if heat:
+            hm, yx = model.heatmaps_and_keypoints(x_shard)
+        else:
+            hm, yx = None, model.predict_keypoints(x_shard)
     return gather_keypoints(yx), hm
 
 
