@@ -140,6 +140,9 @@ def _dp_worker(rank, world, port, q):
                                      - 1).max())
         rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
         res["rm_err"] = abs(rm - float(g["running_checksum"][0])) / max(1.0, abs(rm))
+        m3 = model()                          # the Prediction-level DP entry point with SyncBN
+        yx3, _ = parallel.predict_keypoints_dp(m3, x, sync=True)
+        res["predict_dp_ok"] = bool(np.array_equal(yx3.cpu().numpy(), g["argmax_yx"]))
         m2 = model()                          # per-rank BN (the default): the shard's own statistics
         with torch.no_grad():
             _, _, low2 = net.keypoints_forward(m2.resnet.net, x, K, heat=True, argmax=True)
@@ -169,6 +172,7 @@ def test_syncbn_dp_inference_matches_reference_global_batch(cuda_device):
         assert r["low_err"] < 1e-4, r
         assert r["rowsum_err"] < 1e-4, r
         assert r["argmax_ok"], r                       # all 128 keypoints, bit-exact
+        assert r["predict_dp_ok"], r                   # parallel.predict_keypoints_dp(sync=True)
         assert r["rv_err"] < 1e-4 and r["rm_err"] < 1e-4, r
         assert r["low_err_per_rank_bn"] > 1e-3, r      # without SyncBN the shard misses the batch-32 fixture
     assert [r for r in res if "heat0_err" in r][0]["heat0_err"] < 1e-3
