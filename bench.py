@@ -23,7 +23,6 @@ all-gathered each step (hkp.parallel); training all-reduces gradients over RCCL.
 Prints ONE JSON line on rank 0.
 """
 import argparse
-import contextlib
 import json
 import os
 import socket
@@ -65,7 +64,26 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="main line only (no train / fp32 legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
+    ap.add_argument("--tune", action="append", default=[], metavar="FIELD=VALUE",
+                    help="A/B tooling: a non-default tuning field of hkp.policy.Policy (repeatable)")
+    ap.add_argument("--lib", default=None, help="A/B tooling: load this build of libhulkkp.so instead")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="N>1 on a one-GPU box: ranks share the GPU over gloo (rehearses the multi-rank path; "
+                         "never a measurement — RCCL refuses two ranks on one device)")
     return ap.parse_args()
+
+
+def tuning(args):
+    """--tune FIELD=VALUE pairs → Policy keyword arguments (typed like the defaults)."""
+    from hkp.policy import DEFAULT, TUNING_FIELDS
+    kw = {}
+    for item in args.tune:
+        k, _, v = item.partition("=")
+        if k not in TUNING_FIELDS:
+            raise SystemExit("bench.py: --tune %s: not a tuning field (%s)" % (k, ", ".join(TUNING_FIELDS)))
+        cur = getattr(DEFAULT, k)
+        kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
+    return kw
 
 
 def _free_port():
@@ -152,9 +170,10 @@ def pmc_traffic(kernel_sym, tag):
     exactly (spaces ignored).  A 256x256 conv_x3 launch whose last round runs as
     the split-K tail (conv_x3_tail_kernel, same stream, inside the same event
     pair) gets the tail's bytes and time folded in per main dispatch, so the
-    figures describe what the event timed.  Returns (bytes, source file,
-    rocprof average ms of the same scope, folded kernel or None); Nones if no
-    summary has the kernel."""
+    figures describe what the event timed.  Returns (bytes, source file, the PMC
+    pass's average ms of the same scope — serialised kernels, reported as
+    pmc_pass_avg_ms, not as the launch time — folded kernel or None); Nones if
+    no summary has the kernel."""
     import glob
     want = "::" + _nospace(kernel_sym) + "("
     tail_want = None
@@ -179,6 +198,35 @@ def pmc_traffic(kernel_sym, tag):
                         folded = tname
                 return nbytes, os.path.basename(path), ms or None, folded
     return None, None, None, None
+
+
+def trace_avg_ms(kernel_sym, tag):
+    """Average duration of `kernel_sym` from the newest committed rocprofv3
+    --kernel-trace --stats summary (profiles/*<tag>*kernel_stats*.csv), the same
+    scope the HIP events time: a 256x256 conv_x3 launch's split-K tail
+    (conv_x3_tail_kernel) folded in per main dispatch.  The PMC passes serialise
+    kernels and run at a different clock, so their durations are not used for
+    this.  Returns (ms, source file) or (None, None)."""
+    import csv
+    import glob
+    want = "::" + _nospace(kernel_sym) + "("
+    tail_want = None
+    if kernel_sym.startswith("conv_x3_kernel<256,"):
+        tail_want = "::conv_x3_tail_kernel<256,%s>(" % _nospace(kernel_sym).rstrip(">").split(",")[-1]
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*%s*kernel_stats*.csv" % tag)), reverse=True):
+        try:
+            rows = list(csv.DictReader(open(path)))
+        except (OSError, ValueError):
+            continue
+        main = [r for r in rows if want in _nospace(r["Name"])]
+        if not main:
+            continue
+        calls, tot = int(main[0]["Calls"]), float(main[0]["TotalDurationNs"])
+        for r in rows:
+            if tail_want and tail_want in _nospace(r["Name"]):
+                tot += float(r["TotalDurationNs"])
+        return tot / calls * 1e-6, os.path.basename(path)
+    return None, None
 
 
 def host_cores():
@@ -269,36 +317,36 @@ def cpu_baseline(args, budget_s):
 def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     """Time `steps` steps of one workload; return its metrics (rank 0 gets them)."""
     import hkp
-    from hkp import net as hkp_net
     from hkp import ops, parallel
+    from hkp.policy import Policy
     from oracle import recipe  # synthetic inputs (seeded images / keypoints only)
     from src.model import KeypointsGauss
 
     hkp.lib()
     dist = world > 1
-    hkp_net.set_conv_precision(precision)
+    sync_bn = dist and getattr(args, "sync_bn", False)
     B, K, H, W = batch, args.keypoints, args.height, args.width
     torch.manual_seed(1234 + rank)
-    model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False).to(dev)
+    pol = Policy(precision=precision, **tuning(args))
+    model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=pol).to(dev)
     imgs = recipe.seeded_images_u8(B, H, W, 1234 + rank)
     x = recipe.to_tensor_nchw(imgs).to(dev) if args.input == "f32" else torch.from_numpy(imgs).to(dev)
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99 + rank)).to(dev)
 
     if mode == "infer":
         gathered = torch.empty((world * B, K, 2), device=dev, dtype=torch.int32) if dist else None
-
-        sync = parallel.sync_bn() if dist and getattr(args, "sync_bn", False) else contextlib.nullcontext()
+        if sync_bn:
+            model.policy = model.policy.with_(sync_bn=True)
 
         def step():
-            with torch.no_grad(), sync:
+            with torch.no_grad():
                 hm, yx = model.heatmaps_and_keypoints(x)
                 if dist:                                   # every rank ends with all keypoints
                     parallel.gather_keypoints_fixed(yx, gathered)
                 return hm
     else:
         from hkp import train as hkp_train
-        trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4, distributed=dist,
-                                    sync_bn=dist and getattr(args, "sync_bn", False))
+        trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4, distributed=dist, sync_bn=sync_bn)
 
         def step():
             return trainer.step(x, uv)
@@ -338,7 +386,6 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
         del trainer
     torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(dev)
-    hkp_net.set_conv_precision("f16x3")
 
     value = B * steps * world / elapsed
     fl_img = conv_flops_per_image(args.backbone, K, H, W)
@@ -383,8 +430,10 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
         roof["hbm_bound_share_of_attainable"] = t_hbm / t_att if t_att > 0 else 0.0
     tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
     if (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3":
-        (roof["traffic"], roof["traffic_source"], roof["rocprof_avg_ms"],
+        (roof["traffic"], roof["traffic_source"], roof["pmc_pass_avg_ms"],
          roof["folded_kernel"]) = pmc_traffic(dom_sym, tag)
+        # the kernel trace of the bench command itself (not the serialised PMC pass)
+        roof["rocprof_avg_ms"], roof["rocprof_source"] = trace_avg_ms(dom_sym, tag)
     return {"value": value, "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
             "batch_per_gpu": B, "global_batch": B * world, "roofline": roof,
             "model_tflops": value / world * fl_img * (3 if mode == "train" else 1) / 1e12,
@@ -403,10 +452,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
-    # HKP_DIST_REHEARSE=1: N ranks share the visible GPU(s) over gloo — rehearses
-    # the multi-rank path (relaunch, barriers, max-over-ranks timing, DP wiring) on
-    # a one-GPU box; RCCL refuses two ranks on one device.  Never a measurement.
-    rehearse = dist and os.environ.get("HKP_DIST_REHEARSE") == "1"
+    # --rehearse-gloo: N ranks share the visible GPU(s) over gloo — rehearses the
+    # multi-rank path (relaunch, barriers, max-over-ranks timing, DP wiring) on a
+    # one-GPU box; RCCL refuses two ranks on one device.  Never a measurement.
+    rehearse = dist and args.rehearse_gloo
+    if args.lib:
+        from hkp import _lib
+        _lib.use_library(os.path.abspath(args.lib))
     if rehearse:
         local = local % max(1, torch.cuda.device_count())
     if dist:

@@ -455,7 +455,7 @@ static int fin_one(const char* who, int32_t c, int64_t count, int64_t tiles, int
                        (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,      \
                        running_var, num_batches_tracked, scale_shift, mean_invstd, stats)
 #define HKP_FIN(CPB)                                  \
-    if (tiles >= 4096 && !g_fin_small) { HKP_FIN1(CPB, 1024); } \
+    if (tiles >= 4096) { HKP_FIN1(CPB, 1024); } \
     else { HKP_FIN1(CPB, 256); }
     if (cpb == 8) { HKP_FIN(8); }
     else if (cpb == 4) { HKP_FIN(4); }

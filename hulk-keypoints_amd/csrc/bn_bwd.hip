@@ -408,7 +408,7 @@ static int bwd_fin(int32_t c, int64_t m, const float* partials, const float* max
                        c, (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, maxima,                  \
                        (unsigned*)dy_amax_bits, stats)
 #define HKP_BFIN(CPB)                                  \
-    if (tiles >= 4096 && !g_fin_small) { HKP_BFIN1(CPB, 1024); } \
+    if (tiles >= 4096) { HKP_BFIN1(CPB, 1024); } \
     else { HKP_BFIN1(CPB, 256); }
     if (cpb == 8) { HKP_BFIN(8); }
     else if (cpb == 4) { HKP_BFIN(4); }

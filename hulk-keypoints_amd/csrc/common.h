@@ -97,9 +97,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 // contiguous load (8*CPB bytes) instead of CPB separate sectors; lane sums are
 // combined in a fixed order.  CPB chosen so that C/CPB blocks still fill the chip.
 static inline int partials_cpb(int C) { return C >= 1024 ? 8 : C >= 512 ? 4 : C >= 256 ? 2 : 1; }
-// the BN finalize kernels take 1024-thread blocks for >= 4096 tiles; A/B knob
-// HKP_FIN_SMALL=1 keeps 256
-static const bool g_fin_small = getenv("HKP_FIN_SMALL") != nullptr;
+// (the BN finalize kernels take 1024-thread blocks for >= 4096 tiles)
 
 // NW = waves per block (4: the 256-thread finalize; 16: the 1024-thread one for
 // long tile lists); the per-wave sums are combined pairwise in a fixed order

@@ -7,9 +7,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# HKP_LIB_AB: an alternative build of the same ABI for in-tree A/B runs (tools/ab.sh);
-# unset, the product loads its own in-tree library
-LIB_PATH = os.environ.get("HKP_LIB_AB") or os.path.join(_HERE, "libhulkkp.so")
+# the product loads its own in-tree library; A/B tooling may point this process at
+# another build of the same ABI with use_library() before the first call
+LIB_PATH = os.path.join(_HERE, "libhulkkp.so")
 
 HKP_LAYOUT_NHWC = 0
 HKP_LAYOUT_NCHW = 1
@@ -75,14 +75,10 @@ SIGNATURES = {
     "hkp_bn_apply_head": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
-    "hkp_weight_split": (ctypes.c_int, [_I64, _P, _P, _P, _P]),
-    "hkp_conv2d_fwd_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "hkp_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_x3_sk_workspace_bytes": (_I64, []),
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
-    "hkp_conv_weight_flip_split": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
-    "hkp_conv2d_bwd_data_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
     "hkp_weight_pack_f16": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_f16": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_kernel_name": (_I32, [_CD, _I32, _I32, ctypes.c_char_p, _I32]),
@@ -105,8 +101,6 @@ SIGNATURES = {
     "hkp_weight_pack_x3_batch": (ctypes.c_int, [_I32, ctypes.POINTER(PackJob), _P, _I64, _P]),
     "hkp_conv_bwd_filter_x3_workspace": (_I64, [_CD]),
     "hkp_conv2d_bwd_filter_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
-    "hkp_conv_bwd_filter_split_workspace": (_I64, [_CD]),
-    "hkp_conv2d_bwd_filter_split": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_adam_step": (ctypes.c_int, [_I32, ctypes.POINTER(AdamTensor), _F, _F, _F, _F, _F, _F, _F, _P]),
     # backward
     "hkp_conv_weight_flip":(ctypes.c_int, [_CD, _P, _P, _P]),
@@ -129,6 +123,15 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+def use_library(path):
+    """Tools only (in-process A/B of two builds): load `path` instead of the in-tree
+    library.  Must run before the first kernel call of the process."""
+    global LIB_PATH
+    if _lib is not None:
+        raise HkpError("use_library: %s is already loaded" % LIB_PATH)
+    LIB_PATH = path
 
 
 def lib():

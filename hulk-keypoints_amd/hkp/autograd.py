@@ -16,7 +16,7 @@ from . import net, ops
 class _KeypointsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, model, *params):
-        trace = net.Trace()
+        trace = net.Trace(model.policy)
         hm, _, _ = net.keypoints_forward(model.resnet.net, x, model.num_keypoints, heat=True, trace=trace)
         ctx.trace, ctx.model = trace, model
         return hm
@@ -24,7 +24,10 @@ class _KeypointsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_heat):
         model = ctx.model
-        grads = net.keypoints_backward(model.resnet.net, ctx.trace, d_heat.contiguous(), net.Grads())
+        # model.grad_ready (DP: GradBucketer.ready) sees each gradient as soon as it
+        # exists, so bucket all-reduces overlap the rest of this backward
+        grads = net.keypoints_backward(model.resnet.net, ctx.trace, d_heat.contiguous(),
+                                       net.Grads(on_ready=getattr(model, "grad_ready", None)))
         ctx.trace = None
         out = [None, None]
         for p in model.parameters():

@@ -9,62 +9,78 @@ Forward per BasicBlock (src/resnet.py:53-69), train-mode BN:
     y2 = conv2(a1); s2 = bn_finalize(bn2)
     [yd = ds_conv(x); sd = bn_finalize(ds_bn)]
     out = relu(y2*s2 + (x | yd*sd))
+
+Every entry point takes the network's execution Policy (hkp.policy: conv
+arithmetic, SyncBN group, measured tuning choices) as an argument — None means
+the default policy; nothing here is process-global except caches keyed by
+parameter identity and version.
 """
-import os
 import weakref
 
 import torch
 
 from . import ops, parallel
+from .policy import resolve
 
 
 class Trace:
-    """What a forward keeps for the backward pass (None = inference)."""
+    """What a forward keeps for the backward pass (None = inference), and the
+    policy the forward ran under (the backward uses the same one)."""
 
-    def __init__(self):
+    def __init__(self, policy=None):
+        self.policy = resolve(policy)
         self.blocks = []
         self.stem = None
         self.head = None
 
 
-def _bn_params(bn, part, count, stats_only=False):
-    """scale_shift (+ mean_invstd) for a BN layer: batch stats in training mode
-    (and running-stat update, like nn.BatchNorm2d.forward), running stats otherwise."""
-    if bn.training:
-        sync = parallel.sync_bn_group()
-        if sync is not None:                       # SyncBN: statistics over every rank's shard
-            st = parallel.gather_bn_stats(ops.bn_stats(part, count), sync[0])
-            return ops.bn_finalize_ranks(st, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                                         bn.num_batches_tracked,
-                                         momentum=bn.momentum if bn.momentum is not None else 0.1, eps=bn.eps)
-        return ops.bn_finalize(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                               bn.num_batches_tracked, momentum=bn.momentum if bn.momentum is not None else 0.1,
-                               eps=bn.eps)
-    return ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+def _finalize_args(bn):
+    return dict(momentum=bn.momentum if bn.momentum is not None else 0.1, eps=bn.eps)
+
+
+def _bn_params_many(items, pol):
+    """[(bn, partials, count)] → [(scale_shift, mean_invstd)]: batch statistics in
+    training mode (and the running-stat update, like nn.BatchNorm2d.forward),
+    running stats otherwise.  Under SyncBN the layers' statistics blocks ride ONE
+    all-gather (layers whose statistics are ready together: a block's last BN and
+    its downsample BN)."""
+    sync = parallel.active_sync_group(pol)
+    out = [None] * len(items)
+    gather = []
+    for i, (bn, part, count) in enumerate(items):
+        if not bn.training:
+            out[i] = ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+        elif sync is None:
+            out[i] = ops.bn_finalize(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                     bn.num_batches_tracked, two_level_tiles=pol.fin_two_level_tiles,
+                                     **_finalize_args(bn))
+        else:
+            gather.append((i, ops.bn_stats(part, count, two_level_tiles=pol.fin_two_level_tiles)))
+    if gather:
+        st = parallel.gather_bn_stats(torch.cat([g for _, g in gather]), sync[0])
+        off = 0
+        for i, own in gather:
+            bn = items[i][0]
+            out[i] = ops.bn_finalize_ranks(st[:, off:off + own.numel()], bn.weight, bn.bias, bn.running_mean,
+                                           bn.running_var, bn.num_batches_tracked, **_finalize_args(bn))
+            off += own.numel()
+    return out
+
+
+def _bn_params(bn, part, count, pol):
+    return _bn_params_many([(bn, part, count)], pol)[0]
 
 
 def _i(v):
     return v[0] if isinstance(v, (tuple, list)) else v
 
 
-# Conv arithmetic for the NHWC convs (the stem always runs the fp32 gather kernel):
-#   "fp32"  v_mfma_f32_32x32x2_f32, exact fp32 products
-#   "f16x3" split-precision fp16 MFMA, fp32-accurate (~2^-22 per product)
-#   "f16"   plain fp16 operands and activations, fp32 accumulation (BASELINE
-#           config C4, inference): the LDS-DMA conv kernels with one fp16 MFMA
-#           per MAC, fp16 conv outputs and residual stream (autocast semantics)
-PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
-_precision = os.environ.get("HKP_CONV_PRECISION", "f16x3")
 # id(parameter) → (weakref(parameter), {variant: (version, data_ptr, derived operand)}).
 # The weakref check means a dead parameter's entry is never served to a new
 # tensor that happens to reuse its id, data pointer and version.
 _split_cache = {}
 # (id(resnet), flip) → the last prepack_x3 launch that repacked every operand
 _prepack_plans = {}
-_NO_PREPACK_PLAN = os.environ.get("HKP_NO_PREPACK_PLAN") == "1"     # A/B: always rebuild
-_UNFUSED_HEAD = os.environ.get("HKP_UNFUSED_HEAD") == "1"           # A/B: bn_apply + head_fc
-_F16_TILE_1X1 = int(os.environ.get("HKP_F16_TILE_1X1", "0"))         # A/B: HKP_TILE_* for plain-fp16 1x1 convs
-_F16_TILE_KXK = int(os.environ.get("HKP_F16_TILE_KXK", "0"))
 
 
 def _cache_slot(w):
@@ -100,13 +116,14 @@ def _nhwc_convs(resnet):
                 yield block.downsample[0]
 
 
-def prepack_x3(resnet, flip):
+def prepack_x3(resnet, flip, pol=None):
     """Refresh every stale f16x3 conv operand of the backbone — the forward packs
     and (flip=True, training) the stride-1 convs' flipped dgrad packs — in one
     batched launch pair (hkp_weight_pack_x3_batch) instead of one pack per conv.
     The operands land in the same cache conv_bn / _conv_backward read, with the
     parameter versions they were packed from; buffers are reused across steps."""
-    if _precision != "f16x3":
+    pol = resolve(pol)
+    if pol.precision != "f16x3":
         return
     # fast path: the last call's launch repeated as is when every operand it packed
     # is stale again (a training step: the optimizer bumped every weight) and the
@@ -114,7 +131,7 @@ def prepack_x3(resnet, flip):
     # step left the GPU idle ~0.5 ms
     key = (id(resnet), flip)
     plan = _prepack_plans.get(key)
-    if plan is not None and plan["net"]() is resnet and not _NO_PREPACK_PLAN:
+    if plan is not None and plan["net"]() is resnet and pol.prepack_plan:
         units = [(wr(), per, v, obj) for wr, per, v, obj in plan["units"]]
         if all(u[0] is not None for u in units):
             fresh = [_fresh(w, per.get(v)) for w, per, v, _ in units]
@@ -175,70 +192,54 @@ def prepack_x3(resnet, flip):
         _prepack_plans.pop(key, None)
 
 
-def set_conv_precision(p):
-    global _precision
-    if p not in PRECISIONS:
-        raise ValueError("precision must be one of %s" % sorted(PRECISIONS))
-    _precision = p
-
-
-def conv_precision():
-    return _precision
-
-
-def _split_weight(w, passes):
-    """Cached hi/lo fp16 split of a weight; refreshed whenever the parameter changes
-    (optimizer steps and load_state_dict bump its version counter)."""
-    return _cached_split(w, passes, lambda t: ops.weight_split(t, passes))
-
-
 def _pack_weight_x3(w):
     """Cached packed f16x3 split of a KRSC weight (conv2d_fwd_x3's operand)."""
     return _cached_split(w, "x3", ops.weight_pack_x3)
 
 
-def conv_bn(conv, bn, x, layout="nhwc"):
+def conv_bn(conv, bn, x, pol=None, layout="nhwc"):
     """conv (+ BN partials when training) → (y, scale_shift, mean_invstd).
     x: fp32 NHWC (optionally carrying its producer's operand split), a split-only
     activation (fp16, see ops.bn_apply keep_fp32=False), or NCHW for the stem."""
-    y, part = _conv_fwd(conv, bn, x, layout)
-    count = y.numel() // y.shape[-1]
-    ss, mi = _bn_params(bn, part, count)
+    pol = resolve(pol)
+    y, part = _conv_fwd(conv, bn, x, pol, layout)
+    ss, mi = _bn_params(bn, part, y.numel() // y.shape[-1], pol)
     return y, ss, mi
 
 
-def _conv_fwd(conv, bn, x, layout="nhwc", part_out=None, sk=True):
-    """The conv of conv_bn → (y, BN tile partials or None).  part_out: a caller's
-    buffer for the partials (the x3 / stem x3 paths); sk=False: no stream-K."""
-    passes = PRECISIONS[_precision]
+def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
+    """The conv of conv_bn → (y, BN tile partials or None); sk=False: no stream-K.
+    f16x3 and f16 run on the LDS-DMA MFMA kernels (conv_x3.hip); shapes those do
+    not take (Cout % 64, or Cin % 64 for f16) run the exact fp32 MFMA kernel, which
+    needs the fp32 activation."""
+    passes = pol.passes
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
-    if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd, dl):
-        y, part = ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
-                                         stats=bn.training, part_out=part_out)
-    elif layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
-        y, part = ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training,
-                                    part_out=part_out, sk=sk)
-    elif layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
-        y, part = ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
-                                     stats=bn.training, sk=sk,
-                                     tile=_F16_TILE_1X1 if conv.weight.shape[1] == 1 else _F16_TILE_KXK)
-    elif part_out is not None:
-        raise ops.HkpError("conv %s: partials into a caller buffer need the x3 path" % (tuple(conv.weight.shape),))
-    elif layout == "nhwc" and passes:
-        hi, lo = _split_weight(conv.weight, passes)
-        x_hi = sp[0] if (sp is not None and sp[1] == 1 and passes == 1) else None
-        y, part = ops.conv2d_fwd_split(x if x.dtype == torch.float32 else None, hi, lo, passes, st, pd, dl,
-                                       stats=bn.training, x_hi=x_hi)
-    else:
-        y, part = ops.conv2d_fwd(x, conv.weight, st, pd, dl, layout=layout, stats=bn.training)
-    return y, part
+    if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd,
+                                                                 dl):
+        return ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
+                                      stats=bn.training)
+    if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
+        return ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training, sk=sk)
+    if layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
+        return ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
+                                  stats=bn.training, sk=sk,
+                                  tile=pol.f16_tile_1x1 if conv.weight.shape[1] == 1 else pol.f16_tile_kxk)
+    if x.dtype != torch.float32:
+        raise ops.HkpError("conv %s under precision %r: no LDS-DMA kernel for this shape and no fp32 input "
+                           "for the fp32 kernel" % (tuple(conv.weight.shape), pol.precision))
+    return ops.conv2d_fwd(x, conv.weight, st, pd, dl, layout=layout, stats=bn.training)
 
 
 def _f16_conv_ok(conv):
     """The conv runs on the plain-fp16 LDS-DMA kernel (hkp_conv2d_fwd_f16)."""
     return conv.weight.shape[0] % 64 == 0 and conv.weight.shape[-1] % 64 == 0
+
+
+def _x3_fwd_ok(conv):
+    """The conv's forward takes the packed f16x3 operand (hkp_conv2d_fwd_x3)."""
+    return conv.weight.shape[0] % 64 == 0 and conv.weight.shape[-1] % 32 == 0
 
 
 def image_nchw_shape(x):
@@ -248,7 +249,7 @@ def image_nchw_shape(x):
     return tuple(x.shape)
 
 
-def _image_input(resnet, x, trace):
+def _image_input(resnet, x, trace, pol):
     """The stem's input: uint8 NHWC batches go straight into the f16x3 stem pack
     (ToTensor fused); the fp32 NCHW image is materialised on the
     device only where something needs it (training: the stem wgrad; other
@@ -263,36 +264,50 @@ def _image_input(resnet, x, trace):
         raise ValueError("expected a [B,H,W,3] uint8 batch, got %s" % (tuple(x.shape),))
     x = x.contiguous()
     c1 = resnet.conv1
-    direct = trace is None and PRECISIONS[_precision] == 3 and ops.stem_x3_ok(
+    direct = trace is None and pol.passes == 3 and ops.stem_x3_ok(
         image_nchw_shape(x), tuple(c1.weight.shape), _i(c1.stride), _i(c1.padding), _i(c1.dilation))
     return x if direct else ops.images_u8_to_nchw(x)
 
 
-def _split_for(c):
+def _split_for(c, pol):
     """Operand split the producers of a C-channel activation emit for its consumer convs."""
-    p = PRECISIONS[_precision]
+    p = pol.passes
     return p if (p and c % 32 == 0) else 0
 
 
-def stem_forward(resnet, x_nchw, trace=None):
+def _consumers_take_split(convs, pol):
+    """Every consumer conv reads the producer's split (no fp32 copy needed)."""
+    return pol.passes != 3 or all(_x3_fwd_ok(c) for c in convs)
+
+
+def _block_convs_reading_input(block):
+    return [block.conv1] + ([block.downsample[0]] if block.downsample is not None else [])
+
+
+def stem_forward(resnet, x_nchw, trace=None, pol=None, next_convs=()):
     """conv1 → bn1 → relu → maxpool (src/resnet.py:199-202)."""
-    y, ss, mi = conv_bn(resnet.conv1, resnet.bn1, x_nchw, layout="nchw")
-    sp = _split_for(y.shape[-1])
+    pol = resolve(pol)
+    y, ss, mi = conv_bn(resnet.conv1, resnet.bn1, x_nchw, pol, layout="nchw")
+    sp = _split_for(y.shape[-1], pol)
     # inference: the stem output is only read by layer1's convs and (as the raw
     # residual, hi + lo) its first block → split-only
-    out = ops.bn_relu_maxpool(y, ss, split=sp, route=trace is not None, keep_fp32=trace is not None or sp == 0)
+    keep = trace is not None or sp == 0 or not _consumers_take_split(next_convs, pol)
+    out = ops.bn_relu_maxpool(y, ss, split=sp, route=trace is not None, keep_fp32=keep)
     if trace is not None:
         trace.stem = dict(x=x_nchw, y=y, ss=ss, mi=mi, out=out)
     return out
 
 
-def block_forward(block, x, trace=None, final=False, head=None):
+def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_convs=()):
     """One BasicBlock / Bottleneck.  x: fp32 NHWC (with its split attached) or, in
     inference, a split-only activation.  In inference the block output is written
-    split-only too unless `final` (the head reads fp32): the next block's convs
-    read the split and its residual add reads hi + lo.  head = (w [K,C], bias [K])
-    (inference, last block): the tail BN apply runs fused with the K-row head and
-    the block returns the lowres logits instead (hkp_bn_apply_head)."""
+    split-only too unless `final` (the head reads fp32) or a consumer conv in
+    next_convs needs the fp32 tensor: the next block's convs read the split and
+    its residual add reads hi + lo.  head = (w [K,C], bias [K]) (inference, last
+    block): the tail BN apply runs fused with the K-row head and the block returns
+    the lowres logits instead (hkp_bn_apply_head).  Under SyncBN the last BN and
+    the downsample BN share one statistics gather."""
+    pol = resolve(pol)
     rec = {} if trace is not None else None
     # producers also write the next conv's operand split; an activation only a
     # conv consumes (inside the block, no backward trace) is written split-only
@@ -304,66 +319,79 @@ def block_forward(block, x, trace=None, final=False, head=None):
         # training keeps the fp32 activation only where the backward reads it: an
         # inner activation feeding an x3-backward conv is needed only as its split
         # (its ReLU mask is recomputed from y, its wgrad reads the split)
-        sp = _split_for(y.shape[-1])
-        need32 = keep and not (sp == 3 and _MASK_FROM_Y and _x3_conv_backward_ok(consumer))
+        sp = _split_for(y.shape[-1], pol)
+        need32 = keep and not (sp == 3 and pol.mask_from_y and _x3_conv_backward_ok(consumer, pol))
+        need32 = need32 or not _consumers_take_split([consumer], pol)
         return ops.bn_apply(y, s, relu=True, split=sp, keep_fp32=need32 or not sp)
 
-    if block.kind == "basic":
-        y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
-        a1 = act(y1, s1, block.conv2)
-        y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
-        last_y, last_s = y2, s2
-        if rec is not None:
-            rec.update(x=x, y=[y1, y2], ss=[s1, s2], mi=[m1, m2], act=[a1])
-    else:
-        y1, s1, m1 = conv_bn(block.conv1, block.bn1, x)
-        a1 = act(y1, s1, block.conv2)
-        y2, s2, m2 = conv_bn(block.conv2, block.bn2, a1)
-        a2 = act(y2, s2, block.conv3)
-        y3, s3, m3 = conv_bn(block.conv3, block.bn3, a2)
-        last_y, last_s = y3, s3
-        if rec is not None:
-            rec.update(x=x, y=[y1, y2, y3], ss=[s1, s2, s3], mi=[m1, m2, m3], act=[a1, a2])
-    pl = _split_for(last_y.shape[-1])
-    keep_out = keep or final or pl != 3
-    if head is not None:
-        if last_y.dtype == torch.float16 and x.dtype != torch.float16:
-            x = ops.split_of(x)[0]
-        if block.downsample is not None:
-            yd, sd, _ = conv_bn(block.downsample[0], block.downsample[1], x)
-            return ops.bn_apply_head(last_y, last_s, yd, sd, *head)
-        return ops.bn_apply_head(last_y, last_s, x, None, *head)
-    if last_y.dtype == torch.float16:                 # plain-fp16 path: fp16 residual stream
-        res = x if x.dtype == torch.float16 else ops.split_of(x)[0]
-        if block.downsample is not None:
-            yd, sd, _ = conv_bn(block.downsample[0], block.downsample[1], x)
-            return ops.bn_apply_f16(last_y, last_s, res=yd, res_ss=sd, relu=True, keep_fp32=final)
-        return ops.bn_apply_f16(last_y, last_s, res=res, relu=True, keep_fp32=final)
+    convs = [block.conv1, block.conv2] + ([block.conv3] if block.kind == "bottleneck" else [])
+    bns = [block.bn1, block.bn2] + ([block.bn3] if block.kind == "bottleneck" else [])
+    ys, sss, mis, acts = [], [], [], []
+    a = x
+    for i, (conv, bn) in enumerate(zip(convs, bns)):
+        if i == len(convs) - 1:
+            break
+        y, s, m = conv_bn(conv, bn, a, pol)
+        a = act(y, s, convs[i + 1])
+        ys.append(y), sss.append(s), mis.append(m), acts.append(a)
+    # the last conv and the downsample conv, then both BN parameter sets together
+    y_last, part_last = _conv_fwd(convs[-1], bns[-1], a, pol)
+    items = [(bns[-1], part_last, y_last.numel() // y_last.shape[-1])]
+    yd = None
     if block.downsample is not None:
-        yd, sd, md = conv_bn(block.downsample[0], block.downsample[1], x)
-        out = ops.bn_apply(last_y, last_s, res=yd, res_ss=sd, relu=True, split=pl, keep_fp32=keep_out)
+        xd = x
+        if y_last.dtype == torch.float16 and x.dtype != torch.float16:
+            xd = ops.split_of(x)[0]
+        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], xd, pol)
+        items.append((block.downsample[1], part_d, yd.numel() // yd.shape[-1]))
+    params = _bn_params_many(items, pol)
+    (last_s, last_m) = params[0]
+    sd, md = params[1] if yd is not None else (None, None)
+    ys.append(y_last), sss.append(last_s), mis.append(last_m)
+    if rec is not None:
+        rec.update(x=x, y=ys, ss=sss, mi=mis, act=acts)
+    pl = _split_for(y_last.shape[-1], pol)
+    keep_out = keep or final or pl != 3 or not _consumers_take_split(next_convs, pol)
+    if head is not None:
+        if yd is not None:
+            return ops.bn_apply_head(y_last, last_s, yd, sd, *head)
+        res = ops.split_of(x)[0] if (y_last.dtype == torch.float16 and x.dtype != torch.float16) else x
+        return ops.bn_apply_head(y_last, last_s, res, None, *head)
+    if y_last.dtype == torch.float16:                 # plain-fp16 path: fp16 residual stream
+        if yd is not None:
+            return ops.bn_apply_f16(y_last, last_s, res=yd, res_ss=sd, relu=True, keep_fp32=final)
+        res = x if x.dtype == torch.float16 else ops.split_of(x)[0]
+        return ops.bn_apply_f16(y_last, last_s, res=res, relu=True, keep_fp32=final)
+    if yd is not None:
+        out = ops.bn_apply(y_last, last_s, res=yd, res_ss=sd, relu=True, split=pl, keep_fp32=keep_out)
         if rec is not None:
             rec.update(yd=yd, sd=sd, md=md)
     else:
-        out = ops.bn_apply(last_y, last_s, res=x, relu=True, split=pl, keep_fp32=keep_out)
+        out = ops.bn_apply(y_last, last_s, res=x, relu=True, split=pl, keep_fp32=keep_out)
     if rec is not None:
         rec["out"] = out
         trace.blocks.append(rec)
     return out
 
 
-def backbone_forward(resnet, x_nchw, trace=None, head=None):
+def _blocks(resnet):
+    return [b for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4) for b in layer]
+
+
+def backbone_forward(resnet, x_nchw, trace=None, head=None, pol=None):
     """ResNet.forward up to the fc (src/resnet.py:198-213), NHWC output.  x_nchw:
     the [B,3,H,W] fp32 image or the [B,H,W,3] uint8 batch (see _image_input).
     head = (w [K,C], bias [K]) (inference): returns the head's lowres logits
     [B,K,h,w] instead, the last block's BN apply fused with the head."""
-    x_in = _image_input(resnet, x_nchw, trace)
-    prepack_x3(resnet, flip=trace is not None)
-    x = stem_forward(resnet, x_in, trace)
-    blocks = [b for layer in (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4) for b in layer]
+    pol = trace.policy if trace is not None else resolve(pol)
+    x_in = _image_input(resnet, x_nchw, trace, pol)
+    prepack_x3(resnet, trace is not None, pol)
+    blocks = _blocks(resnet)
+    x = stem_forward(resnet, x_in, trace, pol, next_convs=_block_convs_reading_input(blocks[0]))
     for i, block in enumerate(blocks):
         last = i == len(blocks) - 1
-        x = block_forward(block, x, trace, final=last, head=head if last else None)
+        nxt = () if last else _block_convs_reading_input(blocks[i + 1])
+        x = block_forward(block, x, trace, final=last, head=head if last else None, pol=pol, next_convs=nxt)
     return x
 
 
@@ -378,15 +406,17 @@ def fc_rows(resnet, k):
     return w.reshape(w.shape[0], -1)[:k], resnet.fc.bias[:k]
 
 
-def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None):
-    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22)."""
-    if trace is not None and _precision == "f16":
+def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None, pol=None):
+    """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22).
+    pol: the execution policy (a trace carries its own)."""
+    pol = trace.policy if trace is not None else resolve(pol)
+    if trace is not None and pol.precision == "f16":
         raise ops.HkpError("precision 'f16' (BASELINE config C4) is inference-only; train with 'f16x3' or 'fp32'")
     w, b = fc_rows(resnet, k)
-    if trace is None and not _UNFUSED_HEAD and ops.head_fusable(_feat_channels(resnet), k):
-        feat, low = None, backbone_forward(resnet, x_nchw, None, head=(w, b))
+    if trace is None and pol.fused_head and ops.head_fusable(_feat_channels(resnet), k):
+        feat, low = None, backbone_forward(resnet, x_nchw, None, head=(w, b), pol=pol)
     else:
-        feat = backbone_forward(resnet, x_nchw, trace)
+        feat = backbone_forward(resnet, x_nchw, trace, pol=pol)
         low = ops.head_fc(feat, w, b)
     H, W = image_nchw_shape(x_nchw)[2:]
     hm, yx = ops.upsample_sigmoid(low, H, W, heat=heat, argmax=argmax)
@@ -428,15 +458,6 @@ class Grads(dict):
         self.events = []
 
 
-# wgrad of a conv runs on a side stream, concurrently with its dgrad: the two
-# grids fill each other's last partial round of CUs (HKP_OVERLAP_WGRAD=0: serial)
-OVERLAP_WGRAD = os.environ.get("HKP_OVERLAP_WGRAD", "1") != "0"
-# HKP_TILE_* policy of a dgrad overlapped by its wgrad: 256x256 tiles with the split-K
-# tail where Cout allows, else the planner without stream-K (a stream-K grid takes
-# every CU the wgrad would fill: -1 %); C3 training +1.4-2.4 % over the plain planner
-_DGRAD_OV_TILE = int(os.environ.get("HKP_DGRAD_OV_TILE", "9"))
-# inner BN ReLU masks recomputed from y (HKP_MASK_FROM_Y=0: read the fp32 activation)
-_MASK_FROM_Y = os.environ.get("HKP_MASK_FROM_Y", "1") != "0"
 _side_streams = {}
 _dev_total = {}
 
@@ -460,20 +481,20 @@ def _side_stream(dev):
     return s
 
 
-def _x3_conv_backward_ok(conv):
+def _x3_conv_backward_ok(conv, pol):
     """conv's backward can run entirely on the packed f16x3 path given a packed x
     (dgrad stride 1, or stride 2 without dilation)."""
     k, c = conv.weight.shape[0], conv.weight.shape[-1]
     st, dl = _i(conv.stride), _i(conv.dilation)
-    return _precision == "f16x3" and k % 64 == 0 and c % 64 == 0 and (st == 1 or (st == 2 and dl == 1))
+    return pol.precision == "f16x3" and k % 64 == 0 and c % 64 == 0 and (st == 1 or (st == 2 and dl == 1))
 
 
-def _x3_backward(conv, x):
+def _x3_backward(conv, x, pol):
     """Whether conv's backward runs entirely on the packed f16x3 path (x carries its
     split) — then the BN backward feeding it writes dy directly as the packed
     split (bn_bwd split_only)."""
     xs = ops.split_of(x)
-    return xs is not None and xs[1] == 3 and _x3_conv_backward_ok(conv)
+    return xs is not None and xs[1] == 3 and _x3_conv_backward_ok(conv, pol)
 
 
 def _act_shape(x):
@@ -481,13 +502,12 @@ def _act_shape(x):
     return tuple(x.shape[:-1]) + (ops.channels_of(x),)
 
 
-def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
+def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
     """wgrad (+ dgrad with the residual addend fused) for one NHWC conv.  dy: fp32, or
     (x3 path) already the packed scaled split from bn_bwd(split_only=True)."""
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
-    c, k = ops.channels_of(x), conv.weight.shape[0]
     xs = ops.split_of(x)
-    if _x3_backward(conv, x):
+    if _x3_backward(conv, x, pol):
         # packed split operands: dy split once (scaled by a power of two from
         # max|dy| or its bound) and read by both the dgrad and the wgrad conv
         amax = getattr(dy, "_hkp_amax", None)     # fused into the BN backward
@@ -498,7 +518,7 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
                 amax = ops.absmax(dy)
             dys = ops.split_pack_x3(dy, amax)
         ready = None
-        if OVERLAP_WGRAD and not _memory_tight(dys.device):
+        if pol.overlap_wgrad and not _memory_tight(dys.device):
             main, side = torch.cuda.current_stream(dys.device), _side_stream(dys.device)
             side.wait_stream(main)                     # dy split (and x split) written
             with torch.cuda.stream(side):
@@ -510,86 +530,116 @@ def _conv_backward(conv, x, dy, grads, need_dx=True, add=None):
                 t.record_stream(side)
         dx = None
         if need_dx:
+            ov = ready is not None
             if st == 1:
                 wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
-                ov = ready is not None
+                tile = pol.dgrad_overlap_tile if ov else 0
                 dx = ops.conv2d_bwd_data_x3(dys, wfs, _act_shape(x), pd, dl, add=add, amax=amax,
-                                            sk=not ov or _DGRAD_OV_TILE == 9, tile=_DGRAD_OV_TILE if ov else 0)
+                                            sk=not ov or tile == 9, tile=tile)
             else:                          # stride 2: one stride-1 conv per output phase of dx
                 phs = _cached_split(conv.weight, "phase_x3", lambda t: ops.weight_phase_pack_x3(t, pd))
                 dx = ops.conv2d_bwd_data_x3_strided(dys, phs, _act_shape(x), tuple(conv.weight.shape), pd, add=add,
-                                                    amax=amax, sk=ready is None)
+                                                    amax=amax, sk=not ov)
         if ready is None:
             dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
         grads.put(conv.weight, dw, ready, side if ready is not None else None)
         return dx
-    split_ok = _precision == "f16x3" and c % 64 == 0 and k % 64 == 0
-    amax = ops.absmax(dy) if split_ok else None
+    # exact fp32 kernels (precision fp32, or shapes the x3 kernels do not take)
+    if x.dtype != torch.float32 or dy.dtype != torch.float32:
+        raise ops.HkpError("conv %s backward: the fp32 kernels need the fp32 activation and gradient"
+                           % (tuple(conv.weight.shape),))
     dx = None
     if need_dx:
-        if split_ok and st == 1:
-            hi, lo = _cached_split(conv.weight, "flip", ops.conv_weight_flip_split)
-            dx = ops.conv2d_bwd_data_split(dy, hi, lo, tuple(x.shape), pd, dl, add=add, amax=amax)
-        else:
-            wf = ops.conv_weight_flip(conv.weight)
-            dx = ops.conv2d_bwd_data(dy, wf, tuple(x.shape), st, pd, dl, add=add)
-    if split_ok:
-        dw = ops.conv2d_bwd_filter_split(x, dy, tuple(conv.weight.shape), st, pd, dl, amax=amax)
-    else:
-        dw = ops.conv2d_bwd_filter(x, dy, tuple(conv.weight.shape), st, pd, dl)
-    grads.put(conv.weight, dw)
+        wf = ops.conv_weight_flip(conv.weight)
+        dx = ops.conv2d_bwd_data(dy, wf, tuple(x.shape), st, pd, dl, add=add)
+    grads.put(conv.weight, ops.conv2d_bwd_filter(x, dy, tuple(conv.weight.shape), st, pd, dl))
     return dx
 
 
-def _bn_backward(bn, g, out_mask, y, mi, grads, want_dz=False, split_only=False, relu_ss=None):
-    dy, dgamma, dbeta, dz = ops.bn_bwd(g, out_mask, y, mi, bn.weight, want_dz=want_dz,
-                                       want_amax=_precision == "f16x3", split_only=split_only, relu_ss=relu_ss)
-    grads.put(bn.weight, dgamma)
-    grads.put(bn.bias, dbeta)
-    return dy, dz
+def _bn_bwd_begin(it, pol):
+    return ops.bn_bwd_begin(it["g"], it.get("out_mask"), it["y"], it["mi"], it["bn"].weight,
+                            want_dz=it.get("want_dz", False), want_amax=pol.precision == "f16x3",
+                            split_only=it.get("split_only", False), relu_ss=it.get("relu_ss"))
 
 
-def block_backward(block, rec, g_out, grads):
+def _bn_bwd_finish(states, items, grads, pol):
+    """Finish BN backwards whose reduce passes are launched (states): under SyncBN
+    their channel-sum blocks ride ONE all-gather.  → [(dy, dz)]."""
+    sync = parallel.active_sync_group(pol)
+    if sync is None:
+        res = [ops.bn_bwd_end(s) for s in states]
+    else:
+        own = [ops.bn_bwd_local_stats(s) for s in states]
+        st = parallel.gather_bn_stats(torch.cat(own), sync[0])
+        res, off = [], 0
+        for s, o in zip(states, own):
+            res.append(ops.bn_bwd_end(s, st[:, off:off + o.numel()], o))
+            off += o.numel()
+    out = []
+    for it, (dy, dgamma, dbeta, dz) in zip(items, res):
+        grads.put(it["bn"].weight, dgamma)
+        grads.put(it["bn"].bias, dbeta)
+        out.append((dy, dz))
+    return out
+
+
+def _bn_backward(bn, g, out_mask, y, mi, grads, pol, want_dz=False, split_only=False, relu_ss=None):
+    """Train-mode BN(+ReLU mask) backward of one layer → (dy, dz)."""
+    it = dict(bn=bn, g=g, out_mask=out_mask, y=y, mi=mi, want_dz=want_dz, split_only=split_only, relu_ss=relu_ss)
+    return _bn_bwd_finish([_bn_bwd_begin(it, pol)], [it], grads, pol)[0]
+
+
+def block_backward(block, rec, g_out, grads, pol=None):
     """Reverse of block_forward: g_out = dL/d(block output) → dL/d(block input)."""
+    pol = resolve(pol)
     out, x = rec["out"], rec["x"]
     ys, mis, acts = rec["y"], rec["mi"], rec["act"]
     bns = [block.bn1, block.bn2] + ([block.bn3] if block.kind == "bottleneck" else [])
     convs = [block.conv1, block.conv2] + ([block.conv3] if block.kind == "bottleneck" else [])
-    # last BN: relu mask from the block output; keep dz for the residual branch
-    # a BN backward whose dy only feeds an x3 conv writes it as that conv's split
+    # last BN: relu mask from the block output; keep dz for the residual branch.
+    # A BN backward whose dy only feeds an x3 conv writes it as that conv's split.
     ins = [x] + list(acts)                 # input of convs[i]
-    g, dz = _bn_backward(bns[-1], g_out, out, ys[-1], mis[-1], grads, want_dz=True,
-                         split_only=_x3_backward(convs[-1], ins[len(convs) - 1]))
+    last = dict(bn=bns[-1], g=g_out, out_mask=out, y=ys[-1], mi=mis[-1], want_dz=True,
+                split_only=_x3_backward(convs[-1], ins[len(convs) - 1], pol))
     if block.downsample is not None:
+        # the downsample BN's input gradient is the last BN's dz (the same ReLU
+        # mask): both reduces run, then both finish (one SyncBN gather)
         ds = block.downsample[0]
-        gd, _ = _bn_backward(block.downsample[1], dz, None, rec["yd"], rec["md"], grads,
-                             split_only=_x3_backward(ds, x))
-        dx_res = _conv_backward(ds, x, gd, grads)
+        st_last = _bn_bwd_begin(last, pol)
+        dsi = dict(bn=block.downsample[1], g=st_last["dz"], y=rec["yd"], mi=rec["md"],
+                   split_only=_x3_backward(ds, x, pol))
+        (g, _), (gd, _) = _bn_bwd_finish([st_last, _bn_bwd_begin(dsi, pol)], [last, dsi], grads, pol)
+        dx_res = _conv_backward(ds, x, gd, grads, pol)
     else:
-        dx_res = dz
+        g, dx_res = _bn_backward(last["bn"], g_out, out, ys[-1], mis[-1], grads, pol, want_dz=True,
+                                 split_only=last["split_only"])
     # main path, last conv first; an inner BN's ReLU mask is recomputed from its
     # y and forward scale/shift (bit-identical; the fp32 activation is not read)
     for li in range(len(convs) - 1, 0, -1):
-        da = _conv_backward(convs[li], acts[li - 1], g, grads)
-        if _MASK_FROM_Y:
-            g, _ = _bn_backward(bns[li - 1], da, None, ys[li - 1], mis[li - 1], grads,
-                                split_only=_x3_backward(convs[li - 1], ins[li - 1]), relu_ss=rec["ss"][li - 1])
+        da = _conv_backward(convs[li], acts[li - 1], g, grads, pol)
+        split_only = _x3_backward(convs[li - 1], ins[li - 1], pol)
+        if pol.mask_from_y:
+            g, _ = _bn_backward(bns[li - 1], da, None, ys[li - 1], mis[li - 1], grads, pol, split_only=split_only,
+                                relu_ss=rec["ss"][li - 1])
         else:
-            g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads,
-                                split_only=_x3_backward(convs[li - 1], ins[li - 1]))
-    return _conv_backward(convs[0], x, g, grads, add=dx_res)
+            g, _ = _bn_backward(bns[li - 1], da, acts[li - 1], ys[li - 1], mis[li - 1], grads, pol,
+                                split_only=split_only)
+    return _conv_backward(convs[0], x, g, grads, pol, add=dx_res)
 
 
-def stem_backward(resnet, st, g_pool, grads):
+def stem_backward(resnet, st, g_pool, grads, pol=None):
+    pol = resolve(pol)
     dz = ops.maxpool_bwd(g_pool, st["out"]._hkp_route, tuple(st["y"].shape))
-    dy, _ = _bn_backward(resnet.bn1, dz, None, st["y"], st["mi"], grads)
+    dy, _ = _bn_backward(resnet.bn1, dz, None, st["y"], st["mi"], grads, pol)
     c = resnet.conv1
     grads.put(c.weight, ops.conv2d_bwd_filter(st["x"], dy, tuple(c.weight.shape), _i(c.stride), _i(c.padding),
                                               _i(c.dilation), layout="nchw"))
 
 
 def keypoints_backward(resnet, trace, dheat, grads):
-    """dL/dheat → every parameter gradient (model.py:19-22 backward)."""
+    """dL/dheat → every parameter gradient (model.py:19-22 backward), under the
+    policy the forward ran with (trace.policy)."""
+    pol = trace.policy
     hd = trace.head
     k = hd["k"]
     feat, low = hd["feat"], hd["low"]
@@ -604,18 +654,17 @@ def keypoints_backward(resnet, trace, dheat, grads):
     grads.put(fcw, gw)
     grads.put(fcb, gb)
     g = dfeat
-    for rec, block in zip(reversed(trace.blocks), reversed([b for l in (resnet.layer1, resnet.layer2, resnet.layer3,
-                                                                           resnet.layer4) for b in l])):
-        g = block_backward(block, rec, g, grads)
-    stem_backward(resnet, trace.stem, g, grads)
+    for rec, block in zip(reversed(trace.blocks), reversed(_blocks(resnet))):
+        g = block_backward(block, rec, g, grads, pol)
+    stem_backward(resnet, trace.stem, g, grads, pol)
     grads.sync()
     return grads
 
 
-def logits_forward(resnet, x_nchw, num_outputs=None):
+def logits_forward(resnet, x_nchw, num_outputs=None, pol=None):
     """Resnet34_8s.forward (resnet_dilated.py:24-28): upsampled raw fc logits,
     [B, num_outputs (default 1000), H, W]; computed 16 channels at a time."""
-    feat = backbone_forward(resnet, x_nchw)
+    feat = backbone_forward(resnet, x_nchw, pol=pol)
     n_out = resnet.fc.weight.shape[0] if num_outputs is None else num_outputs
     W2 = resnet.fc.weight.reshape(resnet.fc.weight.shape[0], -1)
     outs = []

@@ -5,7 +5,6 @@ launch (a mis-shaped launch can fault the GPU), launches on PyTorch's current
 stream, and allocates outputs with the caching allocator.  No fallback path.
 """
 import ctypes
-import os
 
 import torch
 
@@ -109,15 +108,6 @@ def conv2d_fwd(x, w, stride=1, pad=0, dil=1, layout="nhwc", stats=True, out=None
         flops = 2.0 * n * ho * wo * k * r * s * c
         _observer(conv_kernel_symbol(layout, k), flops, 4.0 * (x.numel() + w.numel() + y.numel()), launch)
     return y, part
-
-
-def weight_split(w, passes=3):
-    """fp32 weight → (hi fp16, lo fp16 or None) for conv2d_fwd_split."""
-    _need(w, torch.float32, "weight_split.w")
-    hi = torch.empty(w.shape, device=w.device, dtype=torch.float16)
-    lo = torch.empty(w.shape, device=w.device, dtype=torch.float16) if passes == 3 else None
-    call("hkp_weight_split", w.numel(), _ptr(w), _ptr(hi), _ptr(lo), _stream())
-    return hi, lo
 
 
 class PackedWeight(tuple):
@@ -347,59 +337,17 @@ def soft_argmax(heat, beta=1.0):
     return out
 
 
-def conv2d_fwd_split(x, w_hi, w_lo, passes=3, stride=1, pad=0, dil=1, stats=True, out=None, x_hi=None):
-    """Split-precision (f16x3, passes=3) or plain fp16 (passes=1) NHWC conv; fp32 in/out,
-    the activation split inside the conv loop.  x_hi (passes 1): the input's pre-converted
-    fp16 plane (x may then be None)."""
-    if x_hi is not None:
-        if passes != 1:
-            raise HkpError("conv2d_fwd_split: x_hi is for passes 1 (passes 3: conv2d_fwd_x3)")
-        _need(x_hi, torch.float16, "conv2d_fwd_split.x_hi", 4)
-        if x is not None and x_hi.shape != x.shape:
-            raise HkpError("conv2d_fwd_split: x_hi does not match x")
-    else:
-        _need(x, torch.float32, "conv2d_fwd_split.x", 4)
-    xt = x if x is not None else x_hi
-    _need(w_hi, torch.float16, "conv2d_fwd_split.w_hi", 4)
-    if passes == 3:
-        _need(w_lo, torch.float16, "conv2d_fwd_split.w_lo", 4)
-    n, h, wd, c = xt.shape
-    k, r, s, cw = w_hi.shape
-    if cw != c:
-        raise HkpError("conv2d_fwd_split: weight Cin %d != input C %d" % (cw, c))
-    ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
-    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC)
-    y = out if out is not None else torch.empty((n, ho, wo, k), device=xt.device, dtype=torch.float32)
-    part = None
-    if stats:
-        tiles = (n * ho * wo + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
-        part = torch.empty((tiles, k, 2), device=xt.device, dtype=torch.float32)
-
-    def launch():
-        call("hkp_conv2d_fwd_split", ctypes.byref(d), _ptr(x), _ptr(x_hi), _ptr(w_hi), _ptr(w_lo), int(passes),
-             _ptr(y), _ptr(part), _stream())
-
-    if _observer is None:
-        launch()
-    else:
-        bn = 128 if k % 128 == 0 else 64
-        _observer("conv_split_kernel<128, %d, %d, %s>" % (bn, passes, "true" if x_hi is not None else "false"),
-                  2.0 * n * ho * wo * k * r * s * c,
-                  4.0 * (xt.numel() + w_hi.numel() + y.numel()), launch)
-    return y, part
-
-
 # two-level finalize (hkp_bn_finalize_ws) from this many partial tiles on: C4 +2.2 %
 # (R50 C = 2048 convs, 4,800+ tiles); at 300-1,200 tiles (C2 layer2-4, the C3
 # shard) the one-kernel merge already fills the chip and its single launch won
 # (C2 neutral, C3 training -1.2 % with the two-level form everywhere)
 FIN_TWO_LEVEL_TILES = 2048
-_FIN_ONE_KERNEL = os.environ.get("HKP_FIN_ONE_KERNEL") == "1"     # A/B: always the one-kernel merge
 
 
 def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None,
-                momentum=0.1, eps=1e-5, want_mean_invstd=True):
-    """Train-mode BN statistics from conv partials → (scale_shift [2C], mean_invstd [2C])."""
+                momentum=0.1, eps=1e-5, want_mean_invstd=True, two_level_tiles=FIN_TWO_LEVEL_TILES):
+    """Train-mode BN statistics from conv partials → (scale_shift [2C], mean_invstd [2C]).
+    Lists of >= two_level_tiles tiles take the two-level merge (hkp_bn_finalize_ws)."""
     _need(part, torch.float32, "bn_finalize.partials", 3)
     tiles, c, _ = part.shape
     ss = torch.empty(2 * c, device=part.device, dtype=torch.float32)
@@ -411,7 +359,7 @@ def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, n
                 raise HkpError("bn_finalize.%s: %d != C=%d" % (nm, t.numel(), c))
     if num_batches_tracked is not None:
         _need(num_batches_tracked, torch.int64, "bn_finalize.num_batches_tracked")
-    if tiles >= FIN_TWO_LEVEL_TILES and not _FIN_ONE_KERNEL:
+    if tiles >= two_level_tiles:
         # two-level merge (chunks of 128 tiles over [C/64][chunks] blocks, then per channel)
         from ._lib import lib
         nb = lib().hkp_bn_finalize_workspace_bytes(c, tiles)
@@ -425,7 +373,7 @@ def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, n
     return ss, mi
 
 
-def bn_stats(part, count):
+def bn_stats(part, count, two_level_tiles=FIN_TWO_LEVEL_TILES):
     """SyncBN: this rank's per-channel BN statistics from its conv tile partials →
     fp64 [2C+1] = [mean | M2 | count] (hkp_bn_stats; gathered in rank order and
     merged by bn_finalize_ranks)."""
@@ -433,7 +381,7 @@ def bn_stats(part, count):
     tiles, c, _ = part.shape
     st = torch.empty(2 * c + 1, device=part.device, dtype=torch.float64)
     ws, nb = None, 0
-    if tiles >= FIN_TWO_LEVEL_TILES and not _FIN_ONE_KERNEL:
+    if tiles >= two_level_tiles:
         from ._lib import lib
         nb = lib().hkp_bn_finalize_workspace_bytes(c, tiles)
         ws = torch.empty((nb + 7) // 8, device=part.device, dtype=torch.float64)
@@ -711,54 +659,6 @@ def absmax(x):
     return out
 
 
-def conv_weight_flip_split(w):
-    """KRSC [K,R,S,C] fp32 → flipped CRSK (hi, lo) fp16 for conv2d_bwd_data_split."""
-    _need(w, torch.float32, "conv_weight_flip_split.w", 4)
-    k, r, s, c = w.shape
-    d = ConvDesc(1, 1, 1, c, k, r, s, 1, 0, 1, HKP_LAYOUT_NHWC)
-    hi = torch.empty((c, r, s, k), device=w.device, dtype=torch.float16)
-    lo = torch.empty((c, r, s, k), device=w.device, dtype=torch.float16)
-    call("hkp_conv_weight_flip_split", ctypes.byref(d), _ptr(w), _ptr(hi), _ptr(lo), _stream())
-    return hi, lo
-
-
-def conv2d_bwd_data_split(dy, wf_hi, wf_lo, x_shape, pad=0, dil=1, add=None, amax=None):
-    """f16x3 dL/dx of a stride-1 NHWC conv; dy scaled by a power of two from amax."""
-    _need(dy, torch.float32, "conv2d_bwd_data_split.dy", 4)
-    _need(wf_hi, torch.float16, "conv2d_bwd_data_split.wf_hi", 4)
-    _need(wf_lo, torch.float16, "conv2d_bwd_data_split.wf_lo", 4)
-    c, r, s, k = wf_hi.shape
-    d = _fwd_desc(x_shape, (k, r, s, c), 1, pad, dil, "nhwc")
-    ho, wo = conv_out_hw(x_shape[1], x_shape[2], r, s, 1, pad, dil)
-    if tuple(dy.shape) != (x_shape[0], ho, wo, k):
-        raise HkpError("conv2d_bwd_data_split: dy shape %s != %s" % (tuple(dy.shape), (x_shape[0], ho, wo, k)))
-    if add is not None:
-        _need(add, torch.float32, "conv2d_bwd_data_split.add", 4)
-        if tuple(add.shape) != tuple(x_shape):
-            raise HkpError("conv2d_bwd_data_split: add shape mismatch")
-    dx = torch.empty(tuple(x_shape), device=dy.device, dtype=torch.float32)
-    call("hkp_conv2d_bwd_data_split", ctypes.byref(d), _ptr(dy), _ptr(wf_hi), _ptr(wf_lo), _ptr(amax), _ptr(add),
-         _ptr(dx), _stream())
-    return dx
-
-
-def conv2d_bwd_filter_split(x, dy, w_shape, stride=1, pad=0, dil=1, amax=None):
-    """f16x3 dL/dw (KRSC) of an NHWC conv; dy scaled by a power of two from amax."""
-    from ._lib import lib
-    _need(x, torch.float32, "conv2d_bwd_filter_split.x", 4)
-    _need(dy, torch.float32, "conv2d_bwd_filter_split.dy", 4)
-    d = _fwd_desc(tuple(x.shape), tuple(w_shape), stride, pad, dil, "nhwc")
-    ho, wo = conv_out_hw(d.h, d.w, d.r, d.s, stride, pad, dil)
-    if tuple(dy.shape) != (d.n, ho, wo, d.k):
-        raise HkpError("conv2d_bwd_filter_split: dy shape %s != %s" % (tuple(dy.shape), (d.n, ho, wo, d.k)))
-    nbytes = lib().hkp_conv_bwd_filter_split_workspace(ctypes.byref(d))
-    ws = torch.empty(max(nbytes, 4) // 4, device=x.device, dtype=torch.float32)
-    dw = torch.empty(tuple(w_shape), device=x.device, dtype=torch.float32)
-    call("hkp_conv2d_bwd_filter_split", ctypes.byref(d), _ptr(x), _ptr(dy), _ptr(amax), _ptr(dw), _ptr(ws), nbytes,
-         _stream())
-    return dw
-
-
 def split_pack_x3(x, amax=None):
     """fp32 NHWC x (scaled by the power of two of amax, if given) → packed split [.., 2C]."""
     _need(x, torch.float32, "split_pack_x3.x")
@@ -971,15 +871,11 @@ def conv2d_bwd_filter(x, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out
     return dw
 
 
-def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, split_only=False, relu_ss=None):
-    """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None).
-    The ReLU mask is out_mask > 0, or (relu_ss = the forward's scale_shift) is
-    recomputed from y bit-identically — no read of the fp32 activation.
-    want_amax: max|dy| (uint32 IEEE bits, as absmax) is computed in the same pass
-    and attached as dy._hkp_amax.  split_only: dy is returned as the packed f16x3
-    split of dy * 2^e (the x3 backward convs' operand, _hkp_split_passes = 3) with
-    2^e from an upper bound of max|dy| (attached as _hkp_amax, the scale's source);
-    no fp32 dy is written."""
+def bn_bwd_begin(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, split_only=False,
+                 relu_ss=None):
+    """First half of bn_bwd: validates and launches the reduce pass (per-tile
+    channel sums; dz = g*mask when want_dz).  Returns the state bn_bwd_end /
+    bn_bwd_local_stats take; state["dz"] is dz (written once the pass runs)."""
     _need(g, torch.float32, "bn_bwd.g")
     _need(y, torch.float32, "bn_bwd.y")
     if g.shape != y.shape or (out_mask is not None and out_mask.shape != y.shape):
@@ -1002,31 +898,67 @@ def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, s
     dz = torch.empty_like(y) if want_dz else None
     call("hkp_bn_bwd_reduce", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd), _ptr(dz),
          _ptr(part), _ptr(maxima), _ptr(amax if split_only else None), _stream())
+    return dict(g=g, out_mask=out_mask, y=y, mi=mean_invstd, gamma=gamma, relu_ss=relu_ss, m=m, c=c, part=part,
+                maxima=maxima, amax=amax, dz=dz, split_only=split_only, want_amax=want_amax)
+
+
+def bn_bwd_local_stats(st):
+    """SyncBN: this rank's [Σdz | Σdz·(y−mean) | max|dz| | max|y−mean| | m] fp64
+    block (hkp_bn_bwd_stats) of a begun BN backward, to be all-gathered."""
+    own = torch.empty(4 * st["c"] + 1, device=st["y"].device, dtype=torch.float64)
+    call("hkp_bn_bwd_stats", st["c"], st["m"], _ptr(st["part"]), _ptr(st["maxima"]), _ptr(st["mi"]), _ptr(own),
+         _stream())
+    return own
+
+
+def bn_bwd_end(st, ranks=None, own=None):
+    """Second half of bn_bwd: coefficients (from this rank's sums, or — SyncBN —
+    from `ranks` [R, 4C+1], every rank's bn_bwd_local_stats block in rank order,
+    with `own` this rank's) and the apply pass → (dy, dgamma, dbeta, dz)."""
+    y, c, m = st["y"], st["c"], st["m"]
     dgamma = torch.empty(c, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(c, device=y.device, dtype=torch.float32)
     coef = torch.empty(3 * c, device=y.device, dtype=torch.float32)
-    from . import parallel
-    sync = parallel.sync_bn_group()
-    if sync is None:
-        call("hkp_bn_bwd_finalize", c, m, _ptr(part), _ptr(maxima), _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma),
-             _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
-    else:                                          # SyncBN: sums over every rank's shard
-        own = torch.empty(4 * c + 1, device=y.device, dtype=torch.float64)
-        call("hkp_bn_bwd_stats", c, m, _ptr(part), _ptr(maxima), _ptr(mean_invstd), _ptr(own), _stream())
-        st = parallel.gather_bn_stats(own, sync[0])
-        call("hkp_bn_bwd_finalize_ranks", c, st.shape[0], _ptr(st), _ptr(own), 1 if maxima is not None else 0,
-             _ptr(mean_invstd), _ptr(gamma), _ptr(dgamma), _ptr(dbeta), _ptr(coef), _ptr(amax), _stream())
-    if split_only:
+    if ranks is None:
+        call("hkp_bn_bwd_finalize", c, m, _ptr(st["part"]), _ptr(st["maxima"]), _ptr(st["mi"]), _ptr(st["gamma"]),
+             _ptr(dgamma), _ptr(dbeta), _ptr(coef), _ptr(st["amax"]), _stream())
+    else:
+        _need(ranks, torch.float64, "bn_bwd_end.ranks")
+        if ranks.dim() != 2 or ranks.shape[1] != 4 * c + 1 or own is None or own.numel() != 4 * c + 1:
+            raise HkpError("bn_bwd_end: rank statistics must be [R, 4C+1] with this rank's block")
+        call("hkp_bn_bwd_finalize_ranks", c, ranks.shape[0], _ptr(ranks.contiguous()), _ptr(own),
+             1 if st["maxima"] is not None else 0, _ptr(st["mi"]), _ptr(st["gamma"]), _ptr(dgamma), _ptr(dbeta),
+             _ptr(coef), _ptr(st["amax"]), _stream())
+    if st["split_only"]:
         dy = _split_out(y.shape, y.device, 3)
-        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd),
-             _ptr(coef), None, _ptr(amax), _ptr(dy), _stream())
+        call("hkp_bn_bwd_apply", m, c, _ptr(st["g"]), _ptr(st["out_mask"]), _ptr(st["relu_ss"]), _ptr(y),
+             _ptr(st["mi"]), _ptr(coef), None, _ptr(st["amax"]), _ptr(dy), _stream())
     else:
         dy = torch.empty_like(y)
-        call("hkp_bn_bwd_apply", m, c, _ptr(g), _ptr(out_mask), _ptr(relu_ss), _ptr(y), _ptr(mean_invstd),
-             _ptr(coef), _ptr(dy), _ptr(amax), None, _stream())
-    if want_amax or split_only:
-        dy._hkp_amax = amax
-    return dy, dgamma, dbeta, dz
+        call("hkp_bn_bwd_apply", m, c, _ptr(st["g"]), _ptr(st["out_mask"]), _ptr(st["relu_ss"]), _ptr(y),
+             _ptr(st["mi"]), _ptr(coef), _ptr(dy), _ptr(st["amax"]), None, _stream())
+    if st["want_amax"] or st["split_only"]:
+        dy._hkp_amax = st["amax"]
+    return dy, dgamma, dbeta, st["dz"]
+
+
+def bn_bwd(g, out_mask, y, mean_invstd, gamma, want_dz=False, want_amax=False, split_only=False, relu_ss=None,
+           sync_group=None):
+    """Train-mode BN(+ReLU mask) backward → (dy, dgamma, dbeta, dz or None).
+    The ReLU mask is out_mask > 0, or (relu_ss = the forward's scale_shift) is
+    recomputed from y bit-identically — no read of the fp32 activation.
+    want_amax: max|dy| (uint32 IEEE bits, as absmax) is computed in the same pass
+    and attached as dy._hkp_amax.  split_only: dy is returned as the packed f16x3
+    split of dy * 2^e (the x3 backward convs' operand, _hkp_split_passes = 3) with
+    2^e from an upper bound of max|dy| (attached as _hkp_amax, the scale's source);
+    no fp32 dy is written.  sync_group = (group,): SyncBN — the dx coefficients
+    from the channel sums of every rank of group (hkp.parallel.active_sync_group)."""
+    st = bn_bwd_begin(g, out_mask, y, mean_invstd, gamma, want_dz, want_amax, split_only, relu_ss)
+    if sync_group is None:
+        return bn_bwd_end(st)
+    from . import parallel
+    own = bn_bwd_local_stats(st)
+    return bn_bwd_end(st, parallel.gather_bn_stats(own, sync_group[0]), own)
 
 
 def maxpool_bwd(dpool, route, in_shape):

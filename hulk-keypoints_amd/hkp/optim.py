@@ -11,13 +11,10 @@ parameters must be fp32 CUDA tensors.
 """
 import ctypes
 import math
-import os
 
 import torch
 
 from ._lib import AdamTensor, HkpError, call
-
-_NO_FAST = os.environ.get("HKP_ADAM_NO_FAST") == "1"      # A/B: always the slow path
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -49,7 +46,7 @@ class FusedAdam(torch.optim.Optimizer):
     def _fast_step(self, gi, group):
         """One launch from the cached table, or False (cache miss: slow path)."""
         fc = self._fast.get(gi)
-        if fc is None or _NO_FAST:
+        if fc is None:
             return False
         ps = [p for p in group["params"] if p.grad is not None]
         if len(ps) != len(fc["ps"]) or any(a is not b for a, b in zip(ps, fc["ps"])):

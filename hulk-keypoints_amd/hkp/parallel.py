@@ -1,16 +1,15 @@
-"""Data-parallel inference over the GPUs of a node.
+"""Data parallelism over the GPUs of a node: sharded inference
+and SyncBN (training's gradient all-reduce is hkp.train.GradBucketer).
 
 Inference shards by image: every rank runs the fused forward + argmax on its
 own slice of the batch (no collective on the data path; train-mode BN
 statistics are per shard, exactly as a per-shard run of the reference's
-analysis.py would compute them), then the int32 [b, K, 2] (y, x)
+analysis.py would compute them, SURVEY D5 — unless SyncBN is on), then the int32 [b, K, 2] (y, x)
 keypoints — 8 bytes per keypoint — are all-gathered so every rank (and in
 particular rank 0, which writes results) holds the global [B, K, 2] in rank
 order.  One process per GPU, torch.distributed "nccl" = RCCL over xGMI (gloo
 for the CPU tests).
 """
-from contextlib import nullcontext as _nullcontext
-
 import torch
 import torch.distributed as dist
 
@@ -67,66 +66,63 @@ def gather_keypoints_fixed(yx, out=None, group=None):
     return out
 
 
+def check_shards(n_local, group=None):
+    """Every rank holds at least one image (min over ranks, one tiny collective).
+    A SyncBN forward or backward with an empty shard would leave the other ranks
+    waiting in their statistics gathers forever, so every rank raises instead."""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    t = torch.tensor([int(n_local)], device=dev, dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    if int(t.item()) < 1:
+        raise ValueError("SyncBN needs at least one image on every rank (global batch < world size %d)"
+                         % dist.get_world_size(group))
+
+
 @torch.no_grad()
-def predict_keypoints_dp(model, x_shard, heat=False, sync=False):
+def predict_keypoints_dp(model, x_shard, heat=False, sync=False, group=None):
     """Each rank's shard through the fused forward (+ argmax); keypoints gathered.
-    sync: BN statistics over the whole sharded batch (SyncBN, below) — the
-    result then equals one forward over the global batch.
+    sync: BN statistics over the whole sharded batch of `group` (SyncBN, below) —
+    the result then equals one forward over the global batch.
     Returns (global int32 [B, K, 2], this rank's heatmaps or None)."""
-    with (sync_bn() if sync else _nullcontext()):
-        if heat:
-            hm, yx = model.heatmaps_and_keypoints(x_shard)
-        else:
-            hm, yx = None, model.predict_keypoints(x_shard)
-    return gather_keypoints(yx), hm
+    pol = model.policy.with_(sync_bn=True, sync_group=group) if sync else model.policy
+    if sync:
+        check_shards(x_shard.shape[0], group)
+    if heat:
+        hm, yx = model.heatmaps_and_keypoints(x_shard, policy=pol)
+    else:
+        hm, yx = None, model.predict_keypoints(x_shard, policy=pol)
+    return gather_keypoints(yx, group), hm
 
 
 # ---- SyncBN (SURVEY §8(e), caveat D5) ----------------------------------------
-# Off by default: per-rank BN statistics (standard DDP semantics, as above).  On:
+# Off by default: per-rank BN statistics (standard DDP semantics, as above).  On
+# (Policy(sync_bn=True, sync_group=...), carried by the model or the Trainer):
 # every train-mode BN layer's batch statistics are taken over the whole sharded
 # batch — each rank's [mean | M2 | count] block (hkp_bn_stats, fp64) is
 # all-gathered in rank order and merged in fixed order (hkp_bn_finalize_ranks),
-# so every rank applies the same scale/shift and a DP inference over N ranks
-# gives the outputs of one forward over the global batch (torch SyncBatchNorm's
-# forward).  One all_gather of 2C+1 doubles per BN layer (36 for R34).
-# Inference only: the BN backward uses per-rank sums (training keeps DDP BN).
-_sync_bn = None          # None: off; else (group,)
+# so every rank applies the same scale/shift and a DP forward over N ranks gives
+# the outputs of one forward over the global batch (torch SyncBatchNorm's
+# forward).  In training the BN backward's channel sums are gathered the same
+# way (hkp_bn_bwd_stats / hkp_bn_bwd_finalize_ranks: torch SyncBatchNorm's
+# all-reduced sum_dy / sum_dy_xmu), so a step equals one step over the global
+# batch.  A block's downsample BN and its last BN share one gather in each
+# direction (hkp.net); DESIGN.md gives the per-step count.
 
 
-def set_sync_bn(enabled=True, group=None):
-    """Turn cross-rank BN statistics on (over `group`, default the world) or off."""
-    global _sync_bn
-    _sync_bn = (group,) if enabled else None
-
-
-def sync_bn_group():
-    """(group,) while SyncBN is on and more than one rank takes part, else None."""
-    if _sync_bn is None or not dist.is_initialized() or dist.get_world_size(_sync_bn[0]) == 1:
+def active_sync_group(policy):
+    """(group,) while `policy` synchronises BN and more than one rank takes part,
+    else None."""
+    if policy is None or not policy.sync_bn or not dist.is_initialized() \
+            or dist.get_world_size(policy.sync_group) == 1:
         return None
-    return _sync_bn
-
-
-class sync_bn:
-    """Context manager: SyncBN on inside the block, the previous setting after it."""
-
-    def __init__(self, group=None):
-        self.group = group
-
-    def __enter__(self):
-        global _sync_bn
-        self.prev = _sync_bn
-        _sync_bn = (self.group,)
-        return self
-
-    def __exit__(self, *exc):
-        global _sync_bn
-        _sync_bn = self.prev
-        return False
+    return (policy.sync_group,)
 
 
 def gather_bn_stats(st, group=None):
-    """all_gather of each rank's fp64 [2C+1] statistics block → [world, 2C+1] in
-    rank order.  RCCL gathers on the device; other backends (gloo) through host
+    """all_gather of each rank's fp64 statistics block ([2C+1] forward, [4C+1]
+    backward, or several blocks concatenated) → [world, len] in rank order.  RCCL gathers on the device; other backends (gloo) through host
     copies (the blocks are a few KB)."""
     n = dist.get_world_size(group) if dist.is_initialized() else 1
     if n == 1:

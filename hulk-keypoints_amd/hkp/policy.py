@@ -1,0 +1,64 @@
+"""Execution policy of one network: the arithmetic its convs use, whether its
+BN statistics are synchronised across ranks, and the measured tuning choices of
+the kernel walk.  A policy is an immutable value carried by the model
+(``KeypointsGauss.policy``) or passed explicitly to ``hkp.net`` — the product
+keeps no process-global switches and reads no environment variables, so two
+models (or two threads) with different policies never interfere.
+
+Tuning fields hold the measured defaults; A/B tooling builds
+non-default policies explicitly (``tools/knobs.py``, ``bench.py --tune``).
+"""
+from dataclasses import dataclass, fields, replace
+
+# Conv arithmetic of the NHWC convs and the stem:
+#   "fp32"  v_mfma_f32_32x32x2_f32, exact fp32 products
+#   "f16x3" split-precision fp16 MFMA, fp32-accurate (~2^-22 per product)
+#   "f16"   plain fp16 operands and activations, fp32 accumulation (BASELINE
+#           config C4, inference): one fp16 MFMA per MAC, fp16 conv outputs and
+#           residual stream (autocast semantics)
+PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
+
+
+@dataclass(frozen=True)
+class Policy:
+    precision: str = "f16x3"
+    # SyncBN (caveat D5): train-mode BN statistics and their backward
+    # sums over every rank of `sync_group` (None = the default world group)
+    sync_bn: bool = False
+    sync_group: object = None
+    # --- tuning (measured defaults) ----------------------------------------
+    # a conv's wgrad runs on a side stream concurrently with its dgrad
+    overlap_wgrad: bool = True
+    # HKP_TILE_* of a dgrad overlapped by its wgrad (9 = 256x256 + split-K tail)
+    dgrad_overlap_tile: int = 9
+    # inner BN ReLU masks recomputed from y in the backward (no fp32 activation kept)
+    mask_from_y: bool = True
+    # inference: last block's BN apply fused with the K-row head
+    fused_head: bool = True
+    # HKP_TILE_* of the plain-fp16 1x1 / kxk convs (0 = the planner)
+    f16_tile_1x1: int = 0
+    f16_tile_kxk: int = 0
+    # training: repeat the last batched weight-pack launch when it repacks every operand
+    prepack_plan: bool = True
+    # BN finalize: two-level merge from this many partial tiles on
+    fin_two_level_tiles: int = 2048
+
+    def __post_init__(self):
+        if self.precision not in PRECISIONS:
+            raise ValueError("precision must be one of %s, got %r" % (sorted(PRECISIONS), self.precision))
+
+    @property
+    def passes(self):
+        return PRECISIONS[self.precision]
+
+    def with_(self, **kw):
+        return replace(self, **kw)
+
+
+DEFAULT = Policy()
+
+TUNING_FIELDS = tuple(f.name for f in fields(Policy) if f.name not in ("precision", "sync_bn", "sync_group"))
+
+
+def resolve(policy):
+    return DEFAULT if policy is None else policy

@@ -14,12 +14,11 @@ complete its all-reduce is launched asynchronously, so communication of the
 late layers overlaps the backward of the early ones.  BatchNorm statistics
 stay per rank (standard DDP semantics) unless Trainer(sync_bn=True): then the
 BN statistics and the BN backward sums are taken over every rank's shard
-(hkp.parallel.sync_bn), and a step equals one step over the global batch.
+(Policy(sync_bn=True), hkp.parallel), and a step equals one step over the
+global batch.
 Parameters and buffers are broadcast from rank 0 when the Trainer is built
 (broadcast_state).
 """
-import os
-
 import torch
 import torch.distributed as dist
 
@@ -128,11 +127,15 @@ class Trainer:
     """One optimizer step per call, reference semantics (train.py:33-36)."""
 
     def __init__(self, model, lr=1e-4, weight_decay=1e-4, loss="bce", sigma=8.0, distributed=False,
-                 bucket_mb=32, optimizer="fused", sync_bn=False):
-        """sync_bn: BN statistics and their backward sums over every rank's shard
-        (hkp.parallel.sync_bn; the step then equals one step over the global
-        batch), instead of per-rank BN (DDP semantics, the default)."""
+                 bucket_mb=32, optimizer="fused", sync_bn=False, group=None, force_buckets=False):
+        """sync_bn: BN statistics and their backward sums over every rank of
+        `group` (default: the world; the step then equals one step over the
+        global batch), instead of per-rank BN (DDP semantics, the default).
+        force_buckets: the DP gradient path (bucket copies, stream joins) at world
+        size 1, to time its overhead on one GPU."""
         self.model = model
+        self.group = group
+        self.policy = model.policy.with_(sync_bn=True, sync_group=group) if sync_bn else model.policy
         self.sync_bn = sync_bn
         self.params = list(model.parameters())
         self.loss_kind = loss
@@ -141,23 +144,17 @@ class Trainer:
             raise ValueError("optimizer must be 'fused' or 'torch'")
         opt_cls = FusedAdam if optimizer == "fused" else torch.optim.Adam
         self.opt = opt_cls(self.params, lr=lr, weight_decay=weight_decay)
-        use_dp = distributed and dist.is_initialized() and dist.get_world_size() > 1
-        # HKP_FORCE_BUCKETS=1: the DP gradient path (bucket copies, stream joins) at
-        # world size 1, to time its overhead on one GPU
+        use_dp = distributed and dist.is_initialized() and dist.get_world_size(group) > 1
         if use_dp:
-            broadcast_state(model)          # every replica starts from rank 0's weights and BN buffers
-        use_dp = use_dp or os.environ.get("HKP_FORCE_BUCKETS") == "1"
-        self.bucketer = GradBucketer(self.params, bucket_mb << 20) if use_dp else None
+            broadcast_state(model, group=group)   # every replica starts from rank 0's weights and BN buffers
+        self.bucketer = GradBucketer(self.params, bucket_mb << 20, group=group) if (use_dp or force_buckets) \
+            else None
 
     def forward_backward(self, x, uv=None, target=None):
         if self.sync_bn:
-            with parallel.sync_bn():
-                return self._forward_backward(x, uv, target)
-        return self._forward_backward(x, uv, target)
-
-    def _forward_backward(self, x, uv=None, target=None):
+            parallel.check_shards(x.shape[0], self.group)
         m = self.model
-        trace = net.Trace()
+        trace = net.Trace(self.policy)
         hm, _, _ = net.keypoints_forward(m.resnet.net, x, m.num_keypoints, heat=True, trace=trace)
         loss, dheat = ops.heat_loss(hm, target, uv, self.sigma, self.loss_kind, want_grad=True)
         grads = net.Grads(on_ready=self.bucketer.ready if self.bucketer else None)

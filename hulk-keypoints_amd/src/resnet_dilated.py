@@ -5,12 +5,20 @@ state_dict prefix (``resnet.resnet34_8s.*`` for the default backbone)."""
 import torch.nn as nn
 
 from hkp import net
+from hkp.policy import DEFAULT, Policy
 from src import resnet as _resnet
 
 
 class ResnetDilated8s(nn.Module):
-    def __init__(self, backbone="resnet34", num_classes=1000, pretrained=True):
+    """``policy`` (hkp.policy.Policy): how the kernels compute this network —
+    conv arithmetic (default f16x3), SyncBN group, tuning; a plain attribute, so
+    two models with different policies coexist."""
+
+    def __init__(self, backbone="resnet34", num_classes=1000, pretrained=True, policy=None):
         super().__init__()
+        self.policy = DEFAULT if policy is None else policy
+        if not isinstance(self.policy, Policy):
+            raise TypeError("policy must be an hkp.policy.Policy")
         # load (local) pretrained weights, remove avg pool, output stride 8 (resnet_dilated.py:8-13)
         model = getattr(_resnet, backbone)(fully_conv=True, pretrained=pretrained, output_stride=8,
                                            remove_avg_pool_layer=True)
@@ -30,7 +38,7 @@ class ResnetDilated8s(nn.Module):
 
     def forward(self, x):
         """Upsampled raw logits [B,1000,H,W] (resnet_dilated.py:24-28)."""
-        return net.logits_forward(self.net, x)
+        return net.logits_forward(self.net, x, pol=self.policy)
 
 
 class Resnet34_8s(ResnetDilated8s):

@@ -8,8 +8,10 @@ pred.double(), train.py:21,25).
 
 Data parallel: launch with ``torchrun --nproc-per-node N train.py``; each rank
 takes a DistributedSampler shard, gradients are all-reduced over RCCL in
-buckets overlapped with the backward kernels (hkp.train.GradBucketer), rank 0
-prints and checkpoints.
+buckets overlapped with the backward kernels: the model's grad_ready hook hands
+each gradient to hkp.train.GradBucketer as the backward produces it inside
+loss.backward(), a full bucket's all-reduce starts right away, and
+_reduce_grads only waits for the last ones.  Rank 0 prints and checkpoints.
 """
 import os
 import sys
@@ -45,11 +47,23 @@ def forward(sample_batched, model):
 
 
 def _reduce_grads(model):
+    """After loss.backward(): wait for the bucket all-reduces the backward already
+    launched (model.grad_ready = GradBucketer.ready) and point p.grad at the
+    averaged buckets."""
     if _bucketer is None:
         return
-    for p in model.parameters():
-        _bucketer.ready(p, p.grad)
     _bucketer.finish()
+
+
+def setup_data_parallel(model, bucket_mb=32):
+    """DP wiring (torchrun): every rank starts from rank 0's parameters and BN
+    buffers, and the backward hands each gradient to the bucketer as soon as it
+    exists (model.grad_ready), so bucket all-reduces overlap the backward."""
+    global _bucketer
+    broadcast_state(model)
+    _bucketer = GradBucketer(list(model.parameters()), bucket_mb << 20)
+    model.grad_ready = _bucketer.ready
+    return _bucketer
 
 
 def fit(train_data, test_data, model, epochs, checkpoint_path=""):
@@ -82,7 +96,7 @@ def fit(train_data, test_data, model, epochs, checkpoint_path=""):
 
 
 def main(dataset_dir="", output_dir="checkpoints", workers=0):
-    global optimizer, keypoints, _bucketer
+    global optimizer, keypoints
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -106,8 +120,7 @@ def main(dataset_dir="", output_dir="checkpoints", workers=0):
     keypoints = KeypointsGauss(NUM_KEYPOINTS, img_height=IMG_HEIGHT, img_width=IMG_WIDTH, backbone=BACKBONE).cuda()
     optimizer = torch.optim.Adam(keypoints.parameters(), lr=1.0e-4, weight_decay=1.0e-4)   # train.py:79
     if world > 1:
-        broadcast_state(keypoints)            # identical start on every rank (parameters + BN buffers)
-        _bucketer = GradBucketer(list(keypoints.parameters()))
+        setup_data_parallel(keypoints)
     fit(train_data, test_data, keypoints, epochs=epochs, checkpoint_path=save_dir)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -92,21 +92,6 @@ int64_t hkp_conv_stat_tiles(const hkp_conv_desc* d);
 int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const float* w, float* y,
                    float* stat_partials, hkp_stream_t stream);
 
-/* Split-precision forward on fp16 MFMA (v_mfma_f32_32x32x16_f16), same conv and
- * epilogue as hkp_conv2d_fwd, NHWC only.
- *   passes = 3: fp32-accurate "f16x3" — operands split hi = f16(x),
- *               lo = f16((x-hi)*2^11); hi*hi + 2^-11*(hi*lo + lo*hi) in fp32
- *               accumulators (~2^-22 relative per product); needs w_lo.
- *   passes = 1: plain fp16 operands, fp32 accumulation (BASELINE config C4).
- * w_hi / w_lo: the KRSC weight split by hkp_weight_split (fp16 bit patterns).
- * x_hi (passes = 1 only), if given, is the input's pre-converted fp16 plane
- * (from hkp_bn_apply / hkp_bn_relu_maxpool with split_passes = 1) and x may be NULL.
- * Operands must be finite and |x| < 65504. */
-int hkp_weight_split(int64_t n, const float* w, uint16_t* w_hi, uint16_t* w_lo, hkp_stream_t stream);
-int hkp_conv2d_fwd_split(const hkp_conv_desc* d, const float* x, const uint16_t* x_hi,
-                         const uint16_t* w_hi, const uint16_t* w_lo, int32_t passes, float* y,
-                         float* stat_partials, hkp_stream_t stream);
-
 /* The f16x3 conv of the main path (same conv and epilogue as hkp_conv2d_fwd;
  * fp32-class accuracy) on operands pre-split into the "packed split" layout:
  * per pixel (weights: per output channel and filter tap) and per 32-channel
@@ -223,7 +208,7 @@ int hkp_bn_eval_params(int32_t c, const float* gamma, const float* beta, const f
  * fp16 pair with a 22-bit significand instead of fp32).
  * out_split (nullable; needs c % 32 == 0): the same values also written as the
  * next conv's operand — split_passes = 1: fp16 plane [m][c] for
- * hkp_conv2d_fwd_split (passes 1); split_passes = 3: the packed split layout
+ * hkp_conv2d_fwd_f16; split_passes = 3: the packed split layout
  * [m][c/32][hi32|lo32] (hi = f16(out), lo = f16(out-hi)) for
  * hkp_conv2d_fwd_x3.  out may be NULL when out_split is given (an activation
  * only a conv consumes).  hkp_bn_relu_maxpool takes the same optional split. */
@@ -318,25 +303,11 @@ int hkp_conv_weight_flip(const hkp_conv_desc* d, const float* w, float* w_flip, 
 int hkp_conv2d_bwd_data(const hkp_conv_desc* d, const float* dy, const float* w_flip, const float* add, float* dx,
                         hkp_stream_t stream);
 
-/* f16x3 backward-data for stride-1 NHWC convs (the split kernel of
- * hkp_conv2d_fwd_split): the gradient operand dy is scaled by an exact power of
- * two derived from its max |dy| (dy_amax_bits from hkp_absmax, nullable = no
- * scaling) so that tiny gradients keep fp16 precision; wf_hi/wf_lo from
- * hkp_conv_weight_flip_split.  add (nullable) is summed into dx. */
+/* max |x| as an IEEE bit pattern in amax_bits[0] (non-negative floats order like
+ * their bits): the power-of-two gradient scale of the f16x3 backward convs
+ * (dy_amax_bits of hkp_conv2d_bwd_data_x3 / _filter_x3 and hkp_split_pack_x3)
+ * when no BN backward bound is at hand.  n % 4 == 0. */
 int hkp_absmax(int64_t n, const float* x, uint32_t* amax_bits, hkp_stream_t stream);
-int hkp_conv_weight_flip_split(const hkp_conv_desc* d, const float* w, uint16_t* wf_hi, uint16_t* wf_lo,
-                               hkp_stream_t stream);
-int hkp_conv2d_bwd_data_split(const hkp_conv_desc* d, const float* dy, const uint16_t* wf_hi,
-                              const uint16_t* wf_lo, const uint32_t* dy_amax_bits, const float* add, float* dx,
-                              hkp_stream_t stream);
-
-/* f16x3 backward-filter for NHWC convs (Cin, Cout multiples of 64): dw (KRSC)
- * with dy scaled by the power of two from dy_amax_bits (nullable); split-K over
- * pixels into `workspace` (hkp_conv_bwd_filter_split_workspace bytes), fixed-order reduce. */
-int64_t hkp_conv_bwd_filter_split_workspace(const hkp_conv_desc* d);
-int hkp_conv2d_bwd_filter_split(const hkp_conv_desc* d, const float* x, const float* dy,
-                                const uint32_t* dy_amax_bits, float* dw, void* workspace, int64_t ws_bytes,
-                                hkp_stream_t stream);
 
 /* The stem conv (7x7, stride 2, pad 3, NCHW input with C <= 4; src/resnet.py:137,199)
  * on the f16x3 path: hkp_stem_pack_x3 writes the image as zero-padded NHWC4 fp16

@@ -190,6 +190,32 @@ def fwd_batch_case(name, backbone, k, B, H, W, wseed, iseed):
     print(name, "margin min %.3g" % out["margin"].min(), "argmax", out["argmax_yx"].reshape(-1, 2)[:4].tolist())
 
 
+def fwd_subsampled_case(name, backbone, k, B, H, W, wseed, iseed, step=4):
+    """Forward at bench resolution for a wide head (BASELINE config C4's network,
+    R50-8s K=8 at 640x480): the full low-res logits, argmax, margins and heatmap
+    row sums of every plane, and the heatmaps on every `step`-th row and column
+    (a full [B,8,480,640] fp32 heatmap would be ~20 MB)."""
+    imgs = recipe.seeded_images_u8(B, H, W, iseed)
+    x = recipe.to_tensor_nchw(imgs)
+    m = build(backbone, k, wseed)
+    with torch.no_grad():
+        low = lowres_of(m, backbone, x)[:, :k].contiguous()
+        heat = heat_from_lowres(low, x.size()[2:])
+    sd_after = m.state_dict()
+    h = heat.numpy()
+    out = dict(backbone=np.array(backbone), k=np.int32(k), wseed=np.int32(wseed), iseed=np.int32(iseed),
+               batch=np.int32(B), height=np.int32(H), width=np.int32(W), images_sha256=image_digest(imgs),
+               step=np.int32(step), lowres=low.numpy().astype(np.float32),
+               argmax_yx=np.array([[np.unravel_index(h[b, j].argmax(), h[b, j].shape) for j in range(k)]
+                                   for b in range(B)], dtype=np.int32),
+               margin=(lambda t: (t[..., 0] - t[..., 1]).numpy())(torch.topk(heat.reshape(B, k, -1), 2, -1).values),
+               heat_row_sum=h.astype(np.float64).sum(axis=3),
+               heat_sub=np.ascontiguousarray(h[:, :, ::step, ::step]).astype(np.float32),
+               running_checksum=running_checksum(sd_after))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(name, "margin min %.3g" % out["margin"].min(), "argmax", out["argmax_yx"].reshape(-1, 2)[:4].tolist())
+
+
 def check_slice_first_head():
     """heat_from_lowres(K channels) == the reference's full 1000-channel head, bitwise."""
     imgs = recipe.seeded_images_u8(2, 120, 160, 3)
@@ -293,6 +319,9 @@ if __name__ == "__main__":
         check_slice_first_head()
         # BASELINE config C2 at the bench's batch
         fwd_batch_case("fwd_r34_k4_480x640_b32", "resnet34", 4, 32, 480, 640, wseed=10, iseed=20)
+    if want("fwd_r50_k8_480x640_b2"):
+        # BASELINE config C4's network (R50-8s, K=8) at the bench resolution
+        fwd_subsampled_case("fwd_r50_k8_480x640_b2", "resnet50", 8, 2, 480, 640, wseed=30, iseed=31)
     for args in [("train_r18_k2_64x80", "resnet18", 2, 2, 64, 80, 6, 16, 26),
                  ("train_r34_k4_48x64", "resnet34", 4, 2, 48, 64, 7, 17, 27),
                  # R50 K8 (the C4 / C5 network) train steps

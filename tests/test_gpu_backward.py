@@ -361,22 +361,21 @@ def test_backward_deterministic(cuda_device):
         assert torch.equal(a, b.grad)
 
 
-def test_dp_bucket_path_equals_plain(cuda_device, monkeypatch):
+def test_dp_bucket_path_equals_plain(cuda_device):
     """The DP gradient path (bucket copies on the stream each gradient is made on,
     one join per bucket; forced at world size 1) hands the optimizer exactly the
     gradients of the plain path, with the side-stream wgrad on and off."""
-    from hkp import net, train
+    from hkp import train
+    from hkp.policy import DEFAULT
     B, K, H, W = 2, 2, 64, 80
     x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 41)).to(cuda_device)
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 42)).to(cuda_device)
     m = _model("resnet34", K, 43, cuda_device)
     for overlap in (True, False):    # (off: dgrad may take stream-K — another fp32 order)
-        monkeypatch.setattr(net, "OVERLAP_WGRAD", overlap)
-        monkeypatch.setenv("HKP_FORCE_BUCKETS", "0")
+        m.policy = DEFAULT.with_(overlap_wgrad=overlap)
         train.Trainer(m).forward_backward(x, uv=uv)
         ref = [p.grad.clone() for p in m.parameters()]
-        monkeypatch.setenv("HKP_FORCE_BUCKETS", "1")
-        t = train.Trainer(m)
+        t = train.Trainer(m, force_buckets=True)
         assert t.bucketer is not None and len(t.bucketer.buckets) >= 2
         for _ in range(2):                       # buckets reused across steps
             t.forward_backward(x, uv=uv)
@@ -390,32 +389,25 @@ def test_backward_calls_exact(cuda_device, bb, k):
     """Every conv (dgrad, wgrad) and BN backward call of a full training step,
     re-done in fp64 on the CPU from that call's own GPU inputs: kernel error only,
     free of the forward-rounding discontinuities a deep train-mode-BN net has."""
+    from _spy import spy_calls
     from hkp import net, train
     B, H, W = 2, 64, 96
     x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 41)).to(cuda_device)
     uv = torch.from_numpy(recipe.seeded_keypoints(B, k, H, W, 42)).to(cuda_device)
     m = _model(bb, k, 43, cuda_device)
     log = []
-    oc, ob = net._conv_backward, net._bn_backward
 
-    def conv_spy(conv, xx, dy, grads, need_dx=True, add=None):
-        dx = oc(conv, xx, dy, grads, need_dx, add)
-        log.append(("conv", conv, xx, dy, add, dx, grads[conv.weight]))
-        return dx
+    def conv_spy(conv, xx, dy, add, dx, dw):
+        log.append(("conv", conv, xx, dy, add, dx, dw))
 
-    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False, split_only=False, relu_ss=None):
-        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz, split_only, relu_ss=relu_ss)
+    def bn_spy(bn, gr, mask, relu_ss, y, mi, dy, dgamma, dbeta):
         if relu_ss is not None:          # the mask the kernel recomputes: round(round(y*a) + b) > 0
             c = y.shape[-1]
             mask = (y.float() * relu_ss[:c]) + relu_ss[c:]
-        log.append(("bn", bn, gr, mask, y, mi, dy, grads[bn.weight], grads[bn.bias]))
-        return dy, dz
+        log.append(("bn", bn, gr, mask, y, mi, dy, dgamma, dbeta))
 
-    net._conv_backward, net._bn_backward = conv_spy, bn_spy
-    try:
+    with spy_calls(on_conv_bwd=conv_spy, on_bn_bwd=bn_spy):
         train.Trainer(m).forward_backward(x, uv=uv)
-    finally:
-        net._conv_backward, net._bn_backward = oc, ob
     n_conv = sum(1 for r in log if r[0] == "conv")
     assert n_conv == len([mm for mm in m.modules() if mm.__class__.__name__ == "KRSCConv2d"])
 
@@ -493,17 +485,11 @@ def test_bn_finalize_two_level(cuda_device, c, rows):
     gamma = torch.rand(c, device=d, generator=g) + 0.5
     beta = torch.rand(c, device=d, generator=g) - 0.5
     outs = []
-    for one in (True, False):
-        ops._FIN_ONE_KERNEL = one
-        lvl, ops.FIN_TWO_LEVEL_TILES = ops.FIN_TWO_LEVEL_TILES, 129     # every case takes the two-level form
-        try:
-            rm, rv = torch.zeros(c, device=d), torch.ones(c, device=d)
-            nbt = torch.zeros(1, device=d, dtype=torch.int64)
-            ss, mi = ops.bn_finalize(part, rows, gamma, beta, rm, rv, nbt)
-            outs.append((ss, mi, rm, rv, nbt))
-        finally:
-            ops._FIN_ONE_KERNEL = False
-            ops.FIN_TWO_LEVEL_TILES = lvl
+    for two_level in (1 << 40, 129):        # the one-kernel merge, then the two-level form for every case
+        rm, rv = torch.zeros(c, device=d), torch.ones(c, device=d)
+        nbt = torch.zeros(1, device=d, dtype=torch.int64)
+        ss, mi = ops.bn_finalize(part, rows, gamma, beta, rm, rv, nbt, two_level_tiles=two_level)
+        outs.append((ss, mi, rm, rv, nbt))
     torch.cuda.synchronize()
     # the two forms: fp64 merges in different orders, rounded to fp32 -> at most 1 ulp apart
     for a, b in zip(outs[0][:4], outs[1][:4]):
@@ -517,9 +503,5 @@ def test_bn_finalize_two_level(cuda_device, c, rows):
     assert torch.allclose(mi[c:].double(), 1 / torch.sqrt(var + 1e-5), rtol=1e-5)
     assert torch.allclose(rv.double(), 0.9 + 0.1 * y.var(0, unbiased=True), rtol=1e-5)
     # deterministic run to run
-    lvl, ops.FIN_TWO_LEVEL_TILES = ops.FIN_TWO_LEVEL_TILES, 129
-    try:
-        ss2, mi2 = ops.bn_finalize(part, rows, gamma, beta)
-    finally:
-        ops.FIN_TWO_LEVEL_TILES = lvl
+    ss2, mi2 = ops.bn_finalize(part, rows, gamma, beta, two_level_tiles=129)
     assert torch.equal(ss2, ss) and torch.equal(mi2, mi)

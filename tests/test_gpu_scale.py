@@ -1,4 +1,4 @@
-"""Parity at the bench's own configurations (BASELINE.json configs C2 and C5).
+"""Parity at the bench's own configurations (BASELINE.json configs C2-C5).
 
 * C2 (R34-8s, K=4, 640x480, batch 32 inference, train-mode BN over the batch):
   the exact path bench.py times — default f16x3 arithmetic, default tile
@@ -11,6 +11,16 @@
   call of one full step is checked on sampled output elements against an fp64
   recomputation from that call's own inputs (on the GPU, in torch fp64).  This
   is the high-memory path (side-stream wgrad overlap off above 3/4 of HBM).
+* C3 shard (R34-8s, K=4, 640x480, batch 8 training step — bench.py's `train`
+  leg exactly: side-stream wgrad overlap on, the overlapped dgrad on 256x256
+  tiles + split-K tail, column-grouped stream-K forward at 150 m-tiles): the same
+  sampled fp64 check of every call.
+* C4 (R50-8s, K=8, 640x480, batch 128, plain fp16): every conv forward checked
+  on sampled outputs against an fp64 recomputation from the fp16 operands the
+  kernel read (fp32 accumulation ≤ 1e-5 relative, then the fp16 output rounding);
+  and C4's network at bench resolution against a reference fixture
+  (fwd_r50_k8_480x640_b2): f16x3 within the north-star bar, plain fp16's heatmap
+  error and argmax agreement reported.
 """
 import hashlib
 
@@ -24,9 +34,9 @@ from oracle import recipe
 pytestmark = pytest.mark.gpu
 
 
-def _model(bb, k, wseed, dev):
+def _model(bb, k, wseed, dev, precision="f16x3"):
     from src.model import KeypointsGauss
-    m = KeypointsGauss(k, backbone=bb, pretrained=False)
+    m = KeypointsGauss(k, backbone=bb, pretrained=False, precision=precision)
     m.load_state_dict(recipe.seeded_state_dict(bb, wseed))
     return m.to(dev)
 
@@ -46,7 +56,7 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
     def observe(sym, flops, nbytes, launch):
         syms[sym] = syms.get(sym, 0.0) + flops
         launch()
-    assert net.conv_precision() == "f16x3"           # the bench default
+    assert m.policy.precision == "f16x3"             # the bench default
     ops.set_observer(observe)
     try:
         with torch.no_grad():
@@ -75,23 +85,25 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
 
 
 class _Act:
-    """fp64 reader of an NHWC activation: fp32, or a packed f16x3 split ([.., 2C],
-    per 32 channels hi32|lo32, value = (hi + lo) / scale), or an NCHW image."""
+    """fp64 reader of an NHWC activation: fp32, a packed f16x3 split ([.., 2C],
+    per 32 channels hi32|lo32, value = (hi + lo) / scale), a plain fp16 tensor
+    (the f16 path's split=1 operand), or an NCHW image."""
 
     def __init__(self, t, layout="nhwc", scale=1.0):
         self.t, self.layout, self.scale = t, layout, scale
+        self.packed = t.dtype == torch.float16 and getattr(t, "_hkp_split_passes", 3) == 3
         if layout == "nchw":
             self.N, self.C, self.H, self.W = t.shape
         else:
             self.N, self.H, self.W = t.shape[:3]
-            self.C = t.shape[3] // 2 if t.dtype == torch.float16 else t.shape[3]
+            self.C = t.shape[3] // 2 if self.packed else t.shape[3]
 
     def pix(self, n, h, w):
         """[ns, C] values at pixels (n, h, w) (index tensors)."""
         if self.layout == "nchw":
             return self.t[n, :, h, w].double()
         v = self.t[n, h, w]
-        if self.t.dtype == torch.float16:
+        if self.packed:
             g = v.reshape(v.shape[0], self.C // 32, 2, 32).double()
             return (g[:, :, 0] + g[:, :, 1]).reshape(v.shape[0], self.C) / self.scale
         return v.double()
@@ -100,7 +112,7 @@ class _Act:
         """[N, H, W] plane of channel c."""
         if self.layout == "nchw":
             return self.t[:, c].double()
-        if self.t.dtype == torch.float16:
+        if self.packed:
             j = (c // 32) * 64 + c % 32
             return (self.t[..., j].double() + self.t[..., j + 32].double()) / self.scale
         return self.t[..., c].double()
@@ -242,41 +254,36 @@ def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, c
     _check("bn_dy", got, ref, tol, stats)
 
 
-def test_c5_train_step_sampled_fp64(cuda_device):
-    """One C5 training step (R50-8s K=8 1280x960 B=32, bench.py --mode train at
-    the C5 shape): every conv forward / dgrad / wgrad and BN backward call checked
-    on sampled elements against fp64 recomputations from its own inputs."""
+def _sampled_train_step(dev, bb, K, H, W, B, seeds):
+    """One Trainer step (bench.py --mode train's step) with every conv forward /
+    dgrad / wgrad, BN backward and the stem wgrad checked on sampled elements
+    against fp64 recomputations from the call's own inputs.  Returns (loss, call
+    counts, worst error/bound per check, conv kernel symbols, model)."""
+    from _spy import spy_calls
     from hkp import net, ops, train
-    B, K, H, W = 32, 8, 960, 1280
-    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 61)).to(cuda_device)
-    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 62)).to(cuda_device)
-    m = _model("resnet50", K, 63, cuda_device)
-    gen = torch.Generator().manual_seed(64)
-    stats, counts = {}, {"fwd": 0, "bwd": 0, "bn": 0, "stem_wgrad": 0}
-    oc_f, oc_b, ob, o_wst = net._conv_fwd, net._conv_backward, net._bn_backward, ops.conv2d_bwd_filter
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, seeds[0])).to(dev)
+    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, seeds[1])).to(dev)
+    m = _model(bb, K, seeds[2], dev)
+    gen = torch.Generator().manual_seed(seeds[3])
+    stats, counts, syms = {}, {"fwd": 0, "bwd": 0, "bn": 0, "stem_wgrad": 0}, {}
 
-    def fwd_spy(conv, bn, xx, layout="nhwc", part_out=None, sk=True):
-        y, part = oc_f(conv, bn, xx, layout, part_out, sk)
+    def on_fwd(conv, bn, xx, layout, y, part):
         torch.cuda.synchronize()
         w = conv.weight if layout == "nhwc" else conv.weight.permute(0, 2, 3, 1)
         check_conv_fwd(_Act(xx, layout), w, y, net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation),
                        gen, stats)
         counts["fwd"] += 1
-        return y, part
 
-    def bwd_spy(conv, xx, dy, grads, need_dx=True, add=None):
-        dx = oc_b(conv, xx, dy, grads, need_dx, add)
+    def on_bwd(conv, xx, dy, add, dx, dw):
         torch.cuda.synchronize()
         st, pd, dl = net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation)
         dya = _Act(dy, scale=_dy_scale(dy))
         if dx is not None:
             check_conv_dgrad(dya, conv.weight, dx, add, st, pd, dl, gen, stats)
-        check_conv_wgrad(_Act(xx), dya, grads[conv.weight], st, pd, dl, gen, stats)
+        check_conv_wgrad(_Act(xx), dya, dw, st, pd, dl, gen, stats)
         counts["bwd"] += 1
-        return dx
 
-    def bn_spy(bn, gr, mask, y, mi, grads, want_dz=False, split_only=False, relu_ss=None):
-        dy, dz = ob(bn, gr, mask, y, mi, grads, want_dz, split_only, relu_ss=relu_ss)
+    def on_bn(bn, gr, mask, relu_ss, y, mi, dy, dgamma, dbeta):
         torch.cuda.synchronize()
         c = y.shape[-1]
         y2 = y.reshape(-1, c)
@@ -291,28 +298,153 @@ def test_c5_train_step_sampled_fp64(cuda_device):
         else:
             def mask_fn(rows):
                 return torch.ones_like(y2[rows], dtype=torch.float64)
-        check_bn_bwd(bn, gr, mask_fn, y, mi, dy, grads[bn.weight], grads[bn.bias], gen, stats)
+        check_bn_bwd(bn, gr, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats)
         counts["bn"] += 1
-        return dy, dz
 
-    def stem_wgrad_spy(xx, dy, w_shape, stride=1, pad=0, dil=1, layout="nhwc", out=None, accumulate=False):
-        dw = o_wst(xx, dy, w_shape, stride, pad, dil, layout, out, accumulate)
+    def on_stem_wgrad(xx, dy, w_shape, stride, pad, dil, layout, dw):
         torch.cuda.synchronize()
         if layout == "nchw":
             check_conv_wgrad(_Act(xx, "nchw"), _Act(dy), dw.permute(0, 2, 3, 1), stride, pad, dil, gen, stats)
             counts["stem_wgrad"] += 1
-        return dw
 
-    net._conv_fwd, net._conv_backward, net._bn_backward, ops.conv2d_bwd_filter = \
-        fwd_spy, bwd_spy, bn_spy, stem_wgrad_spy
+    def observe(sym, flops, nbytes, launch):
+        syms[sym] = syms.get(sym, 0) + 1
+        launch()
+
+    ops.set_observer(observe)
     try:
-        loss = train.Trainer(m).forward_backward(x, uv=uv)
+        with spy_calls(on_fwd, on_bwd, on_bn, on_stem_wgrad):
+            loss = train.Trainer(m).forward_backward(x, uv=uv)
     finally:
-        net._conv_fwd, net._conv_backward, net._bn_backward, ops.conv2d_bwd_filter = oc_f, oc_b, ob, o_wst
+        ops.set_observer(None)
+    return loss, counts, stats, syms, m
+
+
+def test_c3_shard_train_step_sampled_fp64(cuda_device):
+    """bench.py's `train` leg exactly (C3 shard: R34-8s K=4 640x480 B=8, default
+    policy — side-stream wgrad overlapping a 256x256 + split-K-tail dgrad, the
+    column-grouped stream-K forward): every call vs fp64 on sampled elements."""
+    from hkp import net
+    loss, counts, stats, syms, m = _sampled_train_step(cuda_device, "resnet34", 4, 480, 640, 8, (71, 72, 73, 74))
+    print("C3 shard step: loss %.9f, calls %s, worst error / bound: %s" % (
+        loss.item(), counts, {k: round(v, 4) for k, v in stats.items()}))
+    print("conv kernels:", syms)
     n_conv = len([mm for mm in m.modules() if mm.__class__.__name__ == "KRSCConv2d"])
+    assert counts == {"fwd": n_conv + 1, "bwd": n_conv, "bn": n_conv + 1, "stem_wgrad": 1}
+    assert torch.isfinite(loss).item()
+    # the configuration bench.py times: overlap on (memory not tight), the bench
+    # train leg's roofline symbol and the wgrad kernel among the launches
+    assert m.policy.overlap_wgrad and not net._memory_tight(cuda_device)
+    assert "conv_x3_kernel<256, false, false, 16, false, 3>" in syms and "wgrad_x3_kernel<256>" in syms
+    assert any(s.endswith(", true, 3>") for s in syms), syms          # stream-K forward / dgrad bodies ran
+
+
+def test_c5_train_step_sampled_fp64(cuda_device):
+    """One C5 training step (R50-8s K=8 1280x960 B=32, bench.py --mode train at
+    the C5 shape): every conv forward / dgrad / wgrad and BN backward call checked
+    on sampled elements against fp64 recomputations from its own inputs."""
+    loss, counts, stats, syms, m = _sampled_train_step(cuda_device, "resnet50", 8, 960, 1280, 32, (61, 62, 63, 64))
     print("C5 step: loss %.9f, calls %s, worst error / bound: %s" % (
         loss.item(), counts, {k: round(v, 4) for k, v in stats.items()}))
+    print("conv kernels:", syms)
+    n_conv = len([mm for mm in m.modules() if mm.__class__.__name__ == "KRSCConv2d"])
     assert counts == {"fwd": n_conv + 1, "bwd": n_conv, "bn": n_conv + 1, "stem_wgrad": 1}
     assert torch.isfinite(loss).item()
     assert torch.cuda.max_memory_allocated(cuda_device) > 0.5 * torch.cuda.get_device_properties(
         cuda_device).total_memory          # really the high-memory configuration
+
+
+def check_conv_fwd_f16(x, wp, y, st, pd, dl, gen, stats, ns=256):
+    """Plain-fp16 conv: y (fp16) vs the fp64 sum of the fp16 operands the kernel
+    read (x16, and the packed weight w16 * inv_scale): fp32 accumulation within
+    1e-5 of the sum of |products|, then one fp16 rounding of the output."""
+    N, H, W, C = x.N, x.H, x.W, x.C
+    w16, inv = wp
+    K, R, S, _ = w16.shape
+    _, Ho, Wo, _ = y.shape
+    dev = y.device
+    n, ho, wo, k = (_idx(gen, v, ns, dev) for v in (N, Ho, Wo, K))
+    w64 = w16.double() * inv.double().view(-1, 1, 1, 1)
+    acc = torch.zeros(ns, device=dev, dtype=torch.float64)
+    mag = torch.zeros_like(acc)
+    for r in range(R):
+        for s in range(S):
+            hi, wi = ho * st - pd + r * dl, wo * st - pd + s * dl
+            ok = ((hi >= 0) & (hi < H) & (wi >= 0) & (wi < W)).double()[:, None]
+            xv = x.pix(n, hi.clamp(0, H - 1), wi.clamp(0, W - 1)) * ok
+            p = xv * w64[k, r, s, :]
+            acc += p.sum(1)
+            mag += p.abs().sum(1)
+    got = y[n, ho, wo, k].double()
+    # half an fp16 ulp of the result (normal range: 2^-11 relative; subnormals 2^-25)
+    half_ulp = torch.maximum(got.abs(), acc.abs()) * 2.0 ** -11 + 2.0 ** -25
+    _check("fwd_f16", got, acc, REL * mag + half_ulp, stats)
+
+
+def test_c4_fp16_forward_sampled_fp64(cuda_device):
+    """C4 at the bench's own size (R50-8s K=8 640x480 B=128, plain fp16 — bench.py
+    --backbone resnet50 --keypoints 8 --batch 128 --precision f16): every conv
+    forward on sampled outputs vs fp64 from the operands the kernel read."""
+    from _spy import spy_calls
+    from hkp import net, ops
+    B, K, H, W = 128, 8, 480, 640
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 81)).to(cuda_device)
+    m = _model("resnet50", K, 82, cuda_device, precision="f16")
+    gen = torch.Generator().manual_seed(83)
+    stats, counts, syms = {}, {"stem": 0, "f16": 0}, {}
+
+    def on_fwd(conv, bn, xx, layout, y, part):
+        torch.cuda.synchronize()
+        st, pd, dl = net._i(conv.stride), net._i(conv.padding), net._i(conv.dilation)
+        if layout == "nchw":                     # the stem: f16x3 arithmetic, fp32 output
+            check_conv_fwd(_Act(xx, layout), conv.weight.permute(0, 2, 3, 1), y, st, pd, dl, gen, stats)
+            counts["stem"] += 1
+            return
+        assert y.dtype == torch.float16
+        xs = ops.split_of(xx)[0]
+        assert getattr(xs, "_hkp_split_passes", 0) == 1
+        wp = net._cached_split(conv.weight, "f16", ops.weight_pack_f16)
+        check_conv_fwd_f16(_Act(xs), wp, y, st, pd, dl, gen, stats)
+        counts["f16"] += 1
+
+    def observe(sym, flops, nbytes, launch):
+        syms[sym] = syms.get(sym, 0) + 1
+        launch()
+
+    ops.set_observer(observe)
+    try:
+        with spy_calls(on_conv_fwd=on_fwd), torch.no_grad():
+            hm, yx = m.heatmaps_and_keypoints(x)
+    finally:
+        ops.set_observer(None)
+    n_conv = len([mm for mm in m.modules() if mm.__class__.__name__ == "KRSCConv2d"])
+    print("C4 B=128: calls %s, worst error / bound: %s" % (counts, {k: round(v, 4) for k, v in stats.items()}))
+    print("conv kernels:", syms)
+    assert counts == {"stem": 1, "f16": n_conv}
+    assert "conv_x3_kernel<256, false, false, 16, false, 1>" in syms      # BENCH C4's roofline symbol
+    assert torch.isfinite(hm).all().item() and yx.shape == (B, K, 2)
+
+
+@pytest.mark.parametrize("precision", ["f16x3", "f16"])
+def test_r50_bench_resolution_vs_reference(cuda_device, golden, precision):
+    """C4's network (R50-8s K=8) at 640x480 vs the reference fixture: f16x3 meets
+    the north-star bar (heat < 1e-3, argmax bit-exact); plain fp16 (config C4's
+    arithmetic) is reported — heatmap error and argmax agreement — and gated at
+    the measured values with a margin."""
+    import hashlib
+    g = golden("fwd_r50_k8_480x640_b2")
+    B, H, W, K, st = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["k"]), int(g["step"])
+    imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))
+    assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
+    m = _model("resnet50", K, int(g["wseed"]), cuda_device, precision=precision)
+    with torch.no_grad():
+        hm, yx = m.heatmaps_and_keypoints(recipe.to_tensor_nchw(imgs).to(cuda_device))
+    heat_err = float(np.abs(hm[:, :, ::st, ::st].cpu().numpy() - g["heat_sub"]).max())
+    agree = float((yx.cpu().numpy() == g["argmax_yx"]).all(-1).mean())
+    rows = np.abs(hm.double().sum(3).cpu().numpy() - g["heat_row_sum"]).max()
+    print("R50 K8 640x480 %s: heat max err %.3g, row-sum err %.3g, argmax agreement %.3f (%d/%d), min margin %.3g"
+          % (precision, heat_err, rows, agree, round(agree * B * K), B * K, g["margin"].min()))
+    if precision == "f16x3":
+        assert heat_err < 1e-3 and agree == 1.0
+    else:
+        assert heat_err < 0.2 and agree >= 0.5

@@ -2,7 +2,7 @@
 
 Train-mode BN (the reference never calls .eval()) makes a shard's outputs depend
 on the shard: N ranks with per-rank statistics do not reproduce the reference's
-forward over the global batch.  With hkp.parallel.sync_bn each rank's BN
+forward over the global batch.  With SyncBN (Policy(sync_bn=True)) each rank's BN
 statistics block (hkp_bn_stats) is all-gathered and merged in fixed rank order
 (hkp_bn_finalize_ranks), and the sharded run matches the reference at the
 global batch:
@@ -126,8 +126,9 @@ def _dp_worker(rank, world, port, q):
             m.load_state_dict(recipe.seeded_state_dict("resnet34", int(g["wseed"])))
             return m.to(dev)
         m = model()
-        with torch.no_grad(), parallel.sync_bn():
-            hm, yx, low = net.keypoints_forward(m.resnet.net, x, K, heat=True, argmax=True)
+        with torch.no_grad():
+            hm, yx, low = net.keypoints_forward(m.resnet.net, x, K, heat=True, argmax=True,
+                                                pol=m.policy.with_(sync_bn=True))
         yx_all = parallel.gather_keypoints(yx.to(torch.int32).cpu())        # gloo: host tensors
         res = dict(rank=rank,
                    low_err=float(np.abs(low.cpu().numpy() - g["lowres"][lo:hi]).max()),
@@ -197,12 +198,23 @@ def _train_worker(rank, world, port, out_dir, q):
         imgs = recipe.seeded_images_u8(B, H, W, 21)
         uv_all = recipe.seeded_keypoints(B, K, H, W, 22)
 
+        n_gathers = [0]
+        orig_gather = parallel.gather_bn_stats
+
+        def counting_gather(st, group=None):
+            n_gathers[0] += 1
+            return orig_gather(st, group)
+        parallel.gather_bn_stats = counting_gather
+
         def grads_of(x, uv, sync):
             m = KeypointsGauss(K, backbone="resnet18", pretrained=False)
             m.load_state_dict(recipe.seeded_state_dict("resnet18", 23))
             m = m.to(dev)
             t = train.Trainer(m, distributed=False, sync_bn=sync)
+            n_gathers[0] = 0
             loss = t.forward_backward(x, uv=uv)
+            if sync:
+                res["gathers"] = n_gathers[0]
             torch.cuda.synchronize()
             g = {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
             rm = {n: b.detach().cpu() for n, b in m.named_buffers() if n.endswith("running_mean")}
@@ -244,6 +256,9 @@ def test_syncbn_training_step_equals_global_batch(cuda_device, tmp_path):
     r0 = torch.load(os.path.join(tmp_path, "rank0.pt"), weights_only=True)
     r1 = torch.load(os.path.join(tmp_path, "rank1.pt"), weights_only=True)
     lg, gg, rmg = r0["global"]
+    # R18: 20 BN layers, 3 downsample blocks whose last BN and downsample BN share
+    # one gather in each direction -> 17 forward + 17 backward statistics gathers
+    assert r0["gathers"] == r1["gathers"] == 34, (r0["gathers"], r1["gathers"])
     for kind in ("sync", "local"):
         l0, g0, rm0 = r0[kind]
         l1, g1, rm1 = r1[kind]

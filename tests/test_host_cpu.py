@@ -357,3 +357,112 @@ def test_bench_pmc_traffic_folds_split_k_tail():
     # kernels without a tail are looked up unchanged
     nb2, _, _, f2 = bench.pmc_traffic("wgrad_x3_kernel<256>", "train_c3")
     assert f2 is None
+
+
+def _fit_worker(rank, world, port, out_dir, q):
+    """One rank of a world-2 gloo group running the drop-in train.fit (the
+    reference's loop: zero_grad, forward, loss.backward(), step) with DP wired by
+    train.setup_data_parallel; the per-rank compute is the oracle's CPU autograd
+    (net.keypoints_forward / keypoints_backward / ops.heat_loss replaced), so the
+    test sees the order in which backward hands out gradients and the bucketer
+    launches its all-reduces."""
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.Tensor.cuda = lambda self, *a, **k: self        # CPU-only rehearsal of train.forward's .cuda()
+        import train as train_mod
+        from hkp import net, ops
+        from oracle import cpu_ref, recipe
+        from src.model import KeypointsGauss
+        bb, K, B, H, W = "resnet18", 2, 2, 32, 48
+        torch.manual_seed(200 + rank)
+        m = KeypointsGauss(K, H, W, backbone=bb, pretrained=False)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(0.01 * rank)                          # replicas start different
+        start_sd = None
+        events = []
+        orig_ar = dist.all_reduce
+
+        def logged_all_reduce(t, *a, **k):
+            events.append("all_reduce")
+            return orig_ar(t, *a, **k)
+        dist.all_reduce = logged_all_reduce
+
+        def oracle_forward(resnet, x, k, heat=True, argmax=False, trace=None, pol=None):
+            with torch.enable_grad():
+                hm = cpu_ref.forward(m.state_dict(keep_vars=True), x, bb, k)
+            trace.head = hm
+            return hm.detach(), None, None
+
+        def oracle_loss(hm, target, uv, sigma, kind, want_grad=True):
+            h = hm.detach().requires_grad_(True)
+            with torch.enable_grad():
+                L = cpu_ref.bce_loss(h, cpu_ref.gauss_target(uv, hm.shape[2], hm.shape[3], sigma))
+                (dheat,) = torch.autograd.grad(L, h)
+            return L.detach(), dheat
+
+        def oracle_backward(resnet, trace, dheat, grads):
+            ps = list(m.parameters())
+            gs = torch.autograd.grad(trace.head, ps, dheat)
+            for p, g in reversed(list(zip(ps, gs))):         # backward order: fc side first
+                grads.put(p, g)
+                events.append("grad")
+            events.append("backward_end")
+            return grads
+
+        net.keypoints_forward, net.keypoints_backward, ops.heat_loss = oracle_forward, oracle_backward, oracle_loss
+        train_mod.setup_data_parallel(m, bucket_mb=4)
+        start_sd = {k: v.clone() for k, v in m.state_dict().items()}        # after the broadcast
+        lr = 1e-4
+        train_mod.optimizer = torch.optim.SGD(m.parameters(), lr=lr)       # a plain step: p -= lr * grad
+        imgs = recipe.seeded_images_u8(B * world, H, W, 9)
+        uvs = recipe.seeded_keypoints(B * world, K, H, W, 10)
+        batch = (recipe.to_tensor_nchw(imgs[rank * B:(rank + 1) * B]), torch.from_numpy(uvs[rank * B:(rank + 1) * B]))
+        train_mod.fit([batch], [batch], m, epochs=1, checkpoint_path=out_dir)
+        # reference: the mean of the per-shard oracle gradients from the common start
+        ref = None
+        for r in range(world):
+            sd = {k: v.clone() for k, v in start_sd.items()}
+            _, g, _ = cpu_ref.train_step(sd, recipe.to_tensor_nchw(imgs[r * B:(r + 1) * B]),
+                                         uvs[r * B:(r + 1) * B], bb, K)
+            ref = g if ref is None else {k: ref[k] + g[k] for k in g}
+        err = 0.0
+        for n_, p in m.named_parameters():
+            want = ref[n_] / world
+            got = p.grad if p.grad.shape == want.shape else p.grad.permute(0, 3, 1, 2)
+            err = max(err, ((got - want).abs().max() / (want.abs().max() + 1e-30)).item())
+        first_ar = events.index("all_reduce")
+        q.put(dict(rank=rank, err=err, launched_before_end=first_ar < events.index("backward_end"),
+                   n_all_reduce=events.count("all_reduce"), n_buckets=len(train_mod._bucketer.buckets),
+                   grads_before_first=events[:first_ar].count("grad"), n_grads=events.count("grad")))
+    except Exception as e:
+        q.put(dict(rank=rank, error=repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_fit_dp_overlaps_allreduce_gloo_world2(tmp_path):
+    """The drop-in train.fit over a 2-process gloo group: bucket all-reduces start
+    while the backward is still producing gradients (not after loss.backward()
+    returns), and the averaged gradients equal the mean of the per-shard oracle
+    gradients."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_fit_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(60)
+    print(res)
+    assert all("error" not in r for r in res), res
+    for r in res:
+        assert r["err"] < 1e-5, r
+        assert r["launched_before_end"] and r["grads_before_first"] < r["n_grads"], r
+        assert r["n_all_reduce"] == r["n_buckets"] >= 3, r
+    assert os.path.exists(os.path.join(tmp_path, "model_2_1_0.pth"))

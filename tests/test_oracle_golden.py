@@ -126,3 +126,23 @@ def test_forward_bench_batch_matches_reference(golden):
     assert (cpu_ref.argmax_yx(heat) == g["argmax_yx"]).all()
     rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
     assert abs(rm - g["running_checksum"][0]) < 1e-6 * max(1, abs(rm))
+
+
+def test_forward_r50_bench_resolution_matches_reference(golden):
+    """BASELINE config C4's network (R50-8s, K=8) at 640x480: the oracle reproduces
+    the reference's logits, subsampled heatmaps, row sums and argmax."""
+    import hashlib
+    g = golden("fwd_r50_k8_480x640_b2")
+    B, H, W, st = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["step"])
+    imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))
+    assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
+    sd = recipe.seeded_state_dict("resnet50", int(g["wseed"]))
+    with torch.no_grad():
+        heat, low = cpu_ref.forward(sd, recipe.to_tensor_nchw(imgs), "resnet50", 8, head="k_only",
+                                    return_lowres=True)
+    np.testing.assert_allclose(low.numpy(), g["lowres"], rtol=0, atol=2e-5)
+    np.testing.assert_allclose(heat[:, :, ::st, ::st].numpy(), g["heat_sub"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(heat.double().sum(3).numpy(), g["heat_row_sum"], rtol=1e-6)
+    assert (cpu_ref.argmax_yx(heat) == g["argmax_yx"]).all()
+    rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
+    assert abs(rm - g["running_checksum"][0]) < 1e-6 * max(1, abs(rm))

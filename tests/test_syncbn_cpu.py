@@ -4,7 +4,9 @@
   (mean = sum n_r mean_r / N, M2 = sum M2_r + n_r (mean_r - mean)^2), restated in
   numpy, equals the statistics of the whole batch (ragged shards included);
 * hkp.parallel.gather_bn_stats over a gloo world of 2 returns the blocks in rank
-  order on every rank; sync_bn() / sync_bn_group() switch it on and off.
+  order on every rank; a Policy(sync_bn=True) switches it on (active_sync_group),
+  per policy — no process-global state; check_shards makes every rank raise
+  when one holds no image (instead of hanging in a gather).
 """
 import os
 import socket
@@ -62,18 +64,21 @@ def _gather_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from hkp import parallel
-    ok = parallel.sync_bn_group() is None                      # off by default
-    with parallel.sync_bn():
-        ok &= parallel.sync_bn_group() is not None
-        st = torch.arange(7, dtype=torch.float64) + 100.0 * rank
-        g = parallel.gather_bn_stats(st, parallel.sync_bn_group()[0])
-        ok &= tuple(g.shape) == (world, 7) and g.dtype == torch.float64
-        ok &= all(torch.equal(g[r], torch.arange(7, dtype=torch.float64) + 100.0 * r) for r in range(world))
-    ok &= parallel.sync_bn_group() is None                     # restored
-    parallel.set_sync_bn(True)
-    ok &= parallel.sync_bn_group() is not None
-    parallel.set_sync_bn(False)
-    ok &= parallel.sync_bn_group() is None
+    from hkp.policy import DEFAULT
+    on = DEFAULT.with_(sync_bn=True)
+    ok = parallel.active_sync_group(DEFAULT) is None           # off by default
+    ok &= parallel.active_sync_group(on) is not None
+    st = torch.arange(7, dtype=torch.float64) + 100.0 * rank
+    g = parallel.gather_bn_stats(st, parallel.active_sync_group(on)[0])
+    ok &= tuple(g.shape) == (world, 7) and g.dtype == torch.float64
+    ok &= all(torch.equal(g[r], torch.arange(7, dtype=torch.float64) + 100.0 * r) for r in range(world))
+    ok &= DEFAULT.sync_bn is False                            # the default is untouched
+    parallel.check_shards(1 + rank)                            # every rank holds images: passes
+    try:                                                       # rank 1 empty: EVERY rank raises (no hang)
+        parallel.check_shards(1 - rank)
+        ok = False
+    except ValueError:
+        pass
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
@@ -96,7 +101,8 @@ def test_sync_bn_single_process_is_off():
     import sys
     sys.path[:0] = [REPO, PKG]
     from hkp import parallel
-    with parallel.sync_bn():
-        assert parallel.sync_bn_group() is None                # one rank: nothing to sync
-        st = torch.ones(5, dtype=torch.float64)
-        assert torch.equal(parallel.gather_bn_stats(st), st[None])
+    from hkp.policy import DEFAULT
+    assert parallel.active_sync_group(DEFAULT.with_(sync_bn=True)) is None     # one rank: nothing to sync
+    st = torch.ones(5, dtype=torch.float64)
+    assert torch.equal(parallel.gather_bn_stats(st), st[None])
+    parallel.check_shards(0)                                   # one rank: nothing to check

@@ -46,7 +46,11 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--nostats", action="store_true", help="no BN partials (epilogue cost A/B)")
+    ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B)")
     args = ap.parse_args()
+    if args.lib:
+        from hkp import _lib
+        _lib.use_library(os.path.abspath(args.lib))
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     tiles = [int(v) for v in args.tiles.split(",")]

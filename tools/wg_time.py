@@ -3,7 +3,7 @@
 C3-shard shapes, HIP-event timed on the launching stream, with no dgrad sharing
 the CUs (the training step overlaps them, so its per-kernel trace times include
 the sharing).  Optional in-process A/B against an alternative build of the same
-ABI (HKP_LIB_AB, see tools/ab.sh) is done by running this twice in one call.
+ABI (--lib) is done by running this twice in one call.
 
     python tools/wg_time.py [--shapes t3,t4] [--rounds 7] [--iters 10]
 """
@@ -31,7 +31,11 @@ def main():
     ap.add_argument("--shapes", default="t4,t3,t2,t1")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B)")
     args = ap.parse_args()
+    if args.lib:
+        from hkp import _lib
+        _lib.use_library(os.path.abspath(args.lib))
     from hkp import ops
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
