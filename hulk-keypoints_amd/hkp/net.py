@@ -61,8 +61,9 @@ def _bn_params_many(items, pol):
         off = 0
         for i, own in gather:
             bn = items[i][0]
-            out[i] = ops.bn_finalize_ranks(st[:, off:off + own.numel()], bn.weight, bn.bias, bn.running_mean,
-                                           bn.running_var, bn.num_batches_tracked, **_finalize_args(bn))
+            out[i] = ops.bn_finalize_ranks(st[:, off:off + own.numel()].contiguous(), bn.weight, bn.bias,
+                                           bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                                           **_finalize_args(bn))
             off += own.numel()
     return out
 
@@ -573,7 +574,7 @@ def _bn_bwd_finish(states, items, grads, pol):
         st = parallel.gather_bn_stats(torch.cat(own), sync[0])
         res, off = [], 0
         for s, o in zip(states, own):
-            res.append(ops.bn_bwd_end(s, st[:, off:off + o.numel()], o))
+            res.append(ops.bn_bwd_end(s, st[:, off:off + o.numel()].contiguous(), o))
             off += o.numel()
     out = []
     for it, (dy, dgamma, dbeta, dz) in zip(items, res):

@@ -447,4 +447,5 @@ def test_r50_bench_resolution_vs_reference(cuda_device, golden, precision):
     if precision == "f16x3":
         assert heat_err < 1e-3 and agree == 1.0
     else:
-        assert heat_err < 0.2 and agree >= 0.5
+        # measured (round 3): heat err 0.063, 14 of 16 argmax equal; gated with a margin
+        assert heat_err < 0.08 and agree >= 0.75
