@@ -133,4 +133,28 @@ __device__ __forceinline__ double lanes_max_d(double v, double (*red)[8]) {
     return m;
 }
 
+// scale/shift, mean/invstd and running statistics of channel c from the merged
+// fp64 mean and M2 (sum of squared deviations over all `count` rows)
+__device__ __forceinline__ void bn_fin_store(int c, int C, long count, double mean, double m2, const float* gamma,
+                                             const float* beta, float momentum, float eps, float* rmean, float* rvar,
+                                             int64_t* nbt, float* ss, float* mi) {
+    const double var = m2 / (double)count;
+    const double invstd = 1.0 / sqrt(var + (double)eps);
+    const float inv_f = (float)invstd, mean_f = (float)mean;
+    const float g = gamma ? gamma[c] : 1.f, b = beta ? beta[c] : 0.f;
+    const float alpha = __fmul_rn(inv_f, g);
+    ss[c] = alpha;
+    ss[C + c] = __fsub_rn(b, __fmul_rn(mean_f, alpha));
+    if (mi) {
+        mi[c] = mean_f;
+        mi[C + c] = inv_f;
+    }
+    if (rmean) {
+        const double unbiased = count > 1 ? m2 / (double)(count - 1) : var;
+        rmean[c] = (float)((double)momentum * mean + (1.0 - (double)momentum) * (double)rmean[c]);
+        rvar[c] = (float)((double)momentum * unbiased + (1.0 - (double)momentum) * (double)rvar[c]);
+    }
+    if (nbt && c == 0) nbt[0] += 1;
+}
+
 }  // namespace hkp

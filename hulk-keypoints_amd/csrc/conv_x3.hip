@@ -82,6 +82,12 @@ struct X3Args {
     float* sk_ws = nullptr;
     unsigned* sk_cnt = nullptr;
     unsigned long long* stamps = nullptr;   // debug: per-block phase clocks (hkp_debug_x3_stamps)
+    // fused BN apply of the output (P 1, hkp_conv2d_fwd_f16_bn): out = [relu](y*s + t
+    // [+ res | + res*rs + rt]) on the fp16-rounded y, bn_apply_f16's arithmetic
+    const float* ep_ss = nullptr;          // [2K] scale | shift
+    const _Float16* ep_res = nullptr;      // residual [M][K] fp16, nullable
+    const float* ep_rss = nullptr;         // residual scale | shift [2K], nullable (raw residual)
+    int ep_relu = 0;
 };
 
 // debug phase stamps (s_memrealtime, 100 MHz) of one-tile conv blocks: slot k of
@@ -474,6 +480,72 @@ __device__ __forceinline__ void x3_store_tile_f16(const X3Args& a, const char* s
     }
 }
 
+// BN-apply epilogue of the fp16 tile (hkp_conv2d_fwd_f16_bn): the staged fp16 y
+// chunk, x scale + shift, + the residual chunk (raw or scaled + shifted), ReLU —
+// bn_apply_f16's arithmetic on the same fp16 y, so the fused path returns what
+// conv + hkp_bn_apply_f16 would with the same scale/shift.  ssl: LDS [4][BN]
+// (scale, shift, residual scale, residual shift of the tile's columns).  A
+// thread always handles the same 8 channels (512 % (BN/8) == 0).
+template <int BN>
+__device__ __forceinline__ void x3_store_tile_f16_bn(const X3Args& a, const char* smem, const float* ssl, int m0,
+                                                     int n0, int tid) {
+    constexpr int CH = BN / 8, PITCH = BN + 8;
+    static_assert(512 % CH == 0, "fixed channels per thread");
+    const int cc = tid % CH;
+    float sa[8], sb[8], ra[8], rb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sa[e] = ssl[cc * 8 + e];
+        sb[e] = ssl[BN + cc * 8 + e];
+        ra[e] = ssl[2 * BN + cc * 8 + e];
+        rb[e] = ssl[3 * BN + cc * 8 + e];
+    }
+    const bool res = a.ep_res != nullptr, rsc = a.ep_rss != nullptr, relu = a.ep_relu != 0;
+#pragma unroll 4
+    for (int e = tid; e < 256 * CH; e += 512) {
+        const int row = e / CH;
+        const int m = m0 + row;
+        if (m >= a.M) continue;
+        const long off = (long)m * a.K + n0 + cc * 8;
+        const f16x8 v = *(const f16x8*)(smem + (row * PITCH + cc * 8) * 2);
+        f16x8 r = {};
+        if (res) r = __builtin_nontemporal_load((const f16x8*)(a.ep_res + off));
+        f16x8 h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float o = __fadd_rn(__fmul_rn((float)v[k], sa[k]), sb[k]);
+            if (res) o = rsc ? __fadd_rn(o, __fadd_rn(__fmul_rn((float)r[k], ra[k]), rb[k])) : __fadd_rn(o, (float)r[k]);
+            if (relu) o = o > 0.f ? o : 0.f;
+            h[k] = (_Float16)o;
+        }
+        __builtin_nontemporal_store(h, (f16x8*)(a.y16 + off));
+    }
+}
+
+// the fused epilogue's per-column parameters: thread tid < 2*BN holds scale (tid
+// < BN) or shift of column tid % BN, and the residual's; loaded before the tile
+// is staged (their latency hides behind it), written to LDS after
+struct X3EpSS {
+    float v0 = 0.f, v1 = 0.f;
+};
+template <int BN>
+__device__ __forceinline__ X3EpSS x3_ep_load(const X3Args& a, int n0, int tid) {
+    X3EpSS r;
+    if (a.ep_ss && tid < 2 * BN) {
+        const int h = tid / BN, c = tid - h * BN;
+        r.v0 = a.ep_ss[h * a.K + n0 + c];
+        r.v1 = a.ep_rss ? a.ep_rss[h * a.K + n0 + c] : 0.f;
+    }
+    return r;
+}
+template <int BN>
+__device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid) {
+    if (tid < 2 * BN) {
+        ssl[tid] = r.v0;
+        ssl[2 * BN + tid] = r.v1;
+    }
+}
+
 // Mainloop + epilogue of the 16x16x32-MFMA bodies: one k32 step per half of a
 // 128-B stage row (LDS ring, DMA issue and the swizzled rows exactly as the
 // 32x32 path).  Wave tile 64 x BN/2 = UM x UN 16x16 tiles.
@@ -666,10 +738,13 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
                 [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
         }
+        const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
         lds_sync();                        // the ring is free
         x3_stamp(a, 3);
         _Float16* t = (_Float16*)smem;
         constexpr int PITCH = BN + 8;
+        constexpr int SS_OFF = 256 * PITCH * 2;
+        static_assert(SS_OFF + 4 * BN * 4 <= x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB), "epilogue LDS");
 #pragma unroll
         for (int i = 0; i < UM; ++i)
 #pragma unroll
@@ -678,9 +753,11 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 for (int r = 0; r < 4; ++r)
                     t[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * UN * 16 + j * 16 + r16] =
                         (_Float16)(acc[i][j][r] * sc[j]);
+        if (a.ep_ss) x3_ep_store<BN>((float*)(smem + SS_OFF), eps, tid);
         lds_sync();
         x3_stamp(a, 4);
-        x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
+        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), m0, n0, tid);
+        else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
         x3_stamp(a, 5);
         return;
     }
@@ -998,9 +1075,12 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             x3_bn_partials<BN, TM, TN, 16, 32, 32>(
                 a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
                 [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); });
+        const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
         __syncthreads();
         _Float16* t = (_Float16*)smem;
         constexpr int PITCH = BN + 8;
+        constexpr int SS_OFF = 256 * PITCH * 2;
+        static_assert(SS_OFF + 4 * BN * 4 <= x3_lds_bytes(BN, PAIR, P) + x3_red_bytes(BN, PAIR), "epilogue LDS");
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1009,8 +1089,10 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
                 for (int r = 0; r < 16; ++r)
                     t[(wm * TM * 32 + i * 32 + 4 * kh + (r & 3) + 8 * (r >> 2)) * PITCH + wn * TN * 32 + j * 32 +
                       frow] = (_Float16)acc[i][j][r];
+        if (a.ep_ss) x3_ep_store<BN>((float*)(smem + SS_OFF), eps, tid);
         __syncthreads();
-        x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
+        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), m0, n0, tid);
+        else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
         return;
     }
 
@@ -2360,7 +2442,7 @@ static int check_tile(const hkp_conv_desc* d, const char* who) {
 // forward launch shared by the f16x3 (P 3) and plain-fp16 (P 1) entry points
 static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const uint16_t* ws, const float* wsc,
                               float* y, uint16_t* y16, float* part, void* sk_ws, int64_t sk_bytes, int P,
-                              hkp_stream_t stream, const char* who) {
+                              hkp_stream_t stream, const char* who, const X3Args* ep = nullptr) {
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
@@ -2381,6 +2463,9 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.cch = d->c / cg; a.RS = d->r * d->s;
+    if (ep) {
+        a.ep_ss = ep->ep_ss; a.ep_res = ep->ep_res; a.ep_rss = ep->ep_rss; a.ep_relu = ep->ep_relu;
+    }
     launch_x3(d->k, (M + 255) / 256, d->tile, P, as_stream(stream), a, sk_ws, sk_bytes);
     HKP_LAUNCH_CHECK(who);
     return HKP_OK;
@@ -2400,6 +2485,23 @@ extern "C" int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16,
     HKP_CHECK_ARG(d && y_f16, "hkp_conv2d_fwd_f16: null argument");
     return conv_fwd_x3_common(d, x_f16, w_f16, w_inv_scale, nullptr, y_f16, stat_partials, sk_workspace, sk_ws_bytes,
                               1, stream, "hkp_conv2d_fwd_f16");
+}
+
+extern "C" int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
+                                     const float* w_inv_scale, const float* scale_shift, const uint16_t* res_f16,
+                                     const float* res_scale_shift, int32_t relu, uint16_t* out_f16,
+                                     void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && out_f16 && scale_shift, "hkp_conv2d_fwd_f16_bn: null argument");
+    HKP_CHECK_ARG(!res_scale_shift || res_f16, "hkp_conv2d_fwd_f16_bn: res_scale_shift needs a residual");
+    HKP_CHECK_ARG(d->tile != HKP_TILE_256_PERSIST && d->tile != HKP_TILE_128_PERSIST,
+                  "hkp_conv2d_fwd_f16_bn: the persistent bodies have no fused epilogue");
+    X3Args ep;
+    ep.ep_ss = scale_shift;
+    ep.ep_res = (const _Float16*)res_f16;
+    ep.ep_rss = res_scale_shift;
+    ep.ep_relu = relu ? 1 : 0;
+    return conv_fwd_x3_common(d, x_f16, w_f16, w_inv_scale, nullptr, out_f16, nullptr, sk_workspace, sk_ws_bytes, 1,
+                              stream, "hkp_conv2d_fwd_f16_bn", &ep);
 }
 
 extern "C" int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits,

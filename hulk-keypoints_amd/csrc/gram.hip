@@ -1,0 +1,375 @@
+// BatchNorm statistics of a 1x1 conv's output from the second moments of its
+// input (BASELINE config C4: R50-8s inference, plain fp16).
+//
+// For y = W a (a 1x1 conv, no padding, over M pixels) the batch statistics of
+// output channel k are exact linear-algebra functions of the input's mean mu and
+// covariance Sigma:
+//     mean_k = w_k . mu,      var_k = w_k^T Sigma w_k
+// so train-mode BN (src/resnet.py:85-87,106-108: bn3 of every Bottleneck) needs
+// no pass over y.  Its scale/shift is known BEFORE the conv runs, and the conv
+// epilogue applies bn3 + residual + ReLU itself (hkp_conv2d_fwd_f16_bn): the
+// fp16 y3 (4*planes wide) is never written nor re-read by a separate apply pass.
+// The Gram matrix costs Cin^2/2 MACs per pixel against the conv's Cin*Cout —
+// 1/8 of an expanding conv3's (Cout = 4 Cin).
+//
+//   gram_f16_kernel<TC>   G partials: row splits x upper-triangle TC x TC channel
+//                         tiles; both MFMA operands read TRANSPOSED
+//                         (ds_read_b64_tr_b16) from one row-major LDS image filled
+//                         by LDS-DMA; column sums by one extra MFMA against ones
+//   gram_mean_kernel      mu = sum over splits (fp64, fixed order) / M
+//   gram_cov_kernel       Sigma = sum over splits (fp64, fixed order) / M - mu mu^T
+//   bn_from_gram_kernel   per output channel: mean, var (fp64) -> bn_fin_store
+//                         (the same scale/shift/running-stat formulas as
+//                         hkp_bn_finalize)
+// Deterministic: every reduction is in a fixed order.
+#include "common.h"
+
+namespace hkp {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __attribute__((aligned(256))) uint4 g_gram_zero_line[8];   // 128 B of zeros
+
+struct GramArgs {
+    const _Float16* a;   // [M][C] fp16
+    float* part;         // [splits][tiles][TC*TC] fp32, accumulator order
+    float* psum;         // [splits][nb][TC] fp32 column sums (diagonal tiles)
+    long M;
+    int C, nb, tiles, splits;
+    long rows;           // rows per split (a multiple of 32)
+};
+
+__device__ __forceinline__ void gram_glds16(const void* src, char* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int OFF>
+__device__ __forceinline__ s16x4 gram_tr16(unsigned lds_addr) {
+    s16x4 r;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(lds_addr), "i"(OFF));
+    return r;
+}
+
+__device__ __forceinline__ f16x8 gram_cat(s16x4 lo, s16x4 hi) {
+    return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// upper-triangle tile t -> (ib, jb), ib <= jb
+__device__ __forceinline__ void gram_tile(int t, int nb, int* ib, int* jb) {
+    int i = 0;
+    while (t >= nb - i) {
+        t -= nb - i;
+        ++i;
+    }
+    *ib = i;
+    *jb = i + t;
+}
+
+// Staged row (32 rows per K-step): TC channels of block ib, then TC of block jb,
+// fp16, 16-B chunk P of row r holding logical chunk P ^ f(r),
+// f(r) = 2 * ((r & 3) | ((r >> 3 & 1) << 2)): the two 16-lane groups of a
+// transposed read's 32-lane half touch rows {8g..8g+3} u {8g+8..8g+11} (or the
+// +4 rows), eight distinct f, so their eight 8-B pieces of a chunk pair land in
+// eight distinct 8-bank groups: conflict-free.
+template <int TC>
+__global__ __launch_bounds__(256, 2) void gram_f16_kernel(GramArgs g) {
+    constexpr int ROWB = 2 * TC * 2;       // bytes per staged row
+    constexpr int CPR = ROWB / 16;         // 16-B chunks per row
+    constexpr int RPI = 1024 / ROWB;       // rows per DMA wave-instruction
+    constexpr int KR = 32;                 // rows per K-step
+    constexpr int STAGE = KR * ROWB;
+    constexpr int NST = 4;
+    constexpr int GL = KR / RPI / 4;       // DMA instructions per wave per stage
+    constexpr int WT = TC / 2;             // wave tile (2 x 2 waves)
+    constexpr int UT = WT / 16;            // 16x16 sub-tiles per wave dimension
+    __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE];
+
+    const int b = xcd_remap(blockIdx.x, gridDim.x);          // a split's tiles on one XCD
+    const int s = b / g.tiles, t = b - s * g.tiles;
+    int ib, jb;
+    gram_tile(t, g.nb, &ib, &jb);
+    const bool diag = ib == jb;
+    const long r_begin = (long)s * g.rows;
+    const long r_end = min(g.M, r_begin + g.rows);
+    const int nsteps = r_end > r_begin ? (int)((r_end - r_begin + KR - 1) / KR) : 0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 1, wn = w & 1;
+
+    // ---- DMA sources: instruction i of this wave fills rows RPI*(w*GL+i) .. +RPI-1 ----
+    const _Float16* src[GL];
+    int srow[GL];
+#pragma unroll
+    for (int i = 0; i < GL; ++i) {
+        const int r = RPI * (w * GL + i) + lane / CPR;
+        const int P = lane % CPR;
+        const int f = 2 * ((r & 3) | (((r >> 3) & 1) << 2));
+        const int L = P ^ f;
+        const int ch = L < TC / 8 ? ib * TC + 8 * L : jb * TC + 8 * (L - TC / 8);
+        srow[i] = r;
+        src[i] = g.a + (r_begin + r) * g.C + ch;
+    }
+    const _Float16* zero = (const _Float16*)g_gram_zero_line;
+    auto issue = [&](int step) {
+        char* st = smem + (step & (NST - 1)) * STAGE;
+        const long rb = r_begin + (long)KR * step;
+#pragma unroll
+        for (int i = 0; i < GL; ++i) {
+            const bool in = rb + srow[i] < r_end;
+            gram_glds16(in ? (const void*)(src[i] + (long)KR * step * g.C) : (const void*)zero,
+                        st + RPI * (w * GL + i) * ROWB);
+        }
+    };
+
+    // ---- transposed fragment reads: lane 4q+p of 16-lane group gq supplies row
+    // 8gq+q (second read: +4 rows), channels c0+4p..+3 of the sub-tile ----
+    const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int r0 = 8 * gq + q;
+    const int f0 = 2 * ((r0 & 3) | (((r0 >> 3) & 1) << 2));
+    const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)smem;
+    unsigned aoff[UT], boff[UT];
+#pragma unroll
+    for (int u = 0; u < UT; ++u) {
+        const int ca = wm * WT + 16 * u, cb = TC + wn * WT + 16 * u;     // logical channel columns in the row
+        aoff[u] = lds0 + r0 * ROWB + 16 * (((ca >> 3) + (p >> 1)) ^ f0) + 8 * (p & 1);
+        boff[u] = lds0 + r0 * ROWB + 16 * (((cb >> 3) + (p >> 1)) ^ f0) + 8 * (p & 1);
+    }
+
+    f32x4 acc[UT][UT];
+    f32x4 accs[UT];
+#pragma unroll
+    for (int i = 0; i < UT; ++i) {
+        accs[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < UT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const bool sums = diag && wn == 0;                    // wave-uniform
+    f16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (_Float16)1.0f;
+
+    if (nsteps > 0) {
+#pragma unroll
+        for (int u = 0; u < NST - 1; ++u) issue(u);
+        for (int step = 0; step < nsteps; ++step) {
+            // this wave's DMA of `step` landed (NST-2 younger stages may stay in flight)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * GL) : "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            const unsigned so = (unsigned)((step & (NST - 1)) * STAGE);
+            f16x8 fa[UT], fb[UT];
+#pragma unroll
+            for (int u = 0; u < UT; ++u) {
+                fa[u] = gram_cat(gram_tr16<0>(aoff[u] + so), gram_tr16<4 * ROWB>(aoff[u] + so));
+                fb[u] = gram_cat(gram_tr16<0>(boff[u] + so), gram_tr16<4 * ROWB>(boff[u] + so));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            // stage step+NST-1 goes into the buffer stage step-1 used: every wave
+            // finished reading it before this step's barrier
+            issue(step + NST - 1);
+#pragma unroll
+            for (int i = 0; i < UT; ++i)
+#pragma unroll
+                for (int j = 0; j < UT; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            if (sums) {
+#pragma unroll
+                for (int i = 0; i < UT; ++i)
+                    accs[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], ones, accs[i], 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // the trailing (zero) DMAs
+    }
+
+    // ---- partials: accumulator order [s][t][w][i][j][lane][4] (f32x4 stores) ----
+    f32x4* out = (f32x4*)g.part + ((long)(s * g.tiles + t) * 4 + w) * (UT * UT * 64);
+#pragma unroll
+    for (int i = 0; i < UT; ++i)
+#pragma unroll
+        for (int j = 0; j < UT; ++j) out[(i * UT + j) * 64 + lane] = acc[i][j];
+    if (sums && (lane & 15) == 0) {
+        float* ps = g.psum + ((long)s * g.nb + ib) * TC + wm * WT + 4 * gq;
+#pragma unroll
+        for (int i = 0; i < UT; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ps[16 * i + r] = accs[i][r];
+    }
+}
+
+// mu[c] = sum over splits (fixed order, fp64) of the column-sum partials / M
+__global__ __launch_bounds__(256) void gram_mean_kernel(int C, int TC, int splits, long M, const float* psum,
+                                                        double* mu) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const int nb = C / TC, ib = c / TC, cc = c - ib * TC;
+    double s = 0.0;
+    for (int k = 0; k < splits; ++k) s += (double)psum[((long)k * nb + ib) * TC + cc];
+    mu[c] = s / (double)M;
+}
+
+// Sigma[i][j] = Sigma[j][i] = sum over splits (fixed order, fp64) / M - mu_i mu_j;
+// one thread per element of an upper-triangle tile, in accumulator order
+__global__ __launch_bounds__(256) void gram_cov_kernel(int C, int TC, int tiles, int splits, long M, const float* part,
+                                                       const double* mu, double* cov) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long per = (long)TC * TC;
+    if (e >= per * tiles) return;
+    const int t = (int)(e / per), x = (int)(e - (long)t * per);
+    // x = ((w * UT + i) * UT + j) * 256 + lane * 4 + r   (UT = TC / 32)
+    const int UT = TC / 32, WT = TC / 2;
+    const int r = x & 3, lane = (x >> 2) & 63, ij = x >> 8;
+    const int j = ij % UT, i = (ij / UT) % UT, w = ij / (UT * UT);
+    const int wm = w >> 1, wn = w & 1;
+    int ib, jb;
+    gram_tile(t, C / TC, &ib, &jb);
+    const int ci = ib * TC + wm * WT + 16 * i + 4 * (lane >> 4) + r;
+    const int cj = jb * TC + wn * WT + 16 * j + (lane & 15);
+    double s = 0.0;
+    for (int k = 0; k < splits; ++k) s += (double)part[((long)k * tiles + t) * per + x];
+    const double v = s / (double)M - mu[ci] * mu[cj];
+    cov[(long)ci * C + cj] = v;
+    cov[(long)cj * C + ci] = v;
+}
+
+// Per output channel k of y = W a: mean = w_k . mu, var = w_k^T Sigma w_k (fp64,
+// w_k = the fp16 packed weight row x its inverse scale: the weights the conv
+// multiplies with), then bn_fin_store.  A block takes KB channels; each wave a
+// quarter of Sigma's rows, each lane a slice of its columns; per-lane partial
+// quadratic forms, summed over the block in fixed order.
+constexpr int BFG_KB = 8;
+__global__ __launch_bounds__(256) void bn_from_gram_kernel(int K, int C, long count, const double* mu,
+                                                           const double* cov, const _Float16* w16,
+                                                           const float* w_inv_scale, const float* gamma,
+                                                           const float* beta, float momentum, float eps,
+                                                           float* rmean, float* rvar, int64_t* nbt, float* ss,
+                                                           float* mi) {
+    extern __shared__ double wsh[];                        // [KB][C]
+    __shared__ double red[4][BFG_KB][2];
+    const int k0 = blockIdx.x * BFG_KB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int e = tid; e < BFG_KB * C; e += 256) {
+        const int kk = e / C, c = e - kk * C;
+        const int k = k0 + kk;
+        wsh[e] = k < K ? (double)(float)w16[(long)k * C + c] * (double)w_inv_scale[k] : 0.0;
+    }
+    __syncthreads();
+    double q[BFG_KB], m[BFG_KB];
+#pragma unroll
+    for (int kk = 0; kk < BFG_KB; ++kk) q[kk] = m[kk] = 0.0;
+    for (int i = w; i < C; i += 4) {
+        double wi[BFG_KB];
+#pragma unroll
+        for (int kk = 0; kk < BFG_KB; ++kk) wi[kk] = wsh[kk * C + i];
+        for (int j = lane; j < C; j += 64) {
+            const double gij = cov[(long)i * C + j];
+#pragma unroll
+            for (int kk = 0; kk < BFG_KB; ++kk) q[kk] += wi[kk] * (gij * wsh[kk * C + j]);
+        }
+        if (lane == 0) {
+            const double mui = mu[i];
+#pragma unroll
+            for (int kk = 0; kk < BFG_KB; ++kk) m[kk] += wi[kk] * mui;
+        }
+    }
+#pragma unroll
+    for (int kk = 0; kk < BFG_KB; ++kk) {
+        double v = q[kk], u = m[kk];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            v += __shfl_xor(v, o);
+            u += __shfl_xor(u, o);
+        }
+        if (lane == 0) {
+            red[w][kk][0] = v;
+            red[w][kk][1] = u;
+        }
+    }
+    __syncthreads();
+    if (tid < BFG_KB && k0 + tid < K) {
+        double v = 0.0, u = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            v += red[ww][tid][0];
+            u += red[ww][tid][1];
+        }
+        v = v > 0.0 ? v : 0.0;
+        bn_fin_store(k0 + tid, K, count, u, v * (double)count, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+    }
+}
+
+static int gram_tc(int c) { return c % 128 == 0 ? 128 : 64; }
+
+// rows per split: about two blocks per CU over all tiles, >= 32 rows, <= 16k rows
+// (fp32 accumulation inside a split; fp64 across splits)
+static void gram_plan(long m, int c, int* tc, int* tiles, int* splits, long* rows) {
+    *tc = gram_tc(c);
+    const int nb = c / *tc;
+    *tiles = nb * (nb + 1) / 2;
+    long sp = std::max<long>(1, 512 / *tiles);
+    long r = (m + sp - 1) / sp;
+    if (r > 16384) r = 16384;
+    r = (r + 31) / 32 * 32;
+    *rows = r;
+    *splits = (int)((m + r - 1) / r);
+}
+
+}  // namespace hkp
+
+using namespace hkp;
+
+extern "C" int64_t hkp_gram_f16_workspace_bytes(int64_t m, int32_t c) {
+    if (m <= 0 || c <= 0 || c % 64) return -1;
+    int tc, tiles, splits;
+    long rows;
+    gram_plan(m, c, &tc, &tiles, &splits, &rows);
+    return (int64_t)splits * tiles * tc * tc * 4 + (int64_t)splits * (c / tc) * tc * 4 + 256;
+}
+
+extern "C" int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* cov, void* ws,
+                            int64_t ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(m > 0 && m < (1L << 40) && c > 0 && c % 64 == 0 && c <= 2048 && a && mean && cov && ws,
+                  "hkp_gram_f16: bad args (m=%lld c=%d)", (long long)m, c);
+    HKP_CHECK_ARG(ws_bytes >= hkp_gram_f16_workspace_bytes(m, c), "hkp_gram_f16: workspace too small");
+    int tc, tiles, splits;
+    long rows;
+    gram_plan(m, c, &tc, &tiles, &splits, &rows);
+    GramArgs g;
+    g.a = (const _Float16*)a;
+    g.part = (float*)ws;
+    g.psum = (float*)ws + (long)splits * tiles * tc * tc;
+    g.M = m;
+    g.C = c;
+    g.nb = c / tc;
+    g.tiles = tiles;
+    g.splits = splits;
+    g.rows = rows;
+    hipStream_t st = as_stream(stream);
+    const dim3 grid((unsigned)(splits * tiles));
+    if (tc == 128) hipLaunchKernelGGL(gram_f16_kernel<128>, grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL(gram_f16_kernel<64>, grid, dim3(256), 0, st, g);
+    hipLaunchKernelGGL(gram_mean_kernel, dim3((c + 255) / 256), dim3(256), 0, st, c, tc, splits, (long)m, g.psum,
+                       mean);
+    const long n = (long)tiles * tc * tc;
+    hipLaunchKernelGGL(gram_cov_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c, tc, tiles, splits,
+                       (long)m, (const float*)g.part, (const double*)mean, cov);
+    HKP_LAUNCH_CHECK("hkp_gram_f16");
+    return HKP_OK;
+}
+
+extern "C" int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* cov,
+                                const uint16_t* w_f16, const float* w_inv_scale, const float* gamma,
+                                const float* beta, float momentum, float eps, float* running_mean,
+                                float* running_var, int64_t* num_batches_tracked, float* scale_shift,
+                                float* mean_invstd, hkp_stream_t stream) {
+    HKP_CHECK_ARG(k > 0 && c > 0 && c <= 1024 && count > 0 && mean && cov && w_f16 && w_inv_scale && scale_shift,
+                  "hkp_bn_from_gram: bad args");
+    const size_t sh = (size_t)BFG_KB * c * sizeof(double);
+    hipLaunchKernelGGL(bn_from_gram_kernel, dim3((unsigned)((k + BFG_KB - 1) / BFG_KB)), dim3(256), sh,
+                       as_stream(stream), k, c, (long)count, mean, cov, (const _Float16*)w_f16, w_inv_scale, gamma,
+                       beta, momentum, eps, running_mean, running_var, num_batches_tracked, scale_shift,
+                       mean_invstd);
+    HKP_LAUNCH_CHECK("hkp_bn_from_gram");
+    return HKP_OK;
+}

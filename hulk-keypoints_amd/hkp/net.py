@@ -335,6 +335,8 @@ def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_c
         y, s, m = conv_bn(conv, bn, a, pol)
         a = act(y, s, convs[i + 1])
         ys.append(y), sss.append(s), mis.append(m), acts.append(a)
+    if rec is None and head is None and not final and _gram_fusable(block, a, pol):
+        return _bottleneck_tail_gram(block, x, a, pol)
     # the last conv and the downsample conv, then both BN parameter sets together
     y_last, part_last = _conv_fwd(convs[-1], bns[-1], a, pol)
     items = [(bns[-1], part_last, y_last.numel() // y_last.shape[-1])]
@@ -373,6 +375,44 @@ def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_c
         rec["out"] = out
         trace.blocks.append(rec)
     return out
+
+
+def _gram_fusable(block, a, pol):
+    """Plain-fp16 inference Bottleneck whose conv3 (1x1, stride 1) can take its
+    bn3 parameters from its input's covariance (hkp_gram_f16 + hkp_bn_from_gram)
+    and apply bn3 + residual + ReLU in its epilogue."""
+    if not (pol.gram_bn and pol.precision == "f16" and block.kind == "bottleneck"):
+        return False
+    if parallel.active_sync_group(pol) is not None:    # (statistics per rank only)
+        return False
+    c3 = block.conv3
+    k, r, s, c = c3.weight.shape
+    return ((r, s, _i(c3.stride), _i(c3.padding)) == (1, 1, 1, 0) and _f16_conv_ok(c3) and c <= 1024
+            and a.dtype == torch.float16 and getattr(a, "_hkp_split_passes", 0) == 1)
+
+
+def _bottleneck_tail_gram(block, x, a2, pol):
+    """conv3 → bn3 → (+ residual | + bn(downsample(x))) → ReLU of a plain-fp16
+    inference Bottleneck (src/resnet.py:104-110) in one conv launch: train-mode
+    bn3's batch statistics are exact functions of conv3's input statistics
+    (mean = w.mu, var = w^T Sigma w), so the scale/shift is known before conv3
+    runs and its epilogue writes the block output — y3 is never materialised and
+    no separate apply pass reads it (hkp_conv2d_fwd_f16_bn)."""
+    c3, bn3 = block.conv3, block.bn3
+    wp = _cached_split(c3.weight, "f16", ops.weight_pack_f16)
+    count = a2.numel() // a2.shape[-1]
+    if bn3.training:
+        mean, cov = ops.gram_f16(a2)
+        ss3, _ = ops.bn_from_gram(mean, cov, wp, count, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var,
+                                  bn3.num_batches_tracked, **_finalize_args(bn3))
+    else:
+        ss3, _ = ops.bn_eval_params(bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps)
+    x16 = x if x.dtype == torch.float16 else ops.split_of(x)[0]
+    if block.downsample is not None:
+        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], x16, pol)
+        sd, _ = _bn_params(block.downsample[1], part_d, yd.numel() // yd.shape[-1], pol)
+        return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=yd, res_ss=sd, relu=True)
+    return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=x16, relu=True)
 
 
 def _blocks(resnet):

@@ -246,6 +246,91 @@ def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0)
     return y, part
 
 
+def conv2d_fwd_f16_bn(x16, wp, ss, res=None, res_ss=None, relu=True, stride=1, pad=0, dil=1, sk=True, tile=0):
+    """conv2d_fwd_f16 with the output's BN apply fused into the epilogue
+    (hkp_conv2d_fwd_f16_bn): fp16 out = [relu](y*scale + shift [+ res | + res*rscale
+    + rshift]) — what conv2d_fwd_f16 + bn_apply_f16 return with the same ss, y
+    never written.  ss [2K] must be known before the conv (bn_from_gram, or
+    eval-mode BN).  Returns the fp16 activation (a split=1 operand)."""
+    ws, wsc = wp
+    _need(x16, torch.float16, "conv2d_fwd_f16_bn.x", 4)
+    _need(ws, torch.float16, "conv2d_fwd_f16_bn.w", 4)
+    _need(wsc, torch.float32, "conv2d_fwd_f16_bn.w_inv_scale", 1)
+    _need(ss, torch.float32, "conv2d_fwd_f16_bn.scale_shift", 1)
+    n, h, wd, c = x16.shape
+    k, r, s_, cw = ws.shape
+    if cw != c:
+        raise HkpError("conv2d_fwd_f16_bn: weight Cin %d != input C %d" % (cw, c))
+    if ss.numel() != 2 * k:
+        raise HkpError("conv2d_fwd_f16_bn: scale_shift size %d != 2K" % ss.numel())
+    ho, wo = conv_out_hw(h, wd, r, s_, stride, pad, dil)
+    if res is not None:
+        _need(res, torch.float16, "conv2d_fwd_f16_bn.res", 4)
+        if tuple(res.shape) != (n, ho, wo, k):
+            raise HkpError("conv2d_fwd_f16_bn: residual %s != %s" % (tuple(res.shape), (n, ho, wo, k)))
+    if res_ss is not None:
+        _need(res_ss, torch.float32, "conv2d_fwd_f16_bn.res_scale_shift", 1)
+        if res is None or res_ss.numel() != 2 * k:
+            raise HkpError("conv2d_fwd_f16_bn: res_scale_shift needs a residual and 2K entries")
+    d = ConvDesc(n, h, wd, c, k, r, s_, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
+    out = _split_out((n, ho, wo, k), x16.device, 1)
+
+    def launch():
+        call("hkp_conv2d_fwd_f16_bn", ctypes.byref(d), _ptr(x16), _ptr(ws), _ptr(wsc), _ptr(ss), _ptr(res),
+             _ptr(res_ss), int(bool(relu)), _ptr(out), *_sk_workspace(sk), _stream())
+
+    if _observer is None:
+        launch()
+    else:
+        _observer(kernel_name(d, HKP_KOP_FWD_F16, sk), 2.0 * n * ho * wo * k * r * s_ * c,
+                  2.0 * (x16.numel() + ws.numel() + out.numel() + (res.numel() if res is not None else 0)), launch)
+    return out
+
+
+def gram_f16(a16):
+    """Mean and covariance of the channels of an fp16 activation [.., C] over all
+    its pixels (hkp_gram_f16) → (mean fp64 [C], cov fp64 [C, C])."""
+    from ._lib import lib
+    _need(a16, torch.float16, "gram_f16.a")
+    c = a16.shape[-1]
+    m = a16.numel() // c
+    nb = lib().hkp_gram_f16_workspace_bytes(m, c)
+    if nb < 0:
+        raise HkpError("gram_f16: unsupported shape (m=%d c=%d)" % (m, c))
+    ws = torch.empty((nb + 7) // 8, device=a16.device, dtype=torch.float64)
+    mean = torch.empty(c, device=a16.device, dtype=torch.float64)
+    cov = torch.empty((c, c), device=a16.device, dtype=torch.float64)
+    call("hkp_gram_f16", m, c, _ptr(a16), _ptr(mean), _ptr(cov), _ptr(ws), nb, _stream())
+    return mean, cov
+
+
+def bn_from_gram(mean, cov, wp, count, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None,
+                 momentum=0.1, eps=1e-5):
+    """Train-mode BN parameters of the output of a 1x1 conv with packed fp16 weight
+    wp (weight_pack_f16 of [K,1,1,C]) from its input's mean / covariance
+    (gram_f16) → (scale_shift [2K], mean_invstd [2K]); running stats updated as
+    bn_finalize does."""
+    ws, wsc = wp
+    _need(mean, torch.float64, "bn_from_gram.mean", 1)
+    _need(cov, torch.float64, "bn_from_gram.cov", 2)
+    _need(ws, torch.float16, "bn_from_gram.w", 4)
+    k, r, s_, c = ws.shape
+    if (r, s_) != (1, 1) or mean.numel() != c or tuple(cov.shape) != (c, c):
+        raise HkpError("bn_from_gram: needs a 1x1 weight over the gram's %d channels (got %s)"
+                       % (mean.numel(), tuple(ws.shape)))
+    for t, nm in ((gamma, "gamma"), (beta, "beta"), (running_mean, "running_mean"), (running_var, "running_var")):
+        if t is not None:
+            _need(t, torch.float32, "bn_from_gram." + nm, 1)
+            if t.numel() != k:
+                raise HkpError("bn_from_gram.%s: %d != K=%d" % (nm, t.numel(), k))
+    ss = torch.empty(2 * k, device=ws.device, dtype=torch.float32)
+    mi = torch.empty(2 * k, device=ws.device, dtype=torch.float32)
+    call("hkp_bn_from_gram", k, c, int(count), _ptr(mean), _ptr(cov), _ptr(ws), _ptr(wsc), _ptr(gamma), _ptr(beta),
+         momentum, eps, _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi),
+         _stream())
+    return ss, mi
+
+
 def stem_x3_ok(x_shape, w_shape, stride, pad, dil):
     """Whether the stem conv (NCHW x, OIHW w) takes the f16x3 stem kernel."""
     def one(v):

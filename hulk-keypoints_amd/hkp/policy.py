@@ -42,6 +42,9 @@ class Policy:
     prepack_plan: bool = True
     # BN finalize: two-level merge from this many partial tiles on
     fin_two_level_tiles: int = 2048
+    # plain fp16 inference (C4): a Bottleneck's bn3 statistics from conv3's input
+    # covariance (1x1 conv: exact), bn3 + residual + ReLU in conv3's epilogue
+    gram_bn: bool = True
 
     def __post_init__(self):
         if self.precision not in PRECISIONS:

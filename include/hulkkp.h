@@ -131,6 +131,38 @@ int hkp_weight_pack_f16(int32_t k, int32_t rsc, const float* w, uint16_t* w_f16,
 int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
                        const float* w_inv_scale, uint16_t* y_f16, float* stat_partials, void* sk_workspace,
                        int64_t sk_ws_bytes, hkp_stream_t stream);
+/* The plain-fp16 conv with the output's train-mode BN apply fused into its
+ * epilogue (config C4's Bottleneck tail, src/resnet.py:106-110: bn3, + residual,
+ * ReLU): out_f16 = [relu](y*scale + shift [+ res | + res*rscale + rshift]) on the
+ * fp16-rounded conv output y — hkp_bn_apply_f16's arithmetic, so the result is
+ * what hkp_conv2d_fwd_f16 + hkp_bn_apply_f16 give with the same scale_shift [2k].
+ * y is never written.  res_f16 [n*ho*wo][k] (nullable), res_scale_shift [2k]
+ * (nullable: raw residual).  The scale/shift must be known before the conv:
+ * eval-mode BN, or train-mode statistics from the input's second moments
+ * (hkp_gram_f16 + hkp_bn_from_gram, 1x1 convs).  Not with the persistent tile
+ * policies.  Stream-K workspace as hkp_conv2d_fwd_x3. */
+int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
+                          const float* w_inv_scale, const float* scale_shift, const uint16_t* res_f16,
+                          const float* res_scale_shift, int32_t relu, uint16_t* out_f16, void* sk_workspace,
+                          int64_t sk_ws_bytes, hkp_stream_t stream);
+/* Train-mode BN statistics of a 1x1 conv's output y = W a without a pass over y
+ * (replaces the batch statistics of bn3, src/resnet.py:106-108, for
+ * hkp_conv2d_fwd_f16_bn): hkp_gram_f16 reduces the fp16 input a [m][c] (c % 64
+ * == 0, c <= 2048) to its mean mu [c] and covariance Sigma [c][c] (fp64; fp32
+ * MFMA partials over row splits of <= 16 k rows, merged in fp64 in fixed order;
+ * workspace hkp_gram_f16_workspace_bytes(m, c)); hkp_bn_from_gram takes, per
+ * output channel k of the packed fp16 weight w_f16 [k][c] (x w_inv_scale[k],
+ * hkp_weight_pack_f16 — the weights the conv multiplies with), mean = w.mu and
+ * var = w^T Sigma w (fp64), and writes hkp_bn_finalize's outputs from them
+ * (scale_shift, mean_invstd (nullable), running stats with the unbiased
+ * variance, num_batches_tracked += 1).  c <= 1024 for hkp_bn_from_gram. */
+int64_t hkp_gram_f16_workspace_bytes(int64_t m, int32_t c);
+int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* cov, void* workspace,
+                 int64_t ws_bytes, hkp_stream_t stream);
+int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* cov,
+                     const uint16_t* w_f16, const float* w_inv_scale, const float* gamma, const float* beta,
+                     float momentum, float eps, float* running_mean, float* running_var,
+                     int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd, hkp_stream_t stream);
 /* The kernel a launch with descriptor d runs — its template name as rocprofv3
  * reports it (e.g. "conv_x3_kernel<256, false, false, 16, false, 3>"), for
  * profiling / roofline attribution.  op: HKP_KOP_*; stream_k_ok: whether the
