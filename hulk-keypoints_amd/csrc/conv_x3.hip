@@ -487,8 +487,31 @@ __device__ __forceinline__ void x3_store_tile_f16(const X3Args& a, const char* s
 // (scale, shift, residual scale, residual shift of the tile's columns).  A
 // thread always handles the same 8 channels (512 % (BN/8) == 0).
 template <int BN>
-__device__ __forceinline__ void x3_store_tile_f16_bn(const X3Args& a, const char* smem, const float* ssl, int m0,
-                                                     int n0, int tid) {
+struct X3Res {
+    static constexpr int NPT = 256 * (BN / 8) / 512;     // 16-B chunks per thread
+    f16x8 r[NPT];
+};
+// the residual chunks this thread's store loop will use, loaded before the tile
+// is staged (the loads of a whole tile in flight at once: a per-chunk load in
+// the store loop exposed its HBM latency ~4 times per tile)
+template <int BN>
+__device__ __forceinline__ X3Res<BN> x3_ep_res_load(const X3Args& a, int m0, int n0, int tid) {
+    constexpr int CH = BN / 8;
+    X3Res<BN> res;
+    const int cc = tid % CH;
+#pragma unroll
+    for (int u = 0; u < X3Res<BN>::NPT; ++u) {
+        const int row = (tid + 512 * u) / CH, m = m0 + row;
+        res.r[u] = f16x8{};
+        if (a.ep_res && m < a.M)
+            res.r[u] = __builtin_nontemporal_load((const f16x8*)(a.ep_res + (long)m * a.K + n0 + cc * 8));
+    }
+    return res;
+}
+
+template <int BN>
+__device__ __forceinline__ void x3_store_tile_f16_bn(const X3Args& a, const char* smem, const float* ssl,
+                                                     const X3Res<BN>& res, int m0, int n0, int tid) {
     constexpr int CH = BN / 8, PITCH = BN + 8;
     static_assert(512 % CH == 0, "fixed channels per thread");
     const int cc = tid % CH;
@@ -500,21 +523,20 @@ __device__ __forceinline__ void x3_store_tile_f16_bn(const X3Args& a, const char
         ra[e] = ssl[2 * BN + cc * 8 + e];
         rb[e] = ssl[3 * BN + cc * 8 + e];
     }
-    const bool res = a.ep_res != nullptr, rsc = a.ep_rss != nullptr, relu = a.ep_relu != 0;
-#pragma unroll 4
-    for (int e = tid; e < 256 * CH; e += 512) {
-        const int row = e / CH;
+    const bool hres = a.ep_res != nullptr, rsc = a.ep_rss != nullptr, relu = a.ep_relu != 0;
+#pragma unroll
+    for (int u = 0; u < X3Res<BN>::NPT; ++u) {
+        const int row = (tid + 512 * u) / CH;
         const int m = m0 + row;
         if (m >= a.M) continue;
         const long off = (long)m * a.K + n0 + cc * 8;
         const f16x8 v = *(const f16x8*)(smem + (row * PITCH + cc * 8) * 2);
-        f16x8 r = {};
-        if (res) r = __builtin_nontemporal_load((const f16x8*)(a.ep_res + off));
+        const f16x8 r = res.r[u];
         f16x8 h;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             float o = __fadd_rn(__fmul_rn((float)v[k], sa[k]), sb[k]);
-            if (res) o = rsc ? __fadd_rn(o, __fadd_rn(__fmul_rn((float)r[k], ra[k]), rb[k])) : __fadd_rn(o, (float)r[k]);
+            if (hres) o = rsc ? __fadd_rn(o, __fadd_rn(__fmul_rn((float)r[k], ra[k]), rb[k])) : __fadd_rn(o, (float)r[k]);
             if (relu) o = o > 0.f ? o : 0.f;
             h[k] = (_Float16)o;
         }
@@ -739,6 +761,8 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
         }
         const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
+        X3Res<BN> eres;
+        if (a.ep_ss) eres = x3_ep_res_load<BN>(a, m0, n0, tid);
         lds_sync();                        // the ring is free
         x3_stamp(a, 3);
         _Float16* t = (_Float16*)smem;
@@ -756,7 +780,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         if (a.ep_ss) x3_ep_store<BN>((float*)(smem + SS_OFF), eps, tid);
         lds_sync();
         x3_stamp(a, 4);
-        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), m0, n0, tid);
+        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), eres, m0, n0, tid);
         else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
         x3_stamp(a, 5);
         return;
@@ -1076,6 +1100,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
                 a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
                 [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); });
         const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
+        X3Res<BN> eres;
+        if (a.ep_ss) eres = x3_ep_res_load<BN>(a, m0, n0, tid);
         __syncthreads();
         _Float16* t = (_Float16*)smem;
         constexpr int PITCH = BN + 8;
@@ -1091,7 +1117,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
                       frow] = (_Float16)acc[i][j][r];
         if (a.ep_ss) x3_ep_store<BN>((float*)(smem + SS_OFF), eps, tid);
         __syncthreads();
-        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), m0, n0, tid);
+        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), eres, m0, n0, tid);
         else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
         return;
     }

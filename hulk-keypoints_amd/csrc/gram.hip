@@ -16,9 +16,10 @@
 //                         tiles; both MFMA operands read TRANSPOSED
 //                         (ds_read_b64_tr_b16) from one row-major LDS image filled
 //                         by LDS-DMA; column sums by one extra MFMA against ones
-//   gram_mean_kernel      mu = sum over splits (fp64, fixed order) / M
-//   gram_cov_kernel       Sigma = sum over splits (fp64, fixed order) / M - mu mu^T
-//   bn_from_gram_kernel   per output channel: mean, var (fp64) -> bn_fin_store
+//   gram_reduce_kernel    mu and the second moments E = a^T a / M: the row splits
+//                         summed in fp64 in fixed order
+//   bn_from_gram_kernel   per output channel: mean = w.mu, var = w^T E w - mean^2
+//                         (fp64) -> bn_fin_store
 //                         (the same scale/shift/running-stat formulas as
 //                         hkp_bn_finalize)
 // Deterministic: every reduction is in a fixed order.
@@ -198,25 +199,39 @@ __global__ __launch_bounds__(256, 2) void gram_f16_kernel(GramArgs g) {
     }
 }
 
-// mu[c] = sum over splits (fixed order, fp64) of the column-sum partials / M
-__global__ __launch_bounds__(256) void gram_mean_kernel(int C, int TC, int splits, long M, const float* psum,
-                                                        double* mu) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
-    const int nb = C / TC, ib = c / TC, cc = c - ib * TC;
-    double s = 0.0;
-    for (int k = 0; k < splits; ++k) s += (double)psum[((long)k * nb + ib) * TC + cc];
-    mu[c] = s / (double)M;
-}
-
-// Sigma[i][j] = Sigma[j][i] = sum over splits (fixed order, fp64) / M - mu_i mu_j;
-// one thread per element of an upper-triangle tile, in accumulator order
-__global__ __launch_bounds__(256) void gram_cov_kernel(int C, int TC, int tiles, int splits, long M, const float* part,
-                                                       const double* mu, double* cov) {
-    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long per = (long)TC * TC;
-    if (e >= per * tiles) return;
-    const int t = (int)(e / per), x = (int)(e - (long)t * per);
+// One launch reduces the row splits (fp64, fixed split order; loads batched 8 at a
+// time): blocks [0, nel/256) the Gram elements — E[i][j] = E[j][i] = sum / M in
+// accumulator order of an upper-triangle tile — and the blocks after them the
+// column sums, mu[c] = sum / M.  Centring (Sigma = E - mu mu^T) happens in fp64
+// where the quadratic forms are taken (bn_from_gram_kernel).
+__global__ __launch_bounds__(256) void gram_reduce_kernel(int C, int TC, int tiles, int splits, long M,
+                                                          const float* part, const float* psum, double* mu,
+                                                          double* e2) {
+    const long per = (long)TC * TC, nel = per * tiles;
+    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long eblocks = (nel + 255) / 256;
+    const double inv = 1.0 / (double)M;
+    if ((long)blockIdx.x >= eblocks) {
+        const long c = gid - eblocks * 256;
+        if (c >= C) return;
+        const int nb = C / TC, ib = (int)(c / TC), cc = (int)(c - (long)ib * TC);
+        const float* p = psum + (long)ib * TC + cc;
+        const long st = (long)nb * TC;
+        double s = 0.0;
+        int k = 0;
+        for (; k + 8 <= splits; k += 8) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * st];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += (double)v[u];
+        }
+        for (; k < splits; ++k) s += (double)p[(long)k * st];
+        mu[c] = s * inv;
+        return;
+    }
+    if (gid >= nel) return;
+    const int t = (int)(gid / per), x = (int)(gid - (long)t * per);
     // x = ((w * UT + i) * UT + j) * 256 + lane * 4 + r   (UT = TC / 32)
     const int UT = TC / 32, WT = TC / 2;
     const int r = x & 3, lane = (x >> 2) & 63, ij = x >> 8;
@@ -226,76 +241,110 @@ __global__ __launch_bounds__(256) void gram_cov_kernel(int C, int TC, int tiles,
     gram_tile(t, C / TC, &ib, &jb);
     const int ci = ib * TC + wm * WT + 16 * i + 4 * (lane >> 4) + r;
     const int cj = jb * TC + wn * WT + 16 * j + (lane & 15);
+    const float* p = part + (long)t * per + x;
+    const long st = (long)tiles * per;
     double s = 0.0;
-    for (int k = 0; k < splits; ++k) s += (double)part[((long)k * tiles + t) * per + x];
-    const double v = s / (double)M - mu[ci] * mu[cj];
-    cov[(long)ci * C + cj] = v;
-    cov[(long)cj * C + ci] = v;
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * st];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; k < splits; ++k) s += (double)p[(long)k * st];
+    const double v = s * inv;
+    e2[(long)ci * C + cj] = v;
+    e2[(long)cj * C + ci] = v;
 }
 
-// Per output channel k of y = W a: mean = w_k . mu, var = w_k^T Sigma w_k (fp64,
-// w_k = the fp16 packed weight row x its inverse scale: the weights the conv
-// multiplies with), then bn_fin_store.  A block takes KB channels; each wave a
-// quarter of Sigma's rows, each lane a slice of its columns; per-lane partial
-// quadratic forms, summed over the block in fixed order.
+// Per output channel k of y = W a: mean = w_k . mu and
+// var = w_k^T E w_k - mean^2 (E = the raw second moments; fp64 throughout — the
+// centring loses only log10(1 + mean^2/var) of fp64's digits), with w_k = the
+// fp16 packed weight row x its inverse scale (the weights the conv multiplies
+// with), then bn_fin_store.  A block takes BFG_KB channels (their weights in LDS,
+// read as broadcasts); thread t owns columns j = t, t + 256, ...: for every row i
+// it accumulates s_k[j] += E[i][j] w_k[i] (coalesced row loads of E, 8 rows in
+// flight), then q_k = sum_j s_k[j] w_k[j]; the threads' q_k are summed in fixed
+// order.
 constexpr int BFG_KB = 8;
+constexpr int BFG_MAXJ = 4;                      // C <= 1024
 __global__ __launch_bounds__(256) void bn_from_gram_kernel(int K, int C, long count, const double* mu,
-                                                           const double* cov, const _Float16* w16,
+                                                           const double* e2, const _Float16* w16,
                                                            const float* w_inv_scale, const float* gamma,
                                                            const float* beta, float momentum, float eps,
                                                            float* rmean, float* rvar, int64_t* nbt, float* ss,
                                                            float* mi) {
-    extern __shared__ double wsh[];                        // [KB][C]
-    __shared__ double red[4][BFG_KB][2];
+    extern __shared__ double wsh[];                        // [C][KB]: row i's KB weights contiguous
+    __shared__ double red[256][BFG_KB];
     const int k0 = blockIdx.x * BFG_KB;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x;
     for (int e = tid; e < BFG_KB * C; e += 256) {
-        const int kk = e / C, c = e - kk * C;
+        const int i = e / BFG_KB, kk = e - i * BFG_KB;
         const int k = k0 + kk;
-        wsh[e] = k < K ? (double)(float)w16[(long)k * C + c] * (double)w_inv_scale[k] : 0.0;
+        wsh[e] = k < K ? (double)(float)w16[(long)k * C + i] * (double)w_inv_scale[k] : 0.0;
     }
     __syncthreads();
+    const int nj = (C - tid + 255) / 256;                  // columns of this thread (C % 64 == 0)
+    double s[BFG_MAXJ][BFG_KB];
+#pragma unroll
+    for (int u = 0; u < BFG_MAXJ; ++u)
+#pragma unroll
+        for (int kk = 0; kk < BFG_KB; ++kk) s[u][kk] = 0.0;
+    for (int i0 = 0; i0 < C; i0 += 8) {
+        double ev[8][BFG_MAXJ];
+#pragma unroll
+        for (int di = 0; di < 8; ++di)
+#pragma unroll
+            for (int u = 0; u < BFG_MAXJ; ++u) ev[di][u] = u < nj ? e2[(long)(i0 + di) * C + tid + 256 * u] : 0.0;
+#pragma unroll
+        for (int di = 0; di < 8; ++di) {
+            const double* wi = wsh + (i0 + di) * BFG_KB;
+#pragma unroll
+            for (int kk = 0; kk < BFG_KB; ++kk) {
+                const double w = wi[kk];
+#pragma unroll
+                for (int u = 0; u < BFG_MAXJ; ++u) s[u][kk] += ev[di][u] * w;
+            }
+        }
+    }
     double q[BFG_KB], m[BFG_KB];
 #pragma unroll
     for (int kk = 0; kk < BFG_KB; ++kk) q[kk] = m[kk] = 0.0;
-    for (int i = w; i < C; i += 4) {
-        double wi[BFG_KB];
 #pragma unroll
-        for (int kk = 0; kk < BFG_KB; ++kk) wi[kk] = wsh[kk * C + i];
-        for (int j = lane; j < C; j += 64) {
-            const double gij = cov[(long)i * C + j];
+    for (int u = 0; u < BFG_MAXJ; ++u) {
+        if (u < nj) {
+            const int j = tid + 256 * u;
+            const double muj = mu[j];
 #pragma unroll
-            for (int kk = 0; kk < BFG_KB; ++kk) q[kk] += wi[kk] * (gij * wsh[kk * C + j]);
-        }
-        if (lane == 0) {
-            const double mui = mu[i];
-#pragma unroll
-            for (int kk = 0; kk < BFG_KB; ++kk) m[kk] += wi[kk] * mui;
+            for (int kk = 0; kk < BFG_KB; ++kk) {
+                const double wj = wsh[j * BFG_KB + kk];
+                q[kk] += s[u][kk] * wj;
+                m[kk] += muj * wj;
+            }
         }
     }
 #pragma unroll
-    for (int kk = 0; kk < BFG_KB; ++kk) {
-        double v = q[kk], u = m[kk];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            v += __shfl_xor(v, o);
-            u += __shfl_xor(u, o);
-        }
-        if (lane == 0) {
-            red[w][kk][0] = v;
-            red[w][kk][1] = u;
-        }
+    for (int kk = 0; kk < BFG_KB; ++kk) red[tid][kk] = q[kk];
+    __syncthreads();
+    if (tid < BFG_KB) {
+        double v = 0.0;
+        for (int t2 = 0; t2 < 256; ++t2) v += red[t2][tid];
+        q[0] = v;
     }
     __syncthreads();
-    if (tid < BFG_KB && k0 + tid < K) {
-        double v = 0.0, u = 0.0;
+    // the means: the same fixed-order sum over threads
+    const double qk = tid < BFG_KB ? q[0] : 0.0;
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) {
-            v += red[ww][tid][0];
-            u += red[ww][tid][1];
-        }
-        v = v > 0.0 ? v : 0.0;
-        bn_fin_store(k0 + tid, K, count, u, v * (double)count, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+    for (int kk = 0; kk < BFG_KB; ++kk) red[tid][kk] = m[kk];
+    __syncthreads();
+    if (tid < BFG_KB && k0 + tid < K) {
+        double mean = 0.0;
+        for (int t2 = 0; t2 < 256; ++t2) mean += red[t2][tid];
+        double var = qk - mean * mean;
+        var = var > 0.0 ? var : 0.0;
+        bn_fin_store(k0 + tid, K, count, mean, var * (double)count, gamma, beta, momentum, eps, rmean, rvar, nbt, ss,
+                     mi);
     }
 }
 
@@ -327,9 +376,9 @@ extern "C" int64_t hkp_gram_f16_workspace_bytes(int64_t m, int32_t c) {
     return (int64_t)splits * tiles * tc * tc * 4 + (int64_t)splits * (c / tc) * tc * 4 + 256;
 }
 
-extern "C" int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* cov, void* ws,
+extern "C" int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* second, void* ws,
                             int64_t ws_bytes, hkp_stream_t stream) {
-    HKP_CHECK_ARG(m > 0 && m < (1L << 40) && c > 0 && c % 64 == 0 && c <= 2048 && a && mean && cov && ws,
+    HKP_CHECK_ARG(m > 0 && m < (1L << 40) && c > 0 && c % 64 == 0 && c <= 2048 && a && mean && second && ws,
                   "hkp_gram_f16: bad args (m=%lld c=%d)", (long long)m, c);
     HKP_CHECK_ARG(ws_bytes >= hkp_gram_f16_workspace_bytes(m, c), "hkp_gram_f16: workspace too small");
     int tc, tiles, splits;
@@ -349,25 +398,25 @@ extern "C" int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mea
     const dim3 grid((unsigned)(splits * tiles));
     if (tc == 128) hipLaunchKernelGGL(gram_f16_kernel<128>, grid, dim3(256), 0, st, g);
     else hipLaunchKernelGGL(gram_f16_kernel<64>, grid, dim3(256), 0, st, g);
-    hipLaunchKernelGGL(gram_mean_kernel, dim3((c + 255) / 256), dim3(256), 0, st, c, tc, splits, (long)m, g.psum,
-                       mean);
-    const long n = (long)tiles * tc * tc;
-    hipLaunchKernelGGL(gram_cov_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c, tc, tiles, splits,
-                       (long)m, (const float*)g.part, (const double*)mean, cov);
+    const long nel = (long)tiles * tc * tc;
+    const long blocks = (nel + 255) / 256 + (c + 255) / 256;
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, c, tc, tiles, splits, (long)m,
+                       (const float*)g.part, (const float*)g.psum, mean, second);
     HKP_LAUNCH_CHECK("hkp_gram_f16");
     return HKP_OK;
 }
 
-extern "C" int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* cov,
+extern "C" int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* second,
                                 const uint16_t* w_f16, const float* w_inv_scale, const float* gamma,
                                 const float* beta, float momentum, float eps, float* running_mean,
                                 float* running_var, int64_t* num_batches_tracked, float* scale_shift,
                                 float* mean_invstd, hkp_stream_t stream) {
-    HKP_CHECK_ARG(k > 0 && c > 0 && c <= 1024 && count > 0 && mean && cov && w_f16 && w_inv_scale && scale_shift,
+    HKP_CHECK_ARG(k > 0 && c > 0 && c <= 1024 && c % 64 == 0 && count > 0 && mean && second && w_f16 && w_inv_scale &&
+                      scale_shift,
                   "hkp_bn_from_gram: bad args");
     const size_t sh = (size_t)BFG_KB * c * sizeof(double);
     hipLaunchKernelGGL(bn_from_gram_kernel, dim3((unsigned)((k + BFG_KB - 1) / BFG_KB)), dim3(256), sh,
-                       as_stream(stream), k, c, (long)count, mean, cov, (const _Float16*)w_f16, w_inv_scale, gamma,
+                       as_stream(stream), k, c, (long)count, mean, second, (const _Float16*)w_f16, w_inv_scale, gamma,
                        beta, momentum, eps, running_mean, running_var, num_batches_tracked, scale_shift,
                        mean_invstd);
     HKP_LAUNCH_CHECK("hkp_bn_from_gram");

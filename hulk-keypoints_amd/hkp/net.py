@@ -395,15 +395,15 @@ def _bottleneck_tail_gram(block, x, a2, pol):
     """conv3 → bn3 → (+ residual | + bn(downsample(x))) → ReLU of a plain-fp16
     inference Bottleneck (src/resnet.py:104-110) in one conv launch: train-mode
     bn3's batch statistics are exact functions of conv3's input statistics
-    (mean = w.mu, var = w^T Sigma w), so the scale/shift is known before conv3
+    (mean = w.mu, var = w^T E w - mean^2), so the scale/shift is known before conv3
     runs and its epilogue writes the block output — y3 is never materialised and
     no separate apply pass reads it (hkp_conv2d_fwd_f16_bn)."""
     c3, bn3 = block.conv3, block.bn3
     wp = _cached_split(c3.weight, "f16", ops.weight_pack_f16)
     count = a2.numel() // a2.shape[-1]
     if bn3.training:
-        mean, cov = ops.gram_f16(a2)
-        ss3, _ = ops.bn_from_gram(mean, cov, wp, count, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var,
+        mean, e2 = ops.gram_f16(a2)
+        ss3, _ = ops.bn_from_gram(mean, e2, wp, count, bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var,
                                   bn3.num_batches_tracked, **_finalize_args(bn3))
     else:
         ss3, _ = ops.bn_eval_params(bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps)

@@ -288,8 +288,8 @@ def conv2d_fwd_f16_bn(x16, wp, ss, res=None, res_ss=None, relu=True, stride=1, p
 
 
 def gram_f16(a16):
-    """Mean and covariance of the channels of an fp16 activation [.., C] over all
-    its pixels (hkp_gram_f16) → (mean fp64 [C], cov fp64 [C, C])."""
+    """Mean and second moments of the channels of an fp16 activation [.., C] over
+    all its pixels (hkp_gram_f16) → (mean fp64 [C], E = a^T a / M fp64 [C, C])."""
     from ._lib import lib
     _need(a16, torch.float16, "gram_f16.a")
     c = a16.shape[-1]
@@ -299,23 +299,23 @@ def gram_f16(a16):
         raise HkpError("gram_f16: unsupported shape (m=%d c=%d)" % (m, c))
     ws = torch.empty((nb + 7) // 8, device=a16.device, dtype=torch.float64)
     mean = torch.empty(c, device=a16.device, dtype=torch.float64)
-    cov = torch.empty((c, c), device=a16.device, dtype=torch.float64)
-    call("hkp_gram_f16", m, c, _ptr(a16), _ptr(mean), _ptr(cov), _ptr(ws), nb, _stream())
-    return mean, cov
+    second = torch.empty((c, c), device=a16.device, dtype=torch.float64)
+    call("hkp_gram_f16", m, c, _ptr(a16), _ptr(mean), _ptr(second), _ptr(ws), nb, _stream())
+    return mean, second
 
 
-def bn_from_gram(mean, cov, wp, count, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None,
-                 momentum=0.1, eps=1e-5):
+def bn_from_gram(mean, second, wp, count, gamma, beta, running_mean=None, running_var=None,
+                 num_batches_tracked=None, momentum=0.1, eps=1e-5):
     """Train-mode BN parameters of the output of a 1x1 conv with packed fp16 weight
-    wp (weight_pack_f16 of [K,1,1,C]) from its input's mean / covariance
+    wp (weight_pack_f16 of [K,1,1,C]) from its input's mean / second moments
     (gram_f16) → (scale_shift [2K], mean_invstd [2K]); running stats updated as
     bn_finalize does."""
     ws, wsc = wp
     _need(mean, torch.float64, "bn_from_gram.mean", 1)
-    _need(cov, torch.float64, "bn_from_gram.cov", 2)
+    _need(second, torch.float64, "bn_from_gram.second", 2)
     _need(ws, torch.float16, "bn_from_gram.w", 4)
     k, r, s_, c = ws.shape
-    if (r, s_) != (1, 1) or mean.numel() != c or tuple(cov.shape) != (c, c):
+    if (r, s_) != (1, 1) or mean.numel() != c or tuple(second.shape) != (c, c):
         raise HkpError("bn_from_gram: needs a 1x1 weight over the gram's %d channels (got %s)"
                        % (mean.numel(), tuple(ws.shape)))
     for t, nm in ((gamma, "gamma"), (beta, "beta"), (running_mean, "running_mean"), (running_var, "running_var")):
@@ -325,7 +325,7 @@ def bn_from_gram(mean, cov, wp, count, gamma, beta, running_mean=None, running_v
                 raise HkpError("bn_from_gram.%s: %d != K=%d" % (nm, t.numel(), k))
     ss = torch.empty(2 * k, device=ws.device, dtype=torch.float32)
     mi = torch.empty(2 * k, device=ws.device, dtype=torch.float32)
-    call("hkp_bn_from_gram", k, c, int(count), _ptr(mean), _ptr(cov), _ptr(ws), _ptr(wsc), _ptr(gamma), _ptr(beta),
+    call("hkp_bn_from_gram", k, c, int(count), _ptr(mean), _ptr(second), _ptr(ws), _ptr(wsc), _ptr(gamma), _ptr(beta),
          momentum, eps, _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi),
          _stream())
     return ss, mi

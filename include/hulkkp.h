@@ -148,18 +148,19 @@ int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f16, const u
 /* Train-mode BN statistics of a 1x1 conv's output y = W a without a pass over y
  * (replaces the batch statistics of bn3, src/resnet.py:106-108, for
  * hkp_conv2d_fwd_f16_bn): hkp_gram_f16 reduces the fp16 input a [m][c] (c % 64
- * == 0, c <= 2048) to its mean mu [c] and covariance Sigma [c][c] (fp64; fp32
- * MFMA partials over row splits of <= 16 k rows, merged in fp64 in fixed order;
- * workspace hkp_gram_f16_workspace_bytes(m, c)); hkp_bn_from_gram takes, per
- * output channel k of the packed fp16 weight w_f16 [k][c] (x w_inv_scale[k],
- * hkp_weight_pack_f16 — the weights the conv multiplies with), mean = w.mu and
- * var = w^T Sigma w (fp64), and writes hkp_bn_finalize's outputs from them
+ * == 0, c <= 2048) to its mean mu [c] and second moments E = a^T a / m [c][c]
+ * (fp64; fp32 MFMA partials over row splits of <= 16 k rows, merged in fp64 in
+ * fixed order; workspace hkp_gram_f16_workspace_bytes(m, c)); hkp_bn_from_gram
+ * takes, per output channel k of the packed fp16 weight w_f16 [k][c] (x
+ * w_inv_scale[k], hkp_weight_pack_f16 — the weights the conv multiplies with),
+ * mean = w.mu and var = w^T E w - mean^2 (fp64), and writes hkp_bn_finalize's
+ * outputs from them
  * (scale_shift, mean_invstd (nullable), running stats with the unbiased
  * variance, num_batches_tracked += 1).  c <= 1024 for hkp_bn_from_gram. */
 int64_t hkp_gram_f16_workspace_bytes(int64_t m, int32_t c);
-int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* cov, void* workspace,
+int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* second, void* workspace,
                  int64_t ws_bytes, hkp_stream_t stream);
-int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* cov,
+int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* second,
                      const uint16_t* w_f16, const float* w_inv_scale, const float* gamma, const float* beta,
                      float momentum, float eps, float* running_mean, float* running_var,
                      int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd, hkp_stream_t stream);

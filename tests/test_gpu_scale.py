@@ -381,6 +381,32 @@ def check_conv_fwd_f16(x, wp, y, st, pd, dl, gen, stats, ns=256):
     _check("fwd_f16", got, acc, REL * mag + half_ulp, stats)
 
 
+def check_conv_fwd_f16_bn(x, wp, ss, res, res_ss, out, gen, stats, ns=256):
+    """The fused conv3 + bn3 + residual + ReLU (1x1): out vs relu(f16(y64) * s + t
+    + r) from the fp16 operands the kernel read; the kernel's fp16 y may sit one
+    rounding step from f16(y64) (fp32 accumulation), which the scale carries."""
+    N, H, W, C = x.N, x.H, x.W, x.C
+    w16, inv = wp
+    K = w16.shape[0]
+    dev = out.device
+    n, h, w, k = (_idx(gen, v, ns, dev) for v in (N, H, W, K))
+    w64 = w16.double().reshape(K, C) * inv.double()[:, None]
+    xv = x.pix(n, h, w)
+    p = xv * w64[k]
+    y = p.sum(1)
+    mag = p.abs().sum(1)
+    y16 = y.half().double()
+    s, t = ss[k].double(), ss[K + k].double()
+    o = y16 * s + t
+    if res is not None:
+        r = res[n, h, w, k].double()
+        o = o + (r * res_ss[k].double() + res_ss[K + k].double() if res_ss is not None else r)
+    o = o.clamp_min(0.0)
+    got = out[n, h, w, k].double()
+    tol = s.abs() * (y.abs() * 2.0 ** -11 + REL * mag + 2.0 ** -25) + o.abs() * 2.0 ** -10 + 1e-6
+    _check("fwd_f16_bn", got, o, tol, stats)
+
+
 def test_c4_fp16_forward_sampled_fp64(cuda_device):
     """C4 at the bench's own size (R50-8s K=8 640x480 B=128, plain fp16 — bench.py
     --backbone resnet50 --keypoints 8 --batch 128 --precision f16): every conv
@@ -411,16 +437,30 @@ def test_c4_fp16_forward_sampled_fp64(cuda_device):
         syms[sym] = syms.get(sym, 0) + 1
         launch()
 
+    orig_bn = ops.conv2d_fwd_f16_bn
+
+    def fused_spy(x16, wp, ss, res=None, res_ss=None, relu=True, stride=1, pad=0, dil=1, sk=True, tile=0):
+        out = orig_bn(x16, wp, ss, res, res_ss, relu, stride, pad, dil, sk, tile)
+        torch.cuda.synchronize()
+        check_conv_fwd_f16_bn(_Act(x16), wp, ss, res, res_ss, out, gen, stats)
+        counts["f16_bn"] += 1
+        return out
+
+    counts["f16_bn"] = 0
     ops.set_observer(observe)
+    ops.conv2d_fwd_f16_bn = fused_spy
     try:
         with spy_calls(on_conv_fwd=on_fwd), torch.no_grad():
             hm, yx = m.heatmaps_and_keypoints(x)
     finally:
         ops.set_observer(None)
+        ops.conv2d_fwd_f16_bn = orig_bn
     n_conv = len([mm for mm in m.modules() if mm.__class__.__name__ == "KRSCConv2d"])
     print("C4 B=128: calls %s, worst error / bound: %s" % (counts, {k: round(v, 4) for k, v in stats.items()}))
     print("conv kernels:", syms)
-    assert counts == {"stem": 1, "f16": n_conv}
+    # 15 of the 16 Bottlenecks run conv3 with bn3 + residual + ReLU fused (the
+    # last block's tail is fused with the head instead)
+    assert counts == {"stem": 1, "f16": n_conv - 15, "f16_bn": 15}, counts
     assert "conv_x3_kernel<256, false, false, 16, false, 1>" in syms      # BENCH C4's roofline symbol
     assert torch.isfinite(hm).all().item() and yx.shape == (B, K, 2)
 
