@@ -1203,6 +1203,214 @@ __global__ __launch_bounds__(512, 1) void conv_x3_tail_kernel(X3Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// Halo-tile body (conv_x3_halo_kernel<P>) for stride-1 3x3 convs with pad =
+// dilation = 1 whose output tiles exactly into 8 x 32 pixel patches (Ho % 8 ==
+// 0, Wo % 32 == 0): layer1 of every R-net here (64 channels at 120x160 in
+// C2-C4, 240x320 in C5), forward and stride-1 dgrad.  The one-tile kernels
+// stage, per K-step, a tap-shifted 256-row A window — every input line is
+// fetched from L2 nine times, and at Cin = 64 (2 channel groups x 9 taps) the
+// 256x64 tile is bound by that operand stream, not by its MFMAs.  Here a tile is
+// an 8 x 32 patch of one image: per channel group its (8+2) x (32+2) = 340
+// input lines are staged ONCE by LDS-DMA into a halo image and the nine taps
+// read their fragments from it (tile row m = pixel (m/32, m%32) reads halo line
+// (m/32 + r) * 34 + m%32 + s for tap (r, s)); only the 64-row weight stage
+// streams per K-step (a 3-slot ring).  A tile moves 2 x 42.5 + 18 x 8 = 229 KB
+// from L2 instead of 18 x 40 = 720 KB.  Lines past the image are zero lines.
+// The 16-B chunk swizzle (line >> 1) & 7 is keyed on the halo line, so any 16
+// consecutive lines a fragment read touches are conflict-free, as in the ring.
+// Two blocks per CU (72 KB each): one block's halo reload / epilogue overlaps the
+// other's MFMAs.  256 x 64 tile, 8 waves 4 x 2 (wave tile 64 x 32), 16x16x32
+// MFMAs; epilogue = the one-tile kernels' (BN tile partials from the
+// accumulators, LDS-staged 16-B row chunks), rows remapped to the patch pixels.
+constexpr int HALO_PH = 8, HALO_PW = 32, HALO_LW = HALO_PW + 2, HALO_NL = (HALO_PH + 2) * HALO_LW;   // 340 lines
+constexpr int HALO_GA = 6;                                   // halo DMA instructions per wave (48 x 8 lines >= 340)
+constexpr int HALO_ABYTES = 8 * HALO_GA * 8 * 128;           // 48 KiB: halo image (+ 44 dummy lines)
+constexpr int HALO_NSTB = 3, HALO_BSTAGE = 64 * 128;         // weight ring: 3 x 8 KiB
+constexpr int HALO_LDS = HALO_ABYTES + HALO_NSTB * HALO_BSTAGE;
+
+static bool halo_shape(int stride, int r, int s, int pad, int dil, int ho, int wo, int k) {
+    return stride == 1 && r == 3 && s == 3 && pad == 1 && dil == 1 && ho % HALO_PH == 0 && wo % HALO_PW == 0 &&
+           k % 64 == 0;
+}
+
+template <int P>
+__global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
+    constexpr int BM = 256, BN = 64, WM = 4, WN = 2, ROW = 128;
+    constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);     // 4 x 2 16x16 sub-tiles per wave
+    __shared__ __attribute__((aligned(1024))) char smem[HALO_LDS];
+    static_assert(256 * (BN + 4) * 4 <= HALO_LDS && 8 * BN * 4 <= HALO_LDS, "epilogue staging");
+
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
+    const int pwn = a.Wo / HALO_PW, tpi = (a.Ho / HALO_PH) * pwn;
+    const int img = mt / tpi, rem = mt - img * tpi;
+    const int h0 = (rem / pwn) * HALO_PH, w0 = (rem - (rem / pwn) * pwn) * HALO_PW;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w % WN;
+    const int cstride = a.cch * 64;                             // halves per pixel
+    const int nks = a.nks;                                      // 9 taps x channel groups
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+
+    // ---- halo DMA: instruction i of wave w fills lines 8 (w*GA + i) .. +7 ----
+    unsigned h_off[HALO_GA];                                    // element offsets from a.xs (or ~0u: zero line)
+#pragma unroll
+    for (int i = 0; i < HALO_GA; ++i) {
+        const int L = 8 * (w * HALO_GA + i) + lane / 8;
+        const int Lc = (lane % 8) ^ ((L >> 1) & 7);
+        const int hl = L / HALO_LW, wl = L - hl * HALO_LW;
+        const int hi = h0 - 1 + hl, wi = w0 - 1 + wl;
+        const bool in = L < HALO_NL && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        h_off[i] = in ? (unsigned)((((long)img * a.H + hi) * a.W + wi) * cstride + Lc * 8) : ~0u;
+    }
+    auto issue_halo = [&](int g) {
+#pragma unroll
+        for (int i = 0; i < HALO_GA; ++i)
+            glds16(h_off[i] != ~0u ? a.xs + ((unsigned long)h_off[i] + g * 64) : zero,
+                   smem + 8 * (w * HALO_GA + i) * ROW);
+    };
+    // ---- weight stage DMA: one instruction per wave, rows 8w .. 8w+7 ----
+    const int brow = 8 * w + lane / 8;
+    const int bline = a.RS * a.cch * 64;
+    const unsigned b_off = (unsigned)((n0 + brow) * bline + (((lane % 8) ^ ((brow >> 1) & 7)) * 8));
+    auto issue_b = [&](int t) {
+        const int g = t / 9, u = t - g * 9;
+        glds16(a.ws + (b_off + (unsigned)((u * a.cch + g) * 64)),
+               smem + HALO_ABYTES + (t % HALO_NSTB) * HALO_BSTAGE + 8 * w * ROW);
+    };
+
+    // ---- fragment addressing ----
+    const int r16 = lane & 15, q = lane >> 4;
+    int lb[UM];                                                 // halo line of tap (0, 0) for sub-tile i
+#pragma unroll
+    for (int i = 0; i < UM; ++i) {
+        const int m = wm * 64 + 16 * i + r16;
+        lb[i] = (m >> 5) * HALO_LW + (m & 31);
+    }
+    const int sw = (r16 >> 1) & 7;                              // B rows: 16-row tiles, as the ring's
+    const int fb_h = (wn * 32 + r16) * ROW + ((q ^ sw) << 4), fb_l = (wn * 32 + r16) * ROW + (((4 + q) ^ sw) << 4);
+
+    f32x4 acc[UM][UN];
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+    };
+
+    // column scale (weight scale x gradient scale), issued before the pipeline
+    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;
+    float scv[UN];
+#pragma unroll
+    for (int j = 0; j < UN; ++j) scv[j] = (a.wscale ? a.wscale[n0 + wn * 32 + 16 * j + r16] : 1.f) * ginv;
+
+    // prologue: halo of group 0, weight stages 0 and 1
+    issue_halo(0);
+    issue_b(0);
+    if (nks > 1) issue_b(1);
+    if (nks > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    for (int t = 0; t < nks; ++t) {
+        const int g = t / 9, u = t - g * 9;
+        const int toff = (u / 3) * HALO_LW + (u - (u / 3) * 3);
+        // fragments of step t
+        f16x8 ah[UM], al[UM], bh[UN], bl[UN];
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            const int L = lb[i] + toff;
+            const int ls = (L >> 1) & 7;
+            ah[i] = *(const f16x8*)(smem + L * ROW + ((q ^ ls) << 4));
+            al[i] = *(const f16x8*)(smem + L * ROW + (((4 + q) ^ ls) << 4));
+        }
+        const char* bst = smem + HALO_ABYTES + (t % HALO_NSTB) * HALO_BSTAGE;
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            bh[j] = *(const f16x8*)(bst + j * 16 * ROW + fb_h);
+            bl[j] = *(const f16x8*)(bst + j * 16 * ROW + fb_l);
+        }
+        // weight stage t+2 goes into the slot step t-1 read (every wave is past
+        // this step's barrier, so done reading it)
+        if (t + 2 < nks) issue_b(t + 2);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int j = 0; j < UN; ++j) x3_products<P>(acc[i][j], ah[i], al[i], bh[j], bl[j], mfma);
+        if (t + 1 >= nks) break;
+        if (u == 8) {
+            // the group's last tap: every wave done with the halo, then the next
+            // group's halo (the youngest DMA: wait for everything)
+            lds_barrier();
+            issue_halo(g + 1);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if (t + 2 < nks) {
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");     // stage t+1 landed, t+2 in flight
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        lds_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---- epilogue: BN tile partials (rows all valid: exact patch tiling), then
+    // the scaled tile staged through the drained LDS and written as 16-B row
+    // chunks; tile row m -> pixel (img, h0 + m/32, w0 + m%32) ----
+    const int rbase = m0 + wm * UM * 16 + 4 * q;
+    lds_sync();                                                  // every wave done with the halo / ring
+    if (a.part) {
+        x3_bn_partials_w<BN, UM, UN, 16, 16>(
+            a, (float*)smem, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
+            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; });
+        lds_sync();
+    }
+    auto out_pix = [&](int row) { return ((long)img * a.Ho + h0 + (row >> 5)) * a.Wo + w0 + (row & 31); };
+    if constexpr (P == 1) {
+        constexpr int PITCH = BN + 8, CH = BN / 8;
+        _Float16* st = (_Float16*)smem;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int j = 0; j < UN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * 32 + j * 16 + r16] =
+                        (_Float16)(acc[i][j][r] * scv[j]);
+        lds_sync();
+#pragma unroll 4
+        for (int e = tid; e < BM * CH; e += 512) {
+            const int row = e / CH, cc = e - row * CH;
+            *(uint4*)(a.y16 + out_pix(row) * a.K + n0 + cc * 8) = *(const uint4*)(smem + (row * PITCH + cc * 8) * 2);
+        }
+    } else {
+        constexpr int PITCH = BN + 4, C4 = BN / 4;
+        float* st = (float*)smem;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int j = 0; j < UN; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    st[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * 32 + j * 16 + r16] = acc[i][j][r] * scv[j];
+        lds_sync();
+#pragma unroll 4
+        for (int e = tid; e < BM * C4; e += 512) {
+            const int row = e / C4, c4 = e - row * C4;
+            const long off = out_pix(row) * a.K + n0 + c4 * 4;
+            f32x4 v = *(const f32x4*)(st + row * PITCH + c4 * 4);
+            if (a.add) {
+                const f32x4 ad = *(const f32x4*)(a.add + off);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[k] = v[k] + ad[k];
+            }
+            *(f32x4*)(a.y + off) = v;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Persistent form (conv_x3p_kernel<BN, P>): one block per CU walks tiles
 // lb, lb + G, lb + 2G, ... (lb = the XCD-remapped block index, so the blocks of
 // one XCD work on adjacent tiles at any time, as the one-tile grid's do) and the
@@ -2293,11 +2501,18 @@ struct X3Choice {
     bool pair, sk;
     bool persist = false;              // conv_x3p_kernel<bn, P, one>
     bool one = false;
+    bool halo = false;                 // conv_x3_halo_kernel<P>
 };
 // one: a 1x1 conv without padding; pfit: the persistent kernel's 32-bit byte
 // offsets cover the operands (x3p_fits)
 static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, bool one = false,
-                          bool pfit = false) {
+                          bool pfit = false, bool halo_ok = false) {
+    // the halo-tile body wherever the shape allows it, unless a tile body is forced
+    if (halo_ok && (policy == HKP_TILE_HALO || policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL)) {
+        X3Choice c{64, 16, true, false};
+        c.halo = true;
+        return c;
+    }
     switch (policy) {
         case HKP_TILE_256:
             if (k % 256 == 0) return {256, 16, false, false};
@@ -2334,6 +2549,7 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
 static const X3Choice X3_STEM{64, 16, true, false};
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
+    if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
     if (c.persist) return snprintf(buf, len, "conv_x3p_kernel<%d, %d, %s>", c.bn, P, c.one ? "true" : "false");
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
@@ -2373,6 +2589,13 @@ static bool x3p_fits(long n, long h, long w, long cstride, long pad, long k, lon
 
 static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 
+// the halo-tile body takes this launch (shape, plain dense output, no fused
+// epilogue, 32-bit halo offsets)
+static bool x3_halo_ok(const X3Args& a, int k) {
+    return halo_shape(a.stride, a.R, a.S, a.pad, a.dil, a.Ho, a.Wo, k) && a.ost == 0 && a.ep_ss == nullptr &&
+           a.mt0 == 0 && a.plane == 0 && (long)a.N * a.H * a.W * a.cch * 64L + 64 < (1L << 32);
+}
+
 static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
                       int64_t ws_bytes = 0) {
     a.stamps = g_x3_stamps;
@@ -2380,10 +2603,16 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     const int nks = a.RS * a.cch;
     const bool one = a.RS == 1 && a.pad == 0;
     const bool pfit = x3p_fits(a.N, a.H, a.W, a.cch * 64L, a.pad, a.K, a.RS);
-    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, one, pfit);
+    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, one, pfit, x3_halo_ok(a, k));
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
+    if (c.halo) {
+        const dim3 gh((unsigned)(m_tiles * a.n_tiles));
+        if (P == 3) hipLaunchKernelGGL(conv_x3_halo_kernel<3>, gh, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL(conv_x3_halo_kernel<1>, gh, dim3(512), 0, st, a);
+        return;
+    }
     dim3 grid((unsigned)(m_tiles * a.n_tiles));
     if (c.sk) {
         a.sk_units = m_tiles * a.nks;
@@ -2460,8 +2689,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_256_TAIL, "%s: unknown tile policy %d", who,
-                  d->tile);
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_HALO, "%s: unknown tile policy %d", who, d->tile);
     return HKP_OK;
 }
 
@@ -2802,12 +3030,19 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int nks = d->r * d->s * (d->c / cg);
             const bool one = d->r * d->s == 1 && d->pad == 0;
             const bool pfit = x3p_fits(d->n, d->h, d->w, d->c / cg * 64L, d->pad, d->k, d->r * d->s);
-            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, one, pfit), false, P, buf, len);
+            const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
+                              (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);
+            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, one, pfit, halo), false, P, buf,
+                                  len);
         }
         case HKP_KOP_DGRAD_X3: {
             const long m = (long)d->n * d->h * d->w;
             const int nks = d->r * d->s * (d->k / 32);
-            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile), false, 3, buf, len);
+            const int padp = d->dilation * (d->r - 1) - d->pad;
+            const bool halo = halo_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
+                              (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32);
+            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, false, false, halo), false, 3,
+                                  buf, len);
         }
         case HKP_KOP_STEM_X3:
             return x3_kernel_name(X3_STEM, true, 3, buf, len);

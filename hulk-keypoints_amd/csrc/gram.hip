@@ -262,86 +262,93 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(int C, int TC, int til
 // var = w_k^T E w_k - mean^2 (E = the raw second moments; fp64 throughout — the
 // centring loses only log10(1 + mean^2/var) of fp64's digits), with w_k = the
 // fp16 packed weight row x its inverse scale (the weights the conv multiplies
-// with), then bn_fin_store.  A block takes BFG_KB channels (their weights in LDS,
-// read as broadcasts); thread t owns columns j = t, t + 256, ...: for every row i
-// it accumulates s_k[j] += E[i][j] w_k[i] (coalesced row loads of E, 8 rows in
-// flight), then q_k = sum_j s_k[j] w_k[j]; the threads' q_k are summed in fixed
-// order.
-constexpr int BFG_KB = 8;
-constexpr int BFG_MAXJ = 4;                      // C <= 1024
-__global__ __launch_bounds__(256) void bn_from_gram_kernel(int K, int C, long count, const double* mu,
+// with), then bn_fin_store.  A block takes KB channels (their weights in LDS,
+// read as broadcasts); thread t owns columns j = t, t + 512: for every row i it
+// accumulates s_k[j] += E[i][j] w_k[i] (coalesced row loads of E, 8 rows in
+// flight), then q_k = sum_j s_k[j] w_k[j].  E (C^2 doubles) is re-read from L2
+// by every block: KB = 16 halves that traffic against KB = 8 (the kernel was
+// L2-bound), two waves per SIMD hide the load latency.  The threads' q_k and
+// means are summed in fixed order (wave shuffles, then the eight waves in order).
+template <int KB, int MAXJ>
+__global__ __launch_bounds__(512) void bn_from_gram_kernel(int K, int C, long count, const double* mu,
                                                            const double* e2, const _Float16* w16,
                                                            const float* w_inv_scale, const float* gamma,
                                                            const float* beta, float momentum, float eps,
                                                            float* rmean, float* rvar, int64_t* nbt, float* ss,
                                                            float* mi) {
     extern __shared__ double wsh[];                        // [C][KB]: row i's KB weights contiguous
-    __shared__ double red[256][BFG_KB];
-    const int k0 = blockIdx.x * BFG_KB;
-    const int tid = threadIdx.x;
-    for (int e = tid; e < BFG_KB * C; e += 256) {
-        const int i = e / BFG_KB, kk = e - i * BFG_KB;
+    __shared__ double red[8][KB][2];
+    const int k0 = blockIdx.x * KB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int e = tid; e < KB * C; e += 512) {
+        const int i = e / KB, kk = e - i * KB;
         const int k = k0 + kk;
         wsh[e] = k < K ? (double)(float)w16[(long)k * C + i] * (double)w_inv_scale[k] : 0.0;
     }
     __syncthreads();
-    const int nj = (C - tid + 255) / 256;                  // columns of this thread (C % 64 == 0)
-    double s[BFG_MAXJ][BFG_KB];
+    double s[MAXJ][KB];
 #pragma unroll
-    for (int u = 0; u < BFG_MAXJ; ++u)
+    for (int u = 0; u < MAXJ; ++u)
 #pragma unroll
-        for (int kk = 0; kk < BFG_KB; ++kk) s[u][kk] = 0.0;
+        for (int kk = 0; kk < KB; ++kk) s[u][kk] = 0.0;
     for (int i0 = 0; i0 < C; i0 += 8) {
-        double ev[8][BFG_MAXJ];
+        double ev[8][MAXJ];
 #pragma unroll
         for (int di = 0; di < 8; ++di)
 #pragma unroll
-            for (int u = 0; u < BFG_MAXJ; ++u) ev[di][u] = u < nj ? e2[(long)(i0 + di) * C + tid + 256 * u] : 0.0;
+            for (int u = 0; u < MAXJ; ++u) {
+                const int j = tid + 512 * u;
+                ev[di][u] = j < C ? e2[(long)(i0 + di) * C + j] : 0.0;
+            }
 #pragma unroll
         for (int di = 0; di < 8; ++di) {
-            const double* wi = wsh + (i0 + di) * BFG_KB;
+            const double* wi = wsh + (i0 + di) * KB;
 #pragma unroll
-            for (int kk = 0; kk < BFG_KB; ++kk) {
-                const double w = wi[kk];
+            for (int kk = 0; kk < KB; ++kk) {
+                const double wv = wi[kk];
 #pragma unroll
-                for (int u = 0; u < BFG_MAXJ; ++u) s[u][kk] += ev[di][u] * w;
+                for (int u = 0; u < MAXJ; ++u) s[u][kk] += ev[di][u] * wv;
             }
         }
     }
-    double q[BFG_KB], m[BFG_KB];
+    double q[KB], m[KB];
 #pragma unroll
-    for (int kk = 0; kk < BFG_KB; ++kk) q[kk] = m[kk] = 0.0;
+    for (int kk = 0; kk < KB; ++kk) q[kk] = m[kk] = 0.0;
 #pragma unroll
-    for (int u = 0; u < BFG_MAXJ; ++u) {
-        if (u < nj) {
-            const int j = tid + 256 * u;
+    for (int u = 0; u < MAXJ; ++u) {
+        const int j = tid + 512 * u;
+        if (j < C) {
             const double muj = mu[j];
 #pragma unroll
-            for (int kk = 0; kk < BFG_KB; ++kk) {
-                const double wj = wsh[j * BFG_KB + kk];
+            for (int kk = 0; kk < KB; ++kk) {
+                const double wj = wsh[j * KB + kk];
                 q[kk] += s[u][kk] * wj;
                 m[kk] += muj * wj;
             }
         }
     }
 #pragma unroll
-    for (int kk = 0; kk < BFG_KB; ++kk) red[tid][kk] = q[kk];
-    __syncthreads();
-    if (tid < BFG_KB) {
-        double v = 0.0;
-        for (int t2 = 0; t2 < 256; ++t2) v += red[t2][tid];
-        q[0] = v;
+    for (int kk = 0; kk < KB; ++kk) {
+        double v = q[kk], u = m[kk];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            v += __shfl_xor(v, o);
+            u += __shfl_xor(u, o);
+        }
+        if (lane == 0) {
+            red[w][kk][0] = v;
+            red[w][kk][1] = u;
+        }
     }
     __syncthreads();
-    // the means: the same fixed-order sum over threads
-    const double qk = tid < BFG_KB ? q[0] : 0.0;
+    if (tid < KB && k0 + tid < K) {
+        double v = 0.0, mean = 0.0;
 #pragma unroll
-    for (int kk = 0; kk < BFG_KB; ++kk) red[tid][kk] = m[kk];
-    __syncthreads();
-    if (tid < BFG_KB && k0 + tid < K) {
-        double mean = 0.0;
-        for (int t2 = 0; t2 < 256; ++t2) mean += red[t2][tid];
-        double var = qk - mean * mean;
+        for (int ww = 0; ww < 8; ++ww) {
+            v += red[ww][tid][0];
+            mean += red[ww][tid][1];
+        }
+        double var = v - mean * mean;
         var = var > 0.0 ? var : 0.0;
         bn_fin_store(k0 + tid, K, count, mean, var * (double)count, gamma, beta, momentum, eps, rmean, rvar, nbt, ss,
                      mi);
@@ -414,11 +421,18 @@ extern "C" int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const doubl
     HKP_CHECK_ARG(k > 0 && c > 0 && c <= 1024 && c % 64 == 0 && count > 0 && mean && second && w_f16 && w_inv_scale &&
                       scale_shift,
                   "hkp_bn_from_gram: bad args");
-    const size_t sh = (size_t)BFG_KB * c * sizeof(double);
-    hipLaunchKernelGGL(bn_from_gram_kernel, dim3((unsigned)((k + BFG_KB - 1) / BFG_KB)), dim3(256), sh,
-                       as_stream(stream), k, c, (long)count, mean, second, (const _Float16*)w_f16, w_inv_scale, gamma,
-                       beta, momentum, eps, running_mean, running_var, num_batches_tracked, scale_shift,
-                       mean_invstd);
+    hipStream_t st = as_stream(stream);
+    if (c <= 512) {
+        const size_t sh = (size_t)16 * c * sizeof(double);
+        hipLaunchKernelGGL((bn_from_gram_kernel<16, 1>), dim3((unsigned)((k + 15) / 16)), dim3(512), sh, st, k, c,
+                           (long)count, mean, second, (const _Float16*)w_f16, w_inv_scale, gamma, beta, momentum, eps,
+                           running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd);
+    } else {
+        const size_t sh = (size_t)8 * c * sizeof(double);
+        hipLaunchKernelGGL((bn_from_gram_kernel<8, 2>), dim3((unsigned)((k + 7) / 8)), dim3(512), sh, st, k, c,
+                           (long)count, mean, second, (const _Float16*)w_f16, w_inv_scale, gamma, beta, momentum, eps,
+                           running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd);
+    }
     HKP_LAUNCH_CHECK("hkp_bn_from_gram");
     return HKP_OK;
 }

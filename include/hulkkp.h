@@ -74,6 +74,8 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_256_PERSIST 7        /* persistent 256x256 (conv_x3p_kernel) */
 #define HKP_TILE_128_PERSIST 8        /* persistent 256x128 */
 #define HKP_TILE_256_TAIL 9           /* 256x256; tiles past the last full round as split-K segments */
+#define HKP_TILE_HALO 10              /* 8x32-pixel halo tiles (stride-1 3x3, pad = dil = 1, Ho%8 = Wo%32 = 0;
+                                         the default there under AUTO and 256_TAIL) */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);

@@ -29,6 +29,16 @@ def _unpack_x3(t):
     return g[..., 0, :].reshape(*t.shape[:-1], -1), g[..., 1, :].reshape(*t.shape[:-1], -1)
 
 
+def _bn_stats(part, m):
+    """mean | invstd of a conv's BN tile partials (hkp_bn_finalize): compares
+    partials of bodies whose tiles group the rows differently (the halo body's
+    tiles are 8x32 pixel patches)."""
+    from hkp import ops
+    c = part.shape[1]
+    one = torch.ones(c, device=part.device)
+    return ops.bn_finalize(part, m, one, torch.zeros_like(one))[1]
+
+
 def _pow2(t):
     m, _ = torch.frexp(t)
     return bool((m.abs() == 0.5).all())
@@ -121,6 +131,8 @@ X3_CASES = CASES + [
     (2, 31, 41, 64, 128, 1, 2, 0, 1),       # 1x1 stride-2 downsample
     (1, 9, 14, 32, 192, 3, 1, 2, 2),        # C = 32 (one channel group), K = 192 (BN 64)
     (2, 11, 13, 64, 256, 3, 1, 1, 1),       # 256x256 tiles, ragged M, C = 64
+    (2, 16, 64, 64, 64, 3, 1, 1, 1),        # halo tiles (8x32 patches), Cin 64: 2 channel groups
+    (1, 24, 96, 128, 128, 3, 1, 1, 1),      # halo tiles, 4 channel groups, 2 column tiles
 ]
 
 
@@ -144,15 +156,16 @@ def test_x3_conv_fp32_accurate(cuda_device, case):
     err = (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / scale
     assert err < 2e-6, err
     y32, p32 = ops.conv2d_fwd(x.to(d), wt.to(d), st, pad, dil)
-    assert torch.allclose(p, p32, rtol=1e-4, atol=1e-3)
+    m = y.numel() // cout
+    assert torch.allclose(_bn_stats(p, m), _bn_stats(p32, m), rtol=1e-5, atol=1e-6)
     y3, p3 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, stats=False)
     assert p3 is None and torch.equal(y3, y)
-    for tile in range(1, 10):
+    for tile in range(1, 11):
         yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
         # every tile / stream-K variant is fp32-class vs fp64 (stream-K sums K
         # segments at the end, so variants differ by fp32 summation order)
         assert (yv.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale, tile
-        assert torch.allclose(pv, p, rtol=1e-4, atol=1e-3)
+        assert torch.allclose(_bn_stats(pv, m), _bn_stats(p, m), rtol=1e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("case", [c for c in X3_CASES if c[6] == 1 and c[3] % 64 == 0])
@@ -295,6 +308,57 @@ def test_f16x3_forward_matches_golden(cuda_device, golden, case):
         assert np.abs(hm.cpu().numpy() - g["heat"]).max() < 1e-3
     else:
         np.testing.assert_allclose(hm.double().sum(3).cpu().numpy(), g["heat_row_sum"], rtol=1e-4)
+
+
+HALO_CASES = [(2, 16, 64, 64, 64), (1, 24, 96, 128, 128), (3, 8, 32, 64, 128), (1, 120, 160, 64, 64)]
+
+
+@pytest.mark.parametrize("case", HALO_CASES)
+@pytest.mark.parametrize("prec", ["x3", "f16"])
+def test_halo_tiles_equal_pair_body(cuda_device, case, prec):
+    """The halo-tile body (8x32 patches, the nine taps read from one staged
+    halo image) runs the same MFMAs in the same order as the 256x64 pair body:
+    outputs and BN partials bit-identical (forward, both operand layouts), and
+    the stride-1 dgrad too; the planner picks it for these shapes."""
+    from hkp import ops
+    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_TILE_64_PAIR, ConvDesc
+    n, h, w, cin, cout = case
+    d = cuda_device
+    x = F.relu(rand(n, h, w, cin, seed=31)).to(d)
+    wt = rand(cout, 3, 3, cin, seed=32, scale=(2.0 / (9 * cout)) ** 0.5).to(d)
+    desc = ConvDesc(n, h, w, cin, cout, 3, 3, 1, 1, 1, 0, 0)
+    if prec == "x3":
+        assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_halo_kernel<3>"
+        ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
+        xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
+        wp = ops.weight_pack_x3(wt)
+        y0, p0 = ops.conv2d_fwd_x3(xs, wp, 1, 1, 1)
+        y1, p1 = ops.conv2d_fwd_x3(xs, wp, 1, 1, 1, tile=HKP_TILE_64_PAIR)
+        ref = F.conv2d(x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double(), None, 1, 1, 1)
+        assert (y0.double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * ref.abs().max().item()
+        # dgrad (stride 1): dy of Cout channels, flipped weights
+        gy = rand(n, h, w, cout, seed=33).to(d)
+        amax = ops.absmax(gy)
+        dys = ops.split_pack_x3(gy, amax)
+        wf = ops.weight_flip_pack_x3(wt)
+        add = rand(n, h, w, cin, seed=34).to(d)
+        ddesc = ConvDesc(n, h, w, cin, cout, 3, 3, 1, 1, 1, 0, 0)
+        assert ops.kernel_name(ddesc, HKP_KOP_DGRAD_X3) == "conv_x3_halo_kernel<3>"
+        dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), 1, 1, add=add, amax=amax)
+        dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), 1, 1, add=add, amax=amax, tile=HKP_TILE_64_PAIR)
+        assert torch.equal(dx0, dx1)
+    else:
+        assert ops.kernel_name(desc, HKP_KOP_FWD_F16) == "conv_x3_halo_kernel<1>"
+        x16 = x.half()
+        x16._hkp_split_passes = 1
+        wp = ops.weight_pack_f16(wt)
+        y0, p0 = ops.conv2d_fwd_f16(x16, wp, 1, 1, 1)
+        y1, p1 = ops.conv2d_fwd_f16(x16, wp, 1, 1, 1, tile=HKP_TILE_64_PAIR)
+    assert torch.equal(y0, y1)
+    # BN partials: the same sums over differently grouped rows (patches vs row
+    # runs) -> the same statistics to fp64 merge order
+    m = y0.numel() // cout
+    assert torch.allclose(_bn_stats(p0, m), _bn_stats(p1, m), rtol=1e-6, atol=1e-7)
 
 
 def test_f16_forward_close_to_reference(cuda_device, golden):
@@ -559,6 +623,38 @@ def test_split_k_tail(cuda_device, case):
     assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item()
     assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
     assert torch.equal(y1, y2)
+
+
+def test_split_k_tail_dgrad_back_to_back(cuda_device):
+    """The overlapped dgrad's policy (HKP_TILE_256_TAIL, with the stream-K
+    workspace) on a stride-1 shape whose last round is partial (300 tiles = one
+    round + 44 tail tiles in S segments): the tail's arrival counters must return
+    to zero and its slabs must not leak into the next launch — two launches back
+    to back on one stream give bit-identical dx, equal to the plain grid to fp32
+    summation order, and fp32-class vs fp64."""
+    from hkp import ops
+    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_TILE_256, HKP_TILE_256_TAIL, ConvDesc
+    n, h, w, cin, cout, k, pad, dil = 8, 60, 80, 512, 512, 3, 4, 4          # the C3 shard's layer4 dgrad
+    d = cuda_device
+    g = torch.Generator(device=d).manual_seed(21)
+    wt = torch.randn(cout, k, k, cin, device=d, generator=g) * (2.0 / (k * k * cout)) ** 0.5
+    gy = torch.randn(n, h, w, cout, device=d, generator=g) * 1e-3
+    add = torch.randn(n, h, w, cin, device=d, generator=g) * 1e-3
+    desc = ConvDesc(n, h, w, cin, cout, k, k, 1, pad, dil, 0, HKP_TILE_256_TAIL)
+    assert ops.kernel_name(desc, HKP_KOP_DGRAD_X3).startswith("conv_x3_kernel<256,")
+    amax = ops.absmax(gy)
+    dys = ops.split_pack_x3(gy, amax)
+    wf = ops.weight_flip_pack_x3(wt)
+    dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=HKP_TILE_256_TAIL)
+    dx2 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=HKP_TILE_256_TAIL)
+    dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, sk=False, tile=HKP_TILE_256)
+    assert torch.equal(dx1, dx2)
+    assert (dx1 - dx0).abs().max().item() <= 4e-6 * dx0.abs().max().item()
+    # fp64 on a slice of images
+    ref = torch.nn.grad.conv2d_input((2, cin, h, w), wt.permute(0, 3, 1, 2).double(),
+                                     gy[:2].permute(0, 3, 1, 2).double(), 1, pad, dil) + add[:2].permute(0, 3, 1, 2).double()
+    err = (dx1[:2].permute(0, 3, 1, 2).double() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
 
 
 def test_bn_apply_f16(cuda_device):
