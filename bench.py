@@ -392,11 +392,8 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     # dominant kernel = the conv symbol with the most event-timed time
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
     alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
-    if dom_sym.startswith(("conv_split_kernel", "conv_x3_kernel", "conv_x3p_kernel", "wgrad_x3_kernel")):
-        if dom_sym.startswith("conv_split_kernel"):
-            passes = int(dom_sym.split("<")[1].split(",")[2])
-        else:                                # the x3 LDS-DMA kernels: 3 MFMAs per MAC (f16x3) or 1 (f16)
-            passes = 3 if precision == "f16x3" else 1
+    if dom_sym.startswith(("conv_x3_kernel", "conv_x3_halo_kernel", "wgrad_x3_kernel")):
+        passes = 3 if precision == "f16x3" else 1   # the x3 LDS-DMA kernels: 3 MFMAs per MAC (f16x3) or 1 (f16)
         achieved, peak = alg * passes, PEAK_FP16_MFMA_TFLOPS    # issued fp16 MFMA FLOPs vs dense fp16 peak
     else:
         passes, achieved, peak = 1, alg, PEAK_FP32_MFMA_TFLOPS

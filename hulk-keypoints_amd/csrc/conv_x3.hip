@@ -1411,376 +1411,6 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// Persistent form (conv_x3p_kernel<BN, P>): one block per CU walks tiles
-// lb, lb + G, lb + 2G, ... (lb = the XCD-remapped block index, so the blocks of
-// one XCD work on adjacent tiles at any time, as the one-tile grid's do) and the
-// LDS-DMA stage stream runs across tile boundaries: the last K-steps of a tile
-// already issue the next tile's first stages, so no tile pays a pipeline fill,
-// and no block launch or prologue sits between tiles.  Short-K convs (the R50
-// 1x1 GEMMs of configs C4/C5: 4-16 K-steps per tile) spent ~14 us per tile
-// outside the K loop in the one-tile kernel (~1.4 us per K-step inside it).
-//
-// The MFMAs run with the operands swapped (D^T = W . X^T): a lane's four
-// accumulator values are four consecutive output channels of one pixel, so the
-// epilogue stores 8 B (fp16) / 16 B (fp32) vectors straight from registers — no
-// LDS staging (the ring holds the next tile's stages while the epilogue runs)
-// and no per-element scalar stores.  The BN tile partials use a small LDS
-// scratch past the ring.  Counting: the epilogue's stores share vmcnt with the
-// DMA loads; loads complete in order among themselves, so a counted wait for
-// stage s still proves stage s landed (stores only make it wait longer).
-// Tail past the last tile: zero-filling DMAs keep every K-step's count uniform.
-// ONE: a 1x1 conv without padding (every row < M in-bounds for every K-step):
-// a row past M gets the out-of-range offset once per tile and no per-K-step
-// bounds check is kept (4 VGPRs: the 256x256 body has none to spare).
-template <int BN, int P, bool ONE>
-__global__ __launch_bounds__(512, 1) void conv_x3p_kernel(X3Args a) {
-    constexpr int BM = 256, WM = 4, WN = 2, ROW = 128, CPR = 8, RPI = 8;
-    constexpr int NST = x3_nst(BN, false);
-    constexpr int STAGE = (BM + BN) * ROW;
-    constexpr int GA = BM / RPI / 8;
-    constexpr int GBT = BN / RPI;
-    constexpr int GB = GBT >= 8 ? GBT / 8 : 1;
-    constexpr int GL = GA + GB;
-    constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
-    constexpr int NMC = (P == 3 ? 3 : 2) * UM;
-    static_assert(NST * STAGE + (WM + 2) * BN * 4 <= 160 * 1024, "LDS");
-    __shared__ __attribute__((aligned(1024))) char smem[NST * STAGE + (WM + 2) * BN * 4];
-    float* red = (float*)(smem + NST * STAGE);     // [WM][BN] column sums, then [2][BN] half means
-    float* tmean = red + WM * BN;
-
-    const int G = gridDim.x, lb = xcd_remap(blockIdx.x, G);
-    const long T = (long)((a.M + BM - 1) / BM) * a.n_tiles;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w / WN, wn = w % WN;
-    const int nks = a.nks;
-
-    // ---- issue side: the stage stream over (tile, K-step) ----
-    // byte offsets from xbase = a.xs - pad*(W+1)*cstride halves (the furthest a
-    // padded-out origin reaches before a.xs; the host checks they fit 32 bits)
-    const int cstride = a.cch * 64;
-    const long xbias = (long)a.pad * (a.W + 1) * cstride;
-    const unsigned xbytes = (unsigned)((xbias + (long)a.N * a.H * a.W * cstride) * 2);
-    const i32x4 xrs = buffer_rsrc(a.xs - xbias, xbytes);
-    const unsigned wbytes = (unsigned)((long)a.K * a.RS * cstride * 2);
-    const i32x4 wrs = buffer_rsrc(a.ws, wbytes);
-    const unsigned wdead = wbytes;                     // B voffset past the last tile: zeros
-    const int bline = a.RS * a.cch * 64;
-    int a_org[ONE ? 1 : GA];
-    unsigned a_off[GA];
-    // B rows of this wave: row_j = RPI*((w*GB + j) % GBT) + lane/CPR — for both
-    // tile widths consecutive j are consecutive 8-row groups and the swizzle
-    // depends only on j's parity: two per-lane bases + a scalar step
-    unsigned b_off2[2];
-    const unsigned bstep = (unsigned)(2 * RPI * a.RS * a.cch * 64 * 2);   // bytes per j += 2
-    long it = lb;
-    int q_buf = 0, q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, ik = 0;
-    auto setup_issue = [&]() {
-        const int mt = (int)(it / a.n_tiles), nt = (int)(it - (long)mt * a.n_tiles);
-        const int m0 = mt * BM, n0 = nt * BN;
-#pragma unroll
-        for (int i = 0; i < GA; ++i) {
-            const int row = RPI * (w * GA + i) + lane / CPR;
-            const int Lc = (lane % CPR) ^ ((row >> 1) & 7);
-            const int m = m0 + row;
-            int hb = -16384, wb = -16384;
-            long off = 0;
-            if (m < a.M) {
-                const int hw = a.Ho * a.Wo;
-                const int n = m / hw, rem = m - n * hw;
-                const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-                hb = ho * a.stride - a.pad;
-                wb = wo * a.stride - a.pad;
-                off = (((long)n * a.H + hb) * a.W + wb) * cstride + Lc * 8;
-            }
-            if constexpr (ONE) a_off[i] = m < a.M ? (unsigned)((off + xbias) * 2) : xbytes;
-            else {
-                a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
-                a_off[i] = (unsigned)((off + xbias) * 2);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 2 && j < GB; ++j) {
-            const int bi = (w * GB + j) % GBT;
-            const int row = RPI * bi + lane / CPR;
-            const int Lc = (lane % CPR) ^ ((row >> 1) & 7);
-            b_off2[j] = (unsigned)(((n0 + row) * bline + Lc * 8) * 2);
-        }
-    };
-    auto b_dst = [&](int j) { return (BM + RPI * ((w * GB + j) % GBT)) * ROW; };
-    if (it < T) setup_issue();
-    // issue_stage: the DMA of the stream's next stage (branch-free: past the last
-    // tile every piece loads zeros), inside the scheduled MFMA region; advance:
-    // its bookkeeping, after the region (the tile switch branches)
-    auto issue_stage = [&]() {
-        char* st = smem + q_buf * STAGE;
-        const bool live = it < T;
-        const int dh = q_rr * a.dil, dw = q_ss * a.dil;
-        const unsigned toff = (unsigned)((((long)dh * a.W + dw) * cstride + q_cc * 64) * 2);
-#pragma unroll
-        for (int i = 0; i < GA; ++i) {
-            if constexpr (ONE) {
-                blds16(xrs, a_off[i], toff, st + (RPI * (w * GA + i)) * ROW);
-            } else {
-                const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
-                const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-                blds16(xrs, in ? a_off[i] : xbytes, toff, st + (RPI * (w * GA + i)) * ROW);
-            }
-        }
-        const unsigned boff = (unsigned)((q_tap * a.cch + q_cc) * 128);
-#pragma unroll
-        for (int j = 0; j < GB; ++j)
-            blds16(wrs, live ? b_off2[j & 1] + (unsigned)(j >> 1) * bstep : wdead, boff, st + b_dst(j));
-    };
-    auto advance = [&]() {
-        q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
-        if (++q_ss == a.S) {
-            q_ss = 0;
-            ++q_rr;
-        }
-        if (++q_tap == a.RS) {
-            q_tap = 0;
-            q_rr = 0;
-            ++q_cc;
-        }
-        if (++ik == nks) {                     // the stream moves on to this block's next tile
-            ik = q_cc = q_tap = q_rr = q_ss = 0;
-            it += G;
-            if (it < T) setup_issue();
-            else {
-#pragma unroll
-                for (int i = 0; i < GA; ++i) {
-                    if constexpr (ONE) a_off[i] = xbytes;
-                    else a_org[i] = (int)(((unsigned)-16384 << 16) | ((unsigned)-16384 & 0xFFFFu));
-                }
-            }
-        }
-    };
-    auto issue_next = [&]() {
-        issue_stage();
-        advance();
-    };
-
-    // ---- compute side (MFMA operands swapped: acc[i][j] = channels x pixels) ----
-    const int r16 = lane & 15, q = lane >> 4;
-    const int sw = (r16 >> 1) & 7;
-    const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
-    const int a_base = (wm * UM * 16) * ROW, b_base = (BM + wn * UN * 16) * ROW;
-    struct FA {
-        f16x8 h[UM], l[UM];
-    };
-    f16x8 bh[UN], bl[UN];
-    f32x4 acc[UM][UN];
-    auto read_a = [&](FA& f, const char* st) {
-#pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            f.h[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_h);
-            f.l[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_l);
-        }
-    };
-    auto read_b = [&](int j, const char* st) {
-        bh[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_h);
-        bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
-    };
-    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
-    };
-    auto mma_col = [&](const FA& f, int j) {
-#pragma unroll
-        for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], bh[j], bl[j], f.h[i], f.l[i], mfma);
-    };
-    int cur = 0;
-    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
-
-    // prologue: stages 0 and 1 of the stream issued, stage 0 landed everywhere
-    issue_next();
-    issue_next();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-    lds_barrier();
-
-    for (long ct = lb; ct < T; ct += G) {
-        const int mt = (int)(ct / a.n_tiles), nt = (int)(ct - (long)mt * a.n_tiles);
-        const int m0 = mt * BM, n0 = nt * BN;
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // invariant here: K-step 0 of tile ct landed in slot cur (every wave past a
-        // barrier since), the stream's next stage issued
-        if constexpr (NST == 2) {
-            FA fa;
-            read_a(fa, smem + cur * STAGE);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) read_b(j, smem + cur * STAGE);
-            // K-step t: wait stage t+1, barrier, issue stage t+2 into t's slot (its
-            // fragments are in registers), MFMAs of t while reading t+1's
-            auto kstep = [&](const bool rd) {
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                lds_barrier();
-                cur ^= 1;
-                const char* st = smem + cur * STAGE;
-                issue_stage();
-#pragma unroll
-                for (int j = 0; j < UN; ++j) {
-                    mma_col(fa, j);
-                    if (rd) read_b(j, st);
-                }
-                if (rd) read_a(fa, st);
-#pragma unroll
-                for (int j = 0; j < UN; ++j) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
-                    if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                    if (j * ((GL + UN - 1) / UN) < GL) __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);
-                }
-                if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);
-                __builtin_amdgcn_sched_barrier(0);
-                advance();
-            };
-            for (int t = 0; t + 1 < nks; ++t) kstep(true);
-            kstep(false);
-        } else {
-            FA fa0, fa1;
-            read_a(fa0, smem + cur * STAGE);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) read_b(j, smem + cur * STAGE);
-            // K-step t: issue stage t+2 into t-1's slot (read before the last
-            // barrier), wait stage t+1, barrier, MFMAs of t while reading t+1's
-            auto step = [&](FA& fc, FA& fn, const bool rd) {
-                issue_stage();
-                advance();
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
-                lds_barrier();
-                cur = cur == NST - 1 ? 0 : cur + 1;
-                const char* st = smem + cur * STAGE;
-                if (rd) read_a(fn, st);
-#pragma unroll
-                for (int j = 0; j < UN; ++j) {
-                    mma_col(fc, j);
-                    if (rd) read_b(j, st);
-                }
-                if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);
-#pragma unroll
-                for (int j = 0; j < UN; ++j) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
-                    if (rd) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            };
-            int t = 0;
-            for (; t + 2 < nks; t += 2) {
-                step(fa0, fa1, true);
-                step(fa1, fa0, true);
-            }
-            if (t + 1 < nks) {
-                step(fa0, fa1, true);
-                step(fa1, fa0, false);
-            } else {
-                step(fa0, fa1, false);
-            }
-        }
-
-        // ---- epilogue: scale, BN partials, vector stores from registers ----
-        // (thread indices laundered per tile: the epilogue's address arithmetic
-        // is otherwise hoisted out of the tile loop and held in registers across
-        // the K loop, which spilled)
-        int etid = tid;
-        asm volatile("" : "+v"(etid));
-        const int elane = etid & 63, er16 = elane & 15, eq = elane >> 4;
-        // lane (r16, q) of fragment (i, j): pixel m0 + wm*16*UM + 16i + r16,
-        // channels n0 + wn*16*UN + 16j + 4q .. +3
-        const int pbase = m0 + wm * UM * 16 + er16;
-        const int cbase = n0 + wn * UN * 16 + 4 * eq;
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            const f32x4 sc = a.wscale ? *(const f32x4*)(a.wscale + cbase + 16 * j) : f32x4{1.f, 1.f, 1.f, 1.f};
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc[r] * ginv;
-        }
-        if (a.part) {
-            auto reduce16 = [](float s) {
-#pragma unroll
-                for (int o = 1; o < 16; o <<= 1) s += __shfl_xor(s, o);
-                return s;
-            };
-            const int crow = wn * UN * 16 + 4 * eq;             // tile column of r = 0
-#pragma unroll
-            for (int j = 0; j < UN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    float s = 0.f;
-#pragma unroll
-                    for (int i = 0; i < UM; ++i) s += (pbase + 16 * i < a.M) ? acc[i][j][r] : 0.f;
-                    s = reduce16(s);
-                    if (er16 == 0) red[wm * BN + crow + 16 * j + r] = s;
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            const long tile128 = (long)(m0 >> 7);
-            for (int e = etid; e < 2 * BN; e += 512) {
-                const int h = e / BN, c = e - h * BN;
-                const int cnt = min(128, a.M - (m0 + 128 * h));
-                if (cnt > 0) {
-                    const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
-                    tmean[h * BN + c] = s / (float)cnt;
-                    a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
-                }
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            const float* mu_h = tmean + (wm >> 1) * BN;
-#pragma unroll
-            for (int j = 0; j < UN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float mu = mu_h[crow + 16 * j + r];
-                    float s = 0.f;
-#pragma unroll
-                    for (int i = 0; i < UM; ++i) {
-                        const float d = acc[i][j][r] - mu;
-                        s += (pbase + 16 * i < a.M) ? d * d : 0.f;
-                    }
-                    s = reduce16(s);
-                    if (er16 == 0) red[wm * BN + crow + 16 * j + r] = s;
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            for (int e = etid; e < 2 * BN; e += 512) {
-                const int h = e / BN, c = e - h * BN;
-                if (a.M - (m0 + 128 * h) > 0)
-                    a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
-            }
-            // red / tmean are next written after this tile's successor's K loop
-            // (barriers in between)
-        }
-#pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            const int p = pbase + 16 * i;
-            if (p >= a.M) continue;
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                if constexpr (P == 1) {
-                    const h16x4 h = {(_Float16)acc[i][j][0], (_Float16)acc[i][j][1], (_Float16)acc[i][j][2],
-                                     (_Float16)acc[i][j][3]};
-                    *(h16x4*)(a.y16 + (long)p * a.K + cbase + 16 * j) = h;
-                } else {
-                    const long off = x3_out_off(a, p, cbase + 16 * j);
-                    f32x4 v = acc[i][j];
-                    if (a.add) v += *(const f32x4*)(a.add + off);
-                    *(f32x4*)(a.y + off) = v;
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the zero-line tail DMAs land before the block ends
-}
-
-
-// ---------------------------------------------------------------------------
 // operand packing
 
 __device__ __forceinline__ void split_store(float v, _Float16* hi_p) {   // hi at p, lo at p + 32
@@ -2314,7 +1944,7 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int wo, int* splits, int*
     const long max_sp = std::max(1L, (M + 511) / 512);
     long sp = 1;
     double best = -1.0;
-    for (long c = 1; c <= max_sp; ++c) {
+    for (long c = 1; c <= max_sp && d->tile <= 0; ++c) {
         const long blocks = tiles * c;
         const long rounds = (blocks + 255) / 256;
         if (rounds > 4) break;
@@ -2325,6 +1955,7 @@ static void wg_x3_plan(const hkp_conv_desc* d, long M, int wo, int* splits, int*
             sp = c;
         }
     }
+    if (d->tile > 0) sp = std::max(1L, std::min<long>(max_sp, d->tile / tiles));   // the caller's CU budget
     long m = (M + sp - 1) / sp;
     m = (m + 31) / 32 * 32;
     *splits = (int)((M + m - 1) / m);
@@ -2499,14 +2130,10 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
 struct X3Choice {
     int bn, mfd;
     bool pair, sk;
-    bool persist = false;              // conv_x3p_kernel<bn, P, one>
-    bool one = false;
     bool halo = false;                 // conv_x3_halo_kernel<P>
 };
-// one: a 1x1 conv without padding; pfit: the persistent kernel's 32-bit byte
-// offsets cover the operands (x3p_fits)
-static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, bool one = false,
-                          bool pfit = false, bool halo_ok = false) {
+// halo_ok: the halo-tile body takes the shape (x3_halo_ok)
+static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, bool halo_ok = false) {
     // the halo-tile body wherever the shape allows it, unless a tile body is forced
     if (halo_ok && (policy == HKP_TILE_HALO || policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL)) {
         X3Choice c{64, 16, true, false};
@@ -2525,13 +2152,6 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
             break;
         case HKP_TILE_64_PAIR:
             return {64, 16, true, false};
-        case HKP_TILE_256_PERSIST:         // 256x256 only as the 1x1 body (the KxK one spills)
-            if (pfit && k % 256 == 0 && one) return {256, 16, false, false, true, true};
-            if (pfit && k % 128 == 0) return {128, 16, false, false, true, one};
-            break;
-        case HKP_TILE_128_PERSIST:
-            if (pfit && k % 128 == 0) return {128, 16, false, false, true, one};
-            break;
         case HKP_TILE_256_TAIL:            // 256x256, the partial last round as split-K segments
             if (k % 256 == 0) return {256, 16, false, false};
             break;
@@ -2550,20 +2170,12 @@ static const X3Choice X3_STEM{64, 16, true, false};
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
-    if (c.persist) return snprintf(buf, len, "conv_x3p_kernel<%d, %d, %s>", c.bn, P, c.one ? "true" : "false");
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
 
 template <int P>
 static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Args& a) {
-    if (c.persist) {
-        const unsigned g = (unsigned)std::min<long>((long)grid.x, x3_cus());
-        if (c.bn == 256) hipLaunchKernelGGL((conv_x3p_kernel<256, P, true>), dim3(g), dim3(512), 0, st, a);
-        else if (c.one) hipLaunchKernelGGL((conv_x3p_kernel<128, P, true>), dim3(g), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_x3p_kernel<128, P, false>), dim3(g), dim3(512), 0, st, a);
-        return;
-    }
     if (c.sk && c.bn == 128)
         hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 16, true, P>), grid, dim3(512), 0, st, a);
     else if (c.sk)
@@ -2580,13 +2192,6 @@ static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Ar
 
 // a.RS, a.cch (128-B lines per pixel), a.M ... set by the caller; P = operand
 // layout (3 packed f16x3 split, 1 plain fp16)
-// the persistent kernel addresses its operands with 32-bit BYTE offsets from
-// the input base less the padded-out margin, and from the weights
-static bool x3p_fits(long n, long h, long w, long cstride, long pad, long k, long rs) {
-    return ((long)pad * (w + 1) * cstride + n * h * w * cstride) * 2 < (1L << 32) - 256 &&
-           k * rs * cstride * 2 < (1L << 32) - 256;
-}
-
 static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
@@ -2601,9 +2206,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.stamps = g_x3_stamps;
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
-    const bool one = a.RS == 1 && a.pad == 0;
-    const bool pfit = x3p_fits(a.N, a.H, a.W, a.cch * 64L, a.pad, a.K, a.RS);
-    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, one, pfit, x3_halo_ok(a, k));
+    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_ok(a, k));
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
@@ -2628,7 +2231,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     const long G = x3_cus();
     const long rm = tiles / G * G / a.n_tiles;              // m-tiles of the full rounds
     const long tm = m_tiles - rm;
-    long NG = (!c.sk && !c.persist && c.bn == 256 && sk_ok &&
+    long NG = (!c.sk && c.bn == 256 && sk_ok &&
                (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))
                   ? x3_tail_groups(m_tiles, a.n_tiles, nks) : 0;
     // one round, every group non-empty and inside two tiles, slabs and counters in the workspace
@@ -2690,6 +2293,8 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
     HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_HALO, "%s: unknown tile policy %d", who, d->tile);
+    HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8,
+                  "%s: tile policy %d is retired (the persistent conv, measured slower)", who, d->tile);
     return HKP_OK;
 }
 
@@ -2747,8 +2352,6 @@ extern "C" int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f
                                      void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
     HKP_CHECK_ARG(d && out_f16 && scale_shift, "hkp_conv2d_fwd_f16_bn: null argument");
     HKP_CHECK_ARG(!res_scale_shift || res_f16, "hkp_conv2d_fwd_f16_bn: res_scale_shift needs a residual");
-    HKP_CHECK_ARG(d->tile != HKP_TILE_256_PERSIST && d->tile != HKP_TILE_128_PERSIST,
-                  "hkp_conv2d_fwd_f16_bn: the persistent bodies have no fused epilogue");
     X3Args ep;
     ep.ep_ss = scale_shift;
     ep.ep_res = (const _Float16*)res_f16;
@@ -3018,8 +2621,10 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
     int ho, wo;
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
-    rc = check_tile(d, "hkp_conv_kernel_name");
-    if (rc) return rc;
+    if (op != HKP_KOP_WGRAD_X3) {          // a wgrad's d->tile is its CU budget
+        rc = check_tile(d, "hkp_conv_kernel_name");
+        if (rc) return rc;
+    }
     const bool sk = stream_k_ok != 0;
     switch (op) {
         case HKP_KOP_FWD_X3:
@@ -3028,11 +2633,9 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const long m = (long)d->n * ho * wo;
             const int cg = P == 3 ? 32 : 64;
             const int nks = d->r * d->s * (d->c / cg);
-            const bool one = d->r * d->s == 1 && d->pad == 0;
-            const bool pfit = x3p_fits(d->n, d->h, d->w, d->c / cg * 64L, d->pad, d->k, d->r * d->s);
             const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
                               (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);
-            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, one, pfit, halo), false, P, buf,
+            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, halo), false, P, buf,
                                   len);
         }
         case HKP_KOP_DGRAD_X3: {
@@ -3041,7 +2644,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int padp = d->dilation * (d->r - 1) - d->pad;
             const bool halo = halo_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
                               (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32);
-            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, false, false, halo), false, 3,
+            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, halo), false, 3,
                                   buf, len);
         }
         case HKP_KOP_STEM_X3:

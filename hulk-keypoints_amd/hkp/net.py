@@ -564,7 +564,7 @@ def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
             side.wait_stream(main)                     # dy split (and x split) written
             with torch.cuda.stream(side):
                 dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax,
-                                              alloc_stream=main)
+                                              alloc_stream=main, cus=pol.wgrad_overlap_cus)
                 ready = torch.cuda.Event()
                 ready.record(side)
             for t in (xs[0], dys, amax):              # read on the side stream: keep their memory

@@ -899,8 +899,10 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=
     return dx
 
 
-def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, alloc_stream=None):
+def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, alloc_stream=None, cus=0):
     """f16x3 dL/dw (KRSC) from packed x (forward operand) and packed dy (split_pack_x3 with `amax`).
+    cus: the CUs the grid should occupy (pixel-range splits = max(1, cus / tiles);
+    0: the planner's count, filling whole rounds of every CU).
     alloc_stream: take dw and the workspace from that stream's memory pool (marked
     as used by the launching stream) — a side-stream wgrad then shares the main
     stream's cached blocks instead of growing a second pool (C5 at 245 GB: the
@@ -910,6 +912,7 @@ def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, al
     _need(dys, torch.float16, "conv2d_bwd_filter_x3.dy_split", 4)
     n, h, wd, c2 = xs.shape
     d = _fwd_desc((n, h, wd, c2 // 2), tuple(w_shape), stride, pad, dil, "nhwc")
+    d.tile = int(cus)
     ho, wo = conv_out_hw(h, wd, d.r, d.s, stride, pad, dil)
     if tuple(dys.shape) != (n, ho, wo, 2 * d.k):
         raise HkpError("conv2d_bwd_filter_x3: dy split shape %s != %s" % (tuple(dys.shape), (n, ho, wo, 2 * d.k)))

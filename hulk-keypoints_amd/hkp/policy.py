@@ -31,6 +31,9 @@ class Policy:
     overlap_wgrad: bool = True
     # HKP_TILE_* of a dgrad overlapped by its wgrad (9 = 256x256 + split-K tail)
     dgrad_overlap_tile: int = 9
+    # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
+    # (0 = the planner's split count, filling every CU as if it ran alone)
+    wgrad_overlap_cus: int = 0
     # inner BN ReLU masks recomputed from y in the backward (no fp32 activation kept)
     mask_from_y: bool = True
     # inference: last block's BN apply fused with the K-row head

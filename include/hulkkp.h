@@ -71,8 +71,8 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_128_MF16 4
 #define HKP_TILE_128_MF32 5
 #define HKP_TILE_64_PAIR 6
-#define HKP_TILE_256_PERSIST 7        /* persistent 256x256 (conv_x3p_kernel) */
-#define HKP_TILE_128_PERSIST 8        /* persistent 256x128 */
+#define HKP_TILE_RESERVED_7 7         /* retired: the persistent conv (measured slower */
+#define HKP_TILE_RESERVED_8 8         /* than the one-tile grid); rejected with HKP_ERR_ARG */
 #define HKP_TILE_256_TAIL 9           /* 256x256; tiles past the last full round as split-K segments */
 #define HKP_TILE_HALO 10              /* 8x32-pixel halo tiles (stride-1 3x3, pad = dil = 1, Ho%8 = Wo%32 = 0;
                                          the default there under AUTO and 256_TAIL) */
@@ -380,7 +380,11 @@ int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, cons
  *   hkp_conv2d_bwd_filter_x3: dw (KRSC) from x_split (forward operand) and dy_split;
  *                            split-K over output pixels into `workspace`
  *                            (hkp_conv_bwd_filter_x3_workspace bytes), fixed-order
- *                            reduce; needs Cout % 64 == 0, Cin % 32 == 0.
+ *                            reduce; needs Cout % 64 == 0, Cin % 32 == 0.  Here
+ *                            d->tile is the number of CUs the grid should occupy
+ *                            (0: the planner's split count, which fills whole
+ *                            rounds of all CUs; a wgrad sharing the GPU with a
+ *                            dgrad may take fewer): splits = max(1, tile / tiles).
  * Replace the same cuDNN backward calls as hkp_conv2d_bwd_data / _filter. */
 int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits, uint16_t* x_split,
                       hkp_stream_t stream);

@@ -23,6 +23,7 @@ SHAPES = {
     "layer3": ("x3", 32, 60, 80, 256, 256, 3, 1, 2, 2),
     "layer2": ("x3", 32, 60, 80, 128, 128, 3, 1, 1, 1),
     "layer1": ("x3", 32, 120, 160, 64, 64, 3, 1, 1, 1),
+    "h128": ("x3", 4, 240, 320, 128, 128, 3, 1, 1, 1),           # halo body at 128 channels
     "t4": ("x3", 8, 60, 80, 512, 512, 3, 1, 4, 4),             # training shard (batch 8)
     "t3": ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),
     # R50-8s @640x480, batch 128 (C4, plain fp16)
