@@ -124,6 +124,9 @@ SIGNATURES = {
     "hkp_head_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I64, _P]),
     "hkp_head_fc_bwd_workspace": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_head_fc_bwd": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    # hybrid JPEG decode, device half (the geometry struct: hkp.jpeg.Geom)
+    "hkp_jpeg_planes_bytes": (_I64, [_P]),
+    "hkp_jpeg_reconstruct": (ctypes.c_int, [_I32, _P, _P, _P, _P, _I64, _P, _P]),
 }
 
 _lib = None

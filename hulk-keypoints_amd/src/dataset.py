@@ -142,6 +142,44 @@ class _RawView(Dataset):
         return imread_bgr(self.paths[i]), self.labels[i]
 
 
+class _CoefView(Dataset):
+    """Decode-worker items for DeviceBatches(decode="device"): the host half of the
+    hybrid JPEG decode (hkp.jpeg.entropy_decode: quantised DCT coefficients and
+    tables), or the host-decoded image for a file outside that decoder's subset."""
+
+    def __init__(self, ds):
+        self.paths, self.labels = ds.imgs, ds.labels_np
+
+    def __len__(self):
+        return len(self.paths)
+
+    def __getitem__(self, i):
+        from hkp import jpeg
+        path = self.paths[i]
+        try:
+            with open(path, "rb") as f:
+                coefs, qt, g = jpeg.entropy_decode(f.read())
+        except jpeg.JpegUnsupported:
+            return ("img", imread_bgr(path), self.labels[i], path)
+        return ("coef", (coefs, qt, bytes(g)), self.labels[i], path)
+
+
+def _collate_coef(items):
+    """One batch of _CoefView items: ("coef", coefs int16 [B,nblocks,64], qt
+    [B,ncomp,64], geometry bytes, uv) when every image went through the entropy
+    decoder with one geometry, else ("img", uint8 [B,H,W,3], uv) decoded on the host."""
+    from hkp import jpeg
+    uv = torch.from_numpy(np.stack([it[2] for it in items]))
+    if all(it[0] == "coef" for it in items):
+        geoms = [jpeg.Geom.from_buffer_copy(it[1][2]) for it in items]
+        if all(g.key() == geoms[0].key() for g in geoms):
+            coefs = torch.from_numpy(np.stack([it[1][0] for it in items]))
+            qt = torch.from_numpy(np.stack([it[1][1] for it in items]).view(np.int16))
+            return ("coef", coefs, qt, items[0][1][2], uv)
+    imgs = [it[1] if it[0] == "img" else imread_bgr(it[3]) for it in items]
+    return ("img", torch.from_numpy(np.stack(imgs)), uv)
+
+
 class _EpochBatches:
     """Batch sampler of the persistent decode loader: the current epoch's index
     batches (set by DeviceBatches before each epoch; iterated in the main process)."""
@@ -166,19 +204,28 @@ class DeviceBatches:
     """Iterate a KeypointsDataset as device batches (img uint8 [B,H,W,3], uv fp32
     [B,K,2]) for model.forward / Trainer.step(img, uv=uv).
 
-    Decode happens on the host (cv2 / PIL, as the reference): in the calling thread
-    (workers=0), or in `workers` DataLoader processes that decode and stack whole
-    batches ahead (`prefetch` batches per worker) into pinned memory.  Each batch
-    is copied with non_blocking=True on a side stream while the previous batch
-    computes; the consumer's stream waits on an event.  `shuffle` uses a seeded
-    permutation per epoch (train.py:61-67 shuffles); batches come in order for
-    any worker count."""
+    decode="host": images are decoded on the host (cv2 / PIL, as the reference).
+    decode="device": the hybrid JPEG decode (hkp.jpeg) — the host only
+    entropy-decodes the quantised DCT coefficients; they are copied (about the
+    size of the decoded image) and the IDCT, upsampling and colour conversion run
+    on the GPU on the copy stream, bit-identical to the host decode.  Files
+    outside that decoder's subset (progressive, CMYK, ...) and batches of mixed
+    geometry are decoded on the host instead.
+
+    Host work runs in the calling thread (workers=0), or in `workers` DataLoader
+    processes that decode and stack whole batches ahead (`prefetch` batches per
+    worker) into pinned memory.  Each batch is copied with non_blocking=True on a
+    side stream while the previous batch computes; the consumer's stream waits on
+    an event.  `shuffle` uses a seeded permutation per epoch (train.py:61-67
+    shuffles); batches come in order for any worker count."""
 
     def __init__(self, dataset, batch_size, shuffle=False, seed=0, drop_last=False, device="cuda", workers=0,
-                 prefetch=4):
+                 prefetch=4, decode="host"):
+        if decode not in ("host", "device"):
+            raise ValueError("decode must be 'host' or 'device', got %r" % (decode,))
         self.ds, self.bs, self.shuffle, self.seed, self.drop_last = dataset, batch_size, shuffle, seed, drop_last
         self.device = torch.device(device)
-        self.workers, self.prefetch = workers, prefetch
+        self.workers, self.prefetch, self.decode = workers, prefetch, decode
         self.epoch = 0
         self._loader = None
         self._sampler = _EpochBatches()
@@ -188,19 +235,31 @@ class DeviceBatches:
         return n // self.bs if self.drop_last else (n + self.bs - 1) // self.bs
 
     def _host_batches(self, batches):
-        """(pinned uint8 [B,H,W,3], float32 [B,K,2]) per index batch, in order."""
+        """Per index batch, in order: ("img", pinned uint8 [B,H,W,3], float32 [B,K,2])
+        or (decode="device") ("coef", pinned coefs, pinned qt, geometry bytes, uv)."""
+        view, collate = ((_RawView(self.ds), _collate_u8) if self.decode == "host"
+                         else (_CoefView(self.ds), _collate_coef))
         if self.workers <= 0:
             for idx in batches:
-                imgs, uv = _collate_u8([(imread_bgr(self.ds.imgs[i]), self.ds.labels_np[i]) for i in idx])
-                yield imgs.pin_memory(), uv
+                yield self._tag(collate([view[i] for i in idx]))
             return
         if self._loader is None:               # persistent workers: started once, reused every epoch
             from torch.utils.data import DataLoader
-            self._loader = DataLoader(_RawView(self.ds), batch_sampler=self._sampler, num_workers=self.workers,
-                                      collate_fn=_collate_u8, pin_memory=True, prefetch_factor=self.prefetch,
+            self._loader = DataLoader(view, batch_sampler=self._sampler, num_workers=self.workers,
+                                      collate_fn=collate, pin_memory=True, prefetch_factor=self.prefetch,
                                       persistent_workers=True)
         self._sampler.batches = [list(map(int, b)) for b in batches]
-        yield from self._loader
+        for b in self._loader:
+            yield self._tag(b)
+
+    def _tag(self, b):
+        """Host batches in one form, tensors pinned (the loader pins them already)."""
+        if self.decode == "host":
+            imgs, uv = b
+            return ("img", imgs if imgs.is_pinned() else imgs.pin_memory(), uv)
+        if b[0] == "img":
+            return ("img", b[1] if b[1].is_pinned() else b[1].pin_memory(), b[2])
+        return tuple(t.pin_memory() if torch.is_tensor(t) and not t.is_pinned() else t for t in b)
 
     def __iter__(self):
         n = len(self.ds)
@@ -213,9 +272,18 @@ class DeviceBatches:
         host = self._host_batches(batches)
 
         def stage():
-            buf, uv = next(host)
+            b = next(host)
             with torch.cuda.stream(copy_stream):
-                img = buf.to(self.device, non_blocking=True)
+                if b[0] == "img":
+                    buf, uv = b[1], b[2]
+                    img = buf.to(self.device, non_blocking=True)
+                else:                          # hybrid decode: coefficients up, pixels made on the device
+                    from hkp import jpeg
+                    _, coefs, qt, gbytes, uv = b
+                    buf = (coefs, qt)
+                    g = jpeg.Geom.from_buffer_copy(gbytes)
+                    img = jpeg.reconstruct(coefs.to(self.device, non_blocking=True),
+                                           qt.to(self.device, non_blocking=True), g, coefs.shape[0])
                 uvd = uv.to(self.device, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(copy_stream)

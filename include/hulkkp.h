@@ -25,6 +25,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "hkp_jpeg.h"   /* hkpj_geom: the host half of the hybrid JPEG decode */
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -531,6 +533,19 @@ int64_t hkp_head_fc_bwd_workspace(int32_t n, int32_t hw, int32_t c, int32_t k);
 int hkp_head_fc_bwd(int32_t n, int32_t hw, int32_t c, int32_t k, const float* dlow, const float* feat,
                     const float* w, float* dfeat, float* dw, float* db, void* workspace, int64_t ws_bytes,
                     hkp_stream_t stream);
+
+/* ----------------------------------------------------------- JPEG ---- */
+/* Device half of the hybrid JPEG decode (hkp_jpeg.h; replaces cv2.imread,
+ * src/dataset.py:71): n images of one geometry g (hkpj_probe), coefs = int16
+ * [n][g->nblocks][64] and qt = uint16 [n][g->ncomp][64] from hkpj_decode, on
+ * the device → out_bgr = uint8 [n][H][W][3] BGR, bit-identical to
+ * libjpeg-turbo's default decode (islow IDCT, fancy upsampling).  planes:
+ * workspace of n * hkp_jpeg_planes_bytes(g) bytes (the IDCT'd component
+ * planes).  hkp_jpeg_planes_bytes returns -1 for a geometry the kernels do not
+ * take. */
+int64_t hkp_jpeg_planes_bytes(const hkpj_geom* g);
+int hkp_jpeg_reconstruct(int32_t n, const hkpj_geom* g, const int16_t* coefs, const uint16_t* qt, uint8_t* planes,
+                         int64_t planes_bytes, uint8_t* out_bgr, hkp_stream_t stream);
 
 #ifdef __cplusplus
 }

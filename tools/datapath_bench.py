@@ -6,7 +6,10 @@ dataset.py:71 / train.py:51) and with N DataLoader decode workers, vs the
 compute rate of the C2 inference step.  Synthetic images (smooth gradients +
 noise, JPEG quality 95), written to a temp dir.
 
-    python tools/datapath_bench.py [--n 512] [--batch 32] [--workers 0,4,8,15]
+    python tools/datapath_bench.py [--n 512] [--batch 32] [--workers 0,4,8,15] [--decode host,device]
+
+--decode device: the hybrid decode (hkp.jpeg) — workers only entropy-decode, the
+IDCT / upsampling / colour conversion run on the GPU on the copy stream.
 """
 import argparse
 import json
@@ -40,6 +43,7 @@ def main():
     ap.add_argument("--n", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--workers", default="0,4,8,15")
+    ap.add_argument("--decode", default="host,device")
     args = ap.parse_args()
     from src.dataset import DeviceBatches, KeypointsDataset, transform
     H, W, K = 480, 640, 4
@@ -52,8 +56,8 @@ def main():
             cpus = min(cpus, int(q) // int(per)) if q != "max" else cpus
         except (OSError, ValueError):
             pass
-        for w in [int(v) for v in args.workers.split(",")]:
-            it = DeviceBatches(ds, args.batch, shuffle=True, workers=w)
+        for w, dec in [(int(v), d) for d in args.decode.split(",") for v in args.workers.split(",")]:
+            it = DeviceBatches(ds, args.batch, shuffle=True, workers=w, decode=dec)
             for _ in it:                       # warm epoch: page cache, persistent worker start-up
                 pass
             torch.cuda.synchronize()
@@ -63,7 +67,7 @@ def main():
                 n += img.shape[0]
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"workers": w, "images": n, "seconds": round(dt, 3), "images_per_sec": round(n / dt, 1),
+            print(json.dumps({"decode": dec, "workers": w, "images": n, "seconds": round(dt, 3), "images_per_sec": round(n / dt, 1),
                               "batch": args.batch, "image": "%dx%d JPEG q95" % (W, H),
                               "host_cpu_share": cpus}), flush=True)
 
