@@ -24,6 +24,7 @@ echo "pytest ok: $(tail -1 $O/pytest_gpu.log)"
 timeout -k 10 300 python -u bench.py > $O/bench_infer.log 2>&1
 timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline > $O/bench_train.log 2>&1
 timeout -k 10 300 python -u bench.py $C4 --no-cpu-baseline > $O/bench_c4.log 2>&1
+timeout -k 10 400 python -u tools/datapath_bench.py --n 1024 --workers 0,8,15 --decode host,device > $O/datapath.log 2>&1
 echo "bench ok"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_infer -o run -- python3 bench.py --steps 10 --no-extras --no-cpu-baseline > $O/prof_infer.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run -- python3 bench.py --mode train --steps 10 --no-cpu-baseline > $O/prof_train.log 2>&1
