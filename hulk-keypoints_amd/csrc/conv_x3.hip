@@ -2132,10 +2132,13 @@ struct X3Choice {
     bool pair, sk;
     bool halo = false;                 // conv_x3_halo_kernel<P>
 };
-// halo_ok: the halo-tile body takes the shape (x3_halo_ok)
-static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, bool halo_ok = false) {
+// halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
+// forces it), 2 it is also the default (64 input channels: measured faster;
+// at 128 channels it ties the ring bodies, which then stay)
+static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo = 0) {
     // the halo-tile body wherever the shape allows it, unless a tile body is forced
-    if (halo_ok && (policy == HKP_TILE_HALO || policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL)) {
+    if ((halo >= 1 && policy == HKP_TILE_HALO) ||
+        (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))) {
         X3Choice c{64, 16, true, false};
         c.halo = true;
         return c;
@@ -2196,6 +2199,11 @@ static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
+// lines: 128-B input lines per pixel (32 channels each for P 3, 64 for P 1)
+static int x3_halo_level(bool ok, int lines, int P) {
+    return !ok ? 0 : lines * (P == 3 ? 32 : 64) <= 64 ? 2 : 1;
+}
+
 static bool x3_halo_ok(const X3Args& a, int k) {
     return halo_shape(a.stride, a.R, a.S, a.pad, a.dil, a.Ho, a.Wo, k) && a.ost == 0 && a.ep_ss == nullptr &&
            a.mt0 == 0 && a.plane == 0 && (long)a.N * a.H * a.W * a.cch * 64L + 64 < (1L << 32);
@@ -2206,7 +2214,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.stamps = g_x3_stamps;
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
-    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_ok(a, k));
+    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_level(x3_halo_ok(a, k), a.cch, P));
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
@@ -2635,8 +2643,9 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int nks = d->r * d->s * (d->c / cg);
             const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
                               (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);
-            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, halo), false, P, buf,
-                                  len);
+            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile,
+                                            x3_halo_level(halo, d->c / cg, P)),
+                                  false, P, buf, len);
         }
         case HKP_KOP_DGRAD_X3: {
             const long m = (long)d->n * d->h * d->w;
@@ -2644,8 +2653,8 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int padp = d->dilation * (d->r - 1) - d->pad;
             const bool halo = halo_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
                               (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32);
-            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, halo), false, 3,
-                                  buf, len);
+            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->k / 32, 3)),
+                                  false, 3, buf, len);
         }
         case HKP_KOP_STEM_X3:
             return x3_kernel_name(X3_STEM, true, 3, buf, len);

@@ -77,7 +77,8 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_RESERVED_8 8         /* than the one-tile grid); rejected with HKP_ERR_ARG */
 #define HKP_TILE_256_TAIL 9           /* 256x256; tiles past the last full round as split-K segments */
 #define HKP_TILE_HALO 10              /* 8x32-pixel halo tiles (stride-1 3x3, pad = dil = 1, Ho%8 = Wo%32 = 0;
-                                         the default there under AUTO and 256_TAIL) */
+                                         the default there under AUTO and 256_TAIL when the
+                                         input has 64 channels) */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);

@@ -333,20 +333,24 @@ def test_halo_tiles_equal_pair_body(cuda_device, case, prec):
     """The halo-tile body (8x32 patches, the nine taps read from one staged
     halo image) runs the same MFMAs in the same order as the 256x64 pair body:
     outputs and BN partials bit-identical (forward, both operand layouts), and
-    the stride-1 dgrad too; the planner picks it for these shapes."""
+    the stride-1 dgrad too; the planner picks it for 64-channel inputs (where it
+    measured faster), HKP_TILE_HALO forces it elsewhere."""
     from hkp import ops
-    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_TILE_64_PAIR, ConvDesc
+    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_TILE_64_PAIR, HKP_TILE_HALO, ConvDesc
     n, h, w, cin, cout = case
     d = cuda_device
     x = F.relu(rand(n, h, w, cin, seed=31)).to(d)
     wt = rand(cout, 3, 3, cin, seed=32, scale=(2.0 / (9 * cout)) ** 0.5).to(d)
+    halo = HKP_TILE_HALO
     desc = ConvDesc(n, h, w, cin, cout, 3, 3, 1, 1, 1, 0, 0)
+    forced = ConvDesc(n, h, w, cin, cout, 3, 3, 1, 1, 1, 0, halo)
     if prec == "x3":
-        assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_halo_kernel<3>"
+        assert ops.kernel_name(forced, HKP_KOP_FWD_X3) == "conv_x3_halo_kernel<3>"
+        assert (ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_halo_kernel<3>") == (cin <= 64)
         ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
         xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
         wp = ops.weight_pack_x3(wt)
-        y0, p0 = ops.conv2d_fwd_x3(xs, wp, 1, 1, 1)
+        y0, p0 = ops.conv2d_fwd_x3(xs, wp, 1, 1, 1, tile=halo)
         y1, p1 = ops.conv2d_fwd_x3(xs, wp, 1, 1, 1, tile=HKP_TILE_64_PAIR)
         ref = F.conv2d(x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double(), None, 1, 1, 1)
         assert (y0.double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * ref.abs().max().item()
@@ -356,17 +360,18 @@ def test_halo_tiles_equal_pair_body(cuda_device, case, prec):
         dys = ops.split_pack_x3(gy, amax)
         wf = ops.weight_flip_pack_x3(wt)
         add = rand(n, h, w, cin, seed=34).to(d)
-        ddesc = ConvDesc(n, h, w, cin, cout, 3, 3, 1, 1, 1, 0, 0)
-        assert ops.kernel_name(ddesc, HKP_KOP_DGRAD_X3) == "conv_x3_halo_kernel<3>"
-        dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), 1, 1, add=add, amax=amax)
+        assert ops.kernel_name(forced, HKP_KOP_DGRAD_X3) == "conv_x3_halo_kernel<3>"
+        assert (ops.kernel_name(desc, HKP_KOP_DGRAD_X3) == "conv_x3_halo_kernel<3>") == (cout <= 64)
+        dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), 1, 1, add=add, amax=amax, tile=halo)
         dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), 1, 1, add=add, amax=amax, tile=HKP_TILE_64_PAIR)
         assert torch.equal(dx0, dx1)
     else:
-        assert ops.kernel_name(desc, HKP_KOP_FWD_F16) == "conv_x3_halo_kernel<1>"
+        assert ops.kernel_name(forced, HKP_KOP_FWD_F16) == "conv_x3_halo_kernel<1>"
+        assert (ops.kernel_name(desc, HKP_KOP_FWD_F16) == "conv_x3_halo_kernel<1>") == (cin <= 64)
         x16 = x.half()
         x16._hkp_split_passes = 1
         wp = ops.weight_pack_f16(wt)
-        y0, p0 = ops.conv2d_fwd_f16(x16, wp, 1, 1, 1)
+        y0, p0 = ops.conv2d_fwd_f16(x16, wp, 1, 1, 1, tile=halo)
         y1, p1 = ops.conv2d_fwd_f16(x16, wp, 1, 1, 1, tile=HKP_TILE_64_PAIR)
     assert torch.equal(y0, y1)
     # BN partials: the same sums over differently grouped rows (patches vs row
