@@ -204,132 +204,163 @@ __global__ __launch_bounds__(256, 2) void gram_f16_kernel(GramArgs g) {
 // accumulator order of an upper-triangle tile — and the blocks after them the
 // column sums, mu[c] = sum / M.  Centring (Sigma = E - mu mu^T) happens in fp64
 // where the quadratic forms are taken (bn_from_gram_kernel).
+// SG split groups per value: a block is 256/SG consecutive values (coalesced
+// loads of each split's slab) x SG groups of the splits, each group summing
+// its contiguous split range in order (8 loads in flight), the SG group sums
+// added in group order through LDS — fixed order.  SG = 4 for many splits (R50
+// layer1's 512 split sums by one thread each were latency-bound at 26 us).
+template <int SG>
 __global__ __launch_bounds__(256) void gram_reduce_kernel(int C, int TC, int tiles, int splits, long M,
                                                           const float* part, const float* psum, double* mu,
                                                           double* e2) {
+    constexpr int NV = 256 / SG;                           // values per block
+    __shared__ double red[SG][NV];
     const long per = (long)TC * TC, nel = per * tiles;
-    const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const long eblocks = (nel + 255) / 256;
+    const int v = threadIdx.x % NV, g = threadIdx.x / NV;
+    const long gid = (long)blockIdx.x * NV + v;
     const double inv = 1.0 / (double)M;
-    if ((long)blockIdx.x >= eblocks) {
-        const long c = gid - eblocks * 256;
-        if (c >= C) return;
-        const int nb = C / TC, ib = (int)(c / TC), cc = (int)(c - (long)ib * TC);
-        const float* p = psum + (long)ib * TC + cc;
-        const long st = (long)nb * TC;
+    const int k_lo = (int)((long)splits * g / SG), k_hi = (int)((long)splits * (g + 1) / SG);
+    auto split_sum = [&](const float* p, long st) -> double {
         double s = 0.0;
-        int k = 0;
-        for (; k + 8 <= splits; k += 8) {
-            float v[8];
+        int k = k_lo;
+        for (; k + 8 <= k_hi; k += 8) {
+            float x[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * st];
+            for (int u = 0; u < 8; ++u) x[u] = p[(long)(k + u) * st];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) s += (double)v[u];
+            for (int u = 0; u < 8; ++u) s += (double)x[u];
         }
-        for (; k < splits; ++k) s += (double)p[(long)k * st];
-        mu[c] = s * inv;
-        return;
-    }
-    if (gid >= nel) return;
-    const int t = (int)(gid / per), x = (int)(gid - (long)t * per);
-    // x = ((w * UT + i) * UT + j) * 256 + lane * 4 + r   (UT = TC / 32)
-    const int UT = TC / 32, WT = TC / 2;
-    const int r = x & 3, lane = (x >> 2) & 63, ij = x >> 8;
-    const int j = ij % UT, i = (ij / UT) % UT, w = ij / (UT * UT);
-    const int wm = w >> 1, wn = w & 1;
-    int ib, jb;
-    gram_tile(t, C / TC, &ib, &jb);
-    const int ci = ib * TC + wm * WT + 16 * i + 4 * (lane >> 4) + r;
-    const int cj = jb * TC + wn * WT + 16 * j + (lane & 15);
-    const float* p = part + (long)t * per + x;
-    const long st = (long)tiles * per;
+        for (; k < k_hi; ++k) s += (double)p[(long)k * st];
+        return s;
+    };
+    // value gid: a second moment (gid < nel) or a column sum (the means)
+    const bool is_e = gid < nel, live = gid < nel + C;
     double s = 0.0;
-    int k = 0;
-    for (; k + 8 <= splits; k += 8) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = p[(long)(k + u) * st];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) s += (double)v[u];
+    int ci = 0, cj = 0;
+    if (is_e) {
+        const int t = (int)(gid / per), x = (int)(gid - (long)t * per);
+        // x = ((w * UT + i) * UT + j) * 256 + lane * 4 + r   (UT = TC / 32)
+        const int UT = TC / 32;
+        const int r = x & 3, fl = (x >> 2) & 63, ij = x >> 8;
+        const int j = ij % UT, i = (ij / UT) % UT, w = ij / (UT * UT);
+        const int wm = w >> 1, wn = w & 1, WT = TC / 2;
+        int ib, jb;
+        gram_tile(t, C / TC, &ib, &jb);
+        ci = ib * TC + wm * WT + 16 * i + 4 * (fl >> 4) + r;
+        cj = jb * TC + wn * WT + 16 * j + (fl & 15);
+        s = split_sum(part + (long)t * per + x, (long)tiles * per);
+    } else if (live) {
+        const long c = gid - nel;
+        const int nb = C / TC, ib = (int)(c / TC), cc = (int)(c - (long)ib * TC);
+        s = split_sum(psum + (long)ib * TC + cc, (long)nb * TC);
     }
-    for (; k < splits; ++k) s += (double)p[(long)k * st];
-    const double v = s * inv;
-    e2[(long)ci * C + cj] = v;
-    e2[(long)cj * C + ci] = v;
+    if constexpr (SG > 1) {
+        red[g][v] = s;
+        __syncthreads();
+        if (g != 0) return;
+#pragma unroll
+        for (int q = 1; q < SG; ++q) s += red[q][v];
+    }
+    if (!live) return;
+    if (is_e) {
+        const double val = s * inv;
+        e2[(long)ci * C + cj] = val;
+        e2[(long)cj * C + ci] = val;
+    } else {
+        mu[gid - nel] = s * inv;
+    }
 }
 
 // Per output channel k of y = W a: mean = w_k . mu and
 // var = w_k^T E w_k - mean^2 (E = the raw second moments; fp64 throughout — the
 // centring loses only log10(1 + mean^2/var) of fp64's digits), with w_k = the
 // fp16 packed weight row x its inverse scale (the weights the conv multiplies
-// with), then bn_fin_store.  A block takes KB channels (their weights in LDS,
-// read as broadcasts); thread t owns columns j = t, t + 512: for every row i it
-// accumulates s_k[j] += E[i][j] w_k[i] (coalesced row loads of E, 8 rows in
-// flight), then q_k = sum_j s_k[j] w_k[j].  E (C^2 doubles) is re-read from L2
-// by every block: KB = 16 halves that traffic against KB = 8 (the kernel was
-// L2-bound), two waves per SIMD hide the load latency.  The threads' q_k and
-// means are summed in fixed order (wave shuffles, then the eight waves in order).
-template <int KB, int MAXJ>
-__global__ __launch_bounds__(512) void bn_from_gram_kernel(int K, int C, long count, const double* mu,
-                                                           const double* e2, const _Float16* w16,
-                                                           const float* w_inv_scale, const float* gamma,
-                                                           const float* beta, float momentum, float eps,
-                                                           float* rmean, float* rvar, int64_t* nbt, float* ss,
-                                                           float* mi) {
-    extern __shared__ double wsh[];                        // [C][KB]: row i's KB weights contiguous
-    __shared__ double red[8][KB][2];
-    const int k0 = blockIdx.x * KB;
+// with; exact in fp32: an fp16 value times a power of two).  Two launches:
+//   bn_from_gram_part_kernel  grid (K/16 channel groups) x (C/256 column blocks)
+//                             x (C/64 row groups): thread j of a block sums, for
+//                             its 16 channels, s_k = sum_{i in the 64 rows}
+//                             E[i][j] w_k[i] (coalesced rows of E, 8 in flight,
+//                             the next 8 loading while these are used; weight
+//                             rows / columns in LDS, read as broadcasts), and
+//                             the block sums q_k = sum_j s_k w_k[j] (and, in row
+//                             group 0, m_k = sum_j mu_j w_k[j]) over its 256
+//                             columns in fixed order (wave shuffles, then the 4
+//                             waves in order) → part[jb][rg][k]
+//   bn_from_gram_fin_kernel   per k: the partials in (jb, rg) order → mean, var
+//                             → bn_fin_store
+// (One block per 16 channels over all of E: a thread walked C rows in
+// dependent rounds of 8 loads with one wave per SIMD — latency-bound, 158 us
+// for R50's layer4; with the rows split over blocks the chip holds 8x the loads
+// in flight.)
+constexpr int BFG_KB = 16, BFG_JB = 256, BFG_RB = 64;
+
+__global__ __launch_bounds__(256) void bn_from_gram_part_kernel(int K, int C, const double* __restrict__ mu,
+                                                                const double* __restrict__ e2,
+                                                                const _Float16* __restrict__ w16,
+                                                                const float* __restrict__ w_inv_scale,
+                                                                double* __restrict__ part) {
+    constexpr int KB = BFG_KB, JB = BFG_JB, RB = BFG_RB;
+    __shared__ __attribute__((aligned(16))) double wr[RB][KB];   // weights of this block's rows i (fp64:
+                                                                 // no conversion in the FMA loop)
+    __shared__ float wc[JB][KB];                                 // weights of this block's columns j
+    __shared__ double red[4][KB][2];
+    const int k0 = blockIdx.x * KB, jb = blockIdx.y, rg = blockIdx.z;
+    const int i_base = rg * RB, j_base = jb * JB;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (int e = tid; e < KB * C; e += 512) {
-        const int i = e / KB, kk = e - i * KB;
-        const int k = k0 + kk;
-        wsh[e] = k < K ? (double)(float)w16[(long)k * C + i] * (double)w_inv_scale[k] : 0.0;
+    const int j = j_base + tid;
+    const bool valid = j < C;
+    // the first rows of E and every weight this block needs, all in flight at
+    // once (the kernel is latency-bound: a few dependent rounds in all)
+    constexpr int RR = 8;                                  // rows of E per round
+    double ev[RR], en[RR];
+#pragma unroll
+    for (int di = 0; di < RR; ++di) ev[di] = valid ? e2[(long)(i_base + di) * C + j] : 0.0;
+    {
+        float vr[KB], vc[KB], sc[KB];
+        const int i = i_base + (tid & (RB - 1));
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk) {                  // coalesced along each weight row
+            const int k = k0 + kk;
+            sc[kk] = k < K ? w_inv_scale[k] : 0.f;
+            vr[kk] = k < K ? (float)w16[(long)k * C + i] : 0.f;
+            vc[kk] = (k < K && valid) ? (float)w16[(long)k * C + j] : 0.f;
+        }
+#pragma unroll
+        for (int kk = 0; kk < KB; ++kk) {
+            if (tid < RB) wr[tid][kk] = (double)(vr[kk] * sc[kk]);
+            wc[tid][kk] = vc[kk] * sc[kk];
+        }
     }
     __syncthreads();
-    double s[MAXJ][KB];
+    double s[KB];
 #pragma unroll
-    for (int u = 0; u < MAXJ; ++u)
+    for (int kk = 0; kk < KB; ++kk) s[kk] = 0.0;
+#pragma unroll 1
+    for (int r0 = 0; r0 < RB; r0 += RR) {
+        if (r0 + RR < RB) {
 #pragma unroll
-        for (int kk = 0; kk < KB; ++kk) s[u][kk] = 0.0;
-    for (int i0 = 0; i0 < C; i0 += 8) {
-        double ev[8][MAXJ];
+            for (int di = 0; di < RR; ++di) en[di] = valid ? e2[(long)(i_base + r0 + RR + di) * C + j] : 0.0;
+        }
 #pragma unroll
-        for (int di = 0; di < 8; ++di)
+        for (int di = 0; di < RR; ++di) {
+            const double2* wi = (const double2*)&wr[r0 + di][0];
 #pragma unroll
-            for (int u = 0; u < MAXJ; ++u) {
-                const int j = tid + 512 * u;
-                ev[di][u] = j < C ? e2[(long)(i0 + di) * C + j] : 0.0;
-            }
-#pragma unroll
-        for (int di = 0; di < 8; ++di) {
-            const double* wi = wsh + (i0 + di) * KB;
-#pragma unroll
-            for (int kk = 0; kk < KB; ++kk) {
-                const double wv = wi[kk];
-#pragma unroll
-                for (int u = 0; u < MAXJ; ++u) s[u][kk] += ev[di][u] * wv;
+            for (int q2 = 0; q2 < KB / 2; ++q2) {
+                const double2 w2 = wi[q2];
+                s[2 * q2 + 0] += ev[di] * w2.x;
+                s[2 * q2 + 1] += ev[di] * w2.y;
             }
         }
-    }
-    double q[KB], m[KB];
+        if (r0 + RR < RB) {
 #pragma unroll
-    for (int kk = 0; kk < KB; ++kk) q[kk] = m[kk] = 0.0;
-#pragma unroll
-    for (int u = 0; u < MAXJ; ++u) {
-        const int j = tid + 512 * u;
-        if (j < C) {
-            const double muj = mu[j];
-#pragma unroll
-            for (int kk = 0; kk < KB; ++kk) {
-                const double wj = wsh[j * KB + kk];
-                q[kk] += s[u][kk] * wj;
-                m[kk] += muj * wj;
-            }
+            for (int di = 0; di < RR; ++di) ev[di] = en[di];
         }
     }
+    const double muj = valid && rg == 0 ? mu[j] : 0.0;
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
-        double v = q[kk], u = m[kk];
+        const double wj = valid ? (double)wc[tid][kk] : 0.0;
+        double v = s[kk] * wj, u = muj * wj;
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             v += __shfl_xor(v, o);
@@ -342,17 +373,33 @@ __global__ __launch_bounds__(512) void bn_from_gram_kernel(int K, int C, long co
     }
     __syncthreads();
     if (tid < KB && k0 + tid < K) {
-        double v = 0.0, mean = 0.0;
+        double v = 0.0, m = 0.0;
 #pragma unroll
-        for (int ww = 0; ww < 8; ++ww) {
+        for (int ww = 0; ww < 4; ++ww) {
             v += red[ww][tid][0];
-            mean += red[ww][tid][1];
+            m += red[ww][tid][1];
         }
-        double var = v - mean * mean;
-        var = var > 0.0 ? var : 0.0;
-        bn_fin_store(k0 + tid, K, count, mean, var * (double)count, gamma, beta, momentum, eps, rmean, rvar, nbt, ss,
-                     mi);
+        const long slot = (long)jb * gridDim.z + rg;
+        part[(slot * K + k0 + tid) * 2 + 0] = v;
+        part[(slot * K + k0 + tid) * 2 + 1] = m;
     }
+}
+
+__global__ __launch_bounds__(256) void bn_from_gram_fin_kernel(int K, int nslots, long count,
+                                                               const double* __restrict__ part, const float* gamma,
+                                                               const float* beta, float momentum, float eps,
+                                                               float* rmean, float* rvar, int64_t* nbt, float* ss,
+                                                               float* mi) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= K) return;
+    double v = 0.0, mean = 0.0;
+    for (int sl = 0; sl < nslots; ++sl) {
+        v += part[((long)sl * K + k) * 2 + 0];
+        mean += part[((long)sl * K + k) * 2 + 1];
+    }
+    double var = v - mean * mean;
+    var = var > 0.0 ? var : 0.0;
+    bn_fin_store(k, K, count, mean, var * (double)count, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
 }
 
 static int gram_tc(int c) { return c % 128 == 0 ? 128 : 64; }
@@ -405,34 +452,42 @@ extern "C" int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mea
     const dim3 grid((unsigned)(splits * tiles));
     if (tc == 128) hipLaunchKernelGGL(gram_f16_kernel<128>, grid, dim3(256), 0, st, g);
     else hipLaunchKernelGGL(gram_f16_kernel<64>, grid, dim3(256), 0, st, g);
-    const long nel = (long)tiles * tc * tc;
-    const long blocks = (nel + 255) / 256 + (c + 255) / 256;
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, c, tc, tiles, splits, (long)m,
-                       (const float*)g.part, (const float*)g.psum, mean, second);
+    const long nval = (long)tiles * tc * tc + c;          // second moments, then the means
+    if (splits >= 64)
+        hipLaunchKernelGGL(gram_reduce_kernel<4>, dim3((unsigned)((nval + 63) / 64)), dim3(256), 0, st, c, tc, tiles,
+                           splits, (long)m, (const float*)g.part, (const float*)g.psum, mean, second);
+    else
+        hipLaunchKernelGGL(gram_reduce_kernel<1>, dim3((unsigned)((nval + 255) / 256)), dim3(256), 0, st, c, tc,
+                           tiles, splits, (long)m, (const float*)g.part, (const float*)g.psum, mean, second);
     HKP_LAUNCH_CHECK("hkp_gram_f16");
     return HKP_OK;
+}
+
+static int bfg_slots(int c) { return ((c + BFG_JB - 1) / BFG_JB) * (c / BFG_RB); }
+
+extern "C" int64_t hkp_bn_from_gram_workspace_bytes(int32_t k, int32_t c) {
+    if (k <= 0 || c <= 0 || c % 64) return -1;
+    return (int64_t)bfg_slots(c) * k * 2 * (int64_t)sizeof(double);
 }
 
 extern "C" int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* second,
                                 const uint16_t* w_f16, const float* w_inv_scale, const float* gamma,
                                 const float* beta, float momentum, float eps, float* running_mean,
                                 float* running_var, int64_t* num_batches_tracked, float* scale_shift,
-                                float* mean_invstd, hkp_stream_t stream) {
-    HKP_CHECK_ARG(k > 0 && c > 0 && c <= 1024 && c % 64 == 0 && count > 0 && mean && second && w_f16 && w_inv_scale &&
-                      scale_shift,
+                                float* mean_invstd, void* workspace, int64_t ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(k > 0 && c > 0 && c <= 2048 && c % 64 == 0 && count > 0 && mean && second && w_f16 && w_inv_scale &&
+                      scale_shift && workspace,
                   "hkp_bn_from_gram: bad args");
+    HKP_CHECK_ARG(ws_bytes >= hkp_bn_from_gram_workspace_bytes(k, c), "hkp_bn_from_gram: workspace %lld < %lld",
+                  (long long)ws_bytes, (long long)hkp_bn_from_gram_workspace_bytes(k, c));
     hipStream_t st = as_stream(stream);
-    if (c <= 512) {
-        const size_t sh = (size_t)16 * c * sizeof(double);
-        hipLaunchKernelGGL((bn_from_gram_kernel<16, 1>), dim3((unsigned)((k + 15) / 16)), dim3(512), sh, st, k, c,
-                           (long)count, mean, second, (const _Float16*)w_f16, w_inv_scale, gamma, beta, momentum, eps,
-                           running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd);
-    } else {
-        const size_t sh = (size_t)8 * c * sizeof(double);
-        hipLaunchKernelGGL((bn_from_gram_kernel<8, 2>), dim3((unsigned)((k + 7) / 8)), dim3(512), sh, st, k, c,
-                           (long)count, mean, second, (const _Float16*)w_f16, w_inv_scale, gamma, beta, momentum, eps,
-                           running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd);
-    }
+    const int njb = (c + BFG_JB - 1) / BFG_JB, nrg = c / BFG_RB;
+    hipLaunchKernelGGL(bn_from_gram_part_kernel,
+                       dim3((unsigned)((k + BFG_KB - 1) / BFG_KB), (unsigned)njb, (unsigned)nrg), dim3(256), 0, st,
+                       k, c, mean, second, (const _Float16*)w_f16, w_inv_scale, (double*)workspace);
+    hipLaunchKernelGGL(bn_from_gram_fin_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st, k, njb * nrg,
+                       (long)count, (const double*)workspace, gamma, beta, momentum, eps, running_mean, running_var,
+                       num_batches_tracked, scale_shift, mean_invstd);
     HKP_LAUNCH_CHECK("hkp_bn_from_gram");
     return HKP_OK;
 }

@@ -84,7 +84,9 @@ SIGNATURES = {
     "hkp_conv2d_fwd_f16_bn": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _I64, _P]),
     "hkp_gram_f16_workspace_bytes": (_I64, [_I64, _I32]),
     "hkp_gram_f16": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I64, _P]),
-    "hkp_bn_from_gram": (ctypes.c_int, [_I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
+    "hkp_bn_from_gram_workspace_bytes": (_I64, [_I32, _I32]),
+    "hkp_bn_from_gram": (ctypes.c_int, [_I32, _I32, _I64, _P, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P,
+                                        _I64, _P]),
     "hkp_conv_kernel_name": (_I32, [_CD, _I32, _I32, ctypes.c_char_p, _I32]),
     "hkp_upsample_argmax_ws_bytes": (_I64, [_I32, _I32, _I32, _I32]),
     "hkp_stem_pack_x3_elems": (_I64, [_CD]),

@@ -323,11 +323,14 @@ def bn_from_gram(mean, second, wp, count, gamma, beta, running_mean=None, runnin
             _need(t, torch.float32, "bn_from_gram." + nm, 1)
             if t.numel() != k:
                 raise HkpError("bn_from_gram.%s: %d != K=%d" % (nm, t.numel(), k))
+    from ._lib import lib
     ss = torch.empty(2 * k, device=ws.device, dtype=torch.float32)
     mi = torch.empty(2 * k, device=ws.device, dtype=torch.float32)
+    nb = lib().hkp_bn_from_gram_workspace_bytes(k, c)
+    work = torch.empty((max(nb, 8) + 7) // 8, device=ws.device, dtype=torch.float64)
     call("hkp_bn_from_gram", k, c, int(count), _ptr(mean), _ptr(second), _ptr(ws), _ptr(wsc), _ptr(gamma), _ptr(beta),
          momentum, eps, _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi),
-         _stream())
+         _ptr(work), work.numel() * 8, _stream())
     return ss, mi
 
 

@@ -144,8 +144,8 @@ int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16, const uint
  * y is never written.  res_f16 [n*ho*wo][k] (nullable), res_scale_shift [2k]
  * (nullable: raw residual).  The scale/shift must be known before the conv:
  * eval-mode BN, or train-mode statistics from the input's second moments
- * (hkp_gram_f16 + hkp_bn_from_gram, 1x1 convs).  Not with the persistent tile
- * policies.  Stream-K workspace as hkp_conv2d_fwd_x3. */
+ * (hkp_gram_f16 + hkp_bn_from_gram, 1x1 convs).  Stream-K workspace as
+ * hkp_conv2d_fwd_x3. */
 int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
                           const float* w_inv_scale, const float* scale_shift, const uint16_t* res_f16,
                           const float* res_scale_shift, int32_t relu, uint16_t* out_f16, void* sk_workspace,
@@ -161,14 +161,17 @@ int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f16, const u
  * mean = w.mu and var = w^T E w - mean^2 (fp64), and writes hkp_bn_finalize's
  * outputs from them
  * (scale_shift, mean_invstd (nullable), running stats with the unbiased
- * variance, num_batches_tracked += 1).  c <= 1024 for hkp_bn_from_gram. */
+ * variance, num_batches_tracked += 1); workspace hkp_bn_from_gram_workspace_bytes(k,
+ * c) (per-column-block partial sums, merged in fixed order). */
 int64_t hkp_gram_f16_workspace_bytes(int64_t m, int32_t c);
 int hkp_gram_f16(int64_t m, int32_t c, const uint16_t* a, double* mean, double* second, void* workspace,
                  int64_t ws_bytes, hkp_stream_t stream);
+int64_t hkp_bn_from_gram_workspace_bytes(int32_t k, int32_t c);
 int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, const double* second,
                      const uint16_t* w_f16, const float* w_inv_scale, const float* gamma, const float* beta,
                      float momentum, float eps, float* running_mean, float* running_var,
-                     int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd, hkp_stream_t stream);
+                     int64_t* num_batches_tracked, float* scale_shift, float* mean_invstd, void* workspace,
+                     int64_t ws_bytes, hkp_stream_t stream);
 /* The kernel a launch with descriptor d runs — its template name as rocprofv3
  * reports it (e.g. "conv_x3_kernel<256, false, false, 16, false, 3>"), for
  * profiling / roofline attribution.  op: HKP_KOP_*; stream_k_ok: whether the
