@@ -1,9 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r03
-timeout -k 10 400 python -u -m pytest tests/test_gpu_gram.py tests/test_gpu_precision.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r03/pytest_bfg.log 2>&1 || { echo "pytest failed"; grep -E "Error|error|assert|FAILED" gpurun_out/r03/pytest_bfg.log | head -30; tail -5 gpurun_out/r03/pytest_bfg.log; exit 1; }
-tail -1 gpurun_out/r03/pytest_bfg.log
-C4="--backbone resnet50 --keypoints 8 --batch 128 --precision f16"
-timeout -k 10 300 python -u bench.py $C4 --no-extras --no-cpu-baseline > gpurun_out/r03/c4_bfg.log 2>&1 && tail -1 gpurun_out/r03/c4_bfg.log | cut -c1-200
-timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/r03/prof_c4_bfg -o run -- python3 bench.py $C4 --steps 5 --no-extras --no-cpu-baseline > gpurun_out/r03/prof_c4_bfg.log 2>&1
-echo done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_backward.py -m gpu -x -q -k "priority or deterministic or bucket" --timeout 200 --timeout-method thread > gpurun_out/r03/pytest_prio.log 2>&1 || { echo "pytest failed"; grep -E "Error|error|assert|FAILED" gpurun_out/r03/pytest_prio.log | head -30; tail -5 gpurun_out/r03/pytest_prio.log; exit 1; }
+tail -1 gpurun_out/r03/pytest_prio.log
+bash tools/ab.sh "--mode train" "" "--tune priority_stream=1"
