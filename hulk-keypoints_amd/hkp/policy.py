@@ -34,9 +34,6 @@ class Policy:
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
     wgrad_overlap_cus: int = 0
-    # training: run the step on a high-priority stream, so the critical path's
-    # blocks (forward, dgrad, BN) take CUs ahead of the side-stream wgrads
-    priority_stream: bool = False
     # inner BN ReLU masks recomputed from y in the backward (no fp32 activation kept)
     mask_from_y: bool = True
     # inference: last block's BN apply fused with the K-row head

@@ -167,21 +167,6 @@ class Trainer:
         return loss
 
     def step(self, x, uv=None, target=None):
-        if not (self.policy.priority_stream and x.is_cuda):
-            loss = self.forward_backward(x, uv, target)
-            self.opt.step()
-            return loss
-        # the whole step on a high-priority stream (Policy.priority_stream): the
-        # hardware queue arbiter then hands freed CUs to its blocks before the
-        # side stream's wgrads
-        cur = torch.cuda.current_stream(x.device)
-        if getattr(self, "_prio_stream", None) is None:
-            self._prio_stream = torch.cuda.Stream(x.device, priority=-100)
-        s = self._prio_stream
-        s.wait_stream(cur)
-        with torch.cuda.stream(s):
-            loss = self.forward_backward(x, uv, target)
-            self.opt.step()
-        cur.wait_stream(s)
-        loss.record_stream(cur)
+        loss = self.forward_backward(x, uv, target)
+        self.opt.step()
         return loss

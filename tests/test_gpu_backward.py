@@ -361,26 +361,6 @@ def test_backward_deterministic(cuda_device):
         assert torch.equal(a, b.grad)
 
 
-def test_priority_stream_step_equals_plain(cuda_device):
-    """Policy.priority_stream runs the step on a high-priority stream: the same
-    kernels in the same order, so the same loss and parameters, bit for bit."""
-    from hkp import train
-    from hkp.policy import DEFAULT
-    B, K, H, W = 2, 2, 64, 80
-    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 51)).to(cuda_device)
-    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 52)).to(cuda_device)
-    out = []
-    for prio in (False, True):
-        m = _model("resnet18", K, 53, cuda_device)
-        m.policy = DEFAULT.with_(priority_stream=prio)
-        t = train.Trainer(m)
-        losses = [t.step(x, uv=uv).item() for _ in range(2)]
-        out.append((losses, [p.detach().clone() for p in m.parameters()]))
-    assert out[0][0] == out[1][0]
-    for a, b in zip(out[0][1], out[1][1]):
-        assert torch.equal(a, b)
-
-
 def test_dp_bucket_path_equals_plain(cuda_device):
     """The DP gradient path (bucket copies on the stream each gradient is made on,
     one join per bucket; forced at world size 1) hands the optimizer exactly the
