@@ -1,4 +1,3 @@
 set -o pipefail
 export TMPDIR=/tmp
-C4="--backbone resnet50 --keypoints 8 --batch 128 --precision f16"
-bash tools/ab.sh "$C4" "" "--tune f16_tile_1x1=6" "--tune f16_tile_1x1=4" "--tune f16_tile_kxk=4"
+bash tools/ab.sh "--mode train" "" "--tune dgrad_overlap_tile=0" "--tune dgrad_overlap_tile=3" "--tune overlap_wgrad=0"
