@@ -49,6 +49,7 @@ typedef struct {
     int32_t fast_ac[1 << FAST];
     int32_t maxcode[18];           /* largest code of each length, -1: none */
     int32_t valoff[17];            /* HUFFVAL index = code + valoff[len] */
+    int32_t nval;
     uint8_t val[256];
 } htab;
 
@@ -102,6 +103,7 @@ static int build_htab(htab* t, const uint8_t* bits, const uint8_t* vals, int nva
     }
     t->maxcode[17] = 0x7FFFFFFF;
     memcpy(t->val, vals, (size_t)nvals);
+    t->nval = nvals;
     memset(t->look_len, 0, sizeof t->look_len);
     p = 0;
     for (int l = 1; l <= LOOK; ++l)
@@ -188,6 +190,8 @@ static int parse_headers(const uint8_t* data, int64_t size, parser* ps, hkpj_geo
                 g->ncomp = s[5];
                 if (g->width <= 0 || g->height <= 0)
                     return fail(HKPJ_ERR_UNSUPPORTED, "image size %dx%d (DNL not supported)", g->width, g->height);
+                if ((int64_t)g->width * g->height > (int64_t)1 << 26)
+                    return fail(HKPJ_ERR_UNSUPPORTED, "image size %dx%d (at most 64 Mpixel)", g->width, g->height);
                 if (g->ncomp != 1 && g->ncomp != 3)
                     return fail(HKPJ_ERR_UNSUPPORTED, "%d components (1 or 3 only)", g->ncomp);
                 if (len < 8 + 3 * g->ncomp) return fail(HKPJ_ERR_FORMAT, "SOF: truncated");
@@ -352,8 +356,10 @@ static inline int decode_sym(bitreader* br, const htab* t) {
         code = (int)peek(br, l);
     }
     if (l > 16) return -1;
+    const int idx = code + t->valoff[l];
+    if (idx < 0 || idx >= t->nval) return -1;              /* corrupt data: never index outside HUFFVAL */
     skip(br, l);
-    return t->val[code + t->valoff[l]];
+    return t->val[idx];
 }
 
 /* EXTEND (T.81 Figure F.12) */

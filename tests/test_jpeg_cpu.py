@@ -162,3 +162,33 @@ def test_device_batches_host_side_items(tmp_path):
     # two image sizes cannot form one batch, exactly as on the host-decode path
     with pytest.raises(ValueError):
         _collate_coef([view[0], view[3]])
+
+
+def test_corrupt_inputs_fail_cleanly():
+    """Seeded byte flips, truncations and header garbage: every call either
+    decodes or raises JpegError — never a crash or a read outside the buffer
+    (the entropy decoder parses untrusted files in the loader workers)."""
+    from hkp import jpeg
+    rng = np.random.default_rng(9)
+    bases = [_jpeg(_image(40, 56, 11), quality=80, subsampling=2),
+             _jpeg(_image(33, 47, 12), quality=60, subsampling=0, restart_marker_blocks=2),
+             _jpeg(_image(24, 24, 13, gray=True), quality=90, optimize=True)]
+    outcomes = {"ok": 0, "error": 0}
+    for i in range(600):
+        b = bytearray(bases[i % len(bases)])
+        kind = i % 3
+        if kind == 0:
+            for _ in range(int(rng.integers(1, 6))):
+                b[int(rng.integers(2, len(b)))] = int(rng.integers(0, 256))
+        elif kind == 1:
+            b = b[:int(rng.integers(4, len(b)))]
+        else:
+            j = int(rng.integers(2, min(len(b), 200)))
+            b[j:j + 8] = bytes(rng.integers(0, 256, 8).astype(np.uint8))
+        try:
+            coefs, qt, g = jpeg.entropy_decode(bytes(b))
+            assert coefs.shape == (g.nblocks, 64)
+            outcomes["ok"] += 1
+        except jpeg.JpegError:
+            outcomes["error"] += 1
+    assert outcomes["ok"] > 0 and outcomes["error"] > 0, outcomes
