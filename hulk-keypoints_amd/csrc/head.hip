@@ -191,6 +191,97 @@ __global__ __launch_bounds__(256) void bn_apply_head_kernel(long M, int hw, int 
     }
 }
 
+// Config C4's inference tail (y fp16): the same fp32 BN apply (+ residual, ReLU)
+// as bn_apply_head_kernel<true, …>, then the activation rounded to fp16 (the
+// dtype autocast gives the ReLU output) and the K-row head as
+// v_mfma_f32_16x16x32_f16 against the fp16-rounded head rows (autocast's 1x1
+// conv; fp32 accumulation).  The VALU form spent 16 of its ~22 lane operations
+// per channel on the K dot products and held ~180 VGPRs (two waves per SIMD):
+// at C = 2048 it read its 5 GB at 3.1 TB/s.  Here a wave scores 16 pixels: lane
+// l feeds pixel l & 15, channels 8 (l >> 4) .. +7 of each 32-channel step (A),
+// and head row l & 15 of the same channels (B, from LDS; zero rows k >= K); its
+// accumulator ends holding pixels 4 (l >> 4) + 0..3 of row l & 15.  The scale /
+// shift (and residual scale / shift) sit in LDS, broadcast to the 16 lanes of a
+// channel group; y and the residual are read once, non-temporally, 128 channels
+// (8 x 16 B per lane) in flight per wave; waves stride over 16-pixel groups.
+constexpr int HM_WAVES = 8;
+template <int RES, int KP>
+__global__ __launch_bounds__(64 * HM_WAVES, 2) void head_f16_mfma_kernel(long M, int hw, int C, int K,
+                                                                        const _Float16* __restrict__ y,
+                                                                        const float* __restrict__ ss,
+                                                                        const _Float16* __restrict__ res,
+                                                                        const float* __restrict__ rss,
+                                                                        const float* __restrict__ w,
+                                                                        const float* __restrict__ bias,
+                                                                        float* __restrict__ low) {
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    extern __shared__ __attribute__((aligned(16))) char hsm[];
+    constexpr int NSS = RES == 2 ? 4 : 2;
+    float* const cst = (float*)hsm;                       // [NSS][C]: scale, shift (, rscale, rshift)
+    h8* const wl = (h8*)(hsm + (long)NSS * C * 4);        // [C/8][KP]: channels 8q..8q+7 of head row k
+    const int tid = threadIdx.x;
+    for (int i = tid; i < C; i += 64 * HM_WAVES) {
+        cst[i] = ss[i];
+        cst[C + i] = ss[C + i];
+        if constexpr (RES == 2) {
+            cst[2 * C + i] = rss[i];
+            cst[3 * C + i] = rss[C + i];
+        }
+    }
+    for (int i = tid; i < (C / 8) * KP; i += 64 * HM_WAVES) {
+        const int q = i / KP, k = i - q * KP;
+        h8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = k < K ? (_Float16)w[(long)k * C + 8 * q + e] : (_Float16)0.f;
+        wl[i] = v;
+    }
+    __syncthreads();
+    const int lane = tid & 63, wv = tid >> 6;
+    const int r16 = lane & 15, g = lane >> 4;
+    const h8 zero8 = {};
+    const long groups = (M + 15) / 16;
+    for (long grp = (long)blockIdx.x * HM_WAVES + wv; grp < groups; grp += (long)gridDim.x * HM_WAVES) {
+        const long p = grp * 16 + r16;
+        const bool ok = p < M;
+        const long e0 = (ok ? p : 0) * C + 8 * g;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int c0 = 0; c0 < C; c0 += 128) {
+            h8 yv[4], rv[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                yv[t] = ok ? __builtin_nontemporal_load((const h8*)(y + e0 + c0 + 32 * t)) : zero8;
+                if constexpr (RES != 0) rv[t] = ok ? __builtin_nontemporal_load((const h8*)(res + e0 + c0 + 32 * t)) : zero8;
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int cb = c0 + 32 * t + 8 * g;
+                h8 o16;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    float o = __fadd_rn(__fmul_rn((float)yv[t][e], cst[cb + e]), cst[C + cb + e]);
+                    if constexpr (RES == 1) o = __fadd_rn(o, (float)rv[t][e]);
+                    else if constexpr (RES == 2)
+                        o = __fadd_rn(o, __fadd_rn(__fmul_rn((float)rv[t][e], cst[2 * C + cb + e]), cst[3 * C + cb + e]));
+                    o16[e] = (_Float16)(o > 0.f ? o : 0.f);
+                }
+                const h8 wb = r16 < KP ? wl[(cb >> 3) * KP + r16] : zero8;
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(o16, wb, acc, 0, 0, 0);
+            }
+        }
+        if (r16 < K) {
+            const float b = bias[r16];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const long pp = grp * 16 + 4 * g + i;
+                if (pp < M) {
+                    const long n = pp / hw, q = pp - n * hw;
+                    low[(n * K + r16) * hw + q] = __fadd_rn(acc[i], b);
+                }
+            }
+        }
+    }
+}
+
 struct Lerp {
     int i0, i1;
     float l0, l1;
@@ -374,6 +465,29 @@ extern "C" int hkp_bn_apply_head(int32_t n, int32_t hw, int32_t c, int32_t k, in
                       (res_kind == 2) == (res_scale_shift != nullptr) && !(res_kind == 3 && y_f16),
                   "hkp_bn_apply_head: bad residual (kind %d)", res_kind);
     const long M = (long)n * hw;
+    if (y_f16 && k <= 8) {                 // config C4: the MFMA head (LDS <= 64 KiB at c = 2048)
+        static const int cus = [] {
+            int dev = 0, v = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+                v = 256;
+            return v;
+        }();
+        const long groups = (M + 15) / 16;
+        long gb = (groups + HM_WAVES - 1) / HM_WAVES;
+        if (gb > 2L * cus) gb = 2L * cus;
+        const size_t lds = (size_t)(res_kind == 2 ? 4 : 2) * c * 4 + (size_t)(c / 8) * 8 * 16;
+        hipStream_t hst = as_stream(stream);
+#define HKP_HM(RES)                                                                                               \
+    hipLaunchKernelGGL((head_f16_mfma_kernel<RES, 8>), dim3((unsigned)gb), dim3(64 * HM_WAVES), lds, hst, M, hw, c, k, \
+                       (const _Float16*)y, scale_shift, (const _Float16*)res, res_scale_shift, w, bias, lowres)
+        if (res_kind == 0) HKP_HM(0);
+        else if (res_kind == 1) HKP_HM(1);
+        else HKP_HM(2);
+#undef HKP_HM
+        HKP_LAUNCH_CHECK("hkp_bn_apply_head(f16)");
+        return HKP_OK;
+    }
     const int gpb = 4 / (c / 512);
     long chunks = (M + HEAD_PB - 1) / HEAD_PB;
     long g = (chunks + gpb - 1) / gpb;

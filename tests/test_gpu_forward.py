@@ -170,6 +170,8 @@ HEAD_CASES = [
     (1, 3, 5, 1024, 8, "f32", 0),     # two waves per pixel, ragged M (15 pixels)
     (2, 5, 7, 2048, 8, "f16", 1),     # C4's last Bottleneck (fp16 residual stream)
     (1, 4, 9, 2048, 3, "f16", 2),     # K = 3 < KP
+    (1, 3, 11, 512, 8, "f16", 0),     # fp16, no residual, ragged 16-pixel group
+    (16, 60, 80, 512, 8, "f16", 1),   # fp16, more 16-pixel groups than the grid's waves
 ]
 
 
@@ -177,7 +179,10 @@ HEAD_CASES = [
 def test_bn_apply_head_fused(cuda_device, case):
     """hkp_bn_apply_head = the final block's BN apply (+ residual, ReLU) followed by
     the K-row head, against the same two steps in float64 (and the activation it
-    fuses is exactly hkp_bn_apply's / hkp_bn_apply_f16's)."""
+    fuses is exactly hkp_bn_apply's / hkp_bn_apply_f16's).  fp16 y (config C4,
+    K <= 8): the activation and the head rows enter the head as fp16, as under
+    autocast (MFMA head, fp32 accumulation) — the float64 reference rounds both
+    the same way."""
     from hkp import ops
     n, h, w, c, k, yt, kind = case
     dt = torch.float16 if yt == "f16" else torch.float32
@@ -204,7 +209,15 @@ def test_bn_apply_head_fused(cuda_device, case):
         r = res.double()
         o = o + (r * rss[:c].double() + rss[c:].double() if rss is not None else r)
     o = o.clamp_min(0)
-    ref = torch.einsum("nhwc,kc->nkhw", o, wk.double()) + bk.double()[None, :, None, None]
+    wr = wk.double()
+    if yt == "f16" and k <= 8:
+        # the kernel's fp32 apply (two roundings per op), then fp16: computed the
+        # same way here so no fp16 rounding tie breaks differently
+        o32 = y.float() * ss[:c] + ss[c:]
+        if res is not None:
+            o32 = o32 + (res.float() * rss[:c] + rss[c:] if rss is not None else res.float())
+        o, wr = o32.clamp_min(0).half().double(), wk.half().double()
+    ref = torch.einsum("nhwc,kc->nkhw", o, wr) + bk.double()[None, :, None, None]
     got = low.cpu().double()
     assert got.shape == ref.shape
     assert (got - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())

@@ -21,6 +21,8 @@ def main():
     con = sqlite3.connect(db)
     if "--timeline" in sys.argv:
         return timeline(con, steps)
+    if "--last-step" in sys.argv:
+        return last_step(con, match)
     rows = con.execute("select name, grid_x, grid_y, grid_z, workgroup_x, duration, stream_id from kernels "
                        "order by start").fetchall()
     per = len(rows) // steps
@@ -31,6 +33,30 @@ def main():
         if match in n:
             short = n.replace("void ", "").replace("hkp::", "").split("(")[0][:48]
             print("%-48s grid %7d x%4d x%3d wg %4d  s%d %8.1f us" % (short, gx // max(wx, 1), gy, gz, wx, s, d / 1e3))
+
+
+def _marker(rows):
+    if "--marker" in sys.argv:
+        return sys.argv[sys.argv.index("--marker") + 1]
+    return "heat_loss_kernel" if any("heat_loss_kernel" in r[0] for r in rows) else "argmax_decode_kernel"
+
+
+def last_step(con, match):
+    """Every launch of the last complete step (between the last two marker
+    launches), in launch order, with a running total."""
+    rows = con.execute("select name, grid_x, workgroup_x, end - start from kernels order by start").fetchall()
+    marker = _marker(rows)
+    idx = [i for i, r in enumerate(rows) if marker in r[0]]
+    if len(idx) < 2:
+        raise SystemExit("fewer than two %s launches" % marker)
+    last = rows[idx[-2] + 1:idx[-1] + 1]
+    tot, run = sum(r[3] for r in last), 0
+    print("launches/step %d, kernel time/step %.3f ms" % (len(last), tot / 1e6))
+    for n, gx, wx, d in last:
+        run += d
+        if match in n:
+            short = n.replace("void ", "").replace("hkp::", "").split("(")[0][:56]
+            print("%-56s grid %7d wg %4d %8.1f us  cum %7.3f ms" % (short, gx // max(wx, 1), wx, d / 1e3, run / 1e6))
 
 
 def timeline(con, steps):
