@@ -367,9 +367,81 @@ __device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int 
 // VEC(i, j): the f32x4 of accumulator rows ROW(i, 0..3) of column block j.
 // SC(j): the column's output scale (a power of two: sums scale by it, M2 by its
 // square, exactly) when VEC is the unscaled accumulator.
+//
+// WIDE (full 256-row tiles; scratch of 33 * BN floats that is free once every
+// wave is past its last fragment read, e.g. the drained ring): the lanes' (sum,
+// M2) go to LDS as they are, and one thread per (128-row half, column) merges
+// the four row groups of each wave and then the half's two waves — the order
+// and the formulas of the shuffle tree below (equal counts: Chan's factor is
+// the constant n/2, the 1/n scalings powers of two), so the partials are the
+// same bits, without its 34 dependent lane shuffles and per-merge divisions.
+__device__ __forceinline__ void x3_chan_merge(float& s, float& q, float s2, float q2, float inv_n, float f) {
+    const float d = s2 * inv_n - s * inv_n;
+    s = s + s2;
+    q = (q + q2) + d * d * f;
+}
+
 template <int BN, int NI, int NJ, int CW, int SHF, typename Vec, typename Row, typename Sc>
 __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, int m0, int n0, int wm, int wn,
-                                                 int lane, Vec&& vec, Row&& row, Sc&& sc_of) {
+                                                 int lane, Vec&& vec, Row&& row, Sc&& sc_of,
+                                                 float* wide = nullptr) {
+    if constexpr (CW == 16 && SHF == 16 && NI == 4) {
+        if (wide != nullptr && m0 + 256 <= a.M) {                    // block-uniform
+            const int q = lane >> 4, r16 = lane & 15;
+            constexpr float inv = 1.f / (NI * 4);
+            float ls[NJ], lq[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                f32x4 s4 = vec(0, j);
+#pragma unroll
+                for (int i = 1; i < NI; ++i) s4 += vec(i, j);
+                const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                const f32x4 mu = {s * inv, s * inv, s * inv, s * inv};
+                f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < NI; ++i) {
+                    const f32x4 d = vec(i, j) - mu;
+                    q4 += d * d;
+                }
+                ls[j] = s;
+                lq[j] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+            }
+            lds_sync();                                              // the scratch is free
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int c = wn * NJ * CW + j * CW + r16;
+                wide[(wm * 4 + q) * BN + c] = ls[j];
+                wide[16 * BN + (wm * 4 + q) * BN + c] = lq[j];
+                if (wm == 0 && q == 0) wide[32 * BN + c] = sc_of(j);
+            }
+            lds_sync();
+            for (int t = threadIdx.x; t < 2 * BN; t += blockDim.x) {
+                const int h = t / BN, c = t - h * BN;
+                float S[2], Q[2];
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    const int w4 = (2 * h + v) * 4;
+                    float s[4], qq[4];
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        s[g] = wide[(w4 + g) * BN + c];
+                        qq[g] = wide[16 * BN + (w4 + g) * BN + c];
+                    }
+                    x3_chan_merge(s[0], qq[0], s[1], qq[1], 1.f / 16, 8.f);     // lane pairs l, l ^ 16
+                    x3_chan_merge(s[2], qq[2], s[3], qq[3], 1.f / 16, 8.f);
+                    x3_chan_merge(s[0], qq[0], s[2], qq[2], 1.f / 32, 16.f);    // then l, l ^ 32
+                    S[v] = s[0];
+                    Q[v] = qq[0];
+                }
+                x3_chan_merge(S[0], Q[0], S[1], Q[1], 1.f / 64, 32.f);          // even wave, odd wave
+                const float sc = wide[32 * BN + c];
+                const long tile128 = (long)(m0 >> 7) + h;
+                a.part[(tile128 * a.K + n0 + c) * 2 + 0] = S[0] * sc;
+                a.part[(tile128 * a.K + n0 + c) * 2 + 1] = Q[0] * (sc * sc);
+            }
+            return;
+        }
+    }
     float* rs = red;                                                 // [WM][BN] wave sums
     float* rq = red + 4 * BN;                                        // [WM][BN] wave M2
     const int nw = min(64, max(0, a.M - (m0 + 64 * wm)));          // valid rows of this wave (a prefix)
@@ -758,7 +830,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             if constexpr (PAIRB) lds_sync();           // the scratch is the ring
             x3_bn_partials_w<BN, UM, UN, 16, 16>(
                 a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-                [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
+                [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
         }
         const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
         X3Res<BN> eres;
@@ -793,7 +865,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         if constexpr (PAIRB) lds_sync();               // the scratch is the ring
         x3_bn_partials_w<BN, UM, UN, 16, 16>(
             a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
+            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
     }
     x3_stamp(a, 3);
     {
@@ -1363,7 +1435,7 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
     if (a.part) {
         x3_bn_partials_w<BN, UM, UN, 16, 16>(
             a, (float*)smem, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; });
+            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; }, (float*)smem);
         lds_sync();
     }
     auto out_pix = [&](int row) { return ((long)img * a.Ho + h0 + (row >> 5)) * a.Wo + w0 + (row & 31); };

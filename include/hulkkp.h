@@ -287,7 +287,10 @@ int hkp_head_fc(int32_t n, int32_t hw, int32_t c, int32_t k, const float* feat, 
  * y [n*hw][c] fp32 (y_f16 = 0) or fp16 (y_f16 = 1); res_kind 0: none, 1: raw
  * residual of y's dtype, 2: residual * rscale + rshift (res_scale_shift [2c]),
  * 3: packed split raw residual (fp32 y only); w [k][c], bias [k] →
- * lowres [n][k][hw].  Needs c % 512 == 0, c <= 2048, k <= 16. */
+ * lowres [n][k][hw].  Needs c % 512 == 0, c <= 2048, k <= 16.  fp16 y with
+ * k <= 8 (config C4): the fp32 apply's result enters the head rounded to fp16,
+ * against fp16-rounded head rows, fp32 accumulation (autocast's ReLU output and
+ * 1x1 conv; MFMA). */
 int hkp_bn_apply_head(int32_t n, int32_t hw, int32_t c, int32_t k, int32_t y_f16, const void* y,
                       const float* scale_shift, const void* res, const float* res_scale_shift, int32_t res_kind,
                       const float* w, const float* bias, float* lowres, hkp_stream_t stream);

@@ -35,6 +35,9 @@ SHAPES = {
     "c4_l3_c3": ("f16", 128, 60, 80, 256, 1024, 1, 1, 0, 1),
     "c4_l1_c3": ("f16", 128, 120, 160, 64, 256, 1, 1, 0, 1),
     "c4_l1_c2": ("f16", 128, 120, 160, 64, 64, 3, 1, 1, 1),
+    "c4_l1_c1": ("f16", 128, 120, 160, 256, 64, 1, 1, 0, 1),
+    "c4_l1_c1a": ("f16", 128, 120, 160, 64, 64, 1, 1, 0, 1),
+    "c4_l2_c1a": ("f16", 128, 120, 160, 256, 128, 1, 1, 0, 1),
     "c4_l2_c2": ("f16", 128, 60, 80, 128, 128, 3, 1, 1, 1),
     "c4_l2_c1": ("f16", 128, 60, 80, 512, 128, 1, 1, 0, 1),
 }
