@@ -426,7 +426,10 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
         roof["frac_of_roofline"] = t_att / t_meas
         roof["hbm_bound_share_of_attainable"] = t_hbm / t_att if t_att > 0 else 0.0
     tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
-    if (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3":
+    c4 = (args.backbone, K, H, W) == ("resnet50", 8, 480, 640) and precision == "f16" and mode == "infer"
+    if c4:
+        tag = "infer_c4"
+    if ((args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3") or c4:
         (roof["traffic"], roof["traffic_source"], roof["pmc_pass_avg_ms"],
          roof["folded_kernel"]) = pmc_traffic(dom_sym, tag)
         # the kernel trace of the bench command itself (not the serialised PMC pass)

@@ -30,3 +30,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_infer -o run -- py
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_train -o run -- python3 bench.py --mode train --steps 10 --no-cpu-baseline > $O/prof_train.log 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_c4 -o run -- python3 bench.py $C4 --steps 5 --no-extras --no-cpu-baseline > $O/prof_c4.log 2>&1
 echo "kernel trace ok"
+# per-kernel stats CSV + top list + step timeline of each trace (the files profiles/ keeps)
+for L in infer train c4; do
+    DB=$O/prof_$L/run_results.db
+    [ -f $DB ] || DB=$(ls $O/prof_$L/*/run_results.db 2>/dev/null | head -1)
+    python3 tools/rocpd_stats.py $DB $O/${L}_kernel_stats.csv --top 25 > $O/${L}_kernel_top.txt
+    python3 tools/step_breakdown.py $DB --timeline > $O/${L}_timeline.txt
+    python3 tools/step_breakdown.py $DB --last-step > $O/${L}_last_step.txt
+done
+rm -rf $O/prof_infer $O/prof_train $O/prof_c4
+echo "stats ok"
