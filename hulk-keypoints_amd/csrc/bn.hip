@@ -357,22 +357,26 @@ __global__ __launch_bounds__(256) void bn_apply_f16_kernel(long n8, int C8, cons
     }
 }
 
-// maxpool 3x3 / s2 / p1 (-inf padding) of relu(y*a+b); one thread per 4 channels of one output pixel
+// maxpool 3x3 / s2 / p1 (-inf padding) of relu(y*a+b); one thread per 4 channels of one output pixel.
+// IDX: the index type of the (pixel, channel-group) decomposition — 32-bit when
+// the output and input element counts fit (the stem maps: 64-bit divisions were
+// ~4 per element group)
+template <typename IDX>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int W, int C, int Ho, int Wo,
                                                              const float* __restrict__ y,
                                                              const float* __restrict__ ss,
                                                              float* __restrict__ out, _Float16* __restrict__ osplit,
                                                              int passes, uchar4* __restrict__ route) {
-    const int C4 = C >> 2;
-    const long total = (long)N * Ho * Wo * C4;
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const IDX C4 = (IDX)(C >> 2);
+    const IDX total = (IDX)N * (IDX)Ho * (IDX)Wo * C4;
+    const IDX stride = (IDX)gridDim.x * (IDX)blockDim.x;
+    for (IDX i = (IDX)blockIdx.x * (IDX)blockDim.x + (IDX)threadIdx.x; i < total; i += stride) {
         const int c4 = (int)(i % C4);
-        long p = i / C4;
-        const int wo = (int)(p % Wo);
-        p /= Wo;
-        const int ho = (int)(p % Ho);
-        const int n = (int)(p / Ho);
+        IDX p = i / C4;
+        const int wo = (int)(p % (IDX)Wo);
+        p /= (IDX)Wo;
+        const int ho = (int)(p % (IDX)Ho);
+        const int n = (int)(p / (IDX)Ho);
         const f32x4 a = *(const f32x4*)(ss + 4 * c4), b = *(const f32x4*)(ss + C + 4 * c4);
         f32x4 m = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
         int tap[4] = {0, 0, 0, 0};
@@ -396,8 +400,8 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(int N, int H, int 
                 }
             }
         }
-        if (out) *(f32x4*)(out + i * 4) = m;
-        if (osplit) store_split4(m, i, osplit, passes);
+        if (out) *(f32x4*)(out + (long)i * 4) = m;
+        if (osplit) store_split4(m, (long)i, osplit, passes);
         if (route)   // the tap the window's gradient goes to; 0xFF: max <= 0, ReLU blocks it
             route[i] = make_uchar4(m[0] > 0.f ? tap[0] : 255, m[1] > 0.f ? tap[1] : 255,
                                    m[2] > 0.f ? tap[2] : 255, m[3] > 0.f ? tap[3] : 255);
@@ -576,8 +580,13 @@ extern "C" int hkp_bn_relu_maxpool(int32_t n, int32_t h, int32_t w, int32_t c, c
                   "hkp_bn_relu_maxpool: split output needs split_passes 1|3 and c%%32==0");
     const int ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
     const long work = (long)n * ho * wo * (c / 4);
-    hipLaunchKernelGGL(bn_relu_maxpool_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n, h, w, c,
-                       ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes, (uchar4*)route);
+    const bool idx32 = work * 4 < (1L << 31) && (long)n * h * w * c < (1L << 31);
+    if (idx32)
+        hipLaunchKernelGGL(bn_relu_maxpool_kernel<unsigned>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n,
+                           h, w, c, ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes, (uchar4*)route);
+    else
+        hipLaunchKernelGGL(bn_relu_maxpool_kernel<long>, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), n, h,
+                           w, c, ho, wo, y, scale_shift, out, (_Float16*)out_split, split_passes, (uchar4*)route);
     HKP_LAUNCH_CHECK("hkp_bn_relu_maxpool");
     return HKP_OK;
 }
