@@ -294,6 +294,37 @@ __global__ __launch_bounds__(256) void gram_reduce_kernel(int C, int TC, int til
 // in flight.)
 constexpr int BFG_KB = 16, BFG_JB = 256, BFG_RB = 64;
 
+// Sum of v[0..KP) over a wave's 64 lanes, reduce-scatter form: at offsets 32,
+// 16, ... each lane keeps half of its values plus its partner's copy of that
+// half until one is left, then the remaining offsets fold it — KP-1 +
+// log2(64/KP) fp64 shuffles instead of 6 per value.  Fixed order.
+template <int KP>
+__device__ __forceinline__ double bfg_reduce_scatter(double (&v)[KP], int lane) {
+    int o = 32;
+#pragma unroll
+    for (int n = KP; n > 1; n >>= 1, o >>= 1) {
+        const int half = n >> 1;
+        const bool upper = (lane & o) != 0;
+#pragma unroll
+        for (int i = 0; i < half; ++i) {
+            const double send = upper ? v[i] : v[half + i];
+            const double keep = upper ? v[half + i] : v[i];
+            v[i] = keep + __shfl_xor(send, o);
+        }
+    }
+    double s = v[0];
+#pragma unroll
+    for (; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    return s;
+}
+template <int KP>
+__device__ __forceinline__ int bfg_rs_k(int lane) {
+    int k = 0, o = 32;
+#pragma unroll
+    for (int n = KP; n > 1; n >>= 1, o >>= 1) k += (lane & o) ? (n >> 1) : 0;
+    return k;
+}
+
 __global__ __launch_bounds__(256) void bn_from_gram_part_kernel(int K, int C, const double* __restrict__ mu,
                                                                 const double* __restrict__ e2,
                                                                 const _Float16* __restrict__ w16,
@@ -357,19 +388,22 @@ __global__ __launch_bounds__(256) void bn_from_gram_part_kernel(int K, int C, co
         }
     }
     const double muj = valid && rg == 0 ? mu[j] : 0.0;
+    double v[KB], u[KB];
 #pragma unroll
     for (int kk = 0; kk < KB; ++kk) {
         const double wj = valid ? (double)wc[tid][kk] : 0.0;
-        double v = s[kk] * wj, u = muj * wj;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            v += __shfl_xor(v, o);
-            u += __shfl_xor(u, o);
-        }
-        if (lane == 0) {
-            red[w][kk][0] = v;
-            red[w][kk][1] = u;
-        }
+        v[kk] = s[kk] * wj;
+        u[kk] = muj * wj;
+    }
+    // the wave's 64 lanes summed for all KB channels at once (reduce-scatter:
+    // 17 shuffles instead of 6 per channel, in a fixed order); lane l holds the
+    // total of channel bfg_rs_k(l)
+    const double vs = bfg_reduce_scatter<KB>(v, lane);
+    const double us = rg == 0 ? bfg_reduce_scatter<KB>(u, lane) : 0.0;     // the mean term: row group 0 only
+    if ((lane & (64 / KB - 1)) == 0) {
+        const int kk = bfg_rs_k<KB>(lane);
+        red[w][kk][0] = vs;
+        red[w][kk][1] = us;
     }
     __syncthreads();
     if (tid < KB && k0 + tid < K) {
