@@ -314,6 +314,23 @@ def cpu_baseline(args, budget_s):
             "legs": legs}
 
 
+def workload_name(mode, backbone, k, h, w, precision, batch):
+    """The BASELINE.json config a bench line measures (C2..C5; C3/C5 per-GPU shards of
+    their DP jobs), or "custom" with its shape."""
+    shape = (mode, backbone, k, w, h)
+    if shape == ("infer", "resnet34", 4, 640, 480) and batch == 32 and precision != "f16":
+        return "C2 inference"
+    if shape == ("train", "resnet34", 4, 640, 480) and batch == 8:
+        return "C3 shard (batch 64 over 8 GPUs) training step"
+    if shape == ("infer", "resnet50", 8, 640, 480) and batch == 128 and precision == "f16":
+        return "C4 fp16 inference"
+    if shape == ("train", "resnet50", 8, 1280, 960) and batch == 32:
+        return "C5 shard (batch 256 over 8 GPUs) training step"
+    if shape == ("train", "resnet18", 2, 320, 240) and batch == 4:
+        return "C1 training step"
+    return "custom %s" % ("inference" if mode == "infer" else "training step")
+
+
 def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     """Time `steps` steps of one workload; return its metrics (rank 0 gets them)."""
     import hkp
@@ -434,6 +451,13 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
          roof["folded_kernel"]) = pmc_traffic(dom_sym, tag)
         # the kernel trace of the bench command itself (not the serialised PMC pass)
         roof["rocprof_avg_ms"], roof["rocprof_source"] = trace_avg_ms(dom_sym, tag)
+    if roof["conv_share_of_step"] > 1.0:
+        # training: the event pairs of the side-stream wgrads bracket time in which
+        # the main stream's dgrad shares the CUs, so the conv events add up to more
+        # than the step and `frac` prices shared CU time as exclusive
+        roof["timing"] = "overlapped (side-stream wgrad events share CUs with the main stream)"
+        if roof.get("rocprof_avg_ms"):
+            roof["frac_from_trace"] = (fl / cnt) * passes / (roof["rocprof_avg_ms"] * 1e-3) / 1e12 / peak
     return {"value": value, "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
             "batch_per_gpu": B, "global_batch": B * world, "roofline": roof,
             "model_tflops": value / world * fl_img * (3 if mode == "train" else 1) / 1e12,
@@ -494,10 +518,10 @@ def main():
         "value": main_leg["value"], "unit": "images/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": main_leg["ms_per_step"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": dtype, "data": "synthetic (seeded uint8 BGR images; random-init weights)",
-        "config": {"workload": "%s %s-8s K=%d %dx%d batch %d/GPU (%s)" % (
-            "inference (C2)" if args.mode == "infer" else "training step (C3 shard)", args.backbone,
-            args.keypoints, args.width, args.height, B,
-            "train-mode BN, fused K-ch head, heatmap + argmax, keypoints all-gathered at N>1"
+        "config": {"workload": "%s: %s-8s K=%d %dx%d %s batch %d/GPU (%s)" % (
+            workload_name(args.mode, args.backbone, args.keypoints, args.height, args.width, precision, B),
+            args.backbone, args.keypoints, args.width, args.height, precision,
+            B, "train-mode BN, fused K-ch head, heatmap + argmax, keypoints all-gathered at N>1"
             if args.mode == "infer" else "BCE fp64, Adam lr1e-4 wd1e-4"),
             "mode": args.mode, "backbone": args.backbone, "keypoints": args.keypoints, "height": args.height,
             "width": args.width, "batch_per_gpu": B, "global_batch": B * world, "parallelism": "dp%d" % world,

@@ -222,6 +222,7 @@ static int parse_headers(const uint8_t* data, int64_t size, parser* ps, hkpj_geo
                 break;
             case 0xDA: {                                   /* SOS */
                 if (!ps->sof) return fail(HKPJ_ERR_FORMAT, "SOS before SOF");
+                if (len < 6 + 2 * g->ncomp) return fail(HKPJ_ERR_FORMAT, "SOS: truncated");
                 const int ns = s[0];
                 if (ns != g->ncomp)
                     return fail(HKPJ_ERR_UNSUPPORTED, "scan of %d of %d components (one interleaved scan only)", ns,

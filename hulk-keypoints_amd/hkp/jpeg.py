@@ -70,7 +70,7 @@ def host_lib():
     global _host
     if _host is None:
         if not os.path.exists(HOST_LIB_PATH):
-            raise JpegError("libhkpjpeg.so is not built (%s); run __graft_entry__.build()" % HOST_LIB_PATH)
+            raise RuntimeError("libhkpjpeg.so is not built (%s); run __graft_entry__.build()" % HOST_LIB_PATH)
         L = ctypes.CDLL(HOST_LIB_PATH)
         for name, (res, args) in HOST_SIGNATURES.items():
             fn = getattr(L, name)

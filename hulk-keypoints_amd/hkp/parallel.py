@@ -66,15 +66,48 @@ def gather_keypoints_fixed(yx, out=None, group=None):
     return out
 
 
+_HOST_GROUPS = {}
+
+
+def _ranks(group):
+    return list(range(dist.get_world_size())) if group is None else list(dist.get_process_group_ranks(group))
+
+
+def host_group(group=None):
+    """A gloo group over the ranks of `group` (the group itself when it is gloo),
+    created once per rank set and cached.  Host-side checks (check_shards) run on
+    it so they never wait for the GPU queue: an RCCL collective followed by
+    .item() would block the host until every kernel queued before it had run.
+    Like dist.new_group, the first call for a rank set is collective over the
+    default group."""
+    if dist.get_backend(group) == "gloo":
+        return group
+    key = tuple(_ranks(group))
+    if key not in _HOST_GROUPS:
+        _HOST_GROUPS[key] = dist.new_group(list(key), backend="gloo")
+    return _HOST_GROUPS[key]
+
+
+def new_group_like(group=None):
+    """A separate communicator over the same ranks and backend as `group`.
+    Trainer(sync_bn=True) runs the SyncBN statistics gathers on one: RCCL runs the
+    collectives of one communicator in issue order, so on the gradient buckets'
+    communicator every backward BN gather would queue behind the in-flight 32 MB
+    bucket all-reduce and put it back on the critical path.  Collective over the
+    default group (dist.new_group)."""
+    return dist.new_group(_ranks(group), backend=dist.get_backend(group))
+
+
 def check_shards(n_local, group=None):
     """Every rank holds at least one image (min over ranks, one tiny collective).
     A SyncBN forward or backward with an empty shard would leave the other ranks
-    waiting in their statistics gathers forever, so every rank raises instead."""
+    waiting in their statistics gathers forever, so every rank raises instead.
+    The min runs on a gloo group over host memory (host_group): no GPU sync, so
+    the host keeps queuing the step's kernels ahead of the GPU."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
-    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
-    t = torch.tensor([int(n_local)], device=dev, dtype=torch.int64)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    t = torch.tensor([int(n_local)], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group(group))
     if int(t.item()) < 1:
         raise ValueError("SyncBN needs at least one image on every rank (global batch < world size %d)"
                          % dist.get_world_size(group))

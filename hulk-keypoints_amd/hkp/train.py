@@ -32,6 +32,10 @@ class GradBucketer:
     def __init__(self, params, bucket_bytes=32 << 20, group=None, last_bucket_bytes=None):
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        # RCCL averages inside the all-reduce (ReduceOp.AVG); gloo has no AVG, so
+        # there the sum is scaled by 1/world after the wait
+        self.avg_in_collective = self.world > 1 and dist.get_backend(group) == "nccl"
+        self.op = dist.ReduceOp.AVG if self.avg_in_collective else dist.ReduceOp.SUM
         # backward produces grads roughly in reverse parameter order; buckets are cut
         # from the END of that order (the stem side), the first of them (the last
         # to fill, its all-reduce exposed after backward) capped at
@@ -83,8 +87,7 @@ class GradBucketer:
                 if s is not None and s != cur:
                     cur.wait_stream(s)
             if self.world > 1:
-                self.works[bi] = dist.all_reduce(self.flat[bi], op=dist.ReduceOp.SUM, group=self.group,
-                                                 async_op=True)
+                self.works[bi] = dist.all_reduce(self.flat[bi], op=self.op, group=self.group, async_op=True)
 
     def finish(self):
         """Wait for every bucket; average; point p.grad at the flat buffers."""
@@ -97,7 +100,7 @@ class GradBucketer:
                 for s in self.streams[bi]:
                     if s is not None and s != torch.cuda.current_stream(s.device):
                         torch.cuda.current_stream(s.device).wait_stream(s)
-            if self.world > 1:
+            if self.world > 1 and not self.avg_in_collective:
                 self.flat[bi].mul_(1.0 / self.world)
         for p, (bi, off) in self.slot.items():
             p.grad = self.flat[bi][off:off + p.numel()].view_as(p)
@@ -135,8 +138,13 @@ class Trainer:
         size 1, to time its overhead on one GPU."""
         self.model = model
         self.group = group
-        self.policy = model.policy.with_(sync_bn=True, sync_group=group) if sync_bn else model.policy
         self.sync_bn = sync_bn
+        # SyncBN gathers on their own communicator over the same ranks (RCCL orders
+        # the collectives of one communicator by issue, so the 33 + 33 per-step R34
+        # BN gathers would otherwise wait behind in-flight gradient buckets)
+        self.bn_group = parallel.new_group_like(group) \
+            if sync_bn and dist.is_initialized() and dist.get_world_size(group) > 1 else group
+        self.policy = model.policy.with_(sync_bn=True, sync_group=self.bn_group) if sync_bn else model.policy
         self.params = list(model.parameters())
         self.loss_kind = loss
         self.sigma = sigma

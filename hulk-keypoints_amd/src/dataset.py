@@ -159,7 +159,12 @@ class _CoefView(Dataset):
         try:
             with open(path, "rb") as f:
                 coefs, qt, g = jpeg.entropy_decode(f.read())
-        except jpeg.JpegUnsupported:
+        except jpeg.JpegError:
+            # outside the decoder's subset (JpegUnsupported) or damaged (a missing
+            # RST marker, a bad Huffman code): the host decode, which like
+            # cv2.imread (dataset.py:71) resyncs / zero-fills and still returns an
+            # image, takes this file
+            jpeg.host_lib()                  # ... but a missing library is a setup error, not a file's
             return ("img", imread_bgr(path), self.labels[i], path)
         return ("coef", (coefs, qt, bytes(g)), self.labels[i], path)
 

@@ -262,7 +262,12 @@ def bce_cases():
     print("bce", L.item())
 
 
-def train_case(name, backbone, k, B, H, W, wseed, iseed, kseed, steps=2):
+def train_case(name, backbone, k, B, H, W, wseed, iseed, kseed, steps=2, store_images=True, fp64_step0=False):
+    """`steps` reference train steps (train.py:33-36) on one batch.  store_images=False
+    keeps the images' digest instead (tests regenerate them); fp64_step0 adds the
+    same steps run in float64 (same weights, images, target) so a test can take its
+    tolerance from the problem's measured conditioning (|fp32 - fp64| of the reference
+    itself) rather than from a guess."""
     imgs = recipe.seeded_images_u8(B, H, W, iseed)
     x = recipe.to_tensor_nchw(imgs)
     uv = recipe.seeded_keypoints(B, k, H, W, kseed)
@@ -273,7 +278,27 @@ def train_case(name, backbone, k, B, H, W, wseed, iseed, kseed, steps=2):
                       for b in range(B)])
     names = [n for n, _ in m.named_parameters()]
     out = dict(backbone=np.array(backbone), k=np.int32(k), wseed=np.int32(wseed), iseed=np.int32(iseed),
-               images_u8=imgs, uv=uv, steps=np.int32(steps))
+               uv=uv, steps=np.int32(steps))
+    if store_images:
+        out["images_u8"] = imgs
+    else:
+        out.update(images_sha256=image_digest(imgs), batch=np.int32(B), height=np.int32(H), width=np.int32(W))
+    if fp64_step0:
+        md = build(backbone, k, wseed).double()
+        optd = torch.optim.Adam(md.parameters(), lr=1.0e-4, weight_decay=1.0e-4)
+        for s in range(steps):
+            optd.zero_grad()
+            loss = nn.BCELoss()(md.forward(x.double()), gt)
+            loss.backward()
+            out["f64_loss%d" % s] = np.float64(loss.item())
+            if s == 0:
+                gd = {n: p.grad.detach().clone() for n, p in md.named_parameters()}
+                out["f64_grad_abs0"] = np.array([float(gd[n].abs().sum()) for n in names])
+                out["f64_fc_grad_rows0"] = gd["resnet.%s_8s.fc.weight" % backbone][:k].reshape(k, -1).numpy()
+                out["f64_stem_grad0"] = gd["resnet.%s_8s.conv1.weight" % backbone].numpy()
+            optd.step()
+        sdd = md.state_dict()
+        out["f64_param_abs"] = np.array([float(sdd[n].abs().sum()) for n in names])
     for s in range(steps):
         opt.zero_grad()                                       # train.py:33
         pred = m.forward(x).double()                          # train.py:21
@@ -328,3 +353,7 @@ if __name__ == "__main__":
                  ("train_r50_k8_96x128", "resnet50", 8, 2, 96, 128, 8, 18, 28)]:
         if want(args[0]):
             train_case(*args[:6], wseed=args[6], iseed=args[7], kseed=args[8])
+    if want("train_r18_k2_240x320_b4"):
+        # BASELINE config C1 at its own size: R18-8s, K=2, 320x240, batch 4, two Adam steps
+        train_case("train_r18_k2_240x320_b4", "resnet18", 2, 4, 240, 320, wseed=40, iseed=41, kseed=42,
+                   store_images=False, fp64_step0=True)

@@ -208,10 +208,13 @@ def check_conv_wgrad(x, dy, dw_krsc, st, pd, dl, gen, stats, ns=48):
     _check("wgrad", got, torch.stack(ref), torch.stack(tol) + 1e-30, stats)
 
 
-def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, chunk=1 << 16):
+def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, chunk=1 << 16, local=True):
     """Train-mode BN(+ReLU) backward: dgamma / dbeta against full fp64 channel
     reductions (row chunks) and dy on sampled elements; also the forward batch
-    statistics (mean, invstd) the forward stored."""
+    statistics (mean, invstd) the forward stored.  local=False (SyncBN): the
+    statistics and the dx coefficients come from every rank's shard, so only
+    dgamma / dbeta — this rank's own sums with the statistics the kernels used —
+    are checked here."""
     c = y.shape[-1]
     y2, g2 = y.reshape(-1, c), g.reshape(-1, c)
     M = y2.shape[0]
@@ -223,8 +226,9 @@ def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, c
     for r0 in range(0, M, chunk):
         var += ((y2[r0:r0 + chunk].double() - mean) ** 2).sum(0)
     inv = 1.0 / torch.sqrt(var / M + bn.eps)
-    _check("bn_mean", mi[:c].double(), mean, 1e-5 * torch.sqrt(var / M) + 1e-30, stats)
-    _check("bn_invstd", mi[c:].double(), inv, 1e-5 * inv, stats)
+    if local:
+        _check("bn_mean", mi[:c].double(), mean, 1e-5 * torch.sqrt(var / M) + 1e-30, stats)
+        _check("bn_invstd", mi[c:].double(), inv, 1e-5 * inv, stats)
     mean_k, inv_k = mi[:c].double(), mi[c:].double()            # what the kernels used
     db = torch.zeros_like(s1)
     dgm = torch.zeros_like(s1)
@@ -240,6 +244,8 @@ def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, c
         adgm += (dz * xh).abs().sum(0)
     _check("bn_dbeta", dbeta.double(), db, 1e-5 * adb + 1e-30, stats)
     _check("bn_dgamma", dgamma.double(), dgm, 1e-5 * adgm + 1e-30, stats)
+    if not local:
+        return
     rows = _idx(gen, M, ns, y.device)
     ch = _idx(gen, c, ns, y.device)
     mk = torch.stack([mask_fn(slice(int(r), int(r) + 1))[0, int(cc)] for r, cc in zip(rows.tolist(), ch.tolist())]) \
@@ -256,15 +262,19 @@ def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, c
     _check("bn_dy", got, ref, tol, stats)
 
 
-def _sampled_train_step(dev, bb, K, H, W, B, seeds):
+def _sampled_train_step(dev, bb, K, H, W, B, seeds, x=None, uv=None, sync_bn=False):
     """One Trainer step (bench.py --mode train's step) with every conv forward /
     dgrad / wgrad, BN backward and the stem wgrad checked on sampled elements
-    against fp64 recomputations from the call's own inputs.  Returns (loss, call
-    counts, worst error/bound per check, conv kernel symbols, model)."""
+    against fp64 recomputations from the call's own inputs.  x / uv: this rank's
+    shard instead of the seeded batch; sync_bn: a Trainer(sync_bn=True) step inside
+    an initialised process group (BN checks then cover this rank's dgamma / dbeta).
+    Returns (loss, call counts, worst error/bound per check, conv kernel symbols,
+    model)."""
     from _spy import spy_calls
     from hkp import net, ops, train
-    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, seeds[0])).to(dev)
-    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, seeds[1])).to(dev)
+    if x is None:
+        x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, seeds[0])).to(dev)
+        uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, seeds[1])).to(dev)
     m = _model(bb, K, seeds[2], dev)
     gen = torch.Generator().manual_seed(seeds[3])
     stats, counts, syms = {}, {"fwd": 0, "bwd": 0, "bn": 0, "stem_wgrad": 0}, {}
@@ -300,7 +310,7 @@ def _sampled_train_step(dev, bb, K, H, W, B, seeds):
         else:
             def mask_fn(rows):
                 return torch.ones_like(y2[rows], dtype=torch.float64)
-        check_bn_bwd(bn, gr, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats)
+        check_bn_bwd(bn, gr, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, local=not sync_bn)
         counts["bn"] += 1
 
     def on_stem_wgrad(xx, dy, w_shape, stride, pad, dil, layout, dw):
@@ -316,7 +326,7 @@ def _sampled_train_step(dev, bb, K, H, W, B, seeds):
     ops.set_observer(observe)
     try:
         with spy_calls(on_fwd, on_bwd, on_bn, on_stem_wgrad):
-            loss = train.Trainer(m).forward_backward(x, uv=uv)
+            loss = train.Trainer(m, sync_bn=sync_bn).forward_backward(x, uv=uv)
     finally:
         ops.set_observer(None)
     return loss, counts, stats, syms, m

@@ -184,7 +184,7 @@ def test_syncbn_dp_inference_matches_reference_global_batch(cuda_device):
 
 def _train_worker(rank, world, port, out_dir, q):
     import sys
-    sys.path[:0] = [REPO, PKG]
+    sys.path[:0] = [REPO, PKG, os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     try:
@@ -192,8 +192,9 @@ def _train_worker(rank, world, port, out_dir, q):
         from hkp import parallel, train
         from oracle import recipe
         from src.model import KeypointsGauss
+        from test_gpu_scale import _sampled_train_step
         dev = torch.device("cuda:0")
-        B, H, W, K = 4, 96, 128, 2
+        B, H, W, K = TRAIN_SHAPE
         lo, hi = parallel.shard_range(B, rank, world)
         imgs = recipe.seeded_images_u8(B, H, W, 21)
         uv_all = recipe.seeded_keypoints(B, K, H, W, 22)
@@ -206,14 +207,18 @@ def _train_worker(rank, world, port, out_dir, q):
             return orig_gather(st, group)
         parallel.gather_bn_stats = counting_gather
 
-        def grads_of(x, uv, sync):
+        def grads_of(x, uv, sync, distributed=False):
             m = KeypointsGauss(K, backbone="resnet18", pretrained=False)
             m.load_state_dict(recipe.seeded_state_dict("resnet18", 23))
             m = m.to(dev)
-            t = train.Trainer(m, distributed=False, sync_bn=sync)
+            t = train.Trainer(m, distributed=distributed, sync_bn=sync)
+            if distributed:
+                # the BN gathers run on their own communicator, the buckets on the world's
+                res["groups_differ"] = (t.bn_group is not t.group and t.policy.sync_group is t.bn_group
+                                        and t.bucketer is not None and t.bucketer.group is t.group)
             n_gathers[0] = 0
             loss = t.forward_backward(x, uv=uv)
-            if sync:
+            if sync and not distributed:
                 res["gathers"] = n_gathers[0]
             torch.cuda.synchronize()
             g = {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
@@ -224,6 +229,13 @@ def _train_worker(rank, world, port, out_dir, q):
         res = {}
         res["sync"] = grads_of(x, uv, True)
         res["local"] = grads_of(x, uv, False)
+        res["dp_sync"] = grads_of(x, uv, True, distributed=True)      # + the bucketed gradient all-reduce
+        # the same SyncBN step with every conv forward / dgrad / wgrad call and every
+        # BN backward's dgamma / dbeta checked against fp64 from the call's own inputs
+        # (mask flips cannot hide a kernel error here: each call is checked alone)
+        loss_s, counts, stats, _, _ = _sampled_train_step(dev, "resnet18", K, H, W, hi - lo, (21, 22, 23, 77 + rank),
+                                                          x=x, uv=uv, sync_bn=True)
+        res["spy"] = (float(loss_s), counts, stats)
         if rank == 0:
             res["global"] = grads_of(torch.from_numpy(imgs).to(dev), torch.from_numpy(uv_all).to(dev), False)
         torch.save(res, os.path.join(out_dir, "rank%d.pt" % rank))
@@ -234,21 +246,50 @@ def _train_worker(rank, world, port, out_dir, q):
         raise
 
 
+TRAIN_SHAPE = (4, 96, 128, 2)          # global batch, H, W, K (R18-8s)
+
+
 def _rel(a, b):
     return float((a.double() - b.double()).norm() / max(float(b.double().norm()), 1e-30))
 
 
+def _oracle_grads(dtype):
+    """The reference's step over the whole 4-image batch (oracle, CPU) in `dtype`."""
+    from oracle import cpu_ref, recipe
+    B, H, W, K = TRAIN_SHAPE
+    sd = {k: (v.clone().to(dtype) if v.is_floating_point() else v.clone())
+          for k, v in recipe.seeded_state_dict("resnet18", 23).items()}
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 21)).to(dtype)
+    L, g, _ = cpu_ref.train_step(sd, x, recipe.seeded_keypoints(B, K, H, W, 22), "resnet18", K, adam_state=None)
+    return float(L), g
+
+
+def _as_ref_layout(g, ref):
+    """KRSC conv gradients → the reference's OIHW for comparison."""
+    return {n: (t if t.shape == ref[n].shape else t.permute(0, 3, 1, 2)) for n, t in g.items()}
+
+
 def test_syncbn_training_step_equals_global_batch(cuda_device, tmp_path):
-    """2 ranks x 2 images with SyncBN: the mean of the ranks' gradients (what the
-    DP all-reduce computes) and of their losses == one step over all 4 images;
-    BN running statistics too.  Per-rank BN misses it by orders of magnitude."""
+    """2 ranks x 2 images with SyncBN == one step over all 4 images (R18-8s, 96x128).
+
+    Gradient tolerance from the problem's measured conditioning.  This step has a
+    ReLU kink inside fp32 noise: in the reference's own fp32 run exactly one element
+    of layer4.0's output (image 2, channel 218, (7, 6)), whose pre-ReLU sum is
+    ~1e-6 from zero, falls on the other side of the kink than in fp64 — and that one
+    element carries all of the fp32-vs-fp64 gradient difference (0.6 % at layer4,
+    ~1 % upstream; DESIGN "SyncBN step parity").  Two correct fp32-class
+    computations that round differently (another tile shape / MFMA order) can
+    therefore differ by that much, so the bound is 2x the reference's own fp32
+    distance from its fp64 step (measured here, ~1.1e-2), each path is checked
+    against fp64, and kernel exactness is pinned call by call (spy harness) instead.
+    Per-rank BN misses by ~1.0, far outside the bound."""
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_train_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(60)
     assert all("error" not in r for r in res), res
@@ -256,22 +297,51 @@ def test_syncbn_training_step_equals_global_batch(cuda_device, tmp_path):
     r0 = torch.load(os.path.join(tmp_path, "rank0.pt"), weights_only=True)
     r1 = torch.load(os.path.join(tmp_path, "rank1.pt"), weights_only=True)
     lg, gg, rmg = r0["global"]
+    l64, g64 = _oracle_grads(torch.float64)
+    l32, g32 = _oracle_grads(torch.float32)
+    cond = max(_rel(g32[n], g64[n]) for n in g64)          # the reference's own fp32 distance from fp64
+    bound = 2 * cond
+    gg = _as_ref_layout(gg, g64)
+    print("conditioning: reference fp32 vs fp64 worst grad rel %.3g -> bound %.3g" % (cond, bound))
+    assert 1e-4 < cond < 5e-2, cond                          # the kink is there (and nothing else is off)
     # R18: 20 BN layers, 3 downsample blocks whose last BN and downsample BN share
     # one gather in each direction -> 17 forward + 17 backward statistics gathers
     assert r0["gathers"] == r1["gathers"] == 34, (r0["gathers"], r1["gathers"])
+    assert r0["groups_differ"] and r1["groups_differ"]
+    # every call of the SyncBN step exact vs fp64 from its own inputs (asserted in the
+    # worker; the counts and worst ratios come back for the log)
+    for r in (r0, r1):
+        print("spy: loss %.9f calls %s worst %s" % (r["spy"][0], r["spy"][1],
+                                                   {k: round(v, 4) for k, v in r["spy"][2].items()}))
+        assert r["spy"][1]["fwd"] > 0 and r["spy"][1]["bwd"] > 0 and r["spy"][1]["bn"] > 0
+        assert max(r["spy"][2].values()) <= 1.0
+    glob_err = max(_rel(gg[n], g64[n]) for n in g64)
+    print("global 4-image GPU step vs fp64: worst grad rel %.3g; loss %.3g" % (glob_err, abs(lg - l64) / l64))
+    assert glob_err < bound and abs(lg - l64) < 1e-6 * l64
     for kind in ("sync", "local"):
         l0, g0, rm0 = r0[kind]
         l1, g1, rm1 = r1[kind]
+        mean_g = _as_ref_layout({n: (g0[n] + g1[n]) / 2 for n in g0}, g64)
         loss_err = abs((l0 + l1) / 2 - lg) / abs(lg)
-        grad_err = max(_rel((g0[n] + g1[n]) / 2, gg[n]) for n in gg)
+        grad_err = max(_rel(mean_g[n], gg[n]) for n in gg)
+        exact_err = max(_rel(mean_g[n], g64[n]) for n in g64)
         rm_err = max(_rel(rm0[n], rmg[n]) for n in rmg)
-        print("%s: loss rel err %.3g, worst grad rel err %.3g, running-mean rel err %.3g"
-              % (kind, loss_err, grad_err, rm_err))
+        print("%s: loss rel err %.3g, worst grad rel err vs global GPU %.3g, vs fp64 %.3g, running-mean rel err %.3g"
+              % (kind, loss_err, grad_err, exact_err, rm_err))
         if kind == "sync":
             assert loss_err < 1e-6
-            assert grad_err < 1e-4
+            assert grad_err < bound and exact_err < bound
             assert rm_err < 1e-5
             assert all(torch.equal(rm0[n], rm1[n]) for n in rm0)      # every rank holds the same statistics
-            sync_grad_err = grad_err
         else:
-            assert grad_err > 100 * sync_grad_err                      # per-rank BN: another computation
+            assert exact_err > 20 * bound                               # per-rank BN: another computation
+    # Trainer(distributed=True, sync_bn=True): the all-reduced gradients on each rank
+    # are the global-batch step's, within the same bound
+    for r in (r0, r1):
+        ld, gd, rmd = r["dp_sync"]
+        gd = _as_ref_layout(gd, g64)
+        dp_err = max(_rel(gd[n], g64[n]) for n in g64)
+        print("dp_sync rank: worst grad rel err vs fp64 %.3g" % dp_err)
+        assert dp_err < bound
+        assert max(_rel(rmd[n], rmg[n]) for n in rmg) < 1e-5
+    assert all(torch.equal(r0["dp_sync"][1][n], r1["dp_sync"][1][n]) for n in r0["dp_sync"][1])

@@ -466,3 +466,16 @@ def test_dropin_fit_dp_overlaps_allreduce_gloo_world2(tmp_path):
         assert r["launched_before_end"] and r["grads_before_first"] < r["n_grads"], r
         assert r["n_all_reduce"] == r["n_buckets"] >= 3, r
     assert os.path.exists(os.path.join(tmp_path, "model_2_1_0.pth"))
+
+
+def test_bench_names_each_config():
+    """bench.py names the BASELINE config a line measures (every line said C2)."""
+    sys.path.insert(0, REPO)
+    import bench
+    n = bench.workload_name
+    assert n("infer", "resnet34", 4, 480, 640, "f16x3", 32).startswith("C2")
+    assert n("train", "resnet34", 4, 480, 640, "f16x3", 8).startswith("C3")
+    assert n("infer", "resnet50", 8, 480, 640, "f16", 128).startswith("C4")
+    assert n("train", "resnet50", 8, 960, 1280, "f16x3", 32).startswith("C5")
+    assert n("train", "resnet18", 2, 240, 320, "f16x3", 4).startswith("C1")
+    assert n("infer", "resnet50", 8, 480, 640, "f16x3", 128).startswith("custom")

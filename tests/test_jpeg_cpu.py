@@ -192,3 +192,50 @@ def test_corrupt_inputs_fail_cleanly():
         except jpeg.JpegError:
             outcomes["error"] += 1
     assert outcomes["ok"] > 0 and outcomes["error"] > 0, outcomes
+
+
+def _drop_first_rst(data):
+    """The JPEG with its first RSTn marker (FF D0..D7 inside the scan) removed."""
+    sos = data.index(b"\xff\xda")
+    for j in range(sos + 2, len(data) - 1):
+        if data[j] == 0xFF and 0xD0 <= data[j + 1] <= 0xD7:
+            return data[:j] + data[j + 2:]
+    raise AssertionError("no restart marker")
+
+
+def test_missing_rst_marker_falls_back_to_host_decode(tmp_path):
+    """A file with one RST marker missing: the entropy decoder refuses it
+    (JpegError: it does not resync), and DeviceBatches(decode="device")'s worker
+    item falls back to the host decode — which, like cv2.imread, resyncs and
+    still returns an image — instead of killing the loader worker."""
+    from hkp import jpeg
+    from src.dataset import KeypointsDataset, _CoefView, _collate_coef, transform
+    good = _jpeg(_image(48, 64, 71), quality=85, subsampling=2, restart_marker_blocks=2)
+    bad = _drop_first_rst(good)
+    with pytest.raises(jpeg.JpegError):
+        jpeg.entropy_decode(bad)
+    ref = _pil_bgr(bad)                                   # libjpeg resyncs: an image comes back
+    assert ref.shape == (48, 64, 3)
+    os.makedirs(tmp_path / "images")
+    os.makedirs(tmp_path / "labels")
+    for i, d in enumerate([good, bad]):
+        (tmp_path / "images" / ("%05d.jpg" % i)).write_bytes(d)
+        np.save(tmp_path / "labels" / ("%05d.npy" % i), np.array([[1.0, 2.0]]))
+    ds = KeypointsDataset(str(tmp_path / "images"), str(tmp_path / "labels"), 1, 48, 64, transform, device="cpu")
+    view = _CoefView(ds)
+    assert view[0][0] == "coef"
+    item = view[1]
+    assert item[0] == "img" and np.array_equal(item[1], ref)
+    b = _collate_coef([view[0], view[1]])                 # the batch decodes on the host
+    assert b[0] == "img" and np.array_equal(b[1][1].numpy(), ref)
+
+
+def test_sos_segment_too_short_is_rejected():
+    """An SOS whose length field covers no component bytes, at the very end of the
+    buffer: rejected before any byte past the segment is read."""
+    from hkp import jpeg
+    data = _jpeg(_image(16, 16, 3), quality=80)
+    sos = data.index(b"\xff\xda")
+    for ln in (2, 3, 5):
+        with pytest.raises(jpeg.JpegError, match="SOS"):
+            jpeg.entropy_decode(data[:sos] + b"\xff\xda" + bytes([0, ln]) + bytes(max(0, ln - 2)))

@@ -97,6 +97,48 @@ def test_gather_bn_stats_gloo_world2():
     assert all(ok for _, ok in res), res
 
 
+def _groups_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hkp import parallel, train
+    from src.model import KeypointsGauss
+    m = KeypointsGauss(2, 32, 48, backbone="resnet18", pretrained=False)
+    t = train.Trainer(m, distributed=True, optimizer="torch", sync_bn=True, bucket_mb=1)
+    ok = t.bn_group is not None and t.bn_group is not t.group            # SyncBN: its own communicator
+    ok &= t.policy.sync_group is t.bn_group and t.bucketer.group is t.group
+    ok &= parallel.active_sync_group(t.policy) == (t.bn_group,)
+    ok &= dist.get_process_group_ranks(t.bn_group) == list(range(world))
+    # the BN group carries collectives independently of the default group
+    st = torch.full((3,), float(rank), dtype=torch.float64)
+    g = parallel.gather_bn_stats(st, t.bn_group)
+    ok &= torch.equal(g[:, 0], torch.arange(world, dtype=torch.float64))
+    ok &= not t.bucketer.avg_in_collective        # gloo has no ReduceOp.AVG: sum, then 1/world
+    t2 = train.Trainer(m, distributed=True, optimizer="torch", sync_bn=False, bucket_mb=1)
+    ok &= t2.bn_group is t2.group is None          # no SyncBN: no extra communicator
+    q.put((rank, bool(ok)))
+    dist.destroy_process_group()
+
+
+def test_trainer_syncbn_own_communicator_gloo_world2():
+    """Trainer(sync_bn=True) gives the BN gathers a communicator of their own
+    (RCCL runs one communicator's collectives in issue order: a backward BN gather
+    must not queue behind an in-flight gradient bucket); the step equality itself
+    is checked on the GPU (test_gpu_syncbn.py, dp_sync)."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_groups_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = [q.get(timeout=5) for _ in range(world)]
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(ok for _, ok in res), res
+
+
 def test_sync_bn_single_process_is_off():
     import sys
     sys.path[:0] = [REPO, PKG]
