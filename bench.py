@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--keypoints", type=int, default=4)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--precision", choices=["fp32", "f16x3", "f16"], default=None,
+    ap.add_argument("--precision", choices=["fp32", "f16x3", "f16", "f16x2w", "f16x2a"], default=None,
                     help="NHWC conv arithmetic (default: f16x3 = fp32-accurate split fp16 MFMA)")
     ap.add_argument("--input", choices=["f32", "u8"], default="f32",
                     help="f32: the reference's ToTensor NCHW tensor; u8: the cv2.imread-style uint8 HWC batch "
@@ -410,7 +410,9 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
     alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
     if dom_sym.startswith(("conv_x3_kernel", "conv_x3_halo_kernel", "wgrad_x3_kernel")):
-        passes = 3 if precision == "f16x3" else 1   # the x3 LDS-DMA kernels: 3 MFMAs per MAC (f16x3) or 1 (f16)
+        # the x3 LDS-DMA kernels: fp16 MFMAs per fp32 MAC — 3 (f16x3), 2 (f16x2w / f16x2a: two of
+        # the three products), 1 (f16)
+        passes = {"f16x3": 3, "f16x2w": 2, "f16x2a": 2}.get(precision, 1)
         achieved, peak = alg * passes, PEAK_FP16_MFMA_TFLOPS    # issued fp16 MFMA FLOPs vs dense fp16 peak
     else:
         passes, achieved, peak = 1, alg, PEAK_FP32_MFMA_TFLOPS
@@ -511,7 +513,9 @@ def main():
         if dist:
             torch.distributed.destroy_process_group()
         return
-    dtype = {"fp32": "f32", "f16x3": "f32 (f16x3 split-precision MFMA, fp32-accurate)", "f16": "f16"}[precision]
+    dtype = {"fp32": "f32", "f16x3": "f32 (f16x3 split-precision MFMA, fp32-accurate)", "f16": "f16",
+             "f16x2w": "f32 activations x f16 weights (2 fp16 MFMA products)",
+             "f16x2a": "f16-rounded activations x split weights (2 fp16 MFMA products)"}[precision]
     B = batch
     out = {
         "metric": "images/sec (640x480, N keypoints) inference+train at 1/2/4/8 MI355X",

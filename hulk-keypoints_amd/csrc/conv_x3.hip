@@ -44,11 +44,17 @@
 // default arithmetic); 1 = plain fp16 NHWC activations and KRSC weights (each
 // output channel scaled by a power of two) — BASELINE config C4's "fp16 with
 // MFMA", the same kernel with 2 MFMAs per 64 channels instead of 3 per 32.
+// Intermediate precisions on the packed layout (inference; DESIGN "precision
+// modes"), 2 MFMAs per 32 channels: P = 2 keeps hi_x*hi_w + lo_x*hi_w (the
+// weights rounded to fp16 after their per-channel power-of-two scale, the
+// activation exact to ~2^-22), P = 4 keeps hi_x*hi_w + hi_x*lo_w (the activation
+// rounded to fp16, the weights exact).
 //
 // Replaces the cuDNN convs of src/resnet.py:20-37,77,86,137,184-188 and their
 // backward under loss.backward() (train.py:35).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -274,13 +280,25 @@ __device__ __forceinline__ void x3_store(const X3Args& a, long off, float v, flo
 // The MFMAs of one 128-B stage row pair (A fragment a0/a1, B fragment b0/b1 =
 // the row's chunks 0-3 / 4-7) for operand layout P:
 //   P = 3 (packed f16x3 split, chunks = hi32 | lo32):  hi*hi + hi*lo + lo*hi
+//   P = 2 / 4 (packed split): two of those three products (see the header)
 //   P = 1 (plain fp16, chunks = channels 0-31 | 32-63): two k-slices
+// operand layout of P: the packed hi|lo split (P 2, 3, 4) or plain fp16 (P 1)
+constexpr bool x3_packed(int P) { return P != 1; }
+// fp16 MFMAs per 128-B stage row pair
+constexpr int x3_nprod(int P) { return P == 3 ? 3 : 2; }
+
 template <int P, typename V, typename Acc, typename Mfma>
 __device__ __forceinline__ void x3_products(Acc& acc, const V& a0, const V& a1, const V& b0, const V& b1, Mfma&& mfma) {
     if constexpr (P == 3) {
         acc = mfma(a0, b0, acc);
         acc = mfma(a0, b1, acc);
         acc = mfma(a1, b0, acc);
+    } else if constexpr (P == 2) {         // weights at fp16: (hi_x + lo_x) * hi_w
+        acc = mfma(a0, b0, acc);
+        acc = mfma(a1, b0, acc);
+    } else if constexpr (P == 4) {         // activation at fp16: hi_x * (hi_w + lo_w)
+        acc = mfma(a0, b0, acc);
+        acc = mfma(a0, b1, acc);
     } else {
         acc = mfma(a0, b0, acc);
         acc = mfma(a1, b1, acc);
@@ -657,7 +675,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                                                   Issue& issue_next) {
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
-    constexpr int NMC = (P == 3 ? 3 : 2) * UM;      // MFMAs per column block per K-step
+    constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
     constexpr int RED_OFF = PAIRB ? 0 : x3_lds_bytes(BN, PAIRB, P);
     float* const scl = (float*)(smem + RED_OFF + 2 * 4 * BN * 4);   // [BN] column scales (!PAIRB)
@@ -934,7 +952,8 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // stage), 16 = v_mfma_f32_16x16x32_f16 (one k32 step per stage half; same cycles
 // per FLOP, lower power per FLOP, so the chip holds a higher clock under load —
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
-// P: operand layout (x3_products) — 3 packed f16x3 split, 1 plain fp16.
+// P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
+// packed split with two of its three products, 1 plain fp16.
 template <int BN, bool STEM, bool PAIR, int MFD, int P>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
@@ -949,7 +968,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(MFD == 16 || MFD == 32, "bad conv_x3 MFMA shape");
-    static_assert(P == 3 || (P == 1 && !STEM), "bad conv_x3 operand layout");
+    static_assert(P == 3 || ((P == 1 || P == 2 || P == 4) && !STEM), "bad conv_x3 operand layout");
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
 
@@ -1090,7 +1109,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
 #pragma unroll
             for (int j = 0; j < TN; ++j) x3_products<P>(acc[i][j], f.ah[i], f.al[i], f.bh[j], f.bl[j], mfma);
     };
-    constexpr int NR = 2 * (TM + TN), NM = (P == 3 ? 3 : 2) * TM * TN;   // ds_reads / MFMAs per k16 slice
+    constexpr int NR = 2 * (TM + TN), NM = x3_nprod(P) * TM * TN;   // ds_reads / MFMAs per k16 slice
 
     // prologue: NST-1 stages in flight, stage 0 landed everywhere
     issue_next();
@@ -2273,12 +2292,24 @@ static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 // epilogue, 32-bit halo offsets)
 // lines: 128-B input lines per pixel (32 channels each for P 3, 64 for P 1)
 static int x3_halo_level(bool ok, int lines, int P) {
-    return !ok ? 0 : lines * (P == 3 ? 32 : 64) <= 64 ? 2 : 1;
+    return !ok ? 0 : lines * (x3_packed(P) ? 32 : 64) <= 64 ? 2 : 1;
 }
 
 static bool x3_halo_ok(const X3Args& a, int k) {
     return halo_shape(a.stride, a.R, a.S, a.pad, a.dil, a.Ho, a.Wo, k) && a.ost == 0 && a.ep_ss == nullptr &&
            a.mt0 == 0 && a.plane == 0 && (long)a.N * a.H * a.W * a.cch * 64L + 64 < (1L << 32);
+}
+
+// run f with std::integral_constant<int, P> for a runtime operand layout P
+template <typename F>
+static void x3_dispatch_p(int P, F&& f) {
+    switch (P) {
+        case 3: f(std::integral_constant<int, 3>{}); break;
+        case 1: f(std::integral_constant<int, 1>{}); break;
+        case 2: f(std::integral_constant<int, 2>{}); break;
+        case 4: f(std::integral_constant<int, 4>{}); break;
+        default: break;
+    }
 }
 
 static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
@@ -2292,8 +2323,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.sk_units = 0;
     if (c.halo) {
         const dim3 gh((unsigned)(m_tiles * a.n_tiles));
-        if (P == 3) hipLaunchKernelGGL(conv_x3_halo_kernel<3>, gh, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL(conv_x3_halo_kernel<1>, gh, dim3(512), 0, st, a);
+        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL(conv_x3_halo_kernel<pc.value>, gh, dim3(512), 0, st, a); });
         return;
     }
     dim3 grid((unsigned)(m_tiles * a.n_tiles));
@@ -2322,8 +2352,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     if (tail) {
         if (rm > 0) {
             dim3 g0((unsigned)(rm * a.n_tiles));
-            if (P == 3) launch_x3_p<3>(c, g0, st, a);
-            else launch_x3_p<1>(c, g0, st, a);
+            x3_dispatch_p(P, [&](auto pc) { launch_x3_p<pc.value>(c, g0, st, a); });
         }
         X3Args t = a;
         t.mt0 = (int)rm;
@@ -2331,12 +2360,10 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         t.sk_cnt = (unsigned*)ws;
         t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
         const dim3 gt((unsigned)(NG * a.n_tiles));
-        if (P == 3) hipLaunchKernelGGL((conv_x3_tail_kernel<256, 3>), gt, dim3(512), 0, st, t);
-        else hipLaunchKernelGGL((conv_x3_tail_kernel<256, 1>), gt, dim3(512), 0, st, t);
+        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL((conv_x3_tail_kernel<256, pc.value>), gt, dim3(512), 0, st, t); });
         return;
     }
-    if (P == 3) launch_x3_p<3>(c, grid, st, a);
-    else launch_x3_p<1>(c, grid, st, a);
+    x3_dispatch_p(P, [&](auto pc) { launch_x3_p<pc.value>(c, grid, st, a); });
 }
 
 }  // namespace hkp
@@ -2387,10 +2414,10 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
     if (rc) return rc;
     rc = check_tile(d, who);
     if (rc) return rc;
-    HKP_CHECK_ARG(xs && ws && (P == 3 ? y != nullptr && y16 == nullptr : y == nullptr && y16 != nullptr),
-                  "%s: null tensor (P 3 writes fp32 y, P 1 fp16 y)", who);
+    HKP_CHECK_ARG(xs && ws && (x3_packed(P) ? y != nullptr && y16 == nullptr : y == nullptr && y16 != nullptr),
+                  "%s: null tensor (the packed split writes fp32 y, P 1 fp16 y)", who);
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "%s: NHWC only", who);
-    const int cg = P == 3 ? 32 : 64;
+    const int cg = x3_packed(P) ? 32 : 64;
     HKP_CHECK_ARG(d->c % cg == 0 && d->k % 64 == 0, "%s: need Cin%%%d==0, Cout%%64==0 (c=%d k=%d)", who, cg, d->c,
                   d->k);
     const long M = (long)d->n * ho * wo;
@@ -2416,6 +2443,17 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     HKP_CHECK_ARG(d && y, "hkp_conv2d_fwd_x3: null argument");
     return conv_fwd_x3_common(d, x_split, w_split, w_inv_scale, y, nullptr, stat_partials, sk_workspace, sk_ws_bytes,
                               3, stream, "hkp_conv2d_fwd_x3");
+}
+
+extern "C" int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
+                                          const float* w_inv_scale, int32_t products, float* y, float* stat_partials,
+                                          void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && y, "hkp_conv2d_fwd_x3_products: null argument");
+    HKP_CHECK_ARG(products == HKP_X3_ALL || products == HKP_X3_W16 || products == HKP_X3_X16,
+                  "hkp_conv2d_fwd_x3_products: unknown product set %d", products);
+    const int P = products == HKP_X3_ALL ? 3 : products == HKP_X3_W16 ? 2 : 4;
+    return conv_fwd_x3_common(d, x_split, w_split, w_inv_scale, y, nullptr, stat_partials, sk_workspace, sk_ws_bytes,
+                              P, stream, "hkp_conv2d_fwd_x3_products");
 }
 
 extern "C" int hkp_conv2d_fwd_f16(const hkp_conv_desc* d, const uint16_t* x_f16, const uint16_t* w_f16,
@@ -2708,10 +2746,12 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
     const bool sk = stream_k_ok != 0;
     switch (op) {
         case HKP_KOP_FWD_X3:
+        case HKP_KOP_FWD_X3_W16:
+        case HKP_KOP_FWD_X3_X16:
         case HKP_KOP_FWD_F16: {
-            const int P = op == HKP_KOP_FWD_X3 ? 3 : 1;
+            const int P = op == HKP_KOP_FWD_X3 ? 3 : op == HKP_KOP_FWD_X3_W16 ? 2 : op == HKP_KOP_FWD_X3_X16 ? 4 : 1;
             const long m = (long)d->n * ho * wo;
-            const int cg = P == 3 ? 32 : 64;
+            const int cg = x3_packed(P) ? 32 : 64;
             const int nks = d->r * d->s * (d->c / cg);
             const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
                               (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);

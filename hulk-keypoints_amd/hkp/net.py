@@ -20,7 +20,7 @@ import weakref
 import torch
 
 from . import ops, parallel
-from .policy import resolve
+from .policy import INFERENCE_ONLY, resolve
 
 
 class Trace:
@@ -124,7 +124,7 @@ def prepack_x3(resnet, flip, pol=None):
     The operands land in the same cache conv_bn / _conv_backward read, with the
     parameter versions they were packed from; buffers are reused across steps."""
     pol = resolve(pol)
-    if pol.precision != "f16x3":
+    if pol.passes != 3:
         return
     # fast path: the last call's launch repeated as is when every operand it packed
     # is stale again (a training step: the optimizer bumped every weight) and the
@@ -222,7 +222,8 @@ def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
         return ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
                                       stats=bn.training)
     if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
-        return ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training, sk=sk)
+        return ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training, sk=sk,
+                                 products=pol.products)
     if layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
         return ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
                                   stats=bn.training, sk=sk,
@@ -451,8 +452,8 @@ def keypoints_forward(resnet, x_nchw, k, heat=True, argmax=False, trace=None, po
     """Fused K-channel head: heat = sigmoid(upsample(fc[:K](feat)))  (model.py:19-22).
     pol: the execution policy (a trace carries its own)."""
     pol = trace.policy if trace is not None else resolve(pol)
-    if trace is not None and pol.precision == "f16":
-        raise ops.HkpError("precision 'f16' (BASELINE config C4) is inference-only; train with 'f16x3' or 'fp32'")
+    if trace is not None and pol.precision in INFERENCE_ONLY:
+        raise ops.HkpError("precision %r is inference-only; train with 'f16x3' or 'fp32'" % pol.precision)
     w, b = fc_rows(resnet, k)
     if trace is None and pol.fused_head and ops.head_fusable(_feat_channels(resnet), k):
         feat, low = None, backbone_forward(resnet, x_nchw, None, head=(w, b), pol=pol)

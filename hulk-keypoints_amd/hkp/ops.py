@@ -8,7 +8,8 @@ import ctypes
 
 import torch
 
-from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3,
+from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
+                   HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
                    HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, ConvDesc, HkpError, call)
 
 CONV_TILE_ROWS = 128  # BM of conv_fwd.hip (rows per BN statistic tile)
@@ -175,11 +176,14 @@ def _stat_partials(n_rows, k, device, part_out, name):
     return part_out
 
 
-def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True, tile=0):
+def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True, tile=0,
+                  products=HKP_X3_ALL):
     """f16x3 NHWC conv on packed split operands: xs [N,H,W,2C] (from a producer with
     split=3), wp = weight_pack_x3(w) → fp32 y [N,Ho,Wo,K] (+ BN partials, into
     part_out when given).  sk=False: never stream-K (one tile per block);
-    tile: HKP_TILE_* policy (0 = the planner)."""
+    tile: HKP_TILE_* policy (0 = the planner); products: HKP_X3_ALL (f16x3), or
+    HKP_X3_W16 / HKP_X3_X16 (two of the three products: the weights / the
+    activation at fp16, hkp_conv2d_fwd_x3_products)."""
     ws, wsc = wp
     _need(xs, torch.float16, "conv2d_fwd_x3.x_split", 4)
     _need(ws, torch.float16, "conv2d_fwd_x3.w_split", 4)
@@ -194,14 +198,21 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     y = out if out is not None else torch.empty((n, ho, wo, k), device=xs.device, dtype=torch.float32)
     part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out") if stats else None
 
-    def launch():
-        call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
-             *_sk_workspace(sk), _stream())
+    if products == HKP_X3_ALL:
+        def launch():
+            call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
+                 *_sk_workspace(sk), _stream())
+        kop = HKP_KOP_FWD_X3
+    else:
+        def launch():
+            call("hkp_conv2d_fwd_x3_products", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), int(products),
+                 _ptr(y), _ptr(part), *_sk_workspace(sk), _stream())
+        kop = HKP_KOP_FWD_X3_W16 if products == 2 else HKP_KOP_FWD_X3_X16
 
     if _observer is None:
         launch()
     else:
-        _observer(kernel_name(d, HKP_KOP_FWD_X3, sk), 2.0 * n * ho * wo * k * r * s * c,
+        _observer(kernel_name(d, kop, sk), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
     return y, part
 

@@ -16,7 +16,15 @@ from dataclasses import dataclass, fields, replace
 #   "f16"   plain fp16 operands and activations, fp32 accumulation (BASELINE
 #           config C4, inference): one fp16 MFMA per MAC, fp16 conv outputs and
 #           residual stream (autocast semantics)
-PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1}
+#   "f16x2w" / "f16x2a"  inference modes between the two (DESIGN "precision
+#           modes"): the f16x3 data path (packed split activations, fp32 conv
+#           outputs and BN) with two of the three fp16 products per MAC — the
+#           weights ("w") or the conv's input activation ("a") rounded to fp16
+# value: the operand layout the producers emit (3 packed split, 1 plain fp16, 0 fp32)
+PRECISIONS = {"fp32": 0, "f16x3": 3, "f16": 1, "f16x2w": 3, "f16x2a": 3}
+# hkp_conv2d_fwd_x3_products product set of each packed-split precision
+PRODUCTS = {"f16x3": 3, "f16x2w": 2, "f16x2a": 4}
+INFERENCE_ONLY = ("f16", "f16x2w", "f16x2a")
 
 
 @dataclass(frozen=True)
@@ -56,6 +64,11 @@ class Policy:
     @property
     def passes(self):
         return PRECISIONS[self.precision]
+
+    @property
+    def products(self):
+        """hkp_conv2d_fwd_x3_products product set of the packed-split forward convs."""
+        return PRODUCTS.get(self.precision, 3)
 
     def with_(self, **kw):
         return replace(self, **kw)

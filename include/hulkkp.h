@@ -123,6 +123,20 @@ int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uin
  * leaves them zero (allocate once, zeroed, per stream: calls on one workspace
  * must not run concurrently).  Size: hkp_conv_x3_sk_workspace_bytes(). */
 int64_t hkp_conv_x3_sk_workspace_bytes(void);
+/* hkp_conv2d_fwd_x3 with a chosen subset of the three f16x3 products (inference
+ * precision modes between config C4's plain fp16 and f16x3; same operands,
+ * outputs and workspace).  products: HKP_X3_ALL = hkp_conv2d_fwd_x3;
+ * HKP_X3_W16 = hi_x*hi_w + lo_x*hi_w (the weights rounded to fp16 after their
+ * per-channel power-of-two scale, the activation kept to ~2^-22); HKP_X3_X16 =
+ * hi_x*hi_w + hi_x*lo_w (the activation rounded to fp16, the weights kept).
+ * Two fp16 MFMAs per 32 channels instead of three.  Replaces the same convs as
+ * hkp_conv2d_fwd_x3 (src/resnet.py:20-37,77,86,184-188). */
+#define HKP_X3_ALL 3
+#define HKP_X3_W16 2
+#define HKP_X3_X16 4
+int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
+                               const float* w_inv_scale, int32_t products, float* y, float* stat_partials,
+                               void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream);
 /* Plain-fp16 conv (BASELINE config C4, "fp16 with MFMA"): the same LDS-DMA
  * kernel family as hkp_conv2d_fwd_x3 with one fp16 product per MAC (fp32
  * accumulation).  x_f16: NHWC fp16 [n][h][w][c] (a producer's split_passes = 1
@@ -182,6 +196,8 @@ int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, co
 #define HKP_KOP_FWD_F16 2
 #define HKP_KOP_STEM_X3 3
 #define HKP_KOP_WGRAD_X3 4
+#define HKP_KOP_FWD_X3_W16 5   /* hkp_conv2d_fwd_x3_products(HKP_X3_W16) */
+#define HKP_KOP_FWD_X3_X16 6   /* hkp_conv2d_fwd_x3_products(HKP_X3_X16) */
 int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf, int32_t len);
 
 /* Debug (tools/ only, not thread-safe): one-tile forward conv launches record

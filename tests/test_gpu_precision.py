@@ -657,3 +657,44 @@ def test_bn_apply_f16(cuda_device):
         assert torch.equal(ops.split_of(o)[0], torch.relu(want).half())
         o16 = ops.bn_apply_f16(y, ss, res=res, res_ss=res_ss, relu=False)
         assert o16.dtype == torch.float16 and torch.equal(o16, want.half())
+
+
+@pytest.mark.parametrize("case", X3_CASES)
+@pytest.mark.parametrize("products", [2, 4])
+def test_x3_product_subsets(cuda_device, case, products):
+    """hkp_conv2d_fwd_x3_products: HKP_X3_W16 (2) = the activation exact x the
+    weights rounded to fp16 after their power-of-two scale; HKP_X3_X16 (4) = the
+    activation rounded to fp16 x the weights exact.  Each equals an fp64 conv of
+    the correspondingly rounded operands to fp32-class accuracy (2e-6 of the output
+    scale, as f16x3), on every live tile body; BN partials as the y they produced."""
+    from hkp import ops
+    n, h, w, cin, cout, k, st, pad, dil = case
+    x = F.relu(rand(n, h, w, cin, seed=21))
+    wt = rand(cout, k, k, cin, seed=22, scale=(2.0 / (k * k * cout)) ** 0.5)
+    d = cuda_device
+    ss = torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d)
+    xs = ops.bn_apply(x.to(d), ss, relu=False, split=3, keep_fp32=False)
+    wp = ops.weight_pack_x3(wt.to(d))
+    inv = wp.inv_scale.cpu().view(-1, 1, 1, 1)
+    xr, wr = x.double(), wt.double()
+    if products == 2:                                     # weights: hi of the scaled weight, unscaled
+        wr = ((wt / inv).half().double()) * inv.double()
+    else:                                                 # activation: hi = f16(x)
+        xr = x.half().double()
+    ref = F.conv2d(xr.permute(0, 3, 1, 2), wr.permute(0, 3, 1, 2), None, st, pad, dil)
+    scale = ref.abs().max().item()
+    y, p = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, products=products)
+    err = (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / scale
+    full = F.conv2d(x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double(), None, st, pad, dil)
+    err_full = (y.cpu().double().permute(0, 3, 1, 2) - full).abs().max().item() / scale
+    print("products %d: vs rounded-operand fp64 %.3g, vs exact fp64 %.3g" % (products, err, err_full))
+    assert err < 2e-6, err
+    assert 1e-5 < err_full < 3e-3, err_full              # the fp16 rounding of one operand is visible
+    m = y.numel() // cout
+    y32 = y.reshape(m, cout).double()
+    stats = _bn_stats(p, m)
+    torch.testing.assert_close(stats[:cout].cpu().double(), y32.mean(0).cpu(), rtol=1e-5, atol=1e-6)
+    for tile in LIVE_TILES:
+        yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile, products=products)
+        assert (yv.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale, tile
+

@@ -477,12 +477,13 @@ def test_c4_fp16_forward_sampled_fp64(cuda_device):
     assert torch.isfinite(hm).all().item() and yx.shape == (B, K, 2)
 
 
-@pytest.mark.parametrize("precision", ["f16x3", "f16"])
+@pytest.mark.parametrize("precision", ["f16x3", "f16", "f16x2w", "f16x2a"])
 def test_r50_bench_resolution_vs_reference(cuda_device, golden, precision):
     """C4's network (R50-8s K=8) at 640x480 vs the reference fixture: f16x3 meets
     the north-star bar (heat < 1e-3, argmax bit-exact); plain fp16 (config C4's
-    arithmetic) is reported — heatmap error and argmax agreement — and gated at
-    the measured values with a margin."""
+    arithmetic) and the two-product modes f16x2w / f16x2a (DESIGN "precision
+    modes") are reported — heatmap error and argmax agreement — and gated at the
+    measured values with a margin."""
     import hashlib
     g = golden("fwd_r50_k8_480x640_b2")
     B, H, W, K, st = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["k"]), int(g["step"])
