@@ -88,6 +88,10 @@ struct X3Args {
     float* sk_ws = nullptr;
     unsigned* sk_cnt = nullptr;
     unsigned long long* stamps = nullptr;   // debug: per-block phase clocks (hkp_debug_x3_stamps)
+    // first-round stagger: blocks b < stagger_blocks with (b >> 3) & 1 (half the CUs
+    // of every XCD) wait stagger_ticks (s_memrealtime, 100 MHz) before starting, so
+    // the CUs' epilogues (HBM-bound stores) do not all coincide with each other
+    int stagger_blocks = 0, stagger_ticks = 0;
     // fused BN apply of the output (P 1, hkp_conv2d_fwd_f16_bn): out = [relu](y*s + t
     // [+ res | + res*rs + rt]) on the fp16-rounded y, bn_apply_f16's arithmetic
     const float* ep_ss = nullptr;          // [2K] scale | shift
@@ -1249,9 +1253,19 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
 // raise the register allocation of the one-tile kernels.  PAIR = two blocks per
 // CU (256x64 tiles, the stem: 80 KiB each): one block's prologue / epilogue
 // overlaps the other's main loop.
+// the first-round stagger of X3Args (one wave-uniform wait at block start)
+__device__ __forceinline__ void x3_stagger(const X3Args& a) {
+    const int b = blockIdx.x;
+    if (a.stagger_ticks > 0 && b < a.stagger_blocks && ((b >> 3) & 1)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)a.stagger_ticks) __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 template <int BN, bool STEM, bool PAIR, int MFD, bool SK, int P>
 __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[x3_lds_bytes(BN, PAIR, P) + x3_red_bytes(BN, PAIR)];
+    if constexpr (!SK) x3_stagger(a);
     x3_stamp(a, 0);
     const int G = gridDim.x, b = xcd_remap(blockIdx.x, G);
     if constexpr (!SK) {
@@ -2287,6 +2301,7 @@ static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Ar
 // a.RS, a.cch (128-B lines per pixel), a.M ... set by the caller; P = operand
 // layout (3 packed f16x3 split, 1 plain fp16)
 static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
+static int g_x3_stagger_ns = 0;                        // hkp_debug_x3_stagger
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -2315,6 +2330,8 @@ static void x3_dispatch_p(int P, F&& f) {
 static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
                       int64_t ws_bytes = 0) {
     a.stamps = g_x3_stamps;
+    a.stagger_ticks = g_x3_stagger_ns / 10;
+    a.stagger_blocks = x3_cus();
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
     const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_level(x3_halo_ok(a, k), a.cch, P));
@@ -2787,4 +2804,8 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
 // done, fp16 tile staged, stores issued; 0 where a body records none); NULL
 // turns it off.  Not thread-safe; for tools/ only.
 extern "C" void hkp_debug_x3_stamps(uint64_t* buf) { g_x3_stamps = (unsigned long long*)buf; }
+
+// Debug / tuning (tools/ only, not thread-safe): the first-round stagger of the
+// one-tile forward conv launches, in ns (0 = off; X3Args::stagger_ticks).
+extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns : 0; }
 

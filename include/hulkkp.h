@@ -205,6 +205,10 @@ int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_
  * (start, pipeline filled, K loop done, BN partials done, output staged, stores
  * issued); NULL turns it off. */
 void hkp_debug_x3_stamps(uint64_t* buf);
+/* Debug / tuning (tools/ only, not thread-safe): one-tile forward conv launches
+ * hold half the CUs of every XCD back for ns nanoseconds in their first round of
+ * blocks (0 = off), so the rounds' epilogues do not all coincide. */
+void hkp_debug_x3_stagger(int32_t ns);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
