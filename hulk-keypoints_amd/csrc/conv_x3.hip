@@ -63,6 +63,12 @@ namespace hkp {
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __attribute__((aligned(256))) uint4 g_x3_zero_line[8];   // 128 B of zeros (static, zero-initialised)
+// 128 B of all-ones bytes: a NaN in fp32 and in fp16.  The halo body's
+// out-of-image lines when it applies the input's BN itself (X3Args::in_ss):
+// relu(NaN * s + t) = 0 for any s, t, as a zero-padded post-ReLU input.
+__device__ __attribute__((aligned(256))) uint4 g_x3_nan_line[8] = {
+    {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u},
+    {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}};
 
 struct X3Args {
     const _Float16* xs;
@@ -98,6 +104,10 @@ struct X3Args {
     const _Float16* ep_res = nullptr;      // residual [M][K] fp16, nullable
     const float* ep_rss = nullptr;         // residual scale | shift [2K], nullable (raw residual)
     int ep_relu = 0;
+    // fused input BN (the halo body, inference): xs is the producer conv's raw
+    // NHWC output (fp32 for P 3, fp16 for P 1) and the A operand is
+    // relu(x * s + t) — bn_apply's arithmetic — split into hi | lo (P 3) in LDS
+    const float* in_ss = nullptr;          // [2C] scale | shift
 };
 
 // debug phase stamps (s_memrealtime, 100 MHz) of one-tile conv blocks: slot k of
@@ -183,6 +193,13 @@ constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
     return P == 1 && 256 * (BN + 8) * 2 > x3_nst(BN, PAIR) * (256 + BN) * 128 ? 256 * (BN + 8) * 2
                                                                               : x3_nst(BN, PAIR) * (256 + BN) * 128;
 }
+// A3 (conv_x3_a3_kernel): the 256x256 16x16x32 body with separate A and B rings —
+// A (the activation lines) 3 stages deep, so a stage's DMA has two K-steps to
+// land instead of one (the 1x1 convs of config C4 stream every A line from HBM),
+// B (the weights, L2-resident) 2 stages: 5 x 32 KiB = the whole 160 KiB; the
+// epilogue's scratch and column scales reuse the drained ring.
+constexpr int X3_A3_LDS = 5 * 256 * 128;
+
 // BN-partials scratch (x3_bn_partials_w: [2][WM][BN] floats) past the ring, so
 // the epilogue needs no barrier before it, then the tile's BN column scales
 // (loaded during the pipeline fill: a global load in the epilogue waited ~4 us
@@ -244,17 +261,31 @@ __device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char
     }
     __syncthreads();
     if (!*(volatile int*)flag_lds) return false;
-    // 8 loads in flight per chunk (the accumulators leave few free registers)
-    for (int sg = 0; sg < nseg; ++sg) {
-        const gf32x4* p = slab(b0 + sg);
+    // chunks of 8 slab vectors, double-buffered: the next chunk's 8 loads are in
+    // flight while this one is added (16 loads per thread outstanding: the fragment
+    // registers are dead here).  Summation order unchanged: per element, slab 0,
+    // then + slab 1, + slab 2, ... (the result does not depend on arrival order).
+    static_assert(NV4 % 8 == 0, "sk_combine chunks");
+    constexpr int NC = NV4 / 8;
+    const int total = nseg * NC;
+    f32x4 xa[8], xb[8];
+    auto load = [&](f32x4* x, int c) {
+        const gf32x4* p = slab(b0 + c / NC) + (c % NC) * 8 * 512 + tid;
 #pragma unroll
-        for (int v0 = 0; v0 < NV4; v0 += 8) {
-            f32x4 x[8];
+        for (int v = 0; v < 8; ++v) x[v] = p[v * 512];
+    };
+    auto add = [&](const f32x4* x, int c) {
+        const int sg = c / NC, v0 = (c % NC) * 8;
 #pragma unroll
-            for (int v = 0; v < 8; ++v) x[v] = p[(v0 + v) * 512 + tid];
-#pragma unroll
-            for (int v = 0; v < 8; ++v) set(v0 + v, sg == 0 ? x[v] : get(v0 + v) + x[v]);
-        }
+        for (int v = 0; v < 8; ++v) set(v0 + v, sg == 0 ? x[v] : get(v0 + v) + x[v]);
+    };
+    load(xa, 0);
+    for (int c = 0; c < total; c += 2) {
+        if (c + 1 < total) load(xb, c + 1);
+        add(xa, c);
+        if (c + 1 >= total) break;
+        if (c + 2 < total) load(xa, c + 2);
+        add(xb, c + 1);
     }
     return true;
 }
@@ -673,29 +704,35 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
 // wave's reads of t), barrier, [read A frags of t+1] then per column block j:
 // [MFMAs of t with B_j] [refill B_j with t+1's].  NST 2 (256x256; 256x64 pairs):
 // A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
-template <int BN, int NST, int STAGE, int GL, int P, typename Issue>
+template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, typename Issue, typename IssueA, typename IssueB>
 __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
-                                                  Issue& issue_next) {
+                                                  Issue& issue_next, IssueA& issue_a, IssueB& issue_b) {
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
     constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
-    constexpr int RED_OFF = PAIRB ? 0 : x3_lds_bytes(BN, PAIRB, P);
-    float* const scl = (float*)(smem + RED_OFF + 2 * 4 * BN * 4);   // [BN] column scales (!PAIRB)
+    static_assert(!A3 || (BN == 256 && NST == 2), "A3: the 256x256 body");
+    // PAIRB and A3 have no LDS past the ring: the epilogue's scratch is the drained
+    // ring and the column scales are loaded in the epilogue
+    constexpr bool RINGSCR = PAIRB || A3;
+    constexpr int RED_OFF = RINGSCR ? 0 : x3_lds_bytes(BN, PAIRB, P);
+    constexpr int LDS_ALL = A3 ? X3_A3_LDS : x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB);
+    float* const scl = (float*)(smem + RED_OFF + 2 * 4 * BN * 4);   // [BN] column scales (!RINGSCR)
     float sclv = 1.f;                              // issued before the fill, stored after it
-    if constexpr (!PAIRB) {
+    if constexpr (!RINGSCR) {
         if (tid < BN) sclv = (a.wscale ? a.wscale[n0 + tid] : 1.f) * (a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f);
     }
     auto store_scl = [&]() {
-        if constexpr (!PAIRB) {
+        if constexpr (!RINGSCR) {
             if (tid < BN) scl[tid] = sclv;
         }
     };
     const int r16 = lane & 15, q = lane >> 4;
     const int sw = (r16 >> 1) & 7;                 // the DMA's swizzle of every row ≡ r16 (mod 16)
     const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
-    const int a_base = (wm * UM * 16) * ROW, b_base = (BM + wn * UN * 16) * ROW;
+    // A3: A stages at [0, 3*BM*ROW), B stages past them, each its own ring
+    const int a_base = (wm * UM * 16) * ROW, b_base = ((A3 ? 0 : BM) + wn * UN * 16) * ROW;
 
     f32x4 acc[UM][UN];
 #pragma unroll
@@ -740,7 +777,79 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);   // DMA pieces
         }
     };
-    if constexpr (NST == 2) {
+    // the same with NP DMA pieces in the step (A3: B only, or A and B)
+    auto sched_kstep_n = [&](auto np) {
+        constexpr int NP = decltype(np)::value;
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+            if (NP > 0 && j * ((NP + UN - 1) / UN) < NP)
+                __builtin_amdgcn_sched_group_barrier(0x020, (NP + UN - 1) / UN, 0);
+        }
+    };
+    if constexpr (A3) {
+        // A3: the NST 2 schedule below with A one stage further ahead.  Issue order
+        // per K-step t (after its barrier): B(t+2) into B's slot of t, then A(t+3)
+        // into A's slot of t (both read into registers during step t-1); so at step
+        // t's top, waiting until only A(t+2) is in flight (vmcnt GA) retires A(t+1)
+        // and B(t+1).  Prologue order A0 B0 A1 B1 A2.
+        constexpr int GB = GL - GA;
+        const char* const bring = smem + 3 * BM * ROW;
+        issue_a();
+        issue_b();
+        if (nks > 1) {
+            issue_a();
+            issue_b();
+        }
+        if (nks > 2) issue_a();
+        if (nks > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + GA) : "memory");
+        else if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        lds_barrier();
+        x3_stamp(a, 1);
+        FA fa;
+        read_a(fa, smem);
+#pragma unroll
+        for (int j = 0; j < UN; ++j) read_b(j, bring);
+        int ca = 0, cb = 0;
+        // one K-step: NP DMA pieces issued (GL: B(t+2) and A(t+3); GB: B only; 0),
+        // WA: A(t+2) may stay in flight at the top
+        auto kstep = [&](auto np, auto wa) {
+            constexpr int NP = decltype(np)::value;
+            if constexpr (decltype(wa)::value) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+            ca = ca == 2 ? 0 : ca + 1;
+            cb ^= 1;
+            const char* sta = smem + ca * (BM * ROW);
+            const char* stb = bring + cb * (BN * ROW);
+            if constexpr (NP > 0) issue_b();
+            if constexpr (NP == GL) issue_a();
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                mma_col(fa, j);
+                read_b(j, stb);
+            }
+            read_a(fa, sta);
+            sched_kstep_n(np);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);      // next A frags
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        using IGL = std::integral_constant<int, GL>;
+        using IGB = std::integral_constant<int, GB>;
+        using I0 = std::integral_constant<int, 0>;
+        int t = 0;
+        for (; t + 3 < nks; ++t) kstep(IGL{}, std::true_type{});
+        if (t + 2 < nks) {
+            kstep(IGB{}, std::true_type{});
+            ++t;
+        }
+        if (t + 1 < nks) kstep(I0{}, std::false_type{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < UN; ++j) mma_col(fa, j);
+    } else if constexpr (NST == 2) {
         // 2-stage ring (256x256 tiles; 256x64 at two blocks per CU), A single-buffered
         // (registers: 128 acc + 32 A + 64 B): per K-step t — wait own DMA of t+1,
         // barrier, then per column j [MFMAs of t with B_j] [refill B_j with t+1's]
@@ -839,9 +948,9 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     }
     const int rbase = m0 + wm * UM * 16 + 4 * q;
     // column scale (weight scale x gradient scale): the prefetched LDS copy, or
-    // (PAIRB) loaded now
+    // (PAIRB, A3) loaded now
     auto col_scale = [&](int c) -> float {
-        if constexpr (PAIRB) return (a.wscale ? a.wscale[n0 + c] : 1.f) * (a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f);
+        if constexpr (RINGSCR) return (a.wscale ? a.wscale[n0 + c] : 1.f) * (a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f);
         else return scl[c];
     };
     if constexpr (P == 1) {                // fp16 output: partials, scale, LDS-staged store
@@ -849,7 +958,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
         for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
         if (a.part) {
-            if constexpr (PAIRB) lds_sync();           // the scratch is the ring
+            if constexpr (RINGSCR) lds_sync();         // the scratch is the ring
             x3_bn_partials_w<BN, UM, UN, 16, 16>(
                 a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
                 [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
@@ -862,7 +971,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         _Float16* t = (_Float16*)smem;
         constexpr int PITCH = BN + 8;
         constexpr int SS_OFF = 256 * PITCH * 2;
-        static_assert(SS_OFF + 4 * BN * 4 <= x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB), "epilogue LDS");
+        static_assert(SS_OFF + 4 * BN * 4 <= LDS_ALL, "epilogue LDS");
 #pragma unroll
         for (int i = 0; i < UM; ++i)
 #pragma unroll
@@ -884,7 +993,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
     for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
     if (a.part) {
-        if constexpr (PAIRB) lds_sync();               // the scratch is the ring
+        if constexpr (RINGSCR) lds_sync();             // the scratch is the ring
         x3_bn_partials_w<BN, UM, UN, 16, 16>(
             a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
             [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
@@ -901,7 +1010,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         // completion instead of ending and letting the next block start.
         // 256-wide tiles stage half the rows per pass (128 KiB).
         constexpr int PASSES = BN == 256 ? 2 : 1, RPP = 256 / PASSES, PITCH = BN + 4, C4 = BN / 4;
-        static_assert(RPP * PITCH * 4 <= x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB), "staging");
+        static_assert(RPP * PITCH * 4 <= LDS_ALL, "staging");
         float* t = (float*)smem;
         lds_sync();                                    // every wave done with the ring and the partials' scratch
 #pragma unroll
@@ -958,7 +1067,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-template <int BN, bool STEM, bool PAIR, int MFD, int P>
+template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -975,6 +1084,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(P == 3 || ((P == 1 || P == 2 || P == 4) && !STEM), "bad conv_x3 operand layout");
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
+    static_assert(!A3 || (BN == 256 && !STEM && !PAIR && MFD == 16), "A3: the 256x256 16x16x32 body");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
@@ -1066,9 +1176,46 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         }
     };
 
+    // A3: A and B stages in rings of their own (3 and 2 deep), A issued one K-step
+    // ahead of B — each with its own (channel group, tap) position
+    int qa_buf = 0, qa_cc = q_cc, qa_tap = q_tap, qa_rr = q_rr, qa_ss = q_ss;
+    int qb_buf = 0, qb_cc = q_cc, qb_tap = q_tap;
+    auto issue_a = [&]() {
+        char* st = smem + qa_buf * (BM * ROW);
+        const int dh = qa_rr * a.dil, dw = qa_ss * a.dil;
+        const long toff = ((long)dh * a.W + dw) * cstride + qa_cc * 64;
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+            const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+            glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+        }
+        qa_buf = qa_buf == 2 ? 0 : qa_buf + 1;
+        if (++qa_ss == a.S) {
+            qa_ss = 0;
+            ++qa_rr;
+        }
+        if (++qa_tap == a.RS) {
+            qa_tap = 0;
+            qa_rr = 0;
+            ++qa_cc;
+        }
+    };
+    auto issue_b = [&]() {
+        char* st = smem + 3 * (BM * ROW) + qb_buf * (BN * ROW) - BM * ROW;   // b_dst counts from row BM
+        const int boff = (qb_tap * a.cch + qb_cc) * 64;
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16(a.ws + (unsigned)(b_off[j] + boff), st + b_dst[j]);
+        qb_buf ^= 1;
+        if (++qb_tap == a.RS) {
+            qb_tap = 0;
+            ++qb_cc;
+        }
+    };
+
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL, P>(a, smem, tile, nks, partial, m0, n0, wm, wn, lane, tid,
-                                                 issue_next);
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, nks, partial, m0, n0, wm, wn, lane, tid,
+                                                         issue_next, issue_a, issue_b);
         return;
     } else {
     f32x16 acc[TM][TN];
@@ -1286,6 +1433,15 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
     }
 }
 
+// One 256x256 tile per block on the A3 body (3-stage A ring, 2-stage B ring).
+template <int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
+    x3_stagger(a);
+    x3_stamp(a, 0);
+    conv_x3_tile<256, false, false, 16, P, true>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
+}
+
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
 // each cut into S equal K segments — one block per segment, a single round —
 // summed by the tile's last-arriving segment in segment order (sk_combine; the
@@ -1338,12 +1494,68 @@ static bool halo_shape(int stride, int r, int s, int pad, int dil, int ho, int w
            k % 64 == 0;
 }
 
-template <int P>
-__global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
+// BNIN: the input is the producer's raw output and its BN + ReLU (+ the f16x3
+// split, P 3) is applied to each channel group's halo image in LDS after it
+// lands (X3Args::in_ss) — the bn_apply pass between the two convs disappears.
+// Each lane transforms whole 8-channel pieces: P 3 reads the piece's two fp32
+// chunks and writes its hi and lo chunks in place (the four pieces of a line are
+// four adjacent lanes of one wave instruction, so every read of the line precedes
+// its writes); P 1 rewrites one fp16 chunk.  Out-of-image lines are NaN lines
+// (relu(NaN*s + t) = 0).
+template <int P, bool BNIN>
+__device__ __forceinline__ void x3_halo_bnin(const X3Args& a, char* smem, int g, int tid) {
+    constexpr int ROW = 128;
+    constexpr int PIECES = P == 1 ? 8 : 4;                       // 8-channel pieces per line
+    constexpr int LPI = 512 / PIECES;                            // lines per block-wide pass
+    constexpr int NL = 8 * HALO_GA * 8;                          // halo lines incl. the dummies (384)
+    const int j = tid % PIECES;
+    const int c0 = g * (P == 1 ? 64 : 32) + 8 * j;
+    float sa[8], sb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sa[e] = a.in_ss[c0 + e];
+        sb[e] = a.in_ss[a.C + c0 + e];
+    }
+#pragma unroll
+    for (int L0 = 0; L0 < NL; L0 += LPI) {
+        const int L = L0 + tid / PIECES;
+        const int sw = (L >> 1) & 7;
+        char* line = smem + L * ROW;
+        if constexpr (P == 1) {
+            f16x8* ch = (f16x8*)(line + ((j ^ sw) << 4));
+            const f16x8 v = *ch;
+            f16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float x = __fadd_rn(__fmul_rn((float)v[e], sa[e]), sb[e]);
+                o[e] = (_Float16)(x > 0.f ? x : 0.f);
+            }
+            *ch = o;
+        } else {
+            const f32x4 v0 = *(const f32x4*)(line + (((2 * j) ^ sw) << 4));
+            const f32x4 v1 = *(const f32x4*)(line + (((2 * j + 1) ^ sw) << 4));
+            f16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float y = e < 4 ? v0[e] : v1[e - 4];
+                float x = __fadd_rn(__fmul_rn(y, sa[e]), sb[e]);
+                x = x > 0.f ? x : 0.f;
+                const _Float16 hv = (_Float16)x;
+                h[e] = hv;
+                l[e] = (_Float16)(x - (float)hv);
+            }
+            *(f16x8*)(line + ((j ^ sw) << 4)) = h;
+            *(f16x8*)(line + (((4 + j) ^ sw) << 4)) = l;
+        }
+    }
+}
+
+template <int P, bool BNIN>
+__device__ __forceinline__ void conv_x3_halo_body(const X3Args& a, char* smem) {
     constexpr int BM = 256, BN = 64, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);     // 4 x 2 16x16 sub-tiles per wave
-    __shared__ __attribute__((aligned(1024))) char smem[HALO_LDS];
     static_assert(256 * (BN + 4) * 4 <= HALO_LDS && 8 * BN * 4 <= HALO_LDS, "epilogue staging");
+    static_assert(!BNIN || P == 3 || P == 1, "fused input BN: f16x3 or plain fp16");
 
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
@@ -1356,7 +1568,7 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
     const int wm = w / WN, wn = w % WN;
     const int cstride = a.cch * 64;                             // halves per pixel
     const int nks = a.nks;                                      // 9 taps x channel groups
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    const _Float16* zero = (const _Float16*)(BNIN ? g_x3_nan_line : g_x3_zero_line);
 
     // ---- halo DMA: instruction i of wave w fills lines 8 (w*GA + i) .. +7 ----
     unsigned h_off[HALO_GA];                                    // element offsets from a.xs (or ~0u: zero line)
@@ -1418,6 +1630,10 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
     if (nks > 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
+    if constexpr (BNIN) {
+        x3_halo_bnin<P, BNIN>(a, smem, 0, tid);
+        lds_sync();
+    }
     for (int t = 0; t < nks; ++t) {
         const int g = t / 9, u = t - g * 9;
         const int toff = (u / 3) * HALO_LW + (u - (u / 3) * 3);
@@ -1451,6 +1667,11 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
             lds_barrier();
             issue_halo(g + 1);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if constexpr (BNIN) {
+                lds_barrier();                                   // the whole halo landed
+                x3_halo_bnin<P, BNIN>(a, smem, g + 1, tid);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
         } else if (t + 2 < nks) {
             asm volatile("s_waitcnt vmcnt(1)" ::: "memory");     // stage t+1 landed, t+2 in flight
         } else {
@@ -1513,6 +1734,19 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
             *(f32x4*)(a.y + off) = v;
         }
     }
+}
+
+template <int P>
+__global__ __launch_bounds__(512, 2) void conv_x3_halo_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[HALO_LDS];
+    conv_x3_halo_body<P, false>(a, smem);
+}
+
+// the same with the input's BN + ReLU applied to each halo image (X3Args::in_ss)
+template <int P>
+__global__ __launch_bounds__(512, 2) void conv_x3_halo_bnin_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[HALO_LDS];
+    conv_x3_halo_body<P, true>(a, smem);
 }
 
 // ---------------------------------------------------------------------------
@@ -2236,6 +2470,7 @@ struct X3Choice {
     int bn, mfd;
     bool pair, sk;
     bool halo = false;                 // conv_x3_halo_kernel<P>
+    bool a3 = false;                   // conv_x3_a3_kernel<P> (256x256, 3-stage A ring)
 };
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
@@ -2243,7 +2478,7 @@ struct X3Choice {
 static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo = 0) {
     // the halo-tile body wherever the shape allows it, unless a tile body is forced
     if ((halo >= 1 && policy == HKP_TILE_HALO) ||
-        (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))) {
+        (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3))) {
         X3Choice c{64, 16, true, false};
         c.halo = true;
         return c;
@@ -2263,10 +2498,13 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
         case HKP_TILE_256_TAIL:            // 256x256, the partial last round as split-K segments
             if (k % 256 == 0) return {256, 16, false, false};
             break;
+        case HKP_TILE_256_A3:              // the same on the A3 body
+            if (k % 256 == 0) return {256, 16, false, false, false, true};
+            break;
         default:
             break;
     }
-    const bool sk = sk_ok && policy != HKP_TILE_NO_SK && policy != HKP_TILE_256_TAIL;
+    const bool sk = sk_ok && policy != HKP_TILE_NO_SK && policy != HKP_TILE_256_TAIL && policy != HKP_TILE_256_A3;
     const X3Plan pl = x3_plan(k, m_tiles, nks, sk, policy == HKP_TILE_SK ? 0.0 : sk_over(nks));
     if (pl.sk) return {pl.bn, pl.bn == 128 ? 16 : 32, false, true};
     if (pl.bn == 256) return {256, 16, false, false};
@@ -2278,13 +2516,16 @@ static const X3Choice X3_STEM{64, 16, true, false};
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
+    if (c.a3) return snprintf(buf, len, "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
 
 template <int P>
 static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Args& a) {
-    if (c.sk && c.bn == 128)
+    if (c.a3)
+        hipLaunchKernelGGL(conv_x3_a3_kernel<P>, grid, dim3(512), 0, st, a);
+    else if (c.sk && c.bn == 128)
         hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 16, true, P>), grid, dim3(512), 0, st, a);
     else if (c.sk)
         hipLaunchKernelGGL((conv_x3_kernel<64, false, false, 32, true, P>), grid, dim3(512), 0, st, a);
@@ -2340,7 +2581,12 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.sk_units = 0;
     if (c.halo) {
         const dim3 gh((unsigned)(m_tiles * a.n_tiles));
-        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL(conv_x3_halo_kernel<pc.value>, gh, dim3(512), 0, st, a); });
+        if (a.in_ss) {
+            if (P == 3) hipLaunchKernelGGL(conv_x3_halo_bnin_kernel<3>, gh, dim3(512), 0, st, a);
+            else hipLaunchKernelGGL(conv_x3_halo_bnin_kernel<1>, gh, dim3(512), 0, st, a);
+        } else {
+            x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL(conv_x3_halo_kernel<pc.value>, gh, dim3(512), 0, st, a); });
+        }
         return;
     }
     dim3 grid((unsigned)(m_tiles * a.n_tiles));
@@ -2359,7 +2605,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     const long rm = tiles / G * G / a.n_tiles;              // m-tiles of the full rounds
     const long tm = m_tiles - rm;
     long NG = (!c.sk && c.bn == 256 && sk_ok &&
-               (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL))
+               (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3))
                   ? x3_tail_groups(m_tiles, a.n_tiles, nks) : 0;
     // one round, every group non-empty and inside two tiles, slabs and counters in the workspace
     if (NG > 0 && !(tm > 0 && NG * a.n_tiles <= G && tm * nks >= NG && tm < NG &&
@@ -2416,7 +2662,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_HALO, "%s: unknown tile policy %d", who, d->tile);
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_256_A3, "%s: unknown tile policy %d", who, d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8,
                   "%s: tile policy %d is retired (the persistent conv, measured slower)", who, d->tile);
     return HKP_OK;
@@ -2446,10 +2692,19 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.cch = d->c / cg; a.RS = d->r * d->s;
+    int policy = d->tile;
     if (ep) {
         a.ep_ss = ep->ep_ss; a.ep_res = ep->ep_res; a.ep_rss = ep->ep_rss; a.ep_relu = ep->ep_relu;
+        a.in_ss = ep->in_ss;
     }
-    launch_x3(d->k, (M + 255) / 256, d->tile, P, as_stream(stream), a, sk_ws, sk_bytes);
+    if (a.in_ss) {                         // the fused input BN runs on the halo-tile body only
+        HKP_CHECK_ARG(P == 3 || P == 1, "%s: fused input BN needs f16x3 or plain fp16", who);
+        HKP_CHECK_ARG(x3_halo_ok(a, d->k) && (d->tile == HKP_TILE_AUTO || d->tile == HKP_TILE_HALO),
+                      "%s: the fused input BN needs the halo-tile shape (stride-1 3x3, pad = dil = 1, Ho %% 8 == 0, "
+                      "Wo %% 32 == 0, Cout %% 64 == 0)", who);
+        policy = HKP_TILE_HALO;
+    }
+    launch_x3(d->k, (M + 255) / 256, policy, P, as_stream(stream), a, sk_ws, sk_bytes);
     HKP_LAUNCH_CHECK(who);
     return HKP_OK;
 }
@@ -2460,6 +2715,26 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
     HKP_CHECK_ARG(d && y, "hkp_conv2d_fwd_x3: null argument");
     return conv_fwd_x3_common(d, x_split, w_split, w_inv_scale, y, nullptr, stat_partials, sk_workspace, sk_ws_bytes,
                               3, stream, "hkp_conv2d_fwd_x3");
+}
+
+extern "C" int hkp_conv2d_fwd_x3_bnin(const hkp_conv_desc* d, const float* x_raw, const float* in_scale_shift,
+                                      const uint16_t* w_split, const float* w_inv_scale, float* y, float* stat_partials,
+                                      hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && y && x_raw && in_scale_shift, "hkp_conv2d_fwd_x3_bnin: null argument");
+    X3Args ep;
+    ep.in_ss = in_scale_shift;
+    return conv_fwd_x3_common(d, (const uint16_t*)x_raw, w_split, w_inv_scale, y, nullptr, stat_partials, nullptr, 0, 3,
+                              stream, "hkp_conv2d_fwd_x3_bnin", &ep);
+}
+
+extern "C" int hkp_conv2d_fwd_f16_bnin(const hkp_conv_desc* d, const uint16_t* x_raw_f16, const float* in_scale_shift,
+                                       const uint16_t* w_f16, const float* w_inv_scale, uint16_t* y_f16,
+                                       float* stat_partials, hkp_stream_t stream) {
+    HKP_CHECK_ARG(d && y_f16 && x_raw_f16 && in_scale_shift, "hkp_conv2d_fwd_f16_bnin: null argument");
+    X3Args ep;
+    ep.in_ss = in_scale_shift;
+    return conv_fwd_x3_common(d, x_raw_f16, w_f16, w_inv_scale, nullptr, y_f16, stat_partials, nullptr, 0, 1, stream,
+                              "hkp_conv2d_fwd_f16_bnin", &ep);
 }
 
 extern "C" int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,

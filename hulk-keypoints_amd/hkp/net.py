@@ -215,6 +215,10 @@ def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
     needs the fp32 activation."""
     passes = pol.passes
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
+    if isinstance(x, _PendingBN):
+        wp = _pack_weight_x3(conv.weight) if x.y.dtype == torch.float32 else \
+            _cached_split(conv.weight, "f16", ops.weight_pack_f16)
+        return ops.conv2d_fwd_bnin(x.y, x.ss, wp, st, pd, dl, stats=bn.training)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
     if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd,
@@ -232,6 +236,28 @@ def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
         raise ops.HkpError("conv %s under precision %r: no LDS-DMA kernel for this shape and no fp32 input "
                            "for the fp32 kernel" % (tuple(conv.weight.shape), pol.precision))
     return ops.conv2d_fwd(x, conv.weight, st, pd, dl, layout=layout, stats=bn.training)
+
+
+class _PendingBN:
+    """A conv's raw output whose BN + ReLU its one consumer conv applies itself
+    (ops.conv2d_fwd_bnin): inference only, never a tensor of the network."""
+
+    def __init__(self, y, ss):
+        self.y, self.ss = y, ss
+
+
+def _bnin_ok(conv, y, pol):
+    """The consumer conv takes its input's BN + ReLU (the halo-tile shape; the
+    full f16x3 or plain fp16 arithmetic)."""
+    if not pol.fuse_input_bn:
+        return False
+    if not ((y.dtype == torch.float32 and pol.passes == 3 and pol.products == 3) or
+            (y.dtype == torch.float16 and pol.passes == 1)):
+        return False
+    k, r, s, c = conv.weight.shape
+    n, h, w, _ = y.shape
+    return c == y.shape[-1] and ops.bnin_shape_ok(n, h, w, c, k, r, s, _i(conv.stride), _i(conv.padding),
+                                                  _i(conv.dilation))
 
 
 def _f16_conv_ok(conv):
@@ -334,7 +360,10 @@ def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_c
         if i == len(convs) - 1:
             break
         y, s, m = conv_bn(conv, bn, a, pol)
-        a = act(y, s, convs[i + 1])
+        if rec is None and _bnin_ok(convs[i + 1], y, pol):
+            a = _PendingBN(y, s)                      # the next conv applies bn + ReLU itself
+        else:
+            a = act(y, s, convs[i + 1])
         ys.append(y), sss.append(s), mis.append(m), acts.append(a)
     if rec is None and head is None and not final and _gram_fusable(block, a, pol):
         return _bottleneck_tail_gram(block, x, a, pol)

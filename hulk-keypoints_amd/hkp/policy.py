@@ -56,6 +56,10 @@ class Policy:
     # plain fp16 inference (C4): a Bottleneck's bn3 statistics from conv3's input
     # covariance (1x1 conv: exact), bn3 + residual + ReLU in conv3's epilogue
     gram_bn: bool = True
+    # inference: a block's inner BN + ReLU applied inside the next conv where that
+    # conv runs the halo-tile body (hkp_conv2d_fwd_x3_bnin / _f16_bnin: layer1's
+    # 3x3 convs at 640x480) instead of a separate apply pass
+    fuse_input_bn: bool = True
 
     def __post_init__(self):
         if self.precision not in PRECISIONS:

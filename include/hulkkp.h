@@ -79,6 +79,8 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_HALO 10              /* 8x32-pixel halo tiles (stride-1 3x3, pad = dil = 1, Ho%8 = Wo%32 = 0;
                                          the default there under AUTO and 256_TAIL when the
                                          input has 64 channels) */
+#define HKP_TILE_256_A3 11            /* 256x256 on the A3 body (A ring 3 stages deep, B ring 2: an A
+                                         line has two K-steps to land) + the split-K tail of 9 */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);
@@ -137,6 +139,25 @@ int64_t hkp_conv_x3_sk_workspace_bytes(void);
 int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
                                const float* w_inv_scale, int32_t products, float* y, float* stat_partials,
                                void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream);
+/* Inference: hkp_conv2d_fwd_x3 whose input is the producer conv's raw output,
+ * with the producer's train-mode BN + ReLU applied in the conv itself — the
+ * bn_apply pass between a BasicBlock's / Bottleneck's inner convs
+ * (src/resnet.py:46-48 / 80-86: relu(bn1(conv1 x)) feeding conv2) disappears.
+ * x_raw: fp32 NHWC [n][h][w][c]; in_scale_shift: [2c] scale | shift from
+ * hkp_bn_finalize (or hkp_bn_finalize_ranks) of that output; the A operand is
+ * relu(x * scale + shift) with bn_apply's arithmetic (two roundings), split as
+ * hkp_bn_apply(split = 3) would write it — so y is bit-identical to hkp_bn_apply
+ * followed by hkp_conv2d_fwd_x3.  Runs on the halo-tile body only (stride-1
+ * 3x3, pad = dil = 1, Ho % 8 == 0, Wo % 32 == 0; d->tile AUTO or HALO; no
+ * stream-K workspace); other shapes return HKP_ERR_BAD_ARG. */
+int hkp_conv2d_fwd_x3_bnin(const hkp_conv_desc* d, const float* x_raw, const float* in_scale_shift,
+                           const uint16_t* w_split, const float* w_inv_scale, float* y, float* stat_partials,
+                           hkp_stream_t stream);
+/* The plain-fp16 form (config C4): x_raw_f16 is the producer's fp16 output,
+ * relu(x * scale + shift) rounded to fp16 as hkp_bn_apply_f16 writes it. */
+int hkp_conv2d_fwd_f16_bnin(const hkp_conv_desc* d, const uint16_t* x_raw_f16, const float* in_scale_shift,
+                            const uint16_t* w_f16, const float* w_inv_scale, uint16_t* y_f16, float* stat_partials,
+                            hkp_stream_t stream);
 /* Plain-fp16 conv (BASELINE config C4, "fp16 with MFMA"): the same LDS-DMA
  * kernel family as hkp_conv2d_fwd_x3 with one fp16 product per MAC (fp32
  * accumulation).  x_f16: NHWC fp16 [n][h][w][c] (a producer's split_passes = 1

@@ -8,7 +8,7 @@ import torch.nn.functional as F
 from oracle import cpu_ref, recipe
 
 # every live HKP_TILE_* policy past AUTO (7 and 8 are retired)
-LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10)
+LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11)
 
 pytestmark = pytest.mark.gpu
 
@@ -448,7 +448,7 @@ BODY_CASES = [
 
 
 @pytest.mark.parametrize("case", BODY_CASES)
-@pytest.mark.parametrize("tile", [3, 4, 5, 6, 9, 10])
+@pytest.mark.parametrize("tile", [3, 4, 5, 6, 9, 10, 11])
 def test_x3_tile_bodies_dgrad(cuda_device, case, tile):
     """Every kernel body (256x256 / 256x128 16x16x32 / 256x128 32x32x16 / 256x64
     pairs) on the forward and the stride-1 dgrad with a residual addend:
@@ -698,3 +698,79 @@ def test_x3_product_subsets(cuda_device, case, products):
         yv, pv = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile, products=products)
         assert (yv.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() < 2e-6 * scale, tile
 
+
+
+BNIN_CASES = [
+    (2, 16, 64, 64, 64),        # 2 channel groups (f16x3) / 1 (fp16), 2 x 2 patches per image
+    (1, 24, 96, 128, 128),      # 4 / 2 channel groups, 2 column tiles
+    (1, 8, 32, 32, 64),         # one patch, one f16x3 channel group
+]
+
+
+@pytest.mark.parametrize("case", BNIN_CASES)
+@pytest.mark.parametrize("prec", ["f16x3", "f16"])
+def test_fused_input_bn_equals_apply_then_conv(cuda_device, case, prec):
+    """hkp_conv2d_fwd_x3_bnin / _f16_bnin (the halo body applying its input's BN +
+    ReLU to each halo image in LDS, out-of-image lines as NaN lines) == bn_apply /
+    bn_apply_f16 followed by the halo conv: the same y and BN partials, bit for bit.
+    Scale / shift include negative scales and large shifts (the NaN padding must
+    give 0 whatever their sign)."""
+    from hkp import ops
+    n, h, w, c, k = case
+    if prec == "f16" and c % 64:
+        pytest.skip("plain fp16 needs Cin % 64")
+    d = cuda_device
+    y = (rand(n, h, w, c, seed=91) * 3 + 1).to(d)
+    ss = torch.cat([rand(c, seed=92) * 0.7, rand(c, seed=93) * 2.0]).to(d)     # mixed signs
+    wt = rand(k, 3, 3, c, seed=94, scale=(2.0 / (9 * k)) ** 0.5).to(d)
+    if prec == "f16x3":
+        wp = ops.weight_pack_x3(wt)
+        a = ops.bn_apply(y, ss, relu=True, split=3, keep_fp32=False)
+        ref, pref = ops.conv2d_fwd_x3(a, wp, 1, 1, 1, tile=10)                 # the halo body
+        got, pgot = ops.conv2d_fwd_bnin(y, ss, wp, 1, 1, 1)
+    else:
+        wp = ops.weight_pack_f16(wt)
+        y16 = y.half()
+        a = ops.bn_apply_f16(y16, ss, relu=True)
+        ref, pref = ops.conv2d_fwd_f16(a, wp, 1, 1, 1, tile=10)
+        got, pgot = ops.conv2d_fwd_bnin(y16, ss, wp, 1, 1, 1)
+    assert got.dtype == ref.dtype and torch.equal(got, ref)
+    assert torch.equal(pgot, pref)
+    _, pnone = ops.conv2d_fwd_bnin(y if prec == "f16x3" else y.half(), ss, wp, 1, 1, 1, stats=False)
+    assert pnone is None
+
+
+def test_fused_input_bn_rejects_other_shapes(cuda_device):
+    from hkp import ops
+    d = cuda_device
+    y = rand(1, 12, 32, 64, seed=95).to(d)                  # Ho % 8 != 0: no halo tiling
+    ss = torch.cat([torch.ones(64), torch.zeros(64)]).to(d)
+    wp = ops.weight_pack_x3(rand(64, 3, 3, 64, seed=96, scale=0.05).to(d))
+    with pytest.raises(ops.HkpError, match="halo"):
+        ops.conv2d_fwd_bnin(y, ss, wp, 1, 1, 1)
+
+
+@pytest.mark.parametrize("bb,prec", [("resnet18", "f16x3"), ("resnet50", "f16")])
+def test_fused_input_bn_network_bitexact(cuda_device, bb, prec):
+    """Whole inference forward at a halo-tiled layer1 (128x256 input: layer1 at
+    32x64): Policy.fuse_input_bn on == off, heatmaps and argmax bit for bit, and the
+    fused kernel ran."""
+    from hkp import net, ops
+    m = _model(bb, 4, 7, cuda_device, precision=prec)
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(2, 128, 256, 8)).to(cuda_device)
+    syms = set()
+
+    def observe(sym, flops, nbytes, launch):
+        syms.add(sym)
+        launch()
+    outs = []
+    for fuse in (True, False):
+        ops.set_observer(observe if fuse else None)
+        try:
+            with torch.no_grad():
+                hm, yx = m.heatmaps_and_keypoints(x, policy=m.policy.with_(fuse_input_bn=fuse))
+        finally:
+            ops.set_observer(None)
+        outs.append((hm, yx))
+    assert any(s.startswith("conv_x3_halo_bnin_kernel") for s in syms), syms
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
