@@ -162,6 +162,15 @@ def _nospace(s):
     return s.replace(" ", "")
 
 
+def _tail_of(kernel_sym):
+    """The split-K tail kernel a 256x256 one-tile conv launch ends in (its last,
+    partly filled round), as a rocprof name fragment, or None."""
+    if not kernel_sym.startswith(("conv_x3_kernel<256,", "conv_x3_a3_kernel<")):
+        return None
+    p = _nospace(kernel_sym).rstrip(">").split(",")[-1].split("<")[-1]      # the operand layout P
+    return "::conv_x3_tail_kernel<256,%s>(" % p
+
+
 def pmc_traffic(kernel_sym, tag):
     """HBM bytes per launch of `kernel_sym` from the newest committed rocprofv3 PMC
     summary (profiles/*<tag>*pmc*.json, separate FETCH_SIZE / WRITE_SIZE passes):
@@ -176,9 +185,7 @@ def pmc_traffic(kernel_sym, tag):
     no summary has the kernel."""
     import glob
     want = "::" + _nospace(kernel_sym) + "("
-    tail_want = None
-    if kernel_sym.startswith("conv_x3_kernel<256,"):
-        tail_want = "::conv_x3_tail_kernel<256,%s>(" % _nospace(kernel_sym).rstrip(">").split(",")[-1]
+    tail_want = _tail_of(kernel_sym)
     paths = glob.glob(os.path.join(REPO, "profiles", "*%s*pmc*.json" % tag))
     for path in sorted(paths, reverse=True):       # rNN_..._vNN names: newest round / version first
         try:
@@ -210,9 +217,7 @@ def trace_avg_ms(kernel_sym, tag):
     import csv
     import glob
     want = "::" + _nospace(kernel_sym) + "("
-    tail_want = None
-    if kernel_sym.startswith("conv_x3_kernel<256,"):
-        tail_want = "::conv_x3_tail_kernel<256,%s>(" % _nospace(kernel_sym).rstrip(">").split(",")[-1]
+    tail_want = _tail_of(kernel_sym)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*%s*kernel_stats*.csv" % tag)), reverse=True):
         try:
             rows = list(csv.DictReader(open(path)))
@@ -409,7 +414,7 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     # dominant kernel = the conv symbol with the most event-timed time
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
     alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
-    if dom_sym.startswith(("conv_x3_kernel", "conv_x3_halo_kernel", "wgrad_x3_kernel")):
+    if dom_sym.startswith(("conv_x3_kernel", "conv_x3_a3_kernel", "conv_x3_halo_kernel", "wgrad_x3_kernel")):
         # the x3 LDS-DMA kernels: fp16 MFMAs per fp32 MAC — 3 (f16x3), 2 (f16x2w / f16x2a: two of
         # the three products), 1 (f16)
         passes = {"f16x3": 3, "f16x2w": 2, "f16x2a": 2}.get(precision, 1)

@@ -2475,7 +2475,18 @@ struct X3Choice {
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
 // at 128 channels it ties the ring bodies, which then stay)
+static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo);
+// AUTO (= AUTO_A3): the planner's choice, its 256x256 one-tile grids on the A3
+// body (measured in-process on one box: C2 1721 -> 1741 img/s, C4 2616 -> 2657;
+// per conv -1...-4 % on the 1x1 and 3x3 shapes of C4, -1 % on C2's layer3/4;
+// HKP_TILE_256 / 256_TAIL keep the 2-stage body)
 static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo = 0) {
+    if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
+    X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
+    if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
+    return c;
+}
+static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo) {
     // the halo-tile body wherever the shape allows it, unless a tile body is forced
     if ((halo >= 1 && policy == HKP_TILE_HALO) ||
         (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3))) {
@@ -2605,7 +2616,8 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     const long rm = tiles / G * G / a.n_tiles;              // m-tiles of the full rounds
     const long tm = m_tiles - rm;
     long NG = (!c.sk && c.bn == 256 && sk_ok &&
-               (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3))
+               (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3 ||
+                policy == HKP_TILE_AUTO_A3))
                   ? x3_tail_groups(m_tiles, a.n_tiles, nks) : 0;
     // one round, every group non-empty and inside two tiles, slabs and counters in the workspace
     if (NG > 0 && !(tm > 0 && NG * a.n_tiles <= G && tm * nks >= NG && tm < NG &&
@@ -2662,7 +2674,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_256_A3, "%s: unknown tile policy %d", who, d->tile);
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_AUTO_A3, "%s: unknown tile policy %d", who, d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8,
                   "%s: tile policy %d is retired (the persistent conv, measured slower)", who, d->tile);
     return HKP_OK;
@@ -2699,7 +2711,8 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
     }
     if (a.in_ss) {                         // the fused input BN runs on the halo-tile body only
         HKP_CHECK_ARG(P == 3 || P == 1, "%s: fused input BN needs f16x3 or plain fp16", who);
-        HKP_CHECK_ARG(x3_halo_ok(a, d->k) && (d->tile == HKP_TILE_AUTO || d->tile == HKP_TILE_HALO),
+        HKP_CHECK_ARG(x3_halo_ok(a, d->k) && (d->tile == HKP_TILE_AUTO || d->tile == HKP_TILE_HALO ||
+                                               d->tile == HKP_TILE_AUTO_A3),
                       "%s: the fused input BN needs the halo-tile shape (stride-1 3x3, pad = dil = 1, Ho %% 8 == 0, "
                       "Wo %% 32 == 0, Cout %% 64 == 0)", who);
         policy = HKP_TILE_HALO;

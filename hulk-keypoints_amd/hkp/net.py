@@ -227,7 +227,7 @@ def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
                                       stats=bn.training)
     if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
         return ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training, sk=sk,
-                                 products=pol.products)
+                                 products=pol.products, tile=pol.x3_tile)
     if layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
         return ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
                                   stats=bn.training, sk=sk,
@@ -256,8 +256,11 @@ def _bnin_ok(conv, y, pol):
         return False
     k, r, s, c = conv.weight.shape
     n, h, w, _ = y.shape
-    return c == y.shape[-1] and ops.bnin_shape_ok(n, h, w, c, k, r, s, _i(conv.stride), _i(conv.padding),
-                                                  _i(conv.dilation))
+    # 64 input channels: where the unfused conv runs the halo body too (the planner's
+    # default there), so fusing changes no summation order — the outputs are the
+    # unfused path's bits
+    return c == y.shape[-1] and c <= 64 and ops.bnin_shape_ok(n, h, w, c, k, r, s, _i(conv.stride),
+                                                              _i(conv.padding), _i(conv.dilation))
 
 
 def _f16_conv_ok(conv):

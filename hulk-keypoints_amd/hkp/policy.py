@@ -46,9 +46,11 @@ class Policy:
     mask_from_y: bool = True
     # inference: last block's BN apply fused with the K-row head
     fused_head: bool = True
-    # HKP_TILE_* of the plain-fp16 1x1 / kxk convs (0 = the planner)
+    # HKP_TILE_* of the plain-fp16 1x1 / kxk convs and of the f16x3 forward convs
+    # (0 = the planner)
     f16_tile_1x1: int = 0
     f16_tile_kxk: int = 0
+    x3_tile: int = 0
     # training: repeat the last batched weight-pack launch when it repacks every operand
     prepack_plan: bool = True
     # BN finalize: two-level merge from this many partial tiles on

@@ -79,6 +79,7 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_HALO 10              /* 8x32-pixel halo tiles (stride-1 3x3, pad = dil = 1, Ho%8 = Wo%32 = 0;
                                          the default there under AUTO and 256_TAIL when the
                                          input has 64 channels) */
+#define HKP_TILE_AUTO_A3 12           /* AUTO with its 256x256 one-tile grids on the A3 body */
 #define HKP_TILE_256_A3 11            /* 256x256 on the A3 body (A ring 3 stages deep, B ring 2: an A
                                          line has two K-steps to land) + the split-K tail of 9 */
 

@@ -125,8 +125,10 @@ def test_kernel_name_query():
     from hkp import _lib, ops
     # C2 layer4 conv (R34, 640x480, B=32, dilation 4): 1200 256x256 tiles
     d = _lib.ConvDesc(32, 60, 80, 512, 512, 3, 3, 1, 4, 4, 0)
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"        # 256x256 on the A3 body
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_F16) == "conv_x3_a3_kernel<1>"
+    d.tile = _lib.HKP_TILE_256
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<256, false, false, 16, false, 3>"
-    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_F16) == "conv_x3_kernel<256, false, false, 16, false, 1>"
     assert ops.kernel_name(d, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_kernel<256>"
     d.tile = _lib.HKP_TILE_64_PAIR
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"

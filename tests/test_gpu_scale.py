@@ -65,7 +65,7 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
         ops.set_observer(None)
     # every backbone conv ran on the packed f16x3 (LDS-DMA MFMA) kernels; layer1's
     # 3x3 convs (120x160) on the halo-tile body
-    assert syms and all(s.startswith(("conv_x3_kernel", "conv_x3_halo_kernel")) for s in syms), syms
+    assert syms and all(s.startswith(("conv_x3_kernel", "conv_x3_a3_kernel", "conv_x3_halo_kernel")) for s in syms), syms
     assert "conv_x3_halo_kernel<3>" in syms
     print("conv kernels:", {s: "%.1f GFLOP" % (f / 1e9) for s, f in sorted(syms.items(), key=lambda kv: -kv[1])})
     low_err = (low.cpu().numpy() - g["lowres"]).__abs__().max()
@@ -347,7 +347,7 @@ def test_c3_shard_train_step_sampled_fp64(cuda_device):
     # the configuration bench.py times: overlap on (memory not tight), the bench
     # train leg's roofline symbol and the wgrad kernel among the launches
     assert m.policy.overlap_wgrad and not net._memory_tight(cuda_device)
-    assert "conv_x3_kernel<256, false, false, 16, false, 3>" in syms and "wgrad_x3_kernel<256>" in syms
+    assert "conv_x3_a3_kernel<3>" in syms and "wgrad_x3_kernel<256>" in syms
     assert any(s.endswith(", true, 3>") for s in syms), syms          # stream-K forward / dgrad bodies ran
 
 
@@ -473,7 +473,7 @@ def test_c4_fp16_forward_sampled_fp64(cuda_device):
     # 15 of the 16 Bottlenecks run conv3 with bn3 + residual + ReLU fused (the
     # last block's tail is fused with the head instead)
     assert counts == {"stem": 1, "f16": n_conv - 15, "f16_bn": 15}, counts
-    assert "conv_x3_kernel<256, false, false, 16, false, 1>" in syms      # BENCH C4's roofline symbol
+    assert "conv_x3_a3_kernel<1>" in syms      # BENCH C4's roofline symbol
     assert torch.isfinite(hm).all().item() and yx.shape == (B, K, 2)
 
 

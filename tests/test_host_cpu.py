@@ -354,6 +354,8 @@ def test_bench_pmc_traffic_folds_split_k_tail():
         per = t["dispatches"] / main["dispatches"]
         assert nbytes == pytest.approx(plain + (t["FETCH_SIZE"] * 2 + t["WRITE_SIZE"]) * 1024 * per)
         assert ms == pytest.approx((main["avg_duration_ns"] + t["avg_duration_ns"] * per) * 1e-6)
+    assert bench._tail_of("conv_x3_a3_kernel<1>") == "::conv_x3_tail_kernel<256,1>("
+    assert bench._tail_of(sym) == "::conv_x3_tail_kernel<256,3>("
     # kernels without a tail are looked up unchanged
     nb2, _, _, f2 = bench.pmc_traffic("wgrad_x3_kernel<256>", "train_c3")
     assert f2 is None
