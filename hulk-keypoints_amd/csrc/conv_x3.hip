@@ -2245,26 +2245,57 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 
 
 // dw[i] = sum_split ws[split][i], fixed order
+// Sum of the split-K slabs [splits][n4] (fixed order, deterministic).  G = 1: a
+// thread per float4 element, its slabs summed left to right with 16 loads in
+// flight; G = 4 (8 loads in flight per thread) (many splits: the small layers' wgrads split over up to ~75
+// pixel ranges): the four waves of a block take the same 64 elements, wave g
+// summing slabs g, g+4, g+8, ... left to right, and the four partial sums are
+// added in wave order through LDS — 4x fewer dependent load round trips per
+// element.
+template <int G>
 __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, const f32x4* __restrict__ ws,
                                                           f32x4* __restrict__ dw) {
-    const long stride = (long)gridDim.x * blockDim.x;
-    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-        f32x4 s = ws[i];
-        // up to eight slab loads in flight per thread (one at a time the loop was
-        // latency-bound), summed in the same left-to-right order
-        for (int k = 1; k < splits; k += 8) {
-            const int cnt = min(8, splits - k);
-            f32x4 v[8];
+    constexpr int B = G == 1 ? 16 : 8;      // slab loads in flight per thread
+    auto sum_from = [&](long i, int k0, int step) {
+        f32x4 s = {0.f, 0.f, 0.f, 0.f};
+        bool first = true;
+        for (int k = k0; k < splits; k += B * step) {
+            f32x4 v[B];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (u < cnt) v[u] = __builtin_nontemporal_load(&ws[(long)(k + u) * n4 + i]);
+            for (int u = 0; u < B; ++u)
+                if (k + u * step < splits) v[u] = __builtin_nontemporal_load(&ws[(long)(k + u * step) * n4 + i]);
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (u < cnt)
+            for (int u = 0; u < B; ++u)
+                if (k + u * step < splits) {
+                    if (first) s = v[u];
+                    else
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) s[e] += v[u][e];
+                        for (int e = 0; e < 4; ++e) s[e] += v[u][e];
+                    first = false;
+                }
         }
-        dw[i] = s;
+        return s;
+    };
+    if constexpr (G == 1) {
+        const long stride = (long)gridDim.x * blockDim.x;
+        for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) dw[i] = sum_from(i, 0, 1);
+    } else {
+        static_assert(G == 4, "wg_x3_reduce_kernel: G is 1 or 4");
+        __shared__ f32x4 part[G][64];
+        const int g = threadIdx.x >> 6, l = threadIdx.x & 63;
+        for (long b0 = (long)blockIdx.x * 64; b0 < n4; b0 += (long)gridDim.x * 64) {
+            const long i = b0 + l;
+            if (i < n4 && g < splits) part[g][l] = sum_from(i, g, G);
+            __syncthreads();
+            if (g == 0 && i < n4) {
+                f32x4 s = part[0][l];
+                for (int q = 1; q < G && q < splits; ++q)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) s[e] += part[q][l][e];
+                dw[i] = s;
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -2958,10 +2989,17 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     else if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<64>, dim3(grid), dim3(512), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3");
-    long g = (n / 4 + 255) / 256;
-    if (g > 4096) g = 4096;
-    hipLaunchKernelGGL(wg_x3_reduce_kernel, dim3((unsigned)g), dim3(256), 0, st, n / 4, sp, (const f32x4*)workspace,
-                       (f32x4*)dw);
+    if (sp > 16) {
+        long g = (n / 4 + 63) / 64;
+        if (g > 4096) g = 4096;
+        hipLaunchKernelGGL(wg_x3_reduce_kernel<4>, dim3((unsigned)g), dim3(256), 0, st, n / 4, sp,
+                           (const f32x4*)workspace, (f32x4*)dw);
+    } else {
+        long g = (n / 4 + 255) / 256;
+        if (g > 4096) g = 4096;
+        hipLaunchKernelGGL(wg_x3_reduce_kernel<1>, dim3((unsigned)g), dim3(256), 0, st, n / 4, sp,
+                           (const f32x4*)workspace, (f32x4*)dw);
+    }
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3 (reduce)");
     return HKP_OK;
 }

@@ -37,6 +37,7 @@ for L in infer train c4; do
     python3 tools/rocpd_stats.py $DB $O/${L}_kernel_stats.csv --top 25 > $O/${L}_kernel_top.txt
     python3 tools/step_breakdown.py $DB --timeline > $O/${L}_timeline.txt
     python3 tools/step_breakdown.py $DB --last-step > $O/${L}_last_step.txt
+    python3 tools/step_breakdown.py $DB --walls > $O/${L}_walls.txt
 done
 rm -rf $O/prof_infer $O/prof_train $O/prof_c4
 echo "stats ok"

@@ -5,6 +5,10 @@ each conv launch can be mapped to its layer.
 
     python tools/step_breakdown.py gpurun_out/prof_infer/run_results.db [--match conv_x3] [--steps 10]
 
+With --walls: the last step's launches with their start offset from the step's
+first launch, stream and duration (wall-clock order; concurrent side-stream
+kernels show as overlapping intervals).
+
 With --timeline: per-step wall (first start to last end of the step's launches),
 the union of kernel intervals (GPU busy), idle gaps, and how much kernel time ran
 concurrently (side-stream overlap), by stream; plus the largest idle gaps and the
@@ -23,6 +27,8 @@ def main():
         return timeline(con, steps)
     if "--last-step" in sys.argv:
         return last_step(con, match)
+    if "--walls" in sys.argv:
+        return walls(con, match)
     rows = con.execute("select name, grid_x, grid_y, grid_z, workgroup_x, duration, stream_id from kernels "
                        "order by start").fetchall()
     per = len(rows) // steps
@@ -57,6 +63,22 @@ def last_step(con, match):
         if match in n:
             short = n.replace("void ", "").replace("hkp::", "").split("(")[0][:56]
             print("%-56s grid %7d wg %4d %8.1f us  cum %7.3f ms" % (short, gx // max(wx, 1), wx, d / 1e3, run / 1e6))
+
+
+def walls(con, match):
+    rows = con.execute("select name, start, end, stream_id, grid_x, workgroup_x from kernels order by start").fetchall()
+    marker = _marker(rows)
+    idx = [i for i, r in enumerate(rows) if marker in r[0]]
+    if len(idx) < 2:
+        raise SystemExit("fewer than two %s launches" % marker)
+    last = rows[idx[-2] + 1:idx[-1] + 1]
+    t0 = last[0][1]
+    print("step wall %.3f ms; start / end offsets (us), stream, duration" % ((max(r[2] for r in last) - t0) / 1e6))
+    for n, s_, e, st, gx, wx in last:
+        if match in n:
+            short = n.replace("void ", "").replace("hkp::", "").split("(")[0][:52]
+            print("%9.1f %9.1f  s%-2s %8.1f us  grid %6d  %s" % ((s_ - t0) / 1e3, (e - t0) / 1e3, st, (e - s_) / 1e3,
+                                                               gx // max(wx, 1), short))
 
 
 def timeline(con, steps):
