@@ -247,6 +247,7 @@ WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (1, 30, 40, 96, 256, 3, 2, 1, 1),       # 256x256 tile, RSC 864: column groups past R*S*Cin
     (2, 7, 9, 64, 256, 3, 1, 1, 1),         # Cout 256 with Wo = 9 < 16: the KA-128 fallback wraps rows
     (2, 9, 20, 64, 256, 3, 1, 1, 1),        # 256x256 tile, Wo = 20: 16-pixel stages wrap rows and images
+    (2, 96, 128, 64, 64, 3, 1, 1, 1),       # 3 tiles over 24576 pixels: > 16 splits (the 4-wave slab reduce)
 ]
 
 
