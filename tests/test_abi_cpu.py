@@ -130,6 +130,12 @@ def test_kernel_name_query():
     d.tile = _lib.HKP_TILE_256
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<256, false, false, 16, false, 3>"
     assert ops.kernel_name(d, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_kernel<256>"
+    d.tile = _lib.HKP_TILE_AUTO_A3                                   # an alias of AUTO
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
+    d.tile = _lib.HKP_TILE_256_A3
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3_W16) == "conv_x3_a3_kernel<2>"
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3_X16) == "conv_x3_a3_kernel<4>"
     d.tile = _lib.HKP_TILE_64_PAIR
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"
     d.tile = 99
