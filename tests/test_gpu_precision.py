@@ -274,10 +274,13 @@ def test_x3_wgrad_scaled(cuda_device, case, gscale):
     assert err < 2e-6, err
     # a caller-chosen CU budget (Policy.wgrad_overlap_cus): the same sums over
     # another grouping of pixel ranges (1: a single split)
+    # (one split over all M pixels accumulates M terms in fp32 inside one tile:
+    # the bound grows like sqrt(M) past 4096 pixels — 24576 pixels: x2.45)
+    m_px = n * ho * wo
     for cus in (1, 40, 96):
         dws = ops.conv2d_bwd_filter_x3(xs, dys, (cout, k, k, cin), st, pad, dil, amax=amax, cus=cus)
         e = (dws.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
-        assert e < 2e-6, (cus, e)
+        assert e < 2e-6 * max(1.0, (m_px / 4096) ** 0.5), (cus, e)
         # the observer's symbol query takes the wgrad's CU budget in the same field
         from hkp._lib import HKP_KOP_WGRAD_X3, ConvDesc
         assert ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, cus),
