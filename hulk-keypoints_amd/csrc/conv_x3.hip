@@ -93,6 +93,15 @@ struct X3Args {
     long sk_units = 0;
     float* sk_ws = nullptr;
     unsigned* sk_cnt = nullptr;
+    // the stream-K grid sk_combine works in when it is not the launch's grid: its
+    // block count (0: gridDim.x) and this block's index in it (after the XCD remap)
+    int sk_grid = 0, sk_b = 0;
+    // A3 launches with the split-K tail appended (conv_x3_a3_kernel): blocks
+    // [0, main_blocks) run the full rounds' tiles, the rest the tail's segments —
+    // tail_groups groups of n_tiles blocks over tail_units (m-tile, K-step) units
+    // from m-tile tail_mt0 (the one-launch form of conv_x3_tail_kernel)
+    int main_blocks = 0, tail_groups = 0, tail_mt0 = 0;
+    long tail_units = 0;
     unsigned long long* stamps = nullptr;   // debug: per-block phase clocks (hkp_debug_x3_stamps)
     // first-round stagger: blocks b < stagger_blocks with (b >> 3) & 1 (half the CUs
     // of every XCD) wait stagger_ticks (s_memrealtime, 100 MHz) before starting, so
@@ -233,7 +242,7 @@ typedef unsigned __attribute__((address_space(1))) gu32;
 template <int NV4, typename Get, typename Set>
 __device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char* flag_lds, Get&& get, Set&& set) {
     const long U = a.sk_units;
-    const int NT = a.n_tiles, NG = gridDim.x / NT;
+    const int NT = a.n_tiles, NG = (a.sk_grid ? a.sk_grid : (int)gridDim.x) / NT;
     const int mt = T / NT, nt = T - mt * NT;
     const long t0 = (long)mt * a.nks;
     const int b0 = sk_block_of(t0, U, NG), nseg = sk_block_of(t0 + a.nks - 1, U, NG) - b0 + 1;
@@ -241,7 +250,7 @@ __device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char
         const int which = sk_start(gg, U, NG) >= t0 ? 0 : 1;
         return (gf32x4*)a.sk_ws + (long)(2 * (gg * NT + nt) + which) * NV4 * 512;
     };
-    gf32x4* mine = slab(xcd_remap(blockIdx.x, gridDim.x) / NT);
+    gf32x4* mine = slab((a.sk_grid ? a.sk_b : xcd_remap(blockIdx.x, gridDim.x)) / NT);
 #pragma unroll
     for (int v = 0; v < NV4; ++v) mine[v * 512 + tid] = get(v);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1433,13 +1442,33 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
     }
 }
 
-// One 256x256 tile per block on the A3 body (3-stage A ring, 2-stage B ring).
+// One 256x256 tile per block on the A3 body (3-stage A ring, 2-stage B ring);
+// with a.main_blocks > 0 the blocks past it run the grid's split-K tail (the
+// segments of conv_x3_tail_kernel) in the same launch: they are dispatched as the
+// full rounds' tiles finish, without the second launch's gap — and, in training,
+// ahead of a side-stream wgrad that would otherwise take the freed CUs first.
 template <int P>
 __global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
     x3_stagger(a);
     x3_stamp(a, 0);
-    conv_x3_tile<256, false, false, 16, P, true>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
+    const int b = blockIdx.x;
+    if (a.tail_groups == 0 || b < a.main_blocks) {
+        conv_x3_tile<256, false, false, 16, P, true>(a, smem, xcd_remap(b, a.tail_groups ? a.main_blocks : gridDim.x),
+                                                     0, a.nks, false);
+        return;
+    }
+    X3Args t = a;
+    const int NT = a.n_tiles, G = a.tail_groups * NT;
+    t.mt0 = a.tail_mt0;
+    t.sk_units = a.tail_units;
+    t.sk_grid = G;
+    t.sk_b = xcd_remap(b - a.main_blocks, G);
+    const int g = t.sk_b / NT, nt = t.sk_b - g * NT;
+    const long U = t.sk_units, u0 = sk_start(g, U, a.tail_groups), u1 = sk_start(g + 1, U, a.tail_groups);
+    const int mt = (int)(u0 / a.nks);
+    const int ks = (int)(u0 - (long)mt * a.nks), ke = (int)(u1 - (long)mt * a.nks);
+    conv_x3_tile<256, false, false, 16, P, true>(t, smem, mt * NT + nt, ks, ke - ks, true);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -2655,6 +2684,18 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
                     2L * G * 256 * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
         NG = 0;
     const bool tail = NG > 0;
+    if (tail && c.a3) {                    // one launch: the full rounds, then the tail's segments
+        X3Args t = a;
+        t.main_blocks = (int)(rm * a.n_tiles);
+        t.tail_groups = (int)NG;
+        t.tail_mt0 = (int)rm;
+        t.tail_units = tm * nks;
+        t.sk_cnt = (unsigned*)ws;
+        t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
+        const dim3 g1((unsigned)((rm + NG) * a.n_tiles));
+        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL(conv_x3_a3_kernel<pc.value>, g1, dim3(512), 0, st, t); });
+        return;
+    }
     if (tail) {
         if (rm > 0) {
             dim3 g0((unsigned)(rm * a.n_tiles));

@@ -580,6 +580,7 @@ TAIL_CASES = [
     ("x3", 16, 60, 80, 256, 256, 3, 1, 2, 2),      # C2 layer3 class: 300 tiles = 256 + 44 halves
     ("x3", 9, 60, 80, 256, 512, 3, 1, 4, 4),       # two column tiles, 338 tiles, ragged M
     ("f16", 16, 60, 80, 512, 256, 1, 1, 0, 1),     # plain fp16, 8 K-steps per tile
+    ("x3", 4, 60, 80, 256, 256, 3, 1, 2, 2),       # 75 tiles, no full round: a tail-only grid (S = 3)
 ]
 
 
@@ -590,7 +591,7 @@ def test_split_k_tail(cuda_device, case):
     segment) — the same values as the plain one-tile grid (fp32 summation order),
     the same BN partials, and run to run bit-identical."""
     from hkp import ops
-    from hkp._lib import HKP_TILE_256, HKP_TILE_256_TAIL
+    from hkp._lib import HKP_TILE_256, HKP_TILE_256_A3, HKP_TILE_256_TAIL
     prec, n, h, w, cin, cout, k, st, pad, dil = case
     d = cuda_device
     g = torch.Generator(device=d).manual_seed(9)
@@ -603,12 +604,15 @@ def test_split_k_tail(cuda_device, case):
         xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
         wp, fwd = ops.weight_pack_x3(wt), ops.conv2d_fwd_x3
     y0, p0 = fwd(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256)
-    y1, p1 = fwd(xs, wp, st, pad, dil, tile=HKP_TILE_256_TAIL)
-    y2, _ = fwd(xs, wp, st, pad, dil, tile=HKP_TILE_256_TAIL)
     tol = 2.0 ** -10 if prec == "f16" else 4e-6
-    assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item()
-    assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
-    assert torch.equal(y1, y2)
+    # 256_TAIL: a second launch (conv_x3_tail_kernel); 256_A3 / AUTO: the A3 kernel
+    # with the tail's segments appended to the same launch
+    for tile in (HKP_TILE_256_TAIL, HKP_TILE_256_A3, 0):
+        y1, p1 = fwd(xs, wp, st, pad, dil, tile=tile)
+        y2, _ = fwd(xs, wp, st, pad, dil, tile=tile)
+        assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item(), tile
+        assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3), tile
+        assert torch.equal(y1, y2), tile                       # counters back at zero, fixed order
 
 
 def test_split_k_tail_dgrad_back_to_back(cuda_device):
@@ -619,7 +623,7 @@ def test_split_k_tail_dgrad_back_to_back(cuda_device):
     to back on one stream give bit-identical dx, equal to the plain grid to fp32
     summation order, and fp32-class vs fp64."""
     from hkp import ops
-    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_TILE_256, HKP_TILE_256_TAIL, ConvDesc
+    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_TILE_256, HKP_TILE_256_A3, HKP_TILE_256_TAIL, ConvDesc
     n, h, w, cin, cout, k, pad, dil = 8, 60, 80, 512, 512, 3, 4, 4          # the C3 shard's layer4 dgrad
     d = cuda_device
     g = torch.Generator(device=d).manual_seed(21)
@@ -636,6 +640,10 @@ def test_split_k_tail_dgrad_back_to_back(cuda_device):
     dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, sk=False, tile=HKP_TILE_256)
     assert torch.equal(dx1, dx2)
     assert (dx1 - dx0).abs().max().item() <= 4e-6 * dx0.abs().max().item()
+    dx3 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=HKP_TILE_256_A3)
+    dx4 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=HKP_TILE_256_A3)
+    assert torch.equal(dx3, dx4)                                # the one-launch A3 + tail form
+    assert (dx3 - dx0).abs().max().item() <= 4e-6 * dx0.abs().max().item()
     # fp64 on a slice of images
     ref = torch.nn.grad.conv2d_input((2, cin, h, w), wt.permute(0, 3, 1, 2).double(),
                                      gy[:2].permute(0, 3, 1, 2).double(), 1, pad, dil) + add[:2].permute(0, 3, 1, 2).double()
