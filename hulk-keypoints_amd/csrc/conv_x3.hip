@@ -2614,6 +2614,7 @@ static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Ar
 // layout (3 packed f16x3 split, 1 plain fp16)
 static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 static int g_x3_stagger_ns = 0;                        // hkp_debug_x3_stagger
+static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -2684,7 +2685,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
                     2L * G * 256 * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
         NG = 0;
     const bool tail = NG > 0;
-    if (tail && c.a3) {                    // one launch: the full rounds, then the tail's segments
+    if (tail && c.a3 && !g_x3_split_tail) {  // one launch: the full rounds, then the tail's segments
         X3Args t = a;
         t.main_blocks = (int)(rm * a.n_tiles);
         t.tail_groups = (int)NG;
@@ -2699,7 +2700,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     if (tail) {
         if (rm > 0) {
             dim3 g0((unsigned)(rm * a.n_tiles));
-            x3_dispatch_p(P, [&](auto pc) { launch_x3_p<pc.value>(c, g0, st, a); });
+            x3_dispatch_p(P, [&](auto pc) { launch_x3_p<pc.value>(c, g0, st, a); });     // (A3 body, A/B only)
         }
         X3Args t = a;
         t.mt0 = (int)rm;
@@ -3175,4 +3176,8 @@ extern "C" void hkp_debug_x3_stamps(uint64_t* buf) { g_x3_stamps = (unsigned lon
 // Debug / tuning (tools/ only, not thread-safe): the first-round stagger of the
 // one-tile forward conv launches, in ns (0 = off; X3Args::stagger_ticks).
 extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns : 0; }
+
+// Debug / A/B (tools/ only, not thread-safe): nonzero runs an A3 grid's split-K
+// tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
+extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
 

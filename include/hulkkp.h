@@ -231,6 +231,9 @@ void hkp_debug_x3_stamps(uint64_t* buf);
  * hold half the CUs of every XCD back for ns nanoseconds in their first round of
  * blocks (0 = off), so the rounds' epilogues do not all coincide. */
 void hkp_debug_x3_stagger(int32_t ns);
+/* Debug / A/B (tools/ only, not thread-safe): nonzero runs an A3 grid's split-K
+ * tail as a launch of its own (conv_x3_tail_kernel) instead of appended to it. */
+void hkp_debug_x3_split_tail(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
