@@ -88,6 +88,15 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
 # ---------------------------------------------------------------- C5 sampled
 
 
+def _applied(xx):
+    """The activation a fused-input-BN conv reads (net._PendingBN: a producer's raw
+    output and its BN scale | shift): relu(y*s + t), bn_apply's arithmetic (fp32
+    multiply, then add), rounded to y's dtype."""
+    c = xx.y.shape[-1]
+    v = torch.relu(xx.y.float() * xx.ss[:c] + xx.ss[c:])
+    return v.to(xx.y.dtype)
+
+
 class _Act:
     """fp64 reader of an NHWC activation: fp32, a packed f16x3 split ([.., 2C],
     per 32 channels hi32|lo32, value = (hi + lo) / scale), a plain fp16 tensor
@@ -441,8 +450,12 @@ def test_c4_fp16_forward_sampled_fp64(cuda_device):
             counts["stem"] += 1
             return
         assert y.dtype == torch.float16
-        xs = ops.split_of(xx)[0]
-        assert getattr(xs, "_hkp_split_passes", 0) == 1
+        if isinstance(xx, net._PendingBN):      # fused input BN: the operand is relu(y*s + t) in fp16
+            xs = _applied(xx)
+            xs._hkp_split_passes = 1
+        else:
+            xs = ops.split_of(xx)[0]
+            assert getattr(xs, "_hkp_split_passes", 0) == 1
         wp = net._cached_split(conv.weight, "f16", ops.weight_pack_f16)
         check_conv_fwd_f16(_Act(xs), wp, y, st, pd, dl, gen, stats)
         counts["f16"] += 1
