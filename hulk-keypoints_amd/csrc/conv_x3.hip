@@ -270,31 +270,21 @@ __device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char
     }
     __syncthreads();
     if (!*(volatile int*)flag_lds) return false;
-    // chunks of 8 slab vectors, double-buffered: the next chunk's 8 loads are in
-    // flight while this one is added (16 loads per thread outstanding: the fragment
-    // registers are dead here).  Summation order unchanged: per element, slab 0,
-    // then + slab 1, + slab 2, ... (the result does not depend on arrival order).
-    static_assert(NV4 % 8 == 0, "sk_combine chunks");
-    constexpr int NC = NV4 / 8;
-    const int total = nseg * NC;
-    f32x4 xa[8], xb[8];
-    auto load = [&](f32x4* x, int c) {
-        const gf32x4* p = slab(b0 + c / NC) + (c % NC) * 8 * 512 + tid;
+    // 8 loads in flight per chunk (the accumulators leave few free registers;
+    // double-buffered chunks, or a chunk index computed at run time, put the
+    // 256x256 accumulators into scratch)
+    static_assert(NV4 % 8 == 0 || NV4 < 8, "sk_combine chunks");
+    constexpr int CW = NV4 < 8 ? NV4 : 8;
+    for (int sg = 0; sg < nseg; ++sg) {
+        const gf32x4* p = slab(b0 + sg);
 #pragma unroll
-        for (int v = 0; v < 8; ++v) x[v] = p[v * 512];
-    };
-    auto add = [&](const f32x4* x, int c) {
-        const int sg = c / NC, v0 = (c % NC) * 8;
+        for (int v0 = 0; v0 < NV4; v0 += CW) {
+            f32x4 x[CW];
 #pragma unroll
-        for (int v = 0; v < 8; ++v) set(v0 + v, sg == 0 ? x[v] : get(v0 + v) + x[v]);
-    };
-    load(xa, 0);
-    for (int c = 0; c < total; c += 2) {
-        if (c + 1 < total) load(xb, c + 1);
-        add(xa, c);
-        if (c + 1 >= total) break;
-        if (c + 2 < total) load(xa, c + 2);
-        add(xb, c + 1);
+            for (int v = 0; v < CW; ++v) x[v] = p[(v0 + v) * 512 + tid];
+#pragma unroll
+            for (int v = 0; v < CW; ++v) set(v0 + v, sg == 0 ? x[v] : get(v0 + v) + x[v]);
+        }
     }
     return true;
 }
@@ -713,8 +703,9 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
 // wave's reads of t), barrier, [read A frags of t+1] then per column block j:
 // [MFMAs of t with B_j] [refill B_j with t+1's].  NST 2 (256x256; 256x64 pairs):
 // A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
-template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, typename Issue, typename IssueA, typename IssueB>
-__device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int nks, bool partial,
+template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, bool FB, typename Issue, typename IssueA,
+          typename IssueB>
+__device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
                                                   Issue& issue_next, IssueA& issue_a, IssueB& issue_b) {
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
@@ -722,6 +713,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
     static_assert(!A3 || (BN == 256 && NST == 2), "A3: the 256x256 body");
+    static_assert(!FB || (A3 && P == 3), "FB: the f16x3 A3 body");
     // PAIRB and A3 have no LDS past the ring: the epilogue's scratch is the drained
     // ring and the column scales are loaded in the epilogue
     constexpr bool RINGSCR = PAIRB || A3;
@@ -797,7 +789,151 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 __builtin_amdgcn_sched_group_barrier(0x020, (NP + UN - 1) / UN, 0);
         }
     };
-    if constexpr (A3) {
+    if constexpr (FB) {
+        // FB (conv_x3_a3_bnin_kernel): the A3 rings with the A stages DMA'd from the
+        // producer conv's raw fp32 output (32 channels = 128 B, a packed line's
+        // size) and turned into packed hi | lo lines in place — relu(y * s + t),
+        // bn_apply's arithmetic, then the f16x3 split — by the wave that DMA'd the
+        // rows, so its own vmcnt orders them (no barrier).  B fragments are read one
+        // column ahead instead of a whole stage ahead (-48 VGPRs against the A3
+        // body: room for the turn's scale | shift and raw values).  Per K-step s:
+        //   columns 0..6  MFMAs of s (A(s) fragments in registers, B(s) one column
+        //                 ahead); turn A(s+1)'s rows (wait: own DMA of A(s+1))
+        //   wait own DMA of B(s+1) (A(s+2) stays in flight); barrier M(s)
+        //   load A(s+2)'s scale | shift, DMA B(s+2) into B(s)'s slot and A(s+3)
+        //   into A(s)'s (both read before M(s))
+        //   column 7, then read B(s+1)'s column 0 and A(s+1)'s fragments (turned
+        //   before M(s)) — their latency under the last column's MFMAs
+        // Issue order per step: scale | shift, B, A — the turn's vmcnt(GB + GA)
+        // retires A(s+1) and its scale | shift, M(s)'s vmcnt(GA) B(s+1).  A stage
+        // has ~1.3 K-steps to land, B one.
+        constexpr int GB = GL - GA;
+        char* const bring = smem + 3 * BM * ROW;
+        const int w = wm * WN + wn;
+        const int tj = lane & 3;                       // the 8-channel piece this lane turns,
+        const int trow = 32 * w + (lane >> 2);         // in rows trow and trow + 16 (this wave's DMA rows)
+        const int tsw = (trow >> 1) & 7;               // (both rows swizzle alike)
+        const int o_r0 = trow * ROW + (((2 * tj) ^ tsw) << 4), o_r1 = trow * ROW + (((2 * tj + 1) ^ tsw) << 4);
+        const int o_h = trow * ROW + ((tj ^ tsw) << 4), o_l = trow * ROW + (((4 + tj) ^ tsw) << 4);
+        int tr_cc = ks / a.RS, tr_tap = ks - tr_cc * a.RS;   // K-step position of the next scale | shift load
+        f32x4 ssc[2], ssh[2], raw[4];
+        auto load_ss = [&]() {
+            const float* p = a.in_ss + tr_cc * 32 + 8 * tj;
+            ssc[0] = *(const f32x4*)p;
+            ssc[1] = *(const f32x4*)(p + 4);
+            ssh[0] = *(const f32x4*)(p + a.C);
+            ssh[1] = *(const f32x4*)(p + a.C + 4);
+            if (++tr_tap == a.RS) {
+                tr_tap = 0;
+                ++tr_cc;
+            }
+        };
+        // all four reads before any write: the four pieces of a row are four
+        // adjacent lanes of each instruction, and piece j's hi / lo chunks are
+        // pieces j/2's and 2 + j/2's raw chunks
+        auto turn_read = [&](const char* slot) {
+            raw[0] = *(const f32x4*)(slot + o_r0);
+            raw[1] = *(const f32x4*)(slot + o_r1);
+            raw[2] = *(const f32x4*)(slot + 16 * ROW + o_r0);
+            raw[3] = *(const f32x4*)(slot + 16 * ROW + o_r1);
+        };
+        auto turn_write = [&](char* slot, int k) {
+            f16x8 h, l;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float y = raw[2 * k + (e >> 2)][e & 3];
+                float x = __fadd_rn(__fmul_rn(y, ssc[e >> 2][e & 3]), ssh[e >> 2][e & 3]);
+                x = x > 0.f ? x : 0.f;
+                const _Float16 hv = (_Float16)x;
+                h[e] = hv;
+                l[e] = (_Float16)(x - (float)hv);
+            }
+            *(f16x8*)(slot + k * 16 * ROW + o_h) = h;
+            *(f16x8*)(slot + k * 16 * ROW + o_l) = l;
+        };
+        f16x8 jh[2], jl[2];                            // B column j in slot j & 1
+        auto read_bj = [&](int x, const char* stb, int j) {
+            jh[x] = *(const f16x8*)(stb + b_base + j * 16 * ROW + fo_h);
+            jl[x] = *(const f16x8*)(stb + b_base + j * 16 * ROW + fo_l);
+        };
+        auto mma_bj = [&](const FA& f, int j) {
+#pragma unroll
+            for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], f.h[i], f.l[i], jh[j & 1], jl[j & 1], mfma);
+        };
+
+        // prologue: A(0) turned and B(0) landed everywhere (M(-1)), then the
+        // step-0 state: scale | shift of A(1), B(1), A(2) issued; A(0) and B(0)'s
+        // column 0 in registers
+        load_ss();
+        issue_a();                                     // A(0) -> A slot 0
+        issue_b();                                     // B(0) -> B slot 0
+        if (nks > 1) issue_a();                        // A(1) -> A slot 1
+        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        turn_read(smem);
+        turn_write(smem, 0);
+        turn_write(smem, 1);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        x3_stamp(a, 1);
+        if (nks > 1) {
+            load_ss();
+            issue_b();                                 // B(1) -> B slot 1
+        }
+        if (nks > 2) issue_a();                        // A(2) -> A slot 2
+        FA fa;
+        read_a(fa, smem);
+        read_bj(0, bring, 0);
+        int ca = 0, cb = 0;                            // slots of A(s), B(s)
+        // one K-step s < nks - 1; A2: s + 2 < nks (A(s+2) was issued), A3N: s + 3 < nks
+        auto kstep = [&](auto a2, auto a3n) {
+            constexpr bool A2 = decltype(a2)::value, A3N = decltype(a3n)::value;
+            char* const sa1 = smem + (ca == 2 ? 0 : ca + 1) * (BM * ROW);        // A(s+1)
+            const char* const stb = bring + cb * (BN * ROW);                     // B(s)
+#pragma unroll
+            for (int j = 0; j < UN - 1; ++j) {
+                read_bj((j + 1) & 1, stb, j + 1);
+                mma_bj(fa, j);
+                if (j == 1) {
+                    if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
+                    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
+                    turn_read(sa1);
+                }
+                if (j == 3) turn_write(sa1, 0);
+                if (j == 4) turn_write(sa1, 1);
+            }
+            if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            lds_barrier();                             // M(s)
+            if constexpr (A2) {
+                load_ss();
+                issue_b();                             // B(s+2) -> B(s)'s slot
+            }
+            if constexpr (A3N) issue_a();              // A(s+3) -> A(s)'s slot
+            mma_bj(fa, UN - 1);
+            read_bj(0, bring + (cb ^ 1) * (BN * ROW), 0);
+            read_a(fa, sa1);
+            __builtin_amdgcn_sched_barrier(0);
+            ca = ca == 2 ? 0 : ca + 1;
+            cb ^= 1;
+        };
+        int s = 0;
+        for (; s + 3 < nks; ++s) kstep(std::true_type{}, std::true_type{});
+        if (s + 2 < nks) {
+            kstep(std::true_type{}, std::false_type{});
+            ++s;
+        }
+        if (s + 1 < nks) kstep(std::false_type{}, std::false_type{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        {
+            const char* const stb = bring + cb * (BN * ROW);
+#pragma unroll
+            for (int j = 0; j < UN; ++j) {
+                if (j + 1 < UN) read_bj((j + 1) & 1, stb, j + 1);
+                mma_bj(fa, j);
+            }
+        }
+    } else if constexpr (A3) {
         // A3: the NST 2 schedule below with A one stage further ahead.  Issue order
         // per K-step t (after its barrier): B(t+2) into B's slot of t, then A(t+3)
         // into A's slot of t (both read into registers during step t-1); so at step
@@ -1076,7 +1212,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
+template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false, bool FB = false>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -1152,7 +1288,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         b_off[j] = (n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc));
         b_dst[j] = (BM + RPI * bi) * ROW;
     }
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    // FB: relu(NaN * s + t) = 0 for the zero-padded taps and the rows past M
+    const _Float16* zero = (const _Float16*)(FB ? g_x3_nan_line : g_x3_zero_line);
 
     // staging state of the next K-step to issue (wave-uniform, advanced per issue)
     // (a stream-K segment starts at K-step ks: channel group outer, tap inner)
@@ -1223,8 +1360,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, nks, partial, m0, n0, wm, wn, lane, tid,
-                                                         issue_next, issue_a, issue_b);
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA, FB>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
+                                                             tid, issue_next, issue_a, issue_b);
         return;
     } else {
     f32x16 acc[TM][TN];
@@ -1447,15 +1584,14 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
 // segments of conv_x3_tail_kernel) in the same launch: they are dispatched as the
 // full rounds' tiles finish, without the second launch's gap — and, in training,
 // ahead of a side-stream wgrad that would otherwise take the freed CUs first.
-template <int P>
-__global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
+template <int P, bool FB>
+__device__ __forceinline__ void conv_x3_a3_grid(const X3Args& a, char* smem) {
     x3_stagger(a);
     x3_stamp(a, 0);
     const int b = blockIdx.x;
     if (a.tail_groups == 0 || b < a.main_blocks) {
-        conv_x3_tile<256, false, false, 16, P, true>(a, smem, xcd_remap(b, a.tail_groups ? a.main_blocks : gridDim.x),
-                                                     0, a.nks, false);
+        conv_x3_tile<256, false, false, 16, P, true, FB>(
+            a, smem, xcd_remap(b, a.tail_groups ? a.main_blocks : gridDim.x), 0, a.nks, false);
         return;
     }
     X3Args t = a;
@@ -1468,7 +1604,21 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
     const long U = t.sk_units, u0 = sk_start(g, U, a.tail_groups), u1 = sk_start(g + 1, U, a.tail_groups);
     const int mt = (int)(u0 / a.nks);
     const int ks = (int)(u0 - (long)mt * a.nks), ke = (int)(u1 - (long)mt * a.nks);
-    conv_x3_tile<256, false, false, 16, P, true>(t, smem, mt * NT + nt, ks, ke - ks, true);
+    conv_x3_tile<256, false, false, 16, P, true, FB>(t, smem, mt * NT + nt, ks, ke - ks, true);
+}
+
+template <int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
+    conv_x3_a3_grid<P, false>(a, smem);
+}
+
+// the same with the input's BN + ReLU applied to each A stage in LDS
+// (X3Args::in_ss, the FB body): inference, the f16x3 split
+template <int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_a3_bnin_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
+    conv_x3_a3_grid<P, true>(a, smem);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -2592,10 +2742,23 @@ static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int le
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
 
+// the A3 grid (conv_x3_a3_kernel<P>, or with the input's BN applied in LDS:
+// conv_x3_a3_bnin_kernel<3>)
+template <int P>
+static void launch_a3(dim3 grid, hipStream_t st, const X3Args& a) {
+    if constexpr (P == 3) {
+        if (a.in_ss) {
+            hipLaunchKernelGGL(conv_x3_a3_bnin_kernel<3>, grid, dim3(512), 0, st, a);
+            return;
+        }
+    }
+    hipLaunchKernelGGL(conv_x3_a3_kernel<P>, grid, dim3(512), 0, st, a);
+}
+
 template <int P>
 static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Args& a) {
     if (c.a3)
-        hipLaunchKernelGGL(conv_x3_a3_kernel<P>, grid, dim3(512), 0, st, a);
+        launch_a3<P>(grid, st, a);
     else if (c.sk && c.bn == 128)
         hipLaunchKernelGGL((conv_x3_kernel<128, false, false, 16, true, P>), grid, dim3(512), 0, st, a);
     else if (c.sk)
@@ -2685,7 +2848,9 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
                     2L * G * 256 * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
         NG = 0;
     const bool tail = NG > 0;
-    if (tail && c.a3 && !g_x3_split_tail) {  // one launch: the full rounds, then the tail's segments
+    // one launch: the full rounds, then the tail's segments (always with a fused
+    // input BN: conv_x3_tail_kernel has no FB body)
+    if (tail && c.a3 && (!g_x3_split_tail || a.in_ss)) {
         X3Args t = a;
         t.main_blocks = (int)(rm * a.n_tiles);
         t.tail_groups = (int)NG;
@@ -2694,7 +2859,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         t.sk_cnt = (unsigned*)ws;
         t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
         const dim3 g1((unsigned)((rm + NG) * a.n_tiles));
-        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL(conv_x3_a3_kernel<pc.value>, g1, dim3(512), 0, st, t); });
+        x3_dispatch_p(P, [&](auto pc) { launch_a3<pc.value>(g1, st, t); });
         return;
     }
     if (tail) {
@@ -2782,13 +2947,17 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
         a.ep_ss = ep->ep_ss; a.ep_res = ep->ep_res; a.ep_rss = ep->ep_rss; a.ep_relu = ep->ep_relu;
         a.in_ss = ep->in_ss;
     }
-    if (a.in_ss) {                         // the fused input BN runs on the halo-tile body only
+    if (a.in_ss) {
+        // the fused input BN runs where the unfused conv would run the halo-tile body
+        // or (f16x3) the A3 body — so its output is the unfused path's, bit for bit
         HKP_CHECK_ARG(P == 3 || P == 1, "%s: fused input BN needs f16x3 or plain fp16", who);
-        HKP_CHECK_ARG(x3_halo_ok(a, d->k) && (d->tile == HKP_TILE_AUTO || d->tile == HKP_TILE_HALO ||
-                                               d->tile == HKP_TILE_AUTO_A3),
-                      "%s: the fused input BN needs the halo-tile shape (stride-1 3x3, pad = dil = 1, Ho %% 8 == 0, "
-                      "Wo %% 32 == 0, Cout %% 64 == 0)", who);
-        policy = HKP_TILE_HALO;
+        const bool sk_ok = sk_ws && sk_bytes >= x3_sk_ws_bytes(256);
+        const X3Choice c = x3_choose(d->k, (M + 255) / 256, a.RS * a.cch, sk_ok, d->tile,
+                                     x3_halo_level(x3_halo_ok(a, d->k), a.cch, P));
+        HKP_CHECK_ARG(c.halo || (c.a3 && P == 3),
+                      "%s: the fused input BN needs a launch on the halo-tile body (stride-1 3x3, pad = dil = 1, "
+                      "Ho %% 8 == 0, Wo %% 32 == 0) or, f16x3, on the A3 body (Cout %% 256 == 0, one tile per block)",
+                      who);
     }
     launch_x3(d->k, (M + 255) / 256, policy, P, as_stream(stream), a, sk_ws, sk_bytes);
     HKP_LAUNCH_CHECK(who);
@@ -2805,22 +2974,23 @@ extern "C" int hkp_conv2d_fwd_x3(const hkp_conv_desc* d, const uint16_t* x_split
 
 extern "C" int hkp_conv2d_fwd_x3_bnin(const hkp_conv_desc* d, const float* x_raw, const float* in_scale_shift,
                                       const uint16_t* w_split, const float* w_inv_scale, float* y, float* stat_partials,
-                                      hkp_stream_t stream) {
+                                      void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
     HKP_CHECK_ARG(d && y && x_raw && in_scale_shift, "hkp_conv2d_fwd_x3_bnin: null argument");
     X3Args ep;
     ep.in_ss = in_scale_shift;
-    return conv_fwd_x3_common(d, (const uint16_t*)x_raw, w_split, w_inv_scale, y, nullptr, stat_partials, nullptr, 0, 3,
-                              stream, "hkp_conv2d_fwd_x3_bnin", &ep);
+    return conv_fwd_x3_common(d, (const uint16_t*)x_raw, w_split, w_inv_scale, y, nullptr, stat_partials, sk_workspace,
+                              sk_ws_bytes, 3, stream, "hkp_conv2d_fwd_x3_bnin", &ep);
 }
 
 extern "C" int hkp_conv2d_fwd_f16_bnin(const hkp_conv_desc* d, const uint16_t* x_raw_f16, const float* in_scale_shift,
                                        const uint16_t* w_f16, const float* w_inv_scale, uint16_t* y_f16,
-                                       float* stat_partials, hkp_stream_t stream) {
+                                       float* stat_partials, void* sk_workspace, int64_t sk_ws_bytes,
+                                       hkp_stream_t stream) {
     HKP_CHECK_ARG(d && y_f16 && x_raw_f16 && in_scale_shift, "hkp_conv2d_fwd_f16_bnin: null argument");
     X3Args ep;
     ep.in_ss = in_scale_shift;
-    return conv_fwd_x3_common(d, x_raw_f16, w_f16, w_inv_scale, nullptr, y_f16, stat_partials, nullptr, 0, 1, stream,
-                              "hkp_conv2d_fwd_f16_bnin", &ep);
+    return conv_fwd_x3_common(d, x_raw_f16, w_f16, w_inv_scale, nullptr, y_f16, stat_partials, sk_workspace,
+                              sk_ws_bytes, 1, stream, "hkp_conv2d_fwd_f16_bnin", &ep);
 }
 
 extern "C" int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,

@@ -82,8 +82,8 @@ SIGNATURES = {
     "hkp_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _I32, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv2d_fwd_x3_products": (ctypes.c_int, [_CD, _P, _P, _P, _I32, _P, _P, _P, _I64, _P]),
-    "hkp_conv2d_fwd_x3_bnin": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
-    "hkp_conv2d_fwd_f16_bnin": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P]),
+    "hkp_conv2d_fwd_x3_bnin": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
+    "hkp_conv2d_fwd_f16_bnin": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "hkp_conv_x3_sk_workspace_bytes": (_I64, []),
     "hkp_absmax": (ctypes.c_int, [_I64, _P, _P, _P]),
     "hkp_weight_pack_f16": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),

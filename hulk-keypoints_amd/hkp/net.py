@@ -218,7 +218,8 @@ def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
     if isinstance(x, _PendingBN):
         wp = _pack_weight_x3(conv.weight) if x.y.dtype == torch.float32 else \
             _cached_split(conv.weight, "f16", ops.weight_pack_f16)
-        return ops.conv2d_fwd_bnin(x.y, x.ss, wp, st, pd, dl, stats=bn.training)
+        return ops.conv2d_fwd_bnin(x.y, x.ss, wp, st, pd, dl, stats=bn.training, sk=sk,
+                                   tile=_fwd_tile(conv, pol, x.y.dtype == torch.float16))
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
     if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd,
@@ -246,21 +247,28 @@ class _PendingBN:
         self.y, self.ss = y, ss
 
 
+def _fwd_tile(conv, pol, f16):
+    """The HKP_TILE_* policy _conv_fwd gives this conv's forward launch."""
+    if not f16:
+        return pol.x3_tile
+    return pol.f16_tile_1x1 if conv.weight.shape[1] == 1 else pol.f16_tile_kxk
+
+
 def _bnin_ok(conv, y, pol):
-    """The consumer conv takes its input's BN + ReLU (the halo-tile shape; the
-    full f16x3 or plain fp16 arithmetic)."""
+    """The consumer conv takes its input's BN + ReLU (ops.bnin_kernel: where the
+    unfused conv runs the halo-tile body, or, f16x3, the A3 body — so fusing
+    changes no tile and no summation order: the outputs are the unfused path's
+    bits; the full f16x3 or plain fp16 arithmetic)."""
     if not pol.fuse_input_bn:
         return False
-    if not ((y.dtype == torch.float32 and pol.passes == 3 and pol.products == 3) or
-            (y.dtype == torch.float16 and pol.passes == 1)):
+    f16 = y.dtype == torch.float16
+    if not ((not f16 and y.dtype == torch.float32 and pol.passes == 3 and pol.products == 3) or
+            (f16 and pol.passes == 1 and _f16_conv_ok(conv))):
         return False
     k, r, s, c = conv.weight.shape
     n, h, w, _ = y.shape
-    # 64 input channels: where the unfused conv runs the halo body too (the planner's
-    # default there), so fusing changes no summation order — the outputs are the
-    # unfused path's bits
-    return c == y.shape[-1] and c <= 64 and ops.bnin_shape_ok(n, h, w, c, k, r, s, _i(conv.stride),
-                                                              _i(conv.padding), _i(conv.dilation))
+    return c == y.shape[-1] and ops.bnin_kernel(n, h, w, c, k, r, s, _i(conv.stride), _i(conv.padding),
+                                                _i(conv.dilation), f16, _fwd_tile(conv, pol, f16)) is not None
 
 
 def _f16_conv_ok(conv):

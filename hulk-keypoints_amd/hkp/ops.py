@@ -217,20 +217,34 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     return y, part
 
 
-def bnin_shape_ok(n, h, w, c, k, r, s, stride, pad, dil):
-    """The fused input BN (hkp_conv2d_fwd_x3_bnin / _f16_bnin) takes the shape: the
-    halo-tile body's (stride-1 3x3, pad = dil = 1, Ho % 8 == 0, Wo % 32 == 0)."""
-    return ((r, s, stride, pad, dil) == (3, 3, 1, 1, 1) and h % 8 == 0 and w % 32 == 0 and k % 64 == 0
-            and c % 32 == 0 and n * h * w * c * 2 + 64 < (1 << 32))
+def bnin_kernel(n, h, w, c, k, r, s, stride, pad, dil, f16=False, tile=0, sk=True):
+    """The kernel a fused-input-BN conv (hkp_conv2d_fwd_x3_bnin / _f16_bnin) of this
+    shape runs, or None where it has none: the fused conv runs where the unfused
+    one runs the halo-tile body (conv_x3_halo_bnin_kernel<P>) or, f16x3, the A3
+    body (conv_x3_a3_bnin_kernel<3>) — the same tiles and summation order, so the
+    same bits."""
+    cg = 64 if f16 else 32
+    if c % cg or k % 64:
+        return None
+    try:
+        ho, wo = conv_out_hw(h, w, r, s, stride, pad, dil)
+    except HkpError:
+        return None
+    d = ConvDesc(n, h, w, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
+    name = kernel_name(d, HKP_KOP_FWD_F16 if f16 else HKP_KOP_FWD_X3, sk)
+    if name.startswith("conv_x3_halo_kernel<") or (not f16 and name == "conv_x3_a3_kernel<3>"):
+        return name.replace("_kernel<", "_bnin_kernel<")
+    return None
 
 
-def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True):
+def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True, sk=True, tile=0):
     """Inference conv whose input is the producer conv's raw output y_in with the
     producer's BN + ReLU applied inside the conv (hkp_conv2d_fwd_x3_bnin for fp32
     y_in with wp = weight_pack_x3(w); hkp_conv2d_fwd_f16_bnin for fp16 y_in with
     wp = weight_pack_f16(w)): the same y (and BN partials) as
     conv2d_fwd_x3(bn_apply(y_in, in_ss, relu, split=3)) / conv2d_fwd_f16(
-    bn_apply_f16(y_in, in_ss, relu)), bit for bit, without the apply pass."""
+    bn_apply_f16(y_in, in_ss, relu)) with the same sk / tile, bit for bit, without
+    the apply pass (shapes: bnin_kernel)."""
     ws, wsc = wp
     f16 = y_in.dtype == torch.float16
     _need(y_in, torch.float16 if f16 else torch.float32, "conv2d_fwd_bnin.y_in", 4)
@@ -243,18 +257,20 @@ def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True):
     if in_ss.numel() != 2 * c:
         raise HkpError("conv2d_fwd_bnin: in_scale_shift size %d != 2C" % in_ss.numel())
     ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
-    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, 0)
+    d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = torch.empty((n, ho, wo, k), device=y_in.device, dtype=torch.float16 if f16 else torch.float32)
     part = _stat_partials(n * ho * wo, k, y_in.device, None, "conv2d_fwd_bnin") if stats else None
     fn = "hkp_conv2d_fwd_f16_bnin" if f16 else "hkp_conv2d_fwd_x3_bnin"
 
     def launch():
-        call(fn, ctypes.byref(d), _ptr(y_in), _ptr(in_ss), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part), _stream())
+        call(fn, ctypes.byref(d), _ptr(y_in), _ptr(in_ss), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
+             *_sk_workspace(sk), _stream())
 
     if _observer is None:
         launch()
     else:
-        _observer("conv_x3_halo_bnin_kernel<%d>" % (1 if f16 else 3), 2.0 * n * ho * wo * k * r * s * c,
+        name = kernel_name(d, HKP_KOP_FWD_F16 if f16 else HKP_KOP_FWD_X3, sk).replace("_kernel<", "_bnin_kernel<")
+        _observer(name, 2.0 * n * ho * wo * k * r * s * c,
                   y_in.element_size() * y_in.numel() + 2.0 * ws.numel() + y.element_size() * y.numel(), launch)
     return y, part
 

@@ -148,17 +148,22 @@ int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, 
  * hkp_bn_finalize (or hkp_bn_finalize_ranks) of that output; the A operand is
  * relu(x * scale + shift) with bn_apply's arithmetic (two roundings), split as
  * hkp_bn_apply(split = 3) would write it — so y is bit-identical to hkp_bn_apply
- * followed by hkp_conv2d_fwd_x3.  Runs on the halo-tile body only (stride-1
- * 3x3, pad = dil = 1, Ho % 8 == 0, Wo % 32 == 0; d->tile AUTO or HALO; no
- * stream-K workspace); other shapes return HKP_ERR_BAD_ARG. */
+ * followed by hkp_conv2d_fwd_x3 with the same d->tile and workspace.  Runs
+ * where that unfused launch runs the halo-tile body (stride-1 3x3, pad = dil =
+ * 1, Ho % 8 == 0, Wo % 32 == 0) or the A3 body (256x256 tiles, one per block,
+ * with its split-K tail in the same launch: Cout % 256 == 0 and the planner's
+ * or d->tile's choice) — the kernel hkp_conv_kernel_name names for
+ * HKP_KOP_FWD_X3, with "_bnin" before "_kernel"; other launches return
+ * HKP_ERR_BAD_ARG. */
 int hkp_conv2d_fwd_x3_bnin(const hkp_conv_desc* d, const float* x_raw, const float* in_scale_shift,
                            const uint16_t* w_split, const float* w_inv_scale, float* y, float* stat_partials,
-                           hkp_stream_t stream);
+                           void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream);
 /* The plain-fp16 form (config C4): x_raw_f16 is the producer's fp16 output,
- * relu(x * scale + shift) rounded to fp16 as hkp_bn_apply_f16 writes it. */
+ * relu(x * scale + shift) rounded to fp16 as hkp_bn_apply_f16 writes it; the
+ * halo-tile body only. */
 int hkp_conv2d_fwd_f16_bnin(const hkp_conv_desc* d, const uint16_t* x_raw_f16, const float* in_scale_shift,
                             const uint16_t* w_f16, const float* w_inv_scale, uint16_t* y_f16, float* stat_partials,
-                            hkp_stream_t stream);
+                            void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream);
 /* Plain-fp16 conv (BASELINE config C4, "fp16 with MFMA"): the same LDS-DMA
  * kernel family as hkp_conv2d_fwd_x3 with one fp16 product per MAC (fp32
  * accumulation).  x_f16: NHWC fp16 [n][h][w][c] (a producer's split_passes = 1

@@ -31,6 +31,37 @@ def test_library_exports_every_declared_symbol():
     assert _lib.version().startswith("hulkkp")
 
 
+def _kernel_scratch(blob):
+    """(symbol, private_segment_fixed_size) of every gfx950 kernel in a library's
+    embedded code objects, read from the msgpack kernel metadata (uncompressed)."""
+    key = b".private_segment_fixed_size"
+    out = []
+    for m in re.finditer(re.escape(key), blob):
+        i = m.end()
+        t = blob[i]
+        size = t if t < 0x80 else int.from_bytes(blob[i + 1:i + 1 + {0xcc: 1, 0xcd: 2, 0xce: 4}[t]], "big")
+        j = blob.find(b".symbol", i, i + 4096)
+        sym = "?"
+        if j >= 0:
+            k = j + len(b".symbol")
+            if 0xa0 <= blob[k] <= 0xbf:
+                sym = blob[k + 1:k + 1 + (blob[k] & 0x1f)].decode(errors="replace")
+            elif blob[k] == 0xd9:
+                sym = blob[k + 2:k + 2 + blob[k + 1]].decode(errors="replace")
+        out.append((sym, size))
+    return out
+
+
+def test_no_kernel_uses_scratch():
+    """No kernel of libhulkkp.so spills or keeps an array in scratch (a runtime
+    accumulator index once put the 256x256 conv's whole tile there: 528 B per lane)."""
+    lib = os.path.join(REPO, "hulk-keypoints_amd", "hkp", "libhulkkp.so")
+    ks = _kernel_scratch(open(lib, "rb").read())
+    assert len(ks) >= 100
+    bad = [(s, n) for s, n in ks if n]
+    assert not bad, bad
+
+
 def test_bad_arguments_raise_not_crash():
     from hkp import _lib
     d = _lib.ConvDesc(1, 8, 8, 30, 64, 3, 3, 1, 1, 1, 0)  # Cin=30 is unsupported on the NHWC path
