@@ -739,16 +739,16 @@ def test_fused_input_bn_equals_apply_then_conv(cuda_device, case, prec):
         wp = ops.weight_pack_x3(wt)
         a = ops.bn_apply(y, ss, relu=True, split=3, keep_fp32=False)
         ref, pref = ops.conv2d_fwd_x3(a, wp, 1, 1, 1, tile=10)                 # the halo body
-        got, pgot = ops.conv2d_fwd_bnin(y, ss, wp, 1, 1, 1)
+        got, pgot = ops.conv2d_fwd_bnin(y, ss, wp, 1, 1, 1, tile=10)
     else:
         wp = ops.weight_pack_f16(wt)
         y16 = y.half()
         a = ops.bn_apply_f16(y16, ss, relu=True)
         ref, pref = ops.conv2d_fwd_f16(a, wp, 1, 1, 1, tile=10)
-        got, pgot = ops.conv2d_fwd_bnin(y16, ss, wp, 1, 1, 1)
+        got, pgot = ops.conv2d_fwd_bnin(y16, ss, wp, 1, 1, 1, tile=10)
     assert got.dtype == ref.dtype and torch.equal(got, ref)
     assert torch.equal(pgot, pref)
-    _, pnone = ops.conv2d_fwd_bnin(y if prec == "f16x3" else y.half(), ss, wp, 1, 1, 1, stats=False)
+    _, pnone = ops.conv2d_fwd_bnin(y if prec == "f16x3" else y.half(), ss, wp, 1, 1, 1, stats=False, tile=10)
     assert pnone is None
 
 
