@@ -817,12 +817,18 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         const int o_h = trow * ROW + ((tj ^ tsw) << 4), o_l = trow * ROW + (((4 + tj) ^ tsw) << 4);
         int tr_cc = ks / a.RS, tr_tap = ks - tr_cc * a.RS;   // K-step position of the next scale | shift load
         f32x4 ssc[2], ssh[2], raw[4];
+        // scale | shift of the next stage to turn, by loads the compiler does not
+        // track: the turn's counted vmcnt (they are issued before the DMA pieces)
+        // retires them.  (Compiler-tracked loads got a vmcnt(0) before every turn —
+        // its bookkeeping does not count the LDS-DMA pieces issued after them —
+        // draining the DMA issued one column earlier.)
         auto load_ss = [&]() {
             const float* p = a.in_ss + tr_cc * 32 + 8 * tj;
-            ssc[0] = *(const f32x4*)p;
-            ssc[1] = *(const f32x4*)(p + 4);
-            ssh[0] = *(const f32x4*)(p + a.C);
-            ssh[1] = *(const f32x4*)(p + a.C + 4);
+            const float* q = p + a.C;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ssc[0]) : "v"(p) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(ssc[1]) : "v"(p) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ssh[0]) : "v"(q) : "memory");
+            asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(ssh[1]) : "v"(q) : "memory");
             if (++tr_tap == a.RS) {
                 tr_tap = 0;
                 ++tr_cc;
@@ -894,7 +900,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             for (int j = 0; j < UN - 1; ++j) {
                 read_bj((j + 1) & 1, stb, j + 1);
                 mma_bj(fa, j);
-                if (j == 1) {
+                if (j == 1) {                          // own DMA of A(s+1) and its scale | shift
                     if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
                     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
                     turn_read(sa1);
@@ -902,11 +908,28 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 if (j == 3) turn_write(sa1, 0);
                 if (j == 4) turn_write(sa1, 1);
             }
+            // columns 0..6: B column j+1's reads, then column j's MFMAs; the turn's
+            // reads in column 1, its VALU spread over columns 3 and 4's MFMAs
+#pragma unroll
+            for (int j = 0; j < UN - 1; ++j) {
+                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                if (j == 1) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                if (j == 3 || j == 4) {
+#pragma unroll
+                    for (int m = 0; m < NMC; ++m) {
+                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                    }
+                    __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+                } else {
+                    __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
+                }
+            }
             if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();                             // M(s)
             if constexpr (A2) {
-                load_ss();
+                load_ss();                             // (ahead of the DMA pieces: memory clobbers)
                 issue_b();                             // B(s+2) -> B(s)'s slot
             }
             if constexpr (A3N) issue_a();              // A(s+3) -> A(s)'s slot
