@@ -797,16 +797,17 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         // rows, so its own vmcnt orders them (no barrier).  B fragments are read one
         // column ahead instead of a whole stage ahead (-48 VGPRs against the A3
         // body: room for the turn's scale | shift and raw values).  Per K-step s:
-        //   columns 0..6  MFMAs of s (A(s) fragments in registers, B(s) one column
-        //                 ahead); turn A(s+1)'s rows (wait: own DMA of A(s+1))
+        //   columns 0..3  MFMAs of s (A(s) fragments in registers, B(s) one column
+        //                 ahead), one DMA piece of A(s+2) each (into A(s-1)'s slot)
+        //   column 4      wait own DMA of A(s+1) and its scale | shift; read its rows
+        //   columns 5, 6  turn them (VALU under the MFMAs), write them back
         //   wait own DMA of B(s+1) (A(s+2) stays in flight); barrier M(s)
-        //   load A(s+2)'s scale | shift, DMA B(s+2) into B(s)'s slot and A(s+3)
-        //   into A(s)'s (both read before M(s))
+        //   load A(s+2)'s scale | shift, DMA B(s+2) into B(s)'s slot (read before M(s))
         //   column 7, then read B(s+1)'s column 0 and A(s+1)'s fragments (turned
         //   before M(s)) — their latency under the last column's MFMAs
-        // Issue order per step: scale | shift, B, A — the turn's vmcnt(GB + GA)
-        // retires A(s+1) and its scale | shift, M(s)'s vmcnt(GA) B(s+1).  A stage
-        // has ~1.3 K-steps to land, B one.
+        // VMEM issue order: A(s+2) pieces, scale | shift of A(s+2), B(s+2): the turn
+        // of A(s+1) at column 4 of step s waits vmcnt(GB + GA) (B(s+1), A(s+2) in
+        // flight), M(s) vmcnt(GA).  An A stage has ~1.1 K-steps to land, B ~1.
         constexpr int GB = GL - GA;
         char* const bring = smem + 3 * BM * ROW;
         const int w = wm * WN + wn;
@@ -867,72 +868,78 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], f.h[i], f.l[i], jh[j & 1], jl[j & 1], mfma);
         };
 
-        // prologue: A(0) turned and B(0) landed everywhere (M(-1)), then the
-        // step-0 state: scale | shift of A(1), B(1), A(2) issued; A(0) and B(0)'s
-        // column 0 in registers
-        load_ss();
+        // prologue: A(0) turned and B(0) landed everywhere (M(-1)), then the step-0
+        // state: A(1) in flight, scale | shift of A(1) and B(1) issued after it;
+        // A(0) and B(0)'s column 0 in registers
+        load_ss();                                     // of A(0)
         issue_a();                                     // A(0) -> A slot 0
         issue_b();                                     // B(0) -> B slot 0
         if (nks > 1) issue_a();                        // A(1) -> A slot 1
-        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA) : "memory");
+        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         turn_read(smem);
         turn_write(smem, 0);
         turn_write(smem, 1);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         lds_barrier();
         x3_stamp(a, 1);
         if (nks > 1) {
-            load_ss();
+            load_ss();                                 // of A(1)
             issue_b();                                 // B(1) -> B slot 1
         }
-        if (nks > 2) issue_a();                        // A(2) -> A slot 2
         FA fa;
         read_a(fa, smem);
         read_bj(0, bring, 0);
         int ca = 0, cb = 0;                            // slots of A(s), B(s)
-        // one K-step s < nks - 1; A2: s + 2 < nks (A(s+2) was issued), A3N: s + 3 < nks
-        auto kstep = [&](auto a2, auto a3n) {
-            constexpr bool A2 = decltype(a2)::value, A3N = decltype(a3n)::value;
+        // one K-step s < nks - 1; A2: s + 2 < nks (A(s+2) and B(s+2) to issue)
+        auto kstep = [&](auto a2) {
+            constexpr bool A2 = decltype(a2)::value;
             char* const sa1 = smem + (ca == 2 ? 0 : ca + 1) * (BM * ROW);        // A(s+1)
             const char* const stb = bring + cb * (BN * ROW);                     // B(s)
 #pragma unroll
             for (int j = 0; j < UN - 1; ++j) {
                 read_bj((j + 1) & 1, stb, j + 1);
                 mma_bj(fa, j);
-                if (j == 1) {                          // own DMA of A(s+1) and its scale | shift
+                if (A2 && j < GA) issue_a(j);          // A(s+2) -> A(s-1)'s slot
+                if (A2 && j == GA - 1) issue_a(GA);
+                if (j == 4) {                          // own DMA of A(s+1) and its scale | shift
                     if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
                     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
                     turn_read(sa1);
                 }
-                if (j == 3) turn_write(sa1, 0);
-                if (j == 4) turn_write(sa1, 1);
+                if (j == 5) turn_write(sa1, 0);
+                if (j == 6) turn_write(sa1, 1);
             }
-            // columns 0..6: B column j+1's reads, then column j's MFMAs; the turn's
-            // reads in column 1, its VALU spread over columns 3 and 4's MFMAs
+            // columns 0..6: column j's MFMAs with B column j+1's reads in the middle
+            // (half a column of MFMAs before the wait for them) and an A piece
+            // (0..3) at the end; the turn's reads in column 4, its VALU under
+            // columns 5, 6
 #pragma unroll
             for (int j = 0; j < UN - 1; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                if (j == 1) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                if (j == 3 || j == 4) {
+                if (j == 5 || j == 6) {
 #pragma unroll
                     for (int m = 0; m < NMC; ++m) {
                         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                         __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                        if (m == NMC / 2 - 1) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
                     }
                     __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
                 } else {
-                    __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, NMC / 2, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                    if (j == 4) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, NMC - NMC / 2, 0);
+                    if (A2 && j < GA) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
                 }
             }
             if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();                             // M(s)
             if constexpr (A2) {
-                load_ss();                             // (ahead of the DMA pieces: memory clobbers)
+                load_ss();                             // of A(s+2)   (ahead of B(s+2): memory clobbers)
                 issue_b();                             // B(s+2) -> B(s)'s slot
             }
-            if constexpr (A3N) issue_a();              // A(s+3) -> A(s)'s slot
             mma_bj(fa, UN - 1);
             read_bj(0, bring + (cb ^ 1) * (BN * ROW), 0);
             read_a(fa, sa1);
@@ -941,12 +948,8 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             cb ^= 1;
         };
         int s = 0;
-        for (; s + 3 < nks; ++s) kstep(std::true_type{}, std::true_type{});
-        if (s + 2 < nks) {
-            kstep(std::true_type{}, std::false_type{});
-            ++s;
-        }
-        if (s + 1 < nks) kstep(std::false_type{}, std::false_type{});
+        for (; s + 2 < nks; ++s) kstep(std::true_type{});
+        if (s + 1 < nks) kstep(std::false_type{});
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         {
             const char* const stb = bring + cb * (BN * ROW);
@@ -1349,15 +1352,37 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     // ahead of B — each with its own (channel group, tap) position
     int qa_buf = 0, qa_cc = q_cc, qa_tap = q_tap, qa_rr = q_rr, qa_ss = q_ss;
     int qb_buf = 0, qb_cc = q_cc, qb_tap = q_tap;
-    auto issue_a = [&]() {
+    // issue_a(): the next A stage, then the advance to the stage after it;
+    // issue_a(i), i < GA: only piece i of it; issue_a(GA): only the advance (FB
+    // spreads the pieces over a K-step's columns)
+    auto issue_a_piece = [&](int i) {
         char* st = smem + qa_buf * (BM * ROW);
         const int dh = qa_rr * a.dil, dw = qa_ss * a.dil;
         const long toff = ((long)dh * a.W + dw) * cstride + qa_cc * 64;
+        const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+        const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+        // the source select as bit arithmetic: as a pointer select, LLVM turned it
+        // into a divergent branch around each DMA piece once they were spread
+        const unsigned long mask = 0ul - (unsigned long)in;
+        const unsigned long src = ((unsigned long)(xbase + ((unsigned long)a_off[i] + toff)) & mask) |
+                                  ((unsigned long)zero & ~mask);
+        glds16((const void*)src, st + (RPI * (w * GA + i)) * ROW);
+    };
+    auto issue_a = [&](int piece = -1) {
+        if (piece >= 0 && piece < GA) {
+            issue_a_piece(piece);
+            return;
+        }
+        if (piece < 0) {
+            char* st = smem + qa_buf * (BM * ROW);
+            const int dh = qa_rr * a.dil, dw = qa_ss * a.dil;
+            const long toff = ((long)dh * a.W + dw) * cstride + qa_cc * 64;
 #pragma unroll
-        for (int i = 0; i < GA; ++i) {
-            const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
-            const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-            glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+            for (int i = 0; i < GA; ++i) {
+                const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+                const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+                glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+            }
         }
         qa_buf = qa_buf == 2 ? 0 : qa_buf + 1;
         if (++qa_ss == a.S) {

@@ -267,8 +267,11 @@ def _bnin_ok(conv, y, pol):
         return False
     k, r, s, c = conv.weight.shape
     n, h, w, _ = y.shape
-    return c == y.shape[-1] and ops.bnin_kernel(n, h, w, c, k, r, s, _i(conv.stride), _i(conv.padding),
-                                                _i(conv.dilation), f16, _fwd_tile(conv, pol, f16)) is not None
+    if c != y.shape[-1]:
+        return False
+    name = ops.bnin_kernel(n, h, w, c, k, r, s, _i(conv.stride), _i(conv.padding), _i(conv.dilation), f16,
+                           _fwd_tile(conv, pol, f16))
+    return name is not None and (pol.fuse_input_bn_a3 or not name.startswith("conv_x3_a3_"))
 
 
 def _f16_conv_ok(conv):

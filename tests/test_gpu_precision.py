@@ -821,8 +821,8 @@ def test_fused_input_bn_a3_equals_apply_then_conv(cuda_device, case):
     ("resnet34", "f16x3", 32, (480, 640), "conv_x3_a3_bnin_kernel<3>")])     # C2: layer3/4 on A3
 def test_fused_input_bn_network_bitexact(cuda_device, bb, prec, b, hw, fused):
     """Whole inference forward (128x256: a halo-tiled layer1 at 32x64; C2 640x480
-    B=32: layer3/4's conv2 on the A3 body): Policy.fuse_input_bn on == off,
-    heatmaps and argmax bit for bit, and the fused kernels ran."""
+    B=32: layer3/4's conv2 on the A3 body, Policy.fuse_input_bn_a3): fused ==
+    unfused, heatmaps and argmax bit for bit, and the fused kernels ran."""
     from hkp import net, ops
     m = _model(bb, 4, 7, cuda_device, precision=prec)
     x = recipe.to_tensor_nchw(recipe.seeded_images_u8(b, hw[0], hw[1], 8)).to(cuda_device)
@@ -836,7 +836,8 @@ def test_fused_input_bn_network_bitexact(cuda_device, bb, prec, b, hw, fused):
         ops.set_observer(observe if fuse else None)
         try:
             with torch.no_grad():
-                hm, yx = m.heatmaps_and_keypoints(x, policy=m.policy.with_(fuse_input_bn=fuse))
+                hm, yx = m.heatmaps_and_keypoints(x, policy=m.policy.with_(fuse_input_bn=fuse,
+                                                                           fuse_input_bn_a3=fuse))
         finally:
             ops.set_observer(None)
         outs.append((hm, yx))

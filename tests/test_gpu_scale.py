@@ -69,7 +69,6 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
     assert syms and all(s.startswith(("conv_x3_kernel", "conv_x3_a3_kernel", "conv_x3_halo_kernel",
                                       "conv_x3_halo_bnin_kernel", "conv_x3_a3_bnin_kernel")) for s in syms), syms
     assert "conv_x3_halo_kernel<3>" in syms and "conv_x3_halo_bnin_kernel<3>" in syms
-    assert "conv_x3_a3_bnin_kernel<3>" in syms                # layer3/4 conv2: BN applied in the A3 body
     print("conv kernels:", {s: "%.1f GFLOP" % (f / 1e9) for s, f in sorted(syms.items(), key=lambda kv: -kv[1])})
     low_err = (low.cpu().numpy() - g["lowres"]).__abs__().max()
     heat_err = (hm[0].cpu().numpy() - g["heat0"]).__abs__().max()
