@@ -556,7 +556,17 @@ def _memory_tight(dev):
     tot = _dev_total.get(dev)
     if tot is None:
         tot = _dev_total[dev] = torch.cuda.get_device_properties(dev).total_memory
-    return torch.cuda.memory_reserved(dev) > 0.75 * tot
+    # memory_reserved() builds the allocator's whole statistics dict (~10 us of
+    # host time): refreshed every 16th call
+    c = _tight_cache.setdefault(dev, [0, False])
+    if c[0] == 0:
+        c[1] = torch.cuda.memory_reserved(dev) > 0.75 * tot
+        c[0] = 16
+    c[0] -= 1
+    return c[1]
+
+
+_tight_cache = {}
 
 
 def _side_stream(dev):
@@ -603,7 +613,9 @@ def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
                 amax = ops.absmax(dy)
             dys = ops.split_pack_x3(dy, amax)
         ready = None
-        if pol.overlap_wgrad and not _memory_tight(dys.device):
+        k_, r_, s_, c_ = conv.weight.shape
+        gflop = 2e-9 * dys.numel() / (2 if dys.dtype == torch.float16 else 1) * r_ * s_ * c_
+        if pol.overlap_wgrad and gflop >= pol.overlap_min_gflop and not _memory_tight(dys.device):
             main, side = torch.cuda.current_stream(dys.device), _side_stream(dys.device)
             side.wait_stream(main)                     # dy split (and x split) written
             with torch.cuda.stream(side):

@@ -37,6 +37,10 @@ class Policy:
     # --- tuning (measured defaults) ----------------------------------------
     # a conv's wgrad runs on a side stream concurrently with its dgrad
     overlap_wgrad: bool = True
+    # ... only for convs of at least this many GFLOP per pass (2*M*K*C*R*S): below
+    # it the wgrad's one-block-per-CU grid holds the whole GPU while the dgrad
+    # waits, and the cross-stream join costs more than the overlap saves
+    overlap_min_gflop: float = 0.0
     # HKP_TILE_* of a dgrad overlapped by its wgrad (9 = 256x256 + split-K tail)
     dgrad_overlap_tile: int = 9
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over

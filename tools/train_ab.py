@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""In-process A/B of training-step policies (bench.py's C3-shard step by
+default: R34-8s K=4 640x480 B=8): one model and Trainer, the Policy switched
+between rounds, forms interleaved round-robin, wall time of `--iters` steps
+between two synchronisations; median per form (img/s).
+
+    python tools/train_ab.py "overlap_min_gflop=0" "overlap_min_gflop=20" "overlap_wgrad=0"
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "hulk-keypoints_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+
+def parse(form):
+    from hkp.policy import DEFAULT
+    kw = {}
+    for item in filter(None, form.split(",")):
+        k, _, v = item.partition("=")
+        cur = getattr(DEFAULT, k)
+        kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
+    return kw
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("forms", nargs="+", help="comma-separated FIELD=VALUE Policy overrides per form ('' = default)")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--backbone", default="resnet34")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    import hkp
+    from hkp import train as hkp_train
+    from hkp.policy import Policy
+    from oracle import recipe
+    from src.model import KeypointsGauss
+    hkp.lib()
+    dev = torch.device("cuda", 0)
+    B, K, H, W = args.batch, 4, 480, 640
+    torch.manual_seed(1234)
+    base = Policy()
+    model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=base).to(dev)
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 1234)).to(dev)
+    uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99)).to(dev)
+    trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4)
+    pols = [base.with_(**parse(f)) for f in args.forms]
+    for p in pols:                       # warm every form (kernels, caches, plans)
+        model.policy = trainer.policy = p
+        for _ in range(3):
+            trainer.step(x, uv)
+    torch.cuda.synchronize()
+    res = {f: [] for f in args.forms}
+    for _ in range(args.rounds):
+        for f, p in zip(args.forms, pols):
+            model.policy = trainer.policy = p
+            trainer.step(x, uv)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                trainer.step(x, uv)
+            torch.cuda.synchronize()
+            res[f].append(B * args.iters / (time.perf_counter() - t0))
+    for f in args.forms:
+        print("%-40s %.1f img/s  (%s)" % (f or "(default)", statistics.median(res[f]),
+                                          " ".join("%.1f" % v for v in res[f])), flush=True)
+
+
+if __name__ == "__main__":
+    main()
