@@ -692,6 +692,56 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
     }
 }
 
+// LDS access by inline asm (the FB body's K loop): issued in program order, so
+// counted lgkmcnt waits are exact; the compiler tracks none of them — a wait
+// names the registers it covers ("+v"), so nothing that reads them moves above it
+template <int OFF, typename T>
+__device__ __forceinline__ void lds_rd128(T& d, unsigned a) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "i"(OFF));
+}
+template <int OFF, typename T>
+__device__ __forceinline__ void lds_wr128(unsigned a, const T& v) {
+    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(OFF) : "memory");
+}
+template <int N, typename A, typename B>
+__device__ __forceinline__ void lgkm_wait_tie(A& a, B& b) {
+    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+template <int N, typename A, typename B, typename C, typename D, typename E, typename F>
+__device__ __forceinline__ void lgkm_wait_tie(A& a, B& b, C& c, D& d, E& e, F& f) {
+    asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f) : "n"(N) : "memory");
+}
+template <int N, typename T>
+__device__ __forceinline__ void lgkm_wait_tie(T& a0, T& a1, T& a2, T& a3, T& a4, T& a5, T& a6, T& a7, T& a8, T& a9) {
+    asm volatile("s_waitcnt lgkmcnt(%10)"
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8), "+v"(a9)
+                 : "n"(N)
+                 : "memory");
+}
+// f(std::integral_constant<int, I>) for I in [0, N)
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (I < N) {
+        f(std::integral_constant<int, I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// relu(y * s + t) (bn_apply's two roundings) of 8 fp32 values, split into fp16
+// hi and lo = fp16(x - hi): the packed f16x3 operand of one 8-channel piece
+__device__ __forceinline__ void x3_turn8(const f32x4& y0, const f32x4& y1, const f32x4 (&sc)[2],
+                                         const f32x4 (&sh)[2], f16x8& h, f16x8& l) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const float y = e < 4 ? y0[e] : y1[e - 4];
+        float x = __fadd_rn(__fmul_rn(y, sc[e >> 2][e & 3]), sh[e >> 2][e & 3]);
+        x = x > 0.f ? x : 0.f;
+        const _Float16 hv = (_Float16)x;
+        h[e] = hv;
+        l[e] = (_Float16)(x - (float)hv);
+    }
+}
+
 // Mainloop + epilogue of the 16x16x32-MFMA bodies: one k32 step per half of a
 // 128-B stage row (LDS ring, DMA issue and the swizzled rows exactly as the
 // 32x32 path).  Wave tile 64 x BN/2 = UM x UN 16x16 tiles.
@@ -846,15 +896,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         };
         auto turn_write = [&](char* slot, int k) {
             f16x8 h, l;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float y = raw[2 * k + (e >> 2)][e & 3];
-                float x = __fadd_rn(__fmul_rn(y, ssc[e >> 2][e & 3]), ssh[e >> 2][e & 3]);
-                x = x > 0.f ? x : 0.f;
-                const _Float16 hv = (_Float16)x;
-                h[e] = hv;
-                l[e] = (_Float16)(x - (float)hv);
-            }
+            x3_turn8(raw[2 * k], raw[2 * k + 1], ssc, ssh, h, l);
             *(f16x8*)(slot + k * 16 * ROW + o_h) = h;
             *(f16x8*)(slot + k * 16 * ROW + o_l) = l;
         };
@@ -892,47 +934,59 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         read_a(fa, smem);
         read_bj(0, bring, 0);
         int ca = 0, cb = 0;                            // slots of A(s), B(s)
-        // one K-step s < nks - 1; A2: s + 2 < nks (A(s+2) and B(s+2) to issue)
+        // one K-step s < nks - 1; A2: s + 2 < nks (A(s+2) and B(s+2) to issue).  Its
+        // LDS traffic is inline asm in program order (the compiler's own waits for
+        // the column reads were lgkmcnt(0) — the DMA in flight makes it treat the
+        // LDS counter as out of order — exposing each read), per column j:
+        //   read B(s) column j+1 (2 ops); wait until only those are younger than
+        //   column j's reads (+ the turn's ops issued since); MFMAs of column j
+        // column 3 ends with the turn's 4 reads, columns 5 / 6 carry its two writes.
+        const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)smem;
+        const unsigned bh0 = lds0 + 3 * BM * ROW + b_base + fo_h, bl0 = lds0 + 3 * BM * ROW + b_base + fo_l;
         auto kstep = [&](auto a2) {
             constexpr bool A2 = decltype(a2)::value;
-            char* const sa1 = smem + (ca == 2 ? 0 : ca + 1) * (BM * ROW);        // A(s+1)
-            const char* const stb = bring + cb * (BN * ROW);                     // B(s)
-#pragma unroll
-            for (int j = 0; j < UN - 1; ++j) {
-                read_bj((j + 1) & 1, stb, j + 1);
+            const int ca1 = ca == 2 ? 0 : ca + 1;
+            char* const sa1 = smem + ca1 * (BM * ROW);                           // A(s+1)
+            const unsigned ta = lds0 + ca1 * (BM * ROW);                         // its LDS offset
+            const unsigned bh = bh0 + cb * (BN * ROW), bl = bl0 + cb * (BN * ROW);    // B(s)
+            static_for<0, UN - 1>([&](auto jc) {
+                constexpr int j = decltype(jc)::value, x = (j + 1) & 1;
+                lds_rd128<(j + 1) * 16 * ROW>(jh[x], bh);
+                lds_rd128<(j + 1) * 16 * ROW>(jl[x], bl);
+                // LDS ops younger than column j's reads: column j+1's (2), the turn's
+                // reads while column 5 has not waited for them (4), its first write (2)
+                constexpr int YOUNGER = 2 + (j == 4 ? 4 : 0) + (j == 6 ? 2 : 0);
+                if constexpr (j == 0) {
+                    lgkm_wait_tie<YOUNGER>(fa.h[0], fa.l[0], fa.h[1], fa.l[1], fa.h[2], fa.l[2], fa.h[3], fa.l[3],
+                                           jh[0], jl[0]);
+                } else if constexpr (j == 5) {
+                    lgkm_wait_tie<YOUNGER>(jh[j & 1], jl[j & 1], raw[0], raw[1], raw[2], raw[3]);
+                } else {
+                    lgkm_wait_tie<YOUNGER>(jh[j & 1], jl[j & 1]);
+                }
                 mma_bj(fa, j);
-                if (A2 && j < GA) issue_a(j);          // A(s+2) -> A(s-1)'s slot
-                if (A2 && j == GA - 1) issue_a(GA);
-                if (j == 4) {                          // own DMA of A(s+1) and its scale | shift
+                if constexpr (A2 && j < GA) issue_a(j);             // A(s+2) -> A(s-1)'s slot
+                if constexpr (A2 && j == GA - 1) issue_a(GA);
+                if constexpr (j == 3) {                             // own DMA of A(s+1) and its scale | shift
                     if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
                     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
-                    turn_read(sa1);
+                    lds_rd128<0>(raw[0], ta + o_r0);
+                    lds_rd128<0>(raw[1], ta + o_r1);
+                    lds_rd128<16 * ROW>(raw[2], ta + o_r0);
+                    lds_rd128<16 * ROW>(raw[3], ta + o_r1);
                 }
-                if (j == 5) turn_write(sa1, 0);
-                if (j == 6) turn_write(sa1, 1);
-            }
-            // columns 0..6: column j's MFMAs with B column j+1's reads in the middle
-            // (half a column of MFMAs before the wait for them) and an A piece
-            // (0..3) at the end; the turn's reads in column 4, its VALU under
-            // columns 5, 6
-#pragma unroll
-            for (int j = 0; j < UN - 1; ++j) {
-                if (j == 5 || j == 6) {
-#pragma unroll
-                    for (int m = 0; m < NMC; ++m) {
-                        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                        if (m == NMC / 2 - 1) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                    }
-                    __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-                } else {
-                    __builtin_amdgcn_sched_group_barrier(0x008, NMC / 2, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                    if (j == 4) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, NMC - NMC / 2, 0);
-                    if (A2 && j < GA) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+                if constexpr (j == 5 || j == 6) {
+                    constexpr int k = j - 5;
+                    f16x8 h, l;
+                    x3_turn8(raw[2 * k], raw[2 * k + 1], ssc, ssh, h, l);
+                    lds_wr128<k * 16 * ROW>(ta + o_h, h);
+                    lds_wr128<k * 16 * ROW>(ta + o_l, l);
                 }
-            }
+                // a column is a scheduling region: its MFMAs stay between its
+                // wait and the next column's (the turn's VALU interleaves inside)
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            (void)sa1;
             if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();                             // M(s)
@@ -940,17 +994,26 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 load_ss();                             // of A(s+2)   (ahead of B(s+2): memory clobbers)
                 issue_b();                             // B(s+2) -> B(s)'s slot
             }
+            lgkm_wait_tie<0>(jh[(UN - 1) & 1], jl[(UN - 1) & 1]);     // (retired before M(s))
             mma_bj(fa, UN - 1);
-            read_bj(0, bring + (cb ^ 1) * (BN * ROW), 0);
-            read_a(fa, sa1);
-            __builtin_amdgcn_sched_barrier(0);
-            ca = ca == 2 ? 0 : ca + 1;
+            {
+                const unsigned nbh = bh0 + (cb ^ 1) * (BN * ROW), nbl = bl0 + (cb ^ 1) * (BN * ROW);
+                lds_rd128<0>(jh[0], nbh);
+                lds_rd128<0>(jl[0], nbl);
+                const unsigned fh = ta + a_base + fo_h, fl = ta + a_base + fo_l;
+                static_for<0, UM>([&](auto ic) {
+                    constexpr int i = decltype(ic)::value;
+                    lds_rd128<i * 16 * ROW>(fa.h[i], fh);
+                    lds_rd128<i * 16 * ROW>(fa.l[i], fl);
+                });
+            }
+            ca = ca1;
             cb ^= 1;
         };
         int s = 0;
         for (; s + 2 < nks; ++s) kstep(std::true_type{});
         if (s + 1 < nks) kstep(std::false_type{});
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lgkm_wait_tie<0>(fa.h[0], fa.l[0], fa.h[1], fa.l[1], fa.h[2], fa.l[2], fa.h[3], fa.l[3], jh[0], jl[0]);
         {
             const char* const stb = bring + cb * (BN * ROW);
 #pragma unroll
