@@ -870,7 +870,10 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         f32x4 ssc[2], ssh[2], raw[4];
         // scale | shift of the next stage to turn, by loads the compiler does not
         // track: the turn's counted vmcnt (they are issued before the DMA pieces)
-        // retires them.  (Compiler-tracked loads got a vmcnt(0) before every turn —
+        // retires them.  Every load's registers must stay live until that turn
+        // reads them — a load whose result is never read lets the compiler hand
+        // its registers to other values while it is in flight (an instrument build
+        // without the turn faulted on exactly that).  (Compiler-tracked loads got a vmcnt(0) before every turn —
         // its bookkeeping does not count the LDS-DMA pieces issued after them —
         // draining the DMA issued one column earlier.)
         auto load_ss = [&]() {

@@ -27,7 +27,11 @@ def main():
     ap.add_argument("--shapes", default="layer3,layer4")
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B instrument builds)")
     args = ap.parse_args()
+    if args.lib:
+        from hkp import _lib
+        _lib.use_library(os.path.abspath(args.lib))
     from hkp import ops
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(5)
