@@ -848,15 +848,16 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         // column ahead instead of a whole stage ahead (-48 VGPRs against the A3
         // body: room for the turn's scale | shift and raw values).  Per K-step s:
         //   columns 0..3  MFMAs of s (A(s) fragments in registers, B(s) one column
-        //                 ahead), one DMA piece of A(s+2) each (into A(s-1)'s slot)
-        //   column 4      wait own DMA of A(s+1) and its scale | shift; read its rows
+        //                 ahead), one DMA piece of A(s+2) each (into A(s-1)'s slot);
+        //                 after column 3's MFMAs: wait own DMA of A(s+1) and its
+        //                 scale | shift, read its rows
         //   columns 5, 6  turn them (VALU under the MFMAs), write them back
         //   wait own DMA of B(s+1) (A(s+2) stays in flight); barrier M(s)
         //   load A(s+2)'s scale | shift, DMA B(s+2) into B(s)'s slot (read before M(s))
         //   column 7, then read B(s+1)'s column 0 and A(s+1)'s fragments (turned
         //   before M(s)) — their latency under the last column's MFMAs
         // VMEM issue order: A(s+2) pieces, scale | shift of A(s+2), B(s+2): the turn
-        // of A(s+1) at column 4 of step s waits vmcnt(GB + GA) (B(s+1), A(s+2) in
+        // of A(s+1) in column 3 of step s waits vmcnt(GB + GA) (B(s+1), A(s+2) in
         // flight), M(s) vmcnt(GA).  An A stage has ~1.1 K-steps to land, B ~1.
         constexpr int GB = GL - GA;
         char* const bring = smem + 3 * BM * ROW;
