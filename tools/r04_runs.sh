@@ -1,0 +1,62 @@
+#!/bin/bash
+# The round-4 GPU recipes behind DESIGN's numbers, one per subcommand (each one
+# gpurun call; outputs under gpurun_out/<name>/):
+#   profile   round profile (tools/round_profile.sh r04_v2) + fused-BN per-conv A/B
+#             + training dgrad-tile A/B + C5 line
+#   fb        fused-input-BN parity tests, per-conv A/B (tools/bnin_ab.py), C2 A/B
+#   fb_prof   C2 kernel traces: A3 + fused BN, A3, the round-3 body
+#   host      host enqueue cost per step (tools/host_cost.py) + bench lines
+#   train_ab  training-step policy A/Bs in one process (tools/train_ab.py)
+#   final     GPU suite, smoke(), default bench line
+set -e
+export TMPDIR=/tmp
+cmd=${1:?subcommand}
+O=gpurun_out/$cmd; mkdir -p $O
+case $cmd in
+profile)
+    bash tools/round_profile.sh r04_v2
+    timeout -k 10 300 python -u tools/bnin_ab.py > gpurun_out/r04_v2/bnin_ab.log 2>&1
+    bash tools/bench_ab.sh train_a3 "--mode train" "--mode train --tune dgrad_overlap_tile=11" 2
+    timeout -k 10 600 python -u bench.py --mode train --backbone resnet50 --keypoints 8 --height 960 --width 1280 \
+        --batch 32 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
+    ;;
+fb)
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+        tests/test_gpu_precision.py -k "fused_input_bn" > $O/pytest_fb.log 2>&1
+    timeout -k 10 300 python -u tools/bnin_ab.py > $O/bnin_ab.log 2>&1
+    bash tools/bench_ab.sh fb_fuse "--tune fuse_input_bn_a3=1" "" 3 > $O/ab_fuse.txt 2>&1
+    ;;
+fb_prof)
+    i=0
+    for cfg in "--tune fuse_input_bn_a3=1" "" "--tune x3_tile=9"; do
+        i=$((i + 1))
+        timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/p$i -o run -- python3 bench.py --steps 10 \
+            --no-extras --no-cpu-baseline $cfg > $O/p$i.log 2>&1
+        DB=$O/p$i/run_results.db
+        [ -f $DB ] || DB=$(ls $O/p$i/*/run_results.db 2>/dev/null | head -1)
+        python3 tools/rocpd_stats.py $DB $O/k$i.csv --top 30 > $O/top$i.txt
+        rm -rf $O/p$i
+    done
+    ;;
+host)
+    timeout -k 10 300 python -u tools/host_cost.py --mode train --steps 10 --profile > $O/train.log 2>&1
+    timeout -k 10 300 python -u tools/host_cost.py --mode infer --steps 10 > $O/infer.log 2>&1
+    timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline > $O/bench_train.log 2>&1
+    ;;
+train_ab)
+    timeout -k 10 500 python -u tools/train_ab.py "" "overlap_min_gflop=20" "overlap_min_gflop=60" "overlap_wgrad=0" \
+        --rounds 5 --iters 10 > $O/ab_overlap.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "" "dgrad_overlap_tile=11" "dgrad_overlap_tile=0" \
+        --rounds 7 --iters 10 > $O/ab_dgrad_tile.log 2>&1
+    ;;
+final)
+    timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+    timeout -k 10 300 python -u bench.py > $O/bench.log 2>&1
+    ;;
+*)
+    echo "unknown subcommand $cmd" >&2
+    exit 2
+    ;;
+esac
+echo "$cmd ok"
