@@ -41,8 +41,11 @@ class Policy:
     # it the wgrad's one-block-per-CU grid holds the whole GPU while the dgrad
     # waits, and the cross-stream join costs more than the overlap saves
     overlap_min_gflop: float = 0.0
-    # HKP_TILE_* of a dgrad overlapped by its wgrad (9 = 256x256 + split-K tail)
-    dgrad_overlap_tile: int = 9
+    # HKP_TILE_* of a dgrad overlapped by its wgrad: 11 = the A3 256x256 body, its
+    # last partial round as whole tiles (in-process A/B on the C3 shard, 7 rounds:
+    # 464.3 img/s vs 460.9 for 9 = 2-stage 256x256 + split-K tail launch, 453.0 for
+    # the planner)
+    dgrad_overlap_tile: int = 11
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
     wgrad_overlap_cus: int = 0
