@@ -7,6 +7,7 @@
 #   fb_prof   C2 kernel traces: A3 + fused BN, A3, the round-3 body
 #   host      host enqueue cost per step (tools/host_cost.py) + bench lines
 #   train_ab  training-step policy A/Bs in one process (tools/train_ab.py)
+#   train_check  GPU suite, C3-shard bench line and kernel trace (the default policy)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -48,6 +49,17 @@ train_ab)
         --rounds 5 --iters 10 > $O/ab_overlap.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "" "dgrad_overlap_tile=11" "dgrad_overlap_tile=0" \
         --rounds 7 --iters 10 > $O/ab_dgrad_tile.log 2>&1
+    ;;
+train_check)
+    timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+    timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline > $O/bench_train.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --mode train --steps 10 \
+        --no-cpu-baseline > $O/prof.log 2>&1
+    DB=$O/prof/run_results.db
+    [ -f $DB ] || DB=$(ls $O/prof/*/run_results.db 2>/dev/null | head -1)
+    python3 tools/rocpd_stats.py $DB $O/train_kernel_stats.csv --top 25 > $O/train_kernel_top.txt
+    python3 tools/step_breakdown.py $DB --walls > $O/train_walls.txt
+    rm -rf $O/prof
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
