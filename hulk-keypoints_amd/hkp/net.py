@@ -632,7 +632,7 @@ def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
                 wfs = _cached_split(conv.weight, "flip_x3", ops.weight_flip_pack_x3)
                 tile = pol.dgrad_overlap_tile if ov else 0
                 dx = ops.conv2d_bwd_data_x3(dys, wfs, _act_shape(x), pd, dl, add=add, amax=amax,
-                                            sk=not ov or tile == 9, tile=tile)
+                                            sk=not ov or tile == 9 or pol.dgrad_overlap_sk, tile=tile)
             else:                          # stride 2: one stride-1 conv per output phase of dx
                 phs = _cached_split(conv.weight, "phase_x3", lambda t: ops.weight_phase_pack_x3(t, pd))
                 dx = ops.conv2d_bwd_data_x3_strided(dys, phs, _act_shape(x), tuple(conv.weight.shape), pd, add=add,

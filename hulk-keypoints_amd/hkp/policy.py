@@ -46,6 +46,9 @@ class Policy:
     # 464.3 img/s vs 460.9 for 9 = 2-stage 256x256 + split-K tail launch, 453.0 for
     # the planner)
     dgrad_overlap_tile: int = 11
+    # ... with the split-K workspace (the A3 grid then runs its last partial round
+    # as split-K segments inside the same launch)
+    dgrad_overlap_sk: bool = False
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
     wgrad_overlap_cus: int = 0

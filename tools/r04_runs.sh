@@ -47,8 +47,11 @@ host)
 train_ab)
     timeout -k 10 500 python -u tools/train_ab.py "" "overlap_min_gflop=20" "overlap_min_gflop=60" "overlap_wgrad=0" \
         --rounds 5 --iters 10 > $O/ab_overlap.log 2>&1
-    timeout -k 10 500 python -u tools/train_ab.py "" "dgrad_overlap_tile=11" "dgrad_overlap_tile=0" \
+    timeout -k 10 500 python -u tools/train_ab.py "dgrad_overlap_tile=9" "" "dgrad_overlap_tile=0" \
         --rounds 7 --iters 10 > $O/ab_dgrad_tile.log 2>&1
+    ;;
+train_ab_sk)
+    timeout -k 10 500 python -u tools/train_ab.py "" "dgrad_overlap_sk=1" --rounds 7 --iters 10 > $O/ab_dgrad_sk.log 2>&1
     ;;
 train_check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
