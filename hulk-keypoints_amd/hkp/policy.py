@@ -46,9 +46,10 @@ class Policy:
     # 464.3 img/s vs 460.9 for 9 = 2-stage 256x256 + split-K tail launch, 453.0 for
     # the planner)
     dgrad_overlap_tile: int = 11
-    # ... with the split-K workspace (the A3 grid then runs its last partial round
-    # as split-K segments inside the same launch)
-    dgrad_overlap_sk: bool = False
+    # ... with the split-K workspace: the A3 grid runs its last partial round as
+    # split-K segments inside the same launch (in-process A/B, 7 rounds: 455.8 vs
+    # 453.6 img/s as whole tiles)
+    dgrad_overlap_sk: bool = True
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
     wgrad_overlap_cus: int = 0
