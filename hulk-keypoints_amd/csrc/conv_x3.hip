@@ -950,8 +950,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         auto kstep = [&](auto a2) {
             constexpr bool A2 = decltype(a2)::value;
             const int ca1 = ca == 2 ? 0 : ca + 1;
-            char* const sa1 = smem + ca1 * (BM * ROW);                           // A(s+1)
-            const unsigned ta = lds0 + ca1 * (BM * ROW);                         // its LDS offset
+            const unsigned ta = lds0 + ca1 * (BM * ROW);                         // A(s+1)'s LDS offset
             const unsigned bh = bh0 + cb * (BN * ROW), bl = bl0 + cb * (BN * ROW);    // B(s)
             static_for<0, UN - 1>([&](auto jc) {
                 constexpr int j = decltype(jc)::value, x = (j + 1) & 1;
@@ -990,7 +989,6 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 // wait and the next column's (the turn's VALU interleaves inside)
                 __builtin_amdgcn_sched_barrier(0);
             });
-            (void)sa1;
             if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
             else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
             lds_barrier();                             // M(s)
