@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""In-process A/B of inference policies (bench.py's C2 step by default: R34-8s
+K=4 640x480 B=32, f16x3; --backbone resnet50 --keypoints 8 --batch 128
+--precision f16 for C4): one model, the Policy switched between rounds, forms
+interleaved round-robin, wall time of `--iters` forwards (heatmaps + argmax)
+between two synchronisations; median per form (img/s).
+
+    python tools/infer_ab.py "" "x3_tile=9"
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "hulk-keypoints_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+
+
+def parse(form):
+    from hkp.policy import DEFAULT
+    kw = {}
+    for item in filter(None, form.split(",")):
+        k, _, v = item.partition("=")
+        cur = getattr(DEFAULT, k)
+        kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
+    return kw
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("forms", nargs="+", help="comma-separated FIELD=VALUE Policy overrides per form ('' = default)")
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--backbone", default="resnet34")
+    ap.add_argument("--keypoints", type=int, default=4)
+    ap.add_argument("--precision", default="f16x3")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    import hkp
+    from hkp.policy import Policy
+    from oracle import recipe
+    from src.model import KeypointsGauss
+    hkp.lib()
+    dev = torch.device("cuda", 0)
+    B, K, H, W = args.batch, args.keypoints, 480, 640
+    torch.manual_seed(1234)
+    base = Policy(precision=args.precision)
+    model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=base).to(dev)
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, 1234)).to(dev)
+
+    def step():
+        with torch.no_grad():
+            return model.heatmaps_and_keypoints(x)
+    pols = [base.with_(**parse(f)) for f in args.forms]
+    for p in pols:                       # warm every form (kernels, caches, plans)
+        model.policy = p
+        for _ in range(3):
+            step()
+    torch.cuda.synchronize()
+    res = {f: [] for f in args.forms}
+    for _ in range(args.rounds):
+        for f, p in zip(args.forms, pols):
+            model.policy = p
+            step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                step()
+            torch.cuda.synchronize()
+            res[f].append(B * args.iters / (time.perf_counter() - t0))
+    for f in args.forms:
+        print("%-40s %.1f img/s  (%s)" % (f or "(default)", statistics.median(res[f]),
+                                          " ".join("%.1f" % v for v in res[f])), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -8,6 +8,8 @@
 #   host      host enqueue cost per step (tools/host_cost.py) + bench lines
 #   train_ab  training-step policy A/Bs in one process (tools/train_ab.py)
 #   train_check  GPU suite, C3-shard bench line and kernel trace (the default policy)
+#   infer_ab  C2 / C4 inference policy A/Bs in one process (tools/infer_ab.py): the A3
+#             body vs the 2-stage body + tail launch, the fused input BN on / off
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -52,6 +54,12 @@ train_ab)
     ;;
 train_ab_sk)
     timeout -k 10 500 python -u tools/train_ab.py "" "dgrad_overlap_sk=1" --rounds 7 --iters 10 > $O/ab_dgrad_sk.log 2>&1
+    ;;
+infer_ab)
+    timeout -k 10 400 python -u tools/infer_ab.py "" "x3_tile=9" "fuse_input_bn=0" --rounds 7 --iters 10 \
+        > $O/ab_c2.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "" "f16_tile_1x1=9,f16_tile_kxk=9" --backbone resnet50 --keypoints 8 \
+        --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 train_check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
