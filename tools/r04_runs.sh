@@ -8,6 +8,7 @@
 #   host      host enqueue cost per step (tools/host_cost.py) + bench lines
 #   train_ab  training-step policy A/Bs in one process (tools/train_ab.py)
 #   train_check  GPU suite, C3-shard bench line and kernel trace (the default policy)
+#   knobs     C2 / C4 BN-finalize two-level threshold A/B (tools/infer_ab.py)
 #   infer_ab  C2 / C4 inference policy A/Bs in one process (tools/infer_ab.py): the A3
 #             body vs the 2-stage body + tail launch, the fused input BN on / off
 #   final     GPU suite, smoke(), default bench line
@@ -60,6 +61,12 @@ infer_ab)
         > $O/ab_c2.log 2>&1
     timeout -k 10 400 python -u tools/infer_ab.py "" "f16_tile_1x1=9,f16_tile_kxk=9" --backbone resnet50 --keypoints 8 \
         --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+knobs)
+    timeout -k 10 400 python -u tools/infer_ab.py "" "fin_two_level_tiles=512" "fin_two_level_tiles=8192" \
+        --rounds 5 --iters 10 > $O/ab_c2_fin.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "" "fin_two_level_tiles=512" "fin_two_level_tiles=8192" \
+        --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4_fin.log 2>&1
     ;;
 train_check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
