@@ -8,6 +8,7 @@
 #   host      host enqueue cost per step (tools/host_cost.py) + bench lines
 #   train_ab  training-step policy A/Bs in one process (tools/train_ab.py)
 #   train_check  GPU suite, C3-shard bench line and kernel trace (the default policy)
+#   c4_fuse   C4 with / without the halo-stage fused input BN (tools/infer_ab.py)
 #   knobs     C2 / C4 BN-finalize two-level threshold A/B (tools/infer_ab.py)
 #   infer_ab  C2 / C4 inference policy A/Bs in one process (tools/infer_ab.py): the A3
 #             body vs the 2-stage body + tail launch, the fused input BN on / off
@@ -67,6 +68,10 @@ knobs)
         --rounds 5 --iters 10 > $O/ab_c2_fin.log 2>&1
     timeout -k 10 400 python -u tools/infer_ab.py "" "fin_two_level_tiles=512" "fin_two_level_tiles=8192" \
         --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4_fin.log 2>&1
+    ;;
+c4_fuse)
+    timeout -k 10 400 python -u tools/infer_ab.py "" "fuse_input_bn=0" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4_fuse.log 2>&1
     ;;
 train_check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
