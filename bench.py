@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--mode", choices=["infer", "train"], default="infer")
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default 32 infer / 8 train)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: the job's batch, split over the N ranks (per-rank batch = G/N; rank r "
+                         "takes images [r*G/N, (r+1)*G/N) of the seeded G-image batch)")
     ap.add_argument("--backbone", default="resnet34")
     ap.add_argument("--keypoints", type=int, default=4)
     ap.add_argument("--height", type=int, default=480)
@@ -319,11 +322,18 @@ def cpu_baseline(args, budget_s):
             "legs": legs}
 
 
-def workload_name(mode, backbone, k, h, w, precision, batch):
+def workload_name(mode, backbone, k, h, w, precision, batch, global_batch=None, world=1):
     """The BASELINE.json config a bench line measures (C2..C5; C3/C5 per-GPU shards of
-    their DP jobs), or "custom" with its shape."""
+    their DP jobs; north_star's strong-scaling batch-64 C2 inference), or "custom"
+    with its shape."""
     shape = (mode, backbone, k, w, h)
-    if shape == ("infer", "resnet34", 4, 640, 480) and batch == 32 and precision != "f16":
+    fp32_class = precision in ("fp32", "f16x3")
+    if global_batch:
+        if shape == ("infer", "resnet34", 4, 640, 480) and global_batch == NORTH_STAR_GLOBAL_BATCH and fp32_class:
+            return "north_star scaling: C2 batch %d over %d GPU(s)" % (global_batch, world)
+        return "custom strong-scaling %s (global batch %d)" % ("inference" if mode == "infer" else "training",
+                                                               global_batch)
+    if shape == ("infer", "resnet34", 4, 640, 480) and batch == 32 and fp32_class:
         return "C2 inference"
     if shape == ("train", "resnet34", 4, 640, 480) and batch == 8:
         return "C3 shard (batch 64 over 8 GPUs) training step"
@@ -336,8 +346,35 @@ def workload_name(mode, backbone, k, h, w, precision, batch):
     return "custom %s" % ("inference" if mode == "infer" else "training step")
 
 
-def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
-    """Time `steps` steps of one workload; return its metrics (rank 0 gets them)."""
+NORTH_STAR_GLOBAL_BATCH = 64      # north_star: ">=6x ... 1->8 GPUs on 640x480 batch-64 inference"
+
+
+def north_star_leg(precision, args, dev, rank, world):
+    """north_star's scaling workload: C2 inference (R34-8s K=4 640x480) on a 64-image
+    batch split over the ranks (strong scaling; rank r takes images [r*64/N,
+    (r+1)*64/N) of the seeded batch; train-mode BN per rank = a per-shard run of the
+    reference).  On one GPU it also times the 8-image shard the batch puts
+    on each rank at N = 8, whose rate bounds the 1 -> 8 speedup from compute:
+    8 * img/s(B=8) / img/s(B=64) (the all-gather of 2 KB of keypoints aside)."""
+    G = NORTH_STAR_GLOBAL_BATCH
+    leg = run_leg("infer", precision, G // world, args, dev, rank, world, args.steps, args.warmup,
+                  shard_of=(G, rank))
+    leg["workload"] = "north_star scaling: C2 batch %d over %d GPU(s) (R34-8s K=4 640x480, %d images per rank, " \
+                      "per-rank train-mode BN, keypoints all-gathered at N>1)" % (G, world, G // world)
+    leg["scaling"] = "strong"
+    if world == 1:
+        b8 = run_leg("infer", precision, G // 8, args, dev, rank, 1, args.steps, args.warmup, shard_of=(G, 7))
+        leg["shard_b8"] = {"value": b8["value"], "ms_per_step": b8["ms_per_step"],
+                           "images": "images 56-63 of the seeded 64-image batch (rank 7's shard at N = 8)",
+                           "dominant_kernel": b8["roofline"]["kernel"], "frac": b8["roofline"]["frac"]}
+        leg["predicted_speedup_1to8_compute_ceiling"] = 8.0 * b8["value"] / leg["value"]
+    return leg
+
+
+def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard_of=None):
+    """Time `steps` steps of one workload; return its metrics (rank 0 gets them).
+    shard_of = (G, i): the images are slice i (batch images) of the seeded G-image
+    batch (a strong-scaling shard); default: each rank's own seeded batch."""
     import hkp
     from hkp import ops, parallel
     from hkp.policy import Policy
@@ -351,7 +388,11 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
     torch.manual_seed(1234 + rank)
     pol = Policy(precision=precision, **tuning(args))
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=pol).to(dev)
-    imgs = recipe.seeded_images_u8(B, H, W, 1234 + rank)
+    if shard_of is not None:
+        G, i = shard_of
+        imgs = recipe.seeded_images_u8(G, H, W, 1234)[i * B:(i + 1) * B]
+    else:
+        imgs = recipe.seeded_images_u8(B, H, W, 1234 + rank)
     x = recipe.to_tensor_nchw(imgs).to(dev) if args.input == "f32" else torch.from_numpy(imgs).to(dev)
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99 + rank)).to(dev)
 
@@ -370,8 +411,8 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup):
         from hkp import train as hkp_train
         trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4, distributed=dist, sync_bn=sync_bn)
 
-        def step():
-            return trainer.step(x, uv)
+        def step():      # (SyncBN: equal shards of the global batch, no per-step host collective)
+            return trainer.step(x, uv, global_batch=B * world if sync_bn else None)
 
     timer = LaunchTimer()
     for _ in range(warmup):
@@ -500,13 +541,23 @@ def main():
             torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     precision = args.precision or "f16x3"
-    batch = args.batch or (32 if args.mode == "infer" else 8)
+    shard = None
+    if args.global_batch:
+        if args.global_batch % world or args.batch:
+            print("bench.py: --global-batch %d must split evenly over %d rank(s) and excludes --batch"
+                  % (args.global_batch, world), file=sys.stderr)
+            sys.exit(2)
+        batch, shard = args.global_batch // world, (args.global_batch, rank)
+    else:
+        batch = args.batch or (32 if args.mode == "infer" else 8)
 
-    main_leg = run_leg(args.mode, precision, batch, args, dev, rank, world, args.steps, args.warmup)
+    main_leg = run_leg(args.mode, precision, batch, args, dev, rank, world, args.steps, args.warmup, shard_of=shard)
     extras = {}
     default_c2 = (args.mode, args.backbone, args.keypoints, args.height, args.width) == \
         ("infer", "resnet34", 4, 480, 640)
-    if not args.no_extras and default_c2:
+    if not args.no_extras and default_c2 and not args.global_batch and NORTH_STAR_GLOBAL_BATCH % world == 0:
+        extras["north_star_scaling"] = north_star_leg(precision, args, dev, rank, world)
+    if not args.no_extras and default_c2 and not args.global_batch:
         extras["train"] = run_leg("train", precision, 8, args, dev, rank, world, args.steps, args.warmup)
         extras["train"]["workload"] = "training step (C3 shard) resnet34-8s K=4 640x480 batch 8/GPU " \
                                       "(BCE fp64, backward, RCCL grad all-reduce at N>1, FusedAdam lr1e-4 wd1e-4)"
@@ -525,10 +576,12 @@ def main():
     out = {
         "metric": "images/sec (640x480, N keypoints) inference+train at 1/2/4/8 MI355X",
         "value": main_leg["value"], "unit": "images/sec", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": main_leg["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": main_leg["ms_per_step"], "higher_is_better": True,
+        "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None, "dtype": dtype, "data": "synthetic (seeded uint8 BGR images; random-init weights)",
         "config": {"workload": "%s: %s-8s K=%d %dx%d %s batch %d/GPU (%s)" % (
-            workload_name(args.mode, args.backbone, args.keypoints, args.height, args.width, precision, B),
+            workload_name(args.mode, args.backbone, args.keypoints, args.height, args.width, precision, B,
+                          args.global_batch, world),
             args.backbone, args.keypoints, args.width, args.height, precision,
             B, "train-mode BN, fused K-ch head, heatmap + argmax, keypoints all-gathered at N>1"
             if args.mode == "infer" else "BCE fp64, Adam lr1e-4 wd1e-4"),

@@ -88,40 +88,85 @@ def host_group(group=None):
     return _HOST_GROUPS[key]
 
 
+_LIKE_GROUPS = {}
+
+
 def new_group_like(group=None):
-    """A separate communicator over the same ranks and backend as `group`.
+    """A separate communicator over the same ranks and backend as `group`, created
+    once per (rank set, backend) and cached (every Trainer(sync_bn=True) over the
+    same ranks shares it; communicators are never leaked per Trainer).
     Trainer(sync_bn=True) runs the SyncBN statistics gathers on one: RCCL runs the
     collectives of one communicator in issue order, so on the gradient buckets'
     communicator every backward BN gather would queue behind the in-flight 32 MB
-    bucket all-reduce and put it back on the critical path.  Collective over the
-    default group (dist.new_group)."""
-    return dist.new_group(_ranks(group), backend=dist.get_backend(group))
+    bucket all-reduce and put it back on the critical path.  The first call for a
+    rank set is collective over the default group (dist.new_group)."""
+    key = (tuple(_ranks(group)), str(dist.get_backend(group)))
+    if key not in _LIKE_GROUPS:
+        _LIKE_GROUPS[key] = dist.new_group(list(key[0]), backend=key[1])
+    return _LIKE_GROUPS[key]
+
+
+class ShardCheck:
+    """The SyncBN empty-shard guard of a Trainer.  Given the job's batch size
+    (`global_batch`: the same on every rank, sharded by shard_range) it needs no
+    collective at all: every rank holds >= 1 image iff global_batch >= world, a
+    value all ranks know — so a SyncBN step of the bench or of a sampler-fed loop
+    runs no host round trip.  Without it, one check_shards collective per step:
+    a rank cannot skip on its own (a cache of "sizes already seen" would let the
+    ranks whose size did not change skip while the one whose did waits in the
+    collective forever)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.collectives = 0            # host collectives run (tests)
+
+    def __call__(self, n_local, global_batch=None):
+        if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
+            return
+        n = dist.get_world_size(self.group)
+        if global_batch is not None:
+            lo, hi = shard_range(int(global_batch), _ranks(self.group).index(dist.get_rank()), n)
+            if int(global_batch) < n:
+                raise ValueError("SyncBN needs at least one image on every rank (global batch %d < world size %d)"
+                                 % (global_batch, n))
+            if int(n_local) != hi - lo:
+                raise ValueError("SyncBN: this rank holds %d images, its shard_range share of the global batch %d "
+                                 "is %d" % (n_local, global_batch, hi - lo))
+            return
+        check_shards(n_local, self.group)
+        self.collectives += 1
 
 
 def check_shards(n_local, group=None):
-    """Every rank holds at least one image (min over ranks, one tiny collective).
-    A SyncBN forward or backward with an empty shard would leave the other ranks
-    waiting in their statistics gathers forever, so every rank raises instead.
-    The min runs on a gloo group over host memory (host_group): no GPU sync, so
-    the host keeps queuing the step's kernels ahead of the GPU."""
+    """Every rank holds at least one image (one tiny host collective: the shard
+    sizes all-gathered).  A SyncBN forward or backward with an empty shard would
+    leave the other ranks waiting in their statistics gathers forever, so every
+    rank raises instead.  The gather runs on a gloo group over host memory
+    (host_group): no GPU sync, so the host keeps queuing the step's kernels ahead
+    of the GPU.  Returns every rank's size, in rank order."""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
-        return
+        return [int(n_local)]
+    n = dist.get_world_size(group)
     t = torch.tensor([int(n_local)], dtype=torch.int64)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group(group))
-    if int(t.item()) < 1:
-        raise ValueError("SyncBN needs at least one image on every rank (global batch < world size %d)"
-                         % dist.get_world_size(group))
+    parts = [torch.empty_like(t) for _ in range(n)]
+    dist.all_gather(parts, t, group=host_group(group))
+    sizes = [int(p.item()) for p in parts]
+    if min(sizes) < 1:
+        raise ValueError("SyncBN needs at least one image on every rank (global batch < world size %d)" % n)
+    return sizes
 
 
 @torch.no_grad()
-def predict_keypoints_dp(model, x_shard, heat=False, sync=False, group=None):
+def predict_keypoints_dp(model, x_shard, heat=False, sync=False, group=None, global_batch=None):
     """Each rank's shard through the fused forward (+ argmax); keypoints gathered.
     sync: BN statistics over the whole sharded batch of `group` (SyncBN, below) —
-    the result then equals one forward over the global batch.
+    the result then equals one forward over the global batch.  global_batch (the
+    same on every rank; x_shard its shard_range share) spares the empty-shard
+    guard its host collective (ShardCheck).
     Returns (global int32 [B, K, 2], this rank's heatmaps or None)."""
     pol = model.policy.with_(sync_bn=True, sync_group=group) if sync else model.policy
     if sync:
-        check_shards(x_shard.shape[0], group)
+        ShardCheck(group)(x_shard.shape[0], global_batch)
     if heat:
         hm, yx = model.heatmaps_and_keypoints(x_shard, policy=pol)
     else:

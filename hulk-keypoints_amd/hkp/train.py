@@ -142,8 +142,15 @@ class Trainer:
         # SyncBN gathers on their own communicator over the same ranks (RCCL orders
         # the collectives of one communicator by issue, so the 33 + 33 per-step R34
         # BN gathers would otherwise wait behind in-flight gradient buckets)
-        self.bn_group = parallel.new_group_like(group) \
-            if sync_bn and dist.is_initialized() and dist.get_world_size(group) > 1 else group
+        multi = sync_bn and dist.is_initialized() and dist.get_world_size(group) > 1
+        self.bn_group = parallel.new_group_like(group) if multi else group
+        # the empty-shard check's host (gloo) group, created here — collectively, on
+        # every rank, next to the communicator above — never lazily inside a step
+        # (dist.new_group is collective over the default group: ranks outside a
+        # subgroup would never make the call)
+        if multi:
+            parallel.host_group(group)
+        self.shard_check = parallel.ShardCheck(group)
         self.policy = model.policy.with_(sync_bn=True, sync_group=self.bn_group) if sync_bn else model.policy
         self.params = list(model.parameters())
         self.loss_kind = loss
@@ -158,9 +165,12 @@ class Trainer:
         self.bucketer = GradBucketer(self.params, bucket_mb << 20, group=group) if (use_dp or force_buckets) \
             else None
 
-    def forward_backward(self, x, uv=None, target=None):
+    def forward_backward(self, x, uv=None, target=None, global_batch=None):
+        """global_batch (SyncBN): the job's batch size — the same on every rank, x
+        being this rank's hkp.parallel.shard_range share of it; lets the empty-shard
+        guard run without a host collective (parallel.ShardCheck)."""
         if self.sync_bn:
-            parallel.check_shards(x.shape[0], self.group)
+            self.shard_check(x.shape[0], global_batch)
         m = self.model
         trace = net.Trace(self.policy)
         hm, _, _ = net.keypoints_forward(m.resnet.net, x, m.num_keypoints, heat=True, trace=trace)
@@ -174,7 +184,7 @@ class Trainer:
                 p.grad = grads[p]
         return loss
 
-    def step(self, x, uv=None, target=None):
-        loss = self.forward_backward(x, uv, target)
+    def step(self, x, uv=None, target=None, global_batch=None):
+        loss = self.forward_backward(x, uv, target, global_batch)
         self.opt.step()
         return loss

@@ -163,11 +163,17 @@ def heat_from_lowres(low_k, size):
     return torch.sigmoid(nn.functional.upsample_bilinear(input=low_k, size=size))
 
 
-def fwd_batch_case(name, backbone, k, B, H, W, wseed, iseed):
+def fwd_batch_case(name, backbone, k, B, H, W, wseed, iseed, shard_of=None):
     """Forward at a bench-size batch (BASELINE config C2: R34 K4 640x480 B=32):
     train-mode BN over the whole batch, as analysis.py / Prediction.predict run it.
-    Images are not stored (29 MB); the fixture keeps their digest."""
-    imgs = recipe.seeded_images_u8(B, H, W, iseed)
+    Images are not stored (29 MB); the fixture keeps their digest.  shard_of =
+    (G, i): the batch is slice i of the seeded G-image batch — one rank's shard of
+    a data-parallel job, whose BN statistics are the shard's own."""
+    if shard_of is None:
+        imgs = recipe.seeded_images_u8(B, H, W, iseed)
+    else:
+        G, i = shard_of
+        imgs = np.ascontiguousarray(recipe.seeded_images_u8(G, H, W, iseed)[i * B:(i + 1) * B])
     x = recipe.to_tensor_nchw(imgs)
     m = build(backbone, k, wseed)
     with torch.no_grad():
@@ -177,6 +183,7 @@ def fwd_batch_case(name, backbone, k, B, H, W, wseed, iseed):
     h = heat.numpy()
     out = dict(backbone=np.array(backbone), k=np.int32(k), wseed=np.int32(wseed), iseed=np.int32(iseed),
                batch=np.int32(B), height=np.int32(H), width=np.int32(W), images_sha256=image_digest(imgs),
+               shard_of=np.array(shard_of if shard_of else (B, 0), dtype=np.int32),
                lowres=low.numpy().astype(np.float32),
                argmax_yx=np.array([[np.unravel_index(h[b, j].argmax(), h[b, j].shape) for j in range(k)]
                                    for b in range(B)], dtype=np.int32),
@@ -344,6 +351,11 @@ if __name__ == "__main__":
         check_slice_first_head()
         # BASELINE config C2 at the bench's batch
         fwd_batch_case("fwd_r34_k4_480x640_b32", "resnet34", 4, 32, 480, 640, wseed=10, iseed=20)
+    if want("fwd_r34_k4_480x640_b8_shard7"):
+        # north_star's scaling workload (640x480 batch-64 inference over 8 GPUs): the
+        # 8-image shard of rank 7 (images 56-63 of the 64-image batch), per-shard BN
+        fwd_batch_case("fwd_r34_k4_480x640_b8_shard7", "resnet34", 4, 8, 480, 640, wseed=10, iseed=1234,
+                       shard_of=(64, 7))
     if want("fwd_r50_k8_480x640_b2"):
         # BASELINE config C4's network (R50-8s, K=8) at the bench resolution
         fwd_subsampled_case("fwd_r50_k8_480x640_b2", "resnet50", 8, 2, 480, 640, wseed=30, iseed=31)

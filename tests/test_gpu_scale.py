@@ -41,14 +41,37 @@ def _model(bb, k, wseed, dev, precision="f16x3"):
     return m.to(dev)
 
 
+def _fixture_images(g):
+    """The fixture's uint8 batch, regenerated from its seed (slice i of a G-image
+    batch for a data-parallel shard) and checked against the stored digest."""
+    B, H, W = int(g["batch"]), int(g["height"]), int(g["width"])
+    G, i = (int(v) for v in g["shard_of"]) if "shard_of" in g else (B, 0)
+    imgs = np.ascontiguousarray(recipe.seeded_images_u8(G, H, W, int(g["iseed"]))[i * B:(i + 1) * B])
+    assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
+    return imgs
+
+
 @pytest.mark.parametrize("inp", ["f32", "u8"])
 def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
     """bench.py's default workload (and its --input u8 variant) vs the reference."""
+    syms = _c2_batch_vs_reference(cuda_device, golden("fwd_r34_k4_480x640_b32"), inp)
+    # the kernel bench.py's roofline prices (C2's dominant symbol: layer3 / layer4's
+    # 256x256 one-tile convs) is the one that ran
+    assert "conv_x3_a3_kernel<3>" in syms, syms
+
+
+def test_north_star_shard_b8_matches_reference(cuda_device, golden):
+    """north_star's scaling workload (640x480 batch-64 inference over 8 GPUs): one
+    rank's 8-image shard — images 56-63 of the 64-image batch bench.py's
+    north_star leg runs — vs the reference run on that shard alone (per-shard
+    train-mode BN), at the tile plan the 38,400-row layers get."""
+    _c2_batch_vs_reference(cuda_device, golden("fwd_r34_k4_480x640_b8_shard7"), "f32")
+
+
+def _c2_batch_vs_reference(cuda_device, g, inp):
     from hkp import net, ops
-    g = golden("fwd_r34_k4_480x640_b32")
     B, H, W, K = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["k"])
-    imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))
-    assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
+    imgs = _fixture_images(g)
     m = _model("resnet34", K, int(g["wseed"]), cuda_device)
     x = recipe.to_tensor_nchw(imgs).to(cuda_device) if inp == "f32" else torch.from_numpy(imgs).to(cuda_device)
     syms = {}
@@ -72,8 +95,8 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
     print("conv kernels:", {s: "%.1f GFLOP" % (f / 1e9) for s, f in sorted(syms.items(), key=lambda kv: -kv[1])})
     low_err = (low.cpu().numpy() - g["lowres"]).__abs__().max()
     heat_err = (hm[0].cpu().numpy() - g["heat0"]).__abs__().max()
-    print("C2 B=32: lowres max err %.3g, heat[0] max err %.3g, min argmax margin %.3g"
-          % (low_err, heat_err, g["margin"].min()))
+    print("C2 B=%d: lowres max err %.3g, heat[0] max err %.3g, min argmax margin %.3g"
+          % (B, low_err, heat_err, g["margin"].min()))
     assert low_err < 1e-4
     assert heat_err < 1e-3                                  # north_star: 1e-3 abs per pixel
     np.testing.assert_allclose(hm.double().sum(3).cpu().numpy(), g["heat_row_sum"], rtol=1e-4)
@@ -83,6 +106,7 @@ def test_c2_bench_batch_matches_reference(cuda_device, golden, inp):
                                rtol=1e-4)
     rm = sum(float(v.double().sum()) for kk, v in sd.items() if kk.endswith("running_mean"))
     assert abs(rm - g["running_checksum"][0]) < 1e-4 * max(1.0, abs(rm))
+    return syms
 
 
 # ---------------------------------------------------------------- C5 sampled

@@ -481,3 +481,9 @@ def test_bench_names_each_config():
     assert n("train", "resnet50", 8, 960, 1280, "f16x3", 32).startswith("C5")
     assert n("train", "resnet18", 2, 240, 320, "f16x3", 4).startswith("C1")
     assert n("infer", "resnet50", 8, 480, 640, "f16x3", 128).startswith("custom")
+    # the two-product precision modes are not fp32-class: never reported as C2
+    assert n("infer", "resnet34", 4, 480, 640, "f16x2w", 32).startswith("custom")
+    assert n("infer", "resnet34", 4, 480, 640, "f16x2a", 32).startswith("custom")
+    # north_star's strong-scaling workload: C2 on a 64-image batch split over the ranks
+    assert n("infer", "resnet34", 4, 480, 640, "f16x3", 8, 64, 8).startswith("north_star scaling: C2 batch 64 over 8")
+    assert n("infer", "resnet34", 4, 480, 640, "f16", 8, 64, 8).startswith("custom strong")

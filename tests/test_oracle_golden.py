@@ -114,14 +114,17 @@ def test_train_step_matches_reference(golden, case):
         break  # Adam state is per-call in train_step; step-0 grads pin the math
 
 
-def test_forward_bench_batch_matches_reference(golden):
+@pytest.mark.parametrize("case", ["fwd_r34_k4_480x640_b32", "fwd_r34_k4_480x640_b8_shard7"])
+def test_forward_bench_batch_matches_reference(golden, case):
     """BASELINE config C2 at the bench's own batch (R34 K4 640x480, B=32, train-mode
-    BN over the batch): the oracle reproduces the reference's logits, heatmap,
-    argmax and running statistics.  The fixture stores the images' digest only."""
+    BN over the batch), and north_star's scaling shard (images 56-63 of the 64-image
+    batch, per-shard BN): the oracle reproduces the reference's logits, heatmap,
+    argmax and running statistics.  The fixtures store the images' digest only."""
     import hashlib
-    g = golden("fwd_r34_k4_480x640_b32")
+    g = golden(case)
     B, H, W = int(g["batch"]), int(g["height"]), int(g["width"])
-    imgs = recipe.seeded_images_u8(B, H, W, int(g["iseed"]))
+    G, i = (int(v) for v in g["shard_of"]) if "shard_of" in g else (B, 0)
+    imgs = np.ascontiguousarray(recipe.seeded_images_u8(G, H, W, int(g["iseed"]))[i * B:(i + 1) * B])
     assert hashlib.sha256(imgs.tobytes()).hexdigest() == str(g["images_sha256"])
     sd = recipe.seeded_state_dict("resnet34", int(g["wseed"]))
     with torch.no_grad():

@@ -117,6 +117,22 @@ def _groups_worker(rank, world, port, q):
     ok &= not t.bucketer.avg_in_collective        # gloo has no ReduceOp.AVG: sum, then 1/world
     t2 = train.Trainer(m, distributed=True, optimizer="torch", sync_bn=False, bucket_mb=1)
     ok &= t2.bn_group is t2.group is None          # no SyncBN: no extra communicator
+    t3 = train.Trainer(m, distributed=True, optimizer="torch", sync_bn=True, bucket_mb=1)
+    ok &= t3.bn_group is t.bn_group                # one cached communicator per rank set, not one per Trainer
+    # the empty-shard guard: no host collective over N SyncBN steps that name their
+    # global batch (shard_range shares: 7 images -> 4 + 3), one per step otherwise
+    for _ in range(5):
+        t.shard_check(4 - rank, global_batch=7)
+    ok &= t.shard_check.collectives == 0
+    for _ in range(2):
+        t.shard_check(4 - rank)
+    ok &= t.shard_check.collectives == 2
+    for bad in ((1 - rank, 1), (5, 7)):       # global batch < world; a share that is not shard_range's
+        try:
+            t.shard_check(*bad)
+            ok = False
+        except ValueError:
+            pass
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
