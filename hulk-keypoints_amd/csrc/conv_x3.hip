@@ -692,56 +692,6 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
     }
 }
 
-// LDS access by inline asm (the FB body's K loop): issued in program order, so
-// counted lgkmcnt waits are exact; the compiler tracks none of them — a wait
-// names the registers it covers ("+v"), so nothing that reads them moves above it
-template <int OFF, typename T>
-__device__ __forceinline__ void lds_rd128(T& d, unsigned a) {
-    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(d) : "v"(a), "i"(OFF));
-}
-template <int OFF, typename T>
-__device__ __forceinline__ void lds_wr128(unsigned a, const T& v) {
-    asm volatile("ds_write_b128 %0, %1 offset:%2" ::"v"(a), "v"(v), "i"(OFF) : "memory");
-}
-template <int N, typename A, typename B>
-__device__ __forceinline__ void lgkm_wait_tie(A& a, B& b) {
-    asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
-}
-template <int N, typename A, typename B, typename C, typename D, typename E, typename F>
-__device__ __forceinline__ void lgkm_wait_tie(A& a, B& b, C& c, D& d, E& e, F& f) {
-    asm volatile("s_waitcnt lgkmcnt(%6)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f) : "n"(N) : "memory");
-}
-template <int N, typename T>
-__device__ __forceinline__ void lgkm_wait_tie(T& a0, T& a1, T& a2, T& a3, T& a4, T& a5, T& a6, T& a7, T& a8, T& a9) {
-    asm volatile("s_waitcnt lgkmcnt(%10)"
-                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7), "+v"(a8), "+v"(a9)
-                 : "n"(N)
-                 : "memory");
-}
-// f(std::integral_constant<int, I>) for I in [0, N)
-template <int I, int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-    if constexpr (I < N) {
-        f(std::integral_constant<int, I>{});
-        static_for<I + 1, N>(f);
-    }
-}
-
-// relu(y * s + t) (bn_apply's two roundings) of 8 fp32 values, split into fp16
-// hi and lo = fp16(x - hi): the packed f16x3 operand of one 8-channel piece
-__device__ __forceinline__ void x3_turn8(const f32x4& y0, const f32x4& y1, const f32x4 (&sc)[2],
-                                         const f32x4 (&sh)[2], f16x8& h, f16x8& l) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        const float y = e < 4 ? y0[e] : y1[e - 4];
-        float x = __fadd_rn(__fmul_rn(y, sc[e >> 2][e & 3]), sh[e >> 2][e & 3]);
-        x = x > 0.f ? x : 0.f;
-        const _Float16 hv = (_Float16)x;
-        h[e] = hv;
-        l[e] = (_Float16)(x - (float)hv);
-    }
-}
-
 // Mainloop + epilogue of the 16x16x32-MFMA bodies: one k32 step per half of a
 // 128-B stage row (LDS ring, DMA issue and the swizzled rows exactly as the
 // 32x32 path).  Wave tile 64 x BN/2 = UM x UN 16x16 tiles.
@@ -753,7 +703,7 @@ __device__ __forceinline__ void x3_turn8(const f32x4& y0, const f32x4& y1, const
 // wave's reads of t), barrier, [read A frags of t+1] then per column block j:
 // [MFMAs of t with B_j] [refill B_j with t+1's].  NST 2 (256x256; 256x64 pairs):
 // A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
-template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, bool FB, typename Issue, typename IssueA,
+template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, typename Issue, typename IssueA,
           typename IssueB>
 __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
@@ -763,7 +713,6 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
     static_assert(!A3 || (BN == 256 && NST == 2), "A3: the 256x256 body");
-    static_assert(!FB || (A3 && P == 3), "FB: the f16x3 A3 body");
     // PAIRB and A3 have no LDS past the ring: the epilogue's scratch is the drained
     // ring and the column scales are loaded in the epilogue
     constexpr bool RINGSCR = PAIRB || A3;
@@ -839,192 +788,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 __builtin_amdgcn_sched_group_barrier(0x020, (NP + UN - 1) / UN, 0);
         }
     };
-    if constexpr (FB) {
-        // FB (conv_x3_a3_bnin_kernel): the A3 rings with the A stages DMA'd from the
-        // producer conv's raw fp32 output (32 channels = 128 B, a packed line's
-        // size) and turned into packed hi | lo lines in place — relu(y * s + t),
-        // bn_apply's arithmetic, then the f16x3 split — by the wave that DMA'd the
-        // rows, so its own vmcnt orders them (no barrier).  B fragments are read one
-        // column ahead instead of a whole stage ahead (-48 VGPRs against the A3
-        // body: room for the turn's scale | shift and raw values).  Per K-step s:
-        //   columns 0..3  MFMAs of s (A(s) fragments in registers, B(s) one column
-        //                 ahead), one DMA piece of A(s+2) each (into A(s-1)'s slot);
-        //                 after column 3's MFMAs: wait own DMA of A(s+1) and its
-        //                 scale | shift, read its rows
-        //   columns 5, 6  turn them (VALU under the MFMAs), write them back
-        //   wait own DMA of B(s+1) (A(s+2) stays in flight); barrier M(s)
-        //   load A(s+2)'s scale | shift, DMA B(s+2) into B(s)'s slot (read before M(s))
-        //   column 7, then read B(s+1)'s column 0 and A(s+1)'s fragments (turned
-        //   before M(s)) — their latency under the last column's MFMAs
-        // VMEM issue order: A(s+2) pieces, scale | shift of A(s+2), B(s+2): the turn
-        // of A(s+1) in column 3 of step s waits vmcnt(GB + GA) (B(s+1), A(s+2) in
-        // flight), M(s) vmcnt(GA).  An A stage has ~1.1 K-steps to land, B ~1.
-        constexpr int GB = GL - GA;
-        char* const bring = smem + 3 * BM * ROW;
-        const int w = wm * WN + wn;
-        const int tj = lane & 3;                       // the 8-channel piece this lane turns,
-        const int trow = 32 * w + (lane >> 2);         // in rows trow and trow + 16 (this wave's DMA rows)
-        const int tsw = (trow >> 1) & 7;               // (both rows swizzle alike)
-        const int o_r0 = trow * ROW + (((2 * tj) ^ tsw) << 4), o_r1 = trow * ROW + (((2 * tj + 1) ^ tsw) << 4);
-        const int o_h = trow * ROW + ((tj ^ tsw) << 4), o_l = trow * ROW + (((4 + tj) ^ tsw) << 4);
-        int tr_cc = ks / a.RS, tr_tap = ks - tr_cc * a.RS;   // K-step position of the next scale | shift load
-        f32x4 ssc[2], ssh[2], raw[4];
-        // scale | shift of the next stage to turn, by loads the compiler does not
-        // track: the turn's counted vmcnt (they are issued before the DMA pieces)
-        // retires them.  Every load's registers must stay live until that turn
-        // reads them — a load whose result is never read lets the compiler hand
-        // its registers to other values while it is in flight (an instrument build
-        // without the turn faulted on exactly that).  (Compiler-tracked loads got a vmcnt(0) before every turn —
-        // its bookkeeping does not count the LDS-DMA pieces issued after them —
-        // draining the DMA issued one column earlier.)
-        auto load_ss = [&]() {
-            const float* p = a.in_ss + tr_cc * 32 + 8 * tj;
-            const float* q = p + a.C;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ssc[0]) : "v"(p) : "memory");
-            asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(ssc[1]) : "v"(p) : "memory");
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ssh[0]) : "v"(q) : "memory");
-            asm volatile("global_load_dwordx4 %0, %1, off offset:16" : "=v"(ssh[1]) : "v"(q) : "memory");
-            if (++tr_tap == a.RS) {
-                tr_tap = 0;
-                ++tr_cc;
-            }
-        };
-        // all four reads before any write: the four pieces of a row are four
-        // adjacent lanes of each instruction, and piece j's hi / lo chunks are
-        // pieces j/2's and 2 + j/2's raw chunks
-        auto turn_read = [&](const char* slot) {
-            raw[0] = *(const f32x4*)(slot + o_r0);
-            raw[1] = *(const f32x4*)(slot + o_r1);
-            raw[2] = *(const f32x4*)(slot + 16 * ROW + o_r0);
-            raw[3] = *(const f32x4*)(slot + 16 * ROW + o_r1);
-        };
-        auto turn_write = [&](char* slot, int k) {
-            f16x8 h, l;
-            x3_turn8(raw[2 * k], raw[2 * k + 1], ssc, ssh, h, l);
-            *(f16x8*)(slot + k * 16 * ROW + o_h) = h;
-            *(f16x8*)(slot + k * 16 * ROW + o_l) = l;
-        };
-        f16x8 jh[2], jl[2];                            // B column j in slot j & 1
-        auto read_bj = [&](int x, const char* stb, int j) {
-            jh[x] = *(const f16x8*)(stb + b_base + j * 16 * ROW + fo_h);
-            jl[x] = *(const f16x8*)(stb + b_base + j * 16 * ROW + fo_l);
-        };
-        auto mma_bj = [&](const FA& f, int j) {
-#pragma unroll
-            for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], f.h[i], f.l[i], jh[j & 1], jl[j & 1], mfma);
-        };
-
-        // prologue: A(0) turned and B(0) landed everywhere (M(-1)), then the step-0
-        // state: A(1) in flight, scale | shift of A(1) and B(1) issued after it;
-        // A(0) and B(0)'s column 0 in registers
-        load_ss();                                     // of A(0)
-        issue_a();                                     // A(0) -> A slot 0
-        issue_b();                                     // B(0) -> B slot 0
-        if (nks > 1) issue_a();                        // A(1) -> A slot 1
-        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        turn_read(smem);
-        turn_write(smem, 0);
-        turn_write(smem, 1);
-        if (nks > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
-        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        lds_barrier();
-        x3_stamp(a, 1);
-        if (nks > 1) {
-            load_ss();                                 // of A(1)
-            issue_b();                                 // B(1) -> B slot 1
-        }
-        FA fa;
-        read_a(fa, smem);
-        read_bj(0, bring, 0);
-        int ca = 0, cb = 0;                            // slots of A(s), B(s)
-        // one K-step s < nks - 1; A2: s + 2 < nks (A(s+2) and B(s+2) to issue).  Its
-        // LDS traffic is inline asm in program order (the compiler's own waits for
-        // the column reads were lgkmcnt(0) — the DMA in flight makes it treat the
-        // LDS counter as out of order — exposing each read), per column j:
-        //   read B(s) column j+1 (2 ops); wait until only those are younger than
-        //   column j's reads (+ the turn's ops issued since); MFMAs of column j
-        // column 3 ends with the turn's 4 reads, columns 5 / 6 carry its two writes.
-        const unsigned lds0 = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)smem;
-        const unsigned bh0 = lds0 + 3 * BM * ROW + b_base + fo_h, bl0 = lds0 + 3 * BM * ROW + b_base + fo_l;
-        auto kstep = [&](auto a2) {
-            constexpr bool A2 = decltype(a2)::value;
-            const int ca1 = ca == 2 ? 0 : ca + 1;
-            const unsigned ta = lds0 + ca1 * (BM * ROW);                         // A(s+1)'s LDS offset
-            const unsigned bh = bh0 + cb * (BN * ROW), bl = bl0 + cb * (BN * ROW);    // B(s)
-            static_for<0, UN - 1>([&](auto jc) {
-                constexpr int j = decltype(jc)::value, x = (j + 1) & 1;
-                lds_rd128<(j + 1) * 16 * ROW>(jh[x], bh);
-                lds_rd128<(j + 1) * 16 * ROW>(jl[x], bl);
-                // LDS ops younger than column j's reads: column j+1's (2), the turn's
-                // reads while column 5 has not waited for them (4), its first write (2)
-                constexpr int YOUNGER = 2 + (j == 4 ? 4 : 0) + (j == 6 ? 2 : 0);
-                if constexpr (j == 0) {
-                    lgkm_wait_tie<YOUNGER>(fa.h[0], fa.l[0], fa.h[1], fa.l[1], fa.h[2], fa.l[2], fa.h[3], fa.l[3],
-                                           jh[0], jl[0]);
-                } else if constexpr (j == 5) {
-                    lgkm_wait_tie<YOUNGER>(jh[j & 1], jl[j & 1], raw[0], raw[1], raw[2], raw[3]);
-                } else {
-                    lgkm_wait_tie<YOUNGER>(jh[j & 1], jl[j & 1]);
-                }
-                mma_bj(fa, j);
-                if constexpr (A2 && j < GA) issue_a(j);             // A(s+2) -> A(s-1)'s slot
-                if constexpr (A2 && j == GA - 1) issue_a(GA);
-                if constexpr (j == 3) {                             // own DMA of A(s+1) and its scale | shift
-                    if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB + GA) : "memory");
-                    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
-                    lds_rd128<0>(raw[0], ta + o_r0);
-                    lds_rd128<0>(raw[1], ta + o_r1);
-                    lds_rd128<16 * ROW>(raw[2], ta + o_r0);
-                    lds_rd128<16 * ROW>(raw[3], ta + o_r1);
-                }
-                if constexpr (j == 5 || j == 6) {
-                    constexpr int k = j - 5;
-                    f16x8 h, l;
-                    x3_turn8(raw[2 * k], raw[2 * k + 1], ssc, ssh, h, l);
-                    lds_wr128<k * 16 * ROW>(ta + o_h, h);
-                    lds_wr128<k * 16 * ROW>(ta + o_l, l);
-                }
-                // a column is a scheduling region: its MFMAs stay between its
-                // wait and the next column's (the turn's VALU interleaves inside)
-                __builtin_amdgcn_sched_barrier(0);
-            });
-            if constexpr (A2) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_barrier();                             // M(s)
-            if constexpr (A2) {
-                load_ss();                             // of A(s+2)   (ahead of B(s+2): memory clobbers)
-                issue_b();                             // B(s+2) -> B(s)'s slot
-            }
-            lgkm_wait_tie<0>(jh[(UN - 1) & 1], jl[(UN - 1) & 1]);     // (retired before M(s))
-            mma_bj(fa, UN - 1);
-            {
-                const unsigned nbh = bh0 + (cb ^ 1) * (BN * ROW), nbl = bl0 + (cb ^ 1) * (BN * ROW);
-                lds_rd128<0>(jh[0], nbh);
-                lds_rd128<0>(jl[0], nbl);
-                const unsigned fh = ta + a_base + fo_h, fl = ta + a_base + fo_l;
-                static_for<0, UM>([&](auto ic) {
-                    constexpr int i = decltype(ic)::value;
-                    lds_rd128<i * 16 * ROW>(fa.h[i], fh);
-                    lds_rd128<i * 16 * ROW>(fa.l[i], fl);
-                });
-            }
-            ca = ca1;
-            cb ^= 1;
-        };
-        int s = 0;
-        for (; s + 2 < nks; ++s) kstep(std::true_type{});
-        if (s + 1 < nks) kstep(std::false_type{});
-        lgkm_wait_tie<0>(fa.h[0], fa.l[0], fa.h[1], fa.l[1], fa.h[2], fa.l[2], fa.h[3], fa.l[3], jh[0], jl[0]);
-        {
-            const char* const stb = bring + cb * (BN * ROW);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                if (j + 1 < UN) read_bj((j + 1) & 1, stb, j + 1);
-                mma_bj(fa, j);
-            }
-        }
-    } else if constexpr (A3) {
+    if constexpr (A3) {
         // A3: the NST 2 schedule below with A one stage further ahead.  Issue order
         // per K-step t (after its barrier): B(t+2) into B's slot of t, then A(t+3)
         // into A's slot of t (both read into registers during step t-1); so at step
@@ -1303,7 +1067,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false, bool FB = false>
+template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -1379,8 +1143,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
         b_off[j] = (n0 + row) * bline + (STEM ? Lc * 8 : (int)lofs(Lc));
         b_dst[j] = (BM + RPI * bi) * ROW;
     }
-    // FB: relu(NaN * s + t) = 0 for the zero-padded taps and the rows past M
-    const _Float16* zero = (const _Float16*)(FB ? g_x3_nan_line : g_x3_zero_line);
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
 
     // staging state of the next K-step to issue (wave-uniform, advanced per issue)
     // (a stream-K segment starts at K-step ks: channel group outer, tap inner)
@@ -1417,28 +1180,9 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     // ahead of B — each with its own (channel group, tap) position
     int qa_buf = 0, qa_cc = q_cc, qa_tap = q_tap, qa_rr = q_rr, qa_ss = q_ss;
     int qb_buf = 0, qb_cc = q_cc, qb_tap = q_tap;
-    // issue_a(): the next A stage, then the advance to the stage after it;
-    // issue_a(i), i < GA: only piece i of it; issue_a(GA): only the advance (FB
-    // spreads the pieces over a K-step's columns)
-    auto issue_a_piece = [&](int i) {
-        char* st = smem + qa_buf * (BM * ROW);
-        const int dh = qa_rr * a.dil, dw = qa_ss * a.dil;
-        const long toff = ((long)dh * a.W + dw) * cstride + qa_cc * 64;
-        const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
-        const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-        // the source select as bit arithmetic: as a pointer select, LLVM turned it
-        // into a divergent branch around each DMA piece once they were spread
-        const unsigned long mask = 0ul - (unsigned long)in;
-        const unsigned long src = ((unsigned long)(xbase + ((unsigned long)a_off[i] + toff)) & mask) |
-                                  ((unsigned long)zero & ~mask);
-        glds16((const void*)src, st + (RPI * (w * GA + i)) * ROW);
-    };
-    auto issue_a = [&](int piece = -1) {
-        if (piece >= 0 && piece < GA) {
-            issue_a_piece(piece);
-            return;
-        }
-        if (piece < 0) {
+    // issue_a(): the next A stage, then the advance to the stage after it
+    auto issue_a = [&]() {
+        {
             char* st = smem + qa_buf * (BM * ROW);
             const int dh = qa_rr * a.dil, dw = qa_ss * a.dil;
             const long toff = ((long)dh * a.W + dw) * cstride + qa_cc * 64;
@@ -1473,7 +1217,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA, FB>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
                                                              tid, issue_next, issue_a, issue_b);
         return;
     } else {
@@ -1697,13 +1441,13 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
 // segments of conv_x3_tail_kernel) in the same launch: they are dispatched as the
 // full rounds' tiles finish, without the second launch's gap — and, in training,
 // ahead of a side-stream wgrad that would otherwise take the freed CUs first.
-template <int P, bool FB>
+template <int P>
 __device__ __forceinline__ void conv_x3_a3_grid(const X3Args& a, char* smem) {
     x3_stagger(a);
     x3_stamp(a, 0);
     const int b = blockIdx.x;
     if (a.tail_groups == 0 || b < a.main_blocks) {
-        conv_x3_tile<256, false, false, 16, P, true, FB>(
+        conv_x3_tile<256, false, false, 16, P, true>(
             a, smem, xcd_remap(b, a.tail_groups ? a.main_blocks : gridDim.x), 0, a.nks, false);
         return;
     }
@@ -1717,21 +1461,13 @@ __device__ __forceinline__ void conv_x3_a3_grid(const X3Args& a, char* smem) {
     const long U = t.sk_units, u0 = sk_start(g, U, a.tail_groups), u1 = sk_start(g + 1, U, a.tail_groups);
     const int mt = (int)(u0 / a.nks);
     const int ks = (int)(u0 - (long)mt * a.nks), ke = (int)(u1 - (long)mt * a.nks);
-    conv_x3_tile<256, false, false, 16, P, true, FB>(t, smem, mt * NT + nt, ks, ke - ks, true);
+    conv_x3_tile<256, false, false, 16, P, true>(t, smem, mt * NT + nt, ks, ke - ks, true);
 }
 
 template <int P>
 __global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
-    conv_x3_a3_grid<P, false>(a, smem);
-}
-
-// the same with the input's BN + ReLU applied to each A stage in LDS
-// (X3Args::in_ss, the FB body): inference, the f16x3 split
-template <int P>
-__global__ __launch_bounds__(512, 1) void conv_x3_a3_bnin_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
-    conv_x3_a3_grid<P, true>(a, smem);
+    conv_x3_a3_grid<P>(a, smem);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -2855,16 +2591,9 @@ static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int le
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
 
-// the A3 grid (conv_x3_a3_kernel<P>, or with the input's BN applied in LDS:
-// conv_x3_a3_bnin_kernel<3>)
+// the A3 grid (conv_x3_a3_kernel<P>)
 template <int P>
 static void launch_a3(dim3 grid, hipStream_t st, const X3Args& a) {
-    if constexpr (P == 3) {
-        if (a.in_ss) {
-            hipLaunchKernelGGL(conv_x3_a3_bnin_kernel<3>, grid, dim3(512), 0, st, a);
-            return;
-        }
-    }
     hipLaunchKernelGGL(conv_x3_a3_kernel<P>, grid, dim3(512), 0, st, a);
 }
 
@@ -2961,9 +2690,8 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
                     2L * G * 256 * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
         NG = 0;
     const bool tail = NG > 0;
-    // one launch: the full rounds, then the tail's segments (always with a fused
-    // input BN: conv_x3_tail_kernel has no FB body)
-    if (tail && c.a3 && (!g_x3_split_tail || a.in_ss)) {
+    // one launch: the full rounds, then the tail's segments
+    if (tail && c.a3 && !g_x3_split_tail) {
         X3Args t = a;
         t.main_blocks = (int)(rm * a.n_tiles);
         t.tail_groups = (int)NG;
@@ -3061,16 +2789,15 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
         a.in_ss = ep->in_ss;
     }
     if (a.in_ss) {
-        // the fused input BN runs where the unfused conv would run the halo-tile body
-        // or (f16x3) the A3 body — so its output is the unfused path's, bit for bit
+        // the fused input BN runs where the unfused conv would run the halo-tile body,
+        // so its output is the unfused path's, bit for bit
         HKP_CHECK_ARG(P == 3 || P == 1, "%s: fused input BN needs f16x3 or plain fp16", who);
         const bool sk_ok = sk_ws && sk_bytes >= x3_sk_ws_bytes(256);
         const X3Choice c = x3_choose(d->k, (M + 255) / 256, a.RS * a.cch, sk_ok, d->tile,
                                      x3_halo_level(x3_halo_ok(a, d->k), a.cch, P));
-        HKP_CHECK_ARG(c.halo || (c.a3 && P == 3),
+        HKP_CHECK_ARG(c.halo,
                       "%s: the fused input BN needs a launch on the halo-tile body (stride-1 3x3, pad = dil = 1, "
-                      "Ho %% 8 == 0, Wo %% 32 == 0) or, f16x3, on the A3 body (Cout %% 256 == 0, one tile per block)",
-                      who);
+                      "Ho %% 8 == 0, Wo %% 32 == 0)", who);
     }
     launch_x3(d->k, (M + 255) / 256, policy, P, as_stream(stream), a, sk_ws, sk_bytes);
     HKP_LAUNCH_CHECK(who);

@@ -256,9 +256,9 @@ def _fwd_tile(conv, pol, f16):
 
 def _bnin_ok(conv, y, pol):
     """The consumer conv takes its input's BN + ReLU (ops.bnin_kernel: where the
-    unfused conv runs the halo-tile body, or, f16x3, the A3 body — so fusing
-    changes no tile and no summation order: the outputs are the unfused path's
-    bits; the full f16x3 or plain fp16 arithmetic)."""
+    unfused conv runs the halo-tile body — so fusing changes no tile and no
+    summation order: the outputs are the unfused path's bits; the full f16x3 or
+    plain fp16 arithmetic)."""
     if not pol.fuse_input_bn:
         return False
     f16 = y.dtype == torch.float16
@@ -271,7 +271,7 @@ def _bnin_ok(conv, y, pol):
         return False
     name = ops.bnin_kernel(n, h, w, c, k, r, s, _i(conv.stride), _i(conv.padding), _i(conv.dilation), f16,
                            _fwd_tile(conv, pol, f16))
-    return name is not None and (pol.fuse_input_bn_a3 or not name.startswith("conv_x3_a3_"))
+    return name is not None
 
 
 def _f16_conv_ok(conv):

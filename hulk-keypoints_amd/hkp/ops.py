@@ -220,9 +220,8 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
 def bnin_kernel(n, h, w, c, k, r, s, stride, pad, dil, f16=False, tile=0, sk=True):
     """The kernel a fused-input-BN conv (hkp_conv2d_fwd_x3_bnin / _f16_bnin) of this
     shape runs, or None where it has none: the fused conv runs where the unfused
-    one runs the halo-tile body (conv_x3_halo_bnin_kernel<P>) or, f16x3, the A3
-    body (conv_x3_a3_bnin_kernel<3>) — the same tiles and summation order, so the
-    same bits."""
+    one runs the halo-tile body (conv_x3_halo_bnin_kernel<P>) — the same tiles
+    and summation order, so the same bits."""
     cg = 64 if f16 else 32
     if c % cg or k % 64:
         return None
@@ -232,7 +231,7 @@ def bnin_kernel(n, h, w, c, k, r, s, stride, pad, dil, f16=False, tile=0, sk=Tru
         return None
     d = ConvDesc(n, h, w, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     name = kernel_name(d, HKP_KOP_FWD_F16 if f16 else HKP_KOP_FWD_X3, sk)
-    if name.startswith("conv_x3_halo_kernel<") or (not f16 and name == "conv_x3_a3_kernel<3>"):
+    if name.startswith("conv_x3_halo_kernel<"):
         return name.replace("_kernel<", "_bnin_kernel<")
     return None
 

@@ -73,10 +73,6 @@ class Policy:
     # conv runs the halo-tile body (hkp_conv2d_fwd_x3_bnin / _f16_bnin: layer1's
     # 3x3 convs at 640x480) instead of a separate apply pass
     fuse_input_bn: bool = True
-    # ... and, f16x3, where it runs the A3 body (C2's layer3/4 conv2:
-    # conv_x3_a3_bnin_kernel<3>, bit-identical) — measured slower than the apply
-    # pass + A3 conv (+22-25 % per conv against +6-14 % for the apply): off
-    fuse_input_bn_a3: bool = False
 
     def __post_init__(self):
         if self.precision not in PRECISIONS:

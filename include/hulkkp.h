@@ -150,9 +150,7 @@ int hkp_conv2d_fwd_x3_products(const hkp_conv_desc* d, const uint16_t* x_split, 
  * hkp_bn_apply(split = 3) would write it — so y is bit-identical to hkp_bn_apply
  * followed by hkp_conv2d_fwd_x3 with the same d->tile and workspace.  Runs
  * where that unfused launch runs the halo-tile body (stride-1 3x3, pad = dil =
- * 1, Ho % 8 == 0, Wo % 32 == 0) or the A3 body (256x256 tiles, one per block,
- * with its split-K tail in the same launch: Cout % 256 == 0 and the planner's
- * or d->tile's choice) — the kernel hkp_conv_kernel_name names for
+ * 1, Ho % 8 == 0, Wo % 32 == 0) — the kernel hkp_conv_kernel_name names for
  * HKP_KOP_FWD_X3, with "_bnin" before "_kernel"; other launches return
  * HKP_ERR_BAD_ARG. */
 int hkp_conv2d_fwd_x3_bnin(const hkp_conv_desc* d, const float* x_raw, const float* in_scale_shift,

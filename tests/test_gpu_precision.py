@@ -760,69 +760,22 @@ def test_fused_input_bn_rejects_other_shapes(cuda_device):
     wp = ops.weight_pack_x3(rand(64, 3, 3, 64, seed=96, scale=0.05).to(d))
     with pytest.raises(ops.HkpError, match="halo"):
         ops.conv2d_fwd_bnin(y, ss, wp, 1, 1, 1)
-    # the A3 body is f16x3 only, and needs Cout % 256
+    # the A3 body has no fused form (round 5: removed)
     wp16 = ops.weight_pack_f16(rand(256, 1, 1, 64, seed=97, scale=0.05).to(d))
-    with pytest.raises(ops.HkpError, match="A3"):
+    with pytest.raises(ops.HkpError, match="halo"):
         ops.conv2d_fwd_bnin(y.half(), ss, wp16, 1, 0, 1, tile=11)
     assert ops.bnin_kernel(1, 12, 32, 64, 256, 1, 1, 1, 0, 1, f16=True, tile=11) is None
-    assert ops.bnin_kernel(1, 12, 32, 64, 256, 1, 1, 1, 0, 1, tile=11) == "conv_x3_a3_bnin_kernel<3>"
-    assert ops.bnin_kernel(1, 12, 32, 64, 128, 1, 1, 1, 0, 1, tile=11) is None
-
-
-# (n, h, w, c, k, r, pad, dil): the A3 fused-input-BN body (tile 11 forced) at
-# 1-4 K-steps (the pipeline's short forms), rows past M, two column tiles, the
-# dilated 3x3 of layer3/4 (NaN padding lines), and a grid with a split-K tail in
-# the same launch (300 tiles on 256 CUs)
-A3_BNIN_CASES = [
-    (2, 16, 64, 32, 256, 1, 0, 1),
-    (2, 16, 64, 64, 256, 1, 0, 1),
-    (2, 16, 64, 96, 256, 1, 0, 1),
-    (2, 16, 64, 128, 256, 1, 0, 1),
-    (1, 10, 30, 64, 256, 1, 0, 1),
-    (2, 24, 40, 256, 512, 3, 2, 2),
-    (8, 60, 160, 256, 256, 3, 2, 2),
-]
-
-
-@pytest.mark.parametrize("case", A3_BNIN_CASES)
-def test_fused_input_bn_a3_equals_apply_then_conv(cuda_device, case):
-    """hkp_conv2d_fwd_x3_bnin on the A3 body (conv_x3_a3_bnin_kernel<3>: raw fp32
-    A stages turned into packed hi | lo lines in LDS by the waves that DMA'd them,
-    B fragments read a column ahead) == bn_apply(split 3) followed by the A3 conv:
-    the same y and BN partials, bit for bit, with mixed-sign scales."""
-    from hkp import ops
-    from hkp._lib import HKP_KOP_FWD_X3, ConvDesc
-    n, h, w, c, k, r, pad, dil = case
-    d = cuda_device
-    y = (rand(n, h, w, c, seed=191) * 3 + 1).to(d)
-    ss = torch.cat([rand(c, seed=192) * 0.7, rand(c, seed=193) * 2.0]).to(d)
-    wt = rand(k, r, r, c, seed=194, scale=(2.0 / (r * r * k)) ** 0.5).to(d)
-    wp = ops.weight_pack_x3(wt)
-    assert ops.kernel_name(ConvDesc(n, h, w, c, k, r, r, 1, pad, dil, 0, 11), HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
-    a = ops.bn_apply(y, ss, relu=True, split=3, keep_fp32=False)
-    ref, pref = ops.conv2d_fwd_x3(a, wp, 1, pad, dil, tile=11)
-    got, pgot = ops.conv2d_fwd_bnin(y, ss, wp, 1, pad, dil, tile=11)
-    torch.cuda.synchronize()
-    assert torch.isfinite(got).all()
-    assert torch.equal(got, ref), (got - ref).abs().max().item()
-    assert torch.equal(pgot, pref)
-    if n * h * w > 4096:
-        return
-    # and the value: fp64 of the applied operand
-    ref64 = F.conv2d(torch.relu(y.double() * ss[:c].double() + ss[c:].double()).permute(0, 3, 1, 2),
-                     wt.double().permute(0, 3, 1, 2), padding=pad, dilation=dil).permute(0, 2, 3, 1)
-    err = (got.double() - ref64).abs().max().item()
-    assert err <= 1e-4 * ref64.abs().max().item(), err
+    assert ops.bnin_kernel(1, 12, 32, 64, 256, 1, 1, 1, 0, 1, tile=11) is None
 
 
 @pytest.mark.parametrize("bb,prec,b,hw,fused", [
     ("resnet18", "f16x3", 2, (128, 256), "conv_x3_halo_bnin_kernel<3>"),
     ("resnet50", "f16", 2, (128, 256), "conv_x3_halo_bnin_kernel<1>"),
-    ("resnet34", "f16x3", 32, (480, 640), "conv_x3_a3_bnin_kernel<3>")])     # C2: layer3/4 on A3
+    ("resnet34", "f16x3", 32, (480, 640), "conv_x3_halo_bnin_kernel<3>")])     # C2 itself
 def test_fused_input_bn_network_bitexact(cuda_device, bb, prec, b, hw, fused):
     """Whole inference forward (128x256: a halo-tiled layer1 at 32x64; C2 640x480
-    B=32: layer3/4's conv2 on the A3 body, Policy.fuse_input_bn_a3): fused ==
-    unfused, heatmaps and argmax bit for bit, and the fused kernels ran."""
+    B=32): fused == unfused, heatmaps and argmax bit for bit, and the fused
+    kernels ran."""
     from hkp import net, ops
     m = _model(bb, 4, 7, cuda_device, precision=prec)
     x = recipe.to_tensor_nchw(recipe.seeded_images_u8(b, hw[0], hw[1], 8)).to(cuda_device)
@@ -836,8 +789,7 @@ def test_fused_input_bn_network_bitexact(cuda_device, bb, prec, b, hw, fused):
         ops.set_observer(observe if fuse else None)
         try:
             with torch.no_grad():
-                hm, yx = m.heatmaps_and_keypoints(x, policy=m.policy.with_(fuse_input_bn=fuse,
-                                                                           fuse_input_bn_a3=fuse))
+                hm, yx = m.heatmaps_and_keypoints(x, policy=m.policy.with_(fuse_input_bn=fuse))
         finally:
             ops.set_observer(None)
         outs.append((hm, yx))

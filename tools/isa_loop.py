@@ -5,7 +5,7 @@ M<n> (n MFMAs), R / W (ds_read / ds_write), DMA (global_load_lds), LD (other
 global loads), v (VALU), [waitcnt], BARRIER.  Shows where the compiler put its
 waits and how the DMA pieces and LDS reads interleave with the MFMAs.
 
-    python tools/isa_loop.py conv_x3_a3_bnin_kernel<3> [--src csrc/conv_x3.hip]
+    python tools/isa_loop.py "conv_x3_a3_kernel<3>" [--src csrc/conv_x3.hip]
 """
 import argparse
 import os
