@@ -1778,6 +1778,337 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_bnin_kernel(X3Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// DUO body (conv_x3_duo_kernel<1>): plain-fp16 (P 1, config C4) convs on 256 x 128
+// tiles run by TWO 4-wave blocks per CU.  The one-tile 256x256 bodies hold a
+// whole CU, so each tile's pipeline fill, BN partials, fp16 staging and stores
+// run with the CU's matrix pipes idle — on C4's short-K 1x1 GEMMs (8-16 K-steps
+// per tile) about half of a tile's time (DESIGN "C4's 1x1 GEMMs").  Here two
+// independent blocks share the CU: one block's fill and epilogue run beside the
+// other's K loop, and their vmcnt / barriers are separate (a persistent body's
+// epilogue stores, by contrast, shared vmcnt with its next tile's DMA).
+// Per block: 4 waves as 2 x 2, wave tile 128 x 64 (8 x 4 16x16x32 MFMA tiles,
+// 128 accumulator registers); a 3-stage LDS ring of HALF lines — a stage holds
+// 32 channels (64 B) of every A row (256) and B row (128): 24 KiB — so three
+// stages (72 KiB, which also holds the fp16 epilogue tile) fit twice per CU.
+// K order: channel group (64 channels), tap, half; a half-line is one k32 step,
+// one MFMA per (16-row, 16-column) pair.  64-B rows: lane l of a DMA piece writes
+// row l/4, 16-B chunk l%4; the chunk swizzle (4 - (row >> 2)) & 3 makes every
+// ds_read_b128 lane group of the fragment reads (rows r16 = lane & 15, chunk
+// lane >> 4) hit 16 distinct 16-B bank groups.  Epilogue: BN partials per
+// 128-row half straight from one wave's accumulators (a wave holds a whole
+// half: no LDS merge), then the fp16 tile staged in the drained ring and written
+// as 16-B row chunks, optionally through the fused BN + residual + ReLU
+// (hkp_conv2d_fwd_f16_bn) — the 256x256 body's arithmetic, element for element.
+constexpr int DUO_BM = 256, DUO_BN = 128, DUO_ROW = 64, DUO_NST = 3;
+constexpr int DUO_STAGE = (DUO_BM + DUO_BN) * DUO_ROW;                 // 24 KiB
+constexpr int DUO_LDS = DUO_NST * DUO_STAGE;                           // 72 KiB: two blocks per CU
+static_assert(DUO_BM * (DUO_BN + 8) * 2 + 4 * DUO_BN * 4 <= DUO_LDS, "DUO epilogue staging");
+
+__device__ __forceinline__ int duo_swz(int row) { return (4 - ((row >> 2) & 3)) & 3; }
+
+// BN partials (sum, M2 about the half's mean) of one wave's 128-row half of the
+// tile: each lane reduces its 32 rows of a column, then lanes l, l^16, l^32, l^48
+// (the column's four row groups) merge by Chan's formula — equal counts, so the
+// factors are constants and the result is symmetric in each pair (all four lanes
+// hold the same bits).  Rows past M (the last tile) take the counted form.
+template <int UM, int UN>
+__device__ __forceinline__ void duo_bn_partials(const X3Args& a, const f32x4 (&acc)[UM][UN], const float (&sc)[UN],
+                                                int m0h, int ncol0, int lane) {
+    const int q = lane >> 4, r16 = lane & 15;
+    const long tile128 = (long)(m0h >> 7);
+    if (m0h + 128 <= a.M) {                                  // block-uniform
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            f32x4 s4 = acc[0][j];
+#pragma unroll
+            for (int i = 1; i < UM; ++i) s4 += acc[i][j];
+            float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            constexpr float inv = 1.f / (UM * 4);
+            const f32x4 mu = {s * inv, s * inv, s * inv, s * inv};
+            f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < UM; ++i) {
+                const f32x4 d = acc[i][j] - mu;
+                q4 += d * d;
+            }
+            float m2 = (q4[0] + q4[1]) + (q4[2] + q4[3]);
+            x3_chan_merge(s, m2, __shfl_xor(s, 16), __shfl_xor(m2, 16), 1.f / (UM * 4), UM * 2.f);
+            x3_chan_merge(s, m2, __shfl_xor(s, 32), __shfl_xor(m2, 32), 1.f / (UM * 8), UM * 4.f);
+            if (q == 0) {
+                const int c = ncol0 + 16 * j + r16;
+                a.part[(tile128 * a.K + c) * 2 + 0] = s * sc[j];
+                a.part[(tile128 * a.K + c) * 2 + 1] = m2 * (sc[j] * sc[j]);
+            }
+        }
+        return;
+    }
+    if (m0h >= a.M) return;
+    float ln = 0.f;
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ln += (m0h + 16 * i + 4 * q + r < a.M) ? 1.f : 0.f;
+    const float linv = ln > 0.f ? 1.f / ln : 0.f;
+#pragma unroll
+    for (int j = 0; j < UN; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s += (m0h + 16 * i + 4 * q + r < a.M) ? acc[i][j][r] : 0.f;
+        const float mu = s * linv;
+        float m2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float d = acc[i][j][r] - mu;
+                m2 += (m0h + 16 * i + 4 * q + r < a.M) ? d * d : 0.f;
+            }
+        float n = ln;
+        for (int o = 16; o < 64; o <<= 1) {
+            const float nb = __shfl_xor(n, o), sb = __shfl_xor(s, o), qb = __shfl_xor(m2, o);
+            const float nt = n + nb;
+            const float f = nt > 0.f ? n * nb / nt : 0.f;
+            const float ia = n > 0.f ? 1.f / n : 0.f, ib = nb > 0.f ? 1.f / nb : 0.f;
+            const float d = sb * ib - s * ia;
+            s = s + sb;
+            m2 = (m2 + qb) + d * d * f;
+            n = nt;
+        }
+        if (q == 0) {
+            const int c = ncol0 + 16 * j + r16;
+            a.part[(tile128 * a.K + c) * 2 + 0] = s * sc[j];
+            a.part[(tile128 * a.K + c) * 2 + 1] = m2 * (sc[j] * sc[j]);
+        }
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
+    static_assert(P == 1, "DUO: the plain-fp16 operand layout");
+    __shared__ __attribute__((aligned(1024))) char smem[DUO_LDS];
+    constexpr int BM = DUO_BM, BN = DUO_BN, ROW = DUO_ROW, NST = DUO_NST, STAGE = DUO_STAGE;
+    constexpr int UM = 8, UN = 4;                    // 16x16 tiles per wave (wave tile 128 x 64)
+    constexpr int GA = 4, GB = 2, GL = GA + GB;      // DMA pieces (16 rows each) per wave per stage
+
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w >> 1, wn = w & 1;
+    const int nst = 2 * a.nks;                       // half-line stages
+
+    // ---- DMA sources (the one-tile bodies' bookkeeping, 64-B rows) ----
+    const int cstride = a.cch * 64;                  // halves per pixel
+    const long xbias = (long)a.pad * (a.W + 1) * cstride;
+    const _Float16* xbase = a.xs - xbias;
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    int a_org[GA];
+    unsigned a_off[GA];
+#pragma unroll
+    for (int i = 0; i < GA; ++i) {
+        const int row = 64 * w + 16 * i + (lane >> 2);
+        const int Lc = (lane & 3) ^ duo_swz(row);
+        const int m = m0 + row;
+        int hb = -16384, wb = -16384;
+        long off = 0;
+        if (m < a.M) {
+            const int hw = a.Ho * a.Wo;
+            const int n = m / hw, rem = m - n * hw;
+            const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+            hb = ho * a.stride - a.pad;
+            wb = wo * a.stride - a.pad;
+            off = (((long)n * a.H + hb) * a.W + wb) * cstride + Lc * 8;
+        }
+        a_org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
+        a_off[i] = (unsigned)(off + xbias);
+    }
+    const int bline = a.RS * a.cch * 64;             // halves per weight row
+    int b_off[GB];
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+        const int row = 32 * w + 16 * j + (lane >> 2);
+        b_off[j] = (n0 + row) * bline + ((lane & 3) ^ duo_swz(row)) * 8;
+    }
+    // staging position of the next stage to issue: (channel group, tap, half)
+    int q_buf = 0, q_cc = 0, q_tap = 0, q_rr = 0, q_ss = 0, q_half = 0;
+    auto issue = [&]() {
+        char* st = smem + q_buf * STAGE;
+        const int dh = q_rr * a.dil, dw = q_ss * a.dil;
+        const long toff = ((long)dh * a.W + dw) * cstride + q_cc * 64 + q_half * 32;
+#pragma unroll
+        for (int i = 0; i < GA; ++i) {
+            const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
+            const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
+            glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (64 * w + 16 * i) * ROW);
+        }
+        const int boff = (q_tap * a.cch + q_cc) * 64 + q_half * 32;
+#pragma unroll
+        for (int j = 0; j < GB; ++j) glds16(a.ws + (unsigned)(b_off[j] + boff), st + (BM + 32 * w + 16 * j) * ROW);
+        q_buf = q_buf == NST - 1 ? 0 : q_buf + 1;
+        if (++q_half == 2) {
+            q_half = 0;
+            if (++q_ss == a.S) {
+                q_ss = 0;
+                ++q_rr;
+            }
+            if (++q_tap == a.RS) {
+                q_tap = 0;
+                q_rr = 0;
+                ++q_cc;
+            }
+        }
+    };
+
+    // ---- fragments: lane reads row r16 of a 16-row tile, logical chunk q ----
+    const int r16 = lane & 15, q = lane >> 4;
+    const int fo = r16 * ROW + ((q ^ duo_swz(r16)) << 4);
+    const int a_base = (wm * 128) * ROW + fo, b_base = (BM + wn * 64) * ROW + fo;
+    f32x4 acc[UM][UN];
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x8 fa[UM], fb[UN];
+    auto read_a = [&](const char* st) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) fa[i] = *(const f16x8*)(st + a_base + i * 16 * ROW);
+    };
+    auto read_b = [&](int j, const char* st) { fb[j] = *(const f16x8*)(st + b_base + j * 16 * ROW); };
+    auto mma_col = [&](int j) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+
+    // column scales (weight scale), issued before the fill
+    float sc[UN];
+#pragma unroll
+    for (int j = 0; j < UN; ++j) sc[j] = a.wscale ? a.wscale[n0 + wn * 64 + 16 * j + r16] : 1.f;
+
+    // ---- pipeline (the 3-stage ring schedule of conv_x3_mf16_body): per stage t —
+    // wait own DMA of t+1 (t+2 stays in flight), barrier, DMA of t+3 into t's
+    // buffer (its fragments were read during step t-1) spread over the columns,
+    // per column j [MFMAs of t with B_j] [read B_j of t+1], then A of t+1 ----
+    for (int s = 0; s < NST; ++s)
+        if (s < nst) issue();
+    {
+        const int after = min(nst, NST) - 1;
+        if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
+        else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    read_a(smem);
+#pragma unroll
+    for (int j = 0; j < UN; ++j) read_b(j, smem);
+    int cur = 0;
+    auto kstep = [&](const int t, const bool dma) {
+        if (t + 2 < nst) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GL) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        cur = cur == NST - 1 ? 0 : cur + 1;
+        const char* st = smem + cur * STAGE;
+        if (dma) issue();
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            mma_col(j);
+            read_b(j, st);
+        }
+        read_a(st);
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            __builtin_amdgcn_sched_group_barrier(0x008, UM, 0);     // column j's MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);      // refill B_j
+            if (dma && j * ((GL + UN - 1) / UN) < GL)
+                __builtin_amdgcn_sched_group_barrier(0x020, (GL + UN - 1) / UN, 0);   // DMA pieces
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, UM, 0);         // next A frags
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    int t = 0;
+    for (; t + 3 < nst; ++t) kstep(t, true);
+    for (; t + 1 < nst; ++t) kstep(t, false);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < UN; ++j) mma_col(j);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the ring past here
+
+    // ---- epilogue: BN partials of this wave's 128-row half, then the fp16 tile ----
+    if (a.part) duo_bn_partials<UM, UN>(a, acc, sc, m0 + 128 * wm, n0 + wn * 64, lane);
+    constexpr int PITCH = BN + 8, CH = BN / 8, SS_OFF = BM * PITCH * 2;
+    constexpr int NT = 256, NPT = BM * CH / NT;              // 16-B chunks per thread
+    static_assert(NT % CH == 0, "a thread keeps its 8 channels");
+    const int cc = tid % CH;
+    // fused BN epilogue: per-column parameters and the residual chunks in flight
+    // before the tile is staged (their latency hides behind it)
+    float ep0 = 0.f, ep1 = 0.f;
+    f16x8 res[NPT];
+    if (a.ep_ss) {
+        const int h = tid / BN, c = tid - h * BN;                // tid < 2 * BN: all 256 threads
+        ep0 = a.ep_ss[h * a.K + n0 + c];
+        ep1 = a.ep_rss ? a.ep_rss[h * a.K + n0 + c] : 0.f;
+#pragma unroll
+        for (int u = 0; u < NPT; ++u) {
+            const int row = (tid + NT * u) / CH, m = m0 + row;
+            res[u] = f16x8{};
+            if (a.ep_res && m < a.M)
+                res[u] = __builtin_nontemporal_load((const f16x8*)(a.ep_res + (long)m * a.K + n0 + cc * 8));
+        }
+    }
+    lds_sync();                                              // every wave done reading the ring
+    _Float16* tl = (_Float16*)smem;
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                tl[(wm * 128 + i * 16 + 4 * q + r) * PITCH + wn * 64 + j * 16 + r16] = (_Float16)(acc[i][j][r] * sc[j]);
+    float* ssl = (float*)(smem + SS_OFF);                    // [4][BN]: scale, shift, residual scale, shift
+    if (a.ep_ss) {
+        ssl[tid] = ep0;
+        ssl[2 * BN + tid] = ep1;
+    }
+    lds_sync();
+    if (!a.ep_ss) {
+#pragma unroll 4
+        for (int u = 0; u < NPT; ++u) {
+            const int row = (tid + NT * u) / CH, m = m0 + row;
+            if (m < a.M)
+                *(uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8) = *(const uint4*)(smem + (row * PITCH + cc * 8) * 2);
+        }
+        return;
+    }
+    float sa[8], sb[8], ra[8], rb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        sa[e] = ssl[cc * 8 + e];
+        sb[e] = ssl[BN + cc * 8 + e];
+        ra[e] = ssl[2 * BN + cc * 8 + e];
+        rb[e] = ssl[3 * BN + cc * 8 + e];
+    }
+    const bool hres = a.ep_res != nullptr, rsc = a.ep_rss != nullptr, relu = a.ep_relu != 0;
+#pragma unroll
+    for (int u = 0; u < NPT; ++u) {
+        const int row = (tid + NT * u) / CH, m = m0 + row;
+        if (m >= a.M) continue;
+        const f16x8 v = *(const f16x8*)(smem + (row * PITCH + cc * 8) * 2);
+        const f16x8 rv = res[u];
+        f16x8 h;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            float o = __fadd_rn(__fmul_rn((float)v[k], sa[k]), sb[k]);
+            if (hres) o = rsc ? __fadd_rn(o, __fadd_rn(__fmul_rn((float)rv[k], ra[k]), rb[k])) : __fadd_rn(o, (float)rv[k]);
+            if (relu) o = o > 0.f ? o : 0.f;
+            h[k] = (_Float16)o;
+        }
+        __builtin_nontemporal_store(h, (f16x8*)(a.y16 + (long)m * a.K + n0 + cc * 8));
+    }
+}
+
+// ---------------------------------------------------------------------------
 // operand packing
 
 __device__ __forceinline__ void split_store(float v, _Float16* hi_p) {   // hi at p, lo at p + 32
@@ -2530,16 +2861,28 @@ struct X3Choice {
     bool pair, sk;
     bool halo = false;                 // conv_x3_halo_kernel<P>
     bool a3 = false;                   // conv_x3_a3_kernel<P> (256x256, 3-stage A ring)
+    bool duo = false;                  // conv_x3_duo_kernel<1> (256x128, two 4-wave blocks per CU)
 };
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
 // at 128 channels it ties the ring bodies, which then stay)
 static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo);
+static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo, int P);
 // AUTO (= AUTO_A3): the planner's choice, its 256x256 one-tile grids on the A3
 // body (measured in-process on one box: C2 1721 -> 1741 img/s, C4 2616 -> 2657;
 // per conv -1...-4 % on the 1x1 and 3x3 shapes of C4, -1 % on C2's layer3/4;
 // HKP_TILE_256 / 256_TAIL keep the 2-stage body)
-static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo = 0) {
+// DUO (the plain-fp16 256x128 two-blocks-per-CU body) where forced and legal;
+// other operand layouts plan as AUTO
+static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo, int P) {
+    if (policy == HKP_TILE_DUO) {
+        if (P == 1 && k % DUO_BN == 0) {
+            X3Choice c{DUO_BN, 16, false, false};
+            c.duo = true;
+            return c;
+        }
+        policy = HKP_TILE_AUTO;
+    }
     if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
     X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
     if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
@@ -2586,6 +2929,7 @@ static const X3Choice X3_STEM{64, 16, true, false};
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
+    if (c.duo) return snprintf(buf, len, "conv_x3_duo_kernel<%d>", P);
     if (c.a3) return snprintf(buf, len, "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
@@ -2652,10 +2996,14 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.stagger_blocks = x3_cus();
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
-    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_level(x3_halo_ok(a, k), a.cch, P));
+    const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_level(x3_halo_ok(a, k), a.cch, P), P);
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
+    if (c.duo) {
+        hipLaunchKernelGGL(conv_x3_duo_kernel<1>, dim3((unsigned)(m_tiles * a.n_tiles)), dim3(256), 0, st, a);
+        return;
+    }
     if (c.halo) {
         const dim3 gh((unsigned)(m_tiles * a.n_tiles));
         if (a.in_ss) {
@@ -2753,7 +3101,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_AUTO_A3, "%s: unknown tile policy %d", who, d->tile);
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_DUO, "%s: unknown tile policy %d", who, d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8,
                   "%s: tile policy %d is retired (the persistent conv, measured slower)", who, d->tile);
     return HKP_OK;
@@ -2794,7 +3142,7 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
         HKP_CHECK_ARG(P == 3 || P == 1, "%s: fused input BN needs f16x3 or plain fp16", who);
         const bool sk_ok = sk_ws && sk_bytes >= x3_sk_ws_bytes(256);
         const X3Choice c = x3_choose(d->k, (M + 255) / 256, a.RS * a.cch, sk_ok, d->tile,
-                                     x3_halo_level(x3_halo_ok(a, d->k), a.cch, P));
+                                     x3_halo_level(x3_halo_ok(a, d->k), a.cch, P), P);
         HKP_CHECK_ARG(c.halo,
                       "%s: the fused input BN needs a launch on the halo-tile body (stride-1 3x3, pad = dil = 1, "
                       "Ho %% 8 == 0, Wo %% 32 == 0)", who);
@@ -3151,7 +3499,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
                               (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);
             return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile,
-                                            x3_halo_level(halo, d->c / cg, P)),
+                                            x3_halo_level(halo, d->c / cg, P), P),
                                   false, P, buf, len);
         }
         case HKP_KOP_DGRAD_X3: {
@@ -3160,7 +3508,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int padp = d->dilation * (d->r - 1) - d->pad;
             const bool halo = halo_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
                               (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32);
-            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->k / 32, 3)),
+            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->k / 32, 3), 3),
                                   false, 3, buf, len);
         }
         case HKP_KOP_STEM_X3:

@@ -82,6 +82,10 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_AUTO_A3 12           /* AUTO with its 256x256 one-tile grids on the A3 body */
 #define HKP_TILE_256_A3 11            /* 256x256 on the A3 body (A ring 3 stages deep, B ring 2: an A
                                          line has two K-steps to land) + the split-K tail of 9 */
+#define HKP_TILE_DUO 13               /* plain fp16 (hkp_conv2d_fwd_f16 / _f16_bn) only: 256x128 tiles,
+                                         two 4-wave blocks per CU (one block's fill and epilogue
+                                         beside the other's K loop); Cout % 128 == 0; other
+                                         operand layouts plan as AUTO */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);

@@ -87,7 +87,7 @@ def test_bn_from_gram_matches_output_statistics(cuda_device, n, h, w, c, k):
 
 
 @pytest.mark.parametrize("res_kind", ["none", "raw", "scaled"])
-@pytest.mark.parametrize("tile", [0, 3, 4, 5, 6, 11])
+@pytest.mark.parametrize("tile", [0, 3, 4, 5, 6, 11, 13])
 def test_fused_epilogue_equals_conv_plus_apply(cuda_device, res_kind, tile):
     from hkp import ops
     d = cuda_device

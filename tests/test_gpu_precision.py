@@ -8,7 +8,7 @@ import torch.nn.functional as F
 from oracle import cpu_ref, recipe
 
 # every live HKP_TILE_* policy past AUTO (7 and 8 are retired)
-LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11)
+LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11, 13)
 
 pytestmark = pytest.mark.gpu
 
@@ -527,6 +527,9 @@ F16_CASES = [
     (3, 13, 17, 256, 64, 1, 1, 0, 1),       # 1x1 reduce (bottleneck conv1), 256x64 pairs, ragged M
     (1, 12, 16, 256, 1024, 1, 1, 0, 1),     # 1x1 expand (bottleneck conv3)
     (2, 31, 41, 256, 512, 1, 2, 0, 1),      # 1x1 stride-2 downsample
+    (3, 13, 17, 64, 256, 1, 1, 0, 1),       # K = 64 (one K-step: DUO's two half-line stages), ragged M
+    (1, 12, 16, 128, 128, 1, 1, 0, 1),      # K = 128, one partly filled tile (DUO: rows past M)
+    (2, 9, 11, 192, 384, 3, 1, 2, 2),       # DUO: 3 column tiles, dilated taps at the border
 ]
 
 
@@ -557,6 +560,10 @@ def test_f16_conv_exact_products(cuda_device, case):
     # BN partials (from the fp32 accumulators) as the fp32 conv's on the same fp16-rounded operands
     yr, pr = ops.conv2d_fwd(x.half().float().to(d), w_eff.float().to(d), st, pad, dil)
     assert torch.allclose(p16, pr, rtol=1e-4, atol=1e-3)
+    from hkp._lib import HKP_KOP_FWD_F16, HKP_TILE_DUO, ConvDesc
+    duo = ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, HKP_TILE_DUO), HKP_KOP_FWD_F16)
+    assert duo == ("conv_x3_duo_kernel<1>" if cout % 128 == 0 else ops.kernel_name(
+        ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, 0), HKP_KOP_FWD_F16))
     for tile in LIVE_TILES:
         yv, pv = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, tile=tile)
         assert err_ratio(yv) <= 1.0, tile

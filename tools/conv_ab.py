@@ -30,6 +30,8 @@ SHAPES = {
     "c4_l4_c2": ("f16", 128, 60, 80, 512, 512, 3, 1, 4, 4),
     "c4_l4_c1": ("f16", 128, 60, 80, 2048, 512, 1, 1, 0, 1),
     "c4_l4_c3": ("f16", 128, 60, 80, 512, 2048, 1, 1, 0, 1),
+    "c4_l4_ds": ("f16", 128, 60, 80, 1024, 2048, 1, 1, 0, 1),
+    "c4_l1_ds": ("f16", 128, 120, 160, 64, 256, 1, 1, 0, 1),
     "c4_l3_c2": ("f16", 128, 60, 80, 256, 256, 3, 1, 2, 2),
     "c4_l3_c1": ("f16", 128, 60, 80, 1024, 256, 1, 1, 0, 1),
     "c4_l3_c3": ("f16", 128, 60, 80, 256, 1024, 1, 1, 0, 1),

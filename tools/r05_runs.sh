@@ -1,0 +1,60 @@
+#!/bin/bash
+# The round-5 GPU recipes behind DESIGN's numbers, one per subcommand (each one
+# gpurun call; outputs under gpurun_out/<name>/):
+#   check     GPU suite + the default bench line (C2 + the north_star batch-64 leg)
+#   duo       the DUO body (plain-fp16 256x128, two blocks per CU): its parity tests,
+#             per-conv A/B vs the planner (tools/conv_ab.py), C4 A/B in one process
+#             (tools/infer_ab.py), then the GPU suite and the default bench line
+#   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
+#             trace stats, per-launch listing, PMC passes over every kernel
+#   final     GPU suite, smoke(), default bench line
+set -e
+export TMPDIR=/tmp
+cmd=${1:?subcommand}
+O=gpurun_out/$cmd; mkdir -p $O
+C5="--mode train --backbone resnet50 --keypoints 8 --height 960 --width 1280 --batch 32"
+case $cmd in
+check)
+    timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_gpu.log)"
+    timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
+    ;;
+duo)
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_precision.py \
+        -k "f16_conv_exact_products" tests/test_gpu_gram.py > $O/pytest_duo.log 2>&1
+    echo "pytest duo: $(tail -1 $O/pytest_duo.log)"
+    timeout -k 10 400 python -u tools/conv_ab.py --tiles 0,13 --rounds 5 --iters 5 \
+        --shapes c4_l4_c3,c4_l4_ds,c4_l4_c1,c4_l4_c2,c4_l3_c1,c4_l3_c3,c4_l3_c2,c4_l2_c1,c4_l2_c2,c4_l1_ds > $O/conv_ab.log 2>&1
+    echo "conv_ab ok"
+    timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_1x1=13" "f16_tile_1x1=13,f16_tile_kxk=13" \
+        --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    echo "infer_ab ok"
+    timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_gpu.log)"
+    timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
+    ;;
+c5)
+    timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
+    echo "bench ok"
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py $C5 --steps 3 \
+        --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1
+    DB=$O/prof/run_results.db
+    [ -f $DB ] || DB=$(ls $O/prof/*/run_results.db 2>/dev/null | head -1)
+    python3 tools/rocpd_stats.py $DB $O/c5_kernel_stats.csv --top 40 > $O/c5_kernel_top.txt
+    python3 tools/step_breakdown.py $DB --last-step > $O/c5_last_step.txt
+    python3 tools/step_breakdown.py $DB --walls > $O/c5_walls.txt
+    rm -rf $O/prof
+    echo "trace ok"
+    bash tools/pmc_passes.sh $O/pmc "$C5 --steps 2 --warmup 1" "."
+    ;;
+final)
+    timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+    timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
+    ;;
+*)
+    echo "unknown subcommand $cmd" >&2
+    exit 2
+    ;;
+esac
+echo "$cmd ok"
