@@ -117,7 +117,31 @@ struct X3Args {
     // NHWC output (fp32 for P 3, fp16 for P 1) and the A operand is
     // relu(x * s + t) — bn_apply's arithmetic — split into hi | lo (P 3) in LDS
     const float* in_ss = nullptr;          // [2C] scale | shift
+    // epilogue output stores (A/B: hkp_debug_x3_store): 0 each site's own flavour,
+    // 1 plain, 2 nontemporal, 3 sc1 (written through, not kept in the XCD's L2), 4 sc0 sc1
+    int st_kind = 0;
 };
+
+// One 16-B epilogue output store of flavour `kind` (X3Args::st_kind); dflt: the
+// site's own flavour for kind 0 (1 plain, 2 nontemporal)
+typedef unsigned x3u32x4 __attribute__((ext_vector_type(4)));
+template <typename V>
+__device__ __forceinline__ void x3_st16(V* p, const V& val, int kind, int dflt) {
+    static_assert(sizeof(V) == 16, "16-B store");
+    x3u32x4 v;
+    __builtin_memcpy(&v, &val, 16);
+    x3u32x4* q = (x3u32x4*)p;
+    const int k = kind ? kind : dflt;
+    if (k == 2) {
+        __builtin_nontemporal_store(v, q);
+    } else if (k == 3) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(q), "v"(v) : "memory");
+    } else if (k == 4) {
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(v) : "memory");
+    } else {
+        *q = v;
+    }
+}
 
 // debug phase stamps (s_memrealtime, 100 MHz) of one-tile conv blocks: slot k of
 // block b at stamps[b * 8 + k]; written by lane 0 of wave 0
@@ -600,7 +624,7 @@ __device__ __forceinline__ void x3_store_tile_f16(const X3Args& a, const char* s
         const int row = e / CH, cc = e - row * CH;
         const int m = m0 + row;
         if (m < a.M)
-            *(uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8) = *(const uint4*)(smem + (row * PITCH + cc * 8) * 2);
+            x3_st16((uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8), *(const uint4*)(smem + (row * PITCH + cc * 8) * 2), a.st_kind, 1);
     }
 }
 
@@ -664,7 +688,7 @@ __device__ __forceinline__ void x3_store_tile_f16_bn(const X3Args& a, const char
             if (relu) o = o > 0.f ? o : 0.f;
             h[k] = (_Float16)o;
         }
-        __builtin_nontemporal_store(h, (f16x8*)(a.y16 + off));
+        x3_st16((f16x8*)(a.y16 + off), h, a.st_kind, 2);
     }
 }
 
@@ -1032,7 +1056,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                     const int row = e / C4, c4 = e - row * C4;
                     const int m = m0 + h * RPP + row;
                     if (m < a.M)
-                        *(f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4) = *(const f32x4*)(t + row * PITCH + c4 * 4);
+                        x3_st16((f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4), *(const f32x4*)(t + row * PITCH + c4 * 4), a.st_kind, 1);
                 }
             } else {
 #pragma unroll 2
@@ -1736,7 +1760,7 @@ __device__ __forceinline__ void conv_x3_halo_body(const X3Args& a, char* smem) {
 #pragma unroll 4
         for (int e = tid; e < BM * CH; e += 512) {
             const int row = e / CH, cc = e - row * CH;
-            *(uint4*)(a.y16 + out_pix(row) * a.K + n0 + cc * 8) = *(const uint4*)(smem + (row * PITCH + cc * 8) * 2);
+            x3_st16((uint4*)(a.y16 + out_pix(row) * a.K + n0 + cc * 8), *(const uint4*)(smem + (row * PITCH + cc * 8) * 2), a.st_kind, 1);
         }
     } else {
         constexpr int PITCH = BN + 4, C4 = BN / 4;
@@ -2077,7 +2101,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
         for (int u = 0; u < NPT; ++u) {
             const int row = (tid + NT * u) / CH, m = m0 + row;
             if (m < a.M)
-                *(uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8) = *(const uint4*)(smem + (row * PITCH + cc * 8) * 2);
+                x3_st16((uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8), *(const uint4*)(smem + (row * PITCH + cc * 8) * 2), a.st_kind, 1);
         }
         return;
     }
@@ -2104,7 +2128,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
             if (relu) o = o > 0.f ? o : 0.f;
             h[k] = (_Float16)o;
         }
-        __builtin_nontemporal_store(h, (f16x8*)(a.y16 + (long)m * a.K + n0 + cc * 8));
+        x3_st16((f16x8*)(a.y16 + (long)m * a.K + n0 + cc * 8), h, a.st_kind, 2);
     }
 }
 
@@ -2964,6 +2988,7 @@ static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Ar
 static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 static int g_x3_stagger_ns = 0;                        // hkp_debug_x3_stagger
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
+static int g_x3_store = 0;                             // hkp_debug_x3_store
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -2992,6 +3017,7 @@ static void x3_dispatch_p(int P, F&& f) {
 static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
                       int64_t ws_bytes = 0) {
     a.stamps = g_x3_stamps;
+    a.st_kind = g_x3_store;
     a.stagger_ticks = g_x3_stagger_ns / 10;
     a.stagger_blocks = x3_cus();
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
@@ -3538,4 +3564,9 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // Debug / A/B (tools/ only, not thread-safe): nonzero runs an A3 grid's split-K
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
+
+// Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'
+// epilogue output stores (X3Args::st_kind: 0 each site's own, 1 plain, 2
+// nontemporal, 3 sc1, 4 sc0 sc1).
+extern "C" void hkp_debug_x3_store(int32_t kind) { g_x3_store = kind >= 0 && kind <= 4 ? kind : 0; }
 

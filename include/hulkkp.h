@@ -241,6 +241,10 @@ void hkp_debug_x3_stagger(int32_t ns);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs an A3 grid's split-K
  * tail as a launch of its own (conv_x3_tail_kernel) instead of appended to it. */
 void hkp_debug_x3_split_tail(int32_t on);
+/* Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'
+ * epilogue output stores: 0 each site's own (the default), 1 plain, 2
+ * nontemporal, 3 sc1 (written through, not kept in the XCD's L2), 4 sc0 sc1. */
+void hkp_debug_x3_store(int32_t kind);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

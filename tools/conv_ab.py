@@ -53,13 +53,19 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--nostats", action="store_true", help="no BN partials (epilogue cost A/B)")
     ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B)")
+    ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
+                    "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
     args = ap.parse_args()
     if args.lib:
         from hkp import _lib
         _lib.use_library(os.path.abspath(args.lib))
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
-    tiles = [int(v) for v in args.tiles.split(",")]
+    from hkp._lib import lib
+    forms = [(int(t), int(k)) for t in args.tiles.split(",") for k in args.stores.split(",")]
+
+    def set_store(k):
+        lib().hkp_debug_x3_store(k)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):
@@ -82,28 +88,33 @@ def main():
             def run(t):
                 return ops.conv2d_fwd_f16(xs, ws, st, pd, dl, stats=not args.nostats, tile=t)[0]
         del x
-        outs, times = {}, {t: [] for t in tiles}
+        outs, times = {}, {f: [] for f in forms}
         for r in range(args.rounds):
-            for t in tiles:
+            for f in forms:
+                t = f[0]
+                set_store(f[1])
                 y = run(t)
                 if r == 0:
-                    outs[t] = y.float()
+                    outs[f] = y.float()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(args.iters):
                     run(t)
                 e.record()
                 torch.cuda.synchronize()
-                times[t].append(s.elapsed_time(e) / args.iters)
+                times[f].append(s.elapsed_time(e) / args.iters)
+        set_store(0)
         ho, wo = ops.conv_out_hw(h, w, k, k, st, pd, dl)
         flops = 2.0 * n * ho * wo * co * ci * k * k * passes
-        ref = outs[tiles[0]]
-        same = max((outs[t] - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30) for t in tiles)
-        for t in tiles:
-            ts = sorted(times[t])
+        ref = outs[forms[0]]
+        same = max((outs[f] - ref).abs().max().item() / max(ref.abs().max().item(), 1e-30) for f in forms)
+        for f in forms:
+            t = f[0]
+            ts = sorted(times[f])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
-            print("%-9s tile %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  max rel diff=%.1e" % (
-                name, t, ts[len(ts) // 2], ts[0], flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same), flush=True)
+            print("%-9s tile %d store %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  max rel diff=%.1e" % (
+                name, t, f[1], ts[len(ts) // 2], ts[0], flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same),
+                flush=True)
 
 
 if __name__ == "__main__":

@@ -21,10 +21,14 @@ import torch  # noqa: E402
 
 
 def parse(form):
+    """Policy overrides of a form; the pseudo-field store=K is the library's
+    epilogue store flavour (hkp_debug_x3_store), not a Policy field."""
     from hkp.policy import DEFAULT
     kw = {}
     for item in filter(None, form.split(",")):
         k, _, v = item.partition("=")
+        if k == "store":
+            continue
         cur = getattr(DEFAULT, k)
         kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
     return kw
@@ -56,15 +60,19 @@ def main():
         with torch.no_grad():
             return model.heatmaps_and_keypoints(x)
     pols = [base.with_(**parse(f)) for f in args.forms]
-    for p in pols:                       # warm every form (kernels, caches, plans)
+    stores = [int(dict(i.partition("=")[::2] for i in filter(None, f.split(","))).get("store", 0))
+              for f in args.forms]
+    for p, st in zip(pols, stores):      # warm every form (kernels, caches, plans)
         model.policy = p
+        hkp.lib().hkp_debug_x3_store(st)
         for _ in range(3):
             step()
     torch.cuda.synchronize()
     res = {f: [] for f in args.forms}
     for _ in range(args.rounds):
-        for f, p in zip(args.forms, pols):
+        for f, p, st in zip(args.forms, pols, stores):
             model.policy = p
+            hkp.lib().hkp_debug_x3_store(st)
             step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -72,6 +80,7 @@ def main():
                 step()
             torch.cuda.synchronize()
             res[f].append(B * args.iters / (time.perf_counter() - t0))
+    hkp.lib().hkp_debug_x3_store(0)
     for f in args.forms:
         print("%-40s %.1f img/s  (%s)" % (f or "(default)", statistics.median(res[f]),
                                           " ".join("%.1f" % v for v in res[f])), flush=True)

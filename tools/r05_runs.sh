@@ -5,6 +5,8 @@
 #   duo       the DUO body (plain-fp16 256x128, two blocks per CU): its parity tests,
 #             per-conv A/B vs the planner (tools/conv_ab.py), C4 A/B in one process
 #             (tools/infer_ab.py), then the GPU suite and the default bench line
+#   store     epilogue store flavour A/B (hkp_debug_x3_store: default / nt / sc1) per conv
+#             and end to end on C4 and C2, in one process each
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -32,6 +34,15 @@ duo)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
     echo "pytest: $(tail -1 $O/pytest_gpu.log)"
     timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
+    ;;
+store)
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,13 --stores 0,2,3 --rounds 5 --iters 5 \
+        --shapes c4_l4_c3,c4_l4_ds,c4_l3_c3,c4_l3_c1,c4_l1_ds,layer4,layer3 > $O/conv_ab.log 2>&1
+    echo "conv_ab ok"
+    timeout -k 10 500 python -u tools/infer_ab.py "" "store=2" "store=3" "f16_tile_1x1=13,store=3" \
+        --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    echo "infer_ab c4 ok"
+    timeout -k 10 500 python -u tools/infer_ab.py "" "store=2" "store=3" --rounds 5 --iters 10 > $O/ab_c2.log 2>&1
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
