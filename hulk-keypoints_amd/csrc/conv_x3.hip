@@ -1916,6 +1916,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
     constexpr int UM = 8, UN = 4;                    // 16x16 tiles per wave (wave tile 128 x 64)
     constexpr int GA = 4, GB = 2, GL = GA + GB;      // DMA pieces (16 rows each) per wave per stage
 
+    x3_stamp(a, 0);
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -2024,6 +2025,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();
+    x3_stamp(a, 1);
     read_a(smem);
 #pragma unroll
     for (int j = 0; j < UN; ++j) read_b(j, smem);
@@ -2058,9 +2060,11 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
 #pragma unroll
     for (int j = 0; j < UN; ++j) mma_col(j);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the ring past here
+    x3_stamp(a, 2);
 
     // ---- epilogue: BN partials of this wave's 128-row half, then the fp16 tile ----
     if (a.part) duo_bn_partials<UM, UN>(a, acc, sc, m0 + 128 * wm, n0 + wn * 64, lane);
+    x3_stamp(a, 3);
     constexpr int PITCH = BN + 8, CH = BN / 8, SS_OFF = BM * PITCH * 2;
     constexpr int NT = 256, NPT = BM * CH / NT;              // 16-B chunks per thread
     static_assert(NT % CH == 0, "a thread keeps its 8 channels");
@@ -2096,6 +2100,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
         ssl[2 * BN + tid] = ep1;
     }
     lds_sync();
+    x3_stamp(a, 4);
     if (!a.ep_ss) {
 #pragma unroll 4
         for (int u = 0; u < NPT; ++u) {
@@ -2103,6 +2108,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
             if (m < a.M)
                 x3_st16((uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8), *(const uint4*)(smem + (row * PITCH + cc * 8) * 2), a.st_kind, 1);
         }
+        x3_stamp(a, 5);
         return;
     }
     float sa[8], sb[8], ra[8], rb[8];
@@ -2130,6 +2136,7 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
         }
         x3_st16((f16x8*)(a.y16 + (long)m * a.K + n0 + cc * 8), h, a.st_kind, 2);
     }
+    x3_stamp(a, 5);
 }
 
 // ---------------------------------------------------------------------------

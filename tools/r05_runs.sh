@@ -7,6 +7,8 @@
 #             (tools/infer_ab.py), then the GPU suite and the default bench line
 #   store     epilogue store flavour A/B (hkp_debug_x3_store: default / nt / sc1) per conv
 #             and end to end on C4 and C2, in one process each
+#   stamps    per-block phase clocks of the A3 and DUO bodies on C4's 1x1 shapes
+#             (tools/x3_stamps.py); training store-flavour A/B (tools/train_ab.py)
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -43,6 +45,11 @@ store)
         --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     echo "infer_ab c4 ok"
     timeout -k 10 500 python -u tools/infer_ab.py "" "store=2" "store=3" --rounds 5 --iters 10 > $O/ab_c2.log 2>&1
+    ;;
+stamps)
+    timeout -k 10 300 python -u tools/x3_stamps.py c4_l4_c3 c4_l4_ds c4_l3_c3 c4_l1_ds > $O/stamps_a3.log 2>&1
+    timeout -k 10 300 python -u tools/x3_stamps.py --tile 13 c4_l4_c3 c4_l4_ds c4_l3_c3 c4_l1_ds > $O/stamps_duo.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "" "store=2" "store=3" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1

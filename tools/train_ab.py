@@ -20,10 +20,14 @@ import torch  # noqa: E402
 
 
 def parse(form):
+    """Policy overrides of a form; the pseudo-field store=K is the library's
+    epilogue store flavour (hkp_debug_x3_store), not a Policy field."""
     from hkp.policy import DEFAULT
     kw = {}
     for item in filter(None, form.split(",")):
         k, _, v = item.partition("=")
+        if k == "store":
+            continue
         cur = getattr(DEFAULT, k)
         kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
     return kw
@@ -52,15 +56,19 @@ def main():
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99)).to(dev)
     trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4)
     pols = [base.with_(**parse(f)) for f in args.forms]
-    for p in pols:                       # warm every form (kernels, caches, plans)
+    stores = [int(dict(i.partition("=")[::2] for i in filter(None, f.split(","))).get("store", 0))
+              for f in args.forms]
+    for p, st in zip(pols, stores):      # warm every form (kernels, caches, plans)
         model.policy = trainer.policy = p
+        hkp.lib().hkp_debug_x3_store(st)
         for _ in range(3):
             trainer.step(x, uv)
     torch.cuda.synchronize()
     res = {f: [] for f in args.forms}
     for _ in range(args.rounds):
-        for f, p in zip(args.forms, pols):
+        for f, p, st in zip(args.forms, pols, stores):
             model.policy = trainer.policy = p
+            hkp.lib().hkp_debug_x3_store(st)
             trainer.step(x, uv)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -68,6 +76,7 @@ def main():
                 trainer.step(x, uv)
             torch.cuda.synchronize()
             res[f].append(B * args.iters / (time.perf_counter() - t0))
+    hkp.lib().hkp_debug_x3_store(0)
     for f in args.forms:
         print("%-40s %.1f img/s  (%s)" % (f or "(default)", statistics.median(res[f]),
                                           " ".join("%.1f" % v for v in res[f])), flush=True)

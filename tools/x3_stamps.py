@@ -24,7 +24,13 @@ def main():
     from hkp._lib import lib
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
-    for name in sys.argv[1:]:
+    args = sys.argv[1:]
+    tile = 0
+    if "--tile" in args:                 # HKP_TILE_* (e.g. 13: the DUO body)
+        i = args.index("--tile")
+        tile = int(args[i + 1])
+        del args[i:i + 2]
+    for name in args:
         prec, n, h, w, ci, co, k, st, pd, dl = SHAPES[name]
         x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
         wt = torch.randn(co, k, k, ci, device=dev, generator=g) * (2.0 / (k * k * co)) ** 0.5
@@ -32,15 +38,15 @@ def main():
             ss = torch.cat([torch.ones(ci, device=dev), torch.zeros(ci, device=dev)])
             xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
             ws = ops.weight_pack_x3(wt)
-            run = lambda: ops.conv2d_fwd_x3(xs, ws, st, pd, dl, sk=False)  # noqa: E731
+            run = lambda: ops.conv2d_fwd_x3(xs, ws, st, pd, dl, sk=False, tile=tile)  # noqa: E731
         else:
             xs = x.half()
             ws = ops.weight_pack_f16(wt)
-            run = lambda: ops.conv2d_fwd_f16(xs, ws, st, pd, dl, sk=False)  # noqa: E731
+            run = lambda: ops.conv2d_fwd_f16(xs, ws, st, pd, dl, sk=False, tile=tile)  # noqa: E731
         for _ in range(3):
             run()
         ho, wo = ops.conv_out_hw(h, w, k, k, st, pd, dl)
-        blocks = ((n * ho * wo + 255) // 256) * (co // (256 if co % 256 == 0 else 128)) * 2 + 64
+        blocks = ((n * ho * wo + 255) // 256) * (co // 64) * 2 + 64
         buf = torch.zeros(blocks * 8, dtype=torch.int64, device=dev)
         lib().hkp_debug_x3_stamps(buf.data_ptr())
         run()
@@ -55,8 +61,8 @@ def main():
             d = (s[:, i + 1] - s[:, i]) / 100.0
             out.append("%s %.2f" % (ph, d.median().item()))
         tot = ((s[:, 5] - s[:, 0]) / 100.0).median().item()
-        print("%-9s blocks %d  span %.1f us  per-block median total %.2f us: %s" % (
-            name, s.shape[0], span.item(), tot, ", ".join(out)), flush=True)
+        print("%-9s tile %d blocks %d  span %.1f us  per-block median total %.2f us: %s" % (
+            name, tile, s.shape[0], span.item(), tot, ", ".join(out)), flush=True)
         # start-time spread of consecutive waves of blocks
         starts = ((s[:, 0] - t0) / 100.0).sort().values
         print("          block starts: p10 %.1f p50 %.1f p90 %.1f us" % (
