@@ -148,6 +148,13 @@ __device__ __forceinline__ void x3_st16(V* p, const V& val, int kind, int dflt) 
 __device__ __forceinline__ void x3_stamp(const X3Args& a, int k) {
     if (a.stamps && threadIdx.x == 0) a.stamps[blockIdx.x * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
+// debug: where the block runs — slot 6: HW_REG_HW_ID (CU / SH / SE ids), slot 7: HW_REG_XCC_ID
+__device__ __forceinline__ void x3_stamp_where(const X3Args& a) {
+    if (a.stamps && threadIdx.x == 0) {
+        a.stamps[blockIdx.x * 8 + 6] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+        a.stamps[blockIdx.x * 8 + 7] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
+}
 
 // 2^e putting max|x| in [2^13, 2^14) (1 for 0 / non-finite): exact scaling
 __device__ __forceinline__ float pow2_scale_of(float m) {
@@ -1824,6 +1831,10 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_bnin_kernel(X3Args a) {
 // as 16-B row chunks, optionally through the fused BN + residual + ReLU
 // (hkp_conv2d_fwd_f16_bn) — the 256x256 body's arithmetic, element for element.
 constexpr int DUO_BM = 256, DUO_BN = 128, DUO_ROW = 64, DUO_NST = 3;
+// first-round arrivals per CU (key: XCC id x the HW_ID's SE / SH / CU bits): the
+// second block to arrive on a CU starts late, so the two blocks sharing it run
+// half a block apart (see conv_x3_duo_kernel); parity of a running count, never reset
+__device__ unsigned g_duo_cu_cnt[8 * 128];
 constexpr int DUO_STAGE = (DUO_BM + DUO_BN) * DUO_ROW;                 // 24 KiB
 constexpr int DUO_LDS = DUO_NST * DUO_STAGE;                           // 72 KiB: two blocks per CU
 static_assert(DUO_BM * (DUO_BN + 8) * 2 + 4 * DUO_BN * 4 <= DUO_LDS, "DUO epilogue staging");
@@ -1917,6 +1928,26 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
     constexpr int GA = 4, GB = 2, GL = GA + GB;      // DMA pieces (16 rows each) per wave per stage
 
     x3_stamp(a, 0);
+    x3_stamp_where(a);
+    // Co-resident blocks of a one-round-per-tile grid start together and, doing the
+    // same work, stay in phase: both fill, both run the K loop, both run the
+    // epilogue — nothing overlaps.  In the first round the second block to arrive
+    // on each CU waits about half a block's lifetime (X3Args::stagger_ticks), so
+    // from then on one block's fill and epilogue run beside the other's K loop.
+    if (a.stagger_ticks > 0 && blockIdx.x < (unsigned)a.stagger_blocks) {
+        __shared__ int late;
+        if (threadIdx.x == 0) {
+            const unsigned hw = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+            const unsigned xcc = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);   // HW_REG_XCC_ID
+            const unsigned key = (xcc & 7) * 128 + ((hw >> 8) & 127);
+            late = (int)(atomicAdd(&g_duo_cu_cnt[key], 1u) & 1u);
+        }
+        __syncthreads();
+        if (late) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)a.stagger_ticks) __builtin_amdgcn_s_sleep(8);
+        }
+    }
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = mt * BM, n0 = nt * BN;
@@ -2996,6 +3027,7 @@ static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
 static int g_x3_stagger_ns = 0;                        // hkp_debug_x3_stagger
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
 static int g_x3_store = 0;                             // hkp_debug_x3_store
+static int g_duo_stagger_ns = -1;                      // hkp_debug_duo_stagger
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -3034,7 +3066,14 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.nks = nks;
     a.sk_units = 0;
     if (c.duo) {
-        hipLaunchKernelGGL(conv_x3_duo_kernel<1>, dim3((unsigned)(m_tiles * a.n_tiles)), dim3(256), 0, st, a);
+        // first-round stagger of the second block on each CU: half a block's
+        // lifetime, ~(fill + epilogue + K loop) / 2 — hkp_debug_duo_stagger overrides
+        // (ns; 0 = off, < 0 = this estimate)
+        const long blocks = m_tiles * a.n_tiles;
+        const int ns = g_duo_stagger_ns < 0 ? 5500 + 450 * 2 * nks : g_duo_stagger_ns;
+        a.stagger_ticks = blocks > 2L * x3_cus() ? ns / 10 : 0;
+        a.stagger_blocks = 2 * x3_cus();
+        hipLaunchKernelGGL(conv_x3_duo_kernel<1>, dim3((unsigned)blocks), dim3(256), 0, st, a);
         return;
     }
     if (c.halo) {
@@ -3576,4 +3615,8 @@ extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0;
 // epilogue output stores (X3Args::st_kind: 0 each site's own, 1 plain, 2
 // nontemporal, 3 sc1, 4 sc0 sc1).
 extern "C" void hkp_debug_x3_store(int32_t kind) { g_x3_store = kind >= 0 && kind <= 4 ? kind : 0; }
+
+// Debug / A/B (tools/ only, not thread-safe): the DUO body's first-round stagger of
+// the second block on each CU, in ns (0 = off; < 0 = the planner's estimate).
+extern "C" void hkp_debug_duo_stagger(int32_t ns) { g_duo_stagger_ns = ns; }
 

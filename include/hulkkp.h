@@ -245,6 +245,10 @@ void hkp_debug_x3_split_tail(int32_t on);
  * epilogue output stores: 0 each site's own (the default), 1 plain, 2
  * nontemporal, 3 sc1 (written through, not kept in the XCD's L2), 4 sc0 sc1. */
 void hkp_debug_x3_store(int32_t kind);
+/* Debug / A/B (tools/ only, not thread-safe): the DUO body's (HKP_TILE_DUO)
+ * first-round delay of the second block on each CU, in ns (0 = off, < 0 = the
+ * default estimate of half a block's lifetime). */
+void hkp_debug_duo_stagger(int32_t ns);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--shapes", default=",".join(SHAPES))
     ap.add_argument("--nostats", action="store_true", help="no BN partials (epilogue cost A/B)")
     ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B)")
+    ap.add_argument("--duo-staggers", default="-1", help="DUO first-round stagger(s) in ns to cross with the "
+                    "tiles (hkp_debug_duo_stagger: 0 off, -1 the default estimate)")
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
     args = ap.parse_args()
@@ -62,10 +64,12 @@ def main():
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     from hkp._lib import lib
-    forms = [(int(t), int(k)) for t in args.tiles.split(",") for k in args.stores.split(",")]
+    forms = [(int(t), int(k), int(d)) for t in args.tiles.split(",") for k in args.stores.split(",")
+             for d in args.duo_staggers.split(",")]
 
-    def set_store(k):
+    def set_store(k, d=-1):
         lib().hkp_debug_x3_store(k)
+        lib().hkp_debug_duo_stagger(d)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):
@@ -92,7 +96,7 @@ def main():
         for r in range(args.rounds):
             for f in forms:
                 t = f[0]
-                set_store(f[1])
+                set_store(f[1], f[2])
                 y = run(t)
                 if r == 0:
                     outs[f] = y.float()
@@ -112,8 +116,8 @@ def main():
             t = f[0]
             ts = sorted(times[f])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
-            print("%-9s tile %d store %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  max rel diff=%.1e" % (
-                name, t, f[1], ts[len(ts) // 2], ts[0], flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same),
+            print("%-9s tile %d store %d stagger %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  max rel diff=%.1e" % (
+                name, t, f[1], f[2], ts[len(ts) // 2], ts[0], flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same),
                 flush=True)
 
 

@@ -9,6 +9,8 @@
 #             and end to end on C4 and C2, in one process each
 #   stamps    per-block phase clocks of the A3 and DUO bodies on C4's 1x1 shapes
 #             (tools/x3_stamps.py); training store-flavour A/B (tools/train_ab.py)
+#   duo_stagger  DUO with its first-round per-CU stagger: phase stamps, per-conv and
+#             C4 A/B
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -50,6 +52,16 @@ stamps)
     timeout -k 10 300 python -u tools/x3_stamps.py c4_l4_c3 c4_l4_ds c4_l3_c3 c4_l1_ds > $O/stamps_a3.log 2>&1
     timeout -k 10 300 python -u tools/x3_stamps.py --tile 13 c4_l4_c3 c4_l4_ds c4_l3_c3 c4_l1_ds > $O/stamps_duo.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "" "store=2" "store=3" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
+duo_stagger)
+    for d in 0 -1 4000 10000; do
+        timeout -k 10 300 python -u tools/x3_stamps.py --tile 13 --duo-stagger $d c4_l4_c3 c4_l3_c3 c4_l1_ds \
+            > $O/stamps_duo_$d.log 2>&1
+    done
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,13 --duo-staggers 0,-1,4000,10000 --rounds 5 --iters 5 \
+        --shapes c4_l4_c3,c4_l4_ds,c4_l4_c1,c4_l3_c3,c4_l3_c1,c4_l3_c2,c4_l2_c1,c4_l1_ds > $O/conv_ab.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_1x1=13" "f16_tile_1x1=13,f16_tile_kxk=13" \
+        --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1

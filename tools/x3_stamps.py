@@ -30,6 +30,10 @@ def main():
         i = args.index("--tile")
         tile = int(args[i + 1])
         del args[i:i + 2]
+    if "--duo-stagger" in args:          # hkp_debug_duo_stagger (ns; 0 off, < 0 default)
+        i = args.index("--duo-stagger")
+        lib().hkp_debug_duo_stagger(int(args[i + 1]))
+        del args[i:i + 2]
     for name in args:
         prec, n, h, w, ci, co, k, st, pd, dl = SHAPES[name]
         x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
@@ -63,6 +67,42 @@ def main():
         tot = ((s[:, 5] - s[:, 0]) / 100.0).median().item()
         print("%-9s tile %d blocks %d  span %.1f us  per-block median total %.2f us: %s" % (
             name, tile, s.shape[0], span.item(), tot, ", ".join(out)), flush=True)
+        if tile == 13:
+            # DUO (two blocks per CU): which first-round blocks share a CU (slot 6 = HW_ID,
+            # slot 7 = XCC_ID, recorded by the DUO body), and how far apart they start
+            full = buf.view(-1, 8).cpu()
+            idx = torch.nonzero(full[:, 0] != 0).flatten()
+            st0 = full[idx, 0].double()
+            first = idx[(st0 - st0.min()) / 100.0 < 2.0]             # blocks started within 2 us
+            cu = {}
+            for b in first.tolist():
+                hw, xcc = int(full[b, 6]), int(full[b, 7])
+                key = (xcc & 0xF, (hw >> 13) & 7, (hw >> 12) & 1, (hw >> 8) & 0xF)
+                cu.setdefault(key, []).append(b)
+            pairs = [sorted(v) for v in cu.values() if len(v) == 2]
+            diffs = {}
+            for p in pairs:
+                diffs[p[1] - p[0]] = diffs.get(p[1] - p[0], 0) + 1
+            print("          first-round blocks %d on %d CUs; blocks per CU %s; pair index gaps (count) %s"
+                  % (len(first), len(cu), sorted({len(v) for v in cu.values()}),
+                     sorted(diffs.items(), key=lambda kv: -kv[1])[:6]))
+            print("          sample pairs %s" % pairs[:8])
+            # phase of the two slots of a CU over the whole launch: gap between
+            # consecutive block starts on one CU / block lifetime (0 = in lockstep,
+            # 0.5 = half a block apart)
+            allcu = {}
+            for b in idx.tolist():
+                hw, xcc = int(full[b, 6]), int(full[b, 7])
+                key = (xcc & 0xF, (hw >> 13) & 7, (hw >> 12) & 1, (hw >> 8) & 0xF)
+                allcu.setdefault(key, []).append(int(full[b, 0]))
+            life = float(((full[idx, 5] - full[idx, 0]) / 100.0).median())
+            ph = []
+            for v in allcu.values():
+                v.sort()
+                ph += [min(1.0, (v[i + 1] - v[i]) / 100.0 / life) for i in range(len(v) - 1)]
+            ph = torch.tensor(ph)
+            print("          start gap on a CU / lifetime: p10 %.2f p50 %.2f p90 %.2f" % (
+                ph.quantile(0.1).item(), ph.median().item(), ph.quantile(0.9).item()))
         # start-time spread of consecutive waves of blocks
         starts = ((s[:, 0] - t0) / 100.0).sort().values
         print("          block starts: p10 %.1f p50 %.1f p90 %.1f us" % (
