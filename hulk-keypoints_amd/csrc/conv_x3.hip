@@ -123,7 +123,11 @@ struct X3Args {
 };
 
 // One 16-B epilogue output store of flavour `kind` (X3Args::st_kind); dflt: the
-// site's own flavour for kind 0 (1 plain, 2 nontemporal)
+// site's own flavour for kind 0 (1 plain, 2 nontemporal).  Measured per site
+// (tools/conv_ab.py / infer_ab.py --stores, profiles/r05_store_ab.log): the fp32
+// ring-body tile nontemporal (C2 +0.8 %); the plain-fp16 tile plain (C4: nt -0.4 %,
+// sc1 -1.6 % end to end, although nt wins 4-7 % per conv in isolation), the fused
+// BN epilogue nontemporal
 typedef unsigned x3u32x4 __attribute__((ext_vector_type(4)));
 template <typename V>
 __device__ __forceinline__ void x3_st16(V* p, const V& val, int kind, int dflt) {
@@ -1063,7 +1067,10 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                     const int row = e / C4, c4 = e - row * C4;
                     const int m = m0 + h * RPP + row;
                     if (m < a.M)
-                        x3_st16((f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4), *(const f32x4*)(t + row * PITCH + c4 * 4), a.st_kind, 1);
+                        // nontemporal (in-process A/B, profiles/r05_store_ab.log: C2 1825.7 ->
+                        // 1841.1 img/s; C3 training 464.6 both)
+                        x3_st16((f32x4*)(a.y + (long)m * a.K + n0 + c4 * 4), *(const f32x4*)(t + row * PITCH + c4 * 4),
+                                a.st_kind, 2);
                 }
             } else {
 #pragma unroll 2
@@ -2948,6 +2955,17 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
     if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
     X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
     if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
+    // AUTO, plain fp16: the DUO body where it measured faster than the one-tile
+    // bodies (tools/conv_ab.py, in-process, profiles/r05_duo_*): K-depth 64 (one
+    // K-step: C4's layer1 1x1 expansions, 64 -> 256: -12 %, all fill and epilogue)
+    // and 128-wide outputs (layer2: -4...-10 % against the one-block 256x128 body);
+    // the long-K 256-wide shapes stay on A3 (DUO +10...+33 %: its half-line stream
+    // moves 1.5x the operand bytes per MAC).  AUTO_A3 keeps the round-4 planner.
+    if (policy == HKP_TILE_AUTO && P == 1 && !c.halo && k % DUO_BN == 0 && (nks == 1 || k == DUO_BN)) {
+        X3Choice d{DUO_BN, 16, false, false};
+        d.duo = true;
+        return d;
+    }
     return c;
 }
 static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo) {

@@ -79,7 +79,8 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_HALO 10              /* 8x32-pixel halo tiles (stride-1 3x3, pad = dil = 1, Ho%8 = Wo%32 = 0;
                                          the default there under AUTO and 256_TAIL when the
                                          input has 64 channels) */
-#define HKP_TILE_AUTO_A3 12           /* AUTO with its 256x256 one-tile grids on the A3 body */
+#define HKP_TILE_AUTO_A3 12           /* the round-4 planner: AUTO without its plain-fp16 DUO
+                                         choices (K-depth 64, 128-wide outputs) */
 #define HKP_TILE_256_A3 11            /* 256x256 on the A3 body (A ring 3 stages deep, B ring 2: an A
                                          line has two K-steps to land) + the split-K tail of 9 */
 #define HKP_TILE_DUO 13               /* plain fp16 (hkp_conv2d_fwd_f16 / _f16_bn) only: 256x128 tiles,

@@ -161,8 +161,18 @@ def test_kernel_name_query():
     d.tile = _lib.HKP_TILE_256
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<256, false, false, 16, false, 3>"
     assert ops.kernel_name(d, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_kernel<256>"
-    d.tile = _lib.HKP_TILE_AUTO_A3                                   # an alias of AUTO
+    d.tile = _lib.HKP_TILE_AUTO_A3                                   # AUTO without the DUO choices
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
+    # plain fp16: the DUO body at K-depth 64 and for 128-wide outputs (AUTO), not under AUTO_A3
+    l1 = _lib.ConvDesc(128, 120, 160, 64, 256, 1, 1, 1, 0, 1, 0)
+    l2 = _lib.ConvDesc(128, 60, 80, 128, 128, 3, 3, 1, 1, 1, 0)
+    for dd in (l1, l2):
+        assert ops.kernel_name(dd, _lib.HKP_KOP_FWD_F16) == "conv_x3_duo_kernel<1>"
+        assert ops.kernel_name(dd, _lib.HKP_KOP_FWD_X3) != "conv_x3_duo_kernel<1>"
+        dd.tile = _lib.HKP_TILE_AUTO_A3
+        assert ops.kernel_name(dd, _lib.HKP_KOP_FWD_F16) != "conv_x3_duo_kernel<1>"
+    assert ops.kernel_name(_lib.ConvDesc(128, 60, 80, 512, 2048, 1, 1, 1, 0, 1, 0),
+                           _lib.HKP_KOP_FWD_F16) == "conv_x3_a3_kernel<1>"
     d.tile = _lib.HKP_TILE_256_A3
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3_W16) == "conv_x3_a3_kernel<2>"
