@@ -11,6 +11,8 @@
 #             (tools/x3_stamps.py); training store-flavour A/B (tools/train_ab.py)
 #   duo_stagger  DUO with its first-round per-CU stagger: phase stamps, per-conv and
 #             C4 A/B
+#   verify    GPU suite, C4 planner A/B (DUO choices vs the round-4 planner), default
+#             and C4 bench lines
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -62,6 +64,15 @@ duo_stagger)
         --shapes c4_l4_c3,c4_l4_ds,c4_l4_c1,c4_l3_c3,c4_l3_c1,c4_l3_c2,c4_l2_c1,c4_l1_ds > $O/conv_ab.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_1x1=13" "f16_tile_1x1=13,f16_tile_kxk=13" \
         --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+verify)
+    timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_gpu.log)"
+    timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_1x1=12,f16_tile_kxk=12" \
+        --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 7 --iters 5 > $O/ab_c4.log 2>&1
+    timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
+    timeout -k 10 400 python -u bench.py --backbone resnet50 --keypoints 8 --batch 128 --precision f16 \
+        --no-cpu-baseline > $O/bench_c4.log 2>&1
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
