@@ -492,9 +492,12 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
         roof["hbm_bound_share_of_attainable"] = t_hbm / t_att if t_att > 0 else 0.0
     tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
     c4 = (args.backbone, K, H, W) == ("resnet50", 8, 480, 640) and precision == "f16" and mode == "infer"
+    c5 = (args.backbone, K, H, W) == ("resnet50", 8, 960, 1280) and precision == "f16x3" and mode == "train"
     if c4:
         tag = "infer_c4"
-    if ((args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3") or c4:
+    if c5:
+        tag = "train_c5"
+    if ((args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3") or c4 or c5:
         (roof["traffic"], roof["traffic_source"], roof["pmc_pass_avg_ms"],
          roof["folded_kernel"]) = pmc_traffic(dom_sym, tag)
         # the kernel trace of the bench command itself (not the serialised PMC pass)

@@ -1543,8 +1543,8 @@ __global__ __launch_bounds__(512, 1) void conv_x3_tail_kernel(X3Args a) {
 // (m/32 + r) * 34 + m%32 + s for tap (r, s)); only the 64-row weight stage
 // streams per K-step (a 3-slot ring).  A tile moves 2 x 42.5 + 18 x 8 = 229 KB
 // from L2 instead of 18 x 40 = 720 KB.  Lines past the image are zero lines.
-// The 16-B chunk swizzle (line >> 1) & 7 is keyed on the halo line, so any 16
-// consecutive lines a fragment read touches are conflict-free, as in the ring.
+// The 16-B chunk swizzle (halo_swz: line & 6) is keyed on the halo line, so any
+// 16 consecutive lines a fragment read touches are conflict-free, as in the ring.
 // Two blocks per CU (72 KB each): one block's halo reload / epilogue overlaps the
 // other's MFMAs.  256 x 64 tile, 8 waves 4 x 2 (wave tile 64 x 32), 16x16x32
 // MFMAs; epilogue = the one-tile kernels' (BN tile partials from the
@@ -1554,6 +1554,16 @@ constexpr int HALO_GA = 6;                                   // halo DMA instruc
 constexpr int HALO_ABYTES = 8 * HALO_GA * 8 * 128;           // 48 KiB: halo image (+ 44 dummy lines)
 constexpr int HALO_NSTB = 3, HALO_BSTAGE = 64 * 128;         // weight ring: 3 x 8 KiB
 constexpr int HALO_LDS = HALO_ABYTES + HALO_NSTB * HALO_BSTAGE;
+
+// 16-B chunk swizzle of halo line L: physical chunk = logical ^ (L & 6).  A
+// fragment read covers 16 consecutive lines from ANY start (the tap offsets and
+// the 34-line patch rows put it anywhere), so the ring bodies' (row >> 1) & 7 —
+// conflict-free only from a 4-aligned start — cost ~3 extra LDS cycles per
+// ds_read_b128 here (0.30 of the halo kernels' LDS cycles, PMC r04); keyed on
+// bits 1-2 of L alone, every ds_read_b128 lane group of a read from any start
+// line hits 16 distinct 16-B bank slots (bit 0 of L picks the 128-B half, and the
+// group's two q values differ in bit 0 of the chunk).
+__device__ __forceinline__ int halo_swz(int L) { return L & 6; }
 
 static bool halo_shape(int stride, int r, int s, int pad, int dil, int ho, int wo, int k) {
     return stride == 1 && r == 3 && s == 3 && pad == 1 && dil == 1 && ho % HALO_PH == 0 && wo % HALO_PW == 0 &&
@@ -1585,7 +1595,7 @@ __device__ __forceinline__ void x3_halo_bnin(const X3Args& a, char* smem, int g,
 #pragma unroll
     for (int L0 = 0; L0 < NL; L0 += LPI) {
         const int L = L0 + tid / PIECES;
-        const int sw = (L >> 1) & 7;
+        const int sw = halo_swz(L);
         char* line = smem + L * ROW;
         if constexpr (P == 1) {
             f16x8* ch = (f16x8*)(line + ((j ^ sw) << 4));
@@ -1641,7 +1651,7 @@ __device__ __forceinline__ void conv_x3_halo_body(const X3Args& a, char* smem) {
 #pragma unroll
     for (int i = 0; i < HALO_GA; ++i) {
         const int L = 8 * (w * HALO_GA + i) + lane / 8;
-        const int Lc = (lane % 8) ^ ((L >> 1) & 7);
+        const int Lc = (lane % 8) ^ halo_swz(L);
         const int hl = L / HALO_LW, wl = L - hl * HALO_LW;
         const int hi = h0 - 1 + hl, wi = w0 - 1 + wl;
         const bool in = L < HALO_NL && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
@@ -1708,7 +1718,7 @@ __device__ __forceinline__ void conv_x3_halo_body(const X3Args& a, char* smem) {
 #pragma unroll
         for (int i = 0; i < UM; ++i) {
             const int L = lb[i] + toff;
-            const int ls = (L >> 1) & 7;
+            const int ls = halo_swz(L);
             ah[i] = *(const f16x8*)(smem + L * ROW + ((q ^ ls) << 4));
             al[i] = *(const f16x8*)(smem + L * ROW + (((4 + q) ^ ls) << 4));
         }
