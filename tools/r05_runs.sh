@@ -13,6 +13,9 @@
 #             C4 A/B
 #   verify    GPU suite, C4 planner A/B (DUO choices vs the round-4 planner), default
 #             and C4 bench lines
+#   halo      the conflict-free halo swizzle: bit-identity tests, per-conv A/B against the
+#             previous build (tools/ab_lib/libhulkkp_a.so), LDS bank-conflict PMC on C2 / C4,
+#             C2 bench A/B
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -73,6 +76,25 @@ verify)
     timeout -k 10 400 python -u bench.py > $O/bench.log 2>&1
     timeout -k 10 400 python -u bench.py --backbone resnet50 --keypoints 8 --batch 128 --precision f16 \
         --no-cpu-baseline > $O/bench_c4.log 2>&1
+    ;;
+halo)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_precision.py \
+        -k "halo or fused_input_bn" > $O/pytest_halo.log 2>&1
+    echo "pytest halo: $(tail -1 $O/pytest_halo.log)"
+    timeout -k 10 300 python -u tools/conv_ab.py --tiles 0 --shapes layer1,c4_l1_c2,h128 --rounds 7 --iters 10 \
+        --lib tools/ab_lib/libhulkkp_a.so > $O/conv_a.log 2>&1
+    timeout -k 10 300 python -u tools/conv_ab.py --tiles 0 --shapes layer1,c4_l1_c2,h128 --rounds 7 --iters 10 \
+        > $O/conv_b.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
+        --kernel-include-regex "halo" -d $O/pmc/pass1 -o run -- python3 bench.py --steps 3 --no-extras \
+        --no-cpu-baseline > $O/pmc1.log 2>&1
+    timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE \
+        --kernel-include-regex "halo" -d $O/pmc_c4/pass1 -o run -- python3 bench.py --steps 2 --no-extras \
+        --no-cpu-baseline --backbone resnet50 --keypoints 8 --batch 128 --precision f16 > $O/pmc2.log 2>&1
+    python3 tools/pmc_summary.py $O/pmc $O/pmc_c2.json > $O/pmc_c2.txt
+    python3 tools/pmc_summary.py $O/pmc_c4 $O/pmc_c4.json > $O/pmc_c4.txt
+    rm -rf $O/pmc $O/pmc_c4
+    bash tools/ab.sh "" "--lib tools/ab_lib/libhulkkp_a.so" "" > $O/ab_c2.txt 2>&1
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
