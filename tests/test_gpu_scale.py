@@ -243,27 +243,44 @@ def check_conv_wgrad(x, dy, dw_krsc, st, pd, dl, gen, stats, ns=48):
     _check("wgrad", got, torch.stack(ref), torch.stack(tol) + 1e-30, stats)
 
 
+def _rank_sum(t):
+    """fp64 sum of t over the ranks of the default process group (the SyncBN
+    tests' gloo group), through host memory; t itself without one."""
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return t
+    h = t.detach().double().cpu().clone()
+    dist.all_reduce(h)
+    return h.to(t.device)
+
+
 def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, chunk=1 << 16, local=True):
     """Train-mode BN(+ReLU) backward: dgamma / dbeta against full fp64 channel
     reductions (row chunks) and dy on sampled elements; also the forward batch
     statistics (mean, invstd) the forward stored.  local=False (SyncBN): the
-    statistics and the dx coefficients come from every rank's shard, so only
-    dgamma / dbeta — this rank's own sums with the statistics the kernels used —
-    are checked here."""
+    statistics and the dx coefficients come from every rank's shard — the fp64
+    references are then the global ones (this rank's channel sums summed over the
+    ranks on the host: count, Σy, Σ(y - mean)², Σdz, Σdz·x̂), so the gathered
+    forward statistics and the cross-rank dx coefficients (hkp_bn_finalize_ranks,
+    hkp_bn_bwd_finalize_ranks) are checked call by call; dgamma / dbeta are this
+    rank's own sums with the statistics the kernels used.  Every rank calls this in
+    the same order (the same network walk), as the host collectives require."""
     c = y.shape[-1]
     y2, g2 = y.reshape(-1, c), g.reshape(-1, c)
     M = y2.shape[0]
     s1 = torch.zeros(c, device=y.device, dtype=torch.float64)
     for r0 in range(0, M, chunk):
         s1 += y2[r0:r0 + chunk].double().sum(0)
-    mean = s1 / M
+    Mg = M if local else int(_rank_sum(torch.tensor([float(M)], dtype=torch.float64))[0].item())
+    mean = (s1 if local else _rank_sum(s1)) / Mg
     var = torch.zeros_like(s1)
     for r0 in range(0, M, chunk):
         var += ((y2[r0:r0 + chunk].double() - mean) ** 2).sum(0)
-    inv = 1.0 / torch.sqrt(var / M + bn.eps)
-    if local:
-        _check("bn_mean", mi[:c].double(), mean, 1e-5 * torch.sqrt(var / M) + 1e-30, stats)
-        _check("bn_invstd", mi[c:].double(), inv, 1e-5 * inv, stats)
+    if not local:
+        var = _rank_sum(var)
+    inv = 1.0 / torch.sqrt(var / Mg + bn.eps)
+    _check("bn_mean", mi[:c].double(), mean, 1e-5 * torch.sqrt(var / Mg) + 1e-30, stats)
+    _check("bn_invstd", mi[c:].double(), inv, 1e-5 * inv, stats)
     mean_k, inv_k = mi[:c].double(), mi[c:].double()            # what the kernels used
     db = torch.zeros_like(s1)
     dgm = torch.zeros_like(s1)
@@ -279,8 +296,8 @@ def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, c
         adgm += (dz * xh).abs().sum(0)
     _check("bn_dbeta", dbeta.double(), db, 1e-5 * adb + 1e-30, stats)
     _check("bn_dgamma", dgamma.double(), dgm, 1e-5 * adgm + 1e-30, stats)
-    if not local:
-        return
+    if not local:                       # the dx coefficients use the global sums and count
+        db, dgm, adb, adgm = _rank_sum(db), _rank_sum(dgm), _rank_sum(adb), _rank_sum(adgm)
     rows = _idx(gen, M, ns, y.device)
     ch = _idx(gen, c, ns, y.device)
     mk = torch.stack([mask_fn(slice(int(r), int(r) + 1))[0, int(cc)] for r, cc in zip(rows.tolist(), ch.tolist())]) \
@@ -288,8 +305,8 @@ def check_bn_bwd(bn, g, mask_fn, y, mi, dy, dgamma, dbeta, gen, stats, ns=256, c
     dz = g2[rows, ch].double() * mk
     xh = (y2[rows, ch].double() - mean_k[ch]) * inv_k[ch]
     coef = bn.weight.detach().double()[ch] * inv_k[ch]
-    ref = coef * (dz - db[ch] / M - xh * dgm[ch] / M)
-    tol = 1e-5 * coef.abs() * (dz.abs() + adb[ch] / M + xh.abs() * adgm[ch] / M) + 1e-30
+    ref = coef * (dz - db[ch] / Mg - xh * dgm[ch] / Mg)
+    tol = 1e-5 * coef.abs() * (dz.abs() + adb[ch] / Mg + xh.abs() * adgm[ch] / Mg) + 1e-30
     n_, h_, w_ = y.shape[:3]
     rr = rows
     dyr = _Act(dy, scale=_dy_scale(dy))

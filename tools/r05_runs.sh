@@ -16,6 +16,8 @@
 #   halo      the conflict-free halo swizzle: bit-identity tests, per-conv A/B against the
 #             previous build (tools/ab_lib/libhulkkp_a.so), LDS bank-conflict PMC on C2 / C4,
 #             C2 bench A/B
+#   syncbn    the SyncBN GPU tests (per-call global BN-backward checks) + a 2-rank gloo
+#             rehearsal of bench.py --gpus 2 (relaunch, north_star leg, train leg)
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -95,6 +97,14 @@ halo)
     python3 tools/pmc_summary.py $O/pmc_c4 $O/pmc_c4.json > $O/pmc_c4.txt
     rm -rf $O/pmc $O/pmc_c4
     bash tools/ab.sh "" "--lib tools/ab_lib/libhulkkp_a.so" "" > $O/ab_c2.txt 2>&1
+    ;;
+syncbn)
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread tests/test_gpu_syncbn.py \
+        > $O/pytest_syncbn.log 2>&1
+    echo "pytest syncbn: $(tail -1 $O/pytest_syncbn.log)"
+    timeout -k 10 600 python -u bench.py --gpus 2 --rehearse-gloo --steps 3 --warmup 1 --no-cpu-baseline \
+        > $O/rehearse_n2.log 2>&1
+    echo "rehearsal ok"
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
