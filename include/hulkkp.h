@@ -87,6 +87,10 @@ typedef struct hkp_conv_desc {
                                          two 4-wave blocks per CU (one block's fill and epilogue
                                          beside the other's K loop); Cout % 128 == 0; other
                                          operand layouts plan as AUTO */
+#define HKP_TILE_A3P 14               /* forward, f16x3 or plain fp16, Cout % 256 == 0: the A3 body as a
+                                         persistent grid (one block per CU) whose epilogue overlaps the
+                                         next tile's first DMA stages and stores from registers; other
+                                         launches plan as AUTO */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);

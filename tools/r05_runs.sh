@@ -18,6 +18,7 @@
 #             C2 bench A/B
 #   syncbn    the SyncBN GPU tests (per-call global BN-backward checks) + a 2-rank gloo
 #             rehearsal of bench.py --gpus 2 (relaunch, north_star leg, train leg)
+#   a3p       the persistent A3 body (HKP_TILE_A3P): parity tests, per-conv and C4 / C2 A/B
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   final     GPU suite, smoke(), default bench line
@@ -105,6 +106,17 @@ syncbn)
     timeout -k 10 600 python -u bench.py --gpus 2 --rehearse-gloo --steps 3 --warmup 1 --no-cpu-baseline \
         > $O/rehearse_n2.log 2>&1
     echo "rehearsal ok"
+    ;;
+a3p)
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "a3p" > $O/pytest_a3p.log 2>&1
+    echo "pytest a3p: $(tail -1 $O/pytest_a3p.log)"
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,14 --rounds 5 --iters 5 \
+        --shapes c4_l4_c3,c4_l4_ds,c4_l4_c1,c4_l4_c2,c4_l3_c3,c4_l3_c1,c4_l3_c2,c4_l1_ds,layer4,layer3 > $O/conv_ab.log 2>&1
+    echo "conv_ab ok"
+    timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_1x1=14" "f16_tile_1x1=14,f16_tile_kxk=14" \
+        --backbone resnet50 --keypoints 8 --batch 128 --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "" "x3_tile=14" --rounds 5 --iters 10 > $O/ab_c2.log 2>&1
     ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
