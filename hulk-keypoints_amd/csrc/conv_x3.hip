@@ -2011,6 +2011,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3p_kernel(X3Args a) {
             return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
         };
 
+        x3_stamp(a, 0);
         const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
         const int m0 = mt * BM, n0 = nt * BN;
         Src cur;
@@ -2033,6 +2034,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3p_kernel(X3Args a) {
         else if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
+        x3_stamp(a, 1);
         f32x4 acc[UM][UN];
 #pragma unroll
         for (int i = 0; i < UM; ++i)
@@ -2116,6 +2118,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3p_kernel(X3Args a) {
 #pragma unroll
         for (int j = 0; j < UN; ++j) mma_col(j);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this tile's DMA retired
+        x3_stamp(a, 2);
 
         // ---- epilogue ----
         // lane constants again, opaque: kept from before the K loop they would be
@@ -2193,6 +2196,7 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3p_kernel(X3Args a) {
             x3_bn_partials_w<BN, UM, UN, 16, 16>(
                 a, scr, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
                 [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
+        x3_stamp(a, 3);
         // ---- the output tile from registers ----
         const int b4 = lane & 3;
         if constexpr (P == 3) {
@@ -2257,6 +2261,8 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3p_kernel(X3Args a) {
                     }
                 }
         }
+        x3_stamp(a, 4);
+        x3_stamp(a, 5);
         if (!has_next) return;
         // ---- the next tile's third A stage (its slot held the partials' scratch) ----
         lds_sync();
