@@ -121,6 +121,9 @@ struct X3Args {
     // epilogue output stores (A/B: hkp_debug_x3_store): 0 each site's own flavour,
     // 1 plain, 2 nontemporal, 3 sc1 (written through, not kept in the XCD's L2), 4 sc0 sc1
     int st_kind = 0;
+    // A/B (hkp_debug_x3_prio): static wave priority in the A3 K loop — 0 none, 1
+    // s_setprio 1 on waves 4-7 (the second wave on each SIMD), 2 on waves 0-3
+    int prio = 0;
 };
 
 // One 16-B epilogue output store of flavour `kind` (X3Args::st_kind); dflt: the
@@ -844,6 +847,9 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         lds_barrier();
         x3_stamp(a, 1);
+        const int wv = wm * 2 + wn;
+        if (a.prio == 1 && wv >= 4) __builtin_amdgcn_s_setprio(1);
+        if (a.prio == 2 && wv < 4) __builtin_amdgcn_s_setprio(1);
         FA fa;
         read_a(fa, smem);
 #pragma unroll
@@ -885,6 +891,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int j = 0; j < UN; ++j) mma_col(fa, j);
+        if (a.prio) __builtin_amdgcn_s_setprio(0);
     } else if constexpr (NST == 2) {
         // 2-stage ring (256x256 tiles; 256x64 at two blocks per CU), A single-buffered
         // (registers: 128 acc + 32 A + 64 B): per K-step t — wait own DMA of t+1,
@@ -3518,6 +3525,7 @@ static int g_x3_stagger_ns = 0;                        // hkp_debug_x3_stagger
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
 static int g_x3_store = 0;                             // hkp_debug_x3_store
 static int g_duo_stagger_ns = -1;                      // hkp_debug_duo_stagger
+static int g_x3_prio = 0;                              // hkp_debug_x3_prio
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -3547,6 +3555,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
                       int64_t ws_bytes = 0) {
     a.stamps = g_x3_stamps;
     a.st_kind = g_x3_store;
+    a.prio = g_x3_prio;
     a.stagger_ticks = g_x3_stagger_ns / 10;
     a.stagger_blocks = x3_cus();
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
@@ -4123,4 +4132,8 @@ extern "C" void hkp_debug_x3_store(int32_t kind) { g_x3_store = kind >= 0 && kin
 // Debug / A/B (tools/ only, not thread-safe): the DUO body's first-round stagger of
 // the second block on each CU, in ns (0 = off; < 0 = the planner's estimate).
 extern "C" void hkp_debug_duo_stagger(int32_t ns) { g_duo_stagger_ns = ns; }
+
+// Debug / A/B (tools/ only, not thread-safe): static wave priority in the A3 body's
+// K loop (X3Args::prio: 0 none, 1 waves 4-7, 2 waves 0-3 at s_setprio 1).
+extern "C" void hkp_debug_x3_prio(int32_t mode) { g_x3_prio = mode >= 0 && mode <= 2 ? mode : 0; }
 

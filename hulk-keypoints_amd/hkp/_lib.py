@@ -79,6 +79,7 @@ SIGNATURES = {
     "hkp_debug_x3_split_tail": (None, [_I32]),
     "hkp_debug_x3_store": (None, [_I32]),
     "hkp_debug_duo_stagger": (None, [_I32]),
+    "hkp_debug_x3_prio": (None, [_I32]),
     "hkp_bn_apply_head": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),

@@ -254,6 +254,9 @@ void hkp_debug_x3_store(int32_t kind);
  * first-round delay of the second block on each CU, in ns (0 = off, < 0 = the
  * default estimate of half a block's lifetime). */
 void hkp_debug_duo_stagger(int32_t ns);
+/* Debug / A/B (tools/ only, not thread-safe): static wave priority in the A3 body's
+ * K loop: 0 none (default), 1 s_setprio 1 on waves 4-7, 2 on waves 0-3. */
+void hkp_debug_x3_prio(int32_t mode);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

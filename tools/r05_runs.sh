@@ -122,6 +122,12 @@ a3p_stamps)
     timeout -k 10 300 python -u tools/x3_stamps.py c4_l4_c3 c4_l3_c3 c4_l1_ds layer3 > $O/stamps_a3.log 2>&1
     timeout -k 10 300 python -u tools/x3_stamps.py --tile 14 c4_l4_c3 c4_l3_c3 c4_l1_ds layer3 > $O/stamps_a3p.log 2>&1
     ;;
+prio)
+    timeout -k 10 500 python -u tools/infer_ab.py "" "prio=1" "prio=2" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "" "prio=1" "prio=2" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "" "prio=1" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
     echo "bench ok"

@@ -26,7 +26,7 @@ def parse(form):
     kw = {}
     for item in filter(None, form.split(",")):
         k, _, v = item.partition("=")
-        if k == "store":
+        if k in ("store", "prio"):
             continue
         cur = getattr(DEFAULT, k)
         kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
@@ -58,17 +58,21 @@ def main():
     pols = [base.with_(**parse(f)) for f in args.forms]
     stores = [int(dict(i.partition("=")[::2] for i in filter(None, f.split(","))).get("store", 0))
               for f in args.forms]
-    for p, st in zip(pols, stores):      # warm every form (kernels, caches, plans)
+    prios = [int(dict(i.partition("=")[::2] for i in filter(None, f.split(","))).get("prio", 0))
+             for f in args.forms]
+    for p, st, pr in zip(pols, stores, prios):      # warm every form (kernels, caches, plans)
         model.policy = trainer.policy = p
         hkp.lib().hkp_debug_x3_store(st)
+        hkp.lib().hkp_debug_x3_prio(pr)
         for _ in range(3):
             trainer.step(x, uv)
     torch.cuda.synchronize()
     res = {f: [] for f in args.forms}
     for _ in range(args.rounds):
-        for f, p, st in zip(args.forms, pols, stores):
+        for f, p, st, pr in zip(args.forms, pols, stores, prios):
             model.policy = trainer.policy = p
             hkp.lib().hkp_debug_x3_store(st)
+            hkp.lib().hkp_debug_x3_prio(pr)
             trainer.step(x, uv)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -77,6 +81,7 @@ def main():
             torch.cuda.synchronize()
             res[f].append(B * args.iters / (time.perf_counter() - t0))
     hkp.lib().hkp_debug_x3_store(0)
+    hkp.lib().hkp_debug_x3_prio(0)
     for f in args.forms:
         print("%-40s %.1f img/s  (%s)" % (f or "(default)", statistics.median(res[f]),
                                           " ".join("%.1f" % v for v in res[f])), flush=True)
