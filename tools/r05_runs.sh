@@ -128,6 +128,18 @@ prio)
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "" "prio=1" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     ;;
+b8)
+    # the north_star shard (C2 network, batch 8 on one GPU): bench line + kernel trace
+    timeout -k 10 300 python -u bench.py --batch 8 --no-extras --no-cpu-baseline > $O/bench_b8.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --batch 8 --steps 10 \
+        --no-extras --no-cpu-baseline > $O/prof.log 2>&1
+    DB=$O/prof/run_results.db
+    [ -f $DB ] || DB=$(ls $O/prof/*/run_results.db 2>/dev/null | head -1)
+    python3 tools/rocpd_stats.py $DB $O/b8_kernel_stats.csv --top 30 > $O/b8_kernel_top.txt
+    python3 tools/step_breakdown.py $DB --last-step > $O/b8_last_step.txt
+    python3 tools/step_breakdown.py $DB --timeline > $O/b8_timeline.txt
+    rm -rf $O/prof
+    ;;
 c5)
     timeout -k 10 400 python -u bench.py $C5 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
     echo "bench ok"
