@@ -257,6 +257,11 @@ void hkp_debug_duo_stagger(int32_t ns);
 /* Debug / A/B (tools/ only, not thread-safe): static wave priority in the A3 body's
  * K loop: 0 none (default), 1 s_setprio 1 on waves 4-7, 2 on waves 0-3. */
 void hkp_debug_x3_prio(int32_t mode);
+/* Debug / A/B (tools/ only, not thread-safe): the A3 grid's fractional split-K tail
+ * (conv_x3_a3sk_kernel: the last round balanced over every CU, a block's range
+ * crossing at most one m-tile boundary) — 0 never, 1 where the planner's cost
+ * model prefers it (default), 2 whenever legal (AUTO policy, f16x3 / plain fp16). */
+void hkp_debug_x3_frac_tail(int32_t mode);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -26,6 +26,8 @@ SHAPES = {
     "h128": ("x3", 4, 240, 320, 128, 128, 3, 1, 1, 1),           # halo body at 128 channels
     "t4": ("x3", 8, 60, 80, 512, 512, 3, 1, 4, 4),             # training shard (batch 8)
     "t3": ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),
+    "t3a": ("x3", 8, 60, 80, 128, 256, 3, 1, 2, 2),            # layer3 conv1 at batch 8 (dilated, stride 1)
+    "t4ds": ("x3", 8, 60, 80, 256, 512, 1, 1, 0, 1),
     # R50-8s @640x480, batch 128 (C4, plain fp16)
     "c4_l4_c2": ("f16", 128, 60, 80, 512, 512, 3, 1, 4, 4),
     "c4_l4_c1": ("f16", 128, 60, 80, 2048, 512, 1, 1, 0, 1),
@@ -57,6 +59,8 @@ def main():
                     "tiles (hkp_debug_duo_stagger: 0 off, -1 the default estimate)")
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
+    ap.add_argument("--fracs", default="1", help="A3 fractional-tail modes to cross with the tiles "
+                    "(hkp_debug_x3_frac_tail: 0 never, 1 planner, 2 whenever legal)")
     args = ap.parse_args()
     if args.lib:
         from hkp import _lib
@@ -64,12 +68,13 @@ def main():
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     from hkp._lib import lib
-    forms = [(int(t), int(k), int(d)) for t in args.tiles.split(",") for k in args.stores.split(",")
-             for d in args.duo_staggers.split(",")]
+    forms = [(int(t), int(k), int(d), int(fr)) for t in args.tiles.split(",") for k in args.stores.split(",")
+             for d in args.duo_staggers.split(",") for fr in args.fracs.split(",")]
 
-    def set_store(k, d=-1):
+    def set_store(k, d=-1, fr=1):
         lib().hkp_debug_x3_store(k)
         lib().hkp_debug_duo_stagger(d)
+        lib().hkp_debug_x3_frac_tail(fr)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):
@@ -96,7 +101,7 @@ def main():
         for r in range(args.rounds):
             for f in forms:
                 t = f[0]
-                set_store(f[1], f[2])
+                set_store(f[1], f[2], f[3])
                 y = run(t)
                 if r == 0:
                     outs[f] = y.float()
@@ -115,10 +120,12 @@ def main():
         for f in forms:
             t = f[0]
             ts = sorted(times[f])
+            set_store(f[1], f[2], f[3])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
-            print("%-9s tile %d store %d stagger %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  max rel diff=%.1e" % (
-                name, t, f[1], f[2], ts[len(ts) // 2], ts[0], flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same),
-                flush=True)
+            set_store(0)
+            print("%-9s tile %d store %d stagger %d frac %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
+                  "max rel diff=%.1e" % (name, t, f[1], f[2], f[3], ts[len(ts) // 2], ts[0],
+                                         flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,6 +21,8 @@
 #   a3p       the persistent A3 body (HKP_TILE_A3P): parity tests, per-conv and C4 / C2 A/B
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
+#   frac      the fractional A3 tail (conv_x3_a3sk_kernel): its parity tests, per-conv A/B
+#             (hkp_debug_x3_frac_tail 0 / 1 / 2), C2 / B=8 shard / C4 / C3-train A/B in one process
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -153,6 +155,19 @@ c5)
     rm -rf $O/prof
     echo "trace ok"
     bash tools/pmc_passes.sh $O/pmc "$C5 --steps 2 --warmup 1" "."
+    ;;
+frac)
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "fractional or split_k_tail" > $O/pytest_frac.log 2>&1
+    echo "pytest frac: $(tail -1 $O/pytest_frac.log)"
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0 --fracs 0,1,2 --rounds 5 --iters 5 \
+        --shapes t3,t4,t3a,t4ds,layer3,layer4,c4_l4_c2,c4_l3_c2,c4_l3_c1 > $O/conv_ab.log 2>&1
+    echo "conv_ab ok"
+    timeout -k 10 400 python -u tools/infer_ab.py "frac=0" "" "frac=2" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "frac=0" "" "frac=2" --batch 8 --rounds 7 --iters 20 > $O/ab_b8.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "frac=0" "" "frac=2" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "frac=0" "" "frac=2" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1

@@ -19,14 +19,17 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 
+from infer_ab import KNOBS, knobs, set_knobs  # noqa: E402  (tools/ is on sys.path when run as a script)
+
+
 def parse(form):
-    """Policy overrides of a form; the pseudo-field store=K is the library's
-    epilogue store flavour (hkp_debug_x3_store), not a Policy field."""
+    """Policy overrides of a form; the pseudo-fields store=K, prio=K and frac=K
+    are library debug knobs (infer_ab.KNOBS), not Policy fields."""
     from hkp.policy import DEFAULT
     kw = {}
     for item in filter(None, form.split(",")):
         k, _, v = item.partition("=")
-        if k in ("store", "prio"):
+        if k in KNOBS:
             continue
         cur = getattr(DEFAULT, k)
         kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
@@ -56,23 +59,18 @@ def main():
     uv = torch.from_numpy(recipe.seeded_keypoints(B, K, H, W, 99)).to(dev)
     trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4)
     pols = [base.with_(**parse(f)) for f in args.forms]
-    stores = [int(dict(i.partition("=")[::2] for i in filter(None, f.split(","))).get("store", 0))
-              for f in args.forms]
-    prios = [int(dict(i.partition("=")[::2] for i in filter(None, f.split(","))).get("prio", 0))
-             for f in args.forms]
-    for p, st, pr in zip(pols, stores, prios):      # warm every form (kernels, caches, plans)
+    kns = [knobs(f) for f in args.forms]
+    for p, kv in zip(pols, kns):      # warm every form (kernels, caches, plans)
         model.policy = trainer.policy = p
-        hkp.lib().hkp_debug_x3_store(st)
-        hkp.lib().hkp_debug_x3_prio(pr)
+        set_knobs(hkp.lib(), kv)
         for _ in range(3):
             trainer.step(x, uv)
     torch.cuda.synchronize()
     res = {f: [] for f in args.forms}
     for _ in range(args.rounds):
-        for f, p, st, pr in zip(args.forms, pols, stores, prios):
+        for f, p, kv in zip(args.forms, pols, kns):
             model.policy = trainer.policy = p
-            hkp.lib().hkp_debug_x3_store(st)
-            hkp.lib().hkp_debug_x3_prio(pr)
+            set_knobs(hkp.lib(), kv)
             trainer.step(x, uv)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -80,8 +78,7 @@ def main():
                 trainer.step(x, uv)
             torch.cuda.synchronize()
             res[f].append(B * args.iters / (time.perf_counter() - t0))
-    hkp.lib().hkp_debug_x3_store(0)
-    hkp.lib().hkp_debug_x3_prio(0)
+    set_knobs(hkp.lib(), knobs(""))
     for f in args.forms:
         print("%-40s %.1f img/s  (%s)" % (f or "(default)", statistics.median(res[f]),
                                           " ".join("%.1f" % v for v in res[f])), flush=True)
