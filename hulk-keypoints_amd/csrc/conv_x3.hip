@@ -3363,9 +3363,14 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // Fractional tail (conv_x3_a3sk_kernel, A3 body only): every CU's group takes
 // tm*nks/ngmax units, less than a tile, so a group's range may cross one m-tile
 // boundary (two segments); cost tm*nt/CUs of a round + two segments' fill, slab
-// hand-off and combine.  hkp_debug_x3_frac_tail: 0 never, 1 when cheaper
-// (default), 2 whenever legal.
-static int g_x3_frac_tail = 1;
+// hand-off and combine.  hkp_debug_x3_frac_tail: 0 never (default), 1 when the
+// cost model prefers it, 2 whenever legal.  Measured in one process
+// (profiles/r05_frac_*): per conv -1 % ... +19 % (the B=8 shard's layer3 ties
+// the stream-K 256x128 grid it would replace, 0.140 vs 0.141 ms), end to end
+// C2 -1.2 %, B=8 shard -1.9 %, C4 -1.3 %, C3 training -0.4 % — a tile split
+// across two groups waits for the later one's second segment, then its combine
+// and epilogue, and a full machine runs at a lower clock than a partial round.
+static int g_x3_frac_tail = 0;
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
 constexpr double X3_FRAC_OVER = 0.16;
 static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr, bool allow_frac = false,

@@ -259,8 +259,9 @@ void hkp_debug_duo_stagger(int32_t ns);
 void hkp_debug_x3_prio(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): the A3 grid's fractional split-K tail
  * (conv_x3_a3sk_kernel: the last round balanced over every CU, a block's range
- * crossing at most one m-tile boundary) — 0 never, 1 where the planner's cost
- * model prefers it (default), 2 whenever legal (AUTO policy, f16x3 / plain fp16). */
+ * crossing at most one m-tile boundary) — 0 never (default: measured slower end to
+ * end), 1 where the planner's cost model prefers it, 2 whenever legal (AUTO policy,
+ * f16x3 / plain fp16). */
 void hkp_debug_x3_frac_tail(int32_t mode);
 
 /* ----------------------------------------------------------- batchnorm ---- */

@@ -662,7 +662,7 @@ def test_fractional_tail(cuda_device, case):
         y1, p1 = fwd(xs, wp, st, pad, dil)
         y2, p2 = fwd(xs, wp, st, pad, dil)
     finally:
-        lib().hkp_debug_x3_frac_tail(1)
+        lib().hkp_debug_x3_frac_tail(0)
     assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item()
     assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
     assert torch.equal(y1, y2) and torch.equal(p1, p2)
@@ -691,7 +691,7 @@ def test_fractional_tail_dgrad(cuda_device):
         dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax)
         dx2 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax)
     finally:
-        lib().hkp_debug_x3_frac_tail(1)
+        lib().hkp_debug_x3_frac_tail(0)
     assert torch.equal(dx1, dx2)
     assert (dx1 - dx0).abs().max().item() <= 4e-6 * dx0.abs().max().item()
 

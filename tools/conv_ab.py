@@ -59,7 +59,7 @@ def main():
                     "tiles (hkp_debug_duo_stagger: 0 off, -1 the default estimate)")
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
-    ap.add_argument("--fracs", default="1", help="A3 fractional-tail modes to cross with the tiles "
+    ap.add_argument("--fracs", default="0", help="A3 fractional-tail modes to cross with the tiles "
                     "(hkp_debug_x3_frac_tail: 0 never, 1 planner, 2 whenever legal)")
     args = ap.parse_args()
     if args.lib:
@@ -71,7 +71,7 @@ def main():
     forms = [(int(t), int(k), int(d), int(fr)) for t in args.tiles.split(",") for k in args.stores.split(",")
              for d in args.duo_staggers.split(",") for fr in args.fracs.split(",")]
 
-    def set_store(k, d=-1, fr=1):
+    def set_store(k, d=-1, fr=0):
         lib().hkp_debug_x3_store(k)
         lib().hkp_debug_duo_stagger(d)
         lib().hkp_debug_x3_frac_tail(fr)
