@@ -23,6 +23,8 @@
 #             trace stats, per-launch listing, PMC passes over every kernel
 #   frac      the fractional A3 tail (conv_x3_a3sk_kernel): its parity tests, per-conv A/B
 #             (hkp_debug_x3_frac_tail 0 / 1 / 2), C2 / B=8 shard / C4 / C3-train A/B in one process
+#   rehearse8 bench.py --gpus 4 and --gpus 8 as gloo rehearsals on the one GPU (the driver's
+#             scaling run's relaunch, rendezvous, north_star and train legs; not a measurement)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -168,6 +170,14 @@ frac)
     timeout -k 10 500 python -u tools/infer_ab.py "frac=0" "" "frac=2" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "frac=0" "" "frac=2" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
+rehearse8)
+    timeout -k 10 500 python -u bench.py --gpus 4 --rehearse-gloo --steps 2 --warmup 1 --no-cpu-baseline \
+        > $O/rehearse_n4.log 2>&1
+    echo "n4 ok"
+    timeout -k 10 700 python -u bench.py --gpus 8 --rehearse-gloo --steps 2 --warmup 1 --no-cpu-baseline \
+        > $O/rehearse_n8.log 2>&1
+    echo "n8 ok"
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
