@@ -4116,6 +4116,8 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     a.M = (int)M; a.cch = 1; a.RS = 7; a.nks = 7;
     a.plane = (long)d->n * a.H * a.W * 4;
     a.n_tiles = d->k / 64;
+    a.stamps = g_x3_stamps;
+    a.st_kind = g_x3_store;
     const long m_tiles = (M + 255) / 256;
     // two blocks per CU (7 K-steps per tile: prologue / epilogue dominate one
     // block), 16x16x32 body on a 2-stage ring (the layer1 256x64 pair's body)

@@ -25,6 +25,7 @@
 #             (hkp_debug_x3_frac_tail 0 / 1 / 2), C2 / B=8 shard / C4 / C3-train A/B in one process
 #   rehearse8 bench.py --gpus 4 and --gpus 8 as gloo rehearsals on the one GPU (the driver's
 #             scaling run's relaunch, rendezvous, north_star and train legs; not a measurement)
+#   stem      per-block phase clocks of the stem conv (C2 batch 32, C4 batch 128)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -178,6 +179,9 @@ rehearse8)
     timeout -k 10 700 python -u bench.py --gpus 8 --rehearse-gloo --steps 2 --warmup 1 --no-cpu-baseline \
         > $O/rehearse_n8.log 2>&1
     echo "n8 ok"
+    ;;
+stem)
+    timeout -k 10 300 python -u tools/x3_stamps.py stem:32 stem:128 layer1 > $O/stamps_stem.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1

@@ -35,15 +35,25 @@ def main():
         lib().hkp_debug_duo_stagger(int(args[i + 1]))
         del args[i:i + 2]
     for name in args:
-        prec, n, h, w, ci, co, k, st, pd, dl = SHAPES[name]
-        x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
-        wt = torch.randn(co, k, k, ci, device=dev, generator=g) * (2.0 / (k * k * co)) ** 0.5
-        if prec == "x3":
+        if name.startswith("stem"):          # stem[:N]: the 7x7/s2 stem (hkp_conv2d_fwd_stem_x3), batch N (32)
+            n = int(name.partition(":")[2] or 32)
+            prec, h, w, ci, co, k, st, pd, dl = "stem", 480, 640, 3, 64, 7, 2, 3, 1
+        else:
+            prec, n, h, w, ci, co, k, st, pd, dl = SHAPES[name]
+        if prec == "stem":
+            img = torch.randint(0, 256, (n, h, w, 3), device=dev, dtype=torch.uint8, generator=g)
+            wp = ops.stem_weight_pack_x3(torch.randn(co, ci, k, k, device=dev, generator=g) * 0.05)
+            run = lambda: ops.conv2d_fwd_stem_x3(img, wp, co)  # noqa: E731
+        elif prec == "x3":
+            x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
+            wt = torch.randn(co, k, k, ci, device=dev, generator=g) * (2.0 / (k * k * co)) ** 0.5
             ss = torch.cat([torch.ones(ci, device=dev), torch.zeros(ci, device=dev)])
             xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
             ws = ops.weight_pack_x3(wt)
             run = lambda: ops.conv2d_fwd_x3(xs, ws, st, pd, dl, sk=False, tile=tile)  # noqa: E731
         else:
+            x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
+            wt = torch.randn(co, k, k, ci, device=dev, generator=g) * (2.0 / (k * k * co)) ** 0.5
             xs = x.half()
             ws = ops.weight_pack_f16(wt)
             run = lambda: ops.conv2d_fwd_f16(xs, ws, st, pd, dl, sk=False, tile=tile)  # noqa: E731
