@@ -1858,6 +1858,150 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_bnin_kernel(X3Args a) {
 }
 
 // ---------------------------------------------------------------------------
+// Stem patch body (conv_x3_stem_patch_kernel): the 7x7/s2 stem on the padded
+// NHWC4 hi | lo image planes of hkp_stem_pack_x3, a tile = an 8 x 32 patch of
+// output pixels.  The one-tile stem (conv_x3_kernel<64, STEM, PAIR>) stages per
+// filter row a 256-line im2col window — pixels 2wo .. 2wo+7 of one padded row for
+// every output pixel, each input pixel fetched ~4x per row and 7 rows deep: 224 KB
+// of L2 -> LDS traffic per tile, the stem's bound (C2 288 us for 629 MB of output).
+// Here the patch's (2*8+5) x (2*32+6) = 21 x 70 padded pixels of both planes
+// (23 KB) and all 7 filter rows of the 64 weight rows (56 KB) are staged ONCE by
+// LDS-DMA and the 7 K-steps read their fragments from them with no barrier between:
+// output pixel (i, j), filter row r, chunk q (taps 2q, 2q+1 x 4 channels) is the
+// 16 B at patch row 2i + r, pixel 2j + 2q — 16 consecutive pixels of a fragment
+// read 256 contiguous bytes (every bank once).  B lines keep the ring bodies'
+// (row >> 1) & 7 chunk swizzle.  256 x 64 tile, 8 waves 4 x 2 (wave tile 64 x 32),
+// 16x16x32 MFMAs, 80 KiB: two blocks per CU, one's epilogue beside the other's
+// MFMAs; epilogue = the halo body's (BN tile partials, LDS-staged fp32 row chunks).
+constexpr int STEM_PH = 8, STEM_PW = 32, STEM_PR = 2 * STEM_PH + 5, STEM_PC = 2 * STEM_PW + 6;   // 21 x 70 pixels
+constexpr int STEM_PLANE = STEM_PR * STEM_PC * 8;                // bytes per plane (4 ch fp16 per pixel)
+constexpr int STEM_BBYTES = 7 * 64 * 128;                        // 7 filter rows x 64 weight lines
+constexpr int STEM_PCH = 2 * STEM_PLANE / 16;                    // patch 16-B chunks (1470)
+constexpr int STEM_PGA = (STEM_PCH + 511) / 512;                 // patch DMA instructions per wave (3)
+constexpr int STEM_LDS = STEM_BBYTES + 8 * STEM_PGA * 1024;      // B, then the patch (+ dummy chunks): 80 KiB
+
+static bool stem_patch_shape(int ho, int wo, int k) { return ho % STEM_PH == 0 && wo % STEM_PW == 0 && k % 64 == 0; }
+
+__global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[STEM_LDS];
+    constexpr int BM = 256, BN = 64, WM = 4, WN = 2, ROW = 128;
+    constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);     // 4 x 2 16x16 sub-tiles per wave
+    static_assert(256 * (BN + 4) * 4 <= STEM_LDS && STEM_PGA * 512 >= STEM_PCH, "stem patch LDS");
+    x3_stamp(a, 0);
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
+    const int pwn = a.Wo / STEM_PW, tpi = (a.Ho / STEM_PH) * pwn;
+    const int img = mt / tpi, rem = mt - img * tpi;
+    const int h0 = (rem / pwn) * STEM_PH, w0 = (rem - (rem / pwn) * pwn) * STEM_PW;
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = w / WN, wn = w % WN;
+
+    // ---- staging: the weight lines (7 instructions per wave: LDS row R = r*64 + n
+    // holds logical chunk p ^ ((n >> 1) & 7) at physical chunk p), then the patch
+    // (chunk c: plane c / (PLANE/16), patch row, 16-B column — 35 per row, the 70
+    // padded pixels of a patch row are contiguous in the plane) ----
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        const int R = 8 * (w * 7 + i) + lane / 8;
+        const int r = R >> 6, n = R & 63;
+        const int Lc = (lane % 8) ^ ((n >> 1) & 7);
+        glds16(a.ws + ((long)(n0 + n) * 7 + r) * 64 + Lc * 8, smem + 8 * (w * 7 + i) * ROW);
+    }
+    const _Float16* zero = (const _Float16*)g_x3_zero_line;
+    const long prow0 = ((long)img * a.H + 2 * h0) * a.W + 2 * w0;   // padded pixel of patch (0, 0)
+#pragma unroll
+    for (int i = 0; i < STEM_PGA; ++i) {
+        const int c = 512 * i + 64 * w + lane;                   // instruction i of wave w: chunks 512 i + 64 w + lane
+        const int pl = c >= STEM_PLANE / 16 ? 1 : 0, cc = c - pl * (STEM_PLANE / 16);
+        const int pr = cc / (STEM_PC / 2), pc = cc - pr * (STEM_PC / 2);
+        const _Float16* src = c < STEM_PCH ? a.xs + pl * a.plane + (prow0 + (long)pr * a.W) * 4 + pc * 8 : zero;
+        glds16(src, smem + STEM_BBYTES + (512 * i + 64 * w) * 16);
+    }
+
+    // ---- fragment addressing ----
+    const int r16 = lane & 15, q = lane >> 4;
+    int aoff[UM];                                               // patch byte offset of sub-tile i's pixel, filter row 0, chunk q
+#pragma unroll
+    for (int i = 0; i < UM; ++i) {
+        const int m = wm * 64 + 16 * i + r16;
+        aoff[i] = STEM_BBYTES + ((2 * (m >> 5)) * STEM_PC + 2 * (m & 31) + 2 * q) * 8;
+    }
+    const int sw = (r16 >> 1) & 7;
+    const int fb_h = (wn * 32 + r16) * ROW + ((q ^ sw) << 4), fb_l = (wn * 32 + r16) * ROW + (((4 + q) ^ sw) << 4);
+
+    f32x4 acc[UM][UN];
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
+    };
+    float scv[UN];
+#pragma unroll
+    for (int j = 0; j < UN; ++j) scv[j] = a.wscale ? a.wscale[n0 + wn * 32 + 16 * j + r16] : 1.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    x3_stamp(a, 1);
+    // 7 K-steps (filter rows) from the resident patch and weights: no barriers
+    f16x8 ah[UM], al[UM], bh[UN], bl[UN];
+    auto read_frags = [&](int r) {
+#pragma unroll
+        for (int i = 0; i < UM; ++i) {
+            ah[i] = *(const f16x8*)(smem + aoff[i] + r * STEM_PC * 8);
+            al[i] = *(const f16x8*)(smem + aoff[i] + r * STEM_PC * 8 + STEM_PLANE);
+        }
+#pragma unroll
+        for (int j = 0; j < UN; ++j) {
+            bh[j] = *(const f16x8*)(smem + r * 64 * ROW + j * 16 * ROW + fb_h);
+            bl[j] = *(const f16x8*)(smem + r * 64 * ROW + j * 16 * ROW + fb_l);
+        }
+    };
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        read_frags(r);
+#pragma unroll
+        for (int i = 0; i < UM; ++i)
+#pragma unroll
+            for (int j = 0; j < UN; ++j) x3_products<3>(acc[i][j], ah[i], al[i], bh[j], bl[j], mfma);
+    }
+    x3_stamp(a, 2);
+
+    // ---- epilogue: BN tile partials (rows all valid: exact patch tiling), the
+    // scaled tile staged through the LDS and written as 16-B row chunks; tile row
+    // m -> output pixel (img, h0 + m/32, w0 + m%32) ----
+    const int rbase = m0 + wm * UM * 16 + 4 * q;
+    lds_sync();                                                  // every wave done with the patch and weights
+    if (a.part) {
+        x3_bn_partials_w<BN, UM, UN, 16, 16>(
+            a, (float*)smem, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
+            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; }, (float*)smem);
+        lds_sync();
+    }
+    x3_stamp(a, 3);
+    constexpr int PITCH = BN + 4, C4 = BN / 4;
+    float* st = (float*)smem;
+#pragma unroll
+    for (int i = 0; i < UM; ++i)
+#pragma unroll
+        for (int j = 0; j < UN; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                st[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * 32 + j * 16 + r16] = acc[i][j][r] * scv[j];
+    lds_sync();
+    x3_stamp(a, 4);
+#pragma unroll 4
+    for (int e = tid; e < BM * C4; e += 512) {
+        const int row = e / C4, c4 = e - row * C4;
+        const long off = (((long)img * a.Ho + h0 + (row >> 5)) * a.Wo + w0 + (row & 31)) * a.K + n0 + c4 * 4;
+        x3_st16((f32x4*)(a.y + off), *(const f32x4*)(st + row * PITCH + c4 * 4), a.st_kind, 2);
+    }
+    x3_stamp(a, 5);
+}
+
+// ---------------------------------------------------------------------------
 // A3P (conv_x3_a3p_kernel<P>): the A3 body (256x256 tiles, 3-stage A ring, 2-stage
 // B ring, 8 waves) as a PERSISTENT grid — one block per CU walking the tiles
 // round by round (round r: tiles [r*G, (r+1)*G), XCD-remapped as the one-tile grid)
@@ -4119,6 +4263,13 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     a.stamps = g_x3_stamps;
     a.st_kind = g_x3_store;
     const long m_tiles = (M + 255) / 256;
+    if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR) {
+        // the patch body (patch-divisible outputs: 480x640 and 960x1280 images);
+        // HKP_TILE_64_PAIR keeps the one-tile stem (A/B, parity tests)
+        hipLaunchKernelGGL(conv_x3_stem_patch_kernel, dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+        HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
+        return HKP_OK;
+    }
     // two blocks per CU (7 K-steps per tile: prologue / epilogue dominate one
     // block), 16x16x32 body on a 2-stage ring (the layer1 256x64 pair's body)
     hipLaunchKernelGGL((conv_x3_kernel<64, true, true, 16, false, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
@@ -4165,6 +4316,8 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             return x3_kernel_name(c, false, 3, buf, len);
         }
         case HKP_KOP_STEM_X3:
+            if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR)
+                return snprintf(buf, len, "conv_x3_stem_patch_kernel");
             return x3_kernel_name(X3_STEM, true, 3, buf, len);
         case HKP_KOP_WGRAD_X3: {
             HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv_kernel_name: wgrad needs Cout%%64==0");

@@ -421,10 +421,12 @@ def stem_weight_pack_x3(w):
     return PackedWeight(out, sc)
 
 
-def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None):
+def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0):
     """f16x3 stem conv (7x7/s2/p3) → NHWC fp32 y (+ BN partials).  x: the NCHW fp32
     image, or the uint8 NHWC (BGR) batch cv2.imread gives — ToTensor's /255 is then
-    fused into the stem's operand pack."""
+    fused into the stem's operand pack.  tile: 0 = the patch body
+    where the output tiles into 8 x 32 patches, HKP_TILE_64_PAIR = the one-tile
+    stem (the BN partials then group raster-order rows instead of patches)."""
     from ._lib import lib
     ws, wsc = wp
     u8 = x.dtype == torch.uint8
@@ -434,7 +436,7 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None):
         n, h, wd, c = x.shape
     else:
         n, c, h, wd = x.shape
-    d = ConvDesc(n, h, wd, c, k, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW)
+    d = ConvDesc(n, h, wd, c, k, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW, tile)
     ho, wo = conv_out_hw(h, wd, 7, 7, 2, 3, 1)
     xs = torch.empty(lib().hkp_stem_pack_x3_elems(ctypes.byref(d)), device=x.device, dtype=torch.float16)
     call("hkp_stem_pack_x3_u8" if u8 else "hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())

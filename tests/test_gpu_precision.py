@@ -305,6 +305,52 @@ def test_stem_x3_fp32_accurate(cuda_device, shape):
     assert torch.allclose(part, p32, rtol=1e-4, atol=1e-3)
 
 
+def _merged_stats(part, count):
+    """Per-channel mean and biased variance merged (fp64, Chan) from conv tile
+    partials [tiles][C][2] (sum, M2 about the 128-row tile's mean)."""
+    p = part.double().cpu()
+    tiles = p.shape[0]
+    n_t = torch.full((tiles, 1), 128.0, dtype=torch.float64)
+    n_t[-1] = count - 128 * (tiles - 1)
+    mean = p[:, :, 0].sum(0) / count
+    m2 = (p[:, :, 1] + n_t * (p[:, :, 0] / n_t - mean) ** 2).sum(0)
+    return mean, m2 / count
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 32, 64), (1, 3, 48, 128), (1, 1, 32, 64), (2, 3, 480, 640)])
+def test_stem_patch_body(cuda_device, shape):
+    """The stem patch body (conv_x3_stem_patch_kernel: patch-divisible outputs, the
+    8 x 32 patch's padded input and all 7 weight rows staged once): fp32-class vs
+    fp64, the one-tile stem's values to fp32 summation order (HKP_TILE_64_PAIR),
+    and the same BN statistics merged from its patch-grouped tile partials."""
+    from hkp import ops
+    from hkp._lib import HKP_KOP_STEM_X3, HKP_LAYOUT_NCHW, HKP_TILE_64_PAIR, ConvDesc
+    n, c, h, w = shape
+    assert ops.kernel_name(ConvDesc(n, h, w, c, 64, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW, 0),
+                           HKP_KOP_STEM_X3) == "conv_x3_stem_patch_kernel"
+    assert ops.kernel_name(ConvDesc(n, h, w, c, 64, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW, HKP_TILE_64_PAIR),
+                           HKP_KOP_STEM_X3).startswith("conv_x3_kernel<64, true, true")
+    x = torch.rand(*shape, generator=torch.Generator().manual_seed(5))
+    wt = rand(64, c, 7, 7, seed=6, scale=(2.0 / (49 * 64)) ** 0.5)
+    xd, wd = x.to(cuda_device), wt.to(cuda_device)
+    wp = ops.stem_weight_pack_x3(wd)
+    y, part = ops.conv2d_fwd_stem_x3(xd, wp, 64)
+    y1, part1 = ops.conv2d_fwd_stem_x3(xd, wp, 64, tile=HKP_TILE_64_PAIR)
+    assert (y - y1).abs().max().item() <= 4e-6 * y1.abs().max().item()
+    y2, _ = ops.conv2d_fwd_stem_x3(xd, wp, 64)
+    assert torch.equal(y, y2)
+    count = y.shape[0] * y.shape[1] * y.shape[2]
+    (m0, v0), (m1, v1) = _merged_stats(part, count), _merged_stats(part1, count)
+    assert torch.allclose(m0, m1, rtol=1e-5, atol=1e-6) and torch.allclose(v0, v1, rtol=1e-4, atol=1e-7)
+    if n * h * w <= 2 * 48 * 128:                              # fp64 on the small shapes
+        ref = F.conv2d(x.double(), wt.double(), None, 2, 3)
+        err = (y.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+        assert err < 2e-6, err
+        ym = y.cpu().double().reshape(-1, 64)
+        assert torch.allclose(m0, ym.mean(0), rtol=1e-5, atol=1e-7)
+        assert torch.allclose(v0, ym.var(0, unbiased=False), rtol=1e-4, atol=1e-9)
+
+
 def _model(bb, k, wseed, dev, precision="f16x3"):
     from src.model import KeypointsGauss
     m = KeypointsGauss(k, backbone=bb, pretrained=False, precision=precision)
