@@ -1880,7 +1880,10 @@ constexpr int STEM_PCH = 2 * STEM_PLANE / 16;                    // patch 16-B c
 constexpr int STEM_PGA = (STEM_PCH + 511) / 512;                 // patch DMA instructions per wave (3)
 constexpr int STEM_LDS = STEM_BBYTES + 8 * STEM_PGA * 1024;      // B, then the patch (+ dummy chunks): 80 KiB
 
-static bool stem_patch_shape(int ho, int wo, int k) { return ho % STEM_PH == 0 && wo % STEM_PW == 0 && k % 64 == 0; }
+static int g_stem_pair = 0;                                      // hkp_debug_stem_pair
+static bool stem_patch_shape(int ho, int wo, int k) {
+    return !g_stem_pair && ho % STEM_PH == 0 && wo % STEM_PW == 0 && k % 64 == 0;
+}
 
 __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[STEM_LDS];
@@ -4344,6 +4347,7 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // Debug / A/B (tools/ only, not thread-safe): nonzero runs an A3 grid's split-K
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
+extern "C" void hkp_debug_stem_pair(int32_t on) { g_stem_pair = on != 0; }
 extern "C" void hkp_debug_x3_frac_tail(int32_t mode) { g_x3_frac_tail = mode < 0 ? 0 : mode > 2 ? 2 : mode; }
 
 // Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'

@@ -263,6 +263,9 @@ void hkp_debug_x3_prio(int32_t mode);
  * end), 1 where the planner's cost model prefers it, 2 whenever legal (AUTO policy,
  * f16x3 / plain fp16). */
 void hkp_debug_x3_frac_tail(int32_t mode);
+/* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
+ * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
+void hkp_debug_stem_pair(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -181,7 +181,14 @@ rehearse8)
     echo "n8 ok"
     ;;
 stem)
-    timeout -k 10 300 python -u tools/x3_stamps.py stem:32 stem:128 layer1 > $O/stamps_stem.log 2>&1
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "stem" tests/test_gpu_forward.py > $O/pytest_stem.log 2>&1
+    echo "pytest stem: $(tail -1 $O/pytest_stem.log)"
+    timeout -k 10 300 python -u tools/x3_stamps.py stem:32 stem:128 > $O/stamps_stem.log 2>&1
+    timeout -k 10 300 python -u tools/x3_stamps.py --tile 6 stem:32 stem:128 > $O/stamps_stem_pair.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "stem_pair=1" "" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "stem_pair=1" "" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1

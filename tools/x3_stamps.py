@@ -43,7 +43,7 @@ def main():
         if prec == "stem":
             img = torch.randint(0, 256, (n, h, w, 3), device=dev, dtype=torch.uint8, generator=g)
             wp = ops.stem_weight_pack_x3(torch.randn(co, ci, k, k, device=dev, generator=g) * 0.05)
-            run = lambda: ops.conv2d_fwd_stem_x3(img, wp, co)  # noqa: E731
+            run = lambda: ops.conv2d_fwd_stem_x3(img, wp, co, tile=tile)  # noqa: E731
         elif prec == "x3":
             x = torch.relu(torch.randn(n, h, w, ci, device=dev, generator=g))
             wt = torch.randn(co, k, k, ci, device=dev, generator=g) * (2.0 / (k * k * co)) ** 0.5
