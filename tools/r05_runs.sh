@@ -26,6 +26,7 @@
 #   rehearse8 bench.py --gpus 4 and --gpus 8 as gloo rehearsals on the one GPU (the driver's
 #             scaling run's relaunch, rendezvous, north_star and train legs; not a measurement)
 #   stem      per-block phase clocks of the stem conv (C2 batch 32, C4 batch 128)
+#   stem4     the 4-wave stem patch form: tests, phase clocks, C2 / C4 A/B in one process
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -188,6 +189,15 @@ stem)
     timeout -k 10 300 python -u tools/x3_stamps.py --tile 6 stem:32 stem:128 > $O/stamps_stem_pair.log 2>&1
     timeout -k 10 400 python -u tools/infer_ab.py "stem_pair=1" "" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "stem_pair=1" "" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+stem4)
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "stem" > $O/pytest_stem4.log 2>&1
+    echo "pytest stem4: $(tail -1 $O/pytest_stem4.log)"
+    timeout -k 10 300 python -u tools/x3_stamps.py stem:32 stem4:32 stem:128 stem4:128 > $O/stamps.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "" "stem4=1" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "" "stem4=1" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
