@@ -1881,7 +1881,6 @@ constexpr int STEM_PGA = (STEM_PCH + 511) / 512;                 // patch DMA in
 constexpr int STEM_LDS = STEM_BBYTES + 8 * STEM_PGA * 1024;      // B, then the patch (+ dummy chunks): 80 KiB
 
 static int g_stem_pair = 0;                                      // hkp_debug_stem_pair
-static int g_stem_patch4 = 0;                                    // hkp_debug_stem_patch4
 static bool stem_patch_shape(int ho, int wo, int k) {
     return !g_stem_pair && ho % STEM_PH == 0 && wo % STEM_PW == 0 && k % 64 == 0;
 }
@@ -2005,126 +2004,6 @@ __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
     x3_stamp(a, 5);
 }
 
-// The 4-wave form (conv_x3_stem_patch4_kernel): a 4 x 32 patch (128 output pixels)
-// per 256-thread block, its 13 x 70 padded pixels (14 KB) staged once; the weight
-// fragments come straight from global memory (L1/L2-resident: 56 KB for the whole
-// stem) into registers one filter row ahead, so a block's LDS is its patch and,
-// after the K loop, its 128-row fp32 staging (34 KB): four blocks per CU instead of
-// two, each one's fill and epilogue beside three other blocks' MFMAs.
-constexpr int STEM4_PH = 4, STEM4_PR = 2 * STEM4_PH + 5;         // 13 padded rows
-constexpr int STEM4_PLANE = STEM4_PR * STEM_PC * 8;
-constexpr int STEM4_PCH = 2 * STEM4_PLANE / 16;                  // 910 chunks
-constexpr int STEM4_PGA = (STEM4_PCH + 255) / 256;               // 4 DMA instructions per wave
-constexpr int STEM4_LDS = 128 * (64 + 4) * 4;                    // the staging (34,816 B) >= the patch (16 KB)
-static_assert(STEM4_PGA * 256 * 16 <= STEM4_LDS, "stem patch4 LDS");
-
-__global__ __launch_bounds__(256, 4) void conv_x3_stem_patch4_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[STEM4_LDS];
-    constexpr int BM = 128, BN = 64, WN = 2, ROW = 128;
-    constexpr int UM = 4, UN = 2;                                // wave tile 64 x 32
-    x3_stamp(a, 0);
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
-    const int pwn = a.Wo / STEM_PW, tpi = (a.Ho / STEM4_PH) * pwn;
-    const int img = mt / tpi, rem = mt - img * tpi;
-    const int h0 = (rem / pwn) * STEM4_PH, w0 = (rem - (rem / pwn) * pwn) * STEM_PW;
-    const int m0 = mt * BM, n0 = nt * BN;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w / WN, wn = w % WN;
-    const int r16 = lane & 15, q = lane >> 4;
-
-    // weight fragments of filter row r: line (n, r) of [K][7][hi32 | lo32], this
-    // lane's chunk q of the hi half and of the lo half
-    const _Float16* wrow[UN];
-#pragma unroll
-    for (int j = 0; j < UN; ++j) wrow[j] = a.ws + (long)(n0 + wn * 32 + 16 * j + r16) * 7 * 64 + q * 8;
-    f16x8 bh[2][UN], bl[2][UN];
-    auto load_b = [&](int r, int s) {
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            bh[s][j] = *(const f16x8*)(wrow[j] + r * 64);
-            bl[s][j] = *(const f16x8*)(wrow[j] + r * 64 + 32);
-        }
-    };
-    load_b(0, 0);
-    // the patch: chunk c -> plane, patch row, 16-B column (35 per row)
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
-    const long prow0 = ((long)img * a.H + 2 * h0) * a.W + 2 * w0;
-#pragma unroll
-    for (int i = 0; i < STEM4_PGA; ++i) {
-        const int c = 256 * i + 64 * w + lane;
-        const int pl = c >= STEM4_PLANE / 16 ? 1 : 0, cc = c - pl * (STEM4_PLANE / 16);
-        const int pr = cc / (STEM_PC / 2), pc = cc - pr * (STEM_PC / 2);
-        const _Float16* src = c < STEM4_PCH ? a.xs + pl * a.plane + (prow0 + (long)pr * a.W) * 4 + pc * 8 : zero;
-        glds16(src, smem + (256 * i + 64 * w) * 16);
-    }
-    int aoff[UM];
-#pragma unroll
-    for (int i = 0; i < UM; ++i) {
-        const int m = wm * 64 + 16 * i + r16;
-        aoff[i] = ((2 * (m >> 5)) * STEM_PC + 2 * (m & 31) + 2 * q) * 8;
-    }
-    f32x4 acc[UM][UN];
-#pragma unroll
-    for (int i = 0; i < UM; ++i)
-#pragma unroll
-        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
-    };
-    float scv[UN];
-#pragma unroll
-    for (int j = 0; j < UN; ++j) scv[j] = a.wscale ? a.wscale[n0 + wn * 32 + 16 * j + r16] : 1.f;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    x3_stamp(a, 1);
-    f16x8 ah[UM], al[UM];
-#pragma unroll
-    for (int r = 0; r < 7; ++r) {
-        if (r + 1 < 7) load_b(r + 1, (r + 1) & 1);              // the next row's weights in flight
-#pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            ah[i] = *(const f16x8*)(smem + aoff[i] + r * STEM_PC * 8);
-            al[i] = *(const f16x8*)(smem + aoff[i] + r * STEM_PC * 8 + STEM4_PLANE);
-        }
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int j = 0; j < UN; ++j) x3_products<3>(acc[i][j], ah[i], al[i], bh[r & 1][j], bl[r & 1][j], mfma);
-    }
-    x3_stamp(a, 2);
-
-    // ---- epilogue: BN partials of the tile's one 128-row half (the two row waves
-    // merged through LDS), the scaled tile staged as fp32 rows, 16-B row chunks ----
-    const int rbase = m0 + wm * UM * 16 + 4 * q;
-    lds_sync();                                                  // every wave done with the patch
-    if (a.part) {
-        x3_bn_partials_w<BN, UM, UN, 16, 16>(
-            a, (float*)smem, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; });
-        lds_sync();
-    }
-    x3_stamp(a, 3);
-    constexpr int PITCH = BN + 4, C4 = BN / 4;
-    float* st = (float*)smem;
-#pragma unroll
-    for (int i = 0; i < UM; ++i)
-#pragma unroll
-        for (int j = 0; j < UN; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                st[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * 32 + j * 16 + r16] = acc[i][j][r] * scv[j];
-    lds_sync();
-    x3_stamp(a, 4);
-#pragma unroll 4
-    for (int e = tid; e < BM * C4; e += 256) {
-        const int row = e / C4, c4 = e - row * C4;
-        const long off = (((long)img * a.Ho + h0 + (row >> 5)) * a.Wo + w0 + (row & 31)) * a.K + n0 + c4 * 4;
-        x3_st16((f32x4*)(a.y + off), *(const f32x4*)(st + row * PITCH + c4 * 4), a.st_kind, 2);
-    }
-    x3_stamp(a, 5);
-}
 
 // ---------------------------------------------------------------------------
 // A3P (conv_x3_a3p_kernel<P>): the A3 body (256x256 tiles, 3-stage A ring, 2-stage
@@ -4391,10 +4270,7 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR) {
         // the patch body (patch-divisible outputs: 480x640 and 960x1280 images);
         // HKP_TILE_64_PAIR keeps the one-tile stem (A/B, parity tests)
-        if (g_stem_patch4)
-            hipLaunchKernelGGL(conv_x3_stem_patch4_kernel, dim3(2 * m_tiles * a.n_tiles), dim3(256), 0, as_stream(stream), a);
-        else
-            hipLaunchKernelGGL(conv_x3_stem_patch_kernel, dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+        hipLaunchKernelGGL(conv_x3_stem_patch_kernel, dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
         HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
         return HKP_OK;
     }
@@ -4445,7 +4321,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
         }
         case HKP_KOP_STEM_X3:
             if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR)
-                return snprintf(buf, len, g_stem_patch4 ? "conv_x3_stem_patch4_kernel" : "conv_x3_stem_patch_kernel");
+                return snprintf(buf, len, "conv_x3_stem_patch_kernel");
             return x3_kernel_name(X3_STEM, true, 3, buf, len);
         case HKP_KOP_WGRAD_X3: {
             HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv_kernel_name: wgrad needs Cout%%64==0");
@@ -4473,7 +4349,6 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
 extern "C" void hkp_debug_stem_pair(int32_t on) { g_stem_pair = on != 0; }
-extern "C" void hkp_debug_stem_patch4(int32_t on) { g_stem_patch4 = on != 0; }
 extern "C" void hkp_debug_x3_frac_tail(int32_t mode) { g_x3_frac_tail = mode < 0 ? 0 : mode > 2 ? 2 : mode; }
 
 // Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'

@@ -266,9 +266,6 @@ void hkp_debug_x3_frac_tail(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
-/* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem patch body in its
- * 4-wave form (4 x 32 patches, weights from global memory, four blocks per CU). */
-void hkp_debug_stem_patch4(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -21,7 +21,7 @@ import torch  # noqa: E402
 
 
 KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "frac": ("hkp_debug_x3_frac_tail", 0),
-         "stem_pair": ("hkp_debug_stem_pair", 0), "stem4": ("hkp_debug_stem_patch4", 0)}
+         "stem_pair": ("hkp_debug_stem_pair", 0)}
 
 
 def knobs(form):

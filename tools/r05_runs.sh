@@ -26,7 +26,7 @@
 #   rehearse8 bench.py --gpus 4 and --gpus 8 as gloo rehearsals on the one GPU (the driver's
 #             scaling run's relaunch, rendezvous, north_star and train legs; not a measurement)
 #   stem      per-block phase clocks of the stem conv (C2 batch 32, C4 batch 128)
-#   stem4     the 4-wave stem patch form: tests, phase clocks, C2 / C4 A/B in one process
+#   stem4     the 4-wave stem patch form (removed after this run): tests, phase clocks, C2 / C4 A/B
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp

@@ -35,9 +35,8 @@ def main():
         lib().hkp_debug_duo_stagger(int(args[i + 1]))
         del args[i:i + 2]
     for name in args:
-        if name.startswith("stem"):          # stem[4][:N]: the 7x7/s2 stem (hkp_conv2d_fwd_stem_x3), batch N (32);
-            n = int(name.partition(":")[2] or 32)                  # stem4: the 4-wave patch form
-            lib().hkp_debug_stem_patch4(1 if name.startswith("stem4") else 0)
+        if name.startswith("stem"):          # stem[:N]: the 7x7/s2 stem (hkp_conv2d_fwd_stem_x3), batch N (32)
+            n = int(name.partition(":")[2] or 32)
             prec, h, w, ci, co, k, st, pd, dl = "stem", 480, 640, 3, 64, 7, 2, 3, 1
         else:
             prec, n, h, w, ci, co, k, st, pd, dl = SHAPES[name]
