@@ -96,6 +96,10 @@ struct X3Args {
     // the stream-K grid sk_combine works in when it is not the launch's grid: its
     // block count (0: gridDim.x) and this block's index in it (after the XCD remap)
     int sk_grid = 0, sk_b = 0;
+    // split-K tail with an integral segment count S (every group's range inside one
+    // m-tile): one slab per group (slot gg * n_tiles + nt) instead of two, so a
+    // multi-round tail (tm * S * n_tiles blocks > CUs) fits the workspace
+    int sk_one = 0;
     // A3 launches with the split-K tail appended (conv_x3_a3_kernel): blocks
     // [0, main_blocks) run the full rounds' tiles, the rest the tail's segments —
     // tail_groups groups of n_tiles blocks over tail_units (m-tile, K-step) units
@@ -287,7 +291,7 @@ __device__ __forceinline__ bool sk_combine(const X3Args& a, int T, int tid, char
     const int b0 = sk_block_of(t0, U, NG), nseg = sk_block_of(t0 + a.nks - 1, U, NG) - b0 + 1;
     auto slab = [&](int gg) {
         const int which = sk_start(gg, U, NG) >= t0 ? 0 : 1;
-        return (gf32x4*)a.sk_ws + (long)(2 * (gg * NT + nt) + which) * NV4 * 512;
+        return (gf32x4*)a.sk_ws + (long)(a.sk_one ? gg * NT + nt : 2 * (gg * NT + nt) + which) * NV4 * 512;
     };
     gf32x4* mine = slab((a.sk_grid ? a.sk_b : xcd_remap(blockIdx.x, gridDim.x)) / NT);
 #pragma unroll
@@ -1113,11 +1117,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-// OPQ: the lane id from v_mbcnt in volatile asm, not threadIdx.x — a second tile
-// body inlined after a first (conv_x3_a3sk_kernel) then shares none of the first's
-// lane-derived values, whose live ranges across the first body made it spill.
-__device__ __forceinline__ int x3_lane_opaque();
-template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false, bool OPQ = false>
+template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -1138,9 +1138,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = OPQ ? x3_lane_opaque() : (int)(threadIdx.x & 63);
-    const int tid = OPQ ? w * 64 + lane : (int)threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = w / WN, wn = w % WN;
 
     // swizzled physical chunk of a logical chunk in row r
@@ -1492,12 +1491,7 @@ __global__ __launch_bounds__(512, PAIR ? 2 : 1) void conv_x3_kernel(X3Args a) {
 // segments of conv_x3_tail_kernel) in the same launch: they are dispatched as the
 // full rounds' tiles finish, without the second launch's gap — and, in training,
 // ahead of a side-stream wgrad that would otherwise take the freed CUs first.
-// SEG2 (conv_x3_a3sk_kernel): a tail group's unit range may cross into the next
-// m-tile — the tail balanced over every CU at a fractional number of tiles per
-// block (C2 layer3 / layer4 tails, the 150-m-tile layer3/4 grids of a B=8 shard)
-// — and the block then runs that second segment after the first (both
-// sk_combine segments: slab slot 0 for the group's first m-tile, 1 for its last).
-template <int P, bool SEG2 = false>
+template <int P>
 __device__ __forceinline__ void conv_x3_a3_grid(const X3Args& a, char* smem) {
     x3_stagger(a);
     x3_stamp(a, 0);
@@ -1516,28 +1510,14 @@ __device__ __forceinline__ void conv_x3_a3_grid(const X3Args& a, char* smem) {
     const int g = t.sk_b / NT, nt = t.sk_b - g * NT;
     const long U = t.sk_units, u0 = sk_start(g, U, a.tail_groups), u1 = sk_start(g + 1, U, a.tail_groups);
     const int mt = (int)(u0 / a.nks);
-    const int ks = (int)(u0 - (long)mt * a.nks);
-    const int ke = SEG2 ? (int)min((long)a.nks, u1 - (long)mt * a.nks) : (int)(u1 - (long)mt * a.nks);
+    const int ks = (int)(u0 - (long)mt * a.nks), ke = (int)(u1 - (long)mt * a.nks);
     conv_x3_tile<256, false, false, 16, P, true>(t, smem, mt * NT + nt, ks, ke - ks, true);
-    if constexpr (SEG2) {
-        const long u = (long)mt * a.nks + ke;
-        if (u < u1) {
-            __syncthreads();               // every wave done with the ring and the epilogue's scratch
-            conv_x3_tile<256, false, false, 16, P, true, true>(t, smem, (mt + 1) * NT + nt, 0, (int)(u1 - u), true);
-        }
-    }
 }
 
 template <int P>
 __global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
     conv_x3_a3_grid<P>(a, smem);
-}
-
-template <int P>
-__global__ __launch_bounds__(512, 1) void conv_x3_a3sk_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
-    conv_x3_a3_grid<P, true>(a, smem);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -3503,48 +3483,38 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // 256x256 kernel sits at 255 VGPRs; the stream-K loop would spill).
 // Split-K tail (conv_x3_tail_kernel) for a one-tile grid of m_tiles x nt tiles:
 // the group count NG = tm*S of the tail grid (0: no tail) — each of the tm
-// m-tiles past the last full round in S equal K segments, one per group, in ONE
-// round (tm*S <= CUs/nt) — and its cost in tile times, 1/S + 0.08 (a segment's
-// fill, slab hand-off and combine).  C2 layer3 on 256x256 tiles (88 tail
-// tiles): S = 2, ~0.58 instead of 1; training t4: S = 5.  C2 layer4 (88 tail
-// m-tiles x 2 columns) has no S >= 2 that fits one round.
-// Fractional tail (conv_x3_a3sk_kernel, A3 body only): every CU's group takes
-// tm*nks/ngmax units, less than a tile, so a group's range may cross one m-tile
-// boundary (two segments); cost tm*nt/CUs of a round + two segments' fill, slab
-// hand-off and combine.  hkp_debug_x3_frac_tail: 0 never (default), 1 when the
-// cost model prefers it, 2 whenever legal.  Measured in one process
-// (profiles/r05_frac_*): per conv -1 % ... +19 % (the B=8 shard's layer3 ties
-// the stream-K 256x128 grid it would replace, 0.140 vs 0.141 ms), end to end
-// C2 -1.2 %, B=8 shard -1.9 %, C4 -1.3 %, C3 training -0.4 % — a tile split
-// across two groups waits for the later one's second segment, then its combine
-// and epilogue, and a full machine runs at a lower clock than a partial round.
-static int g_x3_frac_tail = 0;
+// m-tiles past the last full round in S equal K segments, one per group — and its
+// cost in tile times, 1/S + 0.08 (a segment's fill, slab hand-off and combine)
+// per round of segments.  C2 layer3 on 256x256 tiles (88 tail tiles): S = 2,
+// ~0.58 instead of 1; training t4: S = 5.  C2 layer4 (88 tail m-tiles x 2
+// columns) has no S >= 2 that beats one plain round.  (A fractional tail — every
+// CU's group a fraction of a tile, two segments per block — was built in round 5
+// and measured slower end to end: DESIGN "Fractional split-K tail".)
+// Multi-round tail (hkp_debug_x3_multi_tail, default on): S segments per tail
+// m-tile even when tm*S*nt blocks exceed one round — cost rounds x (1/S + 0.08),
+// one slab per block (X3Args::sk_one), at most X3_TAIL_SLABS blocks.  The B=8
+// shard's layer3 (150 m-tiles, no full round, one column tile): S = 3 in two
+// rounds (0.83 tile times) where one round of whole tiles costs 1.
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
-constexpr double X3_FRAC_OVER = 0.16;
-static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr, bool allow_frac = false,
-                           bool* frac = nullptr) {
-    const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G, ngmax = G / nt;
+static int g_x3_multi_tail = 1;                        // hkp_debug_x3_multi_tail
+constexpr long X3_TAIL_SLABS = 512;                    // 128 MiB of 256x256 fp32 slabs (x3_sk_ws_bytes(256))
+static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr, bool allow_multi = false) {
+    const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G;
     const long tm = m_tiles - tiles / G * G / nt;
     double best = 1.0;
     long ng = 0;
-    bool fr = false;
     if (tr > 0) {
-        for (int S = 2; S <= 8 && nks / S >= 4 && tm * S <= ngmax; ++S)
-            if (1.0 / S + 0.08 < best - 1e-9) {
-                best = 1.0 / S + 0.08;
+        for (int S = 2; S <= 8 && nks / S >= 4; ++S) {
+            const long blocks = tm * S * nt, rounds = (blocks + G - 1) / G;
+            if (rounds > 1 && !(allow_multi && g_x3_multi_tail && blocks <= X3_TAIL_SLABS)) continue;
+            const double c = rounds * (1.0 / S + 0.08);
+            if (c < best - 1e-9) {
+                best = c;
                 ng = tm * S;
-            }
-        if (allow_frac && g_x3_frac_tail && tm < ngmax && tm * nks >= 2 * ngmax) {
-            const double fc = (double)tm / ngmax + X3_FRAC_OVER;
-            if (fc < best - 1e-9 || g_x3_frac_tail == 2) {
-                best = fc;
-                ng = ngmax;
-                fr = true;
             }
         }
     }
     if (cost) *cost = tr > 0 ? best : 0.0;
-    if (frac) *frac = fr;
     return ng;
 }
 
@@ -3552,7 +3522,7 @@ struct X3Plan {
     int bn;
     bool sk;
 };
-static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over, bool allow_frac) {
+static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
     const int G = x3_cus();
     X3Plan best{64, false};
     double best_cost = 1e300;
@@ -3561,7 +3531,7 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over, boo
         const long tiles = m_tiles * (k / bn);
         const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
         double tail = (tiles % G) ? 1.0 : 0.0;             // the last, partly filled round
-        if (bn == 256 && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail, allow_frac);
+        if (bn == 256 && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail, true);
         const double dp = ((double)(tiles / G) + tail) * col;
         if (dp < best_cost - 1e-9) {
             best_cost = dp;
@@ -3672,10 +3642,7 @@ static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int pol
             break;
     }
     const bool sk = sk_ok && policy != HKP_TILE_NO_SK && policy != HKP_TILE_256_TAIL && policy != HKP_TILE_256_A3;
-    // the fractional tail runs on the A3 body: planned for AUTO (whose 256x256
-    // one-tile grids are A3's), not AUTO_A3 (the round-4 planner)
-    const X3Plan pl = x3_plan(k, m_tiles, nks, sk, policy == HKP_TILE_SK ? 0.0 : sk_over(nks),
-                              policy == HKP_TILE_AUTO && !g_x3_split_tail);
+    const X3Plan pl = x3_plan(k, m_tiles, nks, sk, policy == HKP_TILE_SK ? 0.0 : sk_over(nks));
     if (pl.sk) return {pl.bn, pl.bn == 128 ? 16 : 32, false, true};
     if (pl.bn == 256) return {256, 16, false, false};
     if (pl.bn == 128) return {128, (double)m_tiles * (k / 128) >= 2.0 * x3_cus() ? 16 : 32, false, false};
@@ -3683,13 +3650,6 @@ static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int pol
 }
 
 static const X3Choice X3_STEM{64, 16, true, false};
-
-// the launch's 256x256 A3 grid has a fractional tail (conv_x3_a3sk_kernel)
-static bool x3_is_frac(const X3Choice& c, int k, long m_tiles, int nks, bool sk_ok, int policy, int P) {
-    if (!(c.a3 && !c.sk && sk_ok && policy == HKP_TILE_AUTO && !g_x3_split_tail && (P == 1 || P == 3))) return false;
-    bool frac = false;
-    return x3_tail_groups(m_tiles, k / 256, nks, nullptr, true, &frac) > 0 && frac;
-}
 
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
@@ -3819,19 +3779,19 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     const long G = x3_cus();
     const long rm = tiles / G * G / a.n_tiles;              // m-tiles of the full rounds
     const long tm = m_tiles - rm;
-    bool frac = false;
     long NG = (!c.sk && c.bn == 256 && sk_ok &&
                (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3 ||
                 policy == HKP_TILE_AUTO_A3))
-                  ? x3_tail_groups(m_tiles, a.n_tiles, nks, nullptr, c.a3 && policy == HKP_TILE_AUTO && !g_x3_split_tail && (P == 1 || P == 3),
-                                   &frac)
+                  ? x3_tail_groups(m_tiles, a.n_tiles, nks, nullptr, true)
                   : 0;
-    // one round, every group non-empty and inside two tiles, slabs and counters in the workspace
-    if (NG > 0 && !(tm > 0 && NG * a.n_tiles <= G && tm * nks >= NG && tm < NG &&
-                    2L * G * 256 * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
+    // every group non-empty and inside one tile (NG = tm * S), one slab per block
+    // and the counters in the workspace
+    if (NG > 0 && !(tm > 0 && NG % tm == 0 && tm * nks >= NG && NG * a.n_tiles * 256L * 1024 + X3_SK_CNT_BYTES <= ws_bytes &&
+                    tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
         NG = 0;
     const bool tail = NG > 0;
-    // one launch: the full rounds, then the tail's segments (fractional: up to two per block)
+    a.sk_one = tail;
+    // one launch: the full rounds, then the tail's segments
     if (tail && c.a3 && !g_x3_split_tail) {
         X3Args t = a;
         t.main_blocks = (int)(rm * a.n_tiles);
@@ -3841,11 +3801,6 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         t.sk_cnt = (unsigned*)ws;
         t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
         const dim3 g1((unsigned)((rm + NG) * a.n_tiles));
-        if (frac) {
-            if (P == 3) hipLaunchKernelGGL(conv_x3_a3sk_kernel<3>, g1, dim3(512), 0, st, t);
-            else if (P == 1) hipLaunchKernelGGL(conv_x3_a3sk_kernel<1>, g1, dim3(512), 0, st, t);
-            return;                        // (P 1 / 3 only: x3_tail_groups' allow_frac)
-        }
         x3_dispatch_p(P, [&](auto pc) { launch_a3<pc.value>(g1, st, t); });
         return;
     }
@@ -4305,9 +4260,8 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int nks = d->r * d->s * (d->c / cg);
             const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
                               (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);
-            const X3Choice c = x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->c / cg, P), P);
-            if (x3_is_frac(c, d->k, (m + 255) / 256, nks, sk, d->tile, P)) return snprintf(buf, len, "conv_x3_a3sk_kernel<%d>", P);
-            return x3_kernel_name(c, false, P, buf, len);
+            return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->c / cg, P), P),
+                                  false, P, buf, len);
         }
         case HKP_KOP_DGRAD_X3: {
             const long m = (long)d->n * d->h * d->w;
@@ -4315,9 +4269,8 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int padp = d->dilation * (d->r - 1) - d->pad;
             const bool halo = halo_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
                               (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32);
-            const X3Choice c = x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->k / 32, 3), 3);
-            if (x3_is_frac(c, d->c, (m + 255) / 256, nks, sk, d->tile, 3)) return snprintf(buf, len, "conv_x3_a3sk_kernel<3>");
-            return x3_kernel_name(c, false, 3, buf, len);
+            return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->k / 32, 3), 3),
+                                  false, 3, buf, len);
         }
         case HKP_KOP_STEM_X3:
             if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR)
@@ -4349,7 +4302,7 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
 extern "C" void hkp_debug_stem_pair(int32_t on) { g_stem_pair = on != 0; }
-extern "C" void hkp_debug_x3_frac_tail(int32_t mode) { g_x3_frac_tail = mode < 0 ? 0 : mode > 2 ? 2 : mode; }
+extern "C" void hkp_debug_x3_multi_tail(int32_t on) { g_x3_multi_tail = on != 0; }
 
 // Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'
 // epilogue output stores (X3Args::st_kind: 0 each site's own, 1 plain, 2

@@ -257,15 +257,13 @@ void hkp_debug_duo_stagger(int32_t ns);
 /* Debug / A/B (tools/ only, not thread-safe): static wave priority in the A3 body's
  * K loop: 0 none (default), 1 s_setprio 1 on waves 4-7, 2 on waves 0-3. */
 void hkp_debug_x3_prio(int32_t mode);
-/* Debug / A/B (tools/ only, not thread-safe): the A3 grid's fractional split-K tail
- * (conv_x3_a3sk_kernel: the last round balanced over every CU, a block's range
- * crossing at most one m-tile boundary) — 0 never (default: measured slower end to
- * end), 1 where the planner's cost model prefers it, 2 whenever legal (AUTO policy,
- * f16x3 / plain fp16). */
-void hkp_debug_x3_frac_tail(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
+/* Debug / A/B (tools/ only, not thread-safe): 0 keeps a 256x256 grid's split-K tail to
+ * one round of segments (the round-4 planner); 1 (default) also plans multi-round
+ * tails (one slab per segment). */
+void hkp_debug_x3_multi_tail(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

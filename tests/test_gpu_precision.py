@@ -634,6 +634,8 @@ TAIL_CASES = [
     ("x3", 9, 60, 80, 256, 512, 3, 1, 4, 4),       # two column tiles, 338 tiles, ragged M
     ("f16", 16, 60, 80, 512, 256, 1, 1, 0, 1),     # plain fp16, 8 K-steps per tile
     ("x3", 4, 60, 80, 256, 256, 3, 1, 2, 2),       # 75 tiles, no full round: a tail-only grid (S = 3)
+    ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),       # 150 tiles: a two-round tail (S = 3, one slab per segment)
+    ("f16", 8, 60, 80, 256, 256, 3, 1, 2, 2),      # the same in plain fp16 (S = 2, 18 K-steps)
 ]
 
 
@@ -666,80 +668,41 @@ def test_split_k_tail(cuda_device, case):
         assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item(), tile
         assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3), tile
         assert torch.equal(y1, y2), tile                       # counters back at zero, fixed order
+    # AUTO plans the 256x256 A3 grid with its tail for these shapes
+    from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
+    assert ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, 0),
+                           HKP_KOP_FWD_F16 if prec == "f16" else HKP_KOP_FWD_X3).startswith("conv_x3_a3_kernel")
 
 
-FRAC_CASES = [
-    # (precision, n, h, w, cin, cout, k, stride, pad, dil): the fractional A3 tail
-    ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),       # north_star shard layer3: 150 tiles, no full round
-    ("x3", 8, 60, 80, 512, 512, 3, 1, 4, 4),       # shard layer4: 150 m-tiles x 2 columns
-    ("x3", 9, 60, 80, 256, 512, 3, 1, 4, 4),       # one full round + 41 m-tiles x 2, ragged M
-    ("x3", 16, 60, 80, 256, 256, 3, 1, 2, 2),      # one full round + 44 tiles
-    ("f16", 8, 60, 80, 1024, 256, 1, 1, 0, 1),     # plain fp16, 16 K-steps per tile
-    ("f16", 8, 60, 80, 256, 256, 3, 1, 2, 2),
-]
-
-
-@pytest.mark.parametrize("case", FRAC_CASES)
-def test_fractional_tail(cuda_device, case):
-    """conv_x3_a3sk_kernel (hkp_debug_x3_frac_tail 2 forces it where legal): the
-    last round's tiles spread over every CU at a fractional share each, a block's
-    unit range crossing at most one m-tile boundary (two sk_combine segments) —
-    the plain one-tile grid's values to fp32 summation order, its BN partials, and
-    run to run bit-identical (counters back at zero, fixed slab order)."""
+@pytest.mark.parametrize("tile", [9, 11])      # HKP_TILE_256_TAIL (separate tail launch), HKP_TILE_256_A3
+def test_multi_round_tail_dgrad(cuda_device, tile):
+    """A split-K tail of more segments than one round holds (the C3 shard's layer3
+    dgrad: 150 m-tiles, S = 3 -> 450 segments over 256 CUs, one slab per segment):
+    bit-identical back to back (counters back at zero, slabs not leaking into the
+    next launch), the plain one-tile grid's dx to fp32 summation order — and with
+    the multi-round tail off (hkp_debug_x3_multi_tail 0) the same values."""
     from hkp import ops
-    from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_TILE_256, ConvDesc, lib
-    prec, n, h, w, cin, cout, k, st, pad, dil = case
-    d = cuda_device
-    g = torch.Generator(device=d).manual_seed(13)
-    x = torch.relu(torch.randn(n, h, w, cin, device=d, generator=g))
-    wt = torch.randn(cout, k, k, cin, device=d, generator=g) * (2.0 / (k * k * cout)) ** 0.5
-    if prec == "f16":
-        xs, wp, fwd, op, P = x.half(), ops.weight_pack_f16(wt), ops.conv2d_fwd_f16, HKP_KOP_FWD_F16, 1
-    else:
-        ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
-        xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
-        wp, fwd, op, P = ops.weight_pack_x3(wt), ops.conv2d_fwd_x3, HKP_KOP_FWD_X3, 3
-    y0, p0 = fwd(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256)
-    tol = 2.0 ** -10 if prec == "f16" else 4e-6
-    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, 0)
-    try:
-        lib().hkp_debug_x3_frac_tail(2)
-        assert ops.kernel_name(desc, op) == "conv_x3_a3sk_kernel<%d>" % P
-        y1, p1 = fwd(xs, wp, st, pad, dil)
-        y2, p2 = fwd(xs, wp, st, pad, dil)
-    finally:
-        lib().hkp_debug_x3_frac_tail(0)
-    assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item()
-    assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
-    assert torch.equal(y1, y2) and torch.equal(p1, p2)
-
-
-def test_fractional_tail_dgrad(cuda_device):
-    """The fractional A3 tail on a stride-1 dgrad (the C3 shard's layer3: 150
-    m-tiles), with the residual addend: bit-identical back to back, the plain
-    grid's dx to fp32 summation order."""
-    from hkp import ops
-    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_TILE_256, ConvDesc, lib
+    from hkp._lib import HKP_TILE_256, lib
     n, h, w, cin, cout, k, pad, dil = 8, 60, 80, 256, 256, 3, 2, 2
     d = cuda_device
-    g = torch.Generator(device=d).manual_seed(23)
+    g = torch.Generator(device=d).manual_seed(29)
     wt = torch.randn(cout, k, k, cin, device=d, generator=g) * (2.0 / (k * k * cout)) ** 0.5
     gy = torch.randn(n, h, w, cout, device=d, generator=g) * 1e-3
     add = torch.randn(n, h, w, cin, device=d, generator=g) * 1e-3
     amax = ops.absmax(gy)
     dys = ops.split_pack_x3(gy, amax)
     wf = ops.weight_flip_pack_x3(wt)
-    dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, sk=False, tile=HKP_TILE_256)
-    try:
-        lib().hkp_debug_x3_frac_tail(2)
-        assert ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, 1, pad, dil, 0, 0),
-                               HKP_KOP_DGRAD_X3) == "conv_x3_a3sk_kernel<3>"
-        dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax)
-        dx2 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax)
-    finally:
-        lib().hkp_debug_x3_frac_tail(0)
+    run = lambda t, **kw: ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=t, **kw)  # noqa: E731
+    dx0 = run(HKP_TILE_256, sk=False)
+    dx1, dx2 = run(tile), run(tile)
     assert torch.equal(dx1, dx2)
     assert (dx1 - dx0).abs().max().item() <= 4e-6 * dx0.abs().max().item()
+    try:
+        lib().hkp_debug_x3_multi_tail(0)
+        dx3 = run(tile)
+    finally:
+        lib().hkp_debug_x3_multi_tail(1)
+    assert (dx3 - dx0).abs().max().item() <= 4e-6 * dx0.abs().max().item()
 
 
 def test_split_k_tail_dgrad_back_to_back(cuda_device):

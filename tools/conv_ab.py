@@ -59,8 +59,8 @@ def main():
                     "tiles (hkp_debug_duo_stagger: 0 off, -1 the default estimate)")
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
-    ap.add_argument("--fracs", default="0", help="A3 fractional-tail modes to cross with the tiles "
-                    "(hkp_debug_x3_frac_tail: 0 never, 1 planner, 2 whenever legal)")
+    ap.add_argument("--multis", default="1", help="multi-round split-K tail modes to cross with the tiles "
+                    "(hkp_debug_x3_multi_tail: 0 one round only, 1 default)")
     args = ap.parse_args()
     if args.lib:
         from hkp import _lib
@@ -69,12 +69,12 @@ def main():
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     from hkp._lib import lib
     forms = [(int(t), int(k), int(d), int(fr)) for t in args.tiles.split(",") for k in args.stores.split(",")
-             for d in args.duo_staggers.split(",") for fr in args.fracs.split(",")]
+             for d in args.duo_staggers.split(",") for fr in args.multis.split(",")]
 
-    def set_store(k, d=-1, fr=0):
+    def set_store(k, d=-1, mt=1):
         lib().hkp_debug_x3_store(k)
         lib().hkp_debug_duo_stagger(d)
-        lib().hkp_debug_x3_frac_tail(fr)
+        lib().hkp_debug_x3_multi_tail(mt)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):
@@ -123,7 +123,7 @@ def main():
             set_store(f[1], f[2], f[3])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
             set_store(0)
-            print("%-9s tile %d store %d stagger %d frac %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
+            print("%-9s tile %d store %d stagger %d multi %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
                   "max rel diff=%.1e" % (name, t, f[1], f[2], f[3], ts[len(ts) // 2], ts[0],
                                          flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same), flush=True)
 

@@ -20,8 +20,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 
-KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "frac": ("hkp_debug_x3_frac_tail", 0),
-         "stem_pair": ("hkp_debug_stem_pair", 0)}
+KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0), "multi": ("hkp_debug_x3_multi_tail", 1)}
 
 
 def knobs(form):
@@ -35,8 +34,8 @@ def set_knobs(lib, kv):
 
 
 def parse(form):
-    """Policy overrides of a form; the pseudo-fields store=K, prio=K and frac=K
-    are library debug knobs (hkp_debug_x3_store / _x3_prio / _x3_frac_tail), not
+    """Policy overrides of a form; the pseudo-fields store=K, prio=K, stem_pair=K and multi=K
+    are library debug knobs (hkp_debug_x3_store / _x3_prio / _stem_pair / _x3_multi_tail), not
     Policy fields."""
     from hkp.policy import DEFAULT
     kw = {}

@@ -27,6 +27,8 @@
 #             scaling run's relaunch, rendezvous, north_star and train legs; not a measurement)
 #   stem      per-block phase clocks of the stem conv (C2 batch 32, C4 batch 128)
 #   stem4     the 4-wave stem patch form (removed after this run): tests, phase clocks, C2 / C4 A/B
+#   multi     the multi-round split-K tail: tail tests, per-conv A/B (hkp_debug_x3_multi_tail 0 / 1),
+#             B=8 shard / C2 / C3-train A/B in one process
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -199,6 +201,17 @@ stem4)
     timeout -k 10 400 python -u tools/infer_ab.py "" "stem4=1" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "" "stem4=1" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+multi)
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "tail" > $O/pytest_multi.log 2>&1
+    echo "pytest multi: $(tail -1 $O/pytest_multi.log)"
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0 --multis 0,1 --rounds 7 --iters 5 \
+        --shapes t3,t3a,t4,layer3,layer4 > $O/conv_ab.log 2>&1
+    echo "conv_ab ok"
+    timeout -k 10 400 python -u tools/infer_ab.py "multi=0" "" --batch 8 --rounds 9 --iters 20 > $O/ab_b8.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "multi=0" "" --batch 64 --rounds 5 --iters 5 > $O/ab_b64.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "multi=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
