@@ -96,9 +96,8 @@ struct X3Args {
     // the stream-K grid sk_combine works in when it is not the launch's grid: its
     // block count (0: gridDim.x) and this block's index in it (after the XCD remap)
     int sk_grid = 0, sk_b = 0;
-    // split-K tail with an integral segment count S (every group's range inside one
-    // m-tile): one slab per group (slot gg * n_tiles + nt) instead of two, so a
-    // multi-round tail (tm * S * n_tiles blocks > CUs) fits the workspace
+    // split-K tail (every group's range inside one m-tile): one slab per group
+    // (slot gg * n_tiles + nt) instead of the stream-K grid's two
     int sk_one = 0;
     // A3 launches with the split-K tail appended (conv_x3_a3_kernel): blocks
     // [0, main_blocks) run the full rounds' tiles, the rest the tail's segments —
@@ -3490,29 +3489,21 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // columns) has no S >= 2 that beats one plain round.  (A fractional tail — every
 // CU's group a fraction of a tile, two segments per block — was built in round 5
 // and measured slower end to end: DESIGN "Fractional split-K tail".)
-// Multi-round tail (hkp_debug_x3_multi_tail, default on): S segments per tail
-// m-tile even when tm*S*nt blocks exceed one round — cost rounds x (1/S + 0.08),
-// one slab per block (X3Args::sk_one), at most X3_TAIL_SLABS blocks.  The B=8
-// shard's layer3 (150 m-tiles, no full round, one column tile): S = 3 in two
-// rounds (0.83 tile times) where one round of whole tiles costs 1.
+// (Multi-round tails — S segments per tail m-tile past one round, one slab per
+// segment — measured slower in round 5: the B=8 shard's layer3 0.138 -> 0.164 ms
+// at S = 3, C2 layer3 0.384 -> 0.418 ms at S = 5; profiles/r05_multi_*.)
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
-static int g_x3_multi_tail = 1;                        // hkp_debug_x3_multi_tail
-constexpr long X3_TAIL_SLABS = 512;                    // 128 MiB of 256x256 fp32 slabs (x3_sk_ws_bytes(256))
-static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr, bool allow_multi = false) {
+static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr) {
     const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G;
     const long tm = m_tiles - tiles / G * G / nt;
     double best = 1.0;
     long ng = 0;
     if (tr > 0) {
-        for (int S = 2; S <= 8 && nks / S >= 4; ++S) {
-            const long blocks = tm * S * nt, rounds = (blocks + G - 1) / G;
-            if (rounds > 1 && !(allow_multi && g_x3_multi_tail && blocks <= X3_TAIL_SLABS)) continue;
-            const double c = rounds * (1.0 / S + 0.08);
-            if (c < best - 1e-9) {
-                best = c;
+        for (int S = 2; S <= 8 && nks / S >= 4 && tm * S * nt <= G; ++S)
+            if (1.0 / S + 0.08 < best - 1e-9) {
+                best = 1.0 / S + 0.08;
                 ng = tm * S;
             }
-        }
     }
     if (cost) *cost = tr > 0 ? best : 0.0;
     return ng;
@@ -3531,7 +3522,7 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
         const long tiles = m_tiles * (k / bn);
         const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
         double tail = (tiles % G) ? 1.0 : 0.0;             // the last, partly filled round
-        if (bn == 256 && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail, true);
+        if (bn == 256 && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail);
         const double dp = ((double)(tiles / G) + tail) * col;
         if (dp < best_cost - 1e-9) {
             best_cost = dp;
@@ -3782,12 +3773,12 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     long NG = (!c.sk && c.bn == 256 && sk_ok &&
                (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3 ||
                 policy == HKP_TILE_AUTO_A3))
-                  ? x3_tail_groups(m_tiles, a.n_tiles, nks, nullptr, true)
+                  ? x3_tail_groups(m_tiles, a.n_tiles, nks)
                   : 0;
-    // every group non-empty and inside one tile (NG = tm * S), one slab per block
-    // and the counters in the workspace
-    if (NG > 0 && !(tm > 0 && NG % tm == 0 && tm * nks >= NG && NG * a.n_tiles * 256L * 1024 + X3_SK_CNT_BYTES <= ws_bytes &&
-                    tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
+    // one round, every group non-empty and inside one tile (NG = tm * S), one slab
+    // per block and the counters in the workspace
+    if (NG > 0 && !(tm > 0 && NG % tm == 0 && NG * a.n_tiles <= G && tm * nks >= NG &&
+                    NG * a.n_tiles * 256L * 1024 + X3_SK_CNT_BYTES <= ws_bytes && tm * a.n_tiles * 4 <= X3_SK_CNT_BYTES))
         NG = 0;
     const bool tail = NG > 0;
     a.sk_one = tail;
@@ -4302,7 +4293,6 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
 extern "C" void hkp_debug_stem_pair(int32_t on) { g_stem_pair = on != 0; }
-extern "C" void hkp_debug_x3_multi_tail(int32_t on) { g_x3_multi_tail = on != 0; }
 
 // Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'
 // epilogue output stores (X3Args::st_kind: 0 each site's own, 1 plain, 2

@@ -260,10 +260,6 @@ void hkp_debug_x3_prio(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
-/* Debug / A/B (tools/ only, not thread-safe): 0 keeps a 256x256 grid's split-K tail to
- * one round of segments (the round-4 planner); 1 (default) also plans multi-round
- * tails (one slab per segment). */
-void hkp_debug_x3_multi_tail(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -59,8 +59,6 @@ def main():
                     "tiles (hkp_debug_duo_stagger: 0 off, -1 the default estimate)")
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
-    ap.add_argument("--multis", default="1", help="multi-round split-K tail modes to cross with the tiles "
-                    "(hkp_debug_x3_multi_tail: 0 one round only, 1 default)")
     args = ap.parse_args()
     if args.lib:
         from hkp import _lib
@@ -68,13 +66,12 @@ def main():
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     from hkp._lib import lib
-    forms = [(int(t), int(k), int(d), int(fr)) for t in args.tiles.split(",") for k in args.stores.split(",")
-             for d in args.duo_staggers.split(",") for fr in args.multis.split(",")]
+    forms = [(int(t), int(k), int(d)) for t in args.tiles.split(",") for k in args.stores.split(",")
+             for d in args.duo_staggers.split(",")]
 
-    def set_store(k, d=-1, mt=1):
+    def set_store(k, d=-1):
         lib().hkp_debug_x3_store(k)
         lib().hkp_debug_duo_stagger(d)
-        lib().hkp_debug_x3_multi_tail(mt)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):
@@ -101,7 +98,7 @@ def main():
         for r in range(args.rounds):
             for f in forms:
                 t = f[0]
-                set_store(f[1], f[2], f[3])
+                set_store(f[1], f[2])
                 y = run(t)
                 if r == 0:
                     outs[f] = y.float()
@@ -120,11 +117,11 @@ def main():
         for f in forms:
             t = f[0]
             ts = sorted(times[f])
-            set_store(f[1], f[2], f[3])
+            set_store(f[1], f[2])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
             set_store(0)
-            print("%-9s tile %d store %d stagger %d multi %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
-                  "max rel diff=%.1e" % (name, t, f[1], f[2], f[3], ts[len(ts) // 2], ts[0],
+            print("%-9s tile %d store %d stagger %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
+                  "max rel diff=%.1e" % (name, t, f[1], f[2], ts[len(ts) // 2], ts[0],
                                          flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same), flush=True)
 
 

@@ -20,7 +20,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 
-KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0), "multi": ("hkp_debug_x3_multi_tail", 1)}
+KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0)}
 
 
 def knobs(form):
@@ -34,8 +34,8 @@ def set_knobs(lib, kv):
 
 
 def parse(form):
-    """Policy overrides of a form; the pseudo-fields store=K, prio=K, stem_pair=K and multi=K
-    are library debug knobs (hkp_debug_x3_store / _x3_prio / _stem_pair / _x3_multi_tail), not
+    """Policy overrides of a form; the pseudo-fields store=K, prio=K and stem_pair=K
+    are library debug knobs (hkp_debug_x3_store / _x3_prio / _stem_pair), not
     Policy fields."""
     from hkp.policy import DEFAULT
     kw = {}

@@ -23,7 +23,7 @@ from infer_ab import KNOBS, knobs, set_knobs  # noqa: E402  (tools/ is on sys.pa
 
 
 def parse(form):
-    """Policy overrides of a form; the pseudo-fields store=K, prio=K, stem_pair=K and multi=K
+    """Policy overrides of a form; the pseudo-fields store=K, prio=K and stem_pair=K
     are library debug knobs (infer_ab.KNOBS), not Policy fields."""
     from hkp.policy import DEFAULT
     kw = {}
