@@ -29,6 +29,7 @@
 #   stem4     the 4-wave stem patch form (removed after this run): tests, phase clocks, C2 / C4 A/B
 #   multi     the multi-round split-K tail: tail tests, per-conv A/B (hkp_debug_x3_multi_tail 0 / 1),
 #             B=8 shard / C2 / C3-train A/B in one process
+#   tail128   the split-K tail on 256x128 grids: tests, per-conv and C2 / C3 / C4 A/B in one process
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -212,6 +213,15 @@ multi)
     timeout -k 10 400 python -u tools/infer_ab.py "multi=0" "" --batch 8 --rounds 9 --iters 20 > $O/ab_b8.log 2>&1
     timeout -k 10 400 python -u tools/infer_ab.py "multi=0" "" --batch 64 --rounds 5 --iters 5 > $O/ab_b64.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "multi=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
+tail128)
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "tail" > $O/pytest_tail128.log 2>&1
+    echo "pytest tail128: $(tail -1 $O/pytest_tail128.log)"
+    timeout -k 10 400 python -u tools/infer_ab.py "tail128=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "tail128=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "tail128=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
