@@ -3493,8 +3493,9 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // segment — measured slower in round 5: the B=8 shard's layer3 0.138 -> 0.164 ms
 // at S = 3, C2 layer3 0.384 -> 0.418 ms at S = 5; profiles/r05_multi_*.)
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
-// the same tail on 256x128 one-tile grids (conv_x3_tail_kernel<128, P>: C2's layer2,
-// 600 tiles = 2 rounds + 88); hkp_debug_x3_tail128 (A/B)
+// the same tail on 256x128 one-tile grids of >= 2 full rounds (conv_x3_tail_kernel<128,
+// P>: C2's layer2, 600 tiles = 2 rounds + 88); hkp_debug_x3_tail128 (A/B).  On the
+// C3 shard's 1.2-round grids it lost (C3 453 -> 446 img/s, profiles/r05_tail128_*_v1)
 static int g_x3_tail128 = 1;
 static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr) {
     const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G;
@@ -3525,7 +3526,7 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
         const long tiles = m_tiles * (k / bn);
         const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
         double tail = (tiles % G) ? 1.0 : 0.0;             // the last, partly filled round
-        if ((bn == 256 || (bn == 128 && g_x3_tail128)) && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail);
+        if ((bn == 256 || (bn == 128 && g_x3_tail128 && tiles >= 2 * G)) && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail);
         const double dp = ((double)(tiles / G) + tail) * col;
         if (dp < best_cost - 1e-9) {
             best_cost = dp;
@@ -3776,7 +3777,8 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     long NG = (!c.sk && sk_ok &&
                ((c.bn == 256 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL ||
                                  policy == HKP_TILE_256_A3 || policy == HKP_TILE_AUTO_A3)) ||
-                (c.bn == 128 && !c.pair && g_x3_tail128 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_AUTO_A3))))
+                (c.bn == 128 && !c.pair && c.mfd == 16 && g_x3_tail128 && m_tiles * a.n_tiles >= 2 * G &&
+                 (policy == HKP_TILE_AUTO || policy == HKP_TILE_AUTO_A3))))
                   ? x3_tail_groups(m_tiles, a.n_tiles, nks)
                   : 0;
     // one round, every group non-empty and inside one tile (NG = tm * S), one slab

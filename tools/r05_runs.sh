@@ -218,7 +218,7 @@ tail128)
     timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
         -k "tail" > $O/pytest_tail128.log 2>&1
     echo "pytest tail128: $(tail -1 $O/pytest_tail128.log)"
-    timeout -k 10 400 python -u tools/infer_ab.py "tail128=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "tail128=0" "" "tail128=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "tail128=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "tail128=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
