@@ -671,14 +671,15 @@ def test_split_k_tail(cuda_device, case):
 TAIL128_CASES = [
     # (precision, n, h, w, cin, cout, k, stride, pad, dil, tile policy): 256x128 grids with a partial last round
     ("x3", 32, 60, 80, 128, 128, 3, 1, 1, 1, 0),    # C2 layer2: 600 tiles = 2 rounds + 88 (S = 2)
-    ("x3", 17, 60, 80, 128, 128, 3, 1, 1, 1, 0),    # 319 tiles, ragged M: 1 round + 63 (S = 4)
+    ("x3", 33, 60, 80, 128, 128, 3, 1, 1, 1, 0),    # 619 tiles, ragged M: 2 rounds + 107 (S = 2)
     ("f16", 16, 60, 80, 512, 128, 1, 1, 0, 1, 12),  # plain fp16 under AUTO_A3 (AUTO plans DUO here)
 ]
 
 
 @pytest.mark.parametrize("case", TAIL128_CASES)
 def test_split_k_tail_128(cuda_device, case):
-    """The split-K tail on 256x128 one-tile grids (conv_x3_tail_kernel<128, P>): the
+    """The split-K tail on 256x128 one-tile grids of >= 2 full rounds
+    (conv_x3_tail_kernel<128, P>): the
     values of the same grid without it (hkp_debug_x3_tail128 0) to fp32 summation
     order — not the same bits, so the tail did run — the same BN partials, and run to
     run bit-identical."""
