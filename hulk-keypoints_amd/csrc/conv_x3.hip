@@ -3491,12 +3491,10 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // and measured slower end to end: DESIGN "Fractional split-K tail".)
 // (Multi-round tails — S segments per tail m-tile past one round, one slab per
 // segment — measured slower in round 5: the B=8 shard's layer3 0.138 -> 0.164 ms
-// at S = 3, C2 layer3 0.384 -> 0.418 ms at S = 5; profiles/r05_multi_*.)
+// at S = 3, C2 layer3 0.384 -> 0.418 ms at S = 5; profiles/r05_multi_*.  The tail
+// on 256x128 grids of >= 2 rounds (C2 layer2) measured neutral: C2 1753.0 vs 1755.5
+// img/s, C4 / C3 unchanged; profiles/r05_tail128_*_v2.)
 static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
-// the same tail on 256x128 one-tile grids of >= 2 full rounds (conv_x3_tail_kernel<128,
-// P>: C2's layer2, 600 tiles = 2 rounds + 88); hkp_debug_x3_tail128 (A/B).  On the
-// C3 shard's 1.2-round grids it lost (C3 453 -> 446 img/s, profiles/r05_tail128_*_v1)
-static int g_x3_tail128 = 1;
 static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr) {
     const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G;
     const long tm = m_tiles - tiles / G * G / nt;
@@ -3526,7 +3524,7 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
         const long tiles = m_tiles * (k / bn);
         const double col = bn * (bn == 256 ? 0.9 : bn == 128 ? 1.0 : 1.25);
         double tail = (tiles % G) ? 1.0 : 0.0;             // the last, partly filled round
-        if ((bn == 256 || (bn == 128 && g_x3_tail128 && tiles >= 2 * G)) && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail);
+        if (bn == 256 && sk_ok) x3_tail_groups(m_tiles, k / bn, nks, &tail);
         const double dp = ((double)(tiles / G) + tail) * col;
         if (dp < best_cost - 1e-9) {
             best_cost = dp;
@@ -3774,11 +3772,9 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     const long G = x3_cus();
     const long rm = tiles / G * G / a.n_tiles;              // m-tiles of the full rounds
     const long tm = m_tiles - rm;
-    long NG = (!c.sk && sk_ok &&
-               ((c.bn == 256 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL ||
-                                 policy == HKP_TILE_256_A3 || policy == HKP_TILE_AUTO_A3)) ||
-                (c.bn == 128 && !c.pair && c.mfd == 16 && g_x3_tail128 && m_tiles * a.n_tiles >= 2 * G &&
-                 (policy == HKP_TILE_AUTO || policy == HKP_TILE_AUTO_A3))))
+    long NG = (!c.sk && c.bn == 256 && sk_ok &&
+               (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3 ||
+                policy == HKP_TILE_AUTO_A3))
                   ? x3_tail_groups(m_tiles, a.n_tiles, nks)
                   : 0;
     // one round, every group non-empty and inside one tile (NG = tm * S), one slab
@@ -3812,10 +3808,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         t.sk_cnt = (unsigned*)ws;
         t.sk_ws = (float*)((char*)ws + X3_SK_CNT_BYTES);
         const dim3 gt((unsigned)(NG * a.n_tiles));
-        if (c.bn == 128)
-            x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL((conv_x3_tail_kernel<128, pc.value>), gt, dim3(512), 0, st, t); });
-        else
-            x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL((conv_x3_tail_kernel<256, pc.value>), gt, dim3(512), 0, st, t); });
+        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL((conv_x3_tail_kernel<256, pc.value>), gt, dim3(512), 0, st, t); });
         return;
     }
     x3_dispatch_p(P, [&](auto pc) { launch_x3_p<pc.value>(c, grid, st, a); });
@@ -4302,7 +4295,6 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
 extern "C" void hkp_debug_stem_pair(int32_t on) { g_stem_pair = on != 0; }
-extern "C" void hkp_debug_x3_tail128(int32_t on) { g_x3_tail128 = on != 0; }
 
 // Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'
 // epilogue output stores (X3Args::st_kind: 0 each site's own, 1 plain, 2

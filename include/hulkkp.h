@@ -260,9 +260,6 @@ void hkp_debug_x3_prio(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
-/* Debug / A/B (tools/ only, not thread-safe): 0 runs 256x128 one-tile grids without
- * the split-K tail of their last round (1, default: conv_x3_tail_kernel<128, P>). */
-void hkp_debug_x3_tail128(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

@@ -668,49 +668,6 @@ def test_split_k_tail(cuda_device, case):
         assert torch.equal(y1, y2), tile                       # counters back at zero, fixed order
 
 
-TAIL128_CASES = [
-    # (precision, n, h, w, cin, cout, k, stride, pad, dil, tile policy): 256x128 grids with a partial last round
-    ("x3", 32, 60, 80, 128, 128, 3, 1, 1, 1, 0),    # C2 layer2: 600 tiles = 2 rounds + 88 (S = 2)
-    ("x3", 33, 60, 80, 128, 128, 3, 1, 1, 1, 0),    # 619 tiles, ragged M: 2 rounds + 107 (S = 2)
-    ("f16", 16, 60, 80, 512, 128, 1, 1, 0, 1, 12),  # plain fp16 under AUTO_A3 (AUTO plans DUO here)
-]
-
-
-@pytest.mark.parametrize("case", TAIL128_CASES)
-def test_split_k_tail_128(cuda_device, case):
-    """The split-K tail on 256x128 one-tile grids of >= 2 full rounds
-    (conv_x3_tail_kernel<128, P>): the
-    values of the same grid without it (hkp_debug_x3_tail128 0) to fp32 summation
-    order — not the same bits, so the tail did run — the same BN partials, and run to
-    run bit-identical."""
-    from hkp import ops
-    from hkp._lib import lib
-    prec, n, h, w, cin, cout, k, st, pad, dil, tile = case
-    d = cuda_device
-    g = torch.Generator(device=d).manual_seed(31)
-    x = torch.relu(torch.randn(n, h, w, cin, device=d, generator=g))
-    wt = torch.randn(cout, k, k, cin, device=d, generator=g) * (2.0 / (k * k * cout)) ** 0.5
-    if prec == "f16":
-        xs, wp, fwd = x.half(), ops.weight_pack_f16(wt), ops.conv2d_fwd_f16
-    else:
-        ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
-        xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
-        wp, fwd = ops.weight_pack_x3(wt), ops.conv2d_fwd_x3
-    try:
-        lib().hkp_debug_x3_tail128(0)
-        y0, p0 = fwd(xs, wp, st, pad, dil, tile=tile)
-    finally:
-        lib().hkp_debug_x3_tail128(1)
-    y1, p1 = fwd(xs, wp, st, pad, dil, tile=tile)
-    y2, p2 = fwd(xs, wp, st, pad, dil, tile=tile)
-    tol = 2.0 ** -10 if prec == "f16" else 4e-6
-    assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item()
-    assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
-    assert torch.equal(y1, y2) and torch.equal(p1, p2)
-    if prec != "f16":                                   # fp16 outputs may round the tail's sums to the same bits
-        assert not torch.equal(y1, y0)
-
-
 def test_split_k_tail_dgrad_back_to_back(cuda_device):
     """The overlapped dgrad's policy (HKP_TILE_256_TAIL, with the stream-K
     workspace) on a stride-1 shape whose last round is partial (300 tiles = one

@@ -29,7 +29,7 @@
 #   stem4     the 4-wave stem patch form (removed after this run): tests, phase clocks, C2 / C4 A/B
 #   multi     the multi-round split-K tail: tail tests, per-conv A/B (hkp_debug_x3_multi_tail 0 / 1),
 #             B=8 shard / C2 / C3-train A/B in one process
-#   tail128   the split-K tail on 256x128 grids: tests, per-conv and C2 / C3 / C4 A/B in one process
+#   tail128   the split-K tail on 256x128 grids (removed after this run): tests, C2 / C3 / C4 A/B
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
