@@ -30,6 +30,7 @@
 #   multi     the multi-round split-K tail: tail tests, per-conv A/B (hkp_debug_x3_multi_tail 0 / 1),
 #             B=8 shard / C2 / C3-train A/B in one process
 #   tail128   the split-K tail on 256x128 grids (removed after this run): tests, C2 / C3 / C4 A/B
+#   fin       the one-pass BN finalize: BN tests, B=8 / C2 / C4 / C3 A/B against the two-pass kernel
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -221,6 +222,16 @@ tail128)
     timeout -k 10 400 python -u tools/infer_ab.py "tail128=0" "" "tail128=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "tail128=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "tail128=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+fin)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_backward.py \
+        tests/test_gpu_forward.py tests/test_gpu_syncbn.py tests/test_gpu_gram.py > $O/pytest_fin.log 2>&1
+    echo "pytest fin: $(tail -1 $O/pytest_fin.log)"
+    timeout -k 10 400 python -u tools/infer_ab.py "fin2=1" "" --batch 8 --rounds 9 --iters 20 > $O/ab_b8.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "fin2=1" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "fin2=1" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "fin2=1" "" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
