@@ -23,99 +23,14 @@ __device__ __forceinline__ void bn_rank_stats_store(int c, int C, long count, do
     if (c == 0) stats[2 * C] = (double)count;
 }
 
-// CPB channels per block (partials_cpb); deterministic fixed-order fp64 merge.
+// CPB channels per block (partials_cpb); deterministic fixed-order fp64 merge
 // NT threads per block: 256, or 1024 for long tile lists (the stem's 19,200
 // tiles at C2: per-thread load chains of 75 tiles took 75 us with 256 threads).
-// One pass (round 5): each lane loads its tiles t = tl, tl + TL, ... (16 in
-// flight) and folds them in that order into (n, mean, M2) by Chan's pairwise
-// formula, n = na + nb, d = mb - ma, mean = ma + d nb/n, M2 = M2a + M2b + d^2 na nb/n;
-// the lanes of a channel then merge the same way — xor-butterfly inside the wave,
-// the waves in index order through LDS.  The two-pass form (global mean, then
-// every tile's M2 about it) read the partials twice behind two block
-// reductions: 6-14 us per BN layer, latency, not bytes, at ~36 layers a step.
-struct ChanD {
-    double n, mean, m2;
-};
-__device__ __forceinline__ ChanD chan_merge(const ChanD& a, const ChanD& b) {
-    if (b.n == 0.0) return a;
-    if (a.n == 0.0) return b;
-    const double n = a.n + b.n, d = b.mean - a.mean;
-    return ChanD{n, a.mean + d * (b.n / n), a.m2 + b.m2 + d * d * (a.n * b.n / n)};
-}
-
+// (A one-pass form — each lane's tiles folded by Chan's pairwise merge, the lanes
+// merged the same way — measured no faster: B=8 shard 1494 -> 1484 img/s, C2 / C4 /
+// C3 unchanged; profiles/r05_fin_*.)
 template <int CPB, int NT = 256>
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
-                                                         const float* __restrict__ part, const float* gamma,
-                                                         const float* beta, float momentum, float eps, float* rmean,
-                                                         float* rvar, int64_t* nbt, float* ss, float* mi,
-                                                         double* stats) {
-    constexpr int TL = NT / CPB, NW = NT / 64, B = 8;
-    __shared__ double red[3][NW][CPB];
-    const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
-    const bool ok = c < C;
-    const long full = count / tile_rows;                         // tiles of tile_rows rows (the last may be short)
-    ChanD st{0.0, 0.0, 0.0};
-    if (ok)
-        for (long t0 = tl; t0 < tiles; t0 += (long)B * TL) {
-            // a batch of B tiles: its mean, then its M2 about it (Chan's two-pass form
-            // on the registers), folded into the lane's running state
-            float2 v[B];
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                const long t = t0 + (long)j * TL;
-                v[j] = t < tiles ? *(const float2*)(part + (t * C + c) * 2) : make_float2(0.f, 0.f);
-            }
-            double nb = 0.0, sb = 0.0;
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                const long t = t0 + (long)j * TL;
-                if (t < tiles) {
-                    nb += (double)(t < full ? tile_rows : count - t * tile_rows);
-                    sb += (double)v[j].x;
-                }
-            }
-            if (nb == 0.0) continue;
-            const double mb = sb / nb;
-            double qb = 0.0;
-#pragma unroll
-            for (int j = 0; j < B; ++j) {
-                const long t = t0 + (long)j * TL;
-                if (t < tiles) {
-                    const double n_t = (double)(t < full ? tile_rows : count - t * tile_rows);
-                    const double dm = (double)v[j].x / n_t - mb;
-                    qb += (double)v[j].y + n_t * dm * dm;
-                }
-            }
-            st = chan_merge(st, ChanD{nb, mb, qb});
-        }
-    // lanes of one channel (stride CPB) inside the wave: lane l merges lane l ^ o's
-    // state after its own (lower lane first), so every lane holds the same bits
-#pragma unroll
-    for (int o = CPB; o < 64; o <<= 1) {
-        const ChanD p{__shfl_xor(st.n, o), __shfl_xor(st.mean, o), __shfl_xor(st.m2, o)};
-        const bool lo = ((threadIdx.x & 63) & o) == 0;
-        st = lo ? chan_merge(st, p) : chan_merge(p, st);
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane < CPB) {
-        red[0][wid][lane] = st.n;
-        red[1][wid][lane] = st.mean;
-        red[2][wid][lane] = st.m2;
-    }
-    __syncthreads();
-    if (threadIdx.x < CPB && ok) {
-        ChanD a{red[0][0][cl], red[1][0][cl], red[2][0][cl]};
-#pragma unroll
-        for (int w = 1; w < NW; ++w) a = chan_merge(a, ChanD{red[0][w][cl], red[1][w][cl], red[2][w][cl]});
-        if (stats) bn_rank_stats_store(c, C, count, a.mean, a.m2, stats);
-        else bn_fin_store(c, C, count, a.mean, a.m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
-    }
-}
-
-// A/B (hkp_debug_bn_fin_twopass): the round-4 two-pass form (global mean, then
-// every tile's M2 about it, two block reductions)
-template <int CPB, int NT = 256>
-__global__ __launch_bounds__(NT) void bn_finalize2_kernel(int C, long count, long tiles, int tile_rows,
                                                          const float* __restrict__ part, const float* gamma,
                                                          const float* beta, float momentum, float eps, float* rmean,
                                                          float* rvar, int64_t* nbt, float* ss, float* mi,
@@ -506,9 +421,6 @@ static inline int grid_for(long work, int block = 256, long cap = 256L * 16) {
 
 using namespace hkp;
 
-static int g_bn_fin_twopass = 0;                       // hkp_debug_bn_fin_twopass
-extern "C" void hkp_debug_bn_fin_twopass(int32_t on) { g_bn_fin_twopass = on != 0; }
-
 // The one-kernel (fin_one) and two-level (fin_two) merges of the tile partials:
 // scale/shift (+ running stats), or (stats != null) the rank's SyncBN statistics.
 static int fin_one(const char* who, int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
@@ -522,14 +434,9 @@ static int fin_one(const char* who, int32_t c, int64_t count, int64_t tiles, int
                   "%s: tiles/tile_rows inconsistent with count", who);
     const int cpb = partials_cpb(c);
 #define HKP_FIN1(CPB, NT)                                                                                          \
-    if (g_bn_fin_twopass)                                                                                          \
-        hipLaunchKernelGGL((bn_finalize2_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), \
-                           c, (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps,            \
-                           running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd, stats);        \
-    else                                                                                                           \
-        hipLaunchKernelGGL((bn_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), \
-                           c, (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps,            \
-                           running_mean, running_var, num_batches_tracked, scale_shift, mean_invstd, stats)
+    hipLaunchKernelGGL((bn_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), c, \
+                       (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,      \
+                       running_var, num_batches_tracked, scale_shift, mean_invstd, stats)
 #define HKP_FIN(CPB)                                  \
     if (tiles >= 4096) { HKP_FIN1(CPB, 1024); } \
     else { HKP_FIN1(CPB, 256); }

@@ -78,7 +78,6 @@ SIGNATURES = {
     "hkp_debug_x3_stagger": (None, [_I32]),
     "hkp_debug_x3_split_tail": (None, [_I32]),
     "hkp_debug_stem_pair": (None, [_I32]),
-    "hkp_debug_bn_fin_twopass": (None, [_I32]),
     "hkp_debug_x3_store": (None, [_I32]),
     "hkp_debug_duo_stagger": (None, [_I32]),
     "hkp_debug_x3_prio": (None, [_I32]),

@@ -260,9 +260,6 @@ void hkp_debug_x3_prio(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
-/* Debug / A/B (tools/ only, not thread-safe): nonzero runs hkp_bn_finalize / hkp_bn_stats
- * as the round-4 two-pass kernel instead of the one-pass Chan merge. */
-void hkp_debug_bn_fin_twopass(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;

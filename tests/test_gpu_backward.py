@@ -505,14 +505,3 @@ def test_bn_finalize_two_level(cuda_device, c, rows):
     # deterministic run to run
     ss2, mi2 = ops.bn_finalize(part, rows, gamma, beta, two_level_tiles=129)
     assert torch.equal(ss2, ss) and torch.equal(mi2, mi)
-    # the one-kernel merge (one pass, Chan per lane) vs the round-4 two-pass kernel
-    # (hkp_debug_bn_fin_twopass), and run to run
-    from hkp._lib import lib
-    ss1, mi1 = ops.bn_finalize(part, rows, gamma, beta, two_level_tiles=1 << 40)
-    assert torch.equal(ss1, outs[0][0]) and torch.equal(mi1, outs[0][1])
-    try:
-        lib().hkp_debug_bn_fin_twopass(1)
-        ss0, mi0 = ops.bn_finalize(part, rows, gamma, beta, two_level_tiles=1 << 40)
-    finally:
-        lib().hkp_debug_bn_fin_twopass(0)
-    assert torch.allclose(ss0, ss1, rtol=2.5e-7, atol=0) and torch.allclose(mi0, mi1, rtol=2.5e-7, atol=0)

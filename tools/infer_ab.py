@@ -20,8 +20,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 
-KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0),
-         "fin2": ("hkp_debug_bn_fin_twopass", 0)}
+KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0)}
 
 
 def knobs(form):

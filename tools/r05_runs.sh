@@ -30,7 +30,7 @@
 #   multi     the multi-round split-K tail: tail tests, per-conv A/B (hkp_debug_x3_multi_tail 0 / 1),
 #             B=8 shard / C2 / C3-train A/B in one process
 #   tail128   the split-K tail on 256x128 grids (removed after this run): tests, C2 / C3 / C4 A/B
-#   fin       the one-pass BN finalize: BN tests, B=8 / C2 / C4 / C3 A/B against the two-pass kernel
+#   fin       the one-pass BN finalize (removed after this run): BN tests, B=8 / C2 / C4 / C3 A/B
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
