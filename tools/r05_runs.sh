@@ -1,6 +1,8 @@
 #!/bin/bash
 # The round-5 GPU recipes behind DESIGN's numbers, one per subcommand (each one
-# gpurun call; outputs under gpurun_out/<name>/):
+# gpurun call; outputs under gpurun_out/<name>/).  The recipes of variants removed
+# after their measurement (frac, multi, tail128, stem4, fin) stay as the record of
+# how those profiles were made; their knobs no longer exist, so they do not re-run.
 #   check     GPU suite + the default bench line (C2 + the north_star batch-64 leg)
 #   duo       the DUO body (plain-fp16 256x128, two blocks per CU): its parity tests,
 #             per-conv A/B vs the planner (tools/conv_ab.py), C4 A/B in one process
@@ -21,13 +23,14 @@
 #   a3p       the persistent A3 body (HKP_TILE_A3P): parity tests, per-conv and C4 / C2 A/B
 #   c5        C5 shard (R50-8s K=8 1280x960 B=32 training step): bench line, kernel
 #             trace stats, per-launch listing, PMC passes over every kernel
-#   frac      the fractional A3 tail (conv_x3_a3sk_kernel): its parity tests, per-conv A/B
-#             (hkp_debug_x3_frac_tail 0 / 1 / 2), C2 / B=8 shard / C4 / C3-train A/B in one process
+#   frac      the fractional A3 tail (conv_x3_a3sk_kernel; removed after this run): its parity tests,
+#             per-conv A/B (hkp_debug_x3_frac_tail 0 / 1 / 2), C2 / B=8 shard / C4 / C3-train A/B
 #   rehearse8 bench.py --gpus 4 and --gpus 8 as gloo rehearsals on the one GPU (the driver's
 #             scaling run's relaunch, rendezvous, north_star and train legs; not a measurement)
 #   stem      per-block phase clocks of the stem conv (C2 batch 32, C4 batch 128)
 #   stem4     the 4-wave stem patch form (removed after this run): tests, phase clocks, C2 / C4 A/B
-#   multi     the multi-round split-K tail: tail tests, per-conv A/B (hkp_debug_x3_multi_tail 0 / 1),
+#   multi     the multi-round split-K tail (removed after this run): tail tests, per-conv A/B
+#             (hkp_debug_x3_multi_tail 0 / 1),
 #             B=8 shard / C2 / C3-train A/B in one process
 #   tail128   the split-K tail on 256x128 grids (removed after this run): tests, C2 / C3 / C4 A/B
 #   fin       the one-pass BN finalize (removed after this run): BN tests, B=8 / C2 / C4 / C3 A/B
