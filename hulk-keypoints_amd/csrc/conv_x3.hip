@@ -1864,6 +1864,12 @@ static bool stem_patch_shape(int ho, int wo, int k) {
     return !g_stem_pair && ho % STEM_PH == 0 && wo % STEM_PW == 0 && k % 64 == 0;
 }
 
+// SRC: 0 the padded hi | lo planes of hkp_stem_pack_x3 (DMA), 1 the fp32 NCHW image,
+// 2 the uint8 NHWC (BGR) batch — for 1 / 2 the patch is built in LDS from the image
+// itself (hkp_stem_pack_x3's arithmetic: x = u8 / 255 for uint8, hi = f16(x),
+// lo = f16(x - hi), zeros outside the image and in channels C..3), so the planes
+// are never written (a.H / a.W / a.C: the image's height, width, channels)
+template <int SRC>
 __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[STEM_LDS];
     constexpr int BM = 256, BN = 64, WM = 4, WN = 2, ROW = 128;
@@ -1891,15 +1897,43 @@ __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
         const int Lc = (lane % 8) ^ ((n >> 1) & 7);
         glds16(a.ws + ((long)(n0 + n) * 7 + r) * 64 + Lc * 8, smem + 8 * (w * 7 + i) * ROW);
     }
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
-    const long prow0 = ((long)img * a.H + 2 * h0) * a.W + 2 * w0;   // padded pixel of patch (0, 0)
+    if constexpr (SRC == 0) {
+        const _Float16* zero = (const _Float16*)g_x3_zero_line;
+        const long prow0 = ((long)img * a.H + 2 * h0) * a.W + 2 * w0;   // padded pixel of patch (0, 0)
 #pragma unroll
-    for (int i = 0; i < STEM_PGA; ++i) {
-        const int c = 512 * i + 64 * w + lane;                   // instruction i of wave w: chunks 512 i + 64 w + lane
-        const int pl = c >= STEM_PLANE / 16 ? 1 : 0, cc = c - pl * (STEM_PLANE / 16);
-        const int pr = cc / (STEM_PC / 2), pc = cc - pr * (STEM_PC / 2);
-        const _Float16* src = c < STEM_PCH ? a.xs + pl * a.plane + (prow0 + (long)pr * a.W) * 4 + pc * 8 : zero;
-        glds16(src, smem + STEM_BBYTES + (512 * i + 64 * w) * 16);
+        for (int i = 0; i < STEM_PGA; ++i) {
+            const int c = 512 * i + 64 * w + lane;               // instruction i of wave w: chunks 512 i + 64 w + lane
+            const int pl = c >= STEM_PLANE / 16 ? 1 : 0, cc = c - pl * (STEM_PLANE / 16);
+            const int pr = cc / (STEM_PC / 2), pc = cc - pr * (STEM_PC / 2);
+            const _Float16* src = c < STEM_PCH ? a.xs + pl * a.plane + (prow0 + (long)pr * a.W) * 4 + pc * 8 : zero;
+            glds16(src, smem + STEM_BBYTES + (512 * i + 64 * w) * 16);
+        }
+    } else {
+        // padded pixel (pr, pc) of the patch = image pixel (2 h0 + pr - 3, 2 w0 + pc - 3)
+        for (int px = tid; px < STEM_PR * STEM_PC; px += 512) {
+            const int pr = px / STEM_PC, pc = px - pr * STEM_PC;
+            const int h = 2 * h0 + pr - 3, wi = 2 * w0 + pc - 3;
+            const bool in = (unsigned)h < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (in && c < a.C) {
+                    if constexpr (SRC == 2)
+                        v[c] = __fdiv_rn((float)((const uint8_t*)a.xs)[(((long)img * a.H + h) * a.W + wi) * a.C + c], 255.f);
+                    else
+                        v[c] = ((const float*)a.xs)[(((long)img * a.C + c) * a.H + h) * a.W + wi];
+                }
+            }
+            h16x4 hv, lv;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const _Float16 hh = (_Float16)v[c];
+                hv[c] = hh;
+                lv[c] = (_Float16)(v[c] - (float)hh);
+            }
+            *(h16x4*)(smem + STEM_BBYTES + px * 8) = hv;
+            *(h16x4*)(smem + STEM_BBYTES + STEM_PLANE + px * 8) = lv;
+        }
     }
 
     // ---- fragment addressing ----
@@ -4218,7 +4252,7 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR) {
         // the patch body (patch-divisible outputs: 480x640 and 960x1280 images);
         // HKP_TILE_64_PAIR keeps the one-tile stem (A/B, parity tests)
-        hipLaunchKernelGGL(conv_x3_stem_patch_kernel, dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
+        hipLaunchKernelGGL(conv_x3_stem_patch_kernel<0>, dim3(m_tiles * a.n_tiles), dim3(512), 0, as_stream(stream), a);
         HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
         return HKP_OK;
     }
@@ -4227,6 +4261,38 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     hipLaunchKernelGGL((conv_x3_kernel<64, true, true, 16, false, 3>), dim3(m_tiles * a.n_tiles), dim3(512), 0,
                        as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3");
+    return HKP_OK;
+}
+
+// the stem straight from the image (conv_x3_stem_patch_kernel<1 | 2>): no packed
+// planes, where the patch body takes the shape (hkp_stem_x3_image_ok)
+extern "C" int32_t hkp_stem_x3_image_ok(const hkp_conv_desc* d) {
+    int ho, wo;
+    if (!stem_x3_shape(d) || hkp_conv_out_hw(d, &ho, &wo) != HKP_OK) return 0;
+    return stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR && (long)d->n * ho * wo < (1L << 31) ? 1 : 0;
+}
+
+extern "C" int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* image, int32_t image_u8,
+                                            const uint16_t* w_split, const float* w_inv_scale, float* y,
+                                            float* stat_partials, hkp_stream_t stream) {
+    HKP_CHECK_ARG(hkp_stem_x3_image_ok(d), "hkp_conv2d_fwd_stem_x3_image: shape not on the patch body "
+                                           "(hkp_stem_x3_image_ok; use hkp_stem_pack_x3 + hkp_conv2d_fwd_stem_x3)");
+    HKP_CHECK_ARG(image && w_split && y, "hkp_conv2d_fwd_stem_x3_image: null tensor");
+    int ho, wo;
+    hkp_conv_out_hw(d, &ho, &wo);
+    X3Args a;
+    a.xs = (const _Float16*)image; a.ws = (const _Float16*)w_split; a.wscale = w_inv_scale;
+    a.y = y; a.part = stat_partials; a.amax = nullptr; a.add = nullptr;
+    a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = 7; a.S = 1;
+    a.stride = 2; a.pad = 0; a.dil = 1; a.Ho = ho; a.Wo = wo;
+    a.M = d->n * ho * wo; a.cch = 1; a.RS = 7; a.nks = 7; a.plane = 0;
+    a.n_tiles = d->k / 64;
+    a.stamps = g_x3_stamps;
+    a.st_kind = g_x3_store;
+    const dim3 grid((unsigned)(((long)a.M + 255) / 256 * a.n_tiles));
+    if (image_u8) hipLaunchKernelGGL(conv_x3_stem_patch_kernel<2>, grid, dim3(512), 0, as_stream(stream), a);
+    else hipLaunchKernelGGL(conv_x3_stem_patch_kernel<1>, grid, dim3(512), 0, as_stream(stream), a);
+    HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3_image");
     return HKP_OK;
 }
 
@@ -4267,8 +4333,12 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
         }
         case HKP_KOP_STEM_X3:
             if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR)
-                return snprintf(buf, len, "conv_x3_stem_patch_kernel");
+                return snprintf(buf, len, "conv_x3_stem_patch_kernel<0>");
             return x3_kernel_name(X3_STEM, true, 3, buf, len);
+        case HKP_KOP_STEM_X3_IMAGE:
+        case HKP_KOP_STEM_X3_IMAGE_U8:
+            HKP_CHECK_ARG(hkp_stem_x3_image_ok(d), "hkp_conv_kernel_name: the image stem needs the patch body's shape");
+            return snprintf(buf, len, "conv_x3_stem_patch_kernel<%d>", op == HKP_KOP_STEM_X3_IMAGE ? 1 : 2);
         case HKP_KOP_WGRAD_X3: {
             HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv_kernel_name: wgrad needs Cout%%64==0");
             int sp, mps, ka, rt;

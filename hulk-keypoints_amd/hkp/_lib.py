@@ -33,7 +33,7 @@ class ConvDesc(ctypes.Structure):
  HKP_TILE_DUO, HKP_TILE_A3P) = range(15)
 # hkp_conv_kernel_name ops
 HKP_KOP_FWD_X3, HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3, HKP_KOP_FWD_X3_W16, \
-    HKP_KOP_FWD_X3_X16 = range(7)
+    HKP_KOP_FWD_X3_X16, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8 = range(9)
 HKP_X3_W16, HKP_X3_ALL, HKP_X3_X16 = 2, 3, 4          # hkp_conv2d_fwd_x3_products product sets
 
 
@@ -109,6 +109,8 @@ SIGNATURES = {
     "hkp_heat_overlay": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P, _P]),
     "hkp_stem_weight_pack_x3": (ctypes.c_int, [_I32, _I32, _P, _P, _P, _P]),
     "hkp_conv2d_fwd_stem_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P]),
+    "hkp_stem_x3_image_ok": (_I32, [_CD]),
+    "hkp_conv2d_fwd_stem_x3_image": (ctypes.c_int, [_CD, _P, _I32, _P, _P, _P, _P, _P]),
     "hkp_split_pack_x3": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P]),
     "hkp_weight_flip_pack_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P]),
     "hkp_conv2d_bwd_data_x3": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),

@@ -9,7 +9,7 @@ import ctypes
 import torch
 
 from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
-                   HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
+                   HKP_KOP_STEM_X3, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
                    HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, ConvDesc, HkpError, call)
 
 CONV_TILE_ROWS = 128  # BM of conv_fwd.hip (rows per BN statistic tile)
@@ -421,12 +421,19 @@ def stem_weight_pack_x3(w):
     return PackedWeight(out, sc)
 
 
-def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0):
+# A/B (tools/infer_ab.py stem_img=0): the image-direct stem off by default in this process
+STEM_IMAGE_DIRECT = True
+
+
+def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0, image_direct=None):
     """f16x3 stem conv (7x7/s2/p3) → NHWC fp32 y (+ BN partials).  x: the NCHW fp32
     image, or the uint8 NHWC (BGR) batch cv2.imread gives — ToTensor's /255 is then
-    fused into the stem's operand pack.  tile: 0 = the patch body
+    fused into the stem's operand split.  tile: 0 = the patch body
     where the output tiles into 8 x 32 patches, HKP_TILE_64_PAIR = the one-tile
-    stem (the BN partials then group raster-order rows instead of patches)."""
+    stem (the BN partials then group raster-order rows instead of patches).  On the
+    patch body the image is split per tile in LDS (hkp_conv2d_fwd_stem_x3_image:
+    no packed planes in HBM) unless image_direct=False (pack + planes, the same
+    bits)."""
     from ._lib import lib
     ws, wsc = wp
     u8 = x.dtype == torch.uint8
@@ -438,20 +445,31 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0):
         n, c, h, wd = x.shape
     d = ConvDesc(n, h, wd, c, k, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW, tile)
     ho, wo = conv_out_hw(h, wd, 7, 7, 2, 3, 1)
-    xs = torch.empty(lib().hkp_stem_pack_x3_elems(ctypes.byref(d)), device=x.device, dtype=torch.float16)
-    call("hkp_stem_pack_x3_u8" if u8 else "hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())
     y = torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
     part = _stat_partials(n * ho * wo, k, x.device, part_out, "conv2d_fwd_stem_x3.part_out") if stats else None
+    if image_direct is None:
+        image_direct = STEM_IMAGE_DIRECT
+    if image_direct and lib().hkp_stem_x3_image_ok(ctypes.byref(d)):
+        xin = x.contiguous()
+        op = HKP_KOP_STEM_X3_IMAGE_U8 if u8 else HKP_KOP_STEM_X3_IMAGE
 
-    def launch():
-        call("hkp_conv2d_fwd_stem_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
-             _stream())
+        def launch():
+            call("hkp_conv2d_fwd_stem_x3_image", ctypes.byref(d), _ptr(xin), 1 if u8 else 0, _ptr(ws), _ptr(wsc),
+                 _ptr(y), _ptr(part), _stream())
+        nbytes = float(xin.numel() * xin.element_size()) + 2.0 * ws.numel() + 4.0 * y.numel()
+    else:
+        xs = torch.empty(lib().hkp_stem_pack_x3_elems(ctypes.byref(d)), device=x.device, dtype=torch.float16)
+        call("hkp_stem_pack_x3_u8" if u8 else "hkp_stem_pack_x3", ctypes.byref(d), _ptr(x), _ptr(xs), _stream())
+        op = HKP_KOP_STEM_X3
 
+        def launch():
+            call("hkp_conv2d_fwd_stem_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
+                 _stream())
+        nbytes = 2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel()
     if _observer is None:
         launch()
     else:
-        _observer(kernel_name(d, HKP_KOP_STEM_X3), 2.0 * n * ho * wo * k * 49 * c,
-                  2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
+        _observer(kernel_name(d, op), 2.0 * n * ho * wo * k * 49 * c, nbytes, launch)
     return y, part
 
 

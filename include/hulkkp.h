@@ -232,6 +232,8 @@ int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, co
 #define HKP_KOP_WGRAD_X3 4
 #define HKP_KOP_FWD_X3_W16 5   /* hkp_conv2d_fwd_x3_products(HKP_X3_W16) */
 #define HKP_KOP_FWD_X3_X16 6   /* hkp_conv2d_fwd_x3_products(HKP_X3_X16) */
+#define HKP_KOP_STEM_X3_IMAGE 7     /* hkp_conv2d_fwd_stem_x3_image, fp32 NCHW image */
+#define HKP_KOP_STEM_X3_IMAGE_U8 8  /* hkp_conv2d_fwd_stem_x3_image, uint8 NHWC batch */
 int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf, int32_t len);
 
 /* Debug (tools/ only, not thread-safe): one-tile forward conv launches record
@@ -445,6 +447,14 @@ int hkp_stem_weight_pack_x3(int32_t k, int32_t c, const float* w_oihw, uint16_t*
                             hkp_stream_t stream);
 int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_split, const uint16_t* w_split,
                            const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream);
+/* The stem straight from the image where the patch body takes the shape (output
+ * height % 8 == 0, width % 32 == 0, d->tile != HKP_TILE_64_PAIR: hkp_stem_x3_image_ok
+ * returns 1): the fp32 NCHW image (image_u8 = 0) or the uint8 NHWC batch (1), split
+ * in LDS per 8x32-pixel tile with hkp_stem_pack_x3's arithmetic — the same y and
+ * partials bit for bit, without writing or reading the packed planes. */
+int32_t hkp_stem_x3_image_ok(const hkp_conv_desc* d);
+int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* image, int32_t image_u8, const uint16_t* w_split,
+                                 const float* w_inv_scale, float* y, float* stat_partials, hkp_stream_t stream);
 
 /* f16x3 backward on packed split operands (the layout of hkp_conv2d_fwd_x3):
  *   hkp_split_pack_x3:       x * 2^e → packed split [n/c][c/32][64]; 2^e from

@@ -183,11 +183,17 @@ def test_kernel_name_query():
     with pytest.raises(_lib.HkpError, match="tile policy"):
         ops.kernel_name(d, _lib.HKP_KOP_FWD_X3)
     stem = _lib.ConvDesc(32, 480, 640, 3, 64, 7, 7, 2, 3, 1, _lib.HKP_LAYOUT_NCHW)
-    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3) == "conv_x3_stem_patch_kernel"       # 240x320: 8x32 patches
+    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3) == "conv_x3_stem_patch_kernel<0>"    # 240x320: 8x32 patches
+    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3_IMAGE) == "conv_x3_stem_patch_kernel<1>"  # straight from the image
+    assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3_IMAGE_U8) == "conv_x3_stem_patch_kernel<2>"
+    assert _lib.lib().hkp_stem_x3_image_ok(ctypes.byref(stem)) == 1
     stem.tile = _lib.HKP_TILE_64_PAIR
     assert ops.kernel_name(stem, _lib.HKP_KOP_STEM_X3) == "conv_x3_kernel<64, true, true, 16, false, 3>"
     odd = _lib.ConvDesc(2, 120, 160, 3, 64, 7, 7, 2, 3, 1, _lib.HKP_LAYOUT_NCHW)              # 60x80: no patch tiling
     assert ops.kernel_name(odd, _lib.HKP_KOP_STEM_X3) == "conv_x3_kernel<64, true, true, 16, false, 3>"
+    assert _lib.lib().hkp_stem_x3_image_ok(ctypes.byref(odd)) == 0
+    with pytest.raises(_lib.HkpError, match="patch body"):
+        ops.kernel_name(odd, _lib.HKP_KOP_STEM_X3_IMAGE)
 
 
 def test_bnin_kernel_eligibility():

@@ -327,14 +327,21 @@ def test_stem_patch_body(cuda_device, shape):
     from hkp._lib import HKP_KOP_STEM_X3, HKP_LAYOUT_NCHW, HKP_TILE_64_PAIR, ConvDesc
     n, c, h, w = shape
     assert ops.kernel_name(ConvDesc(n, h, w, c, 64, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW, 0),
-                           HKP_KOP_STEM_X3) == "conv_x3_stem_patch_kernel"
+                           HKP_KOP_STEM_X3) == "conv_x3_stem_patch_kernel<0>"
     assert ops.kernel_name(ConvDesc(n, h, w, c, 64, 7, 7, 2, 3, 1, HKP_LAYOUT_NCHW, HKP_TILE_64_PAIR),
                            HKP_KOP_STEM_X3).startswith("conv_x3_kernel<64, true, true")
     x = torch.rand(*shape, generator=torch.Generator().manual_seed(5))
     wt = rand(64, c, 7, 7, seed=6, scale=(2.0 / (49 * 64)) ** 0.5)
     xd, wd = x.to(cuda_device), wt.to(cuda_device)
     wp = ops.stem_weight_pack_x3(wd)
-    y, part = ops.conv2d_fwd_stem_x3(xd, wp, 64)
+    y, part = ops.conv2d_fwd_stem_x3(xd, wp, 64)                          # straight from the image
+    yp, partp = ops.conv2d_fwd_stem_x3(xd, wp, 64, image_direct=False)    # packed planes, then the patch body
+    assert torch.equal(y, yp) and torch.equal(part, partp)
+    # the uint8 batch (ToTensor fused): image-direct vs packed, bit for bit
+    img = (x.permute(0, 2, 3, 1) * 255).round().to(torch.uint8).contiguous().to(cuda_device)
+    yu, pu = ops.conv2d_fwd_stem_x3(img, wp, 64)
+    yup, pup = ops.conv2d_fwd_stem_x3(img, wp, 64, image_direct=False)
+    assert torch.equal(yu, yup) and torch.equal(pu, pup)
     y1, part1 = ops.conv2d_fwd_stem_x3(xd, wp, 64, tile=HKP_TILE_64_PAIR)
     assert (y - y1).abs().max().item() <= 4e-6 * y1.abs().max().item()
     y2, _ = ops.conv2d_fwd_stem_x3(xd, wp, 64)

@@ -93,7 +93,7 @@ def _c2_batch_vs_reference(cuda_device, g, inp):
     assert syms and all(s.startswith(("conv_x3_kernel", "conv_x3_a3_kernel", "conv_x3_halo_kernel",
                                       "conv_x3_halo_bnin_kernel", "conv_x3_stem_patch_kernel")) for s in syms), syms
     assert "conv_x3_halo_kernel<3>" in syms and "conv_x3_halo_bnin_kernel<3>" in syms
-    assert "conv_x3_stem_patch_kernel" in syms
+    assert any(s.startswith("conv_x3_stem_patch_kernel") for s in syms)
     print("conv kernels:", {s: "%.1f GFLOP" % (f / 1e9) for s, f in sorted(syms.items(), key=lambda kv: -kv[1])})
     low_err = (low.cpu().numpy() - g["lowres"]).__abs__().max()
     heat_err = (hm[0].cpu().numpy() - g["heat0"]).__abs__().max()

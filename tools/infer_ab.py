@@ -20,7 +20,8 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 
 
-KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0)}
+KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0),
+         "stem_img": (None, 1)}
 
 
 def knobs(form):
@@ -30,7 +31,11 @@ def knobs(form):
 
 def set_knobs(lib, kv):
     for k, v in kv.items():
-        getattr(lib, KNOBS[k][0])(v)
+        if k == "stem_img":                     # a Python-side switch (hkp.ops), not a library knob
+            from hkp import ops
+            ops.STEM_IMAGE_DIRECT = bool(v)
+        else:
+            getattr(lib, KNOBS[k][0])(v)
 
 
 def parse(form):

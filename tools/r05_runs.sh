@@ -34,6 +34,7 @@
 #             B=8 shard / C2 / C3-train A/B in one process
 #   tail128   the split-K tail on 256x128 grids (removed after this run): tests, C2 / C3 / C4 A/B
 #   fin       the one-pass BN finalize (removed after this run): BN tests, B=8 / C2 / C4 / C3 A/B
+#   stemimg   the stem straight from the image (no packed planes): stem / data-path tests, C2 / C4 A/B
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -235,6 +236,14 @@ fin)
     timeout -k 10 400 python -u tools/infer_ab.py "fin2=1" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "fin2=1" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "fin2=1" "" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+stemimg)
+    timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "stem" tests/test_gpu_datapath.py tests/test_gpu_forward.py > $O/pytest_stemimg.log 2>&1
+    echo "pytest stemimg: $(tail -1 $O/pytest_stemimg.log)"
+    timeout -k 10 400 python -u tools/infer_ab.py "stem_img=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "stem_img=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
