@@ -455,8 +455,12 @@ def _bottleneck_tail_gram(block, x, a2, pol):
     if block.downsample is not None:
         yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], x16, pol)
         sd, _ = _bn_params(block.downsample[1], part_d, yd.numel() // yd.shape[-1], pol)
-        return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=yd, res_ss=sd, relu=True, tile=pol.f16_tile_1x1)
-    return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=x16, relu=True, tile=pol.f16_tile_1x1)
+        return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=yd, res_ss=sd, relu=True, tile=_fused_tile(pol))
+    return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=x16, relu=True, tile=_fused_tile(pol))
+
+
+def _fused_tile(pol):
+    return pol.f16_tile_1x1 if pol.f16_tile_fused < 0 else pol.f16_tile_fused
 
 
 def _blocks(resnet):

@@ -61,6 +61,9 @@ class Policy:
     # (0 = the planner)
     f16_tile_1x1: int = 0
     f16_tile_kxk: int = 0
+    # the Bottleneck's conv3 with bn3 + residual + ReLU in its epilogue (C4); -1 =
+    # f16_tile_1x1
+    f16_tile_fused: int = -1
     x3_tile: int = 0
     # training: repeat the last batched weight-pack launch when it repacks every operand
     prepack_plan: bool = True

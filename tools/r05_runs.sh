@@ -35,6 +35,7 @@
 #   tail128   the split-K tail on 256x128 grids (removed after this run): tests, C2 / C3 / C4 A/B
 #   fin       the one-pass BN finalize (removed after this run): BN tests, B=8 / C2 / C4 / C3 A/B
 #   stemimg   the stem straight from the image (no packed planes): stem / data-path tests, C2 / C4 A/B
+#   a3pfused  the persistent A3 body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 14)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -245,6 +246,10 @@ stemimg)
     timeout -k 10 400 python -u tools/infer_ab.py "stem_img=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "stem_img=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+a3pfused)
+    timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_fused=14" "" "f16_tile_fused=14" --backbone resnet50 \
+        --keypoints 8 --batch 128 --precision f16 --rounds 4 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
