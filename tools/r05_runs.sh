@@ -36,6 +36,7 @@
 #   fin       the one-pass BN finalize (removed after this run): BN tests, B=8 / C2 / C4 / C3 A/B
 #   stemimg   the stem straight from the image (no packed planes): stem / data-path tests, C2 / C4 A/B
 #   a3pfused  the persistent A3 body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 14)
+#   duofused  the DUO body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 13)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -249,6 +250,10 @@ stemimg)
     ;;
 a3pfused)
     timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_fused=14" "" "f16_tile_fused=14" --backbone resnet50 \
+        --keypoints 8 --batch 128 --precision f16 --rounds 4 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+duofused)
+    timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_fused=13" "" "f16_tile_fused=13" --backbone resnet50 \
         --keypoints 8 --batch 128 --precision f16 --rounds 4 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
