@@ -1909,27 +1909,37 @@ __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
             glds16(src, smem + STEM_BBYTES + (512 * i + 64 * w) * 16);
         }
     } else {
-        // padded pixel (pr, pc) of the patch = image pixel (2 h0 + pr - 3, 2 w0 + pc - 3)
-        for (int px = tid; px < STEM_PR * STEM_PC; px += 512) {
+        // padded pixel (pr, pc) of the patch = image pixel (2 h0 + pr - 3, 2 w0 + pc - 3);
+        // every load of the thread's pixels issued before the first conversion
+        constexpr int NPX = STEM_PR * STEM_PC, IT = (NPX + 511) / 512;
+        f32x4 v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int px = tid + 512 * it;
             const int pr = px / STEM_PC, pc = px - pr * STEM_PC;
             const int h = 2 * h0 + pr - 3, wi = 2 * w0 + pc - 3;
-            const bool in = (unsigned)h < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-            f32x4 v = {0.f, 0.f, 0.f, 0.f};
+            const bool in = px < NPX && (unsigned)h < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+            v[it] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
                 if (in && c < a.C) {
                     if constexpr (SRC == 2)
-                        v[c] = __fdiv_rn((float)((const uint8_t*)a.xs)[(((long)img * a.H + h) * a.W + wi) * a.C + c], 255.f);
+                        v[it][c] = __fdiv_rn((float)((const uint8_t*)a.xs)[(((long)img * a.H + h) * a.W + wi) * a.C + c], 255.f);
                     else
-                        v[c] = ((const float*)a.xs)[(((long)img * a.C + c) * a.H + h) * a.W + wi];
+                        v[it][c] = ((const float*)a.xs)[(((long)img * a.C + c) * a.H + h) * a.W + wi];
                 }
             }
+        }
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int px = tid + 512 * it;
+            if (px >= NPX) break;
             h16x4 hv, lv;
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
-                const _Float16 hh = (_Float16)v[c];
+                const _Float16 hh = (_Float16)v[it][c];
                 hv[c] = hh;
-                lv[c] = (_Float16)(v[c] - (float)hh);
+                lv[c] = (_Float16)(v[it][c] - (float)hh);
             }
             *(h16x4*)(smem + STEM_BBYTES + px * 8) = hv;
             *(h16x4*)(smem + STEM_BBYTES + STEM_PLANE + px * 8) = lv;
