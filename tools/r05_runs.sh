@@ -37,6 +37,7 @@
 #   stemimg   the stem straight from the image (no packed planes): stem / data-path tests, C2 / C4 A/B
 #   a3pfused  the persistent A3 body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 14)
 #   duofused  the DUO body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 13)
+#   stemimg2  the image-direct stem with its loads batched: stem tests, phase clocks, C2 / C4 A/B
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -255,6 +256,14 @@ a3pfused)
 duofused)
     timeout -k 10 500 python -u tools/infer_ab.py "" "f16_tile_fused=13" "" "f16_tile_fused=13" --backbone resnet50 \
         --keypoints 8 --batch 128 --precision f16 --rounds 4 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+stemimg2)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "stem" > $O/pytest.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest.log)"
+    timeout -k 10 400 python -u tools/infer_ab.py "stem_img=0" "" "stem_img=0" "" --rounds 5 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 500 python -u tools/infer_ab.py "stem_img=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
+        --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
