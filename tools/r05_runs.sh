@@ -38,6 +38,7 @@
 #   a3pfused  the persistent A3 body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 14)
 #   duofused  the DUO body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 13)
 #   stemimg2  the image-direct stem with its loads batched: stem tests, phase clocks, C2 / C4 A/B
+#   a4        the 4-wave A3 body (HKP_TILE_A4): parity tests, per-conv A/B, phase clocks
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -264,6 +265,15 @@ stemimg2)
     timeout -k 10 400 python -u tools/infer_ab.py "stem_img=0" "" "stem_img=0" "" --rounds 5 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "stem_img=0" "" --backbone resnet50 --keypoints 8 --batch 128 \
         --precision f16 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
+    ;;
+a4)
+    timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "a4_equals" > $O/pytest_a4.log 2>&1
+    echo "pytest a4: $(tail -1 $O/pytest_a4.log)"
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 11,15 --rounds 5 --iters 5 \
+        --shapes layer4,layer3,t4,c4_l4_c2,c4_l4_c1,c4_l4_c3,c4_l3_c3 > $O/conv_ab.log 2>&1
+    timeout -k 10 300 python -u tools/x3_stamps.py --tile 15 layer4 c4_l4_c3 > $O/stamps_a4.log 2>&1
+    timeout -k 10 300 python -u tools/x3_stamps.py --tile 11 layer4 c4_l4_c3 > $O/stamps_a3.log 2>&1
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
