@@ -629,98 +629,16 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
     }
 }
 
-// BN tile partials of the 4-wave body (A4): wave wm holds rows [m0 + 128 wm, +128)
-// — exactly one 128-row partial tile — so a column's (sum, M2 about the tile mean)
-// is this wave's alone: per lane over its NI sub-tiles x 4 rows, then the four lane
-// groups merged pairwise by Chan's formula (x3_bn_partials_w's shuffle tree), no LDS.
-template <int NI, int NJ, typename Vec, typename Row, typename Sc>
-__device__ __forceinline__ void x3_bn_partials_w4(const X3Args& a, int m0, int n0, int wm, int wn, int lane, Vec&& vec,
-                                                  Row&& row, Sc&& sc_of) {
-    const int nw = min(128, max(0, a.M - (m0 + 128 * wm)));     // valid rows of this wave (a prefix)
-    if (nw == 0) return;
-    float ls[NJ], lq[NJ], ln;
-    if (nw == 128) {
-        ln = (float)(NI * 4);
-        constexpr float inv = 1.f / (NI * 4);
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            f32x4 s4 = vec(0, j);
-#pragma unroll
-            for (int i = 1; i < NI; ++i) s4 += vec(i, j);
-            const float s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-            const f32x4 mu = {s * inv, s * inv, s * inv, s * inv};
-            f32x4 q4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-                const f32x4 d = vec(i, j) - mu;
-                q4 += d * d;
-            }
-            ls[j] = s;
-            lq[j] = (q4[0] + q4[1]) + (q4[2] + q4[3]);
-        }
-    } else {
-        ln = 0.f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ln += (row(i, r) < a.M) ? 1.f : 0.f;
-        const float linv = ln > 0.f ? 1.f / ln : 0.f;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s += (row(i, r) < a.M) ? vec(i, j)[r] : 0.f;
-            const float mu = s * linv;
-            float q = 0.f;
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float d = vec(i, j)[r] - mu;
-                    q += (row(i, r) < a.M) ? d * d : 0.f;
-                }
-            ls[j] = s;
-            lq[j] = q;
-        }
-    }
-    for (int o = 16; o < 64; o <<= 1) {
-        const float nb = __shfl_xor(ln, o);
-        const float nt = ln + nb;
-        const float f = nt > 0.f ? ln * nb / nt : 0.f;
-        const float ia = ln > 0.f ? 1.f / ln : 0.f, ib = nb > 0.f ? 1.f / nb : 0.f;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const float sb = __shfl_xor(ls[j], o), qb = __shfl_xor(lq[j], o);
-            const float d = sb * ib - ls[j] * ia;
-            ls[j] = ls[j] + sb;
-            lq[j] = (lq[j] + qb) + d * d * f;
-        }
-        ln = nt;
-    }
-    if (lane < 16) {
-        const long tile128 = (long)(m0 >> 7) + wm;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int c = wn * NJ * 16 + j * 16 + lane;
-            const float sc = sc_of(j);
-            a.part[(tile128 * a.K + n0 + c) * 2 + 0] = ls[j] * sc;
-            a.part[(tile128 * a.K + n0 + c) * 2 + 1] = lq[j] * (sc * sc);
-        }
-    }
-}
-
 // fp16 output tile staged in LDS ([256][BN + 8] halves: the 16-B row pad makes
 // the fragment-layout ds_write_b16s conflict-free) and written as whole 16-B
 // row chunks: 8x fewer store instructions than per-element fp16 stores, full
 // 128-B lines — the epilogue of the short-K 1x1 convs of config C4 is most of
 // their time.
-template <int BN, int NT = 512>
+template <int BN>
 __device__ __forceinline__ void x3_store_tile_f16(const X3Args& a, const char* smem, int m0, int n0, int tid) {
     constexpr int CH = BN / 8, PITCH = BN + 8;
 #pragma unroll 4
-    for (int e = tid; e < 256 * CH; e += NT) {
+    for (int e = tid; e < 256 * CH; e += 512) {
         const int row = e / CH, cc = e - row * CH;
         const int m = m0 + row;
         if (m < a.M)
@@ -827,15 +745,12 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
 // wave's reads of t), barrier, [read A frags of t+1] then per column block j:
 // [MFMAs of t with B_j] [refill B_j with t+1's].  NST 2 (256x256; 256x64 pairs):
 // A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
-template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, int NWV, typename Issue, typename IssueA,
+template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, typename Issue, typename IssueA,
           typename IssueB>
 __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
                                                   Issue& issue_next, IssueA& issue_a, IssueB& issue_b) {
-    // NWV: waves per block — 8 (4 x 2, wave tile 64 x BN/2), or 4 (A4: 2 x 2, wave
-    // tile 128 x 128, one wave per SIMD with the accumulators in AGPRs)
-    constexpr int BM = 256, WN = 2, WM = NWV / WN, ROW = 128, NT = 64 * NWV;
-    static_assert(NWV == 8 || (NWV == 4 && A3), "the 4-wave body is the A3 body's");
+    constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
     constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
@@ -1089,22 +1004,14 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
         for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
         if (a.part) {
-            if constexpr (NWV == 4) {
-                x3_bn_partials_w4<UM, UN>(a, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-                                          [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
-            } else {
-                if constexpr (RINGSCR) lds_sync();     // the scratch is the ring
-                x3_bn_partials_w<BN, UM, UN, 16, 16>(
-                    a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-                    [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
-            }
+            if constexpr (RINGSCR) lds_sync();         // the scratch is the ring
+            x3_bn_partials_w<BN, UM, UN, 16, 16>(
+                a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
+                [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
         }
-        X3EpSS eps;
+        const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
         X3Res<BN> eres;
-        if constexpr (NWV == 8) {           // (the 4-wave body takes no fused epilogue: launch_x3)
-            eps = x3_ep_load<BN>(a, n0, tid);
-            if (a.ep_ss) eres = x3_ep_res_load<BN>(a, m0, n0, tid);
-        }
+        if (a.ep_ss) eres = x3_ep_res_load<BN>(a, m0, n0, tid);
         lds_sync();                        // the ring is free
         x3_stamp(a, 3);
         _Float16* t = (_Float16*)smem;
@@ -1119,17 +1026,11 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 for (int r = 0; r < 4; ++r)
                     t[(wm * UM * 16 + i * 16 + 4 * q + r) * PITCH + wn * UN * 16 + j * 16 + r16] =
                         (_Float16)(acc[i][j][r] * sc[j]);
-        if constexpr (NWV == 8) {
-            if (a.ep_ss) x3_ep_store<BN>((float*)(smem + SS_OFF), eps, tid);
-        }
+        if (a.ep_ss) x3_ep_store<BN>((float*)(smem + SS_OFF), eps, tid);
         lds_sync();
         x3_stamp(a, 4);
-        if constexpr (NWV == 8) {
-            if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), eres, m0, n0, tid);
-            else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
-        } else {
-            x3_store_tile_f16<BN, NT>(a, smem, m0, n0, tid);
-        }
+        if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), eres, m0, n0, tid);
+        else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
         x3_stamp(a, 5);
         return;
     }
@@ -1138,15 +1039,10 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 #pragma unroll
     for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
     if (a.part) {
-        if constexpr (NWV == 4) {
-            x3_bn_partials_w4<UM, UN>(a, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-                                      [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
-        } else {
-            if constexpr (RINGSCR) lds_sync();         // the scratch is the ring
-            x3_bn_partials_w<BN, UM, UN, 16, 16>(
-                a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-                [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
-        }
+        if constexpr (RINGSCR) lds_sync();             // the scratch is the ring
+        x3_bn_partials_w<BN, UM, UN, 16, 16>(
+            a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
+            [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
     }
     x3_stamp(a, 3);
     {
@@ -1165,7 +1061,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         lds_sync();                                    // every wave done with the ring and the partials' scratch
 #pragma unroll
         for (int h = 0; h < PASSES; ++h) {
-            if (PASSES == 1 || (wm * UM * 16) / RPP == h) {
+            if (PASSES == 1 || (wm >> 1) == h) {
 #pragma unroll
                 for (int i = 0; i < UM; ++i)
 #pragma unroll
@@ -1178,7 +1074,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
             lds_sync();
             if (!a.add && !a.ost) {
 #pragma unroll 4
-                for (int e = tid; e < RPP * C4; e += NT) {
+                for (int e = tid; e < RPP * C4; e += 512) {
                     const int row = e / C4, c4 = e - row * C4;
                     const int m = m0 + h * RPP + row;
                     if (m < a.M)
@@ -1189,7 +1085,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
                 }
             } else {
 #pragma unroll 2
-                for (int e = tid; e < RPP * C4; e += NT) {
+                for (int e = tid; e < RPP * C4; e += 512) {
                     const int row = e / C4, c4 = e - row * C4;
                     const long off = x3_out_off(a, m0 + h * RPP + row, n0 + c4 * 4);
                     if (off >= 0) {
@@ -1220,7 +1116,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false, int NWV = 8>
+template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -1229,9 +1125,9 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     constexpr int RPI = 1024 / ROW;                // rows per DMA wave-instruction
     constexpr int NST = x3_nst(BN, PAIR);          // LDS ring depth
     constexpr int STAGE = (BM + BN) * ROW;
-    constexpr int GA = BM / RPI / NWV;             // A DMA instructions per wave per stage
+    constexpr int GA = BM / RPI / 8;               // A DMA instructions per wave per stage
     constexpr int GBT = BN / RPI;                  // B DMA instructions per stage (all waves)
-    constexpr int GB = GBT >= NWV ? GBT / NWV : 1; // per wave (GBT < NWV: waves duplicate, same bytes)
+    constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
     static_assert(MFD == 16 || MFD == 32, "bad conv_x3 MFMA shape");
     static_assert(P == 3 || ((P == 1 || P == 2 || P == 4) && !STEM), "bad conv_x3 operand layout");
@@ -1370,8 +1266,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA, NWV>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
-                                                                  tid, issue_next, issue_a, issue_b);
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
+                                                             tid, issue_next, issue_a, issue_b);
         return;
     } else {
     f32x16 acc[TM][TN];
@@ -1621,17 +1517,6 @@ template <int P>
 __global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
     conv_x3_a3_grid<P>(a, smem);
-}
-
-// A4 (HKP_TILE_A4): the A3 body with 4 waves, one per SIMD, each a 128 x 128 wave
-// tile with its 256 accumulators in AGPRs — per K-step and wave 32 fragment reads
-// for 192 MFMAs (A3: 24 for 96, so a third fewer LDS reads per MFMA) and 16 DMA
-// pieces (A3: 8).  One tile per block, no split-K tail, no fused epilogue.
-template <int P>
-__global__ __launch_bounds__(256, 1) void conv_x3_a4_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
-    x3_stamp(a, 0);
-    conv_x3_tile<256, false, false, 16, P, true, 4>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -3719,7 +3604,6 @@ struct X3Choice {
     bool a3 = false;                   // conv_x3_a3_kernel<P> (256x256, 3-stage A ring)
     bool duo = false;                  // conv_x3_duo_kernel<1> (256x128, two 4-wave blocks per CU)
     bool a3p = false;                  // conv_x3_a3p_kernel<P> (persistent A3, next tile's fill in the epilogue)
-    bool a4 = false;                   // conv_x3_a4_kernel<P> (4 waves, 128x128 wave tiles)
 };
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
@@ -3733,14 +3617,6 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
 // DUO (the plain-fp16 256x128 two-blocks-per-CU body) where forced and legal;
 // other operand layouts plan as AUTO
 static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo, int P) {
-    if (policy == HKP_TILE_A4) {
-        if ((P == 1 || P == 3) && k % 256 == 0) {
-            X3Choice c{256, 16, false, false};
-            c.a4 = true;
-            return c;
-        }
-        policy = HKP_TILE_AUTO;
-    }
     if (policy == HKP_TILE_A3P) {
         if ((P == 1 || P == 3) && k % 256 == 0) {
             X3Choice c{256, 16, false, false};
@@ -3816,7 +3692,6 @@ static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int le
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
     if (c.duo) return snprintf(buf, len, "conv_x3_duo_kernel<%d>", P);
     if (c.a3p) return snprintf(buf, len, "conv_x3_a3p_kernel<%d>", P);
-    if (c.a4) return snprintf(buf, len, "conv_x3_a4_kernel<%d>", P);
     if (c.a3) return snprintf(buf, len, "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
@@ -3891,16 +3766,6 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
-    if (c.a4 && (a.add || a.ost || a.in_ss || a.ep_ss)) {
-        launch_x3(k, m_tiles, HKP_TILE_AUTO, P, st, a, ws, ws_bytes);   // forward outputs without a fused epilogue only
-        return;
-    }
-    if (c.a4) {
-        const dim3 g4((unsigned)(m_tiles * a.n_tiles));
-        if (P == 1) hipLaunchKernelGGL(conv_x3_a4_kernel<1>, g4, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(conv_x3_a4_kernel<3>, g4, dim3(256), 0, st, a);
-        return;
-    }
     if (c.a3p && (a.add || a.ost || a.in_ss || (P != 1 && a.ep_ss))) {
         // forward outputs only: other launches plan as AUTO
         launch_x3(k, m_tiles, HKP_TILE_AUTO, P, st, a, ws, ws_bytes);
@@ -4026,7 +3891,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_A4, "%s: unknown tile policy %d", who, d->tile);
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_A3P, "%s: unknown tile policy %d", who, d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8,
                   "%s: tile policy %d is retired (the persistent conv, measured slower)", who, d->tile);
     return HKP_OK;

@@ -91,9 +91,6 @@ typedef struct hkp_conv_desc {
                                          persistent grid (one block per CU) whose epilogue overlaps the
                                          next tile's first DMA stages and stores from registers; other
                                          launches plan as AUTO */
-#define HKP_TILE_A4 15                /* forward, f16x3 or plain fp16, Cout % 256 == 0, no fused epilogue:
-                                         the A3 body with 4 waves of 128x128 wave tiles (one per SIMD);
-                                         A/B (DESIGN round 5) */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);

@@ -872,43 +872,6 @@ A3P_CASES = [
 
 @pytest.mark.parametrize("case", A3P_CASES)
 @pytest.mark.parametrize("prec", ["f16x3", "f16"])
-def test_a4_equals_a3(cuda_device, case, prec):
-    """conv_x3_a4_kernel (HKP_TILE_A4: the A3 body on 4 waves of 128x128 wave
-    tiles) against the one-tile 256x256 body without a split-K tail: the same MFMA
-    sequence per output element, so y is bit-identical; the BN partials (one wave =
-    one 128-row tile here) agree; back to back the same bits."""
-    from hkp import ops
-    from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_TILE_256, HKP_TILE_A4, ConvDesc
-    n, h, w, cin, cout, k, st, pad, dil = case
-    d = cuda_device
-    x = F.relu(rand(n, h, w, cin, seed=211))
-    wt = rand(cout, k, k, cin, seed=212, scale=(2.0 / (k * k * cout)) ** 0.5)
-    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, HKP_TILE_A4)
-    if prec == "f16x3":
-        if cin % 32:
-            pytest.skip("f16x3 needs Cin % 32")
-        xs = ops.bn_apply(x.to(d), torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d), relu=False, split=3,
-                          keep_fp32=False)
-        wp = ops.weight_pack_x3(wt.to(d))
-        assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_a4_kernel<3>"
-        fwd = ops.conv2d_fwd_x3
-    else:
-        if cin % 64:
-            pytest.skip("plain fp16 needs Cin % 64")
-        xs = x.half().to(d)
-        wp = ops.weight_pack_f16(wt.to(d))
-        assert ops.kernel_name(desc, HKP_KOP_FWD_F16) == "conv_x3_a4_kernel<1>"
-        fwd = ops.conv2d_fwd_f16
-    y0, p0 = fwd(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256)
-    y1, p1 = fwd(xs, wp, st, pad, dil, tile=HKP_TILE_A4)
-    y2, p2 = fwd(xs, wp, st, pad, dil, tile=HKP_TILE_A4)
-    assert torch.equal(y1, y0)
-    assert torch.equal(y1, y2) and torch.equal(p1, p2)
-    assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3)
-
-
-@pytest.mark.parametrize("case", A3P_CASES)
-@pytest.mark.parametrize("prec", ["f16x3", "f16"])
 def test_a3p_persistent_equals_a3(cuda_device, case, prec):
     """conv_x3_a3p_kernel (HKP_TILE_A3P: the A3 body as a persistent grid whose
     epilogue prefetches the next tile's first stages and stores from registers)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # The round-5 GPU recipes behind DESIGN's numbers, one per subcommand (each one
 # gpurun call; outputs under gpurun_out/<name>/).  The recipes of variants removed
-# after their measurement (frac, multi, tail128, stem4, fin) stay as the record of
+# after their measurement (frac, multi, tail128, stem4, fin, a4) stay as the record of
 # how those profiles were made; their knobs no longer exist, so they do not re-run.
 #   check     GPU suite + the default bench line (C2 + the north_star batch-64 leg)
 #   duo       the DUO body (plain-fp16 256x128, two blocks per CU): its parity tests,
@@ -38,7 +38,7 @@
 #   a3pfused  the persistent A3 body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 14)
 #   duofused  the DUO body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 13)
 #   stemimg2  the image-direct stem with its loads batched: stem tests, phase clocks, C2 / C4 A/B
-#   a4        the 4-wave A3 body (HKP_TILE_A4): parity tests, per-conv A/B, phase clocks
+#   a4        the 4-wave A3 body (HKP_TILE_A4; removed after this run): parity tests, per-conv A/B, phase clocks
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
