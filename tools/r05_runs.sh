@@ -39,6 +39,8 @@
 #   duofused  the DUO body on C4's fused-epilogue conv3s only (Policy.f16_tile_fused = 13)
 #   stemimg2  the image-direct stem with its loads batched: stem tests, phase clocks, C2 / C4 A/B
 #   a4        the 4-wave A3 body (HKP_TILE_A4; removed after this run): parity tests, per-conv A/B, phase clocks
+#   ups       the upsample + sigmoid + argmax kernel at 4 sub-chunks per block: its tests, kernel
+#             trace of the C2 and C4 benches (upsample_sigmoid_kernel average vs r05_v2)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -274,6 +276,21 @@ a4)
         --shapes layer4,layer3,t4,c4_l4_c2,c4_l4_c1,c4_l4_c3,c4_l3_c3 > $O/conv_ab.log 2>&1
     timeout -k 10 300 python -u tools/x3_stamps.py --tile 15 layer4 c4_l4_c3 > $O/stamps_a4.log 2>&1
     timeout -k 10 300 python -u tools/x3_stamps.py --tile 11 layer4 c4_l4_c3 > $O/stamps_a3.log 2>&1
+    ;;
+ups)
+    timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_forward.py \
+        tests/test_gpu_scale.py tests/test_gpu_dropin.py > $O/pytest_ups.log 2>&1
+    echo "pytest ups: $(tail -1 $O/pytest_ups.log)"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --no-extras \
+        --no-cpu-baseline > $O/prof.log 2>&1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof4 -o run -- python3 bench.py --steps 5 --no-extras \
+        --no-cpu-baseline --backbone resnet50 --keypoints 8 --batch 128 --precision f16 > $O/prof4.log 2>&1
+    for L in prof prof4; do
+        DB=$O/$L/run_results.db
+        [ -f $DB ] || DB=$(ls $O/$L/*/run_results.db 2>/dev/null | head -1)
+        python3 tools/rocpd_stats.py $DB $O/${L}_stats.csv --top 40 > $O/${L}_top.txt
+    done
+    rm -rf $O/prof $O/prof4
     ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
