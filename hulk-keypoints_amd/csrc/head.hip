@@ -329,16 +329,13 @@ __device__ __forceinline__ unsigned long long argmax_key(float p, unsigned idx) 
 
 // grid: x over ceil(H*W/(1024 UPS_G)) chunks — UPS_G sub-chunks of 1024 outputs, 4
 // consecutive outputs per thread in each — y over n*k planes.  (One 1024-output
-// chunk per block, 38,400 blocks of ~4 KB of stores each at C2, wrote at 2.2 TB/s.)
+// chunk per block, 38,400 blocks of ~4 KB of stores each at C2: 70.5 -> 62 us with 4;
+// the kernel is VALU-bound — lerp indices, IEEE expf and division per output — and
+// loading a thread's 3 source columns once for its 4 outputs measured slower,
+// 62 -> 80 us, on its select chains; profiles/r05_ups_*.)
 // ROW4: W % 4 == 0, so a thread's 4 outputs share one output row.
 constexpr int UPS_G = 4;
-// WIN (ROW4, 3 * scale_w < 1: a thread's 4 outputs lie within one low-res pixel, so
-// their columns are a0, a0 + 1, a0 + 2): the 3 columns of both source rows loaded
-// once per thread (6 loads for 4 outputs instead of 16), each output's bilerp on
-// the same values in the same order.
-__device__ __forceinline__ float sel3(const float (&c)[3], int k) { return k == 0 ? c[0] : (k == 1 ? c[1] : c[2]); }
-
-template <bool SIGMOID, bool ROW4, bool WIN = false>
+template <bool SIGMOID, bool ROW4>
 __global__ __launch_bounds__(256) void upsample_sigmoid_kernel(int h, int w, int H, int W, float sh, float sw,
                                                               const float* __restrict__ low, float* __restrict__ heat,
                                                               unsigned long long* __restrict__ keys) {
@@ -356,35 +353,12 @@ __global__ __launch_bounds__(256) void upsample_sigmoid_kernel(int h, int w, int
             const Lerp lh = lerp_index((int)oh, h, H, sh);
             const float* r0 = x + lh.i0 * w;
             const float* r1 = x + lh.i1 * w;
-            if constexpr (WIN) {
-                Lerp lw[4];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) lw[e] = lerp_index((int)ow0 + e, w, W, sw);
-                const int a0 = lw[0].i0;
-                float c0[3], c1[3];
-#pragma unroll
-                for (int t = 0; t < 3; ++t) {
-                    const int col = a0 + t < w - 1 ? a0 + t : w - 1;
-                    c0[t] = r0[col];
-                    c1[t] = r1[col];
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int k0 = lw[e].i0 - a0, k1 = lw[e].i1 - a0;
-                    const float t0 = __builtin_fmaf(sel3(c0, k0), lw[e].l0, sel3(c0, k1) * lw[e].l1);
-                    const float t1 = __builtin_fmaf(sel3(c1, k0), lw[e].l0, sel3(c1, k1) * lw[e].l1);
-                    const float z = __builtin_fmaf(t0, lh.l0, t1 * lh.l1);
-                    v[e] = SIGMOID ? sigmoid_f(z) : z;
-                    best = umax64(best, argmax_key(v[e], base + e));
-                }
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const Lerp lw = lerp_index((int)ow0 + e, w, W, sw);
-                    const float z = bilerp(r0, r1, lh, lw);
-                    v[e] = SIGMOID ? sigmoid_f(z) : z;
-                    best = umax64(best, argmax_key(v[e], base + e));
-                }
+            for (int e = 0; e < 4; ++e) {
+                const Lerp lw = lerp_index((int)ow0 + e, w, W, sw);
+                const float z = bilerp(r0, r1, lh, lw);
+                v[e] = SIGMOID ? sigmoid_f(z) : z;
+                best = umax64(best, argmax_key(v[e], base + e));
             }
             if (heat) *(f32x4*)(heat + (size_t)plane * HW + base) = f32x4{v[0], v[1], v[2], v[3]};
         } else {
@@ -564,13 +538,12 @@ extern "C" int hkp_upsample_sigmoid(int32_t n, int32_t k, int32_t h, int32_t w, 
     const long HW = (long)H * W;
     dim3 grid((unsigned)((HW + 1024 * UPS_G - 1) / (1024 * UPS_G)), (unsigned)nk);
     const bool row4 = (W & 3) == 0;
-    const bool win = row4 && w != W && 3.0f * sw < 1.0f;
-#define HKP_UPS(SG, R4, WN) \
-    hipLaunchKernelGGL((upsample_sigmoid_kernel<SG, R4, WN>), grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat, keys)
+#define HKP_UPS(SG, R4) \
+    hipLaunchKernelGGL((upsample_sigmoid_kernel<SG, R4>), grid, dim3(256), 0, st, h, w, H, W, sh, sw, lowres, heat, keys)
     if (apply_sigmoid) {
-        if (win) HKP_UPS(true, true, true); else if (row4) HKP_UPS(true, true, false); else HKP_UPS(true, false, false);
+        if (row4) HKP_UPS(true, true); else HKP_UPS(true, false);
     } else {
-        if (win) HKP_UPS(false, true, true); else if (row4) HKP_UPS(false, true, false); else HKP_UPS(false, false, false);
+        if (row4) HKP_UPS(false, true); else HKP_UPS(false, false);
     }
 #undef HKP_UPS
     HKP_LAUNCH_CHECK("hkp_upsample_sigmoid");
