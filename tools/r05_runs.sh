@@ -292,6 +292,10 @@ ups)
     done
     rm -rf $O/prof $O/prof4
     ;;
+sprio)
+    timeout -k 10 500 python -u tools/train_ab.py "" "mainprio=-1" "" "mainprio=-1" "sideprio=-1" --rounds 5 \
+        --iters 10 > $O/ab_train.log 2>&1
+    ;;
 final)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1

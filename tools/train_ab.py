@@ -22,6 +22,17 @@ import torch  # noqa: E402
 from infer_ab import KNOBS, knobs, set_knobs  # noqa: E402  (tools/ is on sys.path when run as a script)
 
 
+# pseudo-fields handled here: mainprio=P runs the step on a stream of priority P
+# (torch: lower = higher priority; 0 = the default stream's), sideprio=P recreates
+# the wgrad side stream with priority P
+STREAM_KNOBS = ("mainprio", "sideprio")
+
+
+def stream_knobs(form):
+    d = dict(item.partition("=")[::2] for item in filter(None, form.split(",")))
+    return {k: int(d[k]) for k in STREAM_KNOBS if k in d}
+
+
 def parse(form):
     """Policy overrides of a form; the pseudo-fields store=K, prio=K and stem_pair=K
     are library debug knobs (infer_ab.KNOBS), not Policy fields."""
@@ -29,7 +40,7 @@ def parse(form):
     kw = {}
     for item in filter(None, form.split(",")):
         k, _, v = item.partition("=")
-        if k in KNOBS:
+        if k in KNOBS or k in STREAM_KNOBS:
             continue
         cur = getattr(DEFAULT, k)
         kw[k] = (v.lower() in ("1", "true", "yes")) if isinstance(cur, bool) else type(cur)(v)
@@ -60,22 +71,39 @@ def main():
     trainer = hkp_train.Trainer(model, lr=1e-4, weight_decay=1e-4)
     pols = [base.with_(**parse(f)) for f in args.forms]
     kns = [knobs(f) for f in args.forms]
-    for p, kv in zip(pols, kns):      # warm every form (kernels, caches, plans)
+    from hkp import net as hkp_net
+    default_side = hkp_net._side_stream(dev)
+    sks = []
+    for f in args.forms:
+        sk = stream_knobs(f)
+        main = torch.cuda.Stream(dev, priority=sk["mainprio"]) if "mainprio" in sk else torch.cuda.current_stream(dev)
+        side = torch.cuda.Stream(dev, priority=sk["sideprio"]) if "sideprio" in sk else default_side
+        sks.append((main, side))
+
+    def run(n, ms):
+        main, side = ms
+        hkp_net._side_streams[dev] = side
+        main.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(main):
+            for _ in range(n):
+                trainer.step(x, uv)
+        torch.cuda.current_stream(dev).wait_stream(main)
+
+    print("stream priority range", torch.cuda.Stream.priority_range(), flush=True)
+    for p, kv, ms in zip(pols, kns, sks):      # warm every form (kernels, caches, plans)
         model.policy = trainer.policy = p
         set_knobs(hkp.lib(), kv)
-        for _ in range(3):
-            trainer.step(x, uv)
+        run(3, ms)
     torch.cuda.synchronize()
     res = {f: [] for f in args.forms}
     for _ in range(args.rounds):
-        for f, p, kv in zip(args.forms, pols, kns):
+        for f, p, kv, ms in zip(args.forms, pols, kns, sks):
             model.policy = trainer.policy = p
             set_knobs(hkp.lib(), kv)
-            trainer.step(x, uv)
+            run(1, ms)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            for _ in range(args.iters):
-                trainer.step(x, uv)
+            run(args.iters, ms)
             torch.cuda.synchronize()
             res[f].append(B * args.iters / (time.perf_counter() - t0))
     set_knobs(hkp.lib(), knobs(""))
