@@ -29,7 +29,11 @@ __device__ __forceinline__ void bn_rank_stats_store(int c, int C, long count, do
 // (A one-pass form — each lane's tiles folded by Chan's pairwise merge, the lanes
 // merged the same way — measured no faster: B=8 shard 1494 -> 1484 img/s, C2 / C4 /
 // C3 unchanged; profiles/r05_fin_*.)
-template <int CPB, int NT = 256>
+// NB > 0 (tiles <= NB * TL): every partial of the lane loaded in ONE round and
+// kept in registers for the second pass — the same sums in the same order (so the
+// same bits) with one exposed load latency instead of 2 x ceil(tiles / (8 TL));
+// tile means of full tiles (tile_rows a power of two) by an exact multiply
+template <int CPB, int NT = 256, int NB = 0>
 __global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long tiles, int tile_rows,
                                                          const float* __restrict__ part, const float* gamma,
                                                          const float* beta, float momentum, float eps, float* rmean,
@@ -39,6 +43,37 @@ __global__ __launch_bounds__(NT) void bn_finalize_kernel(int C, long count, long
     __shared__ double red[NW][8];
     const int cl = threadIdx.x % CPB, tl = threadIdx.x / CPB, c = blockIdx.x * CPB + cl;
     const bool ok = c < C;
+    if constexpr (NB > 0) {
+        float2 v[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const long t = tl + (long)j * TL;
+            v[j] = ok && t < tiles ? *(const float2*)(part + (t * C + c) * 2) : make_float2(0.f, 0.f);
+        }
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) s += (double)v[j].x;
+        const double mean = lanes_sum_d<CPB, NW>(s, red) / (double)count;
+        const bool pow2 = (tile_rows & (tile_rows - 1)) == 0;
+        const double inv_rows = 1.0 / (double)tile_rows;   // exact for a power of two
+        double q = 0.0;
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const long t = tl + (long)j * TL;
+            if (ok && t < tiles) {
+                const long n_t = min((long)tile_rows, count - t * tile_rows);
+                const double tm = pow2 && n_t == tile_rows ? (double)v[j].x * inv_rows : (double)v[j].x / (double)n_t;
+                const double dm = tm - mean;
+                q += (double)v[j].y + (double)n_t * dm * dm;
+            }
+        }
+        const double m2 = lanes_sum_d<CPB, NW>(q, red);
+        if (tl == 0 && ok) {
+            if (stats) bn_rank_stats_store(c, C, count, mean, m2, stats);
+            else bn_fin_store(c, C, count, mean, m2, gamma, beta, momentum, eps, rmean, rvar, nbt, ss, mi);
+        }
+        return;
+    }
     // tiles t = tl, tl + TL, ... in order; 8 loads in flight per batch (the loop
     // is latency-bound), zero-filled past the end (exact: s + 0 = s)
     double s = 0.0;
@@ -421,6 +456,12 @@ static inline int grid_for(long work, int block = 256, long cap = 256L * 16) {
 
 using namespace hkp;
 
+// Debug / A/B (tools/ only): 0 runs the finalize merges' batched-load loops where
+// the register-held forms (NB > 0) would run — the same bits
+static int g_fin_regs = 1;
+extern "C" void hkp_debug_fin_regs(int32_t on) { g_fin_regs = on != 0; }
+int hkp_fin_regs() { return g_fin_regs; }
+
 // The one-kernel (fin_one) and two-level (fin_two) merges of the tile partials:
 // scale/shift (+ running stats), or (stats != null) the rank's SyncBN statistics.
 static int fin_one(const char* who, int32_t c, int64_t count, int64_t tiles, int32_t tile_rows, const float* partials,
@@ -433,13 +474,18 @@ static int fin_one(const char* who, int32_t c, int64_t count, int64_t tiles, int
     HKP_CHECK_ARG((tiles - 1) * (int64_t)tile_rows < count && tiles * (int64_t)tile_rows >= count,
                   "%s: tiles/tile_rows inconsistent with count", who);
     const int cpb = partials_cpb(c);
-#define HKP_FIN1(CPB, NT)                                                                                          \
-    hipLaunchKernelGGL((bn_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), c, \
-                       (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,      \
+    // partials per tile lane of the 256-thread form: held in registers up to 32
+    const long per = g_fin_regs ? (tiles + 256 / cpb - 1) / (256 / cpb) : 1L << 40;
+#define HKP_FIN1(CPB, NT, NB)                                                                                      \
+    hipLaunchKernelGGL((bn_finalize_kernel<CPB, NT, NB>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), \
+                       c, (long)count, (long)tiles, tile_rows, partials, gamma, beta, momentum, eps, running_mean,   \
                        running_var, num_batches_tracked, scale_shift, mean_invstd, stats)
 #define HKP_FIN(CPB)                                  \
-    if (tiles >= 4096) { HKP_FIN1(CPB, 1024); } \
-    else { HKP_FIN1(CPB, 256); }
+    if (tiles >= 4096) { HKP_FIN1(CPB, 1024, 0); } \
+    else if (per <= 8) { HKP_FIN1(CPB, 256, 8); } \
+    else if (per <= 16) { HKP_FIN1(CPB, 256, 16); } \
+    else if (per <= 32) { HKP_FIN1(CPB, 256, 32); } \
+    else { HKP_FIN1(CPB, 256, 0); }
     if (cpb == 8) { HKP_FIN(8); }
     else if (cpb == 4) { HKP_FIN(4); }
     else if (cpb == 2) { HKP_FIN(2); }

@@ -126,7 +126,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long M, int C, const
 }
 
 // per channel: dgamma, dbeta, and the apply coefficients (grad_mean, k, invstd*gamma)
-template <int CPB, int NT = 256>
+// NB > 0 (tiles <= NB * TL): the lane's partials (and maxima) loaded in one round
+// into registers — the same sums and maxima in the same order, so the same bits
+template <int CPB, int NT = 256, int NB = 0>
 __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long tiles, const float* __restrict__ part,
                                                              const float* __restrict__ mi, const float* gamma,
                                                              float* dgamma, float* dbeta, float* coef,
@@ -139,7 +141,24 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long
     const bool ok = c < C;
     if (!pmax && amax && !stats && blockIdx.x == 0 && threadIdx.x == 0) *amax = 0u;   // apply's atomicMax starts from 0
     double s = 0.0, d = 0.0;
-    if (ok)   // 8 loads in flight per batch (latency-bound loop); zero-filled past the end
+    double md = 0.0, mv = 0.0;
+    if constexpr (NB > 0) {
+        float2 v[NB], x[NB];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            const long t = tl + (long)j * TL;
+            const bool in = ok && t < tiles;
+            v[j] = in ? *(const float2*)(part + (t * C + c) * 2) : make_float2(0.f, 0.f);
+            x[j] = in && pmax ? *(const float2*)(pmax + (t * C + c) * 2) : make_float2(0.f, 0.f);
+        }
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+            s += (double)v[j].x;
+            d += (double)v[j].y;
+            md = fmax(md, (double)x[j].x);       // maxima of non-negative values: 0 past the end is exact
+            mv = fmax(mv, (double)x[j].y);
+        }
+    } else if (ok) {   // 8 loads in flight per batch (latency-bound loop); zero-filled past the end
         for (long t0 = tl; t0 < tiles; t0 += 8 * TL) {
             float2 v[8];
 #pragma unroll
@@ -153,16 +172,16 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_kernel(int C, long M, long
                 d += (double)v[j].y;
             }
         }
-    const double S = lanes_sum_d<CPB, NW>(s, red);
-    const double D = lanes_sum_d<CPB, NW>(d, red);
-    double md = 0.0, mv = 0.0;
-    if (pmax) {   // per-channel maxima over the tiles (max: any order is exact)
-        if (ok)
+        if (pmax)   // per-channel maxima over the tiles (max: any order is exact)
             for (long t = tl; t < tiles; t += TL) {
                 const float2 v = *(const float2*)(pmax + (t * C + c) * 2);
                 md = fmax(md, (double)v.x);
                 mv = fmax(mv, (double)v.y);
             }
+    }
+    const double S = lanes_sum_d<CPB, NW>(s, red);
+    const double D = lanes_sum_d<CPB, NW>(d, red);
+    if (pmax) {
         md = lanes_max_d<CPB, NW>(md, red);
         mv = lanes_max_d<CPB, NW>(mv, red);
     }
@@ -398,18 +417,23 @@ extern "C" int hkp_bn_bwd_reduce(int64_t m, int32_t c, const float* g, const flo
     return HKP_OK;
 }
 
+int hkp_fin_regs();   // bn.hip: hkp_debug_fin_regs
+
 static int bwd_fin(int32_t c, int64_t m, const float* partials, const float* maxima, const float* mean_invstd,
                    const float* gamma, float* dgamma, float* dbeta, float* coef, uint32_t* dy_amax_bits,
                    double* stats, hkp_stream_t stream) {
     const long tiles = (m + BNB_TILE - 1) / BNB_TILE;
     const int cpb = partials_cpb(c);
-#define HKP_BFIN1(CPB, NT)                                                                                         \
-    hipLaunchKernelGGL((bn_bwd_finalize_kernel<CPB, NT>), dim3((c + CPB - 1) / CPB), dim3(NT), 0, as_stream(stream), \
-                       c, (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef, maxima,                  \
-                       (unsigned*)dy_amax_bits, stats)
+    const long per = hkp_fin_regs() ? (tiles + 256 / cpb - 1) / (256 / cpb) : 1L << 40;   // partials per tile lane
+#define HKP_BFIN1(CPB, NT, NB)                                                                                     \
+    hipLaunchKernelGGL((bn_bwd_finalize_kernel<CPB, NT, NB>), dim3((c + CPB - 1) / CPB), dim3(NT), 0,               \
+                       as_stream(stream), c, (long)m, tiles, partials, mean_invstd, gamma, dgamma, dbeta, coef,       \
+                       maxima, (unsigned*)dy_amax_bits, stats)
 #define HKP_BFIN(CPB)                                  \
-    if (tiles >= 4096) { HKP_BFIN1(CPB, 1024); } \
-    else { HKP_BFIN1(CPB, 256); }
+    if (tiles >= 4096) { HKP_BFIN1(CPB, 1024, 0); } \
+    else if (per <= 8) { HKP_BFIN1(CPB, 256, 8); } \
+    else if (per <= 16) { HKP_BFIN1(CPB, 256, 16); } \
+    else { HKP_BFIN1(CPB, 256, 0); }
     if (cpb == 8) { HKP_BFIN(8); }
     else if (cpb == 4) { HKP_BFIN(4); }
     else if (cpb == 2) { HKP_BFIN(2); }

@@ -262,6 +262,10 @@ void hkp_debug_x3_prio(int32_t mode);
 /* Debug / A/B (tools/ only, not thread-safe): nonzero runs the stem on the one-tile
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
+/* Debug / A/B (tools/ only, not thread-safe): 0 runs the BN finalize merges
+ * (forward and backward) as batched-load loops where the default holds a tile
+ * lane's partials in registers after one load round — the same bits either way. */
+void hkp_debug_fin_regs(int32_t on);
 
 /* ----------------------------------------------------------- batchnorm ---- */
 /* Train-mode BatchNorm2d statistics (src/resnet.py:46,49,78,85,87,139,187;
