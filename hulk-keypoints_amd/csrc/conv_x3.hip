@@ -3592,7 +3592,9 @@ static X3Plan x3_plan(int k, long m_tiles, int nks, bool sk_ok, double over) {
 //                           power, so the chip holds a higher clock —
 //                           MI355X_MICROARCH.md DVFS item 7)
 //   256x128, >= 2 rounds    16x16x32 body, 3-stage ring (C2 layer3 +6 %, layer2 +5 %)
-//   256x128, one round      32x32x16 body (the 16x16 body's longer fill lost 8-11 %)
+//   256x128, one round      32x32x16 body (the 16x16 body's longer fill lost 8-11 %;
+//                           round 5: AUTO on packed f16x3 runs the 16x16 body here
+//                           and 256x64 pairs for >= 1 round — x3_choose)
 //   256x64                  16x16x32 body, two blocks per CU (layer1 0.223 -> 0.166 ms)
 //   stream-K 256x128 / 64   16x16x32 / 32x32x16 bodies (training t4 fwd +3-6 %, t3 +6 %)
 // hkp_conv_desc.tile (HKP_TILE_*) forces one of them — every body is reachable
@@ -3616,6 +3618,7 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
 // HKP_TILE_256 / 256_TAIL keep the 2-stage body)
 // DUO (the plain-fp16 256x128 two-blocks-per-CU body) where forced and legal;
 // other operand layouts plan as AUTO
+static int g_x3_pair128 = 1;                           // hkp_debug_x3_pair128
 static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo, int P) {
     if (policy == HKP_TILE_A3P) {
         if ((P == 1 || P == 3) && k % 256 == 0) {
@@ -3646,6 +3649,17 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
         X3Choice d{DUO_BN, 16, false, false};
         d.duo = true;
         return d;
+    }
+    // AUTO, packed f16x3: where the cost table picks 256x128 tiles, the 256x64
+    // two-blocks-per-CU tiles once their grid fills a round of 128-wide tiles (their
+    // fill and epilogue overlap the other block's K loop: C2 layer2 3x3 0.140 ->
+    // 0.125 ms, its stride-2 conv1 0.086 -> 0.073, the 1x1 downsamples 64 -> 128 0.033
+    // -> 0.025 and 128 -> 256 0.061 -> 0.052), and a one-round 256x128 grid on the
+    // 16x16x32 body (the B=8 shard's layer2 0.053 -> 0.040 ms; the 32x32x16 body's
+    // shorter fill no longer wins) — tools/conv_ab.py, profiles/r05_l2_conv_ab.log
+    if (policy == HKP_TILE_AUTO && P == 3 && !c.halo && c.bn == 128 && g_x3_pair128) {
+        if (m_tiles * (k / 128) >= x3_cus()) return {64, 16, true, false};
+        if (!c.sk) c.mfd = 16;
     }
     return c;
 }
@@ -4375,6 +4389,7 @@ extern "C" void hkp_debug_x3_stagger(int32_t ns) { g_x3_stagger_ns = ns > 0 ? ns
 // tail as its own conv_x3_tail_kernel launch instead of inside the A3 launch.
 extern "C" void hkp_debug_x3_split_tail(int32_t on) { g_x3_split_tail = on != 0; }
 extern "C" void hkp_debug_stem_pair(int32_t on) { g_stem_pair = on != 0; }
+extern "C" void hkp_debug_x3_pair128(int32_t on) { g_x3_pair128 = on != 0; }
 
 // Debug / A/B (tools/ only, not thread-safe): the flavour of the forward convs'
 // epilogue output stores (X3Args::st_kind: 0 each site's own, 1 plain, 2

@@ -79,6 +79,7 @@ SIGNATURES = {
     "hkp_debug_x3_split_tail": (None, [_I32]),
     "hkp_debug_stem_pair": (None, [_I32]),
     "hkp_debug_fin_regs": (None, [_I32]),
+    "hkp_debug_x3_pair128": (None, [_I32]),
     "hkp_debug_x3_store": (None, [_I32]),
     "hkp_debug_duo_stagger": (None, [_I32]),
     "hkp_debug_x3_prio": (None, [_I32]),

@@ -540,12 +540,13 @@ def test_x3_tile_bodies_dgrad(cuda_device, case, tile):
 
 
 def test_x3_mf16_policy_large_grid(cuda_device):
-    """Grids of >= 2 full rounds of 256x128 tiles take the 16x16x32-MFMA body by
-    default; it agrees with the 32x32x16 body (HKP_TILE_128_MF32) to fp32
-    summation order — forward and stride-1 dgrad — and hkp_conv_kernel_name
-    (the observer's symbol) names each."""
+    """The 256x128 16x16x32-MFMA body (HKP_TILE_128_MF16) agrees with the 32x32x16
+    body (HKP_TILE_128_MF32) to fp32 summation order — forward and stride-1 dgrad —
+    and hkp_conv_kernel_name (the observer's symbol) names each; AUTO plans a
+    128-wide output that fills a round of 256x128 tiles on the 256x64
+    two-blocks-per-CU tiles (round 5) and a one-round grid on the 16x16x32 body."""
     from hkp import ops
-    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_KOP_FWD_X3, HKP_TILE_128_MF32, ConvDesc
+    from hkp._lib import HKP_KOP_DGRAD_X3, HKP_KOP_FWD_X3, HKP_TILE_128_MF16, HKP_TILE_128_MF32, ConvDesc
     # 585 tiles; Wo % 32 != 0 keeps the halo body (HKP_TILE_HALO) out of the choice
     n, h, w, cin, cout, k, st, pad, dil = (2, 240, 312, 128, 128, 3, 1, 1, 1)
     d = cuda_device
@@ -555,6 +556,11 @@ def test_x3_mf16_policy_large_grid(cuda_device):
     xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
     wp = ops.weight_pack_x3(wt)
     desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0)
+    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"
+    assert ops.kernel_name(desc, HKP_KOP_DGRAD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"
+    one = ConvDesc(2, 120, 150, cin, cout, k, k, st, pad, dil, 0)     # 141 tiles: under one round
+    assert ops.kernel_name(one, HKP_KOP_FWD_X3) == "conv_x3_kernel<128, false, false, 16, false, 3>"
+    desc.tile = HKP_TILE_128_MF16
     assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_kernel<128, false, false, 16, false, 3>"
     assert ops.kernel_name(desc, HKP_KOP_DGRAD_X3) == "conv_x3_kernel<128, false, false, 16, false, 3>"
     desc.tile = HKP_TILE_128_MF32
@@ -563,8 +569,8 @@ def test_x3_mf16_policy_large_grid(cuda_device):
     amax = ops.absmax(gy)
     dys = ops.split_pack_x3(gy, amax)
     wfp = ops.weight_flip_pack_x3(wt)
-    y16, p16 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil)
-    dx16 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax)
+    y16, p16 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_128_MF16)
+    dx16 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax, tile=HKP_TILE_128_MF16)
     y32, p32 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_128_MF32)
     dx32 = ops.conv2d_bwd_data_x3(dys, wfp, (n, h, w, cin), pad, dil, amax=amax, tile=HKP_TILE_128_MF32)
     assert (y16 - y32).abs().max().item() <= 4e-6 * y32.abs().max().item()

@@ -21,7 +21,7 @@ import torch  # noqa: E402
 
 
 KNOBS = {"store": ("hkp_debug_x3_store", 0), "prio": ("hkp_debug_x3_prio", 0), "stem_pair": ("hkp_debug_stem_pair", 0),
-         "finregs": ("hkp_debug_fin_regs", 1),
+         "finregs": ("hkp_debug_fin_regs", 1), "pair128": ("hkp_debug_x3_pair128", 1),
          "stem_img": (None, 1)}
 
 

@@ -292,6 +292,14 @@ ups)
     done
     rm -rf $O/prof $O/prof4
     ;;
+pair128)
+    timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_precision.py \
+        tests/test_gpu_forward.py tests/test_gpu_backward.py > $O/pytest_pair128.log 2>&1
+    echo "pytest pair128: $(tail -1 $O/pytest_pair128.log)"
+    timeout -k 10 400 python -u tools/infer_ab.py "pair128=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
+    timeout -k 10 400 python -u tools/infer_ab.py "pair128=0" "" --batch 8 --rounds 9 --iters 20 > $O/ab_b8.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "pair128=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
 finregs)
     timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_backward.py \
         tests/test_gpu_forward.py tests/test_gpu_syncbn.py tests/test_gpu_gram.py > $O/pytest_finregs.log 2>&1
