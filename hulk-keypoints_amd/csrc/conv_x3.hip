@@ -3650,16 +3650,19 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
         d.duo = true;
         return d;
     }
-    // AUTO, packed f16x3: where the cost table picks 256x128 tiles, the 256x64
-    // two-blocks-per-CU tiles once their grid fills a round of 128-wide tiles (their
-    // fill and epilogue overlap the other block's K loop: C2 layer2 3x3 0.140 ->
-    // 0.125 ms, its stride-2 conv1 0.086 -> 0.073, the 1x1 downsamples 64 -> 128 0.033
-    // -> 0.025 and 128 -> 256 0.061 -> 0.052), and a one-round 256x128 grid on the
-    // 16x16x32 body (the B=8 shard's layer2 0.053 -> 0.040 ms; the 32x32x16 body's
-    // shorter fill no longer wins) — tools/conv_ab.py, profiles/r05_l2_conv_ab.log
-    if (policy == HKP_TILE_AUTO && P == 3 && !c.halo && c.bn == 128 && g_x3_pair128) {
-        if (m_tiles * (k / 128) >= x3_cus()) return {64, 16, true, false};
-        if (!c.sk) c.mfd = 16;
+    // AUTO, packed f16x3, one-tile grids: the 256x64 two-blocks-per-CU tiles (one
+    // block's fill and epilogue overlap the other's K loop) for short-K convs (the
+    // 1x1 downsamples, K-depth <= 256 channels: C2 128 -> 256 0.061 -> 0.052 ms,
+    // 256 -> 512 0.147 -> 0.142; B=8 0.061 -> 0.040 and 0.021 -> 0.019) and where the
+    // cost table picks 256x128 tiles over at least a round of them (C2 layer2 3x3
+    // 0.140 -> 0.125 ms, its stride-2 conv1 0.086 -> 0.073, the 64 -> 128 downsample
+    // 0.033 -> 0.025); a one-round 256x128 grid on the 16x16x32 body (the B=8 shard's
+    // layer2 0.053 -> 0.040 ms: the 32x32x16 body's shorter fill no longer wins).
+    // Stream-K plans stay (B=8 layer3: 0.128 ms vs 0.138 on pairs).  tools/conv_ab.py,
+    // profiles/r05_l2_conv_ab*.log
+    if (policy == HKP_TILE_AUTO && P == 3 && !c.halo && !c.sk && g_x3_pair128) {
+        if (nks <= 8 || (c.bn == 128 && m_tiles * (k / 128) >= x3_cus())) return {64, 16, true, false};
+        if (c.bn == 128) c.mfd = 16;
     }
     return c;
 }

@@ -263,8 +263,8 @@ void hkp_debug_x3_prio(int32_t mode);
  * kernel (as HKP_TILE_64_PAIR does per call) instead of the patch body. */
 void hkp_debug_stem_pair(int32_t on);
 /* Debug / A/B (tools/ only, not thread-safe): 0 returns AUTO's packed-f16x3 plans
- * for 128-wide-tile grids to the cost table's 256x128 choice (round 4): no 256x64
- * two-blocks-per-CU tiles for grids of >= 1 round, 32x32x16 for one-round grids. */
+ * to the round-4 cost table's: no 256x64 two-blocks-per-CU tiles for short-K convs
+ * and 256x128 grids of >= 1 round, 32x32x16 MFMAs for one-round 256x128 grids. */
 void hkp_debug_x3_pair128(int32_t on);
 /* Debug / A/B (tools/ only, not thread-safe): 0 runs the BN finalize merges
  * (forward and backward) as batched-load loops where the default holds a tile

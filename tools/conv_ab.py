@@ -28,6 +28,11 @@ SHAPES = {
     "l3c1": ("x3", 32, 60, 80, 128, 256, 3, 1, 1, 1),           # layer3 conv1 (128 -> 256)
     "l3ds": ("x3", 32, 60, 80, 128, 256, 1, 1, 0, 1),
     "t2": ("x3", 8, 60, 80, 128, 128, 3, 1, 1, 1),             # layer2 at batch 8
+    "l4c1": ("x3", 32, 60, 80, 256, 512, 3, 1, 2, 2),           # layer4 conv1 (256 -> 512)
+    "l4ds": ("x3", 32, 60, 80, 256, 512, 1, 1, 0, 1),
+    "t2c1": ("x3", 8, 120, 160, 64, 128, 3, 2, 1, 1),           # batch 8: layer2 conv1, downsamples
+    "t2ds": ("x3", 8, 120, 160, 64, 128, 1, 2, 0, 1),
+    "t3ds": ("x3", 8, 60, 80, 128, 256, 1, 1, 0, 1),
     "h128": ("x3", 4, 240, 320, 128, 128, 3, 1, 1, 1),           # halo body at 128 channels
     "t4": ("x3", 8, 60, 80, 512, 512, 3, 1, 4, 4),             # training shard (batch 8)
     "t3": ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),
