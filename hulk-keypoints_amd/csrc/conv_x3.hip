@@ -3652,17 +3652,21 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
     }
     // AUTO, packed f16x3, one-tile grids: the 256x64 two-blocks-per-CU tiles (one
     // block's fill and epilogue overlap the other's K loop) for short-K convs (the
-    // 1x1 downsamples, K-depth <= 256 channels: C2 128 -> 256 0.061 -> 0.052 ms,
-    // 256 -> 512 0.147 -> 0.142; B=8 0.061 -> 0.040 and 0.021 -> 0.019) and where the
+    // 1x1 downsamples, K-depth <= 256 channels: C2 128 -> 256 0.061 -> 0.052 ms;
+    // B=8 256 -> 512 0.061 -> 0.040 and 128 -> 256 0.021 -> 0.019) and where the
     // cost table picks 256x128 tiles over at least a round of them (C2 layer2 3x3
     // 0.140 -> 0.125 ms, its stride-2 conv1 0.086 -> 0.073, the 64 -> 128 downsample
     // 0.033 -> 0.025); a one-round 256x128 grid on the 16x16x32 body (the B=8 shard's
     // layer2 0.053 -> 0.040 ms: the 32x32x16 body's shorter fill no longer wins).
-    // Stream-K plans stay (B=8 layer3: 0.128 ms vs 0.138 on pairs).  tools/conv_ab.py,
-    // profiles/r05_l2_conv_ab*.log
+    // Stream-K plans stay (B=8 layer3: 0.128 ms vs 0.138 on pairs), and so do grids
+    // of more than 3 rounds of 256x256 tiles, where the longer grid's steady state
+    // favours the larger tiles (C2 256 -> 512 downsample at 4.7 rounds: even; config
+    // C5 at 1280x960, 4.7-37 rounds: its 128-wide 3x3 1.05x, its 1x1s 1.04-1.27x
+    // slower on pairs).  tools/conv_ab.py, profiles/r05_l2_conv_ab*.log
     if (policy == HKP_TILE_AUTO && P == 3 && !c.halo && !c.sk && g_x3_pair128) {
-        if (nks <= 8 || (c.bn == 128 && m_tiles * (k / 128) >= x3_cus())) return {64, 16, true, false};
-        if (c.bn == 128) c.mfd = 16;
+        const bool small = (double)m_tiles * k <= 3.0 * 256 * x3_cus();
+        if (small && (nks <= 8 || (c.bn == 128 && m_tiles * (k / 128) >= x3_cus()))) return {64, 16, true, false};
+        if (c.bn == 128 && m_tiles * (k / 128) < x3_cus()) c.mfd = 16;
     }
     return c;
 }

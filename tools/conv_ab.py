@@ -38,6 +38,12 @@ SHAPES = {
     "t3": ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),
     "t3a": ("x3", 8, 60, 80, 128, 256, 3, 1, 2, 2),            # layer3 conv1 at batch 8 (dilated, stride 1)
     "t4ds": ("x3", 8, 60, 80, 256, 512, 1, 1, 0, 1),
+    # R50-8s @1280x960, batch 32 (C5 training, f16x3): short-K 1x1s
+    "c5_l3_c3": ("x3", 32, 120, 160, 256, 1024, 1, 1, 0, 1),
+    "c5_l2_c3": ("x3", 32, 120, 160, 128, 512, 1, 1, 0, 1),
+    "c5_l1_c3": ("x3", 32, 240, 320, 64, 256, 1, 1, 0, 1),
+    "c5_l2_ds": ("x3", 32, 240, 320, 256, 512, 1, 2, 0, 1),
+    "c5_l2_c2": ("x3", 32, 120, 160, 128, 128, 3, 1, 1, 1),
     # R50-8s @640x480, batch 128 (C4, plain fp16)
     "c4_l4_c2": ("f16", 128, 60, 80, 512, 512, 3, 1, 4, 4),
     "c4_l4_c1": ("f16", 128, 60, 80, 2048, 512, 1, 1, 0, 1),
