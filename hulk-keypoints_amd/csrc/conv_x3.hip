@@ -3636,6 +3636,9 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
         }
         policy = HKP_TILE_AUTO;
     }
+    // the overlapped dgrad's A3 request (Policy.dgrad_overlap_tile) on a 64- or
+    // 128-channel output, which A3 cannot take: plan it as AUTO (the rules below)
+    if (policy == HKP_TILE_256_A3 && P == 3 && k % 256 != 0 && g_x3_pair128) policy = HKP_TILE_AUTO;
     if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
     X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
     if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
