@@ -28,6 +28,7 @@ SHAPES = {
     "l3c1": ("x3", 32, 60, 80, 128, 256, 3, 1, 1, 1),           # layer3 conv1 (128 -> 256)
     "l3ds": ("x3", 32, 60, 80, 128, 256, 1, 1, 0, 1),
     "t2": ("x3", 8, 60, 80, 128, 128, 3, 1, 1, 1),             # layer2 at batch 8
+    "t1": ("x3", 8, 120, 160, 64, 64, 3, 1, 1, 1),             # layer1 at batch 8
     "l4c1": ("x3", 32, 60, 80, 256, 512, 3, 1, 2, 2),           # layer4 conv1 (256 -> 512)
     "l4ds": ("x3", 32, 60, 80, 256, 512, 1, 1, 0, 1),
     "t2c1": ("x3", 8, 120, 160, 64, 128, 3, 2, 1, 1),           # batch 8: layer2 conv1, downsamples
