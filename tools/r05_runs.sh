@@ -41,6 +41,11 @@
 #   a4        the 4-wave A3 body (HKP_TILE_A4; removed after this run): parity tests, per-conv A/B, phase clocks
 #   ups       the upsample + sigmoid + argmax kernel at 4 sub-chunks per block: its tests, kernel
 #             trace of the C2 and C4 benches (upsample_sigmoid_kernel average vs r05_v2)
+#   pair128   the planner's 256x64 pairs for short-K / 128-wide f16x3 convs: planner and
+#             forward / backward tests, C2 / B=8 / C3-train A/B (hkp_debug_x3_pair128 0 / 1)
+#   finregs   the register-held BN finalize form: BN tests, B=8 / C2 / C3-train A/B
+#             (hkp_debug_fin_regs 0 / 1)
+#   sprio     the training step on a high-priority stream / the wgrad side stream high
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
