@@ -46,6 +46,8 @@
 #   finregs   the register-held BN finalize form: BN tests, B=8 / C2 / C3-train A/B
 #             (hkp_debug_fin_regs 0 / 1)
 #   sprio     the training step on a high-priority stream / the wgrad side stream high
+#   headdw    the head's fc weight gradient on the wgrad side stream (Policy.overlap_head_dw;
+#             removed after this run: neutral)
 #   final     GPU suite, smoke(), default bench line
 set -e
 export TMPDIR=/tmp
@@ -312,6 +314,13 @@ finregs)
     timeout -k 10 400 python -u tools/infer_ab.py "finregs=0" "" --batch 8 --rounds 9 --iters 20 > $O/ab_b8.log 2>&1
     timeout -k 10 400 python -u tools/infer_ab.py "finregs=0" "" --rounds 9 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "finregs=0" "" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
+headdw)
+    timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_backward.py \
+        tests/test_gpu_scale.py tests/test_gpu_dropin.py tests/test_gpu_syncbn.py > $O/pytest_headdw.log 2>&1
+    echo "pytest headdw: $(tail -1 $O/pytest_headdw.log)"
+    timeout -k 10 600 python -u tools/train_ab.py "overlap_head_dw=0" "" "overlap_head_dw=0" "" --rounds 5 \
+        --iters 10 > $O/ab_train.log 2>&1
     ;;
 sprio)
     timeout -k 10 500 python -u tools/train_ab.py "" "mainprio=-1" "" "mainprio=-1" "sideprio=-1" --rounds 5 \
