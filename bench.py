@@ -385,7 +385,9 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
     dist = world > 1
     sync_bn = dist and getattr(args, "sync_bn", False)
     B, K, H, W = batch, args.keypoints, args.height, args.width
-    torch.manual_seed(1234 + rank)
+    # a strong-scaling shard (shard_of) is a slice of ONE job: every rank runs the same
+    # random-init model; weak scaling gives each rank its own seed
+    torch.manual_seed(1234 if shard_of is not None else 1234 + rank)
     pol = Policy(precision=precision, **tuning(args))
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=pol).to(dev)
     if shard_of is not None:

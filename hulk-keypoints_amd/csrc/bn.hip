@@ -458,8 +458,10 @@ using namespace hkp;
 
 // Debug / A/B (tools/ only): 0 runs the finalize merges' batched-load loops where
 // the register-held forms (NB > 0) would run — the same bits
-static int g_fin_regs = 1;
+HKP_AB_KNOB(int, g_fin_regs, 1);
+#ifdef HKP_AB_KNOBS
 extern "C" void hkp_debug_fin_regs(int32_t on) { g_fin_regs = on != 0; }
+#endif
 int hkp_fin_regs() { return g_fin_regs; }
 
 // The one-kernel (fin_one) and two-level (fin_two) merges of the tile partials:

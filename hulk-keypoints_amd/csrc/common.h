@@ -7,11 +7,24 @@
 #include <string.h>
 
 #include "../../include/hulkkp.h"
+#ifdef HKP_AB_KNOBS
+#include "../../include/hulkkp_ab.h"
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace hkp {
+
+// A/B instruments (tools/ only): the process-global knobs and their hkp_debug_*
+// setters (include/hulkkp_ab.h) exist only in the -DHKP_AB_KNOBS build (`make ab`
+// -> tools/ab_lib/libhulkkp_ab.so); the product library compiles each knob as a
+// constant at its default, so it keeps no process-global switches
+#ifdef HKP_AB_KNOBS
+#define HKP_AB_KNOB(T, name, dflt) static T name = dflt
+#else
+#define HKP_AB_KNOB(T, name, dflt) static constexpr T name = dflt
+#endif
 
 // thread-local last-error message (hkp_last_error)
 void set_error(const char* fmt, ...);

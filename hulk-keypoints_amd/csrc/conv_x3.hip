@@ -104,7 +104,6 @@ struct X3Args {
     // tail_groups groups of n_tiles blocks over tail_units (m-tile, K-step) units
     // from m-tile tail_mt0 (the one-launch form of conv_x3_tail_kernel)
     int main_blocks = 0, tail_groups = 0, tail_mt0 = 0;
-    int p_tiles = 0;       // conv_x3_a3p_kernel: the launch's tiles (m-tiles x column tiles)
     long tail_units = 0;
     unsigned long long* stamps = nullptr;   // debug: per-block phase clocks (hkp_debug_x3_stamps)
     // first-round stagger: blocks b < stagger_blocks with (b >> 3) & 1 (half the CUs
@@ -1859,7 +1858,7 @@ constexpr int STEM_PCH = 2 * STEM_PLANE / 16;                    // patch 16-B c
 constexpr int STEM_PGA = (STEM_PCH + 511) / 512;                 // patch DMA instructions per wave (3)
 constexpr int STEM_LDS = STEM_BBYTES + 8 * STEM_PGA * 1024;      // B, then the patch (+ dummy chunks): 80 KiB
 
-static int g_stem_pair = 0;                                      // hkp_debug_stem_pair
+HKP_AB_KNOB(int, g_stem_pair, 0);                               // hkp_debug_stem_pair
 static bool stem_patch_shape(int ho, int wo, int k) {
     return !g_stem_pair && ho % STEM_PH == 0 && wo % STEM_PW == 0 && k % 64 == 0;
 }
@@ -2027,457 +2026,6 @@ __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
     x3_stamp(a, 5);
 }
 
-
-// ---------------------------------------------------------------------------
-// A3P (conv_x3_a3p_kernel<P>): the A3 body (256x256 tiles, 3-stage A ring, 2-stage
-// B ring, 8 waves) as a PERSISTENT grid — one block per CU walking the tiles
-// round by round (round r: tiles [r*G, (r+1)*G), XCD-remapped as the one-tile grid)
-// — whose epilogue overlaps the NEXT tile's pipeline fill.  Phase clocks of the
-// one-tile A3 grid on C4's 1x1 GEMMs (tools/x3_stamps.py): fill 4.5 us (the first
-// stages' DMA latency under load) of a 17.9-24.2 us tile.  Here, once a tile's
-// K loop is done, the next tile's first two A stages and B stages go out (128 KiB
-// into A slots 0-1 and B slots 0-1) before the epilogue runs, so they land
-// during it; its third A stage follows the epilogue.  What made the round-3
-// persistent conv lose — its epilogue stores shared vmcnt with the next tile's
-// DMA issued after them, so the first counted wait retired the stores too — is
-// avoided by order: the prefetch is OLDER than the stores, and the next tile's
-// first waits count the NOUT stores as younger (exact per full tile; a partial
-// last tile waits for everything).  The epilogue needs no staging ring: each
-// wave's 16x16 accumulator blocks are transposed in registers (two DPP quad
-// stages: a lane then holds 4 consecutive columns of one row) and, plain fp16,
-// paired with the neighbouring column block (DPP row shifts by 4 lanes) into
-// 8-column 16-B chunks; fp32 outputs store their 4 columns as 16 B directly.
-// BN partials use the generic merge (8 KiB of scratch in A slot 2, free until
-// the next tile's third stage is issued after the epilogue); the fused BN-apply
-// epilogue (P 1) keeps bn_apply_f16's arithmetic on the fp16-rounded y, so its
-// outputs are conv_x3_a3_kernel's, bit for bit.  Forward only (no addend, no
-// phase output); no split-K tail (a partial last round runs whole tiles).
-template <int CTRL>
-__device__ __forceinline__ float x3_dpp(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
-}
-// 4x4 transpose across the 4 lanes of a quad: lane b holds v[r] = D[r][b] in,
-// v[r] = D[b][r] out (D: the 4 rows x 4 columns the quad holds)
-__device__ __forceinline__ void x3_quad_transpose(f32x4& v, int b) {
-    f32x4 t;
-    // stage 1: lanes b, b^1 exchange elements r^1 where (r ^ b) & 1
-    t[0] = x3_dpp<0xB1>(v[1]);
-    t[1] = x3_dpp<0xB1>(v[0]);
-    t[2] = x3_dpp<0xB1>(v[3]);
-    t[3] = x3_dpp<0xB1>(v[2]);
-    const bool o1 = b & 1;
-    v[0] = o1 ? t[0] : v[0];
-    v[1] = o1 ? v[1] : t[1];
-    v[2] = o1 ? t[2] : v[2];
-    v[3] = o1 ? v[3] : t[3];
-    // stage 2: lanes b, b^2 exchange elements r^2 where (r ^ b) & 2
-    t[0] = x3_dpp<0x4E>(v[2]);
-    t[1] = x3_dpp<0x4E>(v[3]);
-    t[2] = x3_dpp<0x4E>(v[0]);
-    t[3] = x3_dpp<0x4E>(v[1]);
-    const bool o2 = b & 2;
-    v[0] = o2 ? t[0] : v[0];
-    v[1] = o2 ? t[1] : v[1];
-    v[2] = o2 ? v[2] : t[2];
-    v[3] = o2 ? v[3] : t[3];
-}
-
-// lane id by v_mbcnt in volatile asm: recomputed where used instead of kept live
-// (threadIdx.x itself would stay in a VGPR for the whole persistent loop)
-__device__ __forceinline__ int x3_lane_opaque() {
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-
-// EP: the fused BN-apply epilogue (P 1, hkp_conv2d_fwd_f16_bn: residual chunks in
-// registers, no BN partials) — its own instantiation, so neither form carries the
-// other's registers
-template <int P, bool EP>
-__global__ __launch_bounds__(512, 1) void conv_x3_a3p_kernel(X3Args a) {
-    static_assert(P == 1 || P == 3, "A3P: plain fp16 or the f16x3 split");
-    static_assert(!EP || P == 1, "A3P: the fused epilogue is plain fp16");
-    __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
-    constexpr int BM = 256, BN = 256, WN = 2, ROW = 128, UM = 4, UN = 8;
-    constexpr int RPI = 8, GA = 4, GB = 4, GL = GA + GB;
-    constexpr int NOUT = P == 1 ? UM * UN / 2 : UM * UN;      // output stores per thread (full tile)
-    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int wm = w / WN, wn = w % WN;
-    const int G = gridDim.x, T = a.p_tiles;
-    const int nks = a.nks;
-    char* const bring = smem + 3 * BM * ROW;
-    int tile = xcd_remap(blockIdx.x, G);
-    if (tile >= T) return;
-    bool prefetched = false;          // this tile's first stages came from the previous epilogue
-    bool full_prev = false;           // ... and every thread of it issued NOUT output stores
-    for (;;) {
-        // Everything lane-dependent is derived per tile from a thread id the compiler
-        // cannot hoist out of the loop (volatile asm): hoisted, those values stay
-        // live across the whole tile — K loop and epilogue — and spill the 250-VGPR body.
-        int lane = x3_lane_opaque();
-        const int tid = w * 64 + lane;
-        const int r16 = lane & 15, q = lane >> 4;
-        const int cstride = a.cch * 64;
-        const long xbias = (long)a.pad * (a.W + 1) * cstride;
-        const _Float16* xbase = a.xs - xbias;
-        const _Float16* zero = (const _Float16*)g_x3_zero_line;
-        const int bline = a.RS * a.cch * 64;
-        auto swz = [](int row) { return (row >> 1) & 7; };
-        // per-lane DMA sources of a tile (conv_x3_tile's bookkeeping)
-        struct Src {
-            int org[GA];
-            unsigned off[GA];
-            int boff[GB];
-        };
-        auto src_of = [&](Src& s, int tl) {
-            const int m0_ = (tl / a.n_tiles) * BM, n0_ = (tl - (tl / a.n_tiles) * a.n_tiles) * BN;
-#pragma unroll
-            for (int i = 0; i < GA; ++i) {
-                const int row = RPI * (w * GA + i) + lane / 8;
-                const int Lc = (lane % 8) ^ swz(row);
-                const int m = m0_ + row;
-                int hb = -16384, wb = -16384;
-                long off = 0;
-                if (m < a.M) {
-                    const int hw = a.Ho * a.Wo;
-                    const int n = m / hw, rem = m - n * hw;
-                    const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-                    hb = ho * a.stride - a.pad;
-                    wb = wo * a.stride - a.pad;
-                    off = (((long)n * a.H + hb) * a.W + wb) * cstride + Lc * 8;
-                }
-                s.org[i] = (int)(((unsigned)hb << 16) | ((unsigned)wb & 0xFFFFu));
-                s.off[i] = (unsigned)(off + xbias);
-            }
-#pragma unroll
-            for (int j = 0; j < GB; ++j) {
-                const int row = RPI * (w * GB + j) + lane / 8;
-                s.boff[j] = (n0_ + row) * bline + ((lane % 8) ^ swz(row)) * 8;
-            }
-        };
-        // a stage's position in the K order (channel group outer, tap inner) and its
-        // ring slot: A slots cycle over 3, B slots over 2 — advanced per issue (no
-        // divisions in the K loop), or set from a stage index (the prologue / prefetch)
-        struct Pos {
-            int slot, cc, tap, rr, ss;
-        };
-        auto pos_of = [&](int st, int nslots) {
-            Pos p;
-            p.cc = st / a.RS;
-            p.tap = st - p.cc * a.RS;
-            p.rr = p.tap / a.S;
-            p.ss = p.tap - p.rr * a.S;
-            p.slot = st % nslots;
-            return p;
-        };
-        auto advance = [&](Pos& p, int nslots) {
-            p.slot = p.slot == nslots - 1 ? 0 : p.slot + 1;
-            if (++p.ss == a.S) {
-                p.ss = 0;
-                ++p.rr;
-            }
-            if (++p.tap == a.RS) {
-                p.tap = 0;
-                p.rr = 0;
-                ++p.cc;
-            }
-        };
-        auto issue_a = [&](const Src& s, const Pos& p) {
-            char* dst = smem + p.slot * (BM * ROW);
-            const int dh = p.rr * a.dil, dw = p.ss * a.dil;
-            const long toff = ((long)dh * a.W + dw) * cstride + p.cc * 64;
-#pragma unroll
-            for (int i = 0; i < GA; ++i) {
-                const int hb = s.org[i] >> 16, wb = (int)(short)(s.org[i] & 0xFFFF);
-                const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-                // the 32-bit offset, opaque: the compiler would otherwise hoist the four
-                // 64-bit row pointers out of the K loop (8 more VGPRs: they spilled)
-                unsigned o = s.off[i];
-                asm volatile("" : "+v"(o));
-                glds16(in ? xbase + ((unsigned long)o + toff) : zero, dst + (RPI * (w * GA + i)) * ROW);
-            }
-        };
-        auto issue_b = [&](const Src& s, const Pos& p) {
-            char* dst = bring + p.slot * (BN * ROW);
-            const int boff = (p.tap * a.cch + p.cc) * 64;
-#pragma unroll
-            for (int j = 0; j < GB; ++j) glds16(a.ws + (unsigned)(s.boff[j] + boff), dst + (RPI * (w * GB + j)) * ROW);
-        };
-        auto issue_a_at = [&](const Src& s, int st) { issue_a(s, pos_of(st, 3)); };
-        auto issue_b_at = [&](const Src& s, int st) { issue_b(s, pos_of(st, 2)); };
-        // fragments (the 16x16x32 body's addressing)
-        const int sw = (r16 >> 1) & 7;
-        const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
-        const int a_base = (wm * UM * 16) * ROW, b_base = (wn * UN * 16) * ROW;
-        auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
-            return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
-        };
-
-        x3_stamp(a, 0);
-        const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
-        const int m0 = mt * BM, n0 = nt * BN;
-        Src cur;
-        src_of(cur, tile);
-        if (!prefetched) {
-            // first tile: the A3 prologue (A0 B0 A1 B1 A2)
-            issue_a_at(cur, 0);
-            issue_b_at(cur, 0);
-            if (nks > 1) {
-                issue_a_at(cur, 1);
-                issue_b_at(cur, 1);
-            }
-            if (nks > 2) issue_a_at(cur, 2);
-        }
-        // ---- wait for stage 0 (A0, B0): the prologue's wait, or after a prefetch
-        // the NOUT epilogue stores and A2 may stay in flight (A1, B1 retire too) ----
-        if (prefetched && full_prev && nks > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GA + NOUT) : "memory");
-        else if (prefetched) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (nks > 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + GA) : "memory");
-        else if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lds_barrier();
-        x3_stamp(a, 1);
-        f32x4 acc[UM][UN];
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        f16x8 ah[UM], al[UM], bh[UN], bl[UN];
-        auto read_a = [&](const char* st) {
-#pragma unroll
-            for (int i = 0; i < UM; ++i) {
-                ah[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_h);
-                al[i] = *(const f16x8*)(st + a_base + i * 16 * ROW + fo_l);
-            }
-        };
-        auto read_b = [&](int j, const char* st) {
-            bh[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_h);
-            bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
-        };
-        auto mma_col = [&](int j) {
-#pragma unroll
-            for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], ah[i], al[i], bh[j], bl[j], mfma);
-        };
-        read_a(smem);
-#pragma unroll
-        for (int j = 0; j < UN; ++j) read_b(j, bring);
-        int ca = 0, cb = 0;                                  // slots of A(t), B(t)
-        Pos pa = pos_of(3, 3), pb = pos_of(2, 2);             // the next A / B stages to issue
-        // one K-step (the A3 schedule): NP DMA pieces issued (GL: B(t+2) and A(t+3);
-        // GB: B only; 0); WA: A(t+2) may stay in flight at the top; FIRST: the
-        // previous epilogue's NOUT stores may too
-        auto kstep = [&](auto np, auto wa, auto first) {
-            constexpr int NP = decltype(np)::value;
-            if constexpr (decltype(first)::value) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA + NOUT) : "memory");
-            else if constexpr (decltype(wa)::value) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(GA) : "memory");
-            else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            lds_barrier();
-            ca = ca == 2 ? 0 : ca + 1;
-            cb ^= 1;
-            const char* sta = smem + ca * (BM * ROW);
-            const char* stb = bring + cb * (BN * ROW);
-            if constexpr (NP > 0) {
-                issue_b(cur, pb);
-                advance(pb, 2);
-            }
-            if constexpr (NP == GL) {
-                issue_a(cur, pa);
-                advance(pa, 3);
-            }
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                mma_col(j);
-                read_b(j, stb);
-            }
-            read_a(sta);
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                __builtin_amdgcn_sched_group_barrier(0x008, x3_nprod(P) * UM, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                if (NP > 0 && j * ((NP + UN - 1) / UN) < NP)
-                    __builtin_amdgcn_sched_group_barrier(0x020, (NP + UN - 1) / UN, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        using IGL = std::integral_constant<int, GL>;
-        using IGB = std::integral_constant<int, GB>;
-        using I0 = std::integral_constant<int, 0>;
-        using T1 = std::true_type;
-        using F0 = std::false_type;
-        int t = 0;
-        if (prefetched && full_prev && nks > 3) {
-            kstep(IGL{}, T1{}, T1{});
-            ++t;
-        }
-        for (; t + 3 < nks; ++t) kstep(IGL{}, T1{}, F0{});
-        if (t + 2 < nks) {
-            kstep(IGB{}, T1{}, F0{});
-            ++t;
-        }
-        if (t + 1 < nks) kstep(I0{}, F0{}, F0{});
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int j = 0; j < UN; ++j) mma_col(j);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this tile's DMA retired
-        x3_stamp(a, 2);
-
-        // ---- epilogue ----
-        // lane constants again, opaque: kept from before the K loop they would be
-        // live across it (the spill the per-tile derivation avoids)
-        lane = x3_lane_opaque();
-        const int r16e = lane & 15, qe = lane >> 4;
-        const int rowq = m0 + wm * UM * 16 + 4 * qe + (lane & 3);     // output row of this lane after the transpose, i = 0
-        const int ccol = (((lane >> 2) & 3) & 1) * 16 + (((lane >> 2) & 3) >> 1) * 8;   // P 1: column in a 32-column pair
-        const bool full = m0 + BM <= a.M;                    // every thread issues NOUT output stores
-        const int next = tile + G;
-        const bool has_next = next < T;
-        // A slot 2 (free until the next tile's third stage): the BN partials'
-        // scratch [8][BN], then the tile's column parameters [5][BN] — weight scale,
-        // and (EP) scale, shift, residual scale, residual shift
-        float* scr = (float*)(smem + 2 * BM * ROW);
-        float* prm = scr + 8 * BN;
-        const bool rsc = a.ep_rss != nullptr;
-        lds_sync();                                           // every wave done reading this tile's ring
-        // the column parameters by LDS-DMA, one 1-KiB piece per array (waves 0-4): a
-        // compiler-tracked load used after the prefetch below makes the compiler wait
-        // vmcnt(0) — for the prefetch too — before its first use
-        if (w == 0 && a.wscale) glds16(a.wscale + n0 + 4 * lane, (char*)prm);
-        if constexpr (EP) {
-            if (w == 1) glds16(a.ep_ss + n0 + 4 * lane, (char*)(prm + BN));
-            if (w == 2) glds16(a.ep_ss + a.K + n0 + 4 * lane, (char*)(prm + 2 * BN));
-            if (w == 3 && rsc) glds16(a.ep_rss + n0 + 4 * lane, (char*)(prm + 3 * BN));
-            if (w == 4 && rsc) glds16(a.ep_rss + a.K + n0 + 4 * lane, (char*)(prm + 4 * BN));
-        }
-        // ---- the next tile's first stages, into A slots 0-1 and B slots 0-1 ----
-        if (has_next) {
-            Src nxt;
-            src_of(nxt, next);
-            issue_a_at(nxt, 0);
-            issue_b_at(nxt, 0);
-            if (nks > 1) {
-                issue_a_at(nxt, 1);
-                issue_b_at(nxt, 1);
-            }
-        }
-        // ---- EP: the residual chunks of this lane's outputs (waited for at first
-        // use: with the prefetch, whose latency they share) ----
-        f16x8 res[EP ? UM : 1][UN / 2];
-        if constexpr (EP) {
-            if (a.ep_res) {
-#pragma unroll
-                for (int i = 0; i < UM; ++i)
-#pragma unroll
-                    for (int jp = 0; jp < UN / 2; ++jp) {
-                        const int m = rowq + 16 * i;
-                        res[i][jp] = f16x8{};
-                        if (m < a.M)
-                            res[i][jp] = __builtin_nontemporal_load(
-                                (const f16x8*)(a.ep_res + (long)m * a.K + n0 + wn * UN * 16 + 32 * jp + ccol));
-                    }
-            }
-        }
-        // the parameters' DMA landed (older than the prefetch pieces and the
-        // residual loads), then visible to every wave
-        if (has_next && nks > 1) {
-            if constexpr (EP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL + UM * UN / 2) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GL) : "memory");
-        } else if (has_next) {
-            if constexpr (EP) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL + UM * UN / 2) : "memory");
-            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GL) : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        lds_barrier();
-        float sc[UN];
-#pragma unroll
-        for (int j = 0; j < UN; ++j) sc[j] = a.wscale ? prm[wn * UN * 16 + j * 16 + r16e] : 1.f;
-        // ---- BN partials (generic merge, scratch in A slot 2) ----
-        const int rbase = m0 + wm * UM * 16 + 4 * qe;
-        if (!EP && a.part)
-            x3_bn_partials_w<BN, UM, UN, 16, 16>(
-                a, scr, m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
-                [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; });
-        x3_stamp(a, 3);
-        // ---- the output tile from registers ----
-        const int b4 = lane & 3;
-        if constexpr (P == 3) {
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int j = 0; j < UN; ++j) {
-                    f32x4 v = acc[i][j] * sc[j];
-                    x3_quad_transpose(v, b4);
-                    const int m = rowq + 16 * i;
-                    if (m < a.M)
-                        x3_st16((f32x4*)(a.y + (long)m * a.K + n0 + wn * UN * 16 + 16 * j + 4 * ((lane >> 2) & 3)), v,
-                                a.st_kind, 2);
-                }
-        } else {
-            // the fused epilogue's parameters of this lane's 8 columns come from prm
-            const float* ssl = prm + BN;                      // [4][BN]: scale, shift, residual scale, shift
-            const bool hres = a.ep_res != nullptr, relu = a.ep_relu != 0;
-            const bool aodd = (lane >> 2) & 1;
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int jp = 0; jp < UN / 2; ++jp) {
-                    f32x4 v0 = acc[i][2 * jp] * sc[2 * jp], v1 = acc[i][2 * jp + 1] * sc[2 * jp + 1];
-                    x3_quad_transpose(v0, b4);
-                    x3_quad_transpose(v1, b4);
-                    // fp16 y (the staged tile's rounding), then 8 consecutive columns:
-                    // even lane groups take the next group's block-j columns, odd ones the
-                    // previous group's block-(j+1) columns
-                    f16x8 h;
-                    float lo[4], hi[4];
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const float own = aodd ? v1[e] : v0[e];
-                        const float x0 = x3_dpp<0x104>(v0[e]);      // row_shl:4 (lane + 4)
-                        const float x1 = x3_dpp<0x114>(v1[e]);      // row_shr:4 (lane - 4)
-                        lo[e] = aodd ? x1 : own;
-                        hi[e] = aodd ? own : x0;
-                    }
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        h[e] = (_Float16)lo[e];
-                        h[4 + e] = (_Float16)hi[e];
-                    }
-                    const int m = rowq + 16 * i;
-                    const int col = wn * UN * 16 + 32 * jp + ccol;
-                    if constexpr (EP) {
-                        const f16x8 rv = hres ? res[i][jp] : f16x8{};
-#pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            float o = __fadd_rn(__fmul_rn((float)h[k], ssl[col + k]), ssl[BN + col + k]);
-                            if (hres)
-                                o = rsc ? __fadd_rn(o, __fadd_rn(__fmul_rn((float)rv[k], ssl[2 * BN + col + k]),
-                                                                 ssl[3 * BN + col + k]))
-                                        : __fadd_rn(o, (float)rv[k]);
-                            if (relu) o = o > 0.f ? o : 0.f;
-                            h[k] = (_Float16)o;
-                        }
-                        if (m < a.M) x3_st16((f16x8*)(a.y16 + (long)m * a.K + n0 + col), h, a.st_kind, 2);
-                    } else {
-                        if (m < a.M) x3_st16((f16x8*)(a.y16 + (long)m * a.K + n0 + col), h, a.st_kind, 1);
-                    }
-                }
-        }
-        x3_stamp(a, 4);
-        x3_stamp(a, 5);
-        if (!has_next) return;
-        // ---- the next tile's third A stage (its slot held the partials' scratch) ----
-        lds_sync();
-        if (nks > 2) {
-            Src nxt;
-            src_of(nxt, next);
-            issue_a_at(nxt, 2);
-        }
-        tile = next;
-        prefetched = true;
-        full_prev = full;
-    }
-}
 
 // ---------------------------------------------------------------------------
 // DUO body (conv_x3_duo_kernel<1>): plain-fp16 (P 1, config C4) convs on 256 x 128
@@ -3538,7 +3086,7 @@ static double sk_over(int nks) { return 0.2 + 19.0 / nks; }
 // at S = 3, C2 layer3 0.384 -> 0.418 ms at S = 5; profiles/r05_multi_*.  The tail
 // on 256x128 grids of >= 2 rounds (C2 layer2) measured neutral: C2 1753.0 vs 1755.5
 // img/s, C4 / C3 unchanged; profiles/r05_tail128_*_v2.)
-static int g_x3_split_tail = 0;                        // hkp_debug_x3_split_tail
+HKP_AB_KNOB(int, g_x3_split_tail, 0);                 // hkp_debug_x3_split_tail
 static long x3_tail_groups(long m_tiles, int nt, int nks, double* cost = nullptr) {
     const long G = x3_cus(), tiles = m_tiles * nt, tr = tiles % G;
     const long tm = m_tiles - tiles / G * G / nt;
@@ -3605,7 +3153,6 @@ struct X3Choice {
     bool halo = false;                 // conv_x3_halo_kernel<P>
     bool a3 = false;                   // conv_x3_a3_kernel<P> (256x256, 3-stage A ring)
     bool duo = false;                  // conv_x3_duo_kernel<1> (256x128, two 4-wave blocks per CU)
-    bool a3p = false;                  // conv_x3_a3p_kernel<P> (persistent A3, next tile's fill in the epilogue)
 };
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
@@ -3618,16 +3165,8 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
 // HKP_TILE_256 / 256_TAIL keep the 2-stage body)
 // DUO (the plain-fp16 256x128 two-blocks-per-CU body) where forced and legal;
 // other operand layouts plan as AUTO
-static int g_x3_pair128 = 1;                           // hkp_debug_x3_pair128
+HKP_AB_KNOB(int, g_x3_pair128, 1);                    // hkp_debug_x3_pair128
 static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo, int P) {
-    if (policy == HKP_TILE_A3P) {
-        if ((P == 1 || P == 3) && k % 256 == 0) {
-            X3Choice c{256, 16, false, false};
-            c.a3p = true;
-            return c;
-        }
-        policy = HKP_TILE_AUTO;
-    }
     if (policy == HKP_TILE_DUO) {
         if (P == 1 && k % DUO_BN == 0) {
             X3Choice c{DUO_BN, 16, false, false};
@@ -3715,7 +3254,6 @@ static const X3Choice X3_STEM{64, 16, true, false};
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
     if (c.duo) return snprintf(buf, len, "conv_x3_duo_kernel<%d>", P);
-    if (c.a3p) return snprintf(buf, len, "conv_x3_a3p_kernel<%d>", P);
     if (c.a3) return snprintf(buf, len, "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
@@ -3747,11 +3285,11 @@ static void launch_x3_p(const X3Choice& c, dim3 grid, hipStream_t st, const X3Ar
 
 // a.RS, a.cch (128-B lines per pixel), a.M ... set by the caller; P = operand
 // layout (3 packed f16x3 split, 1 plain fp16)
-static unsigned long long* g_x3_stamps = nullptr;     // hkp_debug_x3_stamps
-static int g_x3_stagger_ns = 0;                        // hkp_debug_x3_stagger
-static int g_x3_store = 0;                             // hkp_debug_x3_store
-static int g_duo_stagger_ns = -1;                      // hkp_debug_duo_stagger
-static int g_x3_prio = 0;                              // hkp_debug_x3_prio
+HKP_AB_KNOB(unsigned long long*, g_x3_stamps, nullptr);   // hkp_debug_x3_stamps
+HKP_AB_KNOB(int, g_x3_stagger_ns, 0);                 // hkp_debug_x3_stagger
+HKP_AB_KNOB(int, g_x3_store, 0);                      // hkp_debug_x3_store
+HKP_AB_KNOB(int, g_duo_stagger_ns, -1);               // hkp_debug_duo_stagger
+HKP_AB_KNOB(int, g_x3_prio, 0);                       // hkp_debug_x3_prio
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -3790,20 +3328,6 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.n_tiles = k / c.bn;
     a.nks = nks;
     a.sk_units = 0;
-    if (c.a3p && (a.add || a.ost || a.in_ss || (P != 1 && a.ep_ss))) {
-        // forward outputs only: other launches plan as AUTO
-        launch_x3(k, m_tiles, HKP_TILE_AUTO, P, st, a, ws, ws_bytes);
-        return;
-    }
-    if (c.a3p) {
-        const long tiles = m_tiles * a.n_tiles;
-        a.p_tiles = (int)tiles;
-        const dim3 gp((unsigned)std::min<long>(tiles, x3_cus()));
-        if (P == 1 && a.ep_ss) hipLaunchKernelGGL((conv_x3_a3p_kernel<1, true>), gp, dim3(512), 0, st, a);
-        else if (P == 1) hipLaunchKernelGGL((conv_x3_a3p_kernel<1, false>), gp, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_x3_a3p_kernel<3, false>), gp, dim3(512), 0, st, a);
-        return;
-    }
     if (c.duo) {
         // first-round stagger of the second block on each CU: half a block's
         // lifetime, ~(fill + epilogue + K loop) / 2 — hkp_debug_duo_stagger overrides
@@ -3915,9 +3439,10 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_A3P, "%s: unknown tile policy %d", who, d->tile);
-    HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8,
-                  "%s: tile policy %d is retired (the persistent conv, measured slower)", who, d->tile);
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_RESERVED_14, "%s: unknown tile policy %d", who,
+                  d->tile);
+    HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8 && d->tile != HKP_TILE_RESERVED_14,
+                  "%s: tile policy %d is retired (a persistent conv body, measured slower)", who, d->tile);
     return HKP_OK;
 }
 
@@ -4385,6 +3910,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
     return HKP_ERR_BAD_ARG;
 }
 
+#ifdef HKP_AB_KNOBS   // the A/B instruments (tools/ab_lib build only; include/hulkkp_ab.h)
 // Debug: forward conv launches record per-block phase clocks into buf (8 slots of
 // s_memrealtime per block: start, pipeline filled, K loop done, BN partials
 // done, fp16 tile staged, stores issued; 0 where a body records none); NULL
@@ -4413,4 +3939,5 @@ extern "C" void hkp_debug_duo_stagger(int32_t ns) { g_duo_stagger_ns = ns; }
 // Debug / A/B (tools/ only, not thread-safe): static wave priority in the A3 body's
 // K loop (X3Args::prio: 0 none, 1 waves 4-7, 2 waves 0-3 at s_setprio 1).
 extern "C" void hkp_debug_x3_prio(int32_t mode) { g_x3_prio = mode >= 0 && mode <= 2 ? mode : 0; }
+#endif
 

@@ -30,7 +30,7 @@ class ConvDesc(ctypes.Structure):
 # hkp_conv_desc.tile policies (include/hulkkp.h)
 (HKP_TILE_AUTO, HKP_TILE_NO_SK, HKP_TILE_SK, HKP_TILE_256, HKP_TILE_128_MF16, HKP_TILE_128_MF32, HKP_TILE_64_PAIR,
  HKP_TILE_RESERVED_7, HKP_TILE_RESERVED_8, HKP_TILE_256_TAIL, HKP_TILE_HALO, HKP_TILE_256_A3, HKP_TILE_AUTO_A3,
- HKP_TILE_DUO, HKP_TILE_A3P) = range(15)
+ HKP_TILE_DUO, HKP_TILE_RESERVED_14) = range(15)
 # hkp_conv_kernel_name ops
 HKP_KOP_FWD_X3, HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3, HKP_KOP_FWD_X3_W16, \
     HKP_KOP_FWD_X3_X16, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8 = range(9)
@@ -74,15 +74,6 @@ SIGNATURES = {
     "hkp_bn_apply_f16": (ctypes.c_int, [_I64, _I32, _P, _P, _P, _P, _I32, _P, _P, _P]),
     "hkp_bn_relu_maxpool": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P]),
     "hkp_head_fc": (ctypes.c_int, [_I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
-    "hkp_debug_x3_stamps": (None, [_P]),
-    "hkp_debug_x3_stagger": (None, [_I32]),
-    "hkp_debug_x3_split_tail": (None, [_I32]),
-    "hkp_debug_stem_pair": (None, [_I32]),
-    "hkp_debug_fin_regs": (None, [_I32]),
-    "hkp_debug_x3_pair128": (None, [_I32]),
-    "hkp_debug_x3_store": (None, [_I32]),
-    "hkp_debug_duo_stagger": (None, [_I32]),
-    "hkp_debug_x3_prio": (None, [_I32]),
     "hkp_bn_apply_head": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, _P, _P, _P, _P]),
     "hkp_upsample_sigmoid": (ctypes.c_int, [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _P]),
     "hkp_gauss_target": (ctypes.c_int, [_I32, _I32, _I32, _I32, _F, _P, _P, _P]),
@@ -147,6 +138,21 @@ SIGNATURES = {
     "hkp_jpeg_reconstruct": (ctypes.c_int, [_I32, _P, _P, _P, _P, _I64, _P, _P]),
 }
 
+# the A/B instruments of the tools-only build (include/hulkkp_ab.h, `make ab`);
+# bound only when the loaded library exports them — the product library does not
+AB_SIGNATURES = {
+    "hkp_debug_x3_stamps": (None, [_P]),
+    "hkp_debug_x3_stagger": (None, [_I32]),
+    "hkp_debug_x3_split_tail": (None, [_I32]),
+    "hkp_debug_stem_pair": (None, [_I32]),
+    "hkp_debug_fin_regs": (None, [_I32]),
+    "hkp_debug_x3_pair128": (None, [_I32]),
+    "hkp_debug_x3_store": (None, [_I32]),
+    "hkp_debug_duo_stagger": (None, [_I32]),
+    "hkp_debug_x3_prio": (None, [_I32]),
+}
+AB_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "tools", "ab_lib", "libhulkkp_ab.so")
+
 _lib = None
 
 
@@ -157,6 +163,14 @@ def use_library(path):
     if _lib is not None:
         raise HkpError("use_library: %s is already loaded" % LIB_PATH)
     LIB_PATH = path
+
+
+def use_ab_library():
+    """Tools only: load the A/B build (tools/ab_lib/libhulkkp_ab.so, `make -C
+    hulk-keypoints_amd/csrc ab`), whose hkp_debug_* knobs the product library lacks."""
+    if not os.path.exists(AB_LIB_PATH):
+        raise HkpError("the A/B build is missing (%s): run `make -C hulk-keypoints_amd/csrc ab`" % AB_LIB_PATH)
+    use_library(AB_LIB_PATH)
 
 
 def lib():
@@ -171,6 +185,11 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in AB_SIGNATURES.items():
+            if hasattr(L, name):
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
         _lib = L
     return _lib
 

@@ -109,29 +109,53 @@ def new_group_like(group=None):
 class ShardCheck:
     """The SyncBN empty-shard guard of a Trainer.  Given the job's batch size
     (`global_batch`: the same on every rank, sharded by shard_range) it needs no
-    collective at all: every rank holds >= 1 image iff global_batch >= world, a
-    value all ranks know — so a SyncBN step of the bench or of a sampler-fed loop
-    runs no host round trip.  Without it, one check_shards collective per step:
-    a rank cannot skip on its own (a cache of "sizes already seen" would let the
-    ranks whose size did not change skip while the one whose did waits in the
-    collective forever)."""
+    collective at all — each outcome is one that every rank reaches, or one that
+    cannot leave a peer waiting:
+      * global_batch < world: some rank's shard is empty; every rank computes the
+        same verdict and raises;
+      * this rank holds >= 1 image: it enters every SyncBN gather, whose merge
+        weights each rank by the row count it gathered (hkp_bn_finalize_ranks,
+        hkp_bn_bwd_finalize_ranks), so the statistics are the global batch's even
+        if the size differs from its shard_range share (a sampler that does not
+        pad its last batch): the step proceeds, with a warning;
+      * this rank holds no image although the global batch covers every rank: it
+        alone would skip the gathers and leave its peers waiting in them, and an
+        exception can be caught and the process kept alive — so the process exits
+        (status 3) after writing why to stderr; the peers' collectives then fail
+        (gloo: connection closed; RCCL: the watchdog) instead of hanging.
+    Without global_batch, one check_shards collective per step: a rank cannot skip
+    on its own (a cache of "sizes already seen" would let the ranks whose size did
+    not change skip while the one whose did waits in the collective forever)."""
 
     def __init__(self, group=None):
         self.group = group
         self.collectives = 0            # host collectives run (tests)
+        self.mismatches = 0             # steps whose local size was not the shard_range share
 
     def __call__(self, n_local, global_batch=None):
         if not dist.is_initialized() or dist.get_world_size(self.group) == 1:
             return
         n = dist.get_world_size(self.group)
         if global_batch is not None:
-            lo, hi = shard_range(int(global_batch), _ranks(self.group).index(dist.get_rank()), n)
             if int(global_batch) < n:
                 raise ValueError("SyncBN needs at least one image on every rank (global batch %d < world size %d)"
                                  % (global_batch, n))
+            lo, hi = shard_range(int(global_batch), _ranks(self.group).index(dist.get_rank()), n)
+            if int(n_local) < 1:
+                import os
+                import sys
+                sys.stderr.write("hkp.parallel.ShardCheck: rank %d holds no image of the global batch %d (its "
+                                 "shard_range share is %d); exiting so that the other ranks' SyncBN gathers fail "
+                                 "instead of waiting for it\n" % (dist.get_rank(), global_batch, hi - lo))
+                sys.stderr.flush()
+                os._exit(3)
             if int(n_local) != hi - lo:
-                raise ValueError("SyncBN: this rank holds %d images, its shard_range share of the global batch %d "
-                                 "is %d" % (n_local, global_batch, hi - lo))
+                if self.mismatches == 0:
+                    import warnings
+                    warnings.warn("SyncBN: rank %d holds %d images, its shard_range share of the global batch %d "
+                                  "is %d; the BN statistics weight each rank by its own count"
+                                  % (dist.get_rank(), n_local, global_batch, hi - lo))
+                self.mismatches += 1
             return
         check_shards(n_local, self.group)
         self.collectives += 1

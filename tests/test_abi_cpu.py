@@ -31,6 +31,20 @@ def test_library_exports_every_declared_symbol():
     assert _lib.version().startswith("hulkkp")
 
 
+def test_product_library_has_no_ab_knobs():
+    """The A/B instruments (hkp_debug_*, include/hulkkp_ab.h) exist only in the tools
+    build: the product library exports none of them and its header declares none."""
+    from hkp import _lib
+    path = os.path.join(REPO, "hulk-keypoints_amd", "hkp", "libhulkkp.so")
+    L = ctypes.CDLL(path)
+    assert _lib.AB_SIGNATURES
+    for n in _lib.AB_SIGNATURES:
+        assert not hasattr(L, n), "product library exports the A/B knob " + n
+    assert not [n for n in declared_functions() if n.startswith("hkp_debug_")]
+    syms = open(path, "rb").read()
+    assert b"hkp_debug_" not in syms
+
+
 def _kernel_scratch(blob):
     """(symbol, private_segment_fixed_size) of every gfx950 kernel in a library's
     embedded code objects, read from the msgpack kernel metadata (uncompressed)."""

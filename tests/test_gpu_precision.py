@@ -861,83 +861,3 @@ def test_fused_input_bn_network_bitexact(cuda_device, bb, prec, b, hw, fused):
         outs.append((hm, yx))
     assert fused in syms, syms
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-
-# (n, h, w, cin, cout, k, stride, pad, dil): the persistent A3 body (HKP_TILE_A3P)
-# over grids of more than one round (the next tile's stages prefetched in the
-# epilogue), K-step counts 1-4 and long, a partial last tile, dilated 3x3 taps
-A3P_CASES = [
-    (8, 30, 80, 64, 256, 1, 1, 0, 1),        # 75 tiles: one per block (no prefetch)
-    (40, 30, 80, 64, 512, 1, 1, 0, 1),       # 750 m-tile x 2 = 750 tiles: 3 rounds, one K-step
-    (40, 30, 80, 128, 256, 1, 1, 0, 1),      # 2 K-steps (plain fp16: 128 channels)
-    (40, 30, 80, 192, 256, 1, 1, 0, 1),      # 3
-    (41, 30, 79, 256, 256, 1, 1, 0, 1),      # 4 K-steps, ragged M (partial last tile)
-    (12, 30, 40, 256, 512, 3, 1, 2, 2),      # dilated 3x3, 36 / 72 K-steps
-    (20, 31, 41, 128, 256, 1, 2, 0, 1),      # 1x1 stride 2
-]
-
-
-@pytest.mark.parametrize("case", A3P_CASES)
-@pytest.mark.parametrize("prec", ["f16x3", "f16"])
-def test_a3p_persistent_equals_a3(cuda_device, case, prec):
-    """conv_x3_a3p_kernel (HKP_TILE_A3P: the A3 body as a persistent grid whose
-    epilogue prefetches the next tile's first stages and stores from registers)
-    against the one-tile 256x256 bodies: the same MFMA sequence per tile, so y is
-    bit-identical to the 2-stage body's (no split-K tail there) and the BN partials
-    agree; and against fp64."""
-    from hkp import ops
-    from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_TILE_256, HKP_TILE_A3P, ConvDesc
-    n, h, w, cin, cout, k, st, pad, dil = case
-    d = cuda_device
-    x = F.relu(rand(n, h, w, cin, seed=201))
-    wt = rand(cout, k, k, cin, seed=202, scale=(2.0 / (k * k * cout)) ** 0.5)
-    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, HKP_TILE_A3P)
-    if prec == "f16x3":
-        if cin % 32:
-            pytest.skip("f16x3 needs Cin % 32")
-        xs = ops.bn_apply(x.to(d), torch.cat([torch.ones(cin), torch.zeros(cin)]).to(d), relu=False, split=3,
-                          keep_fp32=False)
-        wp = ops.weight_pack_x3(wt.to(d))
-        assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_a3p_kernel<3>"
-        y0, p0 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256)
-        y1, p1 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_A3P)
-        y2, p2 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_A3P)       # back to back: same bits
-        ref = F.conv2d(x.double().permute(0, 3, 1, 2), wt.double().permute(0, 3, 1, 2), None, st, pad, dil)
-        err = (y1.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item()
-        assert err < 2e-6 * ref.abs().max().item(), err
-    else:
-        if cin % 64:
-            pytest.skip("plain fp16 needs Cin % 64")
-        x16 = x.half().to(d)
-        wp = ops.weight_pack_f16(wt.to(d))
-        assert ops.kernel_name(desc, HKP_KOP_FWD_F16) == "conv_x3_a3p_kernel<1>"
-        y0, p0 = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, sk=False, tile=HKP_TILE_256)
-        y1, p1 = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, tile=HKP_TILE_A3P)
-        y2, p2 = ops.conv2d_fwd_f16(x16, wp, st, pad, dil, tile=HKP_TILE_A3P)
-    torch.cuda.synchronize()
-    assert torch.equal(y1, y0), (y1.float() - y0.float()).abs().max().item()
-    assert torch.equal(y2, y1) and torch.equal(p2, p1)
-    assert torch.allclose(p1, p0, rtol=1e-5, atol=1e-5 * p0.abs().max().item())
-
-
-@pytest.mark.parametrize("res_kind", ["none", "raw", "scaled"])
-def test_a3p_fused_epilogue_equals_conv_plus_apply(cuda_device, res_kind):
-    """The persistent body's fused BN + residual + ReLU epilogue (plain fp16, the
-    register-transposed 16-B chunks) == its own conv followed by bn_apply_f16, bit
-    for bit, over a multi-round grid with a partial last tile."""
-    from hkp import ops
-    from hkp._lib import HKP_TILE_A3P
-    d = cuda_device
-    n, h, w, c, k = 41, 30, 79, 128, 512
-    g = torch.Generator(device=d).manual_seed(21)
-    x = torch.relu(torch.randn(n, h, w, c, device=d, generator=g)).half()
-    wp = ops.weight_pack_f16(torch.randn(k, 1, 1, c, device=d, generator=g) * 0.1)
-    ss = torch.cat([torch.rand(k, device=d, generator=g) + 0.5, torch.rand(k, device=d, generator=g) - 0.5])
-    res = rss = None
-    if res_kind != "none":
-        res = torch.randn(n, h, w, k, device=d, generator=g).half()
-    if res_kind == "scaled":
-        rss = torch.cat([torch.rand(k, device=d, generator=g) + 0.5, torch.rand(k, device=d, generator=g) - 0.5])
-    y, _ = ops.conv2d_fwd_f16(x, wp, stats=False, tile=HKP_TILE_A3P)
-    ref = ops.bn_apply_f16(y, ss, res=res, res_ss=rss, relu=True)
-    got = ops.conv2d_fwd_f16_bn(x, wp, ss, res=res, res_ss=rss, relu=True, tile=HKP_TILE_A3P)
-    assert torch.equal(got, ref)

@@ -127,14 +127,61 @@ def _groups_worker(rank, world, port, q):
     for _ in range(2):
         t.shard_check(4 - rank)
     ok &= t.shard_check.collectives == 2
-    for bad in ((1 - rank, 1), (5, 7)):       # global batch < world; a share that is not shard_range's
-        try:
-            t.shard_check(*bad)
-            ok = False
-        except ValueError:
-            pass
+    try:                                        # global batch < world: every rank raises
+        t.shard_check(1 - rank, 1)
+        ok = False
+    except ValueError:
+        pass
+    # only rank 1's size differs from its shard_range share (a sampler that does not
+    # pad its last batch): no rank raises, both go on into the gathers, which carry
+    # the counts (a raise on one rank left the other waiting in them)
+    t.shard_check(4 if rank == 0 else 2, global_batch=7)
+    ok &= t.shard_check.mismatches == rank
+    st = torch.tensor([float(rank), 0.0, 4.0 if rank == 0 else 2.0], dtype=torch.float64)
+    g = parallel.gather_bn_stats(st, t.bn_group)
+    ok &= g[:, 2].tolist() == [4.0, 2.0]
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
+
+
+def _empty_shard_worker(rank, world, port, q):
+    import sys
+    sys.path[:0] = [REPO, PKG]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hkp import parallel
+    chk = parallel.ShardCheck()
+    grp = parallel.new_group_like()
+    q.put((rank, "checking"))
+    chk(0 if rank == 1 else 4, global_batch=7)      # rank 1: no image although 7 >= world
+    try:                                            # rank 0 goes on into a SyncBN gather
+        parallel.gather_bn_stats(torch.zeros(3, dtype=torch.float64), grp)
+        q.put((rank, "gathered"))
+    except Exception as e:                          # the peer exited: the gather fails, it does not wait
+        q.put((rank, "failed: %s" % type(e).__name__))
+
+
+def test_shard_check_empty_rank_does_not_hang_peers_gloo_world2():
+    """a rank whose shard is empty while the declared global batch covers
+    every rank exits (status 3) instead of raising, so its peer's next SyncBN gather
+    fails instead of waiting for it forever."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_empty_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode is not None for p in procs), "a rank hung"
+    assert procs[1].exitcode == 3
+    msgs = []
+    while len(msgs) < 3:                            # (rank 1's os._exit may drop its queued message)
+        try:
+            msgs.append(q.get(timeout=5))
+        except Exception:
+            break
+    assert (0, "gathered") not in msgs and any(r == 0 and m.startswith("failed") for r, m in msgs), msgs
 
 
 def test_trainer_syncbn_own_communicator_gloo_world2():

@@ -77,9 +77,11 @@ def main():
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
     args = ap.parse_args()
+    from hkp import _lib
     if args.lib:
-        from hkp import _lib
         _lib.use_library(os.path.abspath(args.lib))
+    elif os.path.exists(_lib.AB_LIB_PATH):
+        _lib.use_ab_library()                   # its hkp_debug_* knobs (include/hulkkp_ab.h)
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     from hkp._lib import lib
@@ -87,8 +89,11 @@ def main():
              for d in args.duo_staggers.split(",")]
 
     def set_store(k, d=-1):
-        lib().hkp_debug_x3_store(k)
-        lib().hkp_debug_duo_stagger(d)
+        if hasattr(lib(), "hkp_debug_x3_store"):
+            lib().hkp_debug_x3_store(k)
+            lib().hkp_debug_duo_stagger(d)
+        elif (k, d) != (0, -1):
+            raise SystemExit("--stores / --duo-staggers need the A/B build: make -C hulk-keypoints_amd/csrc ab")
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):

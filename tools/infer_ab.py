@@ -35,8 +35,11 @@ def set_knobs(lib, kv):
         if k == "stem_img":                     # a Python-side switch (hkp.ops), not a library knob
             from hkp import ops
             ops.STEM_IMAGE_DIRECT = bool(v)
-        else:
+        elif hasattr(lib, KNOBS[k][0]):
             getattr(lib, KNOBS[k][0])(v)
+        elif v != KNOBS[k][1]:      # the product library has no knobs (include/hulkkp_ab.h)
+            raise SystemExit("knob %s=%d needs the A/B build: make -C hulk-keypoints_amd/csrc ab, then --ab"
+                             % (k, v))
 
 
 def parse(form):
@@ -63,7 +66,11 @@ def main():
     ap.add_argument("--precision", default="f16x3")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ab", action="store_true", help="load the A/B build (tools/ab_lib, its hkp_debug_* knobs)")
     args = ap.parse_args()
+    if args.ab:
+        from hkp import _lib
+        _lib.use_ab_library()
     import hkp
     from hkp.policy import Policy
     from oracle import recipe

@@ -13,12 +13,16 @@
 #   infer_ab  C2 / C4 inference policy A/Bs in one process (tools/infer_ab.py): the A3
 #             body vs the 2-stage body + tail launch, the fused input BN on / off
 #   final     GPU suite, smoke(), default bench line
+# Retired (round 5): the fused-BN A3 body (FB), tools/bnin_ab.py and the
+# Policy.fuse_input_bn_a3 field were removed; the profile / fb / fb_prof recipes
+# are kept as the record of how the round-4 profiles were made and refuse to run.
 set -e
 export TMPDIR=/tmp
 cmd=${1:?subcommand}
 O=gpurun_out/$cmd; mkdir -p $O
 case $cmd in
 profile)
+    echo "$cmd: retired recipe (its tool / Policy field no longer exists)" >&2; exit 2
     bash tools/round_profile.sh r04_v2
     timeout -k 10 300 python -u tools/bnin_ab.py > gpurun_out/r04_v2/bnin_ab.log 2>&1
     bash tools/bench_ab.sh train_a3 "--mode train" "--mode train --tune dgrad_overlap_tile=11" 2
@@ -26,12 +30,14 @@ profile)
         --batch 32 --steps 5 --warmup 2 --no-cpu-baseline > $O/bench_c5.log 2>&1
     ;;
 fb)
+    echo "$cmd: retired recipe (its tool / Policy field no longer exists)" >&2; exit 2
     timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
         tests/test_gpu_precision.py -k "fused_input_bn" > $O/pytest_fb.log 2>&1
     timeout -k 10 300 python -u tools/bnin_ab.py > $O/bnin_ab.log 2>&1
     bash tools/bench_ab.sh fb_fuse "--tune fuse_input_bn_a3=1" "" 3 > $O/ab_fuse.txt 2>&1
     ;;
 fb_prof)
+    echo "$cmd: retired recipe (its tool / Policy field no longer exists)" >&2; exit 2
     i=0
     for cfg in "--tune fuse_input_bn_a3=1" "" "--tune x3_tile=9"; do
         i=$((i + 1))

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--shapes", default="c4_l4_c3,c4_l4_c1,c4_l3_c3,c4_l3_c1,c4_l1_c3,c4_l4_c2,layer4,layer3")
     args = ap.parse_args()
     from hkp import ops
+    from hkp import _lib
+    _lib.use_ab_library()                       # the hkp_debug_* knobs (include/hulkkp_ab.h)
     from hkp._lib import lib
     vals = [int(v) for v in args.ns.split(",")]
     dev = torch.device("cuda", 0)

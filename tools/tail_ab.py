@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--shapes", default="layer3,t4,t3,c4_l4_c2,c4_l3_c2")
     args = ap.parse_args()
     from hkp import ops
+    from hkp import _lib
+    _lib.use_ab_library()                       # the hkp_debug_* knobs (include/hulkkp_ab.h)
     from hkp._lib import lib
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)

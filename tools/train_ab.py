@@ -54,7 +54,11 @@ def main():
     ap.add_argument("--backbone", default="resnet34")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--ab", action="store_true", help="load the A/B build (tools/ab_lib, its hkp_debug_* knobs)")
     args = ap.parse_args()
+    if args.ab:
+        from hkp import _lib
+        _lib.use_ab_library()
     import hkp
     from hkp import train as hkp_train
     from hkp.policy import Policy

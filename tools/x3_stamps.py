@@ -21,6 +21,8 @@ PHASES = ["fill", "kloop", "partials|stores(x3)", "stage|partials(x3)", "store"]
 
 def main():
     from hkp import ops
+    from hkp import _lib
+    _lib.use_ab_library()                       # the hkp_debug_* knobs (include/hulkkp_ab.h)
     from hkp._lib import lib
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
