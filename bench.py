@@ -492,14 +492,20 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
     if t_meas > 0:
         roof["frac_of_roofline"] = t_att / t_meas
         roof["hbm_bound_share_of_attainable"] = t_hbm / t_att if t_att > 0 else 0.0
-    tag = {"infer": "infer_c2", "train": "train_c3"}[mode]
-    c4 = (args.backbone, K, H, W) == ("resnet50", 8, 480, 640) and precision == "f16" and mode == "infer"
-    c5 = (args.backbone, K, H, W) == ("resnet50", 8, 960, 1280) and precision == "f16x3" and mode == "train"
+    # the committed profiles of this exact workload (batch included: a trace's average
+    # launch time belongs to its own launch sizes)
+    r34 = (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3"
+    c4 = (args.backbone, K, H, W) == ("resnet50", 8, 480, 640) and precision == "f16" and mode == "infer" and B == 128
+    c5 = (args.backbone, K, H, W) == ("resnet50", 8, 960, 1280) and precision == "f16x3" and mode == "train" \
+        and B == 32
+    tag = None
+    if r34:
+        tag = {("infer", 32): "infer_c2", ("infer", 8): "b8", ("train", 8): "train_c3"}.get((mode, B))
     if c4:
         tag = "infer_c4"
     if c5:
         tag = "train_c5"
-    if ((args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3") or c4 or c5:
+    if tag is not None:
         (roof["traffic"], roof["traffic_source"], roof["pmc_pass_avg_ms"],
          roof["folded_kernel"]) = pmc_traffic(dom_sym, tag)
         # the kernel trace of the bench command itself (not the serialised PMC pass)
@@ -509,8 +515,15 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
         # the main stream's dgrad shares the CUs, so the conv events add up to more
         # than the step and `frac` prices shared CU time as exclusive
         roof["timing"] = "overlapped (side-stream wgrad events share CUs with the main stream)"
-        if roof.get("rocprof_avg_ms"):
-            roof["frac_from_trace"] = (fl / cnt) * passes / (roof["rocprof_avg_ms"] * 1e-3) / 1e12 / peak
+    if roof.get("rocprof_avg_ms"):
+        # the line reproduces from profiles/: `achieved` / `frac` use the committed
+        # rocprofv3 kernel trace's average duration of this symbol; the HIP-event
+        # figures of this run stay beside them
+        roof["achieved_events"], roof["frac_events"] = roof["achieved"], roof["frac"]
+        roof["achieved"] = (fl / cnt) * passes / (roof["rocprof_avg_ms"] * 1e-3) / 1e12
+        roof["frac"] = roof["achieved"] / peak
+        roof["frac_from_trace"] = roof["frac"]
+        roof["frac_source"] = "rocprof trace (%s); frac_events: this run's HIP events" % roof["rocprof_source"]
     return {"value": value, "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
             "batch_per_gpu": B, "global_batch": B * world, "roofline": roof,
             "model_tflops": value / world * fl_img * (3 if mode == "train" else 1) / 1e12,

@@ -15,6 +15,8 @@ arithmetic, SyncBN group, measured tuning choices) as an argument — None means
 the default policy; nothing here is process-global except caches keyed by
 parameter identity and version.
 """
+import json
+import os
 import weakref
 
 import torch
@@ -38,17 +40,31 @@ def _finalize_args(bn):
     return dict(momentum=bn.momentum if bn.momentum is not None else 0.1, eps=bn.eps)
 
 
+def _fold_request(bn, pol):
+    """An ops.FoldBN for the conv producing `bn`'s input when the policy folds the
+    finalize into it (train-mode statistics, per rank), else None."""
+    if not (pol.fold_bn and bn.training) or parallel.active_sync_group(pol) is not None:
+        return None
+    return ops.FoldBN(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                      **_finalize_args(bn))
+
+
 def _bn_params_many(items, pol):
-    """[(bn, partials, count)] → [(scale_shift, mean_invstd)]: batch statistics in
-    training mode (and the running-stat update, like nn.BatchNorm2d.forward),
-    running stats otherwise.  Under SyncBN the layers' statistics blocks ride ONE
-    all-gather (layers whose statistics are ready together: a block's last BN and
-    its downsample BN)."""
+    """[(bn, partials, count[, fold])] → [(scale_shift, mean_invstd)]: batch
+    statistics in training mode (and the running-stat update, like
+    nn.BatchNorm2d.forward) — already computed by the conv where it folded the
+    finalize (fold.done) — running stats otherwise.  Under SyncBN the layers'
+    statistics blocks ride ONE all-gather (layers whose statistics are ready
+    together: a block's last BN and its downsample BN)."""
     sync = parallel.active_sync_group(pol)
     out = [None] * len(items)
     gather = []
-    for i, (bn, part, count) in enumerate(items):
-        if not bn.training:
+    for i, item in enumerate(items):
+        bn, part, count = item[:3]
+        fold = item[3] if len(item) > 3 else None
+        if fold is not None and fold.done:
+            out[i] = (fold.scale_shift, fold.mean_invstd)
+        elif not bn.training:
             out[i] = ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
         elif sync is None:
             out[i] = ops.bn_finalize(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var,
@@ -193,6 +209,49 @@ def prepack_x3(resnet, flip, pol=None):
         _prepack_plans.pop(key, None)
 
 
+# the measured forward tile plan (hkp/tile_plan.json, tools/tile_sweep.py): shape key
+# -> HKP_TILE_* policy; read once (a constant table, not a switch).  Lookups of
+# shapes the table does not hold are counted per key (tests: every conv of the
+# measured workloads is planned).
+_TILE_PLAN = None
+PLAN_MISSES = {}
+
+
+def _tile_plan_table():
+    global _TILE_PLAN
+    if _TILE_PLAN is None:
+        try:
+            with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "tile_plan.json")) as f:
+                shapes = json.load(f)["shapes"]
+            _TILE_PLAN = {k: int(v["tile"]) for k, v in shapes.items()}
+        except (OSError, ValueError, KeyError):
+            _TILE_PLAN = {}
+    return _TILE_PLAN
+
+
+def plan_key(kind, x_shape, conv):
+    """Plan-table key of a forward conv: kind (x3 / f16 / f16bn) | n | h | w | cin |
+    cout | k | stride | pad | dil, from the operand's NHWC shape."""
+    n, h, w, c = x_shape
+    cin = c // 2 if kind == "x3" else c
+    k, r = conv.weight.shape[0], conv.weight.shape[1]
+    return "|".join(str(v) for v in (kind, n, h, w, cin, k, r, _i(conv.stride), _i(conv.padding), _i(conv.dilation)))
+
+
+def _planned_tile(kind, x_shape, conv, pol, forced):
+    """The HKP_TILE_* of a forward conv: the policy's own field when it forces one,
+    else the measured plan's choice for this shape (Policy.tile_plan), else 0 (the
+    C planner)."""
+    if forced or not pol.tile_plan:
+        return forced
+    key = plan_key(kind, x_shape, conv)
+    t = _tile_plan_table().get(key)
+    if t is None:
+        PLAN_MISSES[key] = PLAN_MISSES.get(key, 0) + 1
+        return 0
+    return t
+
+
 def _pack_weight_x3(w):
     """Cached packed f16x3 split of a KRSC weight (conv2d_fwd_x3's operand)."""
     return _cached_split(w, "x3", ops.weight_pack_x3)
@@ -203,36 +262,40 @@ def conv_bn(conv, bn, x, pol=None, layout="nhwc"):
     x: fp32 NHWC (optionally carrying its producer's operand split), a split-only
     activation (fp16, see ops.bn_apply keep_fp32=False), or NCHW for the stem."""
     pol = resolve(pol)
-    y, part = _conv_fwd(conv, bn, x, pol, layout)
-    ss, mi = _bn_params(bn, part, y.numel() // y.shape[-1], pol)
+    fold = _fold_request(bn, pol)
+    y, part = _conv_fwd(conv, bn, x, pol, layout, fold=fold)
+    ss, mi = _bn_params_many([(bn, part, y.numel() // y.shape[-1], fold)], pol)[0]
     return y, ss, mi
 
 
-def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
+def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True, fold=None):
     """The conv of conv_bn → (y, BN tile partials or None); sk=False: no stream-K.
-    f16x3 and f16 run on the LDS-DMA MFMA kernels (conv_x3.hip); shapes those do
-    not take (Cout % 64, or Cin % 64 for f16) run the exact fp32 MFMA kernel, which
-    needs the fp32 activation."""
+    f16x3 and f16 run on the LDS-DMA MFMA kernels (conv_x3.hip), which fold the
+    BN finalize in when given `fold` (ops.FoldBN; fold.done afterwards); shapes
+    those do not take (Cout % 64, or Cin % 64 for f16) run the exact fp32 MFMA
+    kernel, which needs the fp32 activation (and leaves fold undone)."""
     passes = pol.passes
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     if isinstance(x, _PendingBN):
         wp = _pack_weight_x3(conv.weight) if x.y.dtype == torch.float32 else \
             _cached_split(conv.weight, "f16", ops.weight_pack_f16)
         return ops.conv2d_fwd_bnin(x.y, x.ss, wp, st, pd, dl, stats=bn.training, sk=sk,
-                                   tile=_fwd_tile(conv, pol, x.y.dtype == torch.float16))
+                                   tile=_fwd_tile(conv, pol, x.y.dtype == torch.float16), fold=fold)
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
     if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd,
                                                                  dl):
         return ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
-                                      stats=bn.training)
+                                      stats=bn.training, fold=fold)
     if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
         return ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training, sk=sk,
-                                 products=pol.products, tile=pol.x3_tile)
+                                 products=pol.products, tile=_planned_tile("x3", sp[0].shape, conv, pol, pol.x3_tile),
+                                 fold=fold)
     if layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
+        forced = pol.f16_tile_1x1 if conv.weight.shape[1] == 1 else pol.f16_tile_kxk
         return ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
-                                  stats=bn.training, sk=sk,
-                                  tile=pol.f16_tile_1x1 if conv.weight.shape[1] == 1 else pol.f16_tile_kxk)
+                                  stats=bn.training, sk=sk, tile=_planned_tile("f16", sp[0].shape, conv, pol, forced),
+                                  fold=fold)
     if x.dtype != torch.float32:
         raise ops.HkpError("conv %s under precision %r: no LDS-DMA kernel for this shape and no fp32 input "
                            "for the fp32 kernel" % (tuple(conv.weight.shape), pol.precision))
@@ -340,7 +403,7 @@ def stem_forward(resnet, x_nchw, trace=None, pol=None, next_convs=()):
     return out
 
 
-def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_convs=()):
+def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_convs=(), next_pol=None):
     """One BasicBlock / Bottleneck.  x: fp32 NHWC (with its split attached) or, in
     inference, a split-only activation.  In inference the block output is written
     split-only too unless `final` (the head reads fp32) or a consumer conv in
@@ -348,8 +411,11 @@ def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_c
     its residual add reads hi + lo.  head = (w [K,C], bias [K]) (inference, last
     block): the tail BN apply runs fused with the K-row head and the block returns
     the lowres logits instead (hkp_bn_apply_head).  Under SyncBN the last BN and
-    the downsample BN share one statistics gather."""
+    the downsample BN share one statistics gather.  next_pol: the next block's
+    policy where it computes in another arithmetic (Policy.stage_precision; the
+    block output is then written in the next block's operand format)."""
     pol = resolve(pol)
+    npol = next_pol if next_pol is not None else pol
     rec = {} if trace is not None else None
     # producers also write the next conv's operand split; an activation only a
     # conv consumes (inside the block, no backward trace) is written split-only
@@ -379,36 +445,43 @@ def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_c
         else:
             a = act(y, s, convs[i + 1])
         ys.append(y), sss.append(s), mis.append(m), acts.append(a)
-    if rec is None and head is None and not final and _gram_fusable(block, a, pol):
+    if rec is None and head is None and not final and npol.passes == pol.passes and _gram_fusable(block, a, pol):
         return _bottleneck_tail_gram(block, x, a, pol)
     # the last conv and the downsample conv, then both BN parameter sets together
-    y_last, part_last = _conv_fwd(convs[-1], bns[-1], a, pol)
-    items = [(bns[-1], part_last, y_last.numel() // y_last.shape[-1])]
+    fold_last = _fold_request(bns[-1], pol)
+    y_last, part_last = _conv_fwd(convs[-1], bns[-1], a, pol, fold=fold_last)
+    items = [(bns[-1], part_last, y_last.numel() // y_last.shape[-1], fold_last)]
     yd = None
     if block.downsample is not None:
         xd = x
         if y_last.dtype == torch.float16 and x.dtype != torch.float16:
             xd = ops.split_of(x)[0]
-        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], xd, pol)
-        items.append((block.downsample[1], part_d, yd.numel() // yd.shape[-1]))
+        fold_d = _fold_request(block.downsample[1], pol)
+        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], xd, pol, fold=fold_d)
+        items.append((block.downsample[1], part_d, yd.numel() // yd.shape[-1], fold_d))
     params = _bn_params_many(items, pol)
     (last_s, last_m) = params[0]
     sd, md = params[1] if yd is not None else (None, None)
     ys.append(y_last), sss.append(last_s), mis.append(last_m)
     if rec is not None:
         rec.update(x=x, y=ys, ss=sss, mi=mis, act=acts)
-    pl = _split_for(y_last.shape[-1], pol)
-    keep_out = keep or final or pl != 3 or not _consumers_take_split(next_convs, pol)
+    pl = _split_for(y_last.shape[-1], npol)
+    keep_out = keep or final or pl != 3 or not _consumers_take_split(next_convs, npol)
     if head is not None:
         if yd is not None:
             return ops.bn_apply_head(y_last, last_s, yd, sd, *head)
         res = ops.split_of(x)[0] if (y_last.dtype == torch.float16 and x.dtype != torch.float16) else x
         return ops.bn_apply_head(y_last, last_s, res, None, *head)
     if y_last.dtype == torch.float16:                 # plain-fp16 path: fp16 residual stream
+        to_x3 = npol.passes == 3                      # the next stage is f16x3: fp32 + its packed split
         if yd is not None:
-            return ops.bn_apply_f16(y_last, last_s, res=yd, res_ss=sd, relu=True, keep_fp32=final)
-        res = x if x.dtype == torch.float16 else ops.split_of(x)[0]
-        return ops.bn_apply_f16(y_last, last_s, res=res, relu=True, keep_fp32=final)
+            out = ops.bn_apply_f16(y_last, last_s, res=yd, res_ss=sd, relu=True, keep_fp32=final or to_x3)
+        else:
+            res = x if x.dtype == torch.float16 else ops.split_of(x)[0]
+            out = ops.bn_apply_f16(y_last, last_s, res=res, relu=True, keep_fp32=final or to_x3)
+        if to_x3:
+            out._hkp_split = (ops.split_pack_x3(out), 3)
+        return out
     if yd is not None:
         out = ops.bn_apply(y_last, last_s, res=yd, res_ss=sd, relu=True, split=pl, keep_fp32=keep_out)
         if rec is not None:
@@ -453,14 +526,16 @@ def _bottleneck_tail_gram(block, x, a2, pol):
         ss3, _ = ops.bn_eval_params(bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps)
     x16 = x if x.dtype == torch.float16 else ops.split_of(x)[0]
     if block.downsample is not None:
-        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], x16, pol)
-        sd, _ = _bn_params(block.downsample[1], part_d, yd.numel() // yd.shape[-1], pol)
-        return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=yd, res_ss=sd, relu=True, tile=_fused_tile(pol))
-    return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=x16, relu=True, tile=_fused_tile(pol))
+        fold_d = _fold_request(block.downsample[1], pol)
+        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], x16, pol, fold=fold_d)
+        sd, _ = _bn_params_many([(block.downsample[1], part_d, yd.numel() // yd.shape[-1], fold_d)], pol)[0]
+        return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=yd, res_ss=sd, relu=True, tile=_fused_tile(pol, a2, c3))
+    return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=x16, relu=True, tile=_fused_tile(pol, a2, c3))
 
 
-def _fused_tile(pol):
-    return pol.f16_tile_1x1 if pol.f16_tile_fused < 0 else pol.f16_tile_fused
+def _fused_tile(pol, a2, c3):
+    forced = pol.f16_tile_1x1 if pol.f16_tile_fused < 0 else pol.f16_tile_fused
+    return _planned_tile("f16bn", a2.shape, c3, pol, forced)
 
 
 def _blocks(resnet):
@@ -473,15 +548,30 @@ def backbone_forward(resnet, x_nchw, trace=None, head=None, pol=None):
     head = (w [K,C], bias [K]) (inference): returns the head's lowres logits
     [B,K,h,w] instead, the last block's BN apply fused with the head."""
     pol = trace.policy if trace is not None else resolve(pol)
-    x_in = _image_input(resnet, x_nchw, trace, pol)
-    prepack_x3(resnet, trace is not None, pol)
     blocks = _blocks(resnet)
-    x = stem_forward(resnet, x_in, trace, pol, next_convs=_block_convs_reading_input(blocks[0]))
+    pols = _block_policies(resnet, pol)
+    if trace is not None and pol.stage_precision:
+        raise ops.HkpError("Policy.stage_precision is an inference mode")
+    x_in = _image_input(resnet, x_nchw, trace, pols[0])
+    prepack_x3(resnet, trace is not None, pol)
+    x = stem_forward(resnet, x_in, trace, pols[0], next_convs=_block_convs_reading_input(blocks[0]))
     for i, block in enumerate(blocks):
         last = i == len(blocks) - 1
         nxt = () if last else _block_convs_reading_input(blocks[i + 1])
-        x = block_forward(block, x, trace, final=last, head=head if last else None, pol=pol, next_convs=nxt)
+        x = block_forward(block, x, trace, final=last, head=head if last else None, pol=pols[i], next_convs=nxt,
+                          next_pol=None if last or pols[i + 1] is pols[i] else pols[i + 1])
     return x
+
+
+def _block_policies(resnet, pol):
+    """The policy of each block: `pol`, or under Policy.stage_precision its layer's
+    arithmetic (the stem computes as layer1's producer: its conv is fp32-class
+    either way, its pooled output written in layer1's operand format)."""
+    layers = (resnet.layer1, resnet.layer2, resnet.layer3, resnet.layer4)
+    if not pol.stage_precision:
+        return [pol for layer in layers for _ in layer]
+    per = [pol.with_(precision=p, stage_precision=()) for p in pol.stage_precision]
+    return [per[i] for i, layer in enumerate(layers) for _ in layer]
 
 
 def _feat_channels(resnet):

@@ -69,6 +69,10 @@ class Policy:
     prepack_plan: bool = True
     # BN finalize: two-level merge from this many partial tiles on
     fin_two_level_tiles: int = 2048
+    # train-mode BN finalize folded into the producing conv (hkp_bn_fold: the conv's
+    # last-arriving blocks merge its partials; no separate finalize launch) wherever
+    # the conv runs an LDS-DMA kernel and the statistics are per rank
+    fold_bn: bool = True
     # plain fp16 inference (C4): a Bottleneck's bn3 statistics from conv3's input
     # covariance (1x1 conv: exact), bn3 + residual + ReLU in conv3's epilogue
     gram_bn: bool = True
@@ -76,10 +80,23 @@ class Policy:
     # conv runs the halo-tile body (hkp_conv2d_fwd_x3_bnin / _f16_bnin: layer1's
     # 3x3 convs at 640x480) instead of a separate apply pass
     fuse_input_bn: bool = True
+    # forward conv tiles from the measured plan table (hkp/tile_plan.json, written by
+    # tools/tile_sweep.py) where it holds the conv's shape; the C planner elsewhere
+    # (a nonzero x3_tile / f16_tile_* field still forces its policy)
+    tile_plan: bool = True
+    # inference, per-stage conv arithmetic (DESIGN "Per-stage precision"): () = every
+    # stage at `precision`; else one of "f16" / "f16x3" for each of layer1..layer4
+    # (the stem conv is fp32-class in both; the head follows layer4), the
+    # activation converted where two stages meet
+    stage_precision: tuple = ()
 
     def __post_init__(self):
         if self.precision not in PRECISIONS:
             raise ValueError("precision must be one of %s, got %r" % (sorted(PRECISIONS), self.precision))
+        if self.stage_precision and (len(self.stage_precision) != 4 or
+                                     any(p not in ("f16", "f16x3") for p in self.stage_precision)):
+            raise ValueError("stage_precision: four of 'f16' / 'f16x3' (layer1..layer4), got %r"
+                             % (self.stage_precision,))
 
     @property
     def passes(self):
@@ -96,7 +113,8 @@ class Policy:
 
 DEFAULT = Policy()
 
-TUNING_FIELDS = tuple(f.name for f in fields(Policy) if f.name not in ("precision", "sync_bn", "sync_group"))
+TUNING_FIELDS = tuple(f.name for f in fields(Policy) if f.name not in ("precision", "sync_bn", "sync_group",
+                                                                      "stage_precision"))
 
 
 def resolve(policy):

@@ -629,10 +629,11 @@ def test_f16_conv_exact_products(cuda_device, case):
         assert torch.allclose(pv, p16, rtol=1e-4, atol=1e-3)
 
 
-@pytest.mark.parametrize("tile", [7, 8])
+@pytest.mark.parametrize("tile", [7, 8, 14])
 def test_retired_tile_policies_rejected(cuda_device, tile):
-    """Policies 7 and 8 (the persistent conv, measured slower than the one-tile grid
-    and removed) are rejected with HKP_ERR_ARG, not silently re-planned."""
+    """Policies 7, 8 (the persistent conv) and 14 (the persistent A3 body), each
+    measured slower than the one-tile grid and removed, are rejected with
+    HKP_ERR_ARG, not silently re-planned."""
     from hkp import ops
     d = cuda_device
     x16 = torch.ones(1, 8, 8, 64, device=d, dtype=torch.float16)
@@ -861,3 +862,29 @@ def test_fused_input_bn_network_bitexact(cuda_device, bb, prec, b, hw, fused):
         outs.append((hm, yx))
     assert fused in syms, syms
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+def test_stage_precision_plans(cuda_device, golden):
+    """Policy.stage_precision (DESIGN "Per-stage precision"): an all-f16 plan gives
+    the plain-fp16 network's bits and an all-f16x3 plan the f16x3 network's; a mixed
+    plan converts the activation where two stages meet (f16 -> fp32 + packed split,
+    f16x3 -> the fp16 plane) and stays within the plain-fp16 gate of the reference
+    fixture."""
+    g = golden("fwd_r50_k8_480x640_b2")
+    B, H, W, K, st = int(g["batch"]), int(g["height"]), int(g["width"]), int(g["k"]), int(g["step"])
+    m = _model("resnet50", K, int(g["wseed"]), cuda_device, precision="f16")
+    x = recipe.to_tensor_nchw(recipe.seeded_images_u8(B, H, W, int(g["iseed"]))).to(cuda_device)
+
+    def run(**kw):
+        with torch.no_grad():
+            return m.heatmaps_and_keypoints(x, policy=m.policy.with_(**kw))
+    f16, x3 = run(), run(precision="f16x3")
+    a16 = run(stage_precision=("f16",) * 4)
+    a3 = run(stage_precision=("f16x3",) * 4)
+    assert torch.equal(a16[0], f16[0]) and torch.equal(a16[1], f16[1])
+    assert torch.equal(a3[0], x3[0]) and torch.equal(a3[1], x3[1])
+    for plan in (("f16", "f16", "f16x3", "f16x3"), ("f16x3", "f16", "f16x3", "f16")):
+        hm, yx = run(stage_precision=plan)
+        err = float(np.abs(hm[:, :, ::st, ::st].cpu().numpy() - g["heat_sub"]).max())
+        agree = float((yx.cpu().numpy() == g["argmax_yx"]).all(-1).mean())
+        assert torch.isfinite(hm).all() and err < 0.08 and agree >= 0.75, (plan, err, agree)
