@@ -327,7 +327,6 @@ extern "C" int hkp_conv2d_fwd(const hkp_conv_desc* d, const float* x, const floa
     int rc = conv_geometry(d, &ho, &wo);
     if (rc) return rc;
     HKP_CHECK_ARG(x && w && y, "hkp_conv2d_fwd: null tensor");
-    HKP_CHECK_ARG(d->bn_fold == nullptr, "hkp_conv2d_fwd: bn_fold is not taken here (the LDS-DMA convs fold it)");
     HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv2d_fwd: Cout=%d must be a multiple of 64", d->k);
     const long M = (long)d->n * ho * wo;
     HKP_CHECK_ARG(M < (1L << 31) && (long)d->n * d->h * d->w < (1L << 31), "hkp_conv2d_fwd: tensor too large");

@@ -70,20 +70,6 @@ __device__ __attribute__((aligned(256))) uint4 g_x3_nan_line[8] = {
     {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u},
     {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}, {~0u, ~0u, ~0u, ~0u}};
 
-// BN finalize folded into the conv grid (hkp_bn_fold; x3_fold_arrive_tile / x3_fold_merge below)
-struct X3Fold {
-    const float* gamma = nullptr;
-    const float* beta = nullptr;
-    float momentum = 0.f, eps = 0.f;
-    float* rmean = nullptr;
-    float* rvar = nullptr;
-    int64_t* nbt = nullptr;
-    float* ss = nullptr;
-    float* mi = nullptr;
-    double2* ws = nullptr;         // [chunks][K] (S, Q) of each chunk
-    unsigned* cnt = nullptr;       // null: no fold
-};
-
 struct X3Args {
     const _Float16* xs;
     const _Float16* ws;
@@ -140,7 +126,12 @@ struct X3Args {
     // A/B (hkp_debug_x3_prio): static wave priority in the A3 K loop — 0 none, 1
     // s_setprio 1 on waves 4-7 (the second wave on each SIMD), 2 on waves 0-3
     int prio = 0;
-    X3Fold fold;
+#ifdef HKP_AB_KNOBS
+    // A/B probe (hkp_debug_x3_a_wrap): the one-tile and DUO bodies read the A operand of row
+    // m from row m % a_wrap (0: off) — wrong outputs, but an L2-resident A stream —
+    // to time a conv's K loop without the activation lines' HBM / MALL latency
+    int a_wrap = 0;
+#endif
 };
 
 // One 16-B epilogue output store of flavour `kind` (X3Args::st_kind); dflt: the
@@ -264,8 +255,6 @@ constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
 // B (the weights, L2-resident) 2 stages: 5 x 32 KiB = the whole 160 KiB; the
 // epilogue's scratch and column scales reuse the drained ring.
 constexpr int X3_A3_LDS = 5 * 256 * 128;
-// the LDS of the block running conv_x3_tile<BN, STEM, PAIR, MFD, P, A3> (its kernel's smem)
-#define X3_TILE_LDS(BN, PAIR, P, A3) ((A3) ? X3_A3_LDS : x3_lds_bytes(BN, PAIR, P) + x3_red_bytes(BN, PAIR))
 
 // BN-partials scratch (x3_bn_partials_w: [2][WM][BN] floats) past the ring, so
 // the epilogue needs no barrier before it, then the tile's BN column scales
@@ -397,13 +386,6 @@ __device__ __forceinline__ void x3_products(Acc& acc, const V& a0, const V& a1, 
     }
 }
 
-// BN tile partial stores at device scope (global_store sc1: written through the
-// XCD's L2, so the conv's own blocks on other XCDs read them for the folded
-// finalize without an L2 write-back — X3Args::fold); a compiler-tracked store
-__device__ __forceinline__ void x3_part_st(float* p, float v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // BN tile partials of the tile in the accumulators: per 128-row half, the
 // column sum and the sum of squares about the half's mean (Chan-mergeable in
 // bn_finalize).  VAL(i, j, r) / ROW(i, r) address the accumulator element and
@@ -438,7 +420,7 @@ __device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int 
         if (cnt > 0) {
             const float s = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
             tmean[h * BN + c] = s / (float)cnt;
-            x3_part_st(a.part + (((tile128 + h) * a.K + n0 + c) * 2 + 0), s);
+            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 0] = s;
         }
     }
     __syncthreads();
@@ -466,7 +448,7 @@ __device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int 
     for (int e = tid; e < 2 * BN; e += 512) {
         const int h = e / BN, c = e - h * BN;
         if (a.M - (m0 + 128 * h) > 0)
-            x3_part_st(a.part + (((tile128 + h) * a.K + n0 + c) * 2 + 1), red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c]);
+            a.part[((tile128 + h) * a.K + n0 + c) * 2 + 1] = red[(2 * h) * BN + c] + red[(2 * h + 1) * BN + c];
     }
 }
 
@@ -553,8 +535,8 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
                 x3_chan_merge(S[0], Q[0], S[1], Q[1], 1.f / 64, 32.f);          // even wave, odd wave
                 const float sc = wide[32 * BN + c];
                 const long tile128 = (long)(m0 >> 7) + h;
-                x3_part_st(a.part + ((tile128 * a.K + n0 + c) * 2 + 0), S[0] * sc);
-                x3_part_st(a.part + ((tile128 * a.K + n0 + c) * 2 + 1), Q[0] * (sc * sc));
+                a.part[(tile128 * a.K + n0 + c) * 2 + 0] = S[0] * sc;
+                a.part[(tile128 * a.K + n0 + c) * 2 + 1] = Q[0] * (sc * sc);
             }
             return;
         }
@@ -647,203 +629,8 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
         const float sum = nb > 0 ? sa + sb : sa;
         const float m2 = nb > 0 ? (qa + qb) + d * d * f : qa;
         const float sc = sc_of(j);
-        x3_part_st(a.part + ((tile128 * a.K + n0 + c) * 2 + 0), sum * sc);
-        x3_part_st(a.part + ((tile128 * a.K + n0 + c) * 2 + 1), m2 * (sc * sc));
-    }
-}
-
-// ---- BN finalize folded into the conv grid (X3Args::fold, hkp_bn_fold) ----
-// The tile partials this launch writes are merged by its own blocks, bit for bit
-// the two-level finalize (bn.hip: bn_fin_chunk_kernel, then bn_fin_merge_kernel =
-// hkp_bn_finalize_ws): chunk k = the 128 partial rows (128-row tiles) of m-tiles
-// [64k, 64k + 64).  Once a block has written the partials of its tile (m-tile mt,
-// column tile nt), it counts itself on cnt[k * n_tiles + nt]; the last of the
-// chunk's m-tiles to arrive reduces the chunk's partials of the tile's BN channels
-// to (S, Q about the chunk mean) in ws[k][c] — bn_fin_chunk's lanes, loads and
-// pairwise tree, so its bits — and counts the chunk on cnt[chunks * n_tiles + nt];
-// the last chunk merges the chunks (bn_fin_merge's arithmetic) and writes scale /
-// shift, mean / invstd and the running statistics of those channels (nbt by
-// column tile 0).  No launch boundary between the conv and its BN parameters; the
-// merges run on whichever CU finishes a chunk last, beside the other CUs' tiles.
-// Hand-off per cdna_hip_programming.md §6 Guideline 16 (as sk_combine): drain the
-// stores, barrier, one lane releases at agent scope and counts; the last arriver
-// acquires and re-zeroes the counter.  NT threads; CG = NT / 16 channel lanes x 16
-// tile lanes (FIN_TL) per pass over the tile's BN channels.
-constexpr int FOLD_TL = 16, FOLD_TPL = 8, FOLD_CHUNK = FOLD_TL * FOLD_TPL;   // = bn.hip FIN_*
-constexpr int FOLD_MT = FOLD_CHUNK / 2;              // 256-row m-tiles per chunk
-
-// bn.hip fin_col_sum: the 16 tile lanes of a channel summed pairwise in fixed order
-template <int CG>
-__device__ __forceinline__ double x3_fold_col_sum(double v, double* red, int tl, int cl) {
-    __syncthreads();
-    red[tl * CG + cl] = v;
-    __syncthreads();
-    double s[FOLD_TL];
-#pragma unroll
-    for (int i = 0; i < FOLD_TL; ++i) s[i] = red[i * CG + cl];
-#pragma unroll
-    for (int w = FOLD_TL / 2; w >= 1; w >>= 1)
-#pragma unroll
-        for (int i = 0; i < w; ++i) s[i] = s[2 * i] + s[2 * i + 1];
-    return s[0];
-}
-
-// one arrival on counter cnt[idx] of `expect`; true on the block that arrived last
-// (block-uniform).  Everything the block wrote for the merge is a device-scope
-// store (x3_part_st, x3_fold_ws_st), visible once it completed (vmcnt), and the
-// merges read at device scope (sc1 loads): no L2 write-back / invalidate (an
-// agent-scope fence here wrote back the whole L2 of the XCD per tile: -10..-18 %)
-__device__ __forceinline__ bool x3_fold_arrive(unsigned* cnt, long idx, int expect, int* flag) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        gu32* c = (gu32*)cnt + idx;
-        const unsigned prev = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = prev == (unsigned)(expect - 1);
-        if (last) __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *(volatile int*)flag = last;
-    }
-    __syncthreads();
-    return *(volatile int*)flag != 0;
-}
-
-// the arrival of tile (mt: global m-tile, nt) on its chunk, right after the block
-// wrote the tile's partials (so only those stores are drained, and the tile's
-// output stores follow); the flag word sits at the end of the block's LDS (LDSB),
-// past anything an epilogue stages
-template <int LDSB>
-__device__ __forceinline__ bool x3_fold_arrive_tile(const X3Args& a, char* smem, int mt, int nt) {
-    if (a.fold.cnt == nullptr || a.part == nullptr) return false;
-    const long m_tiles = ((long)a.M + 255) / 256;
-    const int k = mt / FOLD_MT;
-    return x3_fold_arrive(a.fold.cnt, (long)k * a.n_tiles + nt, (int)min((long)FOLD_MT, m_tiles - (long)k * FOLD_MT),
-                          (int*)(smem + LDSB - 16));
-}
-
-__device__ __forceinline__ void x3_fold_ws_st(double2* p, double2 v) {
-    __hip_atomic_store((double*)p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((double*)p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// rows x row_bytes (a multiple of 16) from global memory (row r at src + r *
-// stride) into LDS at dst, contiguous, by LDS-DMA at device scope (sc1) — rows >=
-// valid read zeros; then every wave's DMA retired and the block past a barrier
-template <int NT>
-__device__ __forceinline__ void x3_fold_stage(char* dst, const char* src, long stride, int row_bytes, int rows,
-                                              int valid, int tid) {
-    const int pr = row_bytes / 16, pieces = rows * pr, lane = tid & 63, w = tid >> 6;
-    const char* zero = (const char*)g_x3_zero_line + (lane & 7) * 16;
-    for (int i = w; i * 64 < pieces; i += NT / 64) {
-        const int e = i * 64 + lane, r = e / pr, c16 = e - r * pr;
-        __builtin_amdgcn_global_load_lds(r < valid ? src + r * stride + c16 * 16 : zero,
-                                         (__attribute__((address_space(3))) void*)(dst + i * 1024), 16, 0, 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-}
-
-// the merges, on the block whose tile arrived last on its chunk (x3_fold_arrive_tile
-// returned true) once its epilogue is done with the LDS: the chunk's partials of
-// the tile's BN channels, then — on the last chunk of the column tile — the chunks
-template <int BN, int NT, int LDSB>
-__device__ __forceinline__ void x3_fold_merge(const X3Args& a, char* smem, int mt, int nt) {
-    constexpr int CG = NT / FOLD_TL;                                  // channel lanes per pass
-    constexpr int RED = FOLD_TL * CG * 8;                            // col_sum scratch
-    // level-1 staging: HB channels of the chunk's 128 partial rows (8 B each) at a time
-    constexpr int HB = FOLD_CHUNK * BN * 8 + RED + 16 <= LDSB ? BN : FOLD_CHUNK * 128 * 8 + RED + 16 <= LDSB ? 128 : 64;
-    static_assert(BN % HB == 0 && HB % CG == 0 && FOLD_CHUNK * HB * 8 + RED + 16 <= LDSB, "fold level-1 LDS");
-    static_assert(FOLD_TL * BN * 16 + RED + 16 <= LDSB, "fold level-2 LDS");
-    constexpr int L1 = FOLD_CHUNK * HB * 8, L2 = FOLD_TL * BN * 16;
-    const X3Fold& f = a.fold;
-    const long M = a.M, tiles = (M + 127) / 128, chunks = (tiles + FOLD_CHUNK - 1) / FOLD_CHUNK;
-    const int NTL = a.n_tiles, k = mt / FOLD_MT;
-    double* red = (double*)(smem + (L1 > L2 ? L1 : L2));
-    int* flag = (int*)(smem + LDSB - 16);
-    __syncthreads();                                                // the epilogue is done with the LDS
-    // the lane index through an opaque copy: no address below is hoisted into the
-    // K loop (computed early, they would stay live across it)
-    int tid = threadIdx.x;
-    asm volatile("" : "+v"(tid));
-    const int tl = tid / CG, cl = tid % CG, n0 = nt * BN;
-    // level 1 (bn_fin_chunk_kernel's lanes, order and tree): per HB channels, the
-    // chunk's partial rows staged in LDS (one DMA round), then per pass of CG
-    const long t0 = (long)k * FOLD_CHUNK;
-    const long te = min(tiles, t0 + FOLD_CHUNK);
-    const long nk = min(M, te * 128) - t0 * 128;                    // rows in this chunk
-    const float2* st1 = (const float2*)smem;
-#pragma unroll 1
-    for (int h = 0; h < BN; h += HB) {
-        if (h) __syncthreads();                                     // the previous half's reads are done
-        x3_fold_stage<NT>(smem, (const char*)(a.part + (t0 * a.K + n0 + h) * 2), (long)a.K * 8, HB * 8, FOLD_CHUNK,
-                          (int)(te - t0), tid);
-#pragma unroll 1
-        for (int p = 0; p < HB / CG; ++p) {
-            const int cc = p * CG + cl;
-            float2 v[FOLD_TPL];
-#pragma unroll
-            for (int j = 0; j < FOLD_TPL; ++j) v[j] = st1[(tl + FOLD_TL * j) * HB + cc];
-            double s = 0.0;
-#pragma unroll
-            for (int j = 0; j < FOLD_TPL; ++j) s += (double)v[j].x;
-            const double S = x3_fold_col_sum<CG>(s, red, tl, cl);
-            const double mk = S / (double)nk;
-            double q = 0.0;
-#pragma unroll
-            for (int j = 0; j < FOLD_TPL; ++j) {
-                const long t = t0 + tl + (long)FOLD_TL * j;
-                if (t < tiles) {
-                    const long n_t = min(128L, M - t * 128);
-                    const double dm = (double)v[j].x / (double)n_t - mk;
-                    q += (double)v[j].y + (double)n_t * dm * dm;
-                }
-            }
-            const double Q = x3_fold_col_sum<CG>(q, red, tl, cl);
-            if (tl == 0) x3_fold_ws_st(f.ws + (long)k * a.K + n0 + h + cc, make_double2(S, Q));
-        }
-    }
-    // level 2 (bn_fin_merge_kernel's) on the last chunk of this column tile: rounds
-    // of 16 chunk rows staged in LDS; lane tl takes chunks tl, tl + 16, ... in order
-    if (!x3_fold_arrive(f.cnt, chunks * NTL + nt, (int)chunks, flag)) return;
-    const long rows = (long)FOLD_CHUNK * 128;                          // rows per full chunk
-    const double2* st2 = (const double2*)smem;
-    auto stage2 = [&](long r0) {
-        __syncthreads();                                            // the previous round's reads are done
-        x3_fold_stage<NT>(smem, (const char*)(f.ws + r0 * a.K + n0), (long)a.K * 16, BN * 16, FOLD_TL,
-                          (int)min((long)FOLD_TL, chunks - r0), tid);
-    };
-    constexpr int NP = BN / CG;
-    double s[NP], q[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) s[p] = q[p] = 0.0;
-#pragma unroll 1
-    for (long r0 = 0; r0 < chunks; r0 += FOLD_TL) {
-        stage2(r0);
-        if (r0 + tl < chunks)
-#pragma unroll
-            for (int p = 0; p < NP; ++p) s[p] += st2[tl * BN + p * CG + cl].x;
-    }
-    double mean[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) mean[p] = x3_fold_col_sum<CG>(s[p], red, tl, cl) / (double)M;
-#pragma unroll 1
-    for (long r0 = 0; r0 < chunks; r0 += FOLD_TL) {
-        if (chunks > FOLD_TL) stage2(r0);                           // (one round: still staged)
-        if (r0 + tl < chunks) {
-            const long nkk = min(rows, M - (r0 + tl) * rows);
-#pragma unroll
-            for (int p = 0; p < NP; ++p) {
-                const double2 w = st2[tl * BN + p * CG + cl];
-                const double dm = w.x / (double)nkk - mean[p];
-                q[p] += w.y + (double)nkk * dm * dm;
-            }
-        }
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const double m2 = x3_fold_col_sum<CG>(q[p], red, tl, cl);
-        if (tl == 0)
-            bn_fin_store(n0 + p * CG + cl, a.K, M, mean[p], m2, f.gamma, f.beta, f.momentum, f.eps, f.rmean, f.rvar,
-                         f.nbt, f.ss, f.mi);
+        a.part[(tile128 * a.K + n0 + c) * 2 + 0] = sum * sc;
+        a.part[(tile128 * a.K + n0 + c) * 2 + 1] = m2 * (sc * sc);
     }
 }
 
@@ -965,7 +752,7 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
 // A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
 template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, typename Issue, typename IssueA,
           typename IssueB>
-__device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
+__device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
                                                   Issue& issue_next, IssueA& issue_a, IssueB& issue_b) {
     constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
@@ -1208,7 +995,7 @@ __device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, i
     if (partial) {                         // stream-K: fold the tile's segments
         auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
         auto set = [&](int v, f32x4 y) { acc[v / UN][v % UN] = y; };
-        if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return false;
+        if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return;
     }
     const int rbase = m0 + wm * UM * 16 + 4 * q;
     // column scale (weight scale x gradient scale): the prefetched LDS copy, or
@@ -1227,7 +1014,6 @@ __device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, i
                 a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
                 [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
         }
-        const bool fold_last = x3_fold_arrive_tile<LDS_ALL>(a, smem, m0 / 256, n0 / BN);
         const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
         X3Res<BN> eres;
         if (a.ep_ss) eres = x3_ep_res_load<BN>(a, m0, n0, tid);
@@ -1251,8 +1037,7 @@ __device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, i
         if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), eres, m0, n0, tid);
         else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
         x3_stamp(a, 5);
-        if (fold_last) x3_fold_merge<BN, 512, LDS_ALL>(a, smem, m0 / 256, n0 / BN);
-        return true;
+        return;
     }
     // ---- epilogue (fp32 output): BN partials, then the scaled tile ----
     float sc[UN];
@@ -1264,7 +1049,6 @@ __device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, i
             a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
             [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
     }
-    const bool fold_last = x3_fold_arrive_tile<LDS_ALL>(a, smem, m0 / 256, n0 / BN);
     x3_stamp(a, 3);
     {
         // The output tile is staged through the (drained) ring as fp32 rows and
@@ -1325,8 +1109,6 @@ __device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, i
     }
     x3_stamp(a, 4);
     x3_stamp(a, 5);
-    if (fold_last) x3_fold_merge<BN, 512, LDS_ALL>(a, smem, m0 / 256, n0 / BN);
-    return true;
 }
 
 // STEM: the 7x7/s2 stem on the zero-padded NHWC4 image planes of
@@ -1339,10 +1121,8 @@ __device__ __forceinline__ bool conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-// true when this block wrote the tile's output (and BN partials), then folded the
-// BN finalize (X3Args::fold); false for a stream-K segment another block finishes
 template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
-__device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
+__device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
     constexpr int BM = 256, WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     constexpr int ROW = 128;                       // bytes per LDS row (one packed line)
@@ -1393,7 +1173,11 @@ __device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int ti
         const int row = RPI * (w * GA + i) + lane / CPR;
         const int Lc = (lane % CPR) ^ swz(row);
         const long L = lofs(Lc);
+#ifdef HKP_AB_KNOBS
+        const int m = a.a_wrap ? (m0 + row) % a.a_wrap : m0 + row;
+#else
         const int m = m0 + row;
+#endif
         int hb = -16384, wb = -16384;
         long off = 0;
         if (m < a.M) {
@@ -1491,10 +1275,9 @@ __device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     if constexpr (MFD == 16) {
-        const bool done = conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, ks, nks, partial, m0, n0,
-                                                                             wm, wn, lane, tid, issue_next, issue_a,
-                                                                             issue_b);
-        return done;
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
+                                                             tid, issue_next, issue_a, issue_b);
+        return;
     } else {
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -1602,7 +1385,7 @@ __device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int ti
             const int q4 = (v & 3) * 4;
             x[q4] = y[0]; x[q4 + 1] = y[1]; x[q4 + 2] = y[2]; x[q4 + 3] = y[3];
         };
-        if (!sk_combine<TM * TN * 4>(a, tile, tid, smem, get, set)) return false;
+        if (!sk_combine<TM * TN * 4>(a, tile, tid, smem, get, set)) return;
     }
     const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;   // exact (power of two)
     const int rbase = m0 + wm * TM * 32 + 4 * kh;
@@ -1619,7 +1402,6 @@ __device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int ti
             x3_bn_partials<BN, TM, TN, 16, 32, 32>(
                 a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
                 [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); });
-        const bool fold_last = x3_fold_arrive_tile<X3_TILE_LDS(BN, PAIR, P, A3)>(a, smem, mt + a.mt0, nt);
         const X3EpSS eps = x3_ep_load<BN>(a, n0, tid);
         X3Res<BN> eres;
         if (a.ep_ss) eres = x3_ep_res_load<BN>(a, m0, n0, tid);
@@ -1640,8 +1422,7 @@ __device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int ti
         __syncthreads();
         if (a.ep_ss) x3_store_tile_f16_bn<BN>(a, smem, (const float*)(smem + SS_OFF), eres, m0, n0, tid);
         else x3_store_tile_f16<BN>(a, smem, m0, n0, tid);
-        if (fold_last) x3_fold_merge<BN, 512, X3_TILE_LDS(BN, PAIR, P, A3)>(a, smem, mt + a.mt0, nt);
-        return true;
+        return;
     }
 
     // ---- epilogue: NHWC store (x scales, + addend) + BN partials per 128-row tile ----
@@ -1666,13 +1447,10 @@ __device__ __forceinline__ bool conv_x3_tile(const X3Args& a, char* smem, int ti
             }
         }
     }
-    if (a.part == nullptr) return true;
+    if (a.part == nullptr) return;
     x3_bn_partials<BN, TM, TN, 16, 32, 32>(
         a, smem, m0, n0, wm, wn, lane, tid, [&](int i, int j, int r) { return acc[i][j][r]; },
         [&](int i, int r) { return rbase + i * 32 + (r & 3) + 8 * (r >> 2); });
-    if (x3_fold_arrive_tile<X3_TILE_LDS(BN, PAIR, P, A3)>(a, smem, mt + a.mt0, nt))
-        x3_fold_merge<BN, 512, X3_TILE_LDS(BN, PAIR, P, A3)>(a, smem, mt + a.mt0, nt);
-    return true;
     }
 }
 
@@ -2010,7 +1788,6 @@ __device__ __forceinline__ void conv_x3_halo_body(const X3Args& a, char* smem) {
             [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; }, (float*)smem);
         lds_sync();
     }
-    const bool fold_last = x3_fold_arrive_tile<HALO_LDS>(a, smem, mt, nt);
     auto out_pix = [&](int row) { return ((long)img * a.Ho + h0 + (row >> 5)) * a.Wo + w0 + (row & 31); };
     if constexpr (P == 1) {
         constexpr int PITCH = BN + 8, CH = BN / 8;
@@ -2053,7 +1830,6 @@ __device__ __forceinline__ void conv_x3_halo_body(const X3Args& a, char* smem) {
             *(f32x4*)(a.y + off) = v;
         }
     }
-    if (fold_last) x3_fold_merge<BN, 512, HALO_LDS>(a, smem, mt, nt);
 }
 
 template <int P>
@@ -2239,7 +2015,6 @@ __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
             [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return scv[j]; }, (float*)smem);
         lds_sync();
     }
-    const bool fold_last = x3_fold_arrive_tile<STEM_LDS>(a, smem, mt, nt);
     x3_stamp(a, 3);
     constexpr int PITCH = BN + 4, C4 = BN / 4;
     float* st = (float*)smem;
@@ -2259,7 +2034,6 @@ __global__ __launch_bounds__(512, 2) void conv_x3_stem_patch_kernel(X3Args a) {
         x3_st16((f32x4*)(a.y + off), *(const f32x4*)(st + row * PITCH + c4 * 4), a.st_kind, 2);
     }
     x3_stamp(a, 5);
-    if (fold_last) x3_fold_merge<BN, 512, STEM_LDS>(a, smem, mt, nt);
 }
 
 
@@ -2326,8 +2100,8 @@ __device__ __forceinline__ void duo_bn_partials(const X3Args& a, const f32x4 (&a
             x3_chan_merge(s, m2, __shfl_xor(s, 32), __shfl_xor(m2, 32), 1.f / (UM * 8), UM * 4.f);
             if (q == 0) {
                 const int c = ncol0 + 16 * j + r16;
-                x3_part_st(a.part + ((tile128 * a.K + c) * 2 + 0), s * sc[j]);
-                x3_part_st(a.part + ((tile128 * a.K + c) * 2 + 1), m2 * (sc[j] * sc[j]));
+                a.part[(tile128 * a.K + c) * 2 + 0] = s * sc[j];
+                a.part[(tile128 * a.K + c) * 2 + 1] = m2 * (sc[j] * sc[j]);
             }
         }
         return;
@@ -2368,8 +2142,8 @@ __device__ __forceinline__ void duo_bn_partials(const X3Args& a, const f32x4 (&a
         }
         if (q == 0) {
             const int c = ncol0 + 16 * j + r16;
-            x3_part_st(a.part + ((tile128 * a.K + c) * 2 + 0), s * sc[j]);
-            x3_part_st(a.part + ((tile128 * a.K + c) * 2 + 1), m2 * (sc[j] * sc[j]));
+            a.part[(tile128 * a.K + c) * 2 + 0] = s * sc[j];
+            a.part[(tile128 * a.K + c) * 2 + 1] = m2 * (sc[j] * sc[j]);
         }
     }
 }
@@ -2422,7 +2196,11 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
     for (int i = 0; i < GA; ++i) {
         const int row = 64 * w + 16 * i + (lane >> 2);
         const int Lc = (lane & 3) ^ duo_swz(row);
+#ifdef HKP_AB_KNOBS
+        const int m = a.a_wrap ? (m0 + row) % a.a_wrap : m0 + row;
+#else
         const int m = m0 + row;
+#endif
         int hb = -16384, wb = -16384;
         long off = 0;
         if (m < a.M) {
@@ -2550,7 +2328,6 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
 
     // ---- epilogue: BN partials of this wave's 128-row half, then the fp16 tile ----
     if (a.part) duo_bn_partials<UM, UN>(a, acc, sc, m0 + 128 * wm, n0 + wn * 64, lane);
-    const bool fold_last = x3_fold_arrive_tile<DUO_LDS>(a, smem, mt, nt);
     x3_stamp(a, 3);
     constexpr int PITCH = BN + 8, CH = BN / 8, SS_OFF = BM * PITCH * 2;
     constexpr int NT = 256, NPT = BM * CH / NT;              // 16-B chunks per thread
@@ -2596,7 +2373,6 @@ __global__ __launch_bounds__(256, 2) void conv_x3_duo_kernel(X3Args a) {
                 x3_st16((uint4*)(a.y16 + (long)m * a.K + n0 + cc * 8), *(const uint4*)(smem + (row * PITCH + cc * 8) * 2), a.st_kind, 1);
         }
         x3_stamp(a, 5);
-        if (fold_last) x3_fold_merge<BN, NT, DUO_LDS>(a, smem, mt, nt);
         return;
     }
     float sa[8], sb[8], ra[8], rb[8];
@@ -3528,6 +3304,7 @@ HKP_AB_KNOB(int, g_x3_stagger_ns, 0);                 // hkp_debug_x3_stagger
 HKP_AB_KNOB(int, g_x3_store, 0);                      // hkp_debug_x3_store
 HKP_AB_KNOB(int, g_duo_stagger_ns, -1);               // hkp_debug_duo_stagger
 HKP_AB_KNOB(int, g_x3_prio, 0);                       // hkp_debug_x3_prio
+HKP_AB_KNOB(int, g_x3_a_wrap, 0);                     // hkp_debug_x3_a_wrap
 
 // the halo-tile body takes this launch (shape, plain dense output, no fused
 // epilogue, 32-bit halo offsets)
@@ -3558,6 +3335,9 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.stamps = g_x3_stamps;
     a.st_kind = g_x3_store;
     a.prio = g_x3_prio;
+#ifdef HKP_AB_KNOBS
+    a.a_wrap = g_x3_a_wrap;
+#endif
     a.stagger_ticks = g_x3_stagger_ns / 10;
     a.stagger_blocks = x3_cus();
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
@@ -3684,41 +3464,6 @@ static int check_tile(const hkp_conv_desc* d, const char* who) {
     return HKP_OK;
 }
 
-// the folded BN finalize (hkp_bn_fold) of a forward launch with M output rows
-static long fold_counter_bytes(long M, int K) {
-    const long tiles = (M + 127) / 128, chunks = (tiles + FOLD_CHUNK - 1) / FOLD_CHUNK;
-    return (chunks + 1) * (long)(K / 64) * 4;       // per chunk and column tile (64-wide at the most), + per column tile
-}
-
-extern "C" int64_t hkp_bn_fold_counter_bytes(const hkp_conv_desc* d) {
-    int ho, wo;
-    if (!d || hkp_conv_out_hw(d, &ho, &wo) != HKP_OK || d->k % 64) return -1;
-    return fold_counter_bytes((long)d->n * ho * wo, d->k);
-}
-
-static int x3_set_fold(X3Args& a, const hkp_conv_desc* d, const char* who) {
-    const hkp_bn_fold* f = d->bn_fold;
-    if (f == nullptr) return HKP_OK;
-    HKP_CHECK_ARG(a.part != nullptr, "%s: bn_fold needs stat_partials", who);
-    HKP_CHECK_ARG(f->scale_shift != nullptr, "%s: bn_fold.scale_shift is null", who);
-    HKP_CHECK_ARG((f->running_mean == nullptr) == (f->running_var == nullptr), "%s: bn_fold running stats pair", who);
-    const long tiles = ((long)a.M + 127) / 128;
-    HKP_CHECK_ARG(f->workspace && f->ws_bytes >= hkp_bn_finalize_workspace_bytes(a.K, tiles),
-                  "%s: bn_fold.workspace %ld < %ld bytes", who, (long)f->ws_bytes,
-                  (long)hkp_bn_finalize_workspace_bytes(a.K, tiles));
-    HKP_CHECK_ARG(f->counters && f->counter_bytes >= fold_counter_bytes(a.M, a.K), "%s: bn_fold.counters %ld < %ld bytes",
-                  who, (long)f->counter_bytes, fold_counter_bytes(a.M, a.K));
-    a.fold.gamma = f->gamma; a.fold.beta = f->beta; a.fold.momentum = f->momentum; a.fold.eps = f->eps;
-    a.fold.rmean = f->running_mean; a.fold.rvar = f->running_var; a.fold.nbt = f->num_batches_tracked;
-    a.fold.ss = f->scale_shift; a.fold.mi = f->mean_invstd;
-    a.fold.ws = (double2*)f->workspace;
-    a.fold.cnt = (unsigned*)f->counters;
-    return HKP_OK;
-}
-
-// entry points with no folded finalize (backward, fused-epilogue forward)
-#define HKP_NO_FOLD(d, who) HKP_CHECK_ARG((d) == nullptr || (d)->bn_fold == nullptr, "%s: bn_fold is not taken here", who)
-
 // forward launch shared by the f16x3 (P 3) and plain-fp16 (P 1) entry points
 static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const uint16_t* ws, const float* wsc,
                               float* y, uint16_t* y16, float* part, void* sk_ws, int64_t sk_bytes, int P,
@@ -3748,8 +3493,6 @@ static int conv_fwd_x3_common(const hkp_conv_desc* d, const uint16_t* xs, const 
         a.ep_ss = ep->ep_ss; a.ep_res = ep->ep_res; a.ep_rss = ep->ep_rss; a.ep_relu = ep->ep_relu;
         a.in_ss = ep->in_ss;
     }
-    rc = x3_set_fold(a, d, who);
-    if (rc) return rc;
     if (a.in_ss) {
         // the fused input BN runs where the unfused conv would run the halo-tile body,
         // so its output is the unfused path's, bit for bit
@@ -3819,7 +3562,6 @@ extern "C" int hkp_conv2d_fwd_f16_bn(const hkp_conv_desc* d, const uint16_t* x_f
                                      const float* res_scale_shift, int32_t relu, uint16_t* out_f16,
                                      void* sk_workspace, int64_t sk_ws_bytes, hkp_stream_t stream) {
     HKP_CHECK_ARG(d && out_f16 && scale_shift, "hkp_conv2d_fwd_f16_bn: null argument");
-    HKP_NO_FOLD(d, "hkp_conv2d_fwd_f16_bn");
     HKP_CHECK_ARG(!res_scale_shift || res_f16, "hkp_conv2d_fwd_f16_bn: res_scale_shift needs a residual");
     X3Args ep;
     ep.ep_ss = scale_shift;
@@ -3858,7 +3600,6 @@ extern "C" int hkp_conv2d_bwd_data_x3(const hkp_conv_desc* d, const uint16_t* dy
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
     HKP_CHECK_ARG(dy_split && wf_split && dx, "hkp_conv2d_bwd_data_x3: null tensor");
-    HKP_NO_FOLD(d, "hkp_conv2d_bwd_data_x3");
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC && d->stride == 1,
                   "hkp_conv2d_bwd_data_x3: stride-1 NHWC convs only (strided ones use hkp_conv2d_bwd_data)");
     HKP_CHECK_ARG(d->c % 64 == 0 && d->k % 32 == 0, "hkp_conv2d_bwd_data_x3: need Cin%%64==0, Cout%%32==0");
@@ -3925,7 +3666,6 @@ extern "C" int hkp_conv2d_bwd_data_x3_strided(const hkp_conv_desc* d, const uint
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
     HKP_CHECK_ARG(dy_split && phase_split && phase_inv_scale && dx, "hkp_conv2d_bwd_data_x3_strided: null tensor");
-    HKP_NO_FOLD(d, "hkp_conv2d_bwd_data_x3_strided");
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC && d->stride == 2 && d->dilation == 1,
                   "hkp_conv2d_bwd_data_x3_strided: stride-2, dilation-1 NHWC convs only");
     HKP_CHECK_ARG(d->c % 64 == 0 && d->k % 32 == 0, "hkp_conv2d_bwd_data_x3_strided: need Cin%%64==0, Cout%%32==0");
@@ -3984,7 +3724,6 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     int rc = hkp_conv_out_hw(d, &ho, &wo);
     if (rc) return rc;
     HKP_CHECK_ARG(x_split && dy_split && dw && workspace, "hkp_conv2d_bwd_filter_x3: null tensor");
-    HKP_NO_FOLD(d, "hkp_conv2d_bwd_filter_x3");
     HKP_CHECK_ARG(d->in_layout == HKP_LAYOUT_NHWC, "hkp_conv2d_bwd_filter_x3: NHWC convs only");
     HKP_CHECK_ARG(d->k % 64 == 0 && d->c % 32 == 0, "hkp_conv2d_bwd_filter_x3: need Cout%%64==0, Cin%%32==0");
     const long M = (long)d->n * ho * wo;
@@ -4086,8 +3825,6 @@ extern "C" int hkp_conv2d_fwd_stem_x3(const hkp_conv_desc* d, const uint16_t* x_
     a.n_tiles = d->k / 64;
     a.stamps = g_x3_stamps;
     a.st_kind = g_x3_store;
-    rc = x3_set_fold(a, d, "hkp_conv2d_fwd_stem_x3");
-    if (rc) return rc;
     const long m_tiles = (M + 255) / 256;
     if (stem_patch_shape(ho, wo, d->k) && d->tile != HKP_TILE_64_PAIR) {
         // the patch body (patch-divisible outputs: 480x640 and 960x1280 images);
@@ -4129,8 +3866,6 @@ extern "C" int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* 
     a.n_tiles = d->k / 64;
     a.stamps = g_x3_stamps;
     a.st_kind = g_x3_store;
-    const int rc = x3_set_fold(a, d, "hkp_conv2d_fwd_stem_x3_image");
-    if (rc) return rc;
     const dim3 grid((unsigned)(((long)a.M + 255) / 256 * a.n_tiles));
     if (image_u8) hipLaunchKernelGGL(conv_x3_stem_patch_kernel<2>, grid, dim3(512), 0, as_stream(stream), a);
     else hipLaunchKernelGGL(conv_x3_stem_patch_kernel<1>, grid, dim3(512), 0, as_stream(stream), a);
@@ -4222,5 +3957,9 @@ extern "C" void hkp_debug_duo_stagger(int32_t ns) { g_duo_stagger_ns = ns; }
 // Debug / A/B (tools/ only, not thread-safe): static wave priority in the A3 body's
 // K loop (X3Args::prio: 0 none, 1 waves 4-7, 2 waves 0-3 at s_setprio 1).
 extern "C" void hkp_debug_x3_prio(int32_t mode) { g_x3_prio = mode >= 0 && mode <= 2 ? mode : 0; }
+
+// A/B probe (tools/ only, not thread-safe): the one-tile and DUO conv bodies read A row m
+// from row m % rows (0 = off) — an L2-resident activation stream, wrong outputs
+extern "C" void hkp_debug_x3_a_wrap(int32_t rows) { g_x3_a_wrap = rows > 0 ? rows : 0; }
 #endif
 

@@ -21,21 +21,10 @@ class HkpError(RuntimeError):
     pass
 
 
-class BnFold(ctypes.Structure):
-    """hkp_bn_fold: the BN layer whose train-mode finalize a forward conv folds in."""
-    _fields_ = [("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("momentum", ctypes.c_float),
-                ("eps", ctypes.c_float), ("running_mean", ctypes.c_void_p), ("running_var", ctypes.c_void_p),
-                ("num_batches_tracked", ctypes.c_void_p), ("scale_shift", ctypes.c_void_p),
-                ("mean_invstd", ctypes.c_void_p), ("workspace", ctypes.c_void_p), ("ws_bytes", ctypes.c_int64),
-                ("counters", ctypes.c_void_p), ("counter_bytes", ctypes.c_int64)]
-
-
 class ConvDesc(ctypes.Structure):
-    """hkp_conv_desc; `tile` (HKP_TILE_*, default 0 = the planner) is per call;
-    `bn_fold` (a BnFold pointer, forward convs) folds the BN finalize into the conv."""
+    """hkp_conv_desc; `tile` (HKP_TILE_*, default 0 = the planner) is per call."""
     _fields_ = [(n, ctypes.c_int32) for n in
-                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "dilation", "in_layout", "tile")] + \
-        [("bn_fold", ctypes.c_void_p)]
+                ("n", "h", "w", "c", "k", "r", "s", "stride", "pad", "dilation", "in_layout", "tile")]
 
 
 # hkp_conv_desc.tile policies (include/hulkkp.h)
@@ -73,7 +62,6 @@ SIGNATURES = {
     "hkp_version": (ctypes.c_char_p, []),
     "hkp_conv_out_hw": (ctypes.c_int, [_CD, ctypes.POINTER(_I32), ctypes.POINTER(_I32)]),
     "hkp_conv_stat_tiles": (_I64, [_CD]),
-    "hkp_bn_fold_counter_bytes": (_I64, [_CD]),
     "hkp_conv2d_fwd": (ctypes.c_int, [_CD, _P, _P, _P, _P, _P]),
     "hkp_bn_finalize": (ctypes.c_int, [_I32, _I64, _I64, _I32, _P, _P, _P, _F, _F, _P, _P, _P, _P, _P, _P]),
     "hkp_bn_finalize_workspace_bytes": (_I64, [_I32, _I64]),
@@ -162,6 +150,7 @@ AB_SIGNATURES = {
     "hkp_debug_x3_store": (None, [_I32]),
     "hkp_debug_duo_stagger": (None, [_I32]),
     "hkp_debug_x3_prio": (None, [_I32]),
+    "hkp_debug_x3_a_wrap": (None, [_I32]),
 }
 AB_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "tools", "ab_lib", "libhulkkp_ab.so")
 

@@ -40,31 +40,17 @@ def _finalize_args(bn):
     return dict(momentum=bn.momentum if bn.momentum is not None else 0.1, eps=bn.eps)
 
 
-def _fold_request(bn, pol):
-    """An ops.FoldBN for the conv producing `bn`'s input when the policy folds the
-    finalize into it (train-mode statistics, per rank), else None."""
-    if not (pol.fold_bn and bn.training) or parallel.active_sync_group(pol) is not None:
-        return None
-    return ops.FoldBN(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                      **_finalize_args(bn))
-
-
 def _bn_params_many(items, pol):
-    """[(bn, partials, count[, fold])] → [(scale_shift, mean_invstd)]: batch
-    statistics in training mode (and the running-stat update, like
-    nn.BatchNorm2d.forward) — already computed by the conv where it folded the
-    finalize (fold.done) — running stats otherwise.  Under SyncBN the layers'
-    statistics blocks ride ONE all-gather (layers whose statistics are ready
-    together: a block's last BN and its downsample BN)."""
+    """[(bn, partials, count)] → [(scale_shift, mean_invstd)]: batch statistics in
+    training mode (and the running-stat update, like nn.BatchNorm2d.forward),
+    running stats otherwise.  Under SyncBN the layers' statistics blocks ride ONE
+    all-gather (layers whose statistics are ready together: a block's last BN and
+    its downsample BN)."""
     sync = parallel.active_sync_group(pol)
     out = [None] * len(items)
     gather = []
-    for i, item in enumerate(items):
-        bn, part, count = item[:3]
-        fold = item[3] if len(item) > 3 else None
-        if fold is not None and fold.done:
-            out[i] = (fold.scale_shift, fold.mean_invstd)
-        elif not bn.training:
+    for i, (bn, part, count) in enumerate(items):
+        if not bn.training:
             out[i] = ops.bn_eval_params(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
         elif sync is None:
             out[i] = ops.bn_finalize(part, count, bn.weight, bn.bias, bn.running_mean, bn.running_var,
@@ -262,40 +248,36 @@ def conv_bn(conv, bn, x, pol=None, layout="nhwc"):
     x: fp32 NHWC (optionally carrying its producer's operand split), a split-only
     activation (fp16, see ops.bn_apply keep_fp32=False), or NCHW for the stem."""
     pol = resolve(pol)
-    fold = _fold_request(bn, pol)
-    y, part = _conv_fwd(conv, bn, x, pol, layout, fold=fold)
-    ss, mi = _bn_params_many([(bn, part, y.numel() // y.shape[-1], fold)], pol)[0]
+    y, part = _conv_fwd(conv, bn, x, pol, layout)
+    ss, mi = _bn_params(bn, part, y.numel() // y.shape[-1], pol)
     return y, ss, mi
 
 
-def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True, fold=None):
+def _conv_fwd(conv, bn, x, pol, layout="nhwc", sk=True):
     """The conv of conv_bn → (y, BN tile partials or None); sk=False: no stream-K.
-    f16x3 and f16 run on the LDS-DMA MFMA kernels (conv_x3.hip), which fold the
-    BN finalize in when given `fold` (ops.FoldBN; fold.done afterwards); shapes
-    those do not take (Cout % 64, or Cin % 64 for f16) run the exact fp32 MFMA
-    kernel, which needs the fp32 activation (and leaves fold undone)."""
+    f16x3 and f16 run on the LDS-DMA MFMA kernels (conv_x3.hip); shapes those do
+    not take (Cout % 64, or Cin % 64 for f16) run the exact fp32 MFMA kernel, which
+    needs the fp32 activation."""
     passes = pol.passes
     st, pd, dl = _i(conv.stride), _i(conv.padding), _i(conv.dilation)
     if isinstance(x, _PendingBN):
         wp = _pack_weight_x3(conv.weight) if x.y.dtype == torch.float32 else \
             _cached_split(conv.weight, "f16", ops.weight_pack_f16)
         return ops.conv2d_fwd_bnin(x.y, x.ss, wp, st, pd, dl, stats=bn.training, sk=sk,
-                                   tile=_fwd_tile(conv, pol, x.y.dtype == torch.float16), fold=fold)
+                                   tile=_fwd_tile(conv, pol, x.y.dtype == torch.float16))
     sp = ops.split_of(x) if layout == "nhwc" else None
     k = conv.weight.shape[0]
     if layout == "nchw" and passes in (1, 3) and ops.stem_x3_ok(image_nchw_shape(x), tuple(conv.weight.shape), st, pd,
                                                                  dl):
         return ops.conv2d_fwd_stem_x3(x, _cached_split(conv.weight, "stem_x3", ops.stem_weight_pack_x3), k,
-                                      stats=bn.training, fold=fold)
+                                      stats=bn.training)
     if layout == "nhwc" and passes == 3 and sp is not None and sp[1] == 3 and k % 64 == 0:
         return ops.conv2d_fwd_x3(sp[0], _pack_weight_x3(conv.weight), st, pd, dl, stats=bn.training, sk=sk,
-                                 products=pol.products, tile=_planned_tile("x3", sp[0].shape, conv, pol, pol.x3_tile),
-                                 fold=fold)
+                                 products=pol.products, tile=_planned_tile("x3", sp[0].shape, conv, pol, pol.x3_tile))
     if layout == "nhwc" and passes == 1 and sp is not None and sp[1] == 1 and _f16_conv_ok(conv):
         forced = pol.f16_tile_1x1 if conv.weight.shape[1] == 1 else pol.f16_tile_kxk
         return ops.conv2d_fwd_f16(sp[0], _cached_split(conv.weight, "f16", ops.weight_pack_f16), st, pd, dl,
-                                  stats=bn.training, sk=sk, tile=_planned_tile("f16", sp[0].shape, conv, pol, forced),
-                                  fold=fold)
+                                  stats=bn.training, sk=sk, tile=_planned_tile("f16", sp[0].shape, conv, pol, forced))
     if x.dtype != torch.float32:
         raise ops.HkpError("conv %s under precision %r: no LDS-DMA kernel for this shape and no fp32 input "
                            "for the fp32 kernel" % (tuple(conv.weight.shape), pol.precision))
@@ -448,17 +430,15 @@ def block_forward(block, x, trace=None, final=False, head=None, pol=None, next_c
     if rec is None and head is None and not final and npol.passes == pol.passes and _gram_fusable(block, a, pol):
         return _bottleneck_tail_gram(block, x, a, pol)
     # the last conv and the downsample conv, then both BN parameter sets together
-    fold_last = _fold_request(bns[-1], pol)
-    y_last, part_last = _conv_fwd(convs[-1], bns[-1], a, pol, fold=fold_last)
-    items = [(bns[-1], part_last, y_last.numel() // y_last.shape[-1], fold_last)]
+    y_last, part_last = _conv_fwd(convs[-1], bns[-1], a, pol)
+    items = [(bns[-1], part_last, y_last.numel() // y_last.shape[-1])]
     yd = None
     if block.downsample is not None:
         xd = x
         if y_last.dtype == torch.float16 and x.dtype != torch.float16:
             xd = ops.split_of(x)[0]
-        fold_d = _fold_request(block.downsample[1], pol)
-        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], xd, pol, fold=fold_d)
-        items.append((block.downsample[1], part_d, yd.numel() // yd.shape[-1], fold_d))
+        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], xd, pol)
+        items.append((block.downsample[1], part_d, yd.numel() // yd.shape[-1]))
     params = _bn_params_many(items, pol)
     (last_s, last_m) = params[0]
     sd, md = params[1] if yd is not None else (None, None)
@@ -526,9 +506,8 @@ def _bottleneck_tail_gram(block, x, a2, pol):
         ss3, _ = ops.bn_eval_params(bn3.weight, bn3.bias, bn3.running_mean, bn3.running_var, bn3.eps)
     x16 = x if x.dtype == torch.float16 else ops.split_of(x)[0]
     if block.downsample is not None:
-        fold_d = _fold_request(block.downsample[1], pol)
-        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], x16, pol, fold=fold_d)
-        sd, _ = _bn_params_many([(block.downsample[1], part_d, yd.numel() // yd.shape[-1], fold_d)], pol)[0]
+        yd, part_d = _conv_fwd(block.downsample[0], block.downsample[1], x16, pol)
+        sd, _ = _bn_params(block.downsample[1], part_d, yd.numel() // yd.shape[-1], pol)
         return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=yd, res_ss=sd, relu=True, tile=_fused_tile(pol, a2, c3))
     return ops.conv2d_fwd_f16_bn(a2, wp, ss3, res=x16, relu=True, tile=_fused_tile(pol, a2, c3))
 

@@ -8,7 +8,7 @@ import ctypes
 
 import torch
 
-from ._lib import (BnFold, HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
+from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
                    HKP_KOP_STEM_X3, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
                    HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, ConvDesc, HkpError, call)
 
@@ -55,76 +55,6 @@ def _sk_workspace(enable=True):
 
 def _ptr(t):
     return ctypes.c_void_p(0 if t is None else t.data_ptr())
-
-
-class FoldBN:
-    """The train-mode BN layer whose finalize a forward conv folds in (hkp_bn_fold):
-    the conv's own blocks merge the tile partials they write into scale_shift /
-    mean_invstd and the running statistics — hkp_bn_finalize_ws's bits, without the
-    separate finalize launch.  Pass it as `fold=` to conv2d_fwd_x3 / conv2d_fwd_bnin
-    / conv2d_fwd_f16 / conv2d_fwd_stem_x3 (with stats); afterwards `.done` and the
-    outputs `.scale_shift` [2C], `.mean_invstd` [2C] (as bn_finalize returns)."""
-
-    def __init__(self, gamma, beta, running_mean=None, running_var=None, num_batches_tracked=None, momentum=0.1,
-                 eps=1e-5, want_mean_invstd=True):
-        self.gamma, self.beta = gamma, beta
-        self.running_mean, self.running_var, self.num_batches_tracked = running_mean, running_var, num_batches_tracked
-        self.momentum, self.eps, self.want_mean_invstd = momentum, eps, want_mean_invstd
-        self.scale_shift = self.mean_invstd = None
-        self.done = False
-        self._keep = None
-
-
-# the folded finalize's arrival counters, one zeroed buffer per (device, stream):
-# every conv leaves them zero, and launches on one stream never run concurrently
-_fold_cnt = {}
-
-
-def _fold_counters(nbytes):
-    st = torch.cuda.current_stream()
-    key = (st.device_index, st.cuda_stream)
-    buf = _fold_cnt.get(key)
-    if buf is None or buf.numel() < nbytes:
-        buf = torch.zeros(max(nbytes, 1 << 18), device=torch.device("cuda", st.device_index), dtype=torch.uint8)
-        _fold_cnt[key] = buf
-    return buf
-
-
-def _fold_attach(fold, d, k, rows, device):
-    """Fill an hkp_bn_fold for conv descriptor d (k output channels, rows output
-    pixels) from a FoldBN and point d.bn_fold at it; None: no fold."""
-    if fold is None:
-        return
-    from ._lib import lib
-    for t, nm in ((fold.gamma, "gamma"), (fold.beta, "beta"), (fold.running_mean, "running_mean"),
-                  (fold.running_var, "running_var")):
-        if t is not None:
-            _need(t, torch.float32, "fold." + nm, 1)
-            if t.numel() != k:
-                raise HkpError("fold.%s: %d != K=%d" % (nm, t.numel(), k))
-    if fold.num_batches_tracked is not None:
-        _need(fold.num_batches_tracked, torch.int64, "fold.num_batches_tracked")
-    tiles = (rows + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
-    ss = torch.empty(2 * k, device=device, dtype=torch.float32)
-    mi = torch.empty(2 * k, device=device, dtype=torch.float32) if fold.want_mean_invstd else None
-    nb = lib().hkp_bn_finalize_workspace_bytes(k, tiles)
-    ws = torch.empty((nb + 7) // 8, device=device, dtype=torch.float64)
-    nc = lib().hkp_bn_fold_counter_bytes(ctypes.byref(d))
-    if nc < 0:
-        raise HkpError("hkp_bn_fold_counter_bytes: bad descriptor")
-    cnt = _fold_counters(nc)
-    st = BnFold(_ptr(fold.gamma), _ptr(fold.beta), float(fold.momentum), float(fold.eps), _ptr(fold.running_mean),
-                _ptr(fold.running_var), _ptr(fold.num_batches_tracked), _ptr(ss), _ptr(mi), _ptr(ws), ws.numel() * 8,
-                _ptr(cnt), cnt.numel())
-    d.bn_fold = ctypes.addressof(st)
-    fold._keep = (st, ws)            # alive until the launch returned (the struct is read by the host call)
-    fold.scale_shift, fold.mean_invstd = ss, mi
-
-
-def _fold_done(fold):
-    if fold is not None:
-        fold.done = True
-        fold._keep = None
 
 
 def _need(t, dtype, name, ndim=None):
@@ -247,14 +177,13 @@ def _stat_partials(n_rows, k, device, part_out, name):
 
 
 def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True, tile=0,
-                  products=HKP_X3_ALL, fold=None):
+                  products=HKP_X3_ALL):
     """f16x3 NHWC conv on packed split operands: xs [N,H,W,2C] (from a producer with
     split=3), wp = weight_pack_x3(w) → fp32 y [N,Ho,Wo,K] (+ BN partials, into
     part_out when given).  sk=False: never stream-K (one tile per block);
     tile: HKP_TILE_* policy (0 = the planner); products: HKP_X3_ALL (f16x3), or
     HKP_X3_W16 / HKP_X3_X16 (two of the three products: the weights / the
-    activation at fp16, hkp_conv2d_fwd_x3_products); fold: a FoldBN whose
-    finalize the conv folds in (needs stats)."""
+    activation at fp16, hkp_conv2d_fwd_x3_products)."""
     ws, wsc = wp
     _need(xs, torch.float16, "conv2d_fwd_x3.x_split", 4)
     _need(ws, torch.float16, "conv2d_fwd_x3.w_split", 4)
@@ -268,7 +197,6 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = out if out is not None else torch.empty((n, ho, wo, k), device=xs.device, dtype=torch.float32)
     part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out") if stats else None
-    _fold_attach(fold if stats else None, d, k, n * ho * wo, xs.device)
 
     if products == HKP_X3_ALL:
         def launch():
@@ -286,7 +214,6 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     else:
         _observer(kernel_name(d, kop, sk), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (xs.numel() + ws.numel()) + 4.0 * y.numel(), launch)
-    _fold_done(fold if stats else None)
     return y, part
 
 
@@ -309,7 +236,7 @@ def bnin_kernel(n, h, w, c, k, r, s, stride, pad, dil, f16=False, tile=0, sk=Tru
     return None
 
 
-def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True, sk=True, tile=0, fold=None):
+def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True, sk=True, tile=0):
     """Inference conv whose input is the producer conv's raw output y_in with the
     producer's BN + ReLU applied inside the conv (hkp_conv2d_fwd_x3_bnin for fp32
     y_in with wp = weight_pack_x3(w); hkp_conv2d_fwd_f16_bnin for fp16 y_in with
@@ -332,7 +259,6 @@ def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True, sk=True
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = torch.empty((n, ho, wo, k), device=y_in.device, dtype=torch.float16 if f16 else torch.float32)
     part = _stat_partials(n * ho * wo, k, y_in.device, None, "conv2d_fwd_bnin") if stats else None
-    _fold_attach(fold if stats else None, d, k, n * ho * wo, y_in.device)
     fn = "hkp_conv2d_fwd_f16_bnin" if f16 else "hkp_conv2d_fwd_x3_bnin"
 
     def launch():
@@ -345,7 +271,6 @@ def conv2d_fwd_bnin(y_in, in_ss, wp, stride=1, pad=1, dil=1, stats=True, sk=True
         name = kernel_name(d, HKP_KOP_FWD_F16 if f16 else HKP_KOP_FWD_X3, sk).replace("_kernel<", "_bnin_kernel<")
         _observer(name, 2.0 * n * ho * wo * k * r * s * c,
                   y_in.element_size() * y_in.numel() + 2.0 * ws.numel() + y.element_size() * y.numel(), launch)
-    _fold_done(fold if stats else None)
     return y, part
 
 
@@ -360,7 +285,7 @@ def weight_pack_f16(w):
     return PackedWeight(out, sc)
 
 
-def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0, fold=None):
+def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0):
     """Plain-fp16 NHWC conv (BASELINE config C4): x16 fp16 [N,H,W,C] (a producer's
     split=1 output), wp = weight_pack_f16(w) → y fp16 [N,Ho,Wo,K] (autocast
     semantics) + BN partials from the fp32 accumulators."""
@@ -376,7 +301,6 @@ def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0,
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = torch.empty((n, ho, wo, k), device=x16.device, dtype=torch.float16)
     part = _stat_partials(n * ho * wo, k, x16.device, None, "conv2d_fwd_f16") if stats else None
-    _fold_attach(fold if stats else None, d, k, n * ho * wo, x16.device)
 
     def launch():
         call("hkp_conv2d_fwd_f16", ctypes.byref(d), _ptr(x16), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
@@ -387,7 +311,6 @@ def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0,
     else:
         _observer(kernel_name(d, HKP_KOP_FWD_F16, sk), 2.0 * n * ho * wo * k * r * s * c,
                   2.0 * (x16.numel() + ws.numel() + y.numel()), launch)
-    _fold_done(fold if stats else None)
     return y, part
 
 
@@ -502,7 +425,7 @@ def stem_weight_pack_x3(w):
 STEM_IMAGE_DIRECT = True
 
 
-def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0, image_direct=None, fold=None):
+def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0, image_direct=None):
     """f16x3 stem conv (7x7/s2/p3) → NHWC fp32 y (+ BN partials).  x: the NCHW fp32
     image, or the uint8 NHWC (BGR) batch cv2.imread gives — ToTensor's /255 is then
     fused into the stem's operand split.  tile: 0 = the patch body
@@ -524,7 +447,6 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0, image_direct
     ho, wo = conv_out_hw(h, wd, 7, 7, 2, 3, 1)
     y = torch.empty((n, ho, wo, k), device=x.device, dtype=torch.float32)
     part = _stat_partials(n * ho * wo, k, x.device, part_out, "conv2d_fwd_stem_x3.part_out") if stats else None
-    _fold_attach(fold if stats else None, d, k, n * ho * wo, x.device)
     if image_direct is None:
         image_direct = STEM_IMAGE_DIRECT
     if image_direct and lib().hkp_stem_x3_image_ok(ctypes.byref(d)):
@@ -548,7 +470,6 @@ def conv2d_fwd_stem_x3(x, wp, k, stats=True, part_out=None, tile=0, image_direct
         launch()
     else:
         _observer(kernel_name(d, op), 2.0 * n * ho * wo * k * 49 * c, nbytes, launch)
-    _fold_done(fold if stats else None)
     return y, part
 
 

@@ -69,10 +69,6 @@ class Policy:
     prepack_plan: bool = True
     # BN finalize: two-level merge from this many partial tiles on
     fin_two_level_tiles: int = 2048
-    # train-mode BN finalize folded into the producing conv (hkp_bn_fold: the conv's
-    # last-arriving blocks merge its partials; no separate finalize launch) wherever
-    # the conv runs an LDS-DMA kernel and the statistics are per rank
-    fold_bn: bool = True
     # plain fp16 inference (C4): a Bottleneck's bn3 statistics from conv3's input
     # covariance (1x1 conv: exact), bn3 + residual + ReLU in conv3's epilogue
     gram_bn: bool = True

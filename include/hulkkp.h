@@ -49,31 +49,6 @@ const char* hkp_last_error(void);
 const char* hkp_version(void);
 
 /* ---------------------------------------------------------------- conv ---- */
-/* Train-mode BN finalize folded into a forward conv (hkp_conv_desc.bn_fold): the
- * conv's own blocks merge the BN tile partials they write into the BN layer's
- * parameters — no separate hkp_bn_finalize launch.  The last-arriving tile of each
- * chunk of 128 partial tiles (64 m-tiles of 256 rows) and column tile reduces the
- * chunk; the last chunk of each column tile merges the chunks and writes those
- * channels' outputs: hkp_bn_finalize_ws's arithmetic and order, so the outputs are
- * its bits.  Replaces the separate finalize after every conv of
- * src/resnet.py:46,49,57,61,78,85,87,139,187 (nn.BatchNorm2d train-mode forward). */
-typedef struct hkp_bn_fold {
-    const float* gamma;             /* [k], nullable (1)                                */
-    const float* beta;              /* [k], nullable (0)                                */
-    float momentum, eps;            /* nn.BatchNorm2d momentum (0.1) and eps (1e-5)     */
-    float* running_mean;            /* [k] updated in place; nullable with running_var  */
-    float* running_var;             /* [k] (unbiased variance)                          */
-    int64_t* num_batches_tracked;   /* nullable; += 1                                   */
-    float* scale_shift;             /* [2k] out: gamma*invstd | beta - mean*scale       */
-    float* mean_invstd;             /* [2k] out, nullable                               */
-    void* workspace;                /* the chunk results, hkp_bn_finalize_workspace_bytes(k, tiles) */
-    int64_t ws_bytes;
-    uint32_t* counters;             /* arrival counters, hkp_bn_fold_counter_bytes(d): ZERO on
-                                       entry, every call leaves them zero (one set per stream:
-                                       calls on one set must not run concurrently)        */
-    int64_t counter_bytes;
-} hkp_bn_fold;
-
 typedef struct hkp_conv_desc {
     int32_t n, h, w, c;             /* input batch, height, width, channels            */
     int32_t k, r, s;                /* output channels, filter height, filter width    */
@@ -81,15 +56,7 @@ typedef struct hkp_conv_desc {
     int32_t in_layout;              /* HKP_LAYOUT_NHWC, or HKP_LAYOUT_NCHW (stem only)  */
     int32_t tile;                   /* x3 / fp16 conv tile policy, HKP_TILE_* (0: the
                                        planner).  Per call — no process-global state */
-    const hkp_bn_fold* bn_fold;     /* forward convs with stat_partials on the LDS-DMA
-                                       kernels (hkp_conv2d_fwd_x3 / _x3_products / _x3_bnin /
-                                       _f16 / _f16_bnin / _stem_x3 / _stem_x3_image): NULL, or
-                                       the BN layer whose finalize the conv folds in.  Every
-                                       other entry point requires NULL */
 } hkp_conv_desc;
-
-/* counter bytes a folded finalize of this forward conv needs (hkp_bn_fold.counters) */
-int64_t hkp_bn_fold_counter_bytes(const hkp_conv_desc* d);
 
 /* Tile policies of the packed-operand convs (hkp_conv2d_fwd_x3 / _fwd_f16 /
  * _bwd_data_x3 / _bwd_data_x3_strided).  AUTO: fewest rounds of blocks over the

@@ -49,6 +49,11 @@ void hkp_debug_x3_pair128(int32_t on);
  * (forward and backward) as batched-load loops where the default holds a tile
  * lane's partials in registers after one load round — the same bits either way. */
 void hkp_debug_fin_regs(int32_t on);
+/* A/B probe (tools/ only, not thread-safe): the one-tile conv bodies read the A
+ * operand of output row m from row m % rows (0 = off): the outputs are wrong, the
+ * activation stream L2-resident — times a conv's K loop without the HBM / MALL
+ * latency of its activation lines (tools/conv_ab.py --a-wrap). */
+void hkp_debug_x3_a_wrap(int32_t rows);
 
 #ifdef __cplusplus
 }

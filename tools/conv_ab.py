@@ -74,6 +74,8 @@ def main():
     ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B)")
     ap.add_argument("--duo-staggers", default="-1", help="DUO first-round stagger(s) in ns to cross with the "
                     "tiles (hkp_debug_duo_stagger: 0 off, -1 the default estimate)")
+    ap.add_argument("--a-wraps", default="0", help="A-row wraps to cross with the tiles (hkp_debug_x3_a_wrap: "
+                    "0 off; e.g. 2048 = every tile reads the first 8 m-tiles' A rows, an L2-resident stream)")
     ap.add_argument("--stores", default="0", help="epilogue store flavours to cross with the tiles "
                     "(hkp_debug_x3_store: 0 default, 1 plain, 2 nt, 3 sc1, 4 sc0 sc1)")
     args = ap.parse_args()
@@ -85,15 +87,16 @@ def main():
     from hkp import ops
     from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
     from hkp._lib import lib
-    forms = [(int(t), int(k), int(d)) for t in args.tiles.split(",") for k in args.stores.split(",")
-             for d in args.duo_staggers.split(",")]
+    forms = [(int(t), int(k), int(d), int(aw)) for t in args.tiles.split(",") for k in args.stores.split(",")
+             for d in args.duo_staggers.split(",") for aw in args.a_wraps.split(",")]
 
-    def set_store(k, d=-1):
+    def set_store(k, d=-1, aw=0):
         if hasattr(lib(), "hkp_debug_x3_store"):
             lib().hkp_debug_x3_store(k)
             lib().hkp_debug_duo_stagger(d)
-        elif (k, d) != (0, -1):
-            raise SystemExit("--stores / --duo-staggers need the A/B build: make -C hulk-keypoints_amd/csrc ab")
+            lib().hkp_debug_x3_a_wrap(aw)
+        elif (k, d, aw) != (0, -1, 0):
+            raise SystemExit("--stores / --duo-staggers / --a-wraps need the A/B build: make -C hulk-keypoints_amd/csrc ab")
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     for name in args.shapes.split(","):
@@ -120,7 +123,7 @@ def main():
         for r in range(args.rounds):
             for f in forms:
                 t = f[0]
-                set_store(f[1], f[2])
+                set_store(f[1], f[2], f[3])
                 y = run(t)
                 if r == 0:
                     outs[f] = y.float()
@@ -139,11 +142,11 @@ def main():
         for f in forms:
             t = f[0]
             ts = sorted(times[f])
-            set_store(f[1], f[2])
+            set_store(f[1], f[2], f[3])
             kn = ops.kernel_name(ConvDesc(n, h, w, ci, co, k, k, st, pd, dl, 0, t), op)
             set_store(0)
-            print("%-9s tile %d store %d stagger %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
-                  "max rel diff=%.1e" % (name, t, f[1], f[2], ts[len(ts) // 2], ts[0],
+            print("%-9s tile %d store %d stagger %d a_wrap %d: median %.3f ms  min %.3f ms  (%.0f TF/s issued)  %s  "
+                  "max rel diff=%.1e" % (name, t, f[1], f[2], f[3], ts[len(ts) // 2], ts[0],
                                          flops / (ts[len(ts) // 2] * 1e-3) / 1e12, kn, same), flush=True)
 
 

@@ -3,7 +3,9 @@
 # gpurun call; outputs under gpurun_out/<name>/).
 #   hbm       per-kernel HBM tables (kernel trace + PMC passes over every kernel) of
 #             C2 (batch 32) and the north_star shard (batch 8), and the default bench line
-#   fold      the folded BN finalize: its tests, C2 / B=8 / C4 / C3-train A/B (Policy.fold_bn)
+#   (fold / fold2, the folded BN finalize A/Bs, ran against the experiment's commit
+#   0a6ba20 and went with it; their logs are profiles/r06_fold_v*)
+#   awrap     C4 1x1 convs with an L2-resident A window (AB build): what bounds the K loop
 #   prec      per-stage precision plans at C4 (Policy.stage_precision): tests + study table
 #   plan      the measured tile plan (tools/tile_sweep.py) and its A/B against the C planner
 #   check     GPU suite + the default bench line
@@ -39,17 +41,12 @@ hbm)
     python3 tools/hbm_table.py $O/b8_kernel_stats.csv $O/pmc_b8/pmc_summary.json --steps 22 --top 40 > $O/b8_hbm_table.txt
     echo "b8 ok"
     ;;
-fold)
-    # the BN finalize folded into the conv grid: its parity tests, the BN / forward
-    # tests around it, then in-process A/Bs (Policy.fold_bn) on C2, the B=8 shard,
-    # C4 and the C3 training shard
-    timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_fold.py \
-        > $O/pytest_fold.log 2>&1
-    echo "pytest fold: $(tail -1 $O/pytest_fold.log)"
-    timeout -k 10 400 python -u tools/infer_ab.py "" "fold_bn=0" --batch 8 --rounds 7 --iters 20 > $O/ab_b8.log 2>&1
-    timeout -k 10 400 python -u tools/infer_ab.py "" "fold_bn=0" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
-    timeout -k 10 500 python -u tools/infer_ab.py "" "fold_bn=0" $C4 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
-    timeout -k 10 500 python -u tools/train_ab.py "" "fold_bn=0" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+awrap)
+    # verdict item 1 probe (AB build): C4's 1x1 convs with their A rows wrapped to an
+    # L2-resident window (hkp_debug_x3_a_wrap) — if the K loop speeds up to the MFMA
+    # rate, the stream of A from HBM (not the LDS / MFMA schedule) bounds it
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0 --a-wraps 0,4096,1024,256 --rounds 5 --iters 10 \
+        --shapes c4_l4_c3,c4_l4_ds,c4_l4_c1,c4_l3_c3,c4_l3_c1 > $O/conv_ab.log 2>&1
     ;;
 prec)
     # per-stage precision at C4 (Policy.stage_precision): the plan tests, then the study table
@@ -57,26 +54,6 @@ prec)
         -k "stage_precision or r50" tests/test_gpu_scale.py > $O/pytest_prec.log 2>&1
     echo "pytest prec: $(tail -1 $O/pytest_prec.log)"
     timeout -k 10 600 python -u tests/precision_study.py --rounds 3 --iters 3 > $O/precision_study.log 2>&1
-    ;;
-fold2)
-    # the folded finalize with device-scope partial stores and the early arrival: its
-    # tests, in-process A/Bs (Policy.fold_bn), and the pre-fold build (round-6 start,
-    # tools/ab_lib/libhulkkp_base.so) against this one in alternating processes
-    timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_fold.py \
-        > $O/pytest_fold.log 2>&1
-    echo "pytest fold: $(tail -1 $O/pytest_fold.log)"
-    timeout -k 10 400 python -u tools/infer_ab.py "" "fold_bn=0" --batch 8 --rounds 7 --iters 20 > $O/ab_b8.log 2>&1
-    timeout -k 10 400 python -u tools/infer_ab.py "" "fold_bn=0" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
-    timeout -k 10 500 python -u tools/infer_ab.py "" "fold_bn=0" $C4 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
-    timeout -k 10 500 python -u tools/train_ab.py "" "fold_bn=0" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
-    for i in 1 2; do
-        timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline --lib tools/ab_lib/libhulkkp_base.so \
-            --tune fold_bn=0 > $O/bench_base_$i.log 2>&1
-        timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline > $O/bench_new_$i.log 2>&1
-        timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline --batch 8 --lib tools/ab_lib/libhulkkp_base.so \
-            --tune fold_bn=0 > $O/bench_b8_base_$i.log 2>&1
-        timeout -k 10 300 python -u bench.py --no-extras --no-cpu-baseline --batch 8 > $O/bench_b8_new_$i.log 2>&1
-    done
     ;;
 plan)
     # the measured tile plan: sweep every live tile policy over the workloads' forward
