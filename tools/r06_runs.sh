@@ -8,6 +8,7 @@
 #   awrap     C4 1x1 convs with an L2-resident A window (AB build): what bounds the K loop
 #   prec      per-stage precision plans at C4 (Policy.stage_precision): tests + study table
 #   plan      the measured tile plan (tools/tile_sweep.py) and its A/B against the C planner
+#   prof      the final tree's traces (C2 + PMC, B=8, C4, C3 train) and bench lines
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -66,6 +67,28 @@ plan)
     timeout -k 10 400 python -u tools/infer_ab.py "" "tile_plan=0" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "" "tile_plan=0" $C4 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
     timeout -k 10 500 python -u tools/train_ab.py "" "tile_plan=0" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    ;;
+prof)
+    # the final tree's traces and C2 PMC passes (copied into profiles/ on the box so
+    # the bench lines after them read this tree's trace), then the C2, B=8, C4 and
+    # C3-train bench lines
+    trace c2 "--steps 5 --warmup 2"
+    cp $O/c2_kernel_stats.csv profiles/r06_infer_c2_kernel_stats_v2.csv
+    bash tools/pmc_passes.sh $O/pmc_c2 "--steps 2 --warmup 1 --no-extras" "." > $O/pmc_c2.log 2>&1
+    cp $O/pmc_c2/pmc_summary.json profiles/r06_infer_c2_pmc_v2.json
+    python3 tools/hbm_table.py $O/c2_kernel_stats.csv $O/pmc_c2/pmc_summary.json --steps 12 --top 40 > $O/c2_hbm_table.txt
+    echo "c2 ok"
+    trace b8 "--batch 8 --steps 10 --warmup 2"
+    cp $O/b8_kernel_stats.csv profiles/r06_b8_kernel_stats_v2.csv
+    trace c4 "$C4 --steps 5 --warmup 2"
+    cp $O/c4_kernel_stats.csv profiles/r06_infer_c4_kernel_stats_v1.csv
+    trace train "--mode train --steps 5 --warmup 2"
+    cp $O/train_kernel_stats.csv profiles/r06_train_c3_kernel_stats_v1.csv
+    echo "traces ok"
+    timeout -k 10 300 python -u bench.py > $O/bench_c2.log 2>&1
+    timeout -k 10 300 python -u bench.py --batch 8 --no-cpu-baseline --no-extras > $O/bench_b8.log 2>&1
+    timeout -k 10 300 python -u bench.py $C4 --no-cpu-baseline --no-extras > $O/bench_c4.log 2>&1
+    timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline --no-extras > $O/bench_train.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
