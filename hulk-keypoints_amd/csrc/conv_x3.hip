@@ -255,6 +255,8 @@ constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
 // B (the weights, L2-resident) 2 stages: 5 x 32 KiB = the whole 160 KiB; the
 // epilogue's scratch and column scales reuse the drained ring.
 constexpr int X3_A3_LDS = 5 * 256 * 128;
+// ... with BM-row A stages (A3_192: 192-row tiles, 136 KiB)
+constexpr int x3_a3_lds(int BM) { return 3 * BM * 128 + 2 * 256 * 128; }
 
 // BN-partials scratch (x3_bn_partials_w: [2][WM][BN] floats) past the ring, so
 // the epilogue needs no barrier before it, then the tile's BN column scales
@@ -463,6 +465,8 @@ __device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int 
 // scratch (red: [2][WM][BN] floats, outside anything still being read):
 //   n = na + nb,  sum = sa + sb,  M2 = M2a + M2b + (mb - ma)^2 * na*nb / n.
 // Same quantities as x3_bn_partials (sum, M2 about the half-tile mean).
+// A wave covers 16 * NI rows (WM = 4 waves: NI = 4 for the 256-row tiles, 3 for the
+// 192-row A3 tiles), so a partial tile (a half tile) holds 32 * NI rows: 128 / 96.
 // VEC(i, j): the f32x4 of accumulator rows ROW(i, 0..3) of column block j.
 // SC(j): the column's output scale (a power of two: sums scale by it, M2 by its
 // square, exactly) when VEC is the unscaled accumulator.
@@ -484,8 +488,9 @@ template <int BN, int NI, int NJ, int CW, int SHF, typename Vec, typename Row, t
 __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, int m0, int n0, int wm, int wn,
                                                  int lane, Vec&& vec, Row&& row, Sc&& sc_of,
                                                  float* wide = nullptr) {
-    if constexpr (CW == 16 && SHF == 16 && NI == 4) {
-        if (wide != nullptr && m0 + 256 <= a.M) {                    // block-uniform
+    constexpr int WROWS = 16 * NI;                                   // rows per wave
+    if constexpr (CW == 16 && SHF == 16 && (NI == 4 || NI == 3)) {
+        if (wide != nullptr && m0 + 4 * WROWS <= a.M) {              // block-uniform
             const int q = lane >> 4, r16 = lane & 15;
             constexpr float inv = 1.f / (NI * 4);
             float ls[NJ], lq[NJ];
@@ -526,15 +531,17 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
                         s[g] = wide[(w4 + g) * BN + c];
                         qq[g] = wide[16 * BN + (w4 + g) * BN + c];
                     }
-                    x3_chan_merge(s[0], qq[0], s[1], qq[1], 1.f / 16, 8.f);     // lane pairs l, l ^ 16
-                    x3_chan_merge(s[2], qq[2], s[3], qq[3], 1.f / 16, 8.f);
-                    x3_chan_merge(s[0], qq[0], s[2], qq[2], 1.f / 32, 16.f);    // then l, l ^ 32
+                    // groups of n1 = 4 * NI rows: Chan's factor n_a n_b / n = n1 / 2, ...
+                    constexpr float n1 = 4.f * NI;
+                    x3_chan_merge(s[0], qq[0], s[1], qq[1], 1.f / n1, n1 / 2);   // lane pairs l, l ^ 16
+                    x3_chan_merge(s[2], qq[2], s[3], qq[3], 1.f / n1, n1 / 2);
+                    x3_chan_merge(s[0], qq[0], s[2], qq[2], 1.f / (2 * n1), n1); // then l, l ^ 32
                     S[v] = s[0];
                     Q[v] = qq[0];
                 }
-                x3_chan_merge(S[0], Q[0], S[1], Q[1], 1.f / 64, 32.f);          // even wave, odd wave
+                x3_chan_merge(S[0], Q[0], S[1], Q[1], 1.f / (16 * NI), 8.f * NI);   // even wave, odd wave
                 const float sc = wide[32 * BN + c];
-                const long tile128 = (long)(m0 >> 7) + h;
+                const long tile128 = (long)(m0 / (2 * WROWS)) + h;
                 a.part[(tile128 * a.K + n0 + c) * 2 + 0] = S[0] * sc;
                 a.part[(tile128 * a.K + n0 + c) * 2 + 1] = Q[0] * (sc * sc);
             }
@@ -543,9 +550,9 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
     }
     float* rs = red;                                                 // [WM][BN] wave sums
     float* rq = red + 4 * BN;                                        // [WM][BN] wave M2
-    const int nw = min(64, max(0, a.M - (m0 + 64 * wm)));          // valid rows of this wave (a prefix)
+    const int nw = min(WROWS, max(0, a.M - (m0 + WROWS * wm)));    // valid rows of this wave (a prefix)
     float ls[NJ], lq[NJ], ln;
-    if (nw == 64) {                                                  // every row valid: no masks
+    if (nw == WROWS) {                                               // every row valid: no masks
         ln = (float)(NI * 4);
         constexpr float inv = 1.f / (NI * 4);
 #pragma unroll
@@ -615,9 +622,9 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
         }
     }
     lds_sync();
-    const int nb = min(64, max(0, a.M - (m0 + 64 * (wm | 1))));     // valid rows of the odd wave of the half
+    const int nb = min(WROWS, max(0, a.M - (m0 + WROWS * (wm | 1))));   // valid rows of the odd wave of the half
     if ((wm & 1) || nw == 0 || lane >= CW) return;
-    const long tile128 = (long)(m0 >> 7) + (wm >> 1);
+    const long tile128 = (long)(m0 / (2 * WROWS)) + (wm >> 1);
     const float ia = 1.f / (float)nw, ib = nb > 0 ? 1.f / (float)nb : 0.f;
     const float f = (float)nw * (float)nb / (float)(nw + nb);
 #pragma unroll
@@ -750,21 +757,22 @@ __device__ __forceinline__ void x3_ep_store(float* ssl, const X3EpSS& r, int tid
 // wave's reads of t), barrier, [read A frags of t+1] then per column block j:
 // [MFMAs of t with B_j] [refill B_j with t+1's].  NST 2 (256x256; 256x64 pairs):
 // A single-buffered, t+2's DMA issued right after the barrier into t's buffer.
-template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, typename Issue, typename IssueA,
+template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, int BM, typename Issue, typename IssueA,
           typename IssueB>
 __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
                                                   Issue& issue_next, IssueA& issue_a, IssueB& issue_b) {
-    constexpr int BM = 256, WM = 4, WN = 2, ROW = 128;
+    constexpr int WM = 4, WN = 2, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
     constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
+    static_assert(BM == 256 || (A3 && BM == 192 && P != 1), "192-row tiles: the A3 body, packed operands");
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
     static_assert(!A3 || (BN == 256 && NST == 2), "A3: the 256x256 body");
     // PAIRB and A3 have no LDS past the ring: the epilogue's scratch is the drained
     // ring and the column scales are loaded in the epilogue
     constexpr bool RINGSCR = PAIRB || A3;
     constexpr int RED_OFF = RINGSCR ? 0 : x3_lds_bytes(BN, PAIRB, P);
-    constexpr int LDS_ALL = A3 ? X3_A3_LDS : x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB);
+    constexpr int LDS_ALL = A3 ? x3_a3_lds(BM) : x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB);
     float* const scl = (float*)(smem + RED_OFF + 2 * 4 * BN * 4);   // [BN] column scales (!RINGSCR)
     float sclv = 1.f;                              // issued before the fill, stored after it
     if constexpr (!RINGSCR) {
@@ -1060,7 +1068,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         // wave's 63 outstanding memory ops, so the waves stalled on their
         // completion instead of ending and letting the next block start.
         // 256-wide tiles stage half the rows per pass (128 KiB).
-        constexpr int PASSES = BN == 256 ? 2 : 1, RPP = 256 / PASSES, PITCH = BN + 4, C4 = BN / 4;
+        constexpr int PASSES = BN == 256 ? 2 : 1, RPP = BM / PASSES, PITCH = BN + 4, C4 = BN / 4;
         static_assert(RPP * PITCH * 4 <= LDS_ALL, "staging");
         float* t = (float*)smem;
         lds_sync();                                    // every wave done with the ring and the partials' scratch
@@ -1121,9 +1129,9 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // MI355X_MICROARCH.md "DVFS give-back" item 7).
 // P: operand layout and products (x3_products) — 3 packed f16x3 split, 2 / 4
 // packed split with two of its three products, 1 plain fp16.
-template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false>
+template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false, int BM = 256>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
-    constexpr int BM = 256, WM = 4, WN = 2;
+    constexpr int WM = 4, WN = 2;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     constexpr int ROW = 128;                       // bytes per LDS row (one packed line)
     constexpr int CPR = ROW / 16;                  // 16-B chunks per row
@@ -1139,6 +1147,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
     static_assert(!A3 || (BN == 256 && !STEM && !PAIR && MFD == 16), "A3: the 256x256 16x16x32 body");
+    static_assert(BM == 256 || (A3 && BM == 192 && x3_packed(P)), "192-row tiles: A3, packed operands");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
@@ -1275,7 +1284,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     };
 
     if constexpr (MFD == 16) {
-        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
+        conv_x3_mf16_body<BN, NST, STAGE, GL, P, A3, GA, BM>(a, smem, tile, ks, nks, partial, m0, n0, wm, wn, lane,
                                                              tid, issue_next, issue_a, issue_b);
         return;
     } else {
@@ -1526,6 +1535,19 @@ template <int P>
 __global__ __launch_bounds__(512, 1) void conv_x3_a3_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[X3_A3_LDS];
     conv_x3_a3_grid<P>(a, smem);
+}
+
+// The A3 body on 192 x 256 tiles (HKP_TILE_192_A3, packed operands): a grid whose
+// 256-row tiles leave most CUs idle in a single partial round — the B=8 shard's
+// layer3, 150 m-tiles on 256 CUs — runs ceil(M / 192) blocks in the same one
+// round, each 3/4 of a tile (200 m-tiles: 0.78 of the CUs instead of 0.59).
+// Waves 4 x 2 as in A3 (48 x 128 each, 96 accumulators), the A ring 3 stages of
+// 192 lines; BN partials per 96-row half tile (hkp_bn_finalize tile_rows 96).
+template <int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_a3_192_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_a3_lds(192)];
+    x3_stamp(a, 0);
+    conv_x3_tile<256, false, false, 16, P, true, 192>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -3167,6 +3189,7 @@ struct X3Choice {
     bool halo = false;                 // conv_x3_halo_kernel<P>
     bool a3 = false;                   // conv_x3_a3_kernel<P> (256x256, 3-stage A ring)
     bool duo = false;                  // conv_x3_duo_kernel<1> (256x128, two 4-wave blocks per CU)
+    int bm = 256;                      // rows per tile (192: conv_x3_a3_192_kernel<P>)
 };
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
@@ -3192,6 +3215,8 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
     // the overlapped dgrad's A3 request (Policy.dgrad_overlap_tile) on a 64- or
     // 128-channel output, which A3 cannot take: plan it as AUTO (the rules below)
     if (policy == HKP_TILE_256_A3 && P == 3 && k % 256 != 0 && g_x3_pair128) policy = HKP_TILE_AUTO;
+    // 192-row A3 tiles: packed operands with 256-divisible outputs; AUTO otherwise
+    if (policy == HKP_TILE_192_A3 && (!x3_packed(P) || k % 256 != 0)) policy = HKP_TILE_AUTO;
     if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
     X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
     if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
@@ -3229,7 +3254,8 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
 static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int policy, int halo) {
     // the halo-tile body wherever the shape allows it, unless a tile body is forced
     if ((halo >= 1 && policy == HKP_TILE_HALO) ||
-        (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3))) {
+        (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3 ||
+                       policy == HKP_TILE_192_A3))) {
         X3Choice c{64, 16, true, false};
         c.halo = true;
         return c;
@@ -3252,6 +3278,13 @@ static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int pol
         case HKP_TILE_256_A3:              // the same on the A3 body
             if (k % 256 == 0) return {256, 16, false, false, false, true};
             break;
+        case HKP_TILE_192_A3:              // 192x256 tiles on the A3 body (x3_choose checked the operands)
+            if (k % 256 == 0) {
+                X3Choice c{256, 16, false, false, false, true};
+                c.bm = 192;
+                return c;
+            }
+            break;
         default:
             break;
     }
@@ -3268,7 +3301,7 @@ static const X3Choice X3_STEM{64, 16, true, false};
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
     if (c.duo) return snprintf(buf, len, "conv_x3_duo_kernel<%d>", P);
-    if (c.a3) return snprintf(buf, len, "conv_x3_a3_kernel<%d>", P);
+    if (c.a3) return snprintf(buf, len, c.bm == 192 ? "conv_x3_a3_192_kernel<%d>" : "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
@@ -3367,6 +3400,15 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         }
         return;
     }
+    if (c.bm == 192) {                     // one tile per block, no split-K tail
+        const long mt = ((long)a.M + 191) / 192;
+        const dim3 g192((unsigned)(mt * a.n_tiles));
+        x3_dispatch_p(P, [&](auto pc) {
+            if constexpr (x3_packed(pc.value))
+                hipLaunchKernelGGL(conv_x3_a3_192_kernel<pc.value>, g192, dim3(512), 0, st, a);
+        });
+        return;
+    }
     dim3 grid((unsigned)(m_tiles * a.n_tiles));
     if (c.sk) {
         a.sk_units = m_tiles * a.nks;
@@ -3457,7 +3499,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_RESERVED_14, "%s: unknown tile policy %d", who,
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_192_A3, "%s: unknown tile policy %d", who,
                   d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8 && d->tile != HKP_TILE_RESERVED_14,
                   "%s: tile policy %d is retired (a persistent conv body, measured slower)", who, d->tile);
@@ -3871,6 +3913,13 @@ extern "C" int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* 
     else hipLaunchKernelGGL(conv_x3_stem_patch_kernel<1>, grid, dim3(512), 0, as_stream(stream), a);
     HKP_LAUNCH_CHECK("hkp_conv2d_fwd_stem_x3_image");
     return HKP_OK;
+}
+
+// rows per BN statistic tile of a packed forward conv (see hulkkp.h)
+extern "C" int32_t hkp_conv_x3_stat_tile_rows(const hkp_conv_desc* d, int32_t op) {
+    HKP_CHECK_ARG(d, "hkp_conv_x3_stat_tile_rows: null descriptor");
+    const bool packed = op == HKP_KOP_FWD_X3 || op == HKP_KOP_FWD_X3_W16 || op == HKP_KOP_FWD_X3_X16;
+    return packed && d->tile == HKP_TILE_192_A3 && d->k % 256 == 0 ? 96 : 128;
 }
 
 // the kernel symbol a launch with this descriptor runs (see hulkkp.h)

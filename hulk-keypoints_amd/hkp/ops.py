@@ -10,7 +10,7 @@ import torch
 
 from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
                    HKP_KOP_STEM_X3, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
-                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, ConvDesc, HkpError, call)
+                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, HKP_TILE_192_A3, ConvDesc, HkpError, call)
 
 CONV_TILE_ROWS = 128  # BM of conv_fwd.hip (rows per BN statistic tile)
 
@@ -163,17 +163,27 @@ def channels_of(x):
     return x.shape[-1]
 
 
-def _stat_partials(n_rows, k, device, part_out, name):
-    """BN tile partials [tiles, k, 2] of an n_rows-pixel conv output: part_out (a
-    caller's slice of a larger buffer — the inference lanes share one per layer)
-    or a new tensor."""
-    tiles = (n_rows + CONV_TILE_ROWS - 1) // CONV_TILE_ROWS
+def _stat_partials(n_rows, k, device, part_out, name, tile_rows=CONV_TILE_ROWS):
+    """BN tile partials [tiles, k, 2] of an n_rows-pixel conv output, tile_rows rows
+    per tile: part_out (a caller's slice of a larger buffer) or a new tensor.  A
+    tile size other than CONV_TILE_ROWS rides on the tensor (_hkp_tile_rows) to
+    bn_finalize / bn_stats."""
+    tiles = (n_rows + tile_rows - 1) // tile_rows
     if part_out is None:
-        return torch.empty((tiles, k, 2), device=device, dtype=torch.float32)
-    _need(part_out, torch.float32, name, 3)
-    if tuple(part_out.shape) != (tiles, k, 2):
-        raise HkpError("%s: shape %s != %s" % (name, tuple(part_out.shape), (tiles, k, 2)))
-    return part_out
+        part = torch.empty((tiles, k, 2), device=device, dtype=torch.float32)
+    else:
+        _need(part_out, torch.float32, name, 3)
+        if tuple(part_out.shape) != (tiles, k, 2):
+            raise HkpError("%s: shape %s != %s" % (name, tuple(part_out.shape), (tiles, k, 2)))
+        part = part_out
+    if tile_rows != CONV_TILE_ROWS:
+        part._hkp_tile_rows = tile_rows
+    return part
+
+
+def stat_tile_rows(part):
+    """Rows per BN statistic tile of conv partials (hkp_conv_x3_stat_tile_rows)."""
+    return getattr(part, "_hkp_tile_rows", CONV_TILE_ROWS)
 
 
 def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out=None, sk=True, tile=0,
@@ -196,18 +206,23 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = out if out is not None else torch.empty((n, ho, wo, k), device=xs.device, dtype=torch.float32)
-    part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out") if stats else None
+    kop = HKP_KOP_FWD_X3 if products == HKP_X3_ALL else HKP_KOP_FWD_X3_W16 if products == 2 else HKP_KOP_FWD_X3_X16
+    part = None
+    if stats:
+        rows = CONV_TILE_ROWS
+        if tile == HKP_TILE_192_A3:            # 96-row statistic tiles (the library says)
+            from ._lib import lib
+            rows = lib().hkp_conv_x3_stat_tile_rows(ctypes.byref(d), kop)
+        part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out", rows)
 
     if products == HKP_X3_ALL:
         def launch():
             call("hkp_conv2d_fwd_x3", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),
                  *_sk_workspace(sk), _stream())
-        kop = HKP_KOP_FWD_X3
     else:
         def launch():
             call("hkp_conv2d_fwd_x3_products", ctypes.byref(d), _ptr(xs), _ptr(ws), _ptr(wsc), int(products),
                  _ptr(y), _ptr(part), *_sk_workspace(sk), _stream())
-        kop = HKP_KOP_FWD_X3_W16 if products == 2 else HKP_KOP_FWD_X3_X16
 
     if _observer is None:
         launch()
@@ -540,11 +555,11 @@ def bn_finalize(part, count, gamma, beta, running_mean=None, running_var=None, n
         from ._lib import lib
         nb = lib().hkp_bn_finalize_workspace_bytes(c, tiles)
         ws = torch.empty((nb + 7) // 8, device=part.device, dtype=torch.float64)
-        call("hkp_bn_finalize_ws", c, count, tiles, CONV_TILE_ROWS, _ptr(part), _ptr(gamma), _ptr(beta), momentum,
+        call("hkp_bn_finalize_ws", c, count, tiles, stat_tile_rows(part), _ptr(part), _ptr(gamma), _ptr(beta), momentum,
              eps, _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi), _ptr(ws),
              nb, _stream())
         return ss, mi
-    call("hkp_bn_finalize", c, count, tiles, CONV_TILE_ROWS, _ptr(part), _ptr(gamma), _ptr(beta), momentum, eps,
+    call("hkp_bn_finalize", c, count, tiles, stat_tile_rows(part), _ptr(part), _ptr(gamma), _ptr(beta), momentum, eps,
          _ptr(running_mean), _ptr(running_var), _ptr(num_batches_tracked), _ptr(ss), _ptr(mi), _stream())
     return ss, mi
 
@@ -561,7 +576,7 @@ def bn_stats(part, count, two_level_tiles=FIN_TWO_LEVEL_TILES):
         from ._lib import lib
         nb = lib().hkp_bn_finalize_workspace_bytes(c, tiles)
         ws = torch.empty((nb + 7) // 8, device=part.device, dtype=torch.float64)
-    call("hkp_bn_stats", c, count, tiles, CONV_TILE_ROWS, _ptr(part), _ptr(st), _ptr(ws), nb, _stream())
+    call("hkp_bn_stats", c, count, tiles, stat_tile_rows(part), _ptr(part), _ptr(st), _ptr(ws), nb, _stream())
     return st
 
 

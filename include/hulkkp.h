@@ -89,6 +89,11 @@ typedef struct hkp_conv_desc {
                                          operand layouts plan as AUTO */
 #define HKP_TILE_RESERVED_14 14      /* retired: the persistent A3 body (measured slower on every shape,
                                          round 5); rejected with HKP_ERR_BAD_ARG */
+#define HKP_TILE_192_A3 15            /* packed operands (x3 forward / dgrad), Cout % 256 == 0: the A3
+                                         body on 192 x 256 tiles (one partial round of 256-row
+                                         tiles on many fewer tiles than CUs); its BN partials are
+                                         per 96-row tile: hkp_bn_finalize(..., tile_rows = 96, ...)
+                                         over ceil(M / 96) tiles.  Other shapes plan as AUTO */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);
@@ -233,6 +238,12 @@ int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, co
 #define HKP_KOP_STEM_X3_IMAGE 7     /* hkp_conv2d_fwd_stem_x3_image, fp32 NCHW image */
 #define HKP_KOP_STEM_X3_IMAGE_U8 8  /* hkp_conv2d_fwd_stem_x3_image, uint8 NHWC batch */
 int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf, int32_t len);
+/* Rows per BN statistic tile of a packed forward conv (op HKP_KOP_FWD_X3 / _W16 /
+ * _X16) with this descriptor: 96 with d->tile == HKP_TILE_192_A3 (and k % 256 == 0),
+ * else 128 (hkp_conv_stat_tiles' tiles).  stat_partials then holds
+ * ceil(M / rows) * k * 2 floats, and hkp_bn_finalize / _ws / hkp_bn_stats take
+ * tile_rows = rows (src/resnet.py:46,49: the statistics are the same). */
+int32_t hkp_conv_x3_stat_tile_rows(const hkp_conv_desc* d, int32_t op);
 
 /* (The A/B instruments — hkp_debug_* — are not part of this library: they exist only
  * in the tools build, include/hulkkp_ab.h.) */

@@ -191,6 +191,22 @@ def test_kernel_name_query():
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3_W16) == "conv_x3_a3_kernel<2>"
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3_X16) == "conv_x3_a3_kernel<4>"
+    # the 192-row A3 tiles: packed operands with Cout % 256 == 0 (forward and dgrad), 96-row
+    # BN statistic tiles; plain fp16 and narrower outputs plan as AUTO (128-row tiles)
+    d.tile = _lib.HKP_TILE_192_A3
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_192_kernel<3>"
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3_W16) == "conv_x3_a3_192_kernel<2>"
+    assert ops.kernel_name(d, _lib.HKP_KOP_FWD_F16) == ops.kernel_name(
+        _lib.ConvDesc(*[getattr(d, f) for f, _ in d._fields_[:-1]], 0), _lib.HKP_KOP_FWD_F16)
+    rows = _lib.lib().hkp_conv_x3_stat_tile_rows
+    assert rows(ctypes.byref(d), _lib.HKP_KOP_FWD_X3) == 96 and rows(ctypes.byref(d), _lib.HKP_KOP_FWD_F16) == 128
+    b8 = _lib.ConvDesc(8, 60, 80, 256, 256, 3, 3, 1, 2, 2, 0, _lib.HKP_TILE_192_A3)
+    assert ops.kernel_name(b8, _lib.HKP_KOP_DGRAD_X3) == "conv_x3_a3_192_kernel<3>"
+    narrow = _lib.ConvDesc(8, 60, 80, 256, 128, 3, 3, 1, 2, 2, 0, _lib.HKP_TILE_192_A3)
+    assert "a3_192" not in ops.kernel_name(narrow, _lib.HKP_KOP_FWD_X3)
+    assert rows(ctypes.byref(narrow), _lib.HKP_KOP_FWD_X3) == 128
+    b8.tile = 0
+    assert rows(ctypes.byref(b8), _lib.HKP_KOP_FWD_X3) == 128
     d.tile = _lib.HKP_TILE_64_PAIR
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"
     d.tile = 99

@@ -7,8 +7,8 @@ import torch.nn.functional as F
 
 from oracle import cpu_ref, recipe
 
-# every live HKP_TILE_* policy past AUTO (7 and 8 are retired)
-LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11, 13)
+# every live HKP_TILE_* policy past AUTO (7, 8 and 14 are retired)
+LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11, 13, 15)
 
 pytestmark = pytest.mark.gpu
 
@@ -680,6 +680,58 @@ def test_split_k_tail(cuda_device, case):
         assert (y1.float() - y0.float()).abs().max().item() <= tol * y0.float().abs().max().item(), tile
         assert torch.allclose(p1, p0, rtol=1e-4, atol=1e-3), tile
         assert torch.equal(y1, y2), tile                       # counters back at zero, fixed order
+
+
+A3_192_CASES = [
+    # (n, h, w, cin, cout, k, stride, pad, dil)
+    (8, 60, 80, 256, 256, 3, 1, 2, 2),      # the B=8 shard's layer3: 200 192-row tiles, one round
+    (3, 37, 41, 128, 512, 3, 1, 1, 1),      # ragged M (4551 rows: a partial last tile and half tile)
+    (2, 30, 40, 512, 256, 1, 1, 0, 1),      # 1x1, 2400 rows
+    (1, 9, 11, 256, 256, 3, 2, 1, 1),       # stride 2, one partial tile (30 rows)
+]
+
+
+@pytest.mark.parametrize("case", A3_192_CASES)
+def test_a3_192_tiles(cuda_device, case):
+    """HKP_TILE_192_A3 (conv_x3_a3_192_kernel: the A3 body on 192 x 256 tiles): every
+    output is the 256-row A3 body's, bit for bit (the same MFMA sequence per output
+    element), for f16x3 and both two-product sets; its BN partials come per 96-row
+    tile (ceil(M / 96) of them) and finalize to the 128-row tiles' statistics; the
+    stride-1 dgrad (with the residual addend) likewise."""
+    from hkp import ops
+    from hkp._lib import HKP_KOP_FWD_X3, HKP_TILE_192_A3, HKP_TILE_256_A3, HKP_X3_W16, HKP_X3_X16, ConvDesc
+    n, h, w, cin, cout, k, st, pad, dil = case
+    d = cuda_device
+    g = torch.Generator(device=d).manual_seed(31)
+    x = torch.relu(torch.randn(n, h, w, cin, device=d, generator=g))
+    wt = torch.randn(cout, k, k, cin, device=d, generator=g) * (2.0 / (k * k * cout)) ** 0.5
+    ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
+    xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
+    wp = ops.weight_pack_x3(wt)
+    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, HKP_TILE_192_A3)
+    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_a3_192_kernel<3>"
+    # the 256-row reference without the split-K tail (its segment sums reorder the K loop)
+    y0, p0 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256_A3)
+    y1, p1 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_192_A3)
+    m = y0.numel() // cout
+    assert p1.shape == ((m + 95) // 96, cout, 2) and ops.stat_tile_rows(p1) == 96
+    assert torch.equal(y1, y0)
+    assert torch.allclose(_bn_stats(p1, m), _bn_stats(p0, m), rtol=1e-6, atol=1e-7)
+    for prod in (HKP_X3_W16, HKP_X3_X16):
+        a, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256_A3, products=prod)
+        b, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_192_A3, products=prod)
+        assert torch.equal(a, b), prod
+    if st == 1:
+        gy = torch.randn(n, h, w, cout, device=d, generator=g) * 1e-3
+        add = torch.randn(n, h, w, cin, device=d, generator=g) * 1e-3
+        amax = ops.absmax(gy)
+        dys = ops.split_pack_x3(gy, amax)
+        wf = ops.weight_flip_pack_x3(wt)
+        if cin % 256 == 0:
+            dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, sk=False,
+                                         tile=HKP_TILE_256_A3)
+            dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=HKP_TILE_192_A3)
+            assert torch.equal(dx1, dx0)
 
 
 def test_split_k_tail_dgrad_back_to_back(cuda_device):

@@ -9,6 +9,8 @@
 #   prec      per-stage precision plans at C4 (Policy.stage_precision): tests + study table
 #   plan      the measured tile plan (tools/tile_sweep.py) and its A/B against the C planner
 #   prof      the final tree's traces (C2 + PMC, B=8, C4, C3 train) and bench lines
+#   pmc       PMC passes of the final tree for C4 and C3 training
+#   a192      the 192-row A3 tiles: tests and per-conv timing on the B=8 shapes
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -66,7 +68,8 @@ plan)
     timeout -k 10 400 python -u tools/infer_ab.py "" "tile_plan=0" --batch 8 --rounds 7 --iters 20 > $O/ab_b8.log 2>&1
     timeout -k 10 400 python -u tools/infer_ab.py "" "tile_plan=0" --rounds 7 --iters 10 > $O/ab_c2.log 2>&1
     timeout -k 10 500 python -u tools/infer_ab.py "" "tile_plan=0" $C4 --rounds 5 --iters 5 > $O/ab_c4.log 2>&1
-    timeout -k 10 500 python -u tools/train_ab.py "" "tile_plan=0" --rounds 5 --iters 10 > $O/ab_train.log 2>&1
+    timeout -k 10 500 python -u tools/train_ab.py "" "tile_plan=0" "dgrad_overlap_tile=15" --rounds 5 --iters 10 \
+        > $O/ab_train.log 2>&1
     ;;
 prof)
     # the final tree's traces and C2 PMC passes (copied into profiles/ on the box so
@@ -89,6 +92,23 @@ prof)
     timeout -k 10 300 python -u bench.py --batch 8 --no-cpu-baseline --no-extras > $O/bench_b8.log 2>&1
     timeout -k 10 300 python -u bench.py $C4 --no-cpu-baseline --no-extras > $O/bench_c4.log 2>&1
     timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline --no-extras > $O/bench_train.log 2>&1
+    ;;
+pmc)
+    # PMC passes of the final tree for C4 and the C3 training shard (the C2 passes are
+    # in "prof"); kernel traces from "prof" pair with them in the HBM tables
+    bash tools/pmc_passes.sh $O/pmc_c4 "$C4 --steps 2 --warmup 1 --no-extras" "." > $O/pmc_c4.log 2>&1
+    echo "c4 ok"
+    bash tools/pmc_passes.sh $O/pmc_train "--mode train --steps 2 --warmup 1 --no-extras" "." > $O/pmc_train.log 2>&1
+    echo "train ok"
+    ;;
+a192)
+    # the 192-row A3 tiles (HKP_TILE_192_A3): their parity tests, the precision suite
+    # around them, then per-conv timing on the B=8 shard's shapes against A3 / the planner
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_precision.py \
+        > $O/pytest_prec.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_prec.log)"
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,15 --rounds 7 --iters 20 \
+        --shapes t3,t3a,t4,t4ds,t3ds > $O/conv_ab.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
