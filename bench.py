@@ -457,7 +457,7 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
     # dominant kernel = the conv symbol with the most event-timed time
     dom_sym, (cnt, fl, nb, ms) = max(agg.items(), key=lambda kv: kv[1][3])
     alg = (fl / cnt) / ((ms / cnt) * 1e-3) / 1e12          # algorithmic (fp32-equivalent) TFLOP/s
-    if dom_sym.startswith(("conv_x3_kernel", "conv_x3_a3_kernel", "conv_x3_halo_kernel", "wgrad_x3_kernel")):
+    if dom_sym.startswith(("conv_x3_kernel", "conv_x3_a3_", "conv_x3_halo_kernel", "wgrad_x3_kernel")):
         # the x3 LDS-DMA kernels: fp16 MFMAs per fp32 MAC — 3 (f16x3), 2 (f16x2w / f16x2a: two of
         # the three products), 1 (f16)
         passes = {"f16x3": 3, "f16x2w": 2, "f16x2a": 2}.get(precision, 1)

@@ -255,8 +255,12 @@ constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
 // B (the weights, L2-resident) 2 stages: 5 x 32 KiB = the whole 160 KiB; the
 // epilogue's scratch and column scales reuse the drained ring.
 constexpr int X3_A3_LDS = 5 * 256 * 128;
-// ... with BM-row A stages (A3_192: 192-row tiles, 136 KiB)
-constexpr int x3_a3_lds(int BM) { return 3 * BM * 128 + 2 * 256 * 128; }
+// ... with BM-row A stages (A3_192: 192-row tiles, 136 KiB; A3_160: 125 KiB, with a
+// 1 KiB sink for the A DMA pieces past row 160 — 20 pieces over 8 waves, 3 each)
+constexpr int x3_a3_lds(int BM) { return 3 * BM * 128 + 2 * 256 * 128 + (BM % 64 ? 1024 : 0); }
+// waves in M of a BM-row tile (8 waves): 4 (64- / 48-row wave tiles), 2 for 160 rows
+// (40-row wave tiles do not split into 16-row MFMA tiles; 80 x 64 instead)
+constexpr int x3_wm(int BM) { return BM == 160 ? 2 : 4; }
 
 // BN-partials scratch (x3_bn_partials_w: [2][WM][BN] floats) past the ring, so
 // the epilogue needs no barrier before it, then the tile's BN column scales
@@ -467,6 +471,8 @@ __device__ __forceinline__ void x3_bn_partials(const X3Args& a, char* smem, int 
 // Same quantities as x3_bn_partials (sum, M2 about the half-tile mean).
 // A wave covers 16 * NI rows (WM = 4 waves: NI = 4 for the 256-row tiles, 3 for the
 // 192-row A3 tiles), so a partial tile (a half tile) holds 32 * NI rows: 128 / 96.
+// WMP = 2 (the 160-row A3 tiles, NI = 5): a wave's 80 rows are a whole partial tile,
+// written from its lanes after the shuffle merge (no LDS, no WIDE form).
 // VEC(i, j): the f32x4 of accumulator rows ROW(i, 0..3) of column block j.
 // SC(j): the column's output scale (a power of two: sums scale by it, M2 by its
 // square, exactly) when VEC is the unscaled accumulator.
@@ -484,12 +490,12 @@ __device__ __forceinline__ void x3_chan_merge(float& s, float& q, float s2, floa
     q = (q + q2) + d * d * f;
 }
 
-template <int BN, int NI, int NJ, int CW, int SHF, typename Vec, typename Row, typename Sc>
+template <int BN, int NI, int NJ, int CW, int SHF, int WMP = 4, typename Vec, typename Row, typename Sc>
 __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, int m0, int n0, int wm, int wn,
                                                  int lane, Vec&& vec, Row&& row, Sc&& sc_of,
                                                  float* wide = nullptr) {
     constexpr int WROWS = 16 * NI;                                   // rows per wave
-    if constexpr (CW == 16 && SHF == 16 && (NI == 4 || NI == 3)) {
+    if constexpr (CW == 16 && SHF == 16 && WMP == 4 && (NI == 4 || NI == 3)) {
         if (wide != nullptr && m0 + 4 * WROWS <= a.M) {              // block-uniform
             const int q = lane >> 4, r16 = lane & 15;
             constexpr float inv = 1.f / (NI * 4);
@@ -612,6 +618,18 @@ __device__ __forceinline__ void x3_bn_partials_w(const X3Args& a, float* red, in
             lq[j] = (lq[j] + qb) + d * d * f;
         }
         ln = nt;
+    }
+    if constexpr (WMP == 2) {              // 2 waves in M (160-row tiles): a wave IS a partial tile
+        if (nw == 0 || lane >= CW) return;
+        const long pt = (long)(m0 / WROWS) + wm;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int c = wn * NJ * CW + j * CW + lane;
+            const float sc = sc_of(j);
+            a.part[(pt * a.K + n0 + c) * 2 + 0] = ls[j] * sc;
+            a.part[(pt * a.K + n0 + c) * 2 + 1] = lq[j] * (sc * sc);
+        }
+        return;
     }
     if (lane < CW) {
 #pragma unroll
@@ -762,10 +780,11 @@ template <int BN, int NST, int STAGE, int GL, int P, bool A3, int GA, int BM, ty
 __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial,
                                                   int m0, int n0, int wm, int wn, int lane, int tid,
                                                   Issue& issue_next, IssueA& issue_a, IssueB& issue_b) {
-    constexpr int WM = 4, WN = 2, ROW = 128;
+    constexpr int WM = x3_wm(BM), WN = 8 / WM, ROW = 128;
     constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);
     constexpr int NMC = x3_nprod(P) * UM;           // MFMAs per column block per K-step
-    static_assert(BM == 256 || (A3 && BM == 192 && P != 1), "192-row tiles: the A3 body, packed operands");
+    static_assert(BM == 256 || (A3 && (BM == 192 || BM == 160) && P != 1),
+                  "192- / 160-row tiles: the A3 body, packed operands");
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
     static_assert(!A3 || (BN == 256 && NST == 2), "A3: the 256x256 body");
     // PAIRB and A3 have no LDS past the ring: the epilogue's scratch is the drained
@@ -1000,10 +1019,12 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no DMA in flight into the ring past here
     x3_stamp(a, 2);
 
-    if (partial) {                         // stream-K: fold the tile's segments
-        auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
-        auto set = [&](int v, f32x4 y) { acc[v / UN][v % UN] = y; };
-        if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return;
+    if constexpr (BM == 256) {             // (the 192- / 160-row grids run whole tiles)
+        if (partial) {                     // stream-K: fold the tile's segments
+            auto get = [&](int v) -> f32x4 { return acc[v / UN][v % UN]; };
+            auto set = [&](int v, f32x4 y) { acc[v / UN][v % UN] = y; };
+            if (!sk_combine<UM * UN>(a, tile, tid, smem, get, set)) return;
+        }
     }
     const int rbase = m0 + wm * UM * 16 + 4 * q;
     // column scale (weight scale x gradient scale): the prefetched LDS copy, or
@@ -1018,7 +1039,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
         if (a.part) {
             if constexpr (RINGSCR) lds_sync();         // the scratch is the ring
-            x3_bn_partials_w<BN, UM, UN, 16, 16>(
+            x3_bn_partials_w<BN, UM, UN, 16, 16, WM>(
                 a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
                 [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
         }
@@ -1053,7 +1074,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     for (int j = 0; j < UN; ++j) sc[j] = col_scale(wn * UN * 16 + j * 16 + r16);
     if (a.part) {
         if constexpr (RINGSCR) lds_sync();             // the scratch is the ring
-        x3_bn_partials_w<BN, UM, UN, 16, 16>(
+        x3_bn_partials_w<BN, UM, UN, 16, 16, WM>(
             a, (float*)(smem + RED_OFF), m0, n0, wm, wn, lane, [&](int i, int j) { return acc[i][j]; },
             [&](int i, int r) { return rbase + i * 16 + r; }, [&](int j) { return sc[j]; }, (float*)smem);
     }
@@ -1074,7 +1095,7 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
         lds_sync();                                    // every wave done with the ring and the partials' scratch
 #pragma unroll
         for (int h = 0; h < PASSES; ++h) {
-            if (PASSES == 1 || (wm >> 1) == h) {
+            if (PASSES == 1 || (wm * UM * 16) / RPP == h) {          // the pass holding this wave's rows
 #pragma unroll
                 for (int i = 0; i < UM; ++i)
 #pragma unroll
@@ -1131,14 +1152,15 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
 // packed split with two of its three products, 1 plain fp16.
 template <int BN, bool STEM, bool PAIR, int MFD, int P, bool A3 = false, int BM = 256>
 __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int tile, int ks, int nks, bool partial) {
-    constexpr int WM = 4, WN = 2;
+    constexpr int WM = x3_wm(BM), WN = 8 / WM;
     constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
     constexpr int ROW = 128;                       // bytes per LDS row (one packed line)
     constexpr int CPR = ROW / 16;                  // 16-B chunks per row
     constexpr int RPI = 1024 / ROW;                // rows per DMA wave-instruction
     constexpr int NST = x3_nst(BN, PAIR);          // LDS ring depth
     constexpr int STAGE = (BM + BN) * ROW;
-    constexpr int GA = BM / RPI / 8;               // A DMA instructions per wave per stage
+    constexpr int GA = (BM / RPI + 7) / 8;         // A DMA instructions per wave per stage (rounded up)
+    constexpr bool A_SINK = BM / RPI % 8 != 0;    // pieces past row BM load the zero line into a sink
     constexpr int GBT = BN / RPI;                  // B DMA instructions per stage (all waves)
     constexpr int GB = GBT >= 8 ? GBT / 8 : 1;     // per wave (GBT < 8: waves duplicate, same bytes)
     constexpr int GL = GA + GB;                    // DMA instructions per wave per stage
@@ -1147,7 +1169,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
     static_assert(!A3 || (BN == 256 && !STEM && !PAIR && MFD == 16), "A3: the 256x256 16x16x32 body");
-    static_assert(BM == 256 || (A3 && BM == 192 && x3_packed(P)), "192-row tiles: A3, packed operands");
+    static_assert(BM == 256 || (A3 && (BM == 192 || BM == 160) && x3_packed(P)), "192- / 160-row tiles: A3, packed");
+    static_assert(!A_SINK || A3, "the A sink is the A3 body's");
 
     const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
     const int m0 = (mt + a.mt0) * BM, n0 = nt * BN;
@@ -1189,7 +1212,7 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
 #endif
         int hb = -16384, wb = -16384;
         long off = 0;
-        if (m < a.M) {
+        if (m < a.M && (!A_SINK || RPI * (w * GA + i) < BM)) {
             const int hw = a.Ho * a.Wo;
             const int n = m / hw, rem = m - n * hw;
             const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
@@ -1257,7 +1280,10 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
             for (int i = 0; i < GA; ++i) {
                 const int hb = a_org[i] >> 16, wb = (int)(short)(a_org[i] & 0xFFFF);
                 const bool in = (unsigned)(hb + dh) < (unsigned)a.H && (unsigned)(wb + dw) < (unsigned)a.W;
-                glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, st + (RPI * (w * GA + i)) * ROW);
+                const int prow = RPI * (w * GA + i);
+                char* dst = st + prow * ROW;
+                if constexpr (A_SINK) dst = prow < BM ? dst : smem + (3 * BM + 2 * BN) * ROW;   // wave-uniform
+                glds16(in ? xbase + ((unsigned long)a_off[i] + toff) : zero, dst);
             }
         }
         qa_buf = qa_buf == 2 ? 0 : qa_buf + 1;
@@ -1548,6 +1574,16 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3_192_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[x3_a3_lds(192)];
     x3_stamp(a, 0);
     conv_x3_tile<256, false, false, 16, P, true, 192>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
+}
+
+// ... on 160 x 256 tiles (HKP_TILE_160_A3): 240 m-tiles for the B=8 shard's layer3,
+// 0.94 of the CUs, each 5/8 of a 256-row tile.  Waves 2 x 4 (80 x 64 each, 80
+// accumulators); a wave's rows are one 80-row BN partial tile.
+template <int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_a3_160_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_a3_lds(160)];
+    x3_stamp(a, 0);
+    conv_x3_tile<256, false, false, 16, P, true, 160>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -3189,7 +3225,7 @@ struct X3Choice {
     bool halo = false;                 // conv_x3_halo_kernel<P>
     bool a3 = false;                   // conv_x3_a3_kernel<P> (256x256, 3-stage A ring)
     bool duo = false;                  // conv_x3_duo_kernel<1> (256x128, two 4-wave blocks per CU)
-    int bm = 256;                      // rows per tile (192: conv_x3_a3_192_kernel<P>)
+    int bm = 256;                      // rows per tile (192 / 160: conv_x3_a3_192 / _160_kernel<P>)
 };
 // halo: 0 the halo-tile body cannot take the shape, 1 it can (HKP_TILE_HALO
 // forces it), 2 it is also the default (64 input channels: measured faster;
@@ -3216,7 +3252,8 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
     // 128-channel output, which A3 cannot take: plan it as AUTO (the rules below)
     if (policy == HKP_TILE_256_A3 && P == 3 && k % 256 != 0 && g_x3_pair128) policy = HKP_TILE_AUTO;
     // 192-row A3 tiles: packed operands with 256-divisible outputs; AUTO otherwise
-    if (policy == HKP_TILE_192_A3 && (!x3_packed(P) || k % 256 != 0)) policy = HKP_TILE_AUTO;
+    if ((policy == HKP_TILE_192_A3 || policy == HKP_TILE_160_A3) && (!x3_packed(P) || k % 256 != 0))
+        policy = HKP_TILE_AUTO;
     if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
     X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
     if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
@@ -3255,7 +3292,7 @@ static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int pol
     // the halo-tile body wherever the shape allows it, unless a tile body is forced
     if ((halo >= 1 && policy == HKP_TILE_HALO) ||
         (halo == 2 && (policy == HKP_TILE_AUTO || policy == HKP_TILE_256_TAIL || policy == HKP_TILE_256_A3 ||
-                       policy == HKP_TILE_192_A3))) {
+                       policy == HKP_TILE_192_A3 || policy == HKP_TILE_160_A3))) {
         X3Choice c{64, 16, true, false};
         c.halo = true;
         return c;
@@ -3278,10 +3315,11 @@ static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int pol
         case HKP_TILE_256_A3:              // the same on the A3 body
             if (k % 256 == 0) return {256, 16, false, false, false, true};
             break;
-        case HKP_TILE_192_A3:              // 192x256 tiles on the A3 body (x3_choose checked the operands)
+        case HKP_TILE_192_A3:              // 192x256 / 160x256 tiles on the A3 body (x3_choose
+        case HKP_TILE_160_A3:              // checked the operands)
             if (k % 256 == 0) {
                 X3Choice c{256, 16, false, false, false, true};
-                c.bm = 192;
+                c.bm = policy == HKP_TILE_192_A3 ? 192 : 160;
                 return c;
             }
             break;
@@ -3301,7 +3339,9 @@ static const X3Choice X3_STEM{64, 16, true, false};
 static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int len) {
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
     if (c.duo) return snprintf(buf, len, "conv_x3_duo_kernel<%d>", P);
-    if (c.a3) return snprintf(buf, len, c.bm == 192 ? "conv_x3_a3_192_kernel<%d>" : "conv_x3_a3_kernel<%d>", P);
+    if (c.a3)
+        return snprintf(buf, len, c.bm == 192 ? "conv_x3_a3_192_kernel<%d>"
+                                  : c.bm == 160 ? "conv_x3_a3_160_kernel<%d>" : "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
@@ -3400,12 +3440,14 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         }
         return;
     }
-    if (c.bm == 192) {                     // one tile per block, no split-K tail
-        const long mt = ((long)a.M + 191) / 192;
-        const dim3 g192((unsigned)(mt * a.n_tiles));
+    if (c.bm != 256) {                     // one tile per block, no split-K tail
+        const long mt = ((long)a.M + c.bm - 1) / c.bm;
+        const dim3 gm((unsigned)(mt * a.n_tiles));
         x3_dispatch_p(P, [&](auto pc) {
-            if constexpr (x3_packed(pc.value))
-                hipLaunchKernelGGL(conv_x3_a3_192_kernel<pc.value>, g192, dim3(512), 0, st, a);
+            if constexpr (x3_packed(pc.value)) {
+                if (c.bm == 192) hipLaunchKernelGGL(conv_x3_a3_192_kernel<pc.value>, gm, dim3(512), 0, st, a);
+                else hipLaunchKernelGGL(conv_x3_a3_160_kernel<pc.value>, gm, dim3(512), 0, st, a);
+            }
         });
         return;
     }
@@ -3499,7 +3541,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_192_A3, "%s: unknown tile policy %d", who,
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_160_A3, "%s: unknown tile policy %d", who,
                   d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8 && d->tile != HKP_TILE_RESERVED_14,
                   "%s: tile policy %d is retired (a persistent conv body, measured slower)", who, d->tile);
@@ -3919,7 +3961,8 @@ extern "C" int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* 
 extern "C" int32_t hkp_conv_x3_stat_tile_rows(const hkp_conv_desc* d, int32_t op) {
     HKP_CHECK_ARG(d, "hkp_conv_x3_stat_tile_rows: null descriptor");
     const bool packed = op == HKP_KOP_FWD_X3 || op == HKP_KOP_FWD_X3_W16 || op == HKP_KOP_FWD_X3_X16;
-    return packed && d->tile == HKP_TILE_192_A3 && d->k % 256 == 0 ? 96 : 128;
+    if (!packed || d->k % 256 != 0) return 128;
+    return d->tile == HKP_TILE_192_A3 ? 96 : d->tile == HKP_TILE_160_A3 ? 80 : 128;
 }
 
 // the kernel symbol a launch with this descriptor runs (see hulkkp.h)

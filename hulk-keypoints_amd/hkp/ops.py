@@ -10,7 +10,7 @@ import torch
 
 from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
                    HKP_KOP_STEM_X3, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
-                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, HKP_TILE_192_A3, ConvDesc, HkpError, call)
+                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, HKP_TILE_160_A3, HKP_TILE_192_A3, ConvDesc, HkpError, call)
 
 CONV_TILE_ROWS = 128  # BM of conv_fwd.hip (rows per BN statistic tile)
 
@@ -210,7 +210,7 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     part = None
     if stats:
         rows = CONV_TILE_ROWS
-        if tile == HKP_TILE_192_A3:            # 96-row statistic tiles (the library says)
+        if tile in (HKP_TILE_192_A3, HKP_TILE_160_A3):      # 96- / 80-row statistic tiles (the library says)
             from ._lib import lib
             rows = lib().hkp_conv_x3_stat_tile_rows(ctypes.byref(d), kop)
         part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out", rows)

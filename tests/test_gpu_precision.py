@@ -8,7 +8,7 @@ import torch.nn.functional as F
 from oracle import cpu_ref, recipe
 
 # every live HKP_TILE_* policy past AUTO (7, 8 and 14 are retired)
-LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11, 13, 15)
+LIVE_TILES = (1, 2, 3, 4, 5, 6, 9, 10, 11, 13, 15, 16)
 
 pytestmark = pytest.mark.gpu
 
@@ -691,15 +691,19 @@ A3_192_CASES = [
 ]
 
 
+@pytest.mark.parametrize("bm", [192, 160])
 @pytest.mark.parametrize("case", A3_192_CASES)
-def test_a3_192_tiles(cuda_device, case):
-    """HKP_TILE_192_A3 (conv_x3_a3_192_kernel: the A3 body on 192 x 256 tiles): every
-    output is the 256-row A3 body's, bit for bit (the same MFMA sequence per output
-    element), for f16x3 and both two-product sets; its BN partials come per 96-row
-    tile (ceil(M / 96) of them) and finalize to the 128-row tiles' statistics; the
-    stride-1 dgrad (with the residual addend) likewise."""
+def test_a3_192_tiles(cuda_device, case, bm):
+    """HKP_TILE_192_A3 / HKP_TILE_160_A3 (conv_x3_a3_192 / _160_kernel: the A3 body on
+    192 x 256 / 160 x 256 tiles): every output is the 256-row A3 body's, bit for bit
+    (the same MFMA sequence per output element), for f16x3 and both two-product
+    sets; the BN partials come per 96- / 80-row tile (ceil(M / rows) of them) and
+    finalize to the 128-row tiles' statistics; the stride-1 dgrad (with the
+    residual addend) likewise."""
     from hkp import ops
-    from hkp._lib import HKP_KOP_FWD_X3, HKP_TILE_192_A3, HKP_TILE_256_A3, HKP_X3_W16, HKP_X3_X16, ConvDesc
+    from hkp._lib import (HKP_KOP_FWD_X3, HKP_TILE_160_A3, HKP_TILE_192_A3, HKP_TILE_256_A3, HKP_X3_W16,
+                          HKP_X3_X16, ConvDesc)
+    tile, rows = (HKP_TILE_192_A3, 96) if bm == 192 else (HKP_TILE_160_A3, 80)
     n, h, w, cin, cout, k, st, pad, dil = case
     d = cuda_device
     g = torch.Generator(device=d).manual_seed(31)
@@ -708,18 +712,18 @@ def test_a3_192_tiles(cuda_device, case):
     ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
     xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
     wp = ops.weight_pack_x3(wt)
-    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, HKP_TILE_192_A3)
-    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_a3_192_kernel<3>"
+    desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, tile)
+    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_a3_%d_kernel<3>" % bm
     # the 256-row reference without the split-K tail (its segment sums reorder the K loop)
     y0, p0 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256_A3)
-    y1, p1 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_192_A3)
+    y1, p1 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
     m = y0.numel() // cout
-    assert p1.shape == ((m + 95) // 96, cout, 2) and ops.stat_tile_rows(p1) == 96
+    assert p1.shape == ((m + rows - 1) // rows, cout, 2) and ops.stat_tile_rows(p1) == rows
     assert torch.equal(y1, y0)
     assert torch.allclose(_bn_stats(p1, m), _bn_stats(p0, m), rtol=1e-6, atol=1e-7)
     for prod in (HKP_X3_W16, HKP_X3_X16):
         a, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256_A3, products=prod)
-        b, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=HKP_TILE_192_A3, products=prod)
+        b, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile, products=prod)
         assert torch.equal(a, b), prod
     if st == 1:
         gy = torch.randn(n, h, w, cout, device=d, generator=g) * 1e-3
@@ -730,7 +734,7 @@ def test_a3_192_tiles(cuda_device, case):
         if cin % 256 == 0:
             dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, sk=False,
                                          tile=HKP_TILE_256_A3)
-            dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=HKP_TILE_192_A3)
+            dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=tile)
             assert torch.equal(dx1, dx0)
 
 

@@ -35,6 +35,27 @@ def test_plan_is_the_measured_argmin():
         assert ent["tile"] == want, (key, ent)
 
 
+def test_plan_keeps_the_planners_distinct_kernels():
+    """A planned policy launches another kernel than the planner's (a policy a shape
+    does not take plans as AUTO), and shapes the planner puts on the halo body stay
+    there: the fused-input-BN conv runs exactly where the unfused one runs it."""
+    import ctypes  # noqa: F401
+    import sys
+    sys.path.insert(0, PKG)
+    from hkp import ops
+    from hkp._lib import HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, ConvDesc
+    doc = _doc()
+    for key, ent in doc["shapes"].items():
+        kind, n, h, w, cin, cout, k, st, pd, dl = key.split("|")
+        if kind == "f16bn" or ent["tile"] == 0:
+            continue
+        kop = HKP_KOP_FWD_X3 if kind == "x3" else HKP_KOP_FWD_F16
+        args = [int(v) for v in (n, h, w, cin, cout, k, k, st, pd, dl)] + [0]
+        planner = ops.kernel_name(ConvDesc(*args, 0), kop)
+        planned = ops.kernel_name(ConvDesc(*args, ent["tile"]), kop)
+        assert planned != planner and not planner.startswith("conv_x3_halo"), (key, planner, planned)
+
+
 def test_plan_covers_the_workloads():
     doc = _doc()
     seen = set()

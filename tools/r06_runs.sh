@@ -107,7 +107,7 @@ a192)
     timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_precision.py \
         > $O/pytest_prec.log 2>&1
     echo "pytest: $(tail -1 $O/pytest_prec.log)"
-    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,15 --rounds 7 --iters 20 \
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,15,16 --rounds 7 --iters 20 \
         --shapes t3,t3a,t4,t4ds,t3ds > $O/conv_ab.log 2>&1
     ;;
 check)
