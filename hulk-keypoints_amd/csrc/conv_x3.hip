@@ -257,7 +257,7 @@ constexpr int x3_lds_bytes(int BN, bool PAIR, int P) {
 constexpr int X3_A3_LDS = 5 * 256 * 128;
 // ... with BM-row A stages (A3_192: 192-row tiles, 136 KiB; A3_160: 125 KiB, with a
 // 1 KiB sink for the A DMA pieces past row 160 — 20 pieces over 8 waves, 3 each)
-constexpr int x3_a3_lds(int BM) { return 3 * BM * 128 + 2 * 256 * 128 + (BM % 64 ? 1024 : 0); }
+constexpr int x3_a3_lds(int BM, int BN = 256) { return 3 * BM * 128 + 2 * BN * 128 + (BM % 64 ? 1024 : 0); }
 // waves in M of a BM-row tile (8 waves): 4 (64- / 48-row wave tiles), 2 for 160 rows
 // (40-row wave tiles do not split into 16-row MFMA tiles; 80 x 64 instead)
 constexpr int x3_wm(int BM) { return BM == 160 ? 2 : 4; }
@@ -786,12 +786,12 @@ __device__ __forceinline__ void conv_x3_mf16_body(const X3Args& a, char* smem, i
     static_assert(BM == 256 || (A3 && (BM == 192 || BM == 160) && P != 1),
                   "192- / 160-row tiles: the A3 body, packed operands");
     constexpr bool PAIRB = BN == 64 && NST == 2;    // the 256x64 two-blocks-per-CU tiles
-    static_assert(!A3 || (BN == 256 && NST == 2), "A3: the 256x256 body");
+    static_assert(!A3 || (BN == 256 && NST == 2) || (BN == 128 && BM == 160), "A3: 256-wide tiles (128: 160 rows)");
     // PAIRB and A3 have no LDS past the ring: the epilogue's scratch is the drained
     // ring and the column scales are loaded in the epilogue
     constexpr bool RINGSCR = PAIRB || A3;
     constexpr int RED_OFF = RINGSCR ? 0 : x3_lds_bytes(BN, PAIRB, P);
-    constexpr int LDS_ALL = A3 ? x3_a3_lds(BM) : x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB);
+    constexpr int LDS_ALL = A3 ? x3_a3_lds(BM, BN) : x3_lds_bytes(BN, PAIRB, P) + x3_red_bytes(BN, PAIRB);
     float* const scl = (float*)(smem + RED_OFF + 2 * 4 * BN * 4);   // [BN] column scales (!RINGSCR)
     float sclv = 1.f;                              // issued before the fill, stored after it
     if constexpr (!RINGSCR) {
@@ -1168,7 +1168,8 @@ __device__ __forceinline__ void conv_x3_tile(const X3Args& a, char* smem, int ti
     static_assert(P == 3 || ((P == 1 || P == 2 || P == 4) && !STEM), "bad conv_x3 operand layout");
     static_assert(!(MFD == 32 && BN == 256), "256x256 tiles run the 16x16x32 body");
     static_assert(NST * STAGE <= 160 * 1024, "LDS");
-    static_assert(!A3 || (BN == 256 && !STEM && !PAIR && MFD == 16), "A3: the 256x256 16x16x32 body");
+    static_assert(!A3 || ((BN == 256 || (BN == 128 && BM == 160)) && !STEM && !PAIR && MFD == 16),
+                  "A3: the 16x16x32 body on 256-wide tiles (128-wide: 160 rows)");
     static_assert(BM == 256 || (A3 && (BM == 192 || BM == 160) && x3_packed(P)), "192- / 160-row tiles: A3, packed");
     static_assert(!A_SINK || A3, "the A sink is the A3 body's");
 
@@ -1584,6 +1585,16 @@ __global__ __launch_bounds__(512, 1) void conv_x3_a3_160_kernel(X3Args a) {
     __shared__ __attribute__((aligned(1024))) char smem[x3_a3_lds(160)];
     x3_stamp(a, 0);
     conv_x3_tile<256, false, false, 16, P, true, 160>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
+}
+
+// ... on 160 x 128 tiles (HKP_TILE_160_A3 with Cout % 256 != 0, Cout % 128 == 0): the
+// B=8 shard's layer2 (128 channels: 150 256x128 tiles -> 240 160x128); waves 2 x 4
+// of 80 x 32, a 2-stage ring of 128 weight rows
+template <int P>
+__global__ __launch_bounds__(512, 1) void conv_x3_a3_160x128_kernel(X3Args a) {
+    __shared__ __attribute__((aligned(1024))) char smem[x3_a3_lds(160, 128)];
+    x3_stamp(a, 0);
+    conv_x3_tile<128, false, false, 16, P, true, 160>(a, smem, xcd_remap(blockIdx.x, gridDim.x), 0, a.nks, false);
 }
 
 // Split-K tail: the m-tiles of the last, partly filled round of a one-tile grid,
@@ -3252,8 +3263,8 @@ static X3Choice x3_choose(int k, long m_tiles, int nks, bool sk_ok, int policy, 
     // 128-channel output, which A3 cannot take: plan it as AUTO (the rules below)
     if (policy == HKP_TILE_256_A3 && P == 3 && k % 256 != 0 && g_x3_pair128) policy = HKP_TILE_AUTO;
     // 192-row A3 tiles: packed operands with 256-divisible outputs; AUTO otherwise
-    if ((policy == HKP_TILE_192_A3 || policy == HKP_TILE_160_A3) && (!x3_packed(P) || k % 256 != 0))
-        policy = HKP_TILE_AUTO;
+    if (policy == HKP_TILE_192_A3 && (!x3_packed(P) || k % 256 != 0)) policy = HKP_TILE_AUTO;
+    if (policy == HKP_TILE_160_A3 && (!x3_packed(P) || k % 128 != 0)) policy = HKP_TILE_AUTO;
     if (policy != HKP_TILE_AUTO_A3 && policy != HKP_TILE_AUTO) return x3_choose_base(k, m_tiles, nks, sk_ok, policy, halo);
     X3Choice c = x3_choose_base(k, m_tiles, nks, sk_ok, HKP_TILE_AUTO, halo);
     if (c.bn == 256 && !c.sk && !c.halo && !c.pair) c.a3 = true;
@@ -3315,10 +3326,10 @@ static X3Choice x3_choose_base(int k, long m_tiles, int nks, bool sk_ok, int pol
         case HKP_TILE_256_A3:              // the same on the A3 body
             if (k % 256 == 0) return {256, 16, false, false, false, true};
             break;
-        case HKP_TILE_192_A3:              // 192x256 / 160x256 tiles on the A3 body (x3_choose
-        case HKP_TILE_160_A3:              // checked the operands)
-            if (k % 256 == 0) {
-                X3Choice c{256, 16, false, false, false, true};
+        case HKP_TILE_192_A3:              // 192x256 / 160x256 (160x128) tiles on the A3 body
+        case HKP_TILE_160_A3:              // (x3_choose checked the operands)
+            if (k % 256 == 0 || (policy == HKP_TILE_160_A3 && k % 128 == 0)) {
+                X3Choice c{k % 256 == 0 ? 256 : 128, 16, false, false, false, true};
                 c.bm = policy == HKP_TILE_192_A3 ? 192 : 160;
                 return c;
             }
@@ -3340,8 +3351,10 @@ static int x3_kernel_name(const X3Choice& c, bool stem, int P, char* buf, int le
     if (c.halo) return snprintf(buf, len, "conv_x3_halo_kernel<%d>", P);
     if (c.duo) return snprintf(buf, len, "conv_x3_duo_kernel<%d>", P);
     if (c.a3)
-        return snprintf(buf, len, c.bm == 192 ? "conv_x3_a3_192_kernel<%d>"
-                                  : c.bm == 160 ? "conv_x3_a3_160_kernel<%d>" : "conv_x3_a3_kernel<%d>", P);
+        return snprintf(buf, len, c.bm == 192                  ? "conv_x3_a3_192_kernel<%d>"
+                                  : c.bm == 160 && c.bn == 128 ? "conv_x3_a3_160x128_kernel<%d>"
+                                  : c.bm == 160                ? "conv_x3_a3_160_kernel<%d>"
+                                                               : "conv_x3_a3_kernel<%d>", P);
     return snprintf(buf, len, "conv_x3_kernel<%d, %s, %s, %d, %s, %d>", c.bn, stem ? "true" : "false",
                     c.pair ? "true" : "false", c.mfd, c.sk ? "true" : "false", P);
 }
@@ -3446,6 +3459,7 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
         x3_dispatch_p(P, [&](auto pc) {
             if constexpr (x3_packed(pc.value)) {
                 if (c.bm == 192) hipLaunchKernelGGL(conv_x3_a3_192_kernel<pc.value>, gm, dim3(512), 0, st, a);
+                else if (c.bn == 128) hipLaunchKernelGGL(conv_x3_a3_160x128_kernel<pc.value>, gm, dim3(512), 0, st, a);
                 else hipLaunchKernelGGL(conv_x3_a3_160_kernel<pc.value>, gm, dim3(512), 0, st, a);
             }
         });
@@ -3961,8 +3975,9 @@ extern "C" int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* 
 extern "C" int32_t hkp_conv_x3_stat_tile_rows(const hkp_conv_desc* d, int32_t op) {
     HKP_CHECK_ARG(d, "hkp_conv_x3_stat_tile_rows: null descriptor");
     const bool packed = op == HKP_KOP_FWD_X3 || op == HKP_KOP_FWD_X3_W16 || op == HKP_KOP_FWD_X3_X16;
-    if (!packed || d->k % 256 != 0) return 128;
-    return d->tile == HKP_TILE_192_A3 ? 96 : d->tile == HKP_TILE_160_A3 ? 80 : 128;
+    if (packed && d->tile == HKP_TILE_192_A3 && d->k % 256 == 0) return 96;
+    if (packed && d->tile == HKP_TILE_160_A3 && d->k % 128 == 0) return 80;
+    return 128;
 }
 
 // the kernel symbol a launch with this descriptor runs (see hulkkp.h)

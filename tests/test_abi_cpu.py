@@ -205,6 +205,9 @@ def test_kernel_name_query():
     narrow = _lib.ConvDesc(8, 60, 80, 256, 128, 3, 3, 1, 2, 2, 0, _lib.HKP_TILE_192_A3)
     assert "a3_192" not in ops.kernel_name(narrow, _lib.HKP_KOP_FWD_X3)
     assert rows(ctypes.byref(narrow), _lib.HKP_KOP_FWD_X3) == 128
+    narrow.tile = _lib.HKP_TILE_160_A3                                 # 128-wide: the 160x128 form
+    assert ops.kernel_name(narrow, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_160x128_kernel<3>"
+    assert rows(ctypes.byref(narrow), _lib.HKP_KOP_FWD_X3) == 80
     b8.tile = _lib.HKP_TILE_160_A3
     assert ops.kernel_name(b8, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_160_kernel<3>"
     assert rows(ctypes.byref(b8), _lib.HKP_KOP_FWD_X3) == 80

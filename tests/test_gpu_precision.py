@@ -688,6 +688,8 @@ A3_192_CASES = [
     (3, 37, 41, 128, 512, 3, 1, 1, 1),      # ragged M (4551 rows: a partial last tile and half tile)
     (2, 30, 40, 512, 256, 1, 1, 0, 1),      # 1x1, 2400 rows
     (1, 9, 11, 256, 256, 3, 2, 1, 1),       # stride 2, one partial tile (30 rows)
+    (8, 60, 80, 128, 128, 3, 1, 1, 1),      # the B=8 shard's layer2: 128-wide (160x128 tiles; 192: AUTO)
+    (3, 37, 41, 128, 128, 1, 1, 0, 1),      # 128-wide, ragged M
 ]
 
 
@@ -701,8 +703,8 @@ def test_a3_192_tiles(cuda_device, case, bm):
     finalize to the 128-row tiles' statistics; the stride-1 dgrad (with the
     residual addend) likewise."""
     from hkp import ops
-    from hkp._lib import (HKP_KOP_FWD_X3, HKP_TILE_160_A3, HKP_TILE_192_A3, HKP_TILE_256_A3, HKP_X3_W16,
-                          HKP_X3_X16, ConvDesc)
+    from hkp._lib import (HKP_KOP_FWD_X3, HKP_TILE_128_MF16, HKP_TILE_160_A3, HKP_TILE_192_A3, HKP_TILE_256_A3,
+                          HKP_X3_W16, HKP_X3_X16, ConvDesc)
     tile, rows = (HKP_TILE_192_A3, 96) if bm == 192 else (HKP_TILE_160_A3, 80)
     n, h, w, cin, cout, k, st, pad, dil = case
     d = cuda_device
@@ -712,17 +714,24 @@ def test_a3_192_tiles(cuda_device, case, bm):
     ss = torch.cat([torch.ones(cin, device=d), torch.zeros(cin, device=d)])
     xs = ops.bn_apply(x, ss, relu=False, split=3, keep_fp32=False)
     wp = ops.weight_pack_x3(wt)
+    if cout % 256:                       # 128-wide: the 160x128 form; 192 rows plan as AUTO
+        if bm == 192:
+            return
+        tile, ref = HKP_TILE_160_A3, HKP_TILE_128_MF16
+        name = "conv_x3_a3_160x128_kernel<3>"
+    else:
+        ref, name = HKP_TILE_256_A3, "conv_x3_a3_%d_kernel<3>" % bm
     desc = ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, tile)
-    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == "conv_x3_a3_%d_kernel<3>" % bm
+    assert ops.kernel_name(desc, HKP_KOP_FWD_X3) == name
     # the 256-row reference without the split-K tail (its segment sums reorder the K loop)
-    y0, p0 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256_A3)
+    y0, p0 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=ref)
     y1, p1 = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile)
     m = y0.numel() // cout
     assert p1.shape == ((m + rows - 1) // rows, cout, 2) and ops.stat_tile_rows(p1) == rows
     assert torch.equal(y1, y0)
     assert torch.allclose(_bn_stats(p1, m), _bn_stats(p0, m), rtol=1e-6, atol=1e-7)
     for prod in (HKP_X3_W16, HKP_X3_X16):
-        a, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=HKP_TILE_256_A3, products=prod)
+        a, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, sk=False, tile=ref, products=prod)
         b, _ = ops.conv2d_fwd_x3(xs, wp, st, pad, dil, tile=tile, products=prod)
         assert torch.equal(a, b), prod
     if st == 1:
@@ -731,9 +740,10 @@ def test_a3_192_tiles(cuda_device, case, bm):
         amax = ops.absmax(gy)
         dys = ops.split_pack_x3(gy, amax)
         wf = ops.weight_flip_pack_x3(wt)
-        if cin % 256 == 0:
+        dref = HKP_TILE_256_A3 if cin % 256 == 0 else HKP_TILE_128_MF16 if bm == 160 else None
+        if dref is not None:                # (dgrad outputs cin channels)
             dx0 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, sk=False,
-                                         tile=HKP_TILE_256_A3)
+                                         tile=dref)
             dx1 = ops.conv2d_bwd_data_x3(dys, wf, (n, h, w, cin), pad, dil, add=add, amax=amax, tile=tile)
             assert torch.equal(dx1, dx0)
 

@@ -108,7 +108,7 @@ a192)
         > $O/pytest_prec.log 2>&1
     echo "pytest: $(tail -1 $O/pytest_prec.log)"
     timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,15,16 --rounds 7 --iters 20 \
-        --shapes t3,t3a,t4,t4ds,t3ds > $O/conv_ab.log 2>&1
+        --shapes t3,t3a,t2,t2s,t4,t4ds,t3ds > $O/conv_ab.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
