@@ -11,6 +11,7 @@
 #   prof      the final tree's traces (C2 + PMC, B=8, C4, C3 train) and bench lines
 #   pmc       PMC passes of the final tree for C4 and C3 training
 #   a192      the 192-row A3 tiles: tests and per-conv timing on the B=8 shapes
+#   dg        the overlapped dgrad's tile (C3 training) with the 160-row forms
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -109,6 +110,11 @@ a192)
     echo "pytest: $(tail -1 $O/pytest_prec.log)"
     timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,15,16 --rounds 7 --iters 20 \
         --shapes t3,t3a,t2,t2s,t4,t4ds,t3ds > $O/conv_ab.log 2>&1
+    ;;
+dg)
+    # training dgrad tile under the wgrad overlap (Policy.dgrad_overlap_tile) with the 160-row forms
+    timeout -k 10 600 python -u tools/train_ab.py "" "dgrad_overlap_tile=16" "dgrad_overlap_tile=0" \
+        --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
