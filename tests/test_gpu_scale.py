@@ -90,7 +90,7 @@ def _c2_batch_vs_reference(cuda_device, g, inp):
     # 3x3 convs (120x160) on the halo-tile body, each block's conv2 with conv1's BN
     # applied in the halo stage (conv_x3_halo_bnin_kernel); the stem (240x320
     # output) on the patch body
-    assert syms and all(s.startswith(("conv_x3_kernel", "conv_x3_a3_kernel", "conv_x3_halo_kernel",
+    assert syms and all(s.startswith(("conv_x3_kernel", "conv_x3_a3_", "conv_x3_halo_kernel",
                                       "conv_x3_halo_bnin_kernel", "conv_x3_stem_patch_kernel")) for s in syms), syms
     assert "conv_x3_halo_kernel<3>" in syms and "conv_x3_halo_bnin_kernel<3>" in syms
     assert any(s.startswith("conv_x3_stem_patch_kernel") for s in syms)
