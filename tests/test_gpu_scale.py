@@ -388,8 +388,9 @@ def _sampled_train_step(dev, bb, K, H, W, B, seeds, x=None, uv=None, sync_bn=Fal
 
 def test_c3_shard_train_step_sampled_fp64(cuda_device):
     """bench.py's `train` leg exactly (C3 shard: R34-8s K=4 640x480 B=8, default
-    policy — side-stream wgrad overlapping a 256x256 + split-K-tail dgrad, the
-    column-grouped stream-K forward): every call vs fp64 on sampled elements."""
+    policy — side-stream wgrad overlapping a 256x256 dgrad, the forward's 38,400-row
+    layers on the 160-row A3 tiles of the measured plan): every call vs fp64 on
+    sampled elements."""
     from hkp import net
     loss, counts, stats, syms, m = _sampled_train_step(cuda_device, "resnet34", 4, 480, 640, 8, (71, 72, 73, 74))
     print("C3 shard step: loss %.9f, calls %s, worst error / bound: %s" % (
@@ -402,7 +403,7 @@ def test_c3_shard_train_step_sampled_fp64(cuda_device):
     # train leg's roofline symbol and the wgrad kernel among the launches
     assert m.policy.overlap_wgrad and not net._memory_tight(cuda_device)
     assert "conv_x3_a3_kernel<3>" in syms and "wgrad_x3_kernel<256>" in syms
-    assert any(s.endswith(", true, 3>") for s in syms), syms          # stream-K forward / dgrad bodies ran
+    assert "conv_x3_a3_160_kernel<3>" in syms and "conv_x3_a3_160x128_kernel<3>" in syms, syms
 
 
 def test_c5_train_step_sampled_fp64(cuda_device):

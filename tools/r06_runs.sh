@@ -77,17 +77,17 @@ prof)
     # the bench lines after them read this tree's trace), then the C2, B=8, C4 and
     # C3-train bench lines
     trace c2 "--steps 5 --warmup 2"
-    cp $O/c2_kernel_stats.csv profiles/r06_infer_c2_kernel_stats_v2.csv
+    cp $O/c2_kernel_stats.csv profiles/r06_infer_c2_kernel_stats_v3.csv
     bash tools/pmc_passes.sh $O/pmc_c2 "--steps 2 --warmup 1 --no-extras" "." > $O/pmc_c2.log 2>&1
-    cp $O/pmc_c2/pmc_summary.json profiles/r06_infer_c2_pmc_v2.json
+    cp $O/pmc_c2/pmc_summary.json profiles/r06_infer_c2_pmc_v3.json
     python3 tools/hbm_table.py $O/c2_kernel_stats.csv $O/pmc_c2/pmc_summary.json --steps 12 --top 40 > $O/c2_hbm_table.txt
     echo "c2 ok"
     trace b8 "--batch 8 --steps 10 --warmup 2"
-    cp $O/b8_kernel_stats.csv profiles/r06_b8_kernel_stats_v2.csv
+    cp $O/b8_kernel_stats.csv profiles/r06_b8_kernel_stats_v3.csv
     trace c4 "$C4 --steps 5 --warmup 2"
-    cp $O/c4_kernel_stats.csv profiles/r06_infer_c4_kernel_stats_v1.csv
+    cp $O/c4_kernel_stats.csv profiles/r06_infer_c4_kernel_stats_v2.csv
     trace train "--mode train --steps 5 --warmup 2"
-    cp $O/train_kernel_stats.csv profiles/r06_train_c3_kernel_stats_v1.csv
+    cp $O/train_kernel_stats.csv profiles/r06_train_c3_kernel_stats_v2.csv
     echo "traces ok"
     timeout -k 10 300 python -u bench.py > $O/bench_c2.log 2>&1
     timeout -k 10 300 python -u bench.py --batch 8 --no-cpu-baseline --no-extras > $O/bench_b8.log 2>&1
