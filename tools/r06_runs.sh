@@ -12,6 +12,7 @@
 #   pmc       PMC passes of the final tree for C4 and C3 training
 #   a192      the 192-row A3 tiles: tests and per-conv timing on the B=8 shapes
 #   dg        the overlapped dgrad's tile (C3 training) with the 160-row forms
+#   plan16    the batch-16 shard (north_star at N = 4) added to the plan
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -63,7 +64,7 @@ plan)
     # the measured tile plan: sweep every live tile policy over the workloads' forward
     # conv shapes (writes hulk-keypoints_amd/hkp/tile_plan.json, copied back), then the
     # plan vs the C planner in one process (Policy.tile_plan)
-    timeout -k 10 900 python -u tools/tile_sweep.py --workloads c2,b8,c3,c4,c5 --rounds 5 --iters 4 \
+    timeout -k 10 900 python -u tools/tile_sweep.py --workloads ${WL:-c2,b8,c3,c4,c5} --rounds 5 --iters 4 \
         --out $O/tile_plan.json > $O/sweep.log 2>&1
     cp $O/tile_plan.json hulk-keypoints_amd/hkp/tile_plan.json
     timeout -k 10 400 python -u tools/infer_ab.py "" "tile_plan=0" --batch 8 --rounds 7 --iters 20 > $O/ab_b8.log 2>&1
@@ -115,6 +116,14 @@ dg)
     # training dgrad tile under the wgrad overlap (Policy.dgrad_overlap_tile) with the 160-row forms
     timeout -k 10 600 python -u tools/train_ab.py "" "dgrad_overlap_tile=16" "dgrad_overlap_tile=0" \
         --rounds 7 --iters 10 > $O/ab_train.log 2>&1
+    ;;
+plan16)
+    # the north_star shard at N = 4 (batch 16 per rank) added to the committed plan
+    cp hulk-keypoints_amd/hkp/tile_plan.json $O/tile_plan.json
+    timeout -k 10 600 python -u tools/tile_sweep.py --workloads b16 --rounds 5 --iters 4 \
+        --out $O/tile_plan.json > $O/sweep.log 2>&1
+    cp $O/tile_plan.json hulk-keypoints_amd/hkp/tile_plan.json
+    timeout -k 10 400 python -u tools/infer_ab.py "" "tile_plan=0" --batch 16 --rounds 7 --iters 20 > $O/ab_b16.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1

@@ -27,6 +27,7 @@ HYST = 0.015
 WORKLOADS = {   # name: (backbone, keypoints, batch, height, width, precision, mode)
     "c2": ("resnet34", 4, 32, 480, 640, "f16x3", "infer"),
     "b8": ("resnet34", 4, 8, 480, 640, "f16x3", "infer"),
+    "b16": ("resnet34", 4, 16, 480, 640, "f16x3", "infer"),    # north_star batch 64 over 4 GPUs
     "c3": ("resnet34", 4, 8, 480, 640, "f16x3", "train"),
     "c4": ("resnet50", 8, 128, 480, 640, "f16", "infer"),
     "c5": ("resnet50", 8, 32, 960, 1280, "f16x3", "train"),
