@@ -116,6 +116,8 @@ dg)
     # training dgrad tile under the wgrad overlap (Policy.dgrad_overlap_tile) with the 160-row forms
     timeout -k 10 600 python -u tools/train_ab.py "" "dgrad_overlap_tile=16" "dgrad_overlap_tile=0" \
         --rounds 7 --iters 10 > $O/ab_train.log 2>&1
+    timeout -k 10 600 python -u tools/train_ab.py "" "dgrad_overlap_tile=16,wgrad_overlap_cus=64" \
+        "dgrad_overlap_tile=16,wgrad_overlap_cus=128" "overlap_wgrad=0" --rounds 5 --iters 10 > $O/ab_train2.log 2>&1
     ;;
 plan16)
     # the north_star shard at N = 4 (batch 16 per rank) added to the committed plan
