@@ -13,6 +13,7 @@
 #   a192      the 192-row A3 tiles: tests and per-conv timing on the B=8 shapes
 #   dg        the overlapped dgrad's tile (C3 training) with the 160-row forms
 #   plan16    the batch-16 shard (north_star at N = 4) added to the plan
+#   c5        C5 training: the plan vs the C planner
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -126,6 +127,12 @@ plan16)
         --out $O/tile_plan.json > $O/sweep.log 2>&1
     cp $O/tile_plan.json hulk-keypoints_amd/hkp/tile_plan.json
     timeout -k 10 400 python -u tools/infer_ab.py "" "tile_plan=0" --batch 16 --rounds 7 --iters 20 > $O/ab_b16.log 2>&1
+    ;;
+c5)
+    # config C5 (R50-8s K=8 1280x960, the 32-image shard of batch 256 over 8 GPUs): the
+    # measured plan against the C planner in one process
+    timeout -k 10 900 python -u tools/train_ab.py "" "tile_plan=0" --backbone resnet50 --keypoints 8 --height 960 \
+        --width 1280 --batch 32 --rounds 3 --iters 2 > $O/ab_c5.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1

@@ -52,6 +52,9 @@ def main():
     ap.add_argument("forms", nargs="+", help="comma-separated FIELD=VALUE Policy overrides per form ('' = default)")
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--backbone", default="resnet34")
+    ap.add_argument("--keypoints", type=int, default=4)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--ab", action="store_true", help="load the A/B build (tools/ab_lib, its hkp_debug_* knobs)")
@@ -66,7 +69,7 @@ def main():
     from src.model import KeypointsGauss
     hkp.lib()
     dev = torch.device("cuda", 0)
-    B, K, H, W = args.batch, 4, 480, 640
+    B, K, H, W = args.batch, args.keypoints, args.height, args.width
     torch.manual_seed(1234)
     base = Policy()
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=base).to(dev)
