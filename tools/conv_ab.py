@@ -38,6 +38,8 @@ SHAPES = {
     "t4": ("x3", 8, 60, 80, 512, 512, 3, 1, 4, 4),             # training shard (batch 8)
     "t3": ("x3", 8, 60, 80, 256, 256, 3, 1, 2, 2),
     "t2": ("x3", 8, 60, 80, 128, 128, 3, 1, 1, 1),             # layer2 3x3 at batch 8 (128-wide)
+    "c2_l3": ("x3", 32, 60, 80, 256, 256, 3, 1, 2, 2),         # C2 layer3 3x3 (dilation 2)
+    "c2_l3a": ("x3", 32, 60, 80, 128, 256, 3, 1, 2, 2),        # C2 layer3 conv1
     "t2s": ("x3", 8, 120, 160, 64, 128, 3, 2, 1, 1),           # layer2 conv1, stride 2
     "t3a": ("x3", 8, 60, 80, 128, 256, 3, 1, 2, 2),            # layer3 conv1 at batch 8 (dilated, stride 1)
     "t4ds": ("x3", 8, 60, 80, 256, 512, 1, 1, 0, 1),

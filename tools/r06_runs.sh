@@ -14,6 +14,7 @@
 #   dg        the overlapped dgrad's tile (C3 training) with the 160-row forms
 #   plan16    the batch-16 shard (north_star at N = 4) added to the plan
 #   c5        C5 training: the plan vs the C planner
+#   h12       the 12x20 halo-staged A3 body: tests and per-conv timing
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -133,6 +134,14 @@ c5)
     # measured plan against the C planner in one process
     timeout -k 10 900 python -u tools/train_ab.py "" "tile_plan=0" --backbone resnet50 --keypoints 8 --height 960 \
         --width 1280 --batch 32 --rounds 3 --iters 2 > $O/ab_c5.log 2>&1
+    ;;
+h12)
+    # the 12x20 halo-staged A3 body (HKP_TILE_HALO12): its tests, then per-conv timing
+    timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_precision.py \
+        > $O/pytest_prec.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_prec.log)"
+    timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,17 --rounds 7 --iters 10 \
+        --shapes c2_l3,c2_l3a,c4_l3_c2,t3 > $O/conv_ab.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
