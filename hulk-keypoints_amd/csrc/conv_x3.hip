@@ -1915,334 +1915,6 @@ __global__ __launch_bounds__(512, 2) void conv_x3_halo_bnin_kernel(X3Args a) {
 }
 
 // ---------------------------------------------------------------------------
-// The A3 body with its activation operand staged as a halo image
-// (conv_x3_h12_kernel<P>, HKP_TILE_HALO12): stride-1 3x3 convs with pad =
-// dilation <= 2 whose output tiles into 12 x 20 pixel patches (60x80 maps: layer3
-// of the R-nets here at 640x480).  The A3 body stages every activation line once
-// per tap — each line 9 times per channel group — and at 256x256 tiles that stream
-// is what the CU's LDS-DMA rate bounds (plain fp16 needs ~75 GB/s per CU for the
-// MFMAs; the CU delivers ~55-70).  Here a tile is a 12 x 20 patch (240 rows, padded
-// to the 256 MFMA rows of A3's 4 x 2 waves) x 256 output channels: per channel group
-// its (12 + 2d) x (20 + 2d) halo lines (384 at d = 2: 48 KiB) are staged ONCE and
-// the nine taps read their fragments from it (tile row m = pixel (m / 20, m % 20)
-// reads halo line (m / 20 + r d) (20 + 2d) + m % 20 + s d).  Two halo buffers and a
-// 2-stage weight ring fill the 160 KiB: the next group's halo streams in one DMA
-// piece per K-step behind the weights (its six pieces over the group's first six
-// taps, each with a K-step or more to land before a counted wait needs it).  The K
-// order (channel group outer, tap inner) and the MFMA sequence per output are the
-// A3 body's: the outputs are its bits.  BN partials per 240-row tile
-// (hkp_conv_x3_stat_tile_rows); rows 240-255 are computed and dropped.
-constexpr int H12_PH = 12, H12_PW = 20, H12_NLMAX = 384;             // patch; halo lines at d <= 2
-constexpr int H12_GH = H12_NLMAX / 8 / 8;                             // halo DMA pieces per wave (6)
-constexpr int H12_HBYTES = H12_NLMAX * 128;                           // 48 KiB per halo buffer
-constexpr int H12_LDS = 2 * H12_HBYTES + 2 * 256 * 128;               // + the weight ring: 160 KiB
-
-static bool h12_shape(int stride, int r, int s, int pad, int dil, int ho, int wo, int k) {
-    return stride == 1 && r == 3 && s == 3 && pad == dil && dil >= 1 && dil <= 2 && ho % H12_PH == 0 &&
-           wo % H12_PW == 0 && k % 256 == 0;
-}
-
-template <int P>
-__device__ __forceinline__ void conv_x3_h12_body(const X3Args& a, char* smem) {
-    constexpr int BM = 256, BN = 256, WM = 4, WN = 2, ROW = 128;
-    constexpr int UM = BM / (WM * 16), UN = BN / (WN * 16);          // 4 x 8 16x16 sub-tiles per wave
-    constexpr int GB = BN / 8 / 8;                                    // weight DMA pieces per wave (4)
-    constexpr int NMC = x3_nprod(P) * UM;
-    static_assert(128 * (BN + 4) * 4 <= H12_LDS && 3 * WM * BN * 4 <= H12_LDS, "epilogue staging in two passes");
-    static_assert(P != 1 || BM * (BN + 8) * 2 <= H12_LDS, "fp16 staging");
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
-    const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
-    const int pwn = a.Wo / H12_PW, tpi = (a.Ho / H12_PH) * pwn;
-    const int img = mt / tpi, rem = mt - img * tpi;
-    const int h0 = (rem / pwn) * H12_PH, w0 = (rem - (rem / pwn) * pwn) * H12_PW;
-    const int n0 = nt * BN;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = w / WN, wn = w % WN;
-    const int D = a.dil, LW = H12_PW + 2 * D, NL = (H12_PH + 2 * D) * LW;
-    const int cstride = a.cch * 64;                                   // halves per pixel
-    const int nks = a.nks;                                            // 9 taps x channel groups
-    const _Float16* zero = (const _Float16*)g_x3_zero_line;
-    char* const bring = smem + 2 * H12_HBYTES;
-
-    x3_stamp(a, 0);
-    // ---- halo DMA: piece i of wave w fills lines 8 (w GH + i) .. +7 of a buffer ----
-    unsigned h_off[H12_GH];                                           // element offsets from a.xs, or ~0u
-#pragma unroll
-    for (int i = 0; i < H12_GH; ++i) {
-        const int L = 8 * (w * H12_GH + i) + lane / 8;
-        const int Lc = (lane % 8) ^ halo_swz(L);
-        const int hl = L / LW, wl = L - hl * LW;
-        const int hi = h0 - a.pad + hl, wi = w0 - a.pad + wl;
-        const bool in = L < NL && (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        h_off[i] = in ? (unsigned)((((long)img * a.H + hi) * a.W + wi) * cstride + Lc * 8) : ~0u;
-    }
-    auto halo_piece = [&](int g, int i) {
-        glds16(h_off[i] != ~0u ? a.xs + ((unsigned long)h_off[i] + g * 64) : zero,
-               smem + (g & 1) * H12_HBYTES + 8 * (w * H12_GH + i) * ROW);
-    };
-    // ---- weight DMA (A3's B ring): stage t = (group t / 9, tap t % 9) ----
-    // (one base register; a piece's row and swizzle recomputed per issue: the
-    // per-piece offsets held across the K loop pushed the body past 256 VGPRs)
-    const int bline = a.RS * a.cch * 64;
-    const int brow0 = 8 * (w * GB) + lane / 8;
-    const int b_base0 = (n0 + brow0) * bline + (lane % 8) * 8;
-    auto issue_b = [&](int t) {
-        const int g = t / 9, u = t - g * 9;
-        const int boff = (u * a.cch + g) * 64;
-#pragma unroll
-        for (int j = 0; j < GB; ++j) {
-            const int row = brow0 + 8 * j;
-            const int off = b_base0 + 8 * j * bline + (((lane % 8) ^ ((row >> 1) & 7)) - (lane % 8)) * 8;
-            glds16(a.ws + (unsigned)(off + boff), bring + (t & 1) * (BN * ROW) + 8 * (w * GB + j) * ROW);
-        }
-    };
-
-    // ---- fragment addressing ----
-    const int r16 = lane & 15, q = lane >> 4;
-    int lb[UM];                                                       // halo line of tap (0, 0), sub-tile i
-#pragma unroll
-    for (int i = 0; i < UM; ++i) {
-        const int m = wm * 64 + 16 * i + r16;
-        lb[i] = m < H12_PH * H12_PW ? (m / H12_PW) * LW + m % H12_PW : 0;   // padding rows: any line
-    }
-    const int sw = (r16 >> 1) & 7;
-    const int fo_h = r16 * ROW + ((q ^ sw) << 4), fo_l = r16 * ROW + (((4 + q) ^ sw) << 4);
-    const int b_base = (wn * UN * 16) * ROW;
-
-    f32x4 acc[UM][UN];
-#pragma unroll
-    for (int i = 0; i < UM; ++i)
-#pragma unroll
-        for (int j = 0; j < UN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    struct FA {
-        f16x8 h[UM], l[UM];
-    };
-    f16x8 bh[UN], bl[UN];
-    auto read_a = [&](FA& f, int t) {
-        const int g = t / 9, u = t - g * 9;
-        const int toff = (u / 3) * D * LW + (u - (u / 3) * 3) * D;
-        const char* hb = smem + (g & 1) * H12_HBYTES;
-#pragma unroll
-        for (int i = 0; i < UM; ++i) {
-            const int L = lb[i] + toff;
-            const int ls = halo_swz(L);
-            f.h[i] = *(const f16x8*)(hb + L * ROW + ((q ^ ls) << 4));
-            f.l[i] = *(const f16x8*)(hb + L * ROW + (((4 + q) ^ ls) << 4));
-        }
-    };
-    auto read_b = [&](int j, const char* st) {
-        bh[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_h);
-        bl[j] = *(const f16x8*)(st + b_base + j * 16 * ROW + fo_l);
-    };
-    auto mfma = [](const f16x8& x, const f16x8& y, const f32x4& c) {
-        return __builtin_amdgcn_mfma_f32_16x16x32_f16(x, y, c, 0, 0, 0);
-    };
-    auto mma_col = [&](const FA& f, int j) {
-#pragma unroll
-        for (int i = 0; i < UM; ++i) x3_products<P>(acc[i][j], f.h[i], f.l[i], bh[j], bl[j], mfma);
-    };
-    const int ngroups = nks / 9;
-
-    // prologue: halo of group 0, weight stages 0 and 1; stage 0's fragments
-#pragma unroll
-    for (int i = 0; i < H12_GH; ++i) halo_piece(0, i);
-    issue_b(0);
-    if (nks > 1) issue_b(1);
-    if (nks > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GB) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    x3_stamp(a, 1);
-    FA fa;
-    read_a(fa, 0);
-#pragma unroll
-    for (int j = 0; j < UN; ++j) read_b(j, bring);
-    // K-step t (fragments of t already in registers): wait until B(t+1) has landed
-    // (the halo piece issued after it in step t-1 may stay in flight), barrier; B(t+2)
-    // into t's slot, then (taps 0-5 of a group that has a successor) one piece of the
-    // next group's halo; per column: t's MFMAs, B_j of t+1; then A of t+1 from its
-    // halo buffer (the next group's after tap 8: all its pieces landed by the wait)
-    int hp_prev = 0;                                                  // a halo piece issued after B(t+1)
-    for (int t = 0; t + 1 < nks; ++t) {
-        if (hp_prev) asm volatile("s_waitcnt vmcnt(1) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        lds_barrier();
-        const int g = t / 9, u = t - g * 9;
-        if (t + 2 < nks) issue_b(t + 2);
-        hp_prev = 0;
-        if (u < H12_GH && g + 1 < ngroups) {
-            // wave-uniform piece index u
-#pragma unroll
-            for (int i = 0; i < H12_GH; ++i)
-                if (i == u) halo_piece(g + 1, i);
-            hp_prev = 1;
-        }
-        const char* stb = bring + ((t + 1) & 1) * (BN * ROW);
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            mma_col(fa, j);
-            read_b(j, stb);
-        }
-        read_a(fa, t + 1);
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            __builtin_amdgcn_sched_group_barrier(0x008, NMC, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x100, 2 * UM, 0);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < UN; ++j) mma_col(fa, j);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    x3_stamp(a, 2);
-
-    // ---- epilogue ----
-    constexpr int VALID = H12_PH * H12_PW;                            // 240 rows
-    const float ginv = a.amax ? 1.f / pow2_scale_for(a.amax) : 1.f;
-    float sc[UN];
-#pragma unroll
-    for (int j = 0; j < UN; ++j) sc[j] = (a.wscale ? a.wscale[n0 + wn * UN * 16 + j * 16 + r16] : 1.f) * ginv;
-    lds_sync();                                                       // every wave done with the halo / ring
-    if (a.part) {
-        // BN partial of the whole 240-row tile: per lane (sum, M2 about its mean)
-        // over its valid rows, Chan-merged across the 4 lane groups of a column
-        // (shuffles), then across the 4 row waves in order (LDS); counts ride along
-        float ls[UN], lq[UN], ln = 0.f;
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) ln += (wm * 64 + 16 * i + 4 * q + r < VALID) ? 1.f : 0.f;
-        const float linv = ln > 0.f ? 1.f / ln : 0.f;
-#pragma unroll
-        for (int j = 0; j < UN; ++j) {
-            float s = 0.f;
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s += (wm * 64 + 16 * i + 4 * q + r < VALID) ? acc[i][j][r] : 0.f;
-            const float mu = s * linv;
-            float qq = 0.f;
-#pragma unroll
-            for (int i = 0; i < UM; ++i)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float d = acc[i][j][r] - mu;
-                    qq += (wm * 64 + 16 * i + 4 * q + r < VALID) ? d * d : 0.f;
-                }
-            ls[j] = s;
-            lq[j] = qq;
-        }
-        for (int o = 16; o < 64; o <<= 1) {
-            const float nb = __shfl_xor(ln, o);
-            const float ntot = ln + nb;
-            const float f = ntot > 0.f ? ln * nb / ntot : 0.f;
-            const float ia = ln > 0.f ? 1.f / ln : 0.f, ib = nb > 0.f ? 1.f / nb : 0.f;
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                const float sb = __shfl_xor(ls[j], o), qb = __shfl_xor(lq[j], o);
-                const float d = sb * ib - ls[j] * ia;
-                ls[j] = ls[j] + sb;
-                lq[j] = (lq[j] + qb) + d * d * f;
-            }
-            ln = ntot;
-        }
-        float* red = (float*)smem;                                    // [3][WM][BN]: sum, M2, count
-        if (lane < 16) {
-#pragma unroll
-            for (int j = 0; j < UN; ++j) {
-                const int c = wn * UN * 16 + j * 16 + lane;
-                red[(0 * WM + wm) * BN + c] = ls[j];
-                red[(1 * WM + wm) * BN + c] = lq[j];
-                red[(2 * WM + wm) * BN + c] = ln;
-            }
-        }
-        lds_sync();
-        if (tid < BN) {
-            const int c = tid;
-            float S = red[c], Q = red[WM * BN + c], N = red[2 * WM * BN + c];   // wave 0
-            for (int v = 1; v < WM; ++v) {
-                const float sb = red[(0 * WM + v) * BN + c], qb = red[(1 * WM + v) * BN + c];
-                const float nb = red[(2 * WM + v) * BN + c];
-                if (nb > 0.f) {
-                    const float ntot = N + nb;
-                    const float d = sb / nb - S / N;
-                    Q = (Q + qb) + d * d * (N * nb / ntot);
-                    S = S + sb;
-                    N = ntot;
-                }
-            }
-            const float scol = (a.wscale ? a.wscale[n0 + c] : 1.f) * ginv;
-            a.part[((long)mt * a.K + n0 + c) * 2 + 0] = S * scol;
-            a.part[((long)mt * a.K + n0 + c) * 2 + 1] = Q * (scol * scol);
-        }
-        lds_sync();
-    }
-    auto out_pix = [&](int row) {
-        return ((long)img * a.Ho + h0 + row / H12_PW) * a.Wo + w0 + row % H12_PW;
-    };
-    x3_stamp(a, 3);
-    if constexpr (P == 1) {
-        constexpr int PITCH = BN + 8, CH = BN / 8;
-        _Float16* st = (_Float16*)smem;
-#pragma unroll
-        for (int i = 0; i < UM; ++i)
-#pragma unroll
-            for (int j = 0; j < UN; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    st[(wm * 64 + i * 16 + 4 * q + r) * PITCH + wn * UN * 16 + j * 16 + r16] =
-                        (_Float16)(acc[i][j][r] * sc[j]);
-        lds_sync();
-#pragma unroll 4
-        for (int e = tid; e < VALID * CH; e += 512) {
-            const int row = e / CH, cc = e - row * CH;
-            x3_st16((uint4*)(a.y16 + out_pix(row) * a.K + n0 + cc * 8), *(const uint4*)(smem + (row * PITCH + cc * 8) * 2),
-                    a.st_kind, 1);
-        }
-    } else {
-        constexpr int RPP = 128, PITCH = BN + 4, C4 = BN / 4;
-        float* st = (float*)smem;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if ((wm >> 1) == h) {
-#pragma unroll
-                for (int i = 0; i < UM; ++i)
-#pragma unroll
-                    for (int j = 0; j < UN; ++j)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            st[(wm * 64 + i * 16 + 4 * q + r - h * RPP) * PITCH + wn * UN * 16 + j * 16 + r16] =
-                                acc[i][j][r] * sc[j];
-            }
-            lds_sync();
-            const int rows = h == 0 ? RPP : VALID - RPP;
-#pragma unroll 4
-            for (int e = tid; e < rows * C4; e += 512) {
-                const int row = e / C4, c4 = e - row * C4;
-                const long off = out_pix(h * RPP + row) * a.K + n0 + c4 * 4;
-                f32x4 v = *(const f32x4*)(st + row * PITCH + c4 * 4);
-                if (a.add) {
-                    const f32x4 ad = *(const f32x4*)(a.add + off);
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v[k] = v[k] + ad[k];
-                }
-                x3_st16((f32x4*)(a.y + off), v, a.st_kind, 2);
-            }
-            if (h == 0) lds_sync();
-        }
-    }
-    x3_stamp(a, 5);
-}
-
-template <int P>
-__global__ __launch_bounds__(512, 1) void conv_x3_h12_kernel(X3Args a) {
-    __shared__ __attribute__((aligned(1024))) char smem[H12_LDS];
-    conv_x3_h12_body<P>(a, smem);
-}
-
-// ---------------------------------------------------------------------------
 // Stem patch body (conv_x3_stem_patch_kernel): the 7x7/s2 stem on the padded
 // NHWC4 hi | lo image planes of hkp_stem_pack_x3, a tile = an 8 x 32 patch of
 // output pixels.  The one-tile stem (conv_x3_kernel<64, STEM, PAIR>) stages per
@@ -3744,13 +3416,6 @@ static void x3_dispatch_p(int P, F&& f) {
     }
 }
 
-// the 12x20 halo-staged A3 body takes this launch (HKP_TILE_HALO12)
-static bool x3_h12_ok(const X3Args& a, int k) {
-    return h12_shape(a.stride, a.R, a.S, a.pad, a.dil, a.Ho, a.Wo, k) && a.Ho == a.H && a.Wo == a.W && a.ost == 0 &&
-           a.ep_ss == nullptr && a.in_ss == nullptr && a.mt0 == 0 && a.plane == 0 &&
-           (long)a.N * a.H * a.W * a.cch * 64L + 64 < (1L << 32);
-}
-
 static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3Args& a, void* ws = nullptr,
                       int64_t ws_bytes = 0) {
     a.stamps = g_x3_stamps;
@@ -3763,15 +3428,6 @@ static void launch_x3(int k, long m_tiles, int policy, int P, hipStream_t st, X3
     a.stagger_blocks = x3_cus();
     const bool sk_ok = ws && ws_bytes >= x3_sk_ws_bytes(256);
     const int nks = a.RS * a.cch;
-    if (policy == HKP_TILE_HALO12 && x3_h12_ok(a, k)) {
-        a.n_tiles = k / 256;
-        a.nks = nks;
-        a.sk_units = 0;
-        const dim3 gh((unsigned)((long)a.N * (a.Ho / H12_PH) * (a.Wo / H12_PW) * a.n_tiles));
-        x3_dispatch_p(P, [&](auto pc) { hipLaunchKernelGGL(conv_x3_h12_kernel<pc.value>, gh, dim3(512), 0, st, a); });
-        return;
-    }
-    if (policy == HKP_TILE_HALO12) policy = HKP_TILE_AUTO;            // a shape it does not take
     const X3Choice c = x3_choose(k, m_tiles, nks, sk_ok, policy, x3_halo_level(x3_halo_ok(a, k), a.cch, P), P);
     a.n_tiles = k / c.bn;
     a.nks = nks;
@@ -3899,7 +3555,7 @@ static bool x3_offsets_fit(long n, long h, long w, long cstride, long k, long rs
 }
 
 static int check_tile(const hkp_conv_desc* d, const char* who) {
-    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_HALO12, "%s: unknown tile policy %d", who,
+    HKP_CHECK_ARG(d->tile >= HKP_TILE_AUTO && d->tile <= HKP_TILE_160_A3, "%s: unknown tile policy %d", who,
                   d->tile);
     HKP_CHECK_ARG(d->tile != HKP_TILE_RESERVED_7 && d->tile != HKP_TILE_RESERVED_8 && d->tile != HKP_TILE_RESERVED_14,
                   "%s: tile policy %d is retired (a persistent conv body, measured slower)", who, d->tile);
@@ -4319,11 +3975,6 @@ extern "C" int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* 
 extern "C" int32_t hkp_conv_x3_stat_tile_rows(const hkp_conv_desc* d, int32_t op) {
     HKP_CHECK_ARG(d, "hkp_conv_x3_stat_tile_rows: null descriptor");
     const bool packed = op == HKP_KOP_FWD_X3 || op == HKP_KOP_FWD_X3_W16 || op == HKP_KOP_FWD_X3_X16;
-    int ho, wo;
-    if (d->tile == HKP_TILE_HALO12 && (packed || op == HKP_KOP_FWD_F16) && hkp_conv_out_hw(d, &ho, &wo) == HKP_OK &&
-        h12_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
-        (long)d->n * d->h * d->w * (d->c / (packed ? 32 : 64) * 64L) + 64 < (1L << 32))
-        return H12_PH * H12_PW;                                      // (x3_h12_ok's conditions)
     if (packed && d->tile == HKP_TILE_192_A3 && d->k % 256 == 0) return 96;
     if (packed && d->tile == HKP_TILE_160_A3 && d->k % 128 == 0) return 80;
     return 128;
@@ -4352,14 +4003,6 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int nks = d->r * d->s * (d->c / cg);
             const bool halo = halo_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
                               (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32);
-            if (d->tile == HKP_TILE_HALO12) {
-                if (h12_shape(d->stride, d->r, d->s, d->pad, d->dilation, ho, wo, d->k) &&
-                    (long)d->n * d->h * d->w * (d->c / cg * 64L) + 64 < (1L << 32))
-                    return snprintf(buf, len, "conv_x3_h12_kernel<%d>", P);
-                hkp_conv_desc e = *d;
-                e.tile = HKP_TILE_AUTO;
-                return hkp_conv_kernel_name(&e, op, stream_k_ok, buf, len);
-            }
             return x3_kernel_name(x3_choose(d->k, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->c / cg, P), P),
                                   false, P, buf, len);
         }
@@ -4369,14 +4012,6 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             const int padp = d->dilation * (d->r - 1) - d->pad;
             const bool halo = halo_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
                               (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32);
-            if (d->tile == HKP_TILE_HALO12) {
-                if (h12_shape(d->stride, d->r, d->s, padp, d->dilation, d->h, d->w, d->c) &&
-                    (long)d->n * ho * wo * (d->k / 32 * 64L) + 64 < (1L << 32))
-                    return snprintf(buf, len, "conv_x3_h12_kernel<3>");
-                hkp_conv_desc e = *d;
-                e.tile = HKP_TILE_AUTO;
-                return hkp_conv_kernel_name(&e, op, stream_k_ok, buf, len);
-            }
             return x3_kernel_name(x3_choose(d->c, (m + 255) / 256, nks, sk, d->tile, x3_halo_level(halo, d->k / 32, 3), 3),
                                   false, 3, buf, len);
         }

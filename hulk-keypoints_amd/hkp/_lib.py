@@ -30,7 +30,7 @@ class ConvDesc(ctypes.Structure):
 # hkp_conv_desc.tile policies (include/hulkkp.h)
 (HKP_TILE_AUTO, HKP_TILE_NO_SK, HKP_TILE_SK, HKP_TILE_256, HKP_TILE_128_MF16, HKP_TILE_128_MF32, HKP_TILE_64_PAIR,
  HKP_TILE_RESERVED_7, HKP_TILE_RESERVED_8, HKP_TILE_256_TAIL, HKP_TILE_HALO, HKP_TILE_256_A3, HKP_TILE_AUTO_A3,
- HKP_TILE_DUO, HKP_TILE_RESERVED_14, HKP_TILE_192_A3, HKP_TILE_160_A3, HKP_TILE_HALO12) = range(18)
+ HKP_TILE_DUO, HKP_TILE_RESERVED_14, HKP_TILE_192_A3, HKP_TILE_160_A3) = range(17)
 # hkp_conv_kernel_name ops
 HKP_KOP_FWD_X3, HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_STEM_X3, HKP_KOP_WGRAD_X3, HKP_KOP_FWD_X3_W16, \
     HKP_KOP_FWD_X3_X16, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8 = range(9)

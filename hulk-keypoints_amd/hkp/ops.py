@@ -10,7 +10,7 @@ import torch
 
 from ._lib import (HKP_KOP_DGRAD_X3, HKP_KOP_FWD_F16, HKP_KOP_FWD_X3, HKP_KOP_FWD_X3_W16, HKP_KOP_FWD_X3_X16,
                    HKP_KOP_STEM_X3, HKP_KOP_STEM_X3_IMAGE, HKP_KOP_STEM_X3_IMAGE_U8, HKP_KOP_WGRAD_X3, HKP_X3_ALL,
-                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, HKP_TILE_160_A3, HKP_TILE_192_A3, HKP_TILE_HALO12, ConvDesc, HkpError, call)
+                   HKP_LAYOUT_NCHW, HKP_LAYOUT_NHWC, HKP_TILE_160_A3, HKP_TILE_192_A3, ConvDesc, HkpError, call)
 
 CONV_TILE_ROWS = 128  # BM of conv_fwd.hip (rows per BN statistic tile)
 
@@ -181,9 +181,6 @@ def _stat_partials(n_rows, k, device, part_out, name, tile_rows=CONV_TILE_ROWS):
     return part
 
 
-_ROWS_TILES = (HKP_TILE_192_A3, HKP_TILE_160_A3, HKP_TILE_HALO12)   # tiles whose BN partials are not 128-row
-
-
 def stat_tile_rows(part):
     """Rows per BN statistic tile of conv partials (hkp_conv_x3_stat_tile_rows)."""
     return getattr(part, "_hkp_tile_rows", CONV_TILE_ROWS)
@@ -213,7 +210,7 @@ def conv2d_fwd_x3(xs, wp, stride=1, pad=0, dil=1, stats=True, out=None, part_out
     part = None
     if stats:
         rows = CONV_TILE_ROWS
-        if tile in _ROWS_TILES:               # 96- / 80- / 240-row statistic tiles (the library says)
+        if tile in (HKP_TILE_192_A3, HKP_TILE_160_A3):      # 96- / 80-row statistic tiles (the library says)
             from ._lib import lib
             rows = lib().hkp_conv_x3_stat_tile_rows(ctypes.byref(d), kop)
         part = _stat_partials(n * ho * wo, k, xs.device, part_out, "conv2d_fwd_x3.part_out", rows)
@@ -318,13 +315,7 @@ def conv2d_fwd_f16(x16, wp, stride=1, pad=0, dil=1, stats=True, sk=True, tile=0)
     ho, wo = conv_out_hw(h, wd, r, s, stride, pad, dil)
     d = ConvDesc(n, h, wd, c, k, r, s, stride, pad, dil, HKP_LAYOUT_NHWC, tile)
     y = torch.empty((n, ho, wo, k), device=x16.device, dtype=torch.float16)
-    part = None
-    if stats:
-        rows = CONV_TILE_ROWS
-        if tile in _ROWS_TILES:
-            from ._lib import lib
-            rows = lib().hkp_conv_x3_stat_tile_rows(ctypes.byref(d), HKP_KOP_FWD_F16)
-        part = _stat_partials(n * ho * wo, k, x16.device, None, "conv2d_fwd_f16", rows)
+    part = _stat_partials(n * ho * wo, k, x16.device, None, "conv2d_fwd_f16") if stats else None
 
     def launch():
         call("hkp_conv2d_fwd_f16", ctypes.byref(d), _ptr(x16), _ptr(ws), _ptr(wsc), _ptr(y), _ptr(part),

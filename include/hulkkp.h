@@ -97,12 +97,6 @@ typedef struct hkp_conv_desc {
 #define HKP_TILE_160_A3 16            /* the same on 160 x 256 tiles (waves 2 x 4; 160 x 128 where
                                          Cout % 256 != 0, Cout % 128 == 0), BN partials per 80-row
                                          tile (tile_rows = 80) */
-#define HKP_TILE_HALO12 17            /* stride-1 3x3 convs with pad = dilation <= 2, output 12x20-
-                                         divisible, Cout % 256 == 0 (forward, any operand layout, and
-                                         the stride-1 dgrad): the A3 body with each channel group's
-                                         activation staged once as a 12x20-patch halo image; BN
-                                         partials per 240-row tile (tile_rows 240).  Other shapes
-                                         plan as AUTO */
 
 /* output spatial size: (h + 2*pad - dilation*(r-1) - 1)/stride + 1 */
 int hkp_conv_out_hw(const hkp_conv_desc* d, int32_t* ho, int32_t* wo);
@@ -248,9 +242,8 @@ int hkp_bn_from_gram(int32_t k, int32_t c, int64_t count, const double* mean, co
 #define HKP_KOP_STEM_X3_IMAGE_U8 8  /* hkp_conv2d_fwd_stem_x3_image, uint8 NHWC batch */
 int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int32_t stream_k_ok, char* buf, int32_t len);
 /* Rows per BN statistic tile of a packed forward conv (op HKP_KOP_FWD_X3 / _W16 /
- * _X16, or HKP_KOP_FWD_F16) with this descriptor: 96 with d->tile == HKP_TILE_192_A3
- * (k % 256 == 0), 80 with HKP_TILE_160_A3 (k % 128 == 0), 240 with HKP_TILE_HALO12 on a
- * shape it takes, else 128 (hkp_conv_stat_tiles' tiles).  stat_partials then holds
+ * _X16) with this descriptor: 96 with d->tile == HKP_TILE_192_A3 (k % 256 == 0), 80
+ * with HKP_TILE_160_A3 (k % 128 == 0), else 128 (hkp_conv_stat_tiles' tiles).  stat_partials then holds
  * ceil(M / rows) * k * 2 floats, and hkp_bn_finalize / _ws / hkp_bn_stats take
  * tile_rows = rows (src/resnet.py:46,49: the statistics are the same). */
 int32_t hkp_conv_x3_stat_tile_rows(const hkp_conv_desc* d, int32_t op);

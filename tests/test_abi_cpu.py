@@ -213,15 +213,6 @@ def test_kernel_name_query():
     assert rows(ctypes.byref(b8), _lib.HKP_KOP_FWD_X3) == 80
     b8.tile = 0
     assert rows(ctypes.byref(b8), _lib.HKP_KOP_FWD_X3) == 128
-    # the 12x20 halo-staged A3 body: stride-1 3x3, pad = dil <= 2, 12x20-divisible, Cout % 256
-    b8.tile = _lib.HKP_TILE_HALO12
-    assert ops.kernel_name(b8, _lib.HKP_KOP_FWD_X3) == "conv_x3_h12_kernel<3>"
-    assert ops.kernel_name(b8, _lib.HKP_KOP_FWD_F16) == "conv_x3_h12_kernel<1>"
-    assert ops.kernel_name(b8, _lib.HKP_KOP_DGRAD_X3) == "conv_x3_h12_kernel<3>"
-    assert rows(ctypes.byref(b8), _lib.HKP_KOP_FWD_X3) == 240 and rows(ctypes.byref(b8), _lib.HKP_KOP_FWD_F16) == 240
-    l4 = _lib.ConvDesc(8, 60, 80, 512, 512, 3, 3, 1, 4, 4, 0, _lib.HKP_TILE_HALO12)        # dilation 4: AUTO
-    assert ops.kernel_name(l4, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
-    assert rows(ctypes.byref(l4), _lib.HKP_KOP_FWD_X3) == 128
     d.tile = _lib.HKP_TILE_64_PAIR
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<64, false, true, 16, false, 3>"
     d.tile = 99

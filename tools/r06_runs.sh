@@ -14,7 +14,8 @@
 #   dg        the overlapped dgrad's tile (C3 training) with the 160-row forms
 #   plan16    the batch-16 shard (north_star at N = 4) added to the plan
 #   c5        C5 training: the plan vs the C planner
-#   h12       the 12x20 halo-staged A3 body: tests and per-conv timing
+#   h12       the 12x20 halo-staged A3 body: tests and per-conv timing (ran against commit 5d8eaa7;
+#             measured slower and removed with it: profiles/r06_h12_*)
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
