@@ -64,6 +64,9 @@ def parse():
                          "(ToTensor fused into the stem, SURVEY 8(f1))")
     ap.add_argument("--sync-bn", action="store_true",
                     help="N>1: BN statistics (and, training, their backward sums) over the global batch")
+    ap.add_argument("--stage-precision", default=None, metavar="L1,L2,L3,L4",
+                    help="inference with --precision f16: per-stage conv arithmetic, each of f16 / f16x3 for "
+                         "layer1..layer4 (Policy.stage_precision; DESIGN 'Per-stage precision')")
     ap.add_argument("--no-extras", action="store_true", help="main line only (no train / fp32 legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget for the CPU baseline sample")
@@ -388,7 +391,9 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
     # a strong-scaling shard (shard_of) is a slice of ONE job: every rank runs the same
     # random-init model; weak scaling gives each rank its own seed
     torch.manual_seed(1234 if shard_of is not None else 1234 + rank)
-    pol = Policy(precision=precision, **tuning(args))
+    stage = tuple(args.stage_precision.split(",")) if getattr(args, "stage_precision", None) else ()
+    pol = Policy(precision=precision, stage_precision=stage if mode == "infer" and precision == "f16" else (),
+                 **tuning(args))
     model = KeypointsGauss(K, H, W, backbone=args.backbone, pretrained=False, policy=pol).to(dev)
     if shard_of is not None:
         G, i = shard_of
@@ -495,7 +500,8 @@ def run_leg(mode, precision, batch, args, dev, rank, world, steps, warmup, shard
     # the committed profiles of this exact workload (batch included: a trace's average
     # launch time belongs to its own launch sizes)
     r34 = (args.backbone, K, H, W) == ("resnet34", 4, 480, 640) and precision == "f16x3"
-    c4 = (args.backbone, K, H, W) == ("resnet50", 8, 480, 640) and precision == "f16" and mode == "infer" and B == 128
+    c4 = (args.backbone, K, H, W) == ("resnet50", 8, 480, 640) and precision == "f16" and mode == "infer" and B == 128 \
+        and not args.stage_precision
     c5 = (args.backbone, K, H, W) == ("resnet50", 8, 960, 1280) and precision == "f16x3" and mode == "train" \
         and B == 32
     tag = None
@@ -587,6 +593,8 @@ def main():
         if dist:
             torch.distributed.destroy_process_group()
         return
+    if args.stage_precision and precision != "f16":
+        raise SystemExit("bench.py: --stage-precision plans the plain-fp16 network (--precision f16)")
     dtype = {"fp32": "f32", "f16x3": "f32 (f16x3 split-precision MFMA, fp32-accurate)", "f16": "f16",
              "f16x2w": "f32 activations x f16 weights (2 fp16 MFMA products)",
              "f16x2a": "f16-rounded activations x split weights (2 fp16 MFMA products)"}[precision]
@@ -598,9 +606,10 @@ def main():
         "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None, "dtype": dtype, "data": "synthetic (seeded uint8 BGR images; random-init weights)",
         "config": {"workload": "%s: %s-8s K=%d %dx%d %s batch %d/GPU (%s)" % (
-            workload_name(args.mode, args.backbone, args.keypoints, args.height, args.width, precision, B,
-                          args.global_batch, world),
-            args.backbone, args.keypoints, args.width, args.height, precision,
+            workload_name(args.mode, args.backbone, args.keypoints, args.height, args.width,
+                          "f16+f16x3 stages" if args.stage_precision else precision, B, args.global_batch, world),
+            args.backbone, args.keypoints, args.width, args.height,
+            precision + (" (stages %s)" % args.stage_precision if args.stage_precision else ""),
             B, "train-mode BN, fused K-ch head, heatmap + argmax, keypoints all-gathered at N>1"
             if args.mode == "infer" else "BCE fp64, Adam lr1e-4 wd1e-4"),
             "mode": args.mode, "backbone": args.backbone, "keypoints": args.keypoints, "height": args.height,
