@@ -16,6 +16,8 @@
 #   c5        C5 training: the plan vs the C planner
 #   h12       the 12x20 halo-staged A3 body: tests and per-conv timing (ran against commit 5d8eaa7;
 #             measured slower and removed with it: profiles/r06_h12_*)
+#   bnr/bnrt  BN backward reduce with batched row loads: tests, C3 old vs new build, traces
+#             (measured slower when sharing CUs with the wgrad; not kept: profiles/r06_bnr_*)
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -143,6 +145,24 @@ h12)
     echo "pytest: $(tail -1 $O/pytest_prec.log)"
     timeout -k 10 500 python -u tools/conv_ab.py --tiles 0,11,17 --rounds 7 --iters 10 \
         --shapes c2_l3,c2_l3a,c4_l3_c2,t3 > $O/conv_ab.log 2>&1
+    ;;
+bnr)
+    # the BN backward reduce with its rows' loads batched (8 in flight per thread):
+    # the backward tests, then the C3 training bench line of the previous build
+    # (tools/ab_lib/libhulkkp_base.so) against this one in alternating processes
+    timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu \
+        -k "backward or bwd or train or syncbn or c3 or grad" > $O/pytest_bwd.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_bwd.log)"
+    for i in 1 2; do
+        timeout -k 10 300 python -u bench.py --mode train --no-extras --no-cpu-baseline \
+            --lib tools/ab_lib/libhulkkp_base.so > $O/bench_base_$i.log 2>&1
+        timeout -k 10 300 python -u bench.py --mode train --no-extras --no-cpu-baseline > $O/bench_new_$i.log 2>&1
+    done
+    ;;
+bnrt)
+    # kernel traces of the C3 step, previous build vs this one (BN backward reduce)
+    trace train_new "--mode train --steps 5 --warmup 2"
+    trace train_base "--mode train --steps 5 --warmup 2 --lib tools/ab_lib/libhulkkp_base.so"
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
