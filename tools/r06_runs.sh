@@ -18,6 +18,8 @@
 #             measured slower and removed with it: profiles/r06_h12_*)
 #   bnr/bnrt  BN backward reduce with batched row loads: tests, C3 old vs new build, traces
 #             (measured slower when sharing CUs with the wgrad; not kept: profiles/r06_bnr_*)
+#   wab       the overlapped wgrad behind the next BN backward: C3 A/B (ran with a Policy field
+#             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -163,6 +165,12 @@ bnrt)
     # kernel traces of the C3 step, previous build vs this one (BN backward reduce)
     trace train_new "--mode train --steps 5 --warmup 2"
     trace train_base "--mode train --steps 5 --warmup 2 --lib tools/ab_lib/libhulkkp_base.so"
+    ;;
+wab)
+    # the overlapped wgrad launched behind the next BN backward (Policy.wgrad_after_bn)
+    timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_after_bn=1" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
+    timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu \
+        -k "backward or bwd or train or c3 or grad" > $O/pytest_bwd.log 2>&1
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
