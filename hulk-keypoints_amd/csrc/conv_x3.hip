@@ -2862,8 +2862,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
                 step(t, x0, x1);
                 step(t + 1, x1, x0);
             }
+            // the x fragments' reads retire before the join's register copies read
+            // them (asm reads are untracked; tools/trcheck.py)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
             if (t + 1 < nsteps) {
                 step(t, x0, x1);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
                 x0 = x1;                                     // one last() call site
             }
             last(x0);
@@ -2966,6 +2972,302 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
     }
 }
 
+// Weight gradient of a 3x3, stride-1, pad-1, dilation-1 conv from one staged halo
+// (round 6; the small-channel layers).  The tiled body above stages a pixel's x
+// line once per 256-column group — for C = 64 three groups, the third 1/4 used —
+// so its K-step moves 40 KiB per 64x256 tile and runs at MFMA busy 0.25.  Here a
+// block owns 64 output channels x all 9 taps x 64 input channels (576 slab
+// columns); a K-step is 32 output pixels = two 16-pixel row segments (Wo % 16 ==
+// 0), each staged as 3 input rows x 18 columns x 2 channel groups (every tap of
+// the segment reads from it) beside the segments' dy lines: 35 KiB for 2.25x the
+// tiled body's MACs.  16x16x32 MFMAs: wave w owns K rows 32*(w&1).. (2 m-tiles) x
+// input channels 16*(w>>1).. of every tap (9 n-tiles, 72 accumulators); the x
+// fragment of tap (r, s) is staged row r read s lines further.  Both operands
+// come from ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).
+// Swizzle: 16-B chunk ^= 2*(((j>>1)&1) | ((j>>3)&1)<<1) for line j of a run, so
+// the 8 lines a 32-lane half of a transposed read touches ({a..a+3} u
+// {a+8..a+11}, any shift a) fall on 8 distinct 32-B bank slots.  4-stage ring,
+// one barrier per K-step; slabs [split][K][R*S*C] as wgrad_x3_kernel's (same
+// reduce).
+constexpr int WGH_LX = 18, WGH_XL = 12 * WGH_LX, WGH_SL = WGH_XL + 64, WGH_STAGE = WGH_SL * 128, WGH_NS = 4;
+constexpr int WGH_PITCH = 580;                       // epilogue rows: 576 slab columns + 4 (conflict-free stores)
+__global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
+    constexpr int ROW = 128, LX = WGH_LX, XL = WGH_XL, STAGE = WGH_STAGE, NS = WGH_NS;
+    // DMA pieces per stage: XP x pieces as slots 0-3 of the 8 waves (piece w + 8 i;
+    // past XP the sink), the 8 dy pieces as slot 4 (piece w)
+    constexpr int XP = XL / 8, XS = 4, SLOTS = XS + 1;
+    static_assert(XP <= 8 * XS, "x pieces");
+    constexpr int SINK = NS * STAGE;
+    static_assert(XL % 8 == 0 && 32 * WGH_PITCH * 4 <= SINK, "wgrad halo LDS");
+    __shared__ __attribute__((aligned(1024))) char smem[SINK + 1024];
+
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);       // same pixel range → same XCD
+    const int split = bid / a.tiles, tile = bid - split * a.tiles;
+    const int kt = tile / a.r_tiles, ct = tile - kt * a.r_tiles;
+    const int k0 = kt * 64, c0 = ct * 64;
+    const int p_begin = split * a.mps;
+    const int p_end = min(a.M, p_begin + a.mps);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto xsw = [](int j) { return (((j >> 1) & 1) | (((j >> 3) & 1) << 1)) << 1; };
+
+    // ---- DMA sources: raw-buffer loads (an offset past num_records loads zeros:
+    // halo lines outside the image, pixels past the range, the sink pieces; the
+    // operands are under 2 GiB, wg_halo_shape, so bit 31 marks them).
+    // Stride 1, pad 1: the input pixel of halo line (segment sg, filter row r,
+    // column j) of the stage at output pixel p0 is p0 + 16 sg + (r - 1) W + j - 1,
+    // so a lane's byte offset is the stage's p0 * 4C plus a constant ----
+    const i32x4 xr = buffer_rsrc(a.xs, (unsigned)((long)a.N * a.H * a.W * a.C * 4));
+    const i32x4 dr = buffer_rsrc(a.dys, (unsigned)((long)a.M * a.K * 4));
+    int xk[XS];                 // byte offset from the stage's p0 * 4C (signed)
+    int xg[XS];                 // segment | filter row << 1 | left-edge line << 3 | right-edge line << 4
+#pragma unroll
+    for (int i = 0; i < XS; ++i) {
+        const int pc = min(w + 8 * i, XP - 1);               // past XP: a valid line, loaded into the sink
+        const int L = 8 * pc + (lane >> 3), run = L / LX, j = L - run * LX;
+        const int seg = run / 6, r = (run >> 1) % 3, cg = run & 1;
+        xk[i] = (16 * seg + (r - 1) * a.W + j - 1) * (a.C * 4) + ((c0 / 32 + cg) * 64 + ((lane & 7) ^ xsw(j)) * 8) * 2;
+        xg[i] = seg | (r << 1) | ((j == 0) << 3) | ((j == LX - 1) << 4);
+    }
+    int dk;                     // dy: byte offset from the stage's p0 * 4K; dpx: pixel in the K-step
+    const int dpx = (8 * w + (lane >> 3)) & 31;
+    dk = dpx * (a.K * 4) + ((k0 / 32 + ((8 * w + (lane >> 3)) >> 5)) * 64 + ((lane & 7) ^ xsw(dpx)) * 8) * 2;
+    // output position (row, column) of the issue stage's first segment, advanced 32 pixels per issue
+    const int hw = a.Ho * a.Wo;
+    int g_ho, g_wo;
+    {
+        const int rem = p_begin - (p_begin / hw) * hw;
+        g_ho = rem / a.Wo;
+        g_wo = rem - g_ho * a.Wo;
+    }
+    // the stage being issued: index and first pixel; its segments' rows, edge
+    // flags and validity (wave-uniform)
+    int q_t = 0, q_p0 = p_begin, ho0 = 0, ho1 = 0, ed0 = 0, ed1 = 0, v0 = 0, v1 = 0;
+    auto begin_issue = [&]() {
+        int ho = g_ho, wo = g_wo + 16;                       // the second segment (Wo % 16 == 0)
+        if (wo == a.Wo) {
+            wo = 0;
+            ho = ho + 1 == a.Ho ? 0 : ho + 1;
+        }
+        ho0 = g_ho;
+        ho1 = ho;
+        ed0 = (g_wo == 0 ? 1 : 0) | (g_wo + 16 == a.Wo ? 2 : 0);
+        ed1 = (wo == 0 ? 1 : 0) | (wo + 16 == a.Wo ? 2 : 0);
+        v0 = q_p0 < p_end;
+        v1 = q_p0 + 16 < p_end;
+    };
+    auto piece = [&](const int i) {
+        char* st = smem + (q_t & (NS - 1)) * STAGE;
+        if (i < XS) {
+            const int pc = w + 8 * i;                        // wave-uniform
+            // branch-free: an invalid line gets bit 31 (past num_records) or'd in
+            const int g = xg[i], sg = g & 1, r = (g >> 1) & 3;
+            const int ho = sg ? ho1 : ho0, ed = sg ? ed1 : ed0, vs = sg ? v1 : v0;
+            const unsigned bad = (unsigned)(vs ^ 1) | (unsigned)((unsigned)(ho + r - 1) >= (unsigned)a.H) |
+                                 (unsigned)(((g >> 3) & ed) != 0) | (unsigned)(pc >= XP);
+            blds16(xr, (unsigned)(q_p0 * (a.C * 4) + xk[i]) | (bad << 31), 0, pc < XP ? st + pc * 1024 : smem + SINK);
+        } else {
+            const unsigned bad = (unsigned)(q_p0 + dpx >= p_end);
+            blds16(dr, (unsigned)(q_p0 * (a.K * 4) + dk) | (bad << 31), 0, st + XL * ROW + w * 1024);
+        }
+    };
+    auto end_issue = [&]() {                                 // the next stage: 32 pixels on
+        ++q_t;
+        q_p0 += 32;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            g_wo += 16;
+            if (g_wo == a.Wo) {
+                g_wo = 0;
+                g_ho = g_ho + 1 == a.Ho ? 0 : g_ho + 1;
+            }
+        }
+    };
+    auto issue = [&]() {
+        begin_issue();
+#pragma unroll
+        for (int i = 0; i < SLOTS; ++i) piece(i);
+        end_issue();
+    };
+
+    f32x4 acc[2][9];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // ---- transposed-read addresses (stage-relative bytes): 16-lane group G reads
+    // pixels 8G + q (+4 the second read) of 16 channels; lane 4q + pp supplies
+    // row q, channels 4pp..4pp+3 ----
+    const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+    const int kh = w & 1, cb4 = w >> 1, cg = cb4 >> 1, cbl = cb4 & 1;
+    unsigned a_ad[2][2];        // dy: [m-tile][plane]; line 8G + q of the wave's K group (+4: same swizzle)
+    {
+        const int j = 8 * G + q;
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+                a_ad[mi][pl] = (unsigned)((XL + 32 * kh + j) * ROW + ((((pl * 4 + mi * 2 + (pp >> 1)) ^ xsw(j))) << 4) +
+                                          8 * (pp & 1));
+    }
+    unsigned b_ad[3][2][2];     // x: [tap column s][read half][plane], filter row 0 (row r: + r * 2 * LX lines)
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+            const int j = 8 * (G & 1) + q + s + 4 * h2;
+            const int run = (G >> 1) * 6 + cg;
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+                b_ad[s][h2][pl] = (unsigned)((run * LX + j) * ROW + ((((pl * 4 + cbl * 2 + (pp >> 1)) ^ xsw(j))) << 4) +
+                                             8 * (pp & 1));
+        }
+    const unsigned lds0 = lds_addr_of(smem);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) a_ad[mi][pl] += lds0;
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl) b_ad[s][h2][pl] += lds0;
+
+    // Per K-step t (stage t in LDS): taps 0-6 with each tap's x fragments read two
+    // taps ahead; then the step's one barrier (stage t+1 landed everywhere, stage
+    // t-1 read by everyone), stage t+1's dy and first x fragments read beside taps
+    // 7-8, and stage t+NS-1's DMA pieces (into stage t-1's buffer) issued between
+    // them — so the barrier and the next stage's first LDS latency sit behind
+    // this wave's own MFMAs.  lgkmcnt counts this wave's transposed reads in
+    // issue order (at most 15 outstanding: the waits below are 8 and 12).
+    const int nsteps = (p_end - p_begin + 31) / 32;
+    f16x8 dfa[2][2], dfb[2][2], xfr[3][2];
+    auto read_d = [&](f16x8 (&d)[2][2], const unsigned so) {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+            for (int pl = 0; pl < 2; ++pl)
+                d[mi][pl] = cat_tr(ds_tr16<0>(a_ad[mi][pl] + so), ds_tr16<4 * ROW>(a_ad[mi][pl] + so));
+    };
+    auto read_x = [&](const int tap, const unsigned so) {
+        const int r = tap / 3, s = tap - 3 * (tap / 3);
+#pragma unroll
+        for (int pl = 0; pl < 2; ++pl) {
+            const unsigned r0 = b_ad[s][0][pl] + so + r * 2 * LX * ROW, r1 = b_ad[s][1][pl] + so + r * 2 * LX * ROW;
+            xfr[tap % 3][pl] = cat_tr(ds_tr16<0>(r0), ds_tr16<0>(r1));
+        }
+    };
+    auto mfma_tap = [&](const f16x8 (&d)[2][2], const int tap) {
+        const f16x8* xf = xfr[tap % 3];
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+            acc[mi][tap] = __builtin_amdgcn_mfma_f32_16x16x32_f16(d[mi][0], xf[0], acc[mi][tap], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+            acc[mi][tap] = __builtin_amdgcn_mfma_f32_16x16x32_f16(d[mi][0], xf[1], acc[mi][tap], 0, 0, 0);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+            acc[mi][tap] = __builtin_amdgcn_mfma_f32_16x16x32_f16(d[mi][1], xf[0], acc[mi][tap], 0, 0, 0);
+    };
+    if (nsteps > 0) {
+#pragma unroll
+        for (int u = 0; u < NS - 1; ++u) issue();           // stages past the end: zero lines, never read
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * SLOTS) : "memory");
+        lds_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        read_d(dfa, 0u);
+        read_x(0, 0u);
+        read_x(1, 0u);
+        unsigned so = 0;
+        // next: stage t+1 exists.  The last step issues no reads of a stage after it:
+        // an asm read whose result is never used leaves its registers free to the
+        // compiler while the read is still in flight (it would land on whatever the
+        // compiler put there — here the DMA addresses of the same step)
+        auto step = [&](f16x8 (&dc)[2][2], f16x8 (&dn)[2][2], const bool next) {
+            const unsigned sn = so == (unsigned)((NS - 1) * STAGE) ? 0u : so + STAGE;
+#pragma unroll
+            for (int tap = 0; tap < 7; ++tap) {
+                read_x(tap + 2, so);
+                asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");      // tap's x (and at tap 0 the dy) landed
+                __builtin_amdgcn_sched_barrier(0);
+                mfma_tap(dc, tap);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 3) * SLOTS) : "memory");
+            lds_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (next) {
+                read_d(dn, sn);
+                asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");     // x of tap 7
+            } else {
+                asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_tap(dc, 7);
+            __builtin_amdgcn_sched_barrier(0);
+            if (next) read_x(0, sn);
+            begin_issue();
+            piece(0);
+            piece(1);
+            piece(2);
+            if (next) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");   // x of tap 8
+            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_tap(dc, 8);
+            __builtin_amdgcn_sched_barrier(0);
+            if (next) read_x(1, sn);
+#pragma unroll
+            for (int i = 3; i < SLOTS; ++i) piece(i);
+            end_issue();
+            __builtin_amdgcn_sched_barrier(0);
+            so = sn;
+        };
+        int t = 0;
+        for (; t + 2 < nsteps; t += 2) {
+            step(dfa, dfb, true);
+            step(dfb, dfa, true);
+        }
+        if (t + 1 < nsteps) {
+            step(dfa, dfb, true);
+            step(dfb, dfa, false);
+        } else {
+            step(dfa, dfb, false);
+        }
+    }
+
+    // ---- epilogue: the 64 x 576 slab tile through the drained ring in two passes
+    // of 32 K rows (one per wave row), stored as 16-B row chunks ----
+    const float inv = 1.f / pow2_scale_for(a.amax);
+    float* out = a.ws + (long)split * a.K * a.RSC;
+    float* T = (float*)smem;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // + the DMAs past the end
+    lds_barrier();
+#pragma unroll
+    for (int ps = 0; ps < 2; ++ps) {
+        if (kh == ps) {
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        T[(16 * mi + 4 * G + e) * WGH_PITCH + tap * 64 + 16 * cb4 + (lane & 15)] = acc[mi][tap][e] * inv;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lds_barrier();
+        for (int e = tid; e < 32 * 144; e += 512) {
+            const int row = e / 144, c4 = e - row * 144, tap = c4 >> 4, cc = (c4 & 15) * 4;
+            *(f32x4*)(out + (long)(k0 + 32 * ps + row) * a.RSC + tap * a.C + c0 + cc) =
+                *(const f32x4*)(T + row * WGH_PITCH + tap * 64 + cc);
+        }
+        if (ps == 0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lds_barrier();
+        }
+    }
+}
 
 // dw[i] = sum_split ws[split][i], fixed order
 // Sum of the split-K slabs [splits][n4] (fixed order, deterministic).  G = 1: a
@@ -3022,7 +3324,30 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
     }
 }
 
+// wgrad_x3_halo_kernel's shapes: 3x3, stride 1, pad = dilation = 1, C and K
+// multiples of 64 up to 128 (the layers it was measured on), whole 16-pixel row
+// segments, operands under 2 GiB (32-bit byte offsets); d->tile == -1 keeps the
+// tiled body (A/B, tests)
+static bool wg_halo_shape(const hkp_conv_desc* d, int ho, int wo) {
+    return d->tile != -1 && d->r == 3 && d->s == 3 && d->stride == 1 && d->pad == 1 && d->dilation == 1 &&
+           d->k % 64 == 0 && d->c % 64 == 0 && d->k <= 128 && d->c <= 128 && wo % 16 == 0 && ho == d->h &&
+           wo == d->w && (long)d->n * d->h * d->w * d->c * 4 < (1L << 31) && (long)d->n * ho * wo * d->k * 4 < (1L << 31);
+}
+
+// ka = 0: the halo body (r_tiles = its 64-channel column tiles)
 static void wg_x3_plan(const hkp_conv_desc* d, long M, int wo, int* splits, int* mps, int* ka, int* r_tiles) {
+    if (wg_halo_shape(d, (int)(M / ((long)d->n * wo)), wo)) {
+        const long tiles = (long)(d->k / 64) * (d->c / 64), nsl = (M + 31) / 32;
+        // one 144 KiB block per CU: one round of 256, or the caller's CU budget
+        long sp = std::max(1L, (d->tile > 0 ? d->tile : 256) / tiles);
+        sp = std::min(sp, nsl);
+        const long per = (nsl + sp - 1) / sp;
+        *ka = 0;
+        *r_tiles = d->c / 64;
+        *mps = (int)(per * 32);
+        *splits = (int)((M + per * 32 - 1) / (per * 32));
+        return;
+    }
     // KA 256's 16-pixel stages advance each x slot with at most one row wrap
     // (and 32-bit byte offsets into both operands)
     const bool ka256 = d->k % 256 == 0 && wo >= 16 && (long)d->n * d->h * d->w * d->c * 4 < (1L << 32) &&
@@ -3837,10 +4162,11 @@ extern "C" int hkp_conv2d_bwd_filter_x3(const hkp_conv_desc* d, const uint16_t* 
     a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.K = d->k; a.R = d->r; a.S = d->s;
     a.stride = d->stride; a.pad = d->pad; a.dil = d->dilation; a.Ho = ho; a.Wo = wo;
     a.M = (int)M; a.RSC = d->r * d->s * d->c; a.r_tiles = rt; a.mps = mps;
-    a.tiles = (d->k / ka) * rt;
+    a.tiles = (d->k / (ka ? ka : 64)) * rt;
     hipStream_t st = as_stream(stream);
     const unsigned grid = (unsigned)(a.tiles * sp);
-    if (ka == 256) hipLaunchKernelGGL(wgrad_x3_kernel<256>, dim3(grid), dim3(512), 0, st, a);
+    if (ka == 0) hipLaunchKernelGGL(wgrad_x3_halo_kernel, dim3(grid), dim3(512), 0, st, a);
+    else if (ka == 256) hipLaunchKernelGGL(wgrad_x3_kernel<256>, dim3(grid), dim3(512), 0, st, a);
     else if (ka == 128) hipLaunchKernelGGL(wgrad_x3_kernel<128>, dim3(grid), dim3(512), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<64>, dim3(grid), dim3(512), 0, st, a);
     HKP_LAUNCH_CHECK("hkp_conv2d_bwd_filter_x3");
@@ -4027,6 +4353,7 @@ extern "C" int32_t hkp_conv_kernel_name(const hkp_conv_desc* d, int32_t op, int3
             HKP_CHECK_ARG(d->k % 64 == 0, "hkp_conv_kernel_name: wgrad needs Cout%%64==0");
             int sp, mps, ka, rt;
             wg_x3_plan(d, (long)d->n * ho * wo, wo, &sp, &mps, &ka, &rt);
+            if (ka == 0) return snprintf(buf, len, "wgrad_x3_halo_kernel");
             return snprintf(buf, len, "wgrad_x3_kernel<%d>", ka);
         }
         default:

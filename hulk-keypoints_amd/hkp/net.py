@@ -693,7 +693,8 @@ def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
             side.wait_stream(main)                     # dy split (and x split) written
             with torch.cuda.stream(side):
                 dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax,
-                                              alloc_stream=main, cus=pol.wgrad_overlap_cus)
+                                              alloc_stream=main,
+                                              cus=pol.wgrad_overlap_cus if pol.wgrad_halo else -1)
                 ready = torch.cuda.Event()
                 ready.record(side)
             for t in (xs[0], dys, amax):              # read on the side stream: keep their memory
@@ -711,7 +712,8 @@ def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
                 dx = ops.conv2d_bwd_data_x3_strided(dys, phs, _act_shape(x), tuple(conv.weight.shape), pd, add=add,
                                                     amax=amax, sk=not ov)
         if ready is None:
-            dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax)
+            dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax,
+                                          cus=0 if pol.wgrad_halo else -1)
         grads.put(conv.weight, dw, ready, side if ready is not None else None)
         return dx
     # exact fp32 kernels (precision fp32, or shapes the x3 kernels do not take)

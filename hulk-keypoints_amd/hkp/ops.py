@@ -1008,7 +1008,8 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=
 def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, alloc_stream=None, cus=0):
     """f16x3 dL/dw (KRSC) from packed x (forward operand) and packed dy (split_pack_x3 with `amax`).
     cus: the CUs the grid should occupy (pixel-range splits = max(1, cus / tiles);
-    0: the planner's count, filling whole rounds of every CU).
+    0: the planner's count, filling whole rounds of every CU; -1: the planner's
+    count on the tiled body — the halo body of 3x3 stride-1 convs off).
     alloc_stream: take dw and the workspace from that stream's memory pool (marked
     as used by the launching stream) — a side-stream wgrad then shares the main
     stream's cached blocks instead of growing a second pool (C5 at 245 GB: the

@@ -53,6 +53,9 @@ class Policy:
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
     wgrad_overlap_cus: int = 0
+    # the halo wgrad body for the 3x3 stride-1 convs of <= 128 channels (the
+    # library's planner choice); False keeps the tiled body (A/B)
+    wgrad_halo: bool = True
     # inner BN ReLU masks recomputed from y in the backward (no fp32 activation kept)
     mask_from_y: bool = True
     # inference: last block's BN apply fused with the K-row head

@@ -175,7 +175,17 @@ def test_kernel_name_query():
     d.tile = _lib.HKP_TILE_256
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_kernel<256, false, false, 16, false, 3>"
     assert ops.kernel_name(d, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_kernel<256>"
-    d.tile = _lib.HKP_TILE_AUTO_A3                                   # AUTO without the DUO choices
+    # the C3 shard's layer1 / layer2 3x3 wgrads: the halo body; tile -1 keeps the tiled one
+    for c, h, w in ((64, 120, 160), (128, 60, 80)):
+        dw = _lib.ConvDesc(8, h, w, c, c, 3, 3, 1, 1, 1, 0)
+        assert ops.kernel_name(dw, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_halo_kernel"
+        dw.tile = -1
+        assert ops.kernel_name(dw, _lib.HKP_KOP_WGRAD_X3) == "wgrad_x3_kernel<%d>" % (64 if c == 64 else 128)
+    # stride 2 / dilation 2 / Wo % 16 != 0: the tiled body
+    for dw in (_lib.ConvDesc(8, 120, 160, 64, 128, 3, 3, 2, 1, 1, 0), _lib.ConvDesc(8, 60, 80, 128, 128, 3, 3, 1, 2, 2, 0),
+               _lib.ConvDesc(2, 17, 23, 64, 64, 3, 3, 1, 1, 1, 0)):
+        assert ops.kernel_name(dw, _lib.HKP_KOP_WGRAD_X3).startswith("wgrad_x3_kernel<")
+    d.tile = _lib.HKP_TILE_AUTO_A3                                  # AUTO without the DUO choices
     assert ops.kernel_name(d, _lib.HKP_KOP_FWD_X3) == "conv_x3_a3_kernel<3>"
     # plain fp16: the DUO body at K-depth 64 and for 128-wide outputs (AUTO), not under AUTO_A3
     l1 = _lib.ConvDesc(128, 120, 160, 64, 256, 1, 1, 1, 0, 1, 0)

@@ -248,7 +248,18 @@ WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (2, 7, 9, 64, 256, 3, 1, 1, 1),         # Cout 256 with Wo = 9 < 16: the KA-128 fallback wraps rows
     (2, 9, 20, 64, 256, 3, 1, 1, 1),        # 256x256 tile, Wo = 20: 16-pixel stages wrap rows and images
     (2, 96, 128, 64, 64, 3, 1, 1, 1),       # 3 tiles over 24576 pixels: > 16 splits (the 4-wave slab reduce)
+    # the halo body (3x3 stride 1 pad 1, C and K 64 / 128, Wo % 16 == 0)
+    (3, 5, 16, 64, 64, 3, 1, 1, 1),         # Wo = 16: every segment its own row, images wrap; M = 240 (half K-step)
+    (1, 24, 48, 64, 128, 3, 1, 1, 1),       # two K tiles
+    (2, 10, 32, 128, 64, 3, 1, 1, 1),       # two channel tiles
+    (1, 8, 16, 128, 128, 3, 1, 1, 1),       # 4 K-steps: fewer pixel ranges than CUs
 ]
+
+
+def _wg_halo(case):
+    n, h, w, cin, cout, k, st, pad, dil = case
+    return (k == 3 and st == 1 and pad == 1 and dil == 1 and cin % 64 == 0 and cout % 64 == 0 and cin <= 128
+            and cout <= 128 and w % 16 == 0)
 
 
 @pytest.mark.parametrize("case", WG_X3_CASES)
@@ -283,8 +294,15 @@ def test_x3_wgrad_scaled(cuda_device, case, gscale):
         assert e < 2e-6 * max(1.0, (m_px / 4096) ** 0.5), (cus, e)
         # the observer's symbol query takes the wgrad's CU budget in the same field
         from hkp._lib import HKP_KOP_WGRAD_X3, ConvDesc
-        assert ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, cus),
-                               HKP_KOP_WGRAD_X3).startswith("wgrad_x3_kernel<")
+        name = ops.kernel_name(ConvDesc(n, h, w, cin, cout, k, k, st, pad, dil, 0, cus), HKP_KOP_WGRAD_X3)
+        assert name == "wgrad_x3_halo_kernel" if _wg_halo(case) else name.startswith("wgrad_x3_kernel<"), name
+    if _wg_halo(case):
+        # the tiled body on the same operands (tile -1): the same bound; the halo
+        # body run twice: bit-identical (fixed-order slabs)
+        dwt = ops.conv2d_bwd_filter_x3(xs, dys, (cout, k, k, cin), st, pad, dil, amax=amax, cus=-1)
+        e = (dwt.cpu().double().permute(0, 3, 1, 2) - ref).abs().max().item() / ref.abs().max().item()
+        assert e < 2e-6, e
+        assert torch.equal(dw, ops.conv2d_bwd_filter_x3(xs, dys, (cout, k, k, cin), st, pad, dil, amax=amax))
 
 
 @pytest.mark.parametrize("shape", [(2, 3, 50, 70), (3, 3, 33, 41), (1, 1, 20, 26), (2, 3, 480 // 4, 640 // 4)])

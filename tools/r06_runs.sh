@@ -20,6 +20,8 @@
 #             (measured slower when sharing CUs with the wgrad; not kept: profiles/r06_bnr_*)
 #   wab       the overlapped wgrad behind the next BN backward: C3 A/B (ran with a Policy field
 #             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
+#   wgh       the halo wgrad body (3x3 stride-1 layers of <= 128 channels): tests, standalone
+#             timing vs the tiled body, C3 training A/B
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -171,6 +173,15 @@ wab)
     timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_after_bn=1" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu \
         -k "backward or bwd or train or c3 or grad" > $O/pytest_bwd.log 2>&1
+    ;;
+wgh)
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "wgrad" > $O/pytest_wgrad.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_wgrad.log)"
+    timeout -k 10 300 python -u tools/wg_time.py --shapes t1,t2 --variants 0,-1 > $O/wg_time.log 2>&1
+    cat $O/wg_time.log
+    timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_halo=0" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
+    tail -4 $O/ab_train.log
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--lib", default=None, help="another build of libhulkkp.so (A/B)")
+    ap.add_argument("--variants", default="0", help="CU budgets (d->tile) to time per shape: 0 = the planner, "
+                    "-1 = the tiled body (no halo body)")
     args = ap.parse_args()
     if args.lib:
         from hkp import _lib
@@ -50,25 +52,32 @@ def main():
         dys = ops.split_pack_x3(dy, amax)
         del x, dy
 
-        def run():
-            return ops.conv2d_bwd_filter_x3(xs, dys, (co, k, k, ci), st, pd, dl, amax=amax)
+        from hkp._lib import HKP_KOP_WGRAD_X3
+        first = None
+        for v in [int(t) for t in args.variants.split(",")]:
+            def run():
+                return ops.conv2d_bwd_filter_x3(xs, dys, (co, k, k, ci), st, pd, dl, amax=amax, cus=v)
 
-        ref = run()
-        times = []
-        for _ in range(args.rounds):
-            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            s.record()
-            for _ in range(args.iters):
-                run()
-            e.record()
-            torch.cuda.synchronize()
-            times.append(s.elapsed_time(e) / args.iters)
-        times.sort()
-        med = times[len(times) // 2]
-        flops = 2.0 * n * ho * wo * co * ci * k * k * 3
-        print("%-4s wgrad median %.3f ms  min %.3f ms  (%.0f TF/s issued = %.3f of 2.5 PF)  |dw| sum %.6e" % (
-            name, med, times[0], flops / (med * 1e-3) / 1e12, flops / (med * 1e-3) / 2.5e15,
-            ref.double().abs().sum().item()), flush=True)
+            ref = run()
+            first = ref if first is None else first
+            times = []
+            for _ in range(args.rounds):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(args.iters):
+                    run()
+                e.record()
+                torch.cuda.synchronize()
+                times.append(s.elapsed_time(e) / args.iters)
+            times.sort()
+            med = times[len(times) // 2]
+            flops = 2.0 * n * ho * wo * co * ci * k * k * 3
+            d = ops._fwd_desc((n, h, w, ci), (co, k, k, ci), st, pd, dl, "nhwc")
+            d.tile = v
+            rel = ((ref - first).abs().max() / first.abs().max()).item()
+            print("%-4s %-24s median %.4f ms  min %.4f ms  (%.0f TF/s issued = %.3f of 2.5 PF)  vs first %.2e" % (
+                name, ops.kernel_name(d, HKP_KOP_WGRAD_X3), med, times[0], flops / (med * 1e-3) / 1e12,
+                flops / (med * 1e-3) / 2.5e15, rel), flush=True)
 
 
 if __name__ == "__main__":
