@@ -649,6 +649,22 @@ def _side_stream(dev):
     return s
 
 
+_WG_HALO = {}
+
+
+def _wgrad_halo(x_shape, w_shape, st, pd, dl):
+    """Whether the library's wgrad planner runs the halo body for this conv (its
+    own symbol query, cached per shape)."""
+    key = (tuple(x_shape), tuple(w_shape), st, pd, dl)
+    if key not in _WG_HALO:
+        from ._lib import HKP_KOP_WGRAD_X3, ConvDesc
+        n, h, w, c = key[0]
+        k, r, s, _ = key[1]
+        _WG_HALO[key] = ops.kernel_name(ConvDesc(n, h, w, c, k, r, s, st, pd, dl, 0, 0),
+                                        HKP_KOP_WGRAD_X3) == "wgrad_x3_halo_kernel"
+    return _WG_HALO[key]
+
+
 def _x3_conv_backward_ok(conv, pol):
     """conv's backward can run entirely on the packed f16x3 path given a packed x
     (dgrad stride 1, or stride 2 without dilation)."""
@@ -692,9 +708,14 @@ def _conv_backward(conv, x, dy, grads, pol, need_dx=True, add=None):
             main, side = torch.cuda.current_stream(dys.device), _side_stream(dys.device)
             side.wait_stream(main)                     # dy split (and x split) written
             with torch.cuda.stream(side):
+                if not pol.wgrad_halo:
+                    cus = -1
+                elif pol.wgrad_halo_cus and _wgrad_halo(_act_shape(x), conv.weight.shape, st, pd, dl):
+                    cus = pol.wgrad_halo_cus
+                else:
+                    cus = pol.wgrad_overlap_cus
                 dw = ops.conv2d_bwd_filter_x3(xs[0], dys, tuple(conv.weight.shape), st, pd, dl, amax=amax,
-                                              alloc_stream=main,
-                                              cus=pol.wgrad_overlap_cus if pol.wgrad_halo else -1)
+                                              alloc_stream=main, cus=cus)
                 ready = torch.cuda.Event()
                 ready.record(side)
             for t in (xs[0], dys, amax):              # read on the side stream: keep their memory

@@ -52,10 +52,16 @@ class Policy:
     dgrad_overlap_sk: bool = True
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
-    wgrad_overlap_cus: int = 0
+    wgrad_overlap_cus: int = 192
     # the halo wgrad body for the 3x3 stride-1 convs of <= 128 channels (the
     # library's planner choice); False keeps the tiled body (A/B)
     wgrad_halo: bool = True
+    # ... and the CUs an overlapped halo wgrad spreads its pixel ranges over (0:
+    # wgrad_overlap_cus): fewer than all leave CUs to the dgrad it overlaps.  C3
+    # shard, in-process A/B, 9 rounds: 488.3 img/s (192 / 160) vs 481.8 for the
+    # tiled body at 0 / 0 and 485.9 for 192 / 192 (profiles/r06_wgh_ab_train_cus5.log);
+    # C5 77.4 vs 77.0 (halo vs tiled; the budgets neutral there)
+    wgrad_halo_cus: int = 160
     # inner BN ReLU masks recomputed from y in the backward (no fp32 activation kept)
     mask_from_y: bool = True
     # inference: last block's BN apply fused with the K-row head

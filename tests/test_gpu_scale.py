@@ -404,6 +404,7 @@ def test_c3_shard_train_step_sampled_fp64(cuda_device):
     assert m.policy.overlap_wgrad and not net._memory_tight(cuda_device)
     assert "conv_x3_a3_kernel<3>" in syms and "wgrad_x3_kernel<256>" in syms
     assert "conv_x3_a3_160_kernel<3>" in syms and "conv_x3_a3_160x128_kernel<3>" in syms, syms
+    assert "wgrad_x3_halo_kernel" in syms, syms          # layer1 / layer2's stride-1 3x3 wgrads
 
 
 def test_c5_train_step_sampled_fp64(cuda_device):
