@@ -2977,25 +2977,35 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_kernel(WgX3Args a) {
 // line once per 256-column group — for C = 64 three groups, the third 1/4 used —
 // so its K-step moves 40 KiB per 64x256 tile and runs at MFMA busy 0.25.  Here a
 // block owns 64 output channels x all 9 taps x 64 input channels (576 slab
-// columns); a K-step is 32 output pixels = two 16-pixel row segments (Wo % 16 ==
-// 0), each staged as 3 input rows x 18 columns x 2 channel groups (every tap of
-// the segment reads from it) beside the segments' dy lines: 35 KiB for 2.25x the
-// tiled body's MACs.  16x16x32 MFMAs: wave w owns K rows 32*(w&1).. (2 m-tiles) x
-// input channels 16*(w>>1).. of every tap (9 n-tiles, 72 accumulators); the x
-// fragment of tap (r, s) is staged row r read s lines further.  Both operands
-// come from ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).
-// Swizzle: 16-B chunk ^= 2*(((j>>1)&1) | ((j>>3)&1)<<1) for line j of a run, so
-// the 8 lines a 32-lane half of a transposed read touches ({a..a+3} u
-// {a+8..a+11}, any shift a) fall on 8 distinct 32-B bank slots.  4-stage ring,
-// one barrier per K-step; slabs [split][K][R*S*C] as wgrad_x3_kernel's (same
-// reduce).
-constexpr int WGH_LX = 18, WGH_XL = 12 * WGH_LX, WGH_SL = WGH_XL + 64, WGH_STAGE = WGH_SL * 128, WGH_NS = 4;
+// columns); a K-step is one patch of 4 output rows x 16 columns (Ho % 4 == 0,
+// Wo % 16 == 0), staged as its 6 x 18 input halo x 2 channel groups (every tap
+// of every row of the patch reads from it) beside the patch's dy lines: 43 KiB
+// for 64 pixels.  16x16x32 MFMAs over two 32-pixel k-slices (patch rows 0-1,
+// 2-3): wave w owns K rows 32*(w&1).. (2 m-tiles) x input channels 16*(w>>1)..
+// of every tap (9 n-tiles, 72 accumulators); the x fragment of tap (r, s) for
+// patch row i is staged row i + r read s lines further.  Both operands come from
+// ds_read_b64_tr_b16 (8 consecutive pixels of one channel per lane).  Swizzle:
+// 16-B chunk ^= 2*(((j>>1)&1) | ((j>>3)&1)<<1) for line j of a run, so the 8
+// lines a 32-lane half of a transposed read touches ({a..a+3} u {a+8..a+11}, any
+// shift a) fall on 8 distinct 32-B bank slots.  3-stage ring, one barrier per
+// K-step; slabs [split][K][R*S*C] as wgrad_x3_kernel's (same reduce), the pixel
+// ranges whole patches.
+constexpr int WGH_LX = 18, WGH_XL = 12 * WGH_LX, WGH_SL = WGH_XL + 128, WGH_STAGE = WGH_SL * 128, WGH_NS = 3;
 constexpr int WGH_PITCH = 580;                       // epilogue rows: 576 slab columns + 4 (conflict-free stores)
+// s_waitcnt lgkmcnt(N) for a compile-time N (after unrolling)
+__device__ __forceinline__ void wait_lgkm(const int n) {
+    switch (n) {
+        case 0: asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); break;
+        case 4: asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory"); break;
+        case 8: asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory"); break;
+        default: asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory"); break;
+    }
+}
 __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
     constexpr int ROW = 128, LX = WGH_LX, XL = WGH_XL, STAGE = WGH_STAGE, NS = WGH_NS;
     // DMA pieces per stage: XP x pieces as slots 0-3 of the 8 waves (piece w + 8 i;
-    // past XP the sink), the 8 dy pieces as slot 4 (piece w)
-    constexpr int XP = XL / 8, XS = 4, SLOTS = XS + 1;
+    // past XP the sink), the 16 dy pieces as slots 4-5 (piece w + 8 (i - 4))
+    constexpr int XP = XL / 8, XS = 4, SLOTS = XS + 2;
     static_assert(XP <= 8 * XS, "x pieces");
     constexpr int SINK = NS * STAGE;
     static_assert(XL % 8 == 0 && 32 * WGH_PITCH * 4 <= SINK, "wgrad halo LDS");
@@ -3005,82 +3015,70 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
     const int split = bid / a.tiles, tile = bid - split * a.tiles;
     const int kt = tile / a.r_tiles, ct = tile - kt * a.r_tiles;
     const int k0 = kt * 64, c0 = ct * 64;
-    const int p_begin = split * a.mps;
-    const int p_end = min(a.M, p_begin + a.mps);
+    const int HP = a.Ho / 4, WP = a.Wo / 16, npatch = a.N * HP * WP;
+    const int P0 = split * a.mps;                            // this split's patches [P0, P1)
+    const int P1 = min(npatch, P0 + a.mps);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     auto xsw = [](int j) { return (((j >> 1) & 1) | (((j >> 3) & 1) << 1)) << 1; };
 
     // ---- DMA sources: raw-buffer loads (an offset past num_records loads zeros:
-    // halo lines outside the image, pixels past the range, the sink pieces; the
-    // operands are under 2 GiB, wg_halo_shape, so bit 31 marks them).
-    // Stride 1, pad 1: the input pixel of halo line (segment sg, filter row r,
-    // column j) of the stage at output pixel p0 is p0 + 16 sg + (r - 1) W + j - 1,
-    // so a lane's byte offset is the stage's p0 * 4C plus a constant ----
+    // halo lines outside the image, patches past the range, the sink pieces; the
+    // operands are under 2 GiB, wg_halo_shape, so bit 31 marks them).  Stride 1,
+    // pad 1: input pixel of halo line (staged row R, column j) of the patch at
+    // output pixel p (its top-left) is p + (R - 1) W + j - 1, so a lane's byte
+    // offset is the stage's p * 4C plus a constant ----
     const i32x4 xr = buffer_rsrc(a.xs, (unsigned)((long)a.N * a.H * a.W * a.C * 4));
     const i32x4 dr = buffer_rsrc(a.dys, (unsigned)((long)a.M * a.K * 4));
-    int xk[XS];                 // byte offset from the stage's p0 * 4C (signed)
-    int xg[XS];                 // segment | filter row << 1 | left-edge line << 3 | right-edge line << 4
+    int xk[XS];                 // byte offset from the stage's p * 4C (signed)
+    int xg[XS];                 // halo edge of the line: top row | bottom row << 1 | left column << 2 | right << 3
 #pragma unroll
     for (int i = 0; i < XS; ++i) {
         const int pc = min(w + 8 * i, XP - 1);               // past XP: a valid line, loaded into the sink
         const int L = 8 * pc + (lane >> 3), run = L / LX, j = L - run * LX;
-        const int seg = run / 6, r = (run >> 1) % 3, cg = run & 1;
-        xk[i] = (16 * seg + (r - 1) * a.W + j - 1) * (a.C * 4) + ((c0 / 32 + cg) * 64 + ((lane & 7) ^ xsw(j)) * 8) * 2;
-        xg[i] = seg | (r << 1) | ((j == 0) << 3) | ((j == LX - 1) << 4);
+        const int R = run >> 1, cg = run & 1;
+        xk[i] = ((R - 1) * a.W + j - 1) * (a.C * 4) + ((c0 / 32 + cg) * 64 + ((lane & 7) ^ xsw(j)) * 8) * 2;
+        xg[i] = (R == 0 ? 1 : 0) | (R == 5 ? 2 : 0) | (j == 0 ? 4 : 0) | (j == LX - 1 ? 8 : 0);
     }
-    int dk;                     // dy: byte offset from the stage's p0 * 4K; dpx: pixel in the K-step
-    const int dpx = (8 * w + (lane >> 3)) & 31;
-    dk = dpx * (a.K * 4) + ((k0 / 32 + ((8 * w + (lane >> 3)) >> 5)) * 64 + ((lane & 7) ^ xsw(dpx)) * 8) * 2;
-    // output position (row, column) of the issue stage's first segment, advanced 32 pixels per issue
-    const int hw = a.Ho * a.Wo;
-    int g_ho, g_wo;
+    int dk[2];                  // dy: byte offset from the stage's p * 4K (line: K group | patch row | column)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int L = 8 * (w + 8 * i) + (lane >> 3), pr = (L >> 4) & 3, cc = L & 15;
+        dk[i] = (pr * a.W + cc) * (a.K * 4) + ((k0 / 32 + (L >> 6)) * 64 + ((lane & 7) ^ xsw(L & 31)) * 8) * 2;
+    }
+    // the patch being issued: index, top-left output pixel, patch row / column (wave-uniform)
+    int q_P = P0, q_hp, q_wp, q_p;
     {
-        const int rem = p_begin - (p_begin / hw) * hw;
-        g_ho = rem / a.Wo;
-        g_wo = rem - g_ho * a.Wo;
+        const int n = P0 / (HP * WP), rem = P0 - n * (HP * WP);
+        q_hp = rem / WP;
+        q_wp = rem - q_hp * WP;
+        q_p = (n * a.Ho + 4 * q_hp) * a.Wo + 16 * q_wp;
     }
-    // the stage being issued: index and first pixel; its segments' rows, edge
-    // flags and validity (wave-uniform)
-    int q_t = 0, q_p0 = p_begin, ho0 = 0, ho1 = 0, ed0 = 0, ed1 = 0, v0 = 0, v1 = 0;
+    int q_t = 0, q_em = 0, q_bad = 0;
     auto begin_issue = [&]() {
-        int ho = g_ho, wo = g_wo + 16;                       // the second segment (Wo % 16 == 0)
-        if (wo == a.Wo) {
-            wo = 0;
-            ho = ho + 1 == a.Ho ? 0 : ho + 1;
-        }
-        ho0 = g_ho;
-        ho1 = ho;
-        ed0 = (g_wo == 0 ? 1 : 0) | (g_wo + 16 == a.Wo ? 2 : 0);
-        ed1 = (wo == 0 ? 1 : 0) | (wo + 16 == a.Wo ? 2 : 0);
-        v0 = q_p0 < p_end;
-        v1 = q_p0 + 16 < p_end;
+        q_em = (q_hp == 0 ? 1 : 0) | (q_hp == HP - 1 ? 2 : 0) | (q_wp == 0 ? 4 : 0) | (q_wp == WP - 1 ? 8 : 0);
+        q_bad = q_P >= P1 ? 1 : 0;
     };
     auto piece = [&](const int i) {
-        char* st = smem + (q_t & (NS - 1)) * STAGE;
+        char* st = smem + (q_t % NS) * STAGE;
         if (i < XS) {
-            const int pc = w + 8 * i;                        // wave-uniform
             // branch-free: an invalid line gets bit 31 (past num_records) or'd in
-            const int g = xg[i], sg = g & 1, r = (g >> 1) & 3;
-            const int ho = sg ? ho1 : ho0, ed = sg ? ed1 : ed0, vs = sg ? v1 : v0;
-            const unsigned bad = (unsigned)(vs ^ 1) | (unsigned)((unsigned)(ho + r - 1) >= (unsigned)a.H) |
-                                 (unsigned)(((g >> 3) & ed) != 0) | (unsigned)(pc >= XP);
-            blds16(xr, (unsigned)(q_p0 * (a.C * 4) + xk[i]) | (bad << 31), 0, pc < XP ? st + pc * 1024 : smem + SINK);
+            const int pc = w + 8 * i;                        // wave-uniform
+            const unsigned bad = (unsigned)q_bad | (unsigned)((xg[i] & q_em) != 0) | (unsigned)(pc >= XP);
+            blds16(xr, (unsigned)(q_p * (a.C * 4) + xk[i]) | (bad << 31), 0, pc < XP ? st + pc * 1024 : smem + SINK);
         } else {
-            const unsigned bad = (unsigned)(q_p0 + dpx >= p_end);
-            blds16(dr, (unsigned)(q_p0 * (a.K * 4) + dk) | (bad << 31), 0, st + XL * ROW + w * 1024);
+            blds16(dr, (unsigned)(q_p * (a.K * 4) + dk[i - XS]) | ((unsigned)q_bad << 31), 0,
+                   st + XL * ROW + (w + 8 * (i - XS)) * 1024);
         }
     };
-    auto end_issue = [&]() {                                 // the next stage: 32 pixels on
+    auto end_issue = [&]() {                                 // the next patch
         ++q_t;
-        q_p0 += 32;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            g_wo += 16;
-            if (g_wo == a.Wo) {
-                g_wo = 0;
-                g_ho = g_ho + 1 == a.Ho ? 0 : g_ho + 1;
-            }
+        ++q_P;
+        q_p += 16;
+        if (++q_wp == WP) {
+            q_wp = 0;
+            q_p += 3 * a.Wo;
+            q_hp = q_hp + 1 == HP ? 0 : q_hp + 1;
         }
     };
     auto issue = [&]() {
@@ -3096,9 +3094,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
 #pragma unroll
         for (int t = 0; t < 9; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // ---- transposed-read addresses (stage-relative bytes): 16-lane group G reads
-    // pixels 8G + q (+4 the second read) of 16 channels; lane 4q + pp supplies
-    // row q, channels 4pp..4pp+3 ----
+    // ---- transposed-read addresses (stage-relative bytes, k-slice 0): 16-lane
+    // group G reads patch row G >> 1 (+2 in k-slice 1), pixels 8 (G & 1) + q (+4 the
+    // second read) of 16 channels; lane 4q + pp supplies row q, channels 4pp..4pp+3 ----
     const int G = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
     const int kh = w & 1, cb4 = w >> 1, cg = cb4 >> 1, cbl = cb4 & 1;
     unsigned a_ad[2][2];        // dy: [m-tile][plane]; line 8G + q of the wave's K group (+4: same swizzle)
@@ -3108,16 +3106,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
         for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
-                a_ad[mi][pl] = (unsigned)((XL + 32 * kh + j) * ROW + ((((pl * 4 + mi * 2 + (pp >> 1)) ^ xsw(j))) << 4) +
+                a_ad[mi][pl] = (unsigned)((XL + 64 * kh + j) * ROW + ((((pl * 4 + mi * 2 + (pp >> 1)) ^ xsw(j))) << 4) +
                                           8 * (pp & 1));
     }
-    unsigned b_ad[3][2][2];     // x: [tap column s][read half][plane], filter row 0 (row r: + r * 2 * LX lines)
+    unsigned b_ad[3][2][2];     // x: [tap column s][read half][plane], staged row G >> 1 (+ k-slice * 2 + r)
 #pragma unroll
     for (int s = 0; s < 3; ++s)
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
             const int j = 8 * (G & 1) + q + s + 4 * h2;
-            const int run = (G >> 1) * 6 + cg;
+            const int run = (G >> 1) * 2 + cg;
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl)
                 b_ad[s][h2][pl] = (unsigned)((run * LX + j) * ROW + ((((pl * 4 + cbl * 2 + (pp >> 1)) ^ xsw(j))) << 4) +
@@ -3135,32 +3133,33 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
 #pragma unroll
             for (int pl = 0; pl < 2; ++pl) b_ad[s][h2][pl] += lds0;
 
-    // Per K-step t (stage t in LDS): taps 0-6 with each tap's x fragments read two
-    // taps ahead; then the step's one barrier (stage t+1 landed everywhere, stage
-    // t-1 read by everyone), stage t+1's dy and first x fragments read beside taps
-    // 7-8, and stage t+NS-1's DMA pieces (into stage t-1's buffer) issued between
-    // them — so the barrier and the next stage's first LDS latency sit behind
-    // this wave's own MFMAs.  lgkmcnt counts this wave's transposed reads in
-    // issue order (at most 15 outstanding: the waits below are 8 and 12).
-    const int nsteps = (p_end - p_begin + 31) / 32;
+    // Per K-step t (stage t in LDS): 18 tap-slices v = 9 * k-slice + tap, each's x
+    // fragments read two ahead, k-slice 1's dy fragments in two halves at v = 3 and
+    // 6; after v = 15 the step's one barrier (stage t+1 landed everywhere, stage
+    // t-1 read by everyone), then stage t+1's k-slice-0 dy and first x fragments
+    // read beside v = 16-17, and stage t+NS-1's DMA pieces (into stage t-1's
+    // buffer) issued between them — the barrier and the next stage's first LDS
+    // latency sit behind this wave's own MFMAs.  lgkmcnt counts this wave's
+    // transposed reads in issue order (at most 15 outstanding: waits of 8 and 12).
+    // A step with no stage after it reads none (an asm read whose result is never
+    // used leaves its registers free to the compiler while it is in flight).
+    const int nsteps = P1 - P0;
     f16x8 dfa[2][2], dfb[2][2], xfr[3][2];
-    auto read_d = [&](f16x8 (&d)[2][2], const unsigned so) {
+    auto read_d = [&](f16x8 (&d)[2][2], const int mi, const unsigned so) {
 #pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-            for (int pl = 0; pl < 2; ++pl)
-                d[mi][pl] = cat_tr(ds_tr16<0>(a_ad[mi][pl] + so), ds_tr16<4 * ROW>(a_ad[mi][pl] + so));
+        for (int pl = 0; pl < 2; ++pl)
+            d[mi][pl] = cat_tr(ds_tr16<0>(a_ad[mi][pl] + so), ds_tr16<4 * ROW>(a_ad[mi][pl] + so));
     };
-    auto read_x = [&](const int tap, const unsigned so) {
-        const int r = tap / 3, s = tap - 3 * (tap / 3);
+    auto read_x = [&](const int v, const unsigned so) {
+        const int kk = v / 9, tap = v - 9 * (v / 9), r = tap / 3, s = tap - 3 * (tap / 3);
+        const unsigned ro = so + (unsigned)((2 * kk + r) * 2 * LX * ROW);
 #pragma unroll
-        for (int pl = 0; pl < 2; ++pl) {
-            const unsigned r0 = b_ad[s][0][pl] + so + r * 2 * LX * ROW, r1 = b_ad[s][1][pl] + so + r * 2 * LX * ROW;
-            xfr[tap % 3][pl] = cat_tr(ds_tr16<0>(r0), ds_tr16<0>(r1));
-        }
+        for (int pl = 0; pl < 2; ++pl)
+            xfr[v % 3][pl] = cat_tr(ds_tr16<0>(b_ad[s][0][pl] + ro), ds_tr16<0>(b_ad[s][1][pl] + ro));
     };
-    auto mfma_tap = [&](const f16x8 (&d)[2][2], const int tap) {
-        const f16x8* xf = xfr[tap % 3];
+    auto mfma_v = [&](const f16x8 (&d)[2][2], const int v) {
+        const int tap = v % 9;
+        const f16x8* xf = xfr[v % 3];
 #pragma unroll
         for (int mi = 0; mi < 2; ++mi)
             acc[mi][tap] = __builtin_amdgcn_mfma_f32_16x16x32_f16(d[mi][0], xf[0], acc[mi][tap], 0, 0, 0);
@@ -3177,45 +3176,44 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * SLOTS) : "memory");
         lds_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        read_d(dfa, 0u);
+        read_d(dfa, 0, 0u);
+        read_d(dfa, 1, 0u);
         read_x(0, 0u);
         read_x(1, 0u);
         unsigned so = 0;
-        // next: stage t+1 exists.  The last step issues no reads of a stage after it:
-        // an asm read whose result is never used leaves its registers free to the
-        // compiler while the read is still in flight (it would land on whatever the
-        // compiler put there — here the DMA addresses of the same step)
-        auto step = [&](f16x8 (&dc)[2][2], f16x8 (&dn)[2][2], const bool next) {
+        auto step = [&](const bool next) {
             const unsigned sn = so == (unsigned)((NS - 1) * STAGE) ? 0u : so + STAGE;
 #pragma unroll
-            for (int tap = 0; tap < 7; ++tap) {
-                read_x(tap + 2, so);
-                asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");      // tap's x (and at tap 0 the dy) landed
+            for (int v = 0; v < 16; ++v) {
+                read_x(v + 2, so);
+                if (v == 3) read_d(dfb, 0, so + 32 * ROW);
+                if (v == 6) read_d(dfb, 1, so + 32 * ROW);
+                wait_lgkm(v >= 3 && v <= 8 ? 12 : 8);
                 __builtin_amdgcn_sched_barrier(0);
-                mfma_tap(dc, tap);
+                mfma_v(v < 9 ? dfa : dfb, v);
                 __builtin_amdgcn_sched_barrier(0);
             }
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 3) * SLOTS) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 3) * SLOTS) : "memory");   // stage t+1
             lds_barrier();
             __builtin_amdgcn_sched_barrier(0);
             if (next) {
-                read_d(dn, sn);
-                asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");     // x of tap 7
+                read_d(dfa, 0, sn);
+                read_d(dfa, 1, sn);
+                wait_lgkm(12);                                          // x of v = 16
             } else {
-                asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+                wait_lgkm(4);
             }
             __builtin_amdgcn_sched_barrier(0);
-            mfma_tap(dc, 7);
+            mfma_v(dfb, 16);
             __builtin_amdgcn_sched_barrier(0);
             if (next) read_x(0, sn);
             begin_issue();
             piece(0);
             piece(1);
             piece(2);
-            if (next) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");   // x of tap 8
-            else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            wait_lgkm(next ? 12 : 0);                                   // x of v = 17
             __builtin_amdgcn_sched_barrier(0);
-            mfma_tap(dc, 8);
+            mfma_v(dfb, 17);
             __builtin_amdgcn_sched_barrier(0);
             if (next) read_x(1, sn);
 #pragma unroll
@@ -3224,17 +3222,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_x3_halo_kernel(WgX3Args a) {
             __builtin_amdgcn_sched_barrier(0);
             so = sn;
         };
-        int t = 0;
-        for (; t + 2 < nsteps; t += 2) {
-            step(dfa, dfb, true);
-            step(dfb, dfa, true);
-        }
-        if (t + 1 < nsteps) {
-            step(dfa, dfb, true);
-            step(dfb, dfa, false);
-        } else {
-            step(dfa, dfb, false);
-        }
+        for (int t = 0; t + 1 < nsteps; ++t) step(true);
+        step(false);
     }
 
     // ---- epilogue: the 64 x 576 slab tile through the drained ring in two passes
@@ -3325,27 +3314,28 @@ __global__ __launch_bounds__(256) void wg_x3_reduce_kernel(long n4, int splits, 
 }
 
 // wgrad_x3_halo_kernel's shapes: 3x3, stride 1, pad = dilation = 1, C and K
-// multiples of 64 up to 128 (the layers it was measured on), whole 16-pixel row
-// segments, operands under 2 GiB (32-bit byte offsets); d->tile == -1 keeps the
+// multiples of 64 up to 128 (the layers it was measured on), whole 4x16-pixel
+// patches, operands under 2 GiB (32-bit byte offsets); d->tile == -1 keeps the
 // tiled body (A/B, tests)
 static bool wg_halo_shape(const hkp_conv_desc* d, int ho, int wo) {
     return d->tile != -1 && d->r == 3 && d->s == 3 && d->stride == 1 && d->pad == 1 && d->dilation == 1 &&
-           d->k % 64 == 0 && d->c % 64 == 0 && d->k <= 128 && d->c <= 128 && wo % 16 == 0 && ho == d->h &&
+           d->k % 64 == 0 && d->c % 64 == 0 && d->k <= 128 && d->c <= 128 && wo % 16 == 0 && ho % 4 == 0 &&
+           ho == d->h &&
            wo == d->w && (long)d->n * d->h * d->w * d->c * 4 < (1L << 31) && (long)d->n * ho * wo * d->k * 4 < (1L << 31);
 }
 
-// ka = 0: the halo body (r_tiles = its 64-channel column tiles)
+// ka = 0: the halo body (r_tiles = its 64-channel column tiles, mps = patches per split)
 static void wg_x3_plan(const hkp_conv_desc* d, long M, int wo, int* splits, int* mps, int* ka, int* r_tiles) {
     if (wg_halo_shape(d, (int)(M / ((long)d->n * wo)), wo)) {
-        const long tiles = (long)(d->k / 64) * (d->c / 64), nsl = (M + 31) / 32;
-        // one 144 KiB block per CU: one round of 256, or the caller's CU budget
+        const long tiles = (long)(d->k / 64) * (d->c / 64), np = M / 64;   // 4x16-pixel patches
+        // one 130 KiB block per CU: one round of 256, or the caller's CU budget
         long sp = std::max(1L, (d->tile > 0 ? d->tile : 256) / tiles);
-        sp = std::min(sp, nsl);
-        const long per = (nsl + sp - 1) / sp;
+        sp = std::min(sp, np);
+        const long per = (np + sp - 1) / sp;
         *ka = 0;
         *r_tiles = d->c / 64;
-        *mps = (int)(per * 32);
-        *splits = (int)((M + per * 32 - 1) / (per * 32));
+        *mps = (int)per;                                   // patches per split
+        *splits = (int)((np + per - 1) / per);
         return;
     }
     // KA 256's 16-pixel stages advance each x slot with at most one row wrap

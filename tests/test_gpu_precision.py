@@ -248,18 +248,19 @@ WG_X3_CASES = [c for c in X3_CASES if c[4] % 64 == 0] + [
     (2, 7, 9, 64, 256, 3, 1, 1, 1),         # Cout 256 with Wo = 9 < 16: the KA-128 fallback wraps rows
     (2, 9, 20, 64, 256, 3, 1, 1, 1),        # 256x256 tile, Wo = 20: 16-pixel stages wrap rows and images
     (2, 96, 128, 64, 64, 3, 1, 1, 1),       # 3 tiles over 24576 pixels: > 16 splits (the 4-wave slab reduce)
-    # the halo body (3x3 stride 1 pad 1, C and K 64 / 128, Wo % 16 == 0)
-    (3, 5, 16, 64, 64, 3, 1, 1, 1),         # Wo = 16: every segment its own row, images wrap; M = 240 (half K-step)
+    # the halo body (3x3 stride 1 pad 1, C and K 64 / 128, 4x16-pixel patches)
+    (3, 8, 16, 64, 64, 3, 1, 1, 1),         # Wo = 16: one patch per row band, images wrap
     (1, 24, 48, 64, 128, 3, 1, 1, 1),       # two K tiles
-    (2, 10, 32, 128, 64, 3, 1, 1, 1),       # two channel tiles
-    (1, 8, 16, 128, 128, 3, 1, 1, 1),       # 4 K-steps: fewer pixel ranges than CUs
+    (2, 12, 32, 128, 64, 3, 1, 1, 1),       # two channel tiles
+    (1, 8, 16, 128, 128, 3, 1, 1, 1),       # 2 patches: fewer pixel ranges than CUs
+    (2, 10, 32, 64, 64, 3, 1, 1, 1),        # Ho % 4 != 0: the tiled body
 ]
 
 
 def _wg_halo(case):
     n, h, w, cin, cout, k, st, pad, dil = case
     return (k == 3 and st == 1 and pad == 1 and dil == 1 and cin % 64 == 0 and cout % 64 == 0 and cin <= 128
-            and cout <= 128 and w % 16 == 0)
+            and cout <= 128 and w % 16 == 0 and h % 4 == 0)
 
 
 @pytest.mark.parametrize("case", WG_X3_CASES)

@@ -22,6 +22,7 @@
 #             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
 #   wgh       the halo wgrad body (3x3 stride-1 layers of <= 128 channels): tests, standalone
 #             timing vs the tiled body, C3 training A/B
+#   wghpmc    PMC passes over the standalone halo and tiled wgrads (layer1 shape)
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
 set -e
@@ -182,6 +183,14 @@ wgh)
     cat $O/wg_time.log
     timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_halo=0" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     tail -4 $O/ab_train.log
+    ;;
+wghpmc)
+    # PMC passes over the standalone halo wgrad (layer1 shape) and the tiled body
+    PROG=tools/wg_time.py bash tools/pmc_passes.sh $O/halo "--shapes t1 --variants 0 --rounds 2 --iters 3" \
+        "wgrad_x3_halo" > $O/halo.log 2>&1
+    PROG=tools/wg_time.py bash tools/pmc_passes.sh $O/tiled "--shapes t1 --variants -1 --rounds 2 --iters 3" \
+        "wgrad_x3_kernel" > $O/tiled.log 2>&1
+    cat $O/halo/pmc_summary.txt $O/tiled/pmc_summary.txt
     ;;
 check)
     timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
