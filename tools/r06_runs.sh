@@ -22,6 +22,7 @@
 #             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
 #   wgh       the halo wgrad body (3x3 stride-1 layers of <= 128 channels): tests, standalone
 #             timing vs the tiled body, C3 training A/B
+#   wgh2      a halo wgrad build vs the previous build (tests, timing, C3 bench lines)
 #   wghpmc    PMC passes over the standalone halo and tiled wgrads (layer1 shape)
 #   check     GPU suite + the default bench line
 #   final     GPU suite, smoke(), default bench line
@@ -183,6 +184,27 @@ wgh)
     cat $O/wg_time.log
     timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_halo=0" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     tail -4 $O/ab_train.log
+    ;;
+wgh2)
+    # a halo wgrad build against the previous one (tools/ab_lib/libhulkkp_base.so):
+    # tests, standalone timing per build, C3 training bench lines alternating
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_precision.py \
+        -k "wgrad" > $O/pytest_wgrad.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_wgrad.log)"
+    for i in 1 2; do
+        timeout -k 10 200 python -u tools/wg_time.py --shapes t1,t2 --variants 0 > $O/wg_new_$i.log 2>&1
+        timeout -k 10 200 python -u tools/wg_time.py --shapes t1,t2 --variants 0 --lib tools/ab_lib/libhulkkp_base.so \
+            > $O/wg_base_$i.log 2>&1
+    done
+    grep -h wgrad $O/wg_new_*.log $O/wg_base_*.log
+    for i in 1 2 3; do
+        timeout -k 10 300 python -u bench.py --mode train --no-extras --no-cpu-baseline > $O/train_new_$i.log 2>&1
+        timeout -k 10 300 python -u bench.py --mode train --no-extras --no-cpu-baseline \
+            --lib tools/ab_lib/libhulkkp_base.so > $O/train_base_$i.log 2>&1
+    done
+    for f in $O/train_new_*.log $O/train_base_*.log; do
+        echo "$f $(grep '^{' $f | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["value"])')"
+    done
     ;;
 wghpmc)
     # PMC passes over the standalone halo wgrad (layer1 shape) and the tiled body
