@@ -22,6 +22,7 @@
 #             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
 #   wgh       the halo wgrad body (3x3 stride-1 layers of <= 128 channels): tests, standalone
 #             timing vs the tiled body, C3 training A/B
+#   proftrain the C3 training trace, PMC and bench line after the halo wgrad
 #   wgh2      a halo wgrad build vs the previous build (tests, timing, C3 bench lines)
 #   wghpmc    PMC passes over the standalone halo and tiled wgrads (layer1 shape)
 #   check     GPU suite + the default bench line
@@ -184,6 +185,18 @@ wgh)
     cat $O/wg_time.log
     timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_halo=0" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     tail -4 $O/ab_train.log
+    ;;
+proftrain)
+    # the C3 training step after the halo wgrad / CU budgets: kernel trace (copied into
+    # profiles/ on the box so the bench line after it reads it), PMC passes, bench line
+    trace train "--mode train --steps 5 --warmup 2"
+    cp $O/train_kernel_stats.csv profiles/r06_train_c3_kernel_stats_v3.csv
+    bash tools/pmc_passes.sh $O/pmc_train "--mode train --steps 2 --warmup 1 --no-extras" "." > $O/pmc_train.log 2>&1
+    cp $O/pmc_train/pmc_summary.json profiles/r06_train_c3_pmc_v2.json
+    cp $O/pmc_train/pmc_summary.txt profiles/r06_train_c3_pmc_v2.txt
+    python3 tools/hbm_table.py $O/train_kernel_stats.csv $O/pmc_train/pmc_summary.json --steps 7 --top 40 \
+        > $O/train_hbm_table.txt
+    timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline --no-extras > $O/bench_train.log 2>&1
     ;;
 wgh2)
     # a halo wgrad build against the previous one (tools/ab_lib/libhulkkp_base.so):
