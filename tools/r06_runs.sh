@@ -22,6 +22,7 @@
 #             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
 #   wgh       the halo wgrad body (3x3 stride-1 layers of <= 128 channels): tests, standalone
 #             timing vs the tiled body, C3 training A/B
+#   trainab   this build vs tools/ab_lib/libhulkkp_base.so: backward tests, C3 bench lines
 #   proftrain the C3 training trace, PMC and bench line after the halo wgrad
 #   wgh2      a halo wgrad build vs the previous build (tests, timing, C3 bench lines)
 #   wghpmc    PMC passes over the standalone halo and tiled wgrads (layer1 shape)
@@ -185,6 +186,21 @@ wgh)
     cat $O/wg_time.log
     timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_halo=0" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     tail -4 $O/ab_train.log
+    ;;
+trainab)
+    # this build against tools/ab_lib/libhulkkp_base.so: the backward tests, then C3
+    # training bench lines alternating
+    timeout -k 10 500 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests -m gpu \
+        -k "backward or bwd or train or c3 or grad or dgrad" > $O/pytest_bwd.log 2>&1
+    echo "pytest: $(tail -1 $O/pytest_bwd.log)"
+    for i in 1 2 3 4; do
+        timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline --no-extras > $O/train_new_$i.log 2>&1
+        timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline --no-extras \
+            --lib tools/ab_lib/libhulkkp_base.so > $O/train_base_$i.log 2>&1
+    done
+    for f in $O/train_new_*.log $O/train_base_*.log; do
+        echo "$f $(grep '^{' $f | python3 -c 'import json,sys; print(json.loads(sys.stdin.read())["value"])')"
+    done
     ;;
 proftrain)
     # the C3 training step after the halo wgrad / CU budgets: kernel trace (copied into
