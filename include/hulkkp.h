@@ -463,6 +463,11 @@ int hkp_conv2d_fwd_stem_x3_image(const hkp_conv_desc* d, const void* image, int3
  *                            (0: the planner's split count, which fills whole
  *                            rounds of all CUs; a wgrad sharing the GPU with a
  *                            dgrad may take fewer): splits = max(1, tile / tiles).
+ *                            3x3 stride-1 pad-1 convs with Cin, Cout in {64, 128},
+ *                            Ho % 4 == 0 and Wo % 16 == 0 run the halo body
+ *                            (wgrad_x3_halo_kernel: 64 Cout x 9 taps x 64 Cin per
+ *                            block, 4x16-pixel patches staged once for every tap);
+ *                            tile == -1 keeps the tiled body for them.
  * Replace the same cuDNN backward calls as hkp_conv2d_bwd_data / _filter. */
 int hkp_split_pack_x3(int64_t n, int32_t c, const float* x, const uint32_t* amax_bits, uint16_t* x_split,
                       hkp_stream_t stream);
