@@ -22,6 +22,7 @@
 #             that was not kept: 471 vs 480 img/s, profiles/r06_wgrad_after_bn_ab_train.log)
 #   wgh       the halo wgrad body (3x3 stride-1 layers of <= 128 channels): tests, standalone
 #             timing vs the tiled body, C3 training A/B
+#   gap       C3 traces with the halo wgrads on 64 vs 160 CUs (the cross-stream gaps)
 #   trainab   this build vs tools/ab_lib/libhulkkp_base.so: backward tests, C3 bench lines
 #   proftrain the C3 training trace, PMC and bench line after the halo wgrad
 #   wgh2      a halo wgrad build vs the previous build (tests, timing, C3 bench lines)
@@ -186,6 +187,12 @@ wgh)
     cat $O/wg_time.log
     timeout -k 10 600 python -u tools/train_ab.py "" "wgrad_halo=0" --rounds 7 --iters 10 > $O/ab_train.log 2>&1
     tail -4 $O/ab_train.log
+    ;;
+gap)
+    # the layer1/2 cross-stream gaps: traces of the C3 step with the halo wgrads on 64
+    # CUs (192 left to the dgrad) and on the default 160
+    trace train_h64 "--mode train --steps 5 --warmup 2 --tune wgrad_halo_cus=64"
+    trace train_h160 "--mode train --steps 5 --warmup 2"
     ;;
 trainab)
     # this build against tools/ab_lib/libhulkkp_base.so: the backward tests, then C3
