@@ -46,10 +46,12 @@ class Policy:
     # 464.3 img/s vs 460.9 for 9 = 2-stage 256x256 + split-K tail launch, 453.0 for
     # the planner)
     dgrad_overlap_tile: int = 11
-    # ... with the split-K workspace: the A3 grid runs its last partial round as
-    # split-K segments inside the same launch (in-process A/B, 7 rounds: 455.8 vs
-    # 453.6 img/s as whole tiles)
-    dgrad_overlap_sk: bool = True
+    # ... with the split-K workspace (the A3 grid's last partial round as split-K
+    # segments inside the same launch, stream-K plans for the 64/128-wide dgrads):
+    # measured +0.5 % in round 4, but beside the halo wgrads and the CU budgets
+    # below, without it: 487.7 vs 484.8 and 489.0 vs 485.7 img/s (in-process A/Bs,
+    # 11 / 7 rounds, profiles/r06_gapsk_ab.log, r06_wgh_ab_train_dgsk.log)
+    dgrad_overlap_sk: bool = False
     # CUs a wgrad overlapped by its dgrad spreads its pixel-range splits over
     # (0 = the planner's split count, filling every CU as if it ran alone)
     wgrad_overlap_cus: int = 192

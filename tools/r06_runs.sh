@@ -194,6 +194,12 @@ gap)
     trace train_h64 "--mode train --steps 5 --warmup 2 --tune wgrad_halo_cus=64"
     trace train_h160 "--mode train --steps 5 --warmup 2"
     ;;
+gapsk)
+    # the overlapped dgrads without the stream-K workspace: A/B and a trace
+    timeout -k 10 550 python -u tools/train_ab.py "" "dgrad_overlap_sk=0" --rounds 11 --iters 10 > $O/ab.log 2>&1
+    tail -2 $O/ab.log
+    trace train_nosk "--mode train --steps 5 --warmup 2 --tune dgrad_overlap_sk=0"
+    ;;
 trainab)
     # this build against tools/ab_lib/libhulkkp_base.so: the backward tests, then C3
     # training bench lines alternating
