@@ -219,10 +219,10 @@ proftrain)
     # the C3 training step after the halo wgrad / CU budgets: kernel trace (copied into
     # profiles/ on the box so the bench line after it reads it), PMC passes, bench line
     trace train "--mode train --steps 5 --warmup 2"
-    cp $O/train_kernel_stats.csv profiles/r06_train_c3_kernel_stats_v3.csv
+    cp $O/train_kernel_stats.csv profiles/r06_train_c3_kernel_stats_v4.csv
     bash tools/pmc_passes.sh $O/pmc_train "--mode train --steps 2 --warmup 1 --no-extras" "." > $O/pmc_train.log 2>&1
-    cp $O/pmc_train/pmc_summary.json profiles/r06_train_c3_pmc_v2.json
-    cp $O/pmc_train/pmc_summary.txt profiles/r06_train_c3_pmc_v2.txt
+    cp $O/pmc_train/pmc_summary.json profiles/r06_train_c3_pmc_v3.json
+    cp $O/pmc_train/pmc_summary.txt profiles/r06_train_c3_pmc_v3.txt
     python3 tools/hbm_table.py $O/train_kernel_stats.csv $O/pmc_train/pmc_summary.json --steps 7 --top 40 \
         > $O/train_hbm_table.txt
     timeout -k 10 300 python -u bench.py --mode train --no-cpu-baseline --no-extras > $O/bench_train.log 2>&1
