@@ -1005,12 +1005,39 @@ def conv2d_bwd_data_x3(dys, wfp, x_shape, pad=0, dil=1, add=None, amax=None, sk=
     return dx
 
 
+# The wgrad's split-K slabs, one buffer per (device, launching stream), grown to the
+# largest request: the launches on a stream run in order, each reading its slabs back
+# (the reduce) before the next writes them.  A per-call allocation instead left each
+# side-stream workspace pending on its stream's progress when freed: the caching
+# allocator levelled off at 38 GB of blocks after ~25 C3 training steps, 28 GB with
+# this buffer (5.6 GB without the overlap; step time unchanged; tools/alloc_probe.py).
+_wg_ws = {}
+
+
+def _wgrad_workspace(device, nbytes, alloc_stream=None):
+    st = torch.cuda.current_stream(device)
+    key = (st.device_index, st.cuda_stream)
+    ws = _wg_ws.get(key)
+    if ws is None or ws.numel() * 4 < nbytes:
+        if ws is not None:
+            ws.record_stream(st)                     # the last launches on st may still read it
+        n = max(nbytes, 4) // 4
+        if alloc_stream is None:
+            ws = torch.empty(n, device=device, dtype=torch.float32)
+        else:
+            with torch.cuda.stream(alloc_stream):
+                ws = torch.empty(n, device=device, dtype=torch.float32)
+            ws.record_stream(st)
+        _wg_ws[key] = ws
+    return ws
+
+
 def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, alloc_stream=None, cus=0):
     """f16x3 dL/dw (KRSC) from packed x (forward operand) and packed dy (split_pack_x3 with `amax`).
     cus: the CUs the grid should occupy (pixel-range splits = max(1, cus / tiles);
     0: the planner's count, filling whole rounds of every CU; -1: the planner's
     count on the tiled body — the halo body of 3x3 stride-1 convs off).
-    alloc_stream: take dw and the workspace from that stream's memory pool (marked
+    alloc_stream: take dw (and a new workspace buffer) from that stream's memory pool (marked
     as used by the launching stream) — a side-stream wgrad then shares the main
     stream's cached blocks instead of growing a second pool (C5 at 245 GB: the
     second pool forced allocator flushes every step, 5x slower)."""
@@ -1024,15 +1051,13 @@ def conv2d_bwd_filter_x3(xs, dys, w_shape, stride=1, pad=0, dil=1, amax=None, al
     if tuple(dys.shape) != (n, ho, wo, 2 * d.k):
         raise HkpError("conv2d_bwd_filter_x3: dy split shape %s != %s" % (tuple(dys.shape), (n, ho, wo, 2 * d.k)))
     nbytes = lib().hkp_conv_bwd_filter_x3_workspace(ctypes.byref(d))
+    ws = _wgrad_workspace(xs.device, nbytes, alloc_stream)
     if alloc_stream is None:
-        ws = torch.empty(max(nbytes, 4) // 4, device=xs.device, dtype=torch.float32)
         dw = torch.empty(tuple(w_shape), device=xs.device, dtype=torch.float32)
     else:
         launching = torch.cuda.current_stream(xs.device)
         with torch.cuda.stream(alloc_stream):
-            ws = torch.empty(max(nbytes, 4) // 4, device=xs.device, dtype=torch.float32)
             dw = torch.empty(tuple(w_shape), device=xs.device, dtype=torch.float32)
-        ws.record_stream(launching)
         dw.record_stream(launching)
 
     def launch():
